@@ -35,9 +35,10 @@ def lib():
         L.or_create.argtypes = [C.POINTER(A.SgConfig)]
         L.or_destroy.argtypes = [P]
         L.or_register.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
-        L.or_load_flow_rules.argtypes = [P, C.POINTER(A.SgFlowRule), C.c_uint32, C.POINTER(C.c_uint32)]
-        L.or_load_degrade_rules.argtypes = [P, C.POINTER(A.SgDegradeRule), C.c_uint32, C.POINTER(C.c_uint32)]
-        L.or_load_param_rules.argtypes = [P, C.POINTER(A.SgParamRule), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.or_register_many.argtypes = [P, C.c_void_p, C.c_uint32]
+        L.or_load_flow_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.or_load_degrade_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.or_load_param_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
         L.or_rule_order.argtypes = [P, C.c_uint32, C.c_int, C.POINTER(C.c_int32), C.c_int]
         L.or_param_key.restype = C.c_uint64
         L.or_param_key.argtypes = [C.c_char_p, C.c_char_p]
@@ -129,23 +130,27 @@ class Oracle:
         assert lib().or_register(self.h, name.encode(), C.byref(out)) == 0
         return out.value
 
+    def register_ptrs(self, names_ptr, n: int):
+        assert lib().or_register_many(self.h, names_ptr, n) == 0
+
+    def _load(self, fn, rules, struct):
+        if isinstance(rules, tuple):
+            ptr, n = rules
+        else:
+            arr = (struct * max(1, len(rules)))(*rules)
+            ptr, n = C.cast(arr, C.c_void_p), len(rules)
+        out = C.c_uint32()
+        assert fn(self.h, ptr, n, C.byref(out)) == 0
+        return out.value
+
     def load_flow_rules(self, rules) -> int:
-        arr = (A.SgFlowRule * max(1, len(rules)))(*rules)
-        n = C.c_uint32()
-        assert lib().or_load_flow_rules(self.h, arr, len(rules), C.byref(n)) == 0
-        return n.value
+        return self._load(lib().or_load_flow_rules, rules, A.SgFlowRule)
 
     def load_degrade_rules(self, rules) -> int:
-        arr = (A.SgDegradeRule * max(1, len(rules)))(*rules)
-        n = C.c_uint32()
-        assert lib().or_load_degrade_rules(self.h, arr, len(rules), C.byref(n)) == 0
-        return n.value
+        return self._load(lib().or_load_degrade_rules, rules, A.SgDegradeRule)
 
     def load_param_rules(self, rules) -> int:
-        arr = (A.SgParamRule * max(1, len(rules)))(*rules)
-        n = C.c_uint32()
-        assert lib().or_load_param_rules(self.h, arr, len(rules), C.byref(n)) == 0
-        return n.value
+        return self._load(lib().or_load_param_rules, rules, A.SgParamRule)
 
     def rule_order(self, res: int, kind: int):
         out = (C.c_int32 * 64)()

@@ -923,6 +923,14 @@ int or_register(or_engine* e, const char* name, uint32_t* out_id) {
     return SG_OK;
 }
 
+int or_register_many(or_engine* e, const char* const* names, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        int rc = or_register(e, names[i], NULL);
+        if (rc) return rc;
+    }
+    return SG_OK;
+}
+
 /* ---- FlowRuleUtil.isValidRule (FlowRuleUtil.java:174-228) -------------- */
 static int flow_valid(const sg_flow_rule* r) {
     if (!r || str_blank(r->resource) || !(r->count >= 0) || r->grade < 0 || r->strategy < 0 || r->control_behavior < 0)
@@ -1000,7 +1008,6 @@ int or_load_flow_rules(or_engine* e, const sg_flow_rule* r, uint32_t n, uint32_t
     for (uint32_t i = 0; i < e->n_res; ++i) { free(e->res[i].flow); e->res[i].flow = NULL; e->res[i].n_flow = 0; }
 
     /* validate, default limitApp, build a fresh controller per rule, group per resource into HashSets */
-    int* grp_res = (int*)malloc(sizeof(int) * (n ? n : 1));
     for (uint32_t i = 0; i < n; ++i) {
         if (!flow_valid(&r[i])) continue;
         oflow* f = &e->flows[e->n_flows];
@@ -1011,26 +1018,22 @@ int or_load_flow_rules(or_engine* e, const sg_flow_rule* r, uint32_t n, uint32_t
                   f->r.grade, f->r.count, f->r.warm_up_period_sec, f->r.max_queueing_time_ms, e->c.cold_factor);
         uint32_t rid;
         or_register(e, f->r.resource, &rid);
+        ores* rs = res_get(e, rid);
         /* HashSet.add: drop if an equal rule is already in this resource's set */
         int dup = 0;
-        for (int k = 0; k < e->n_flows; ++k)
-            if (grp_res[k] == (int)rid && flow_equals(&e->flows[k], f)) { dup = 1; break; }
+        for (int k = 0; k < rs->n_flow; ++k)
+            if (flow_equals(&e->flows[rs->flow[k]], f)) { dup = 1; break; }
         if (dup) { free_flow(f); memset(f, 0, sizeof(*f)); continue; }
-        grp_res[e->n_flows] = (int)rid;
+        rs->flow = (int*)realloc(rs->flow, sizeof(int) * (size_t)(rs->n_flow + 1));
+        rs->flow[rs->n_flow++] = e->n_flows;
         e->n_flows++;
     }
-    for (int k = 0; k < e->n_flows; ++k) {
-        ores* rs = res_get(e, (uint32_t)grp_res[k]);
-        rs->flow = (int*)realloc(rs->flow, sizeof(int) * (size_t)(rs->n_flow + 1));
-        rs->flow[rs->n_flow++] = k;
-    }
+    int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * (size_t)(e->n_flows > 0 ? (unsigned)e->n_flows : 1u));
+    for (int k = 0; k < e->n_flows; ++k) hs[k] = e->flows[k].hash;
     for (uint32_t i = 0; i < e->n_res; ++i) {
         ores* rs = &e->res[i];
         if (rs->n_flow <= 1) continue;
-        int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * (size_t)e->n_flows);
-        for (int k = 0; k < e->n_flows; ++k) hs[k] = e->flows[k].hash;
         java_hashset_order(hs, rs->flow, rs->n_flow);   /* new ArrayList<>(HashSet) */
-        free(hs);
         /* Collections.sort(rules, FlowRuleComparator): stable insertion sort */
         for (int a = 1; a < rs->n_flow; ++a) {
             int v = rs->flow[a], b = a - 1;
@@ -1038,7 +1041,7 @@ int or_load_flow_rules(or_engine* e, const sg_flow_rule* r, uint32_t n, uint32_t
             rs->flow[b + 1] = v;
         }
     }
-    free(grp_res);
+    free(hs);
     if (n_loaded) *n_loaded = (uint32_t)e->n_flows;
 
     /* token server view: ClusterFlowRuleManager keeps cluster-mode rules by flowId */
@@ -1094,7 +1097,6 @@ int or_load_degrade_rules(or_engine* e, const sg_degrade_rule* r, uint32_t n, ui
     e->n_degrades = 0;
     e->degrade_loaded = 1;
     for (uint32_t i = 0; i < e->n_res; ++i) { free(e->res[i].degrade); e->res[i].degrade = NULL; e->res[i].n_degrade = 0; }
-    int* grp = (int*)malloc(sizeof(int) * (n ? n : 1));
     for (uint32_t i = 0; i < n; ++i) {
         if (!degrade_valid(&r[i])) continue;
         odegrade* d = &e->degrades[e->n_degrades];
@@ -1106,22 +1108,20 @@ int or_load_degrade_rules(or_engine* e, const sg_degrade_rule* r, uint32_t n, ui
         d->src_index = (int)i;
         uint32_t rid;
         or_register(e, d->r.resource, &rid);
+        ores* rs = res_get(e, rid);
         int dup = 0;
-        for (int k = 0; k < e->n_degrades; ++k)
-            if (grp[k] == (int)rid && degrade_equals(&e->degrades[k], d)) { dup = 1; break; }
+        for (int k = 0; k < rs->n_degrade; ++k)
+            if (degrade_equals(&e->degrades[rs->degrade[k]], d)) { dup = 1; break; }
         if (dup) { free((char*)d->r.resource); free((char*)d->r.limit_app); continue; }
-        grp[e->n_degrades++] = (int)rid;
-    }
-    for (int k = 0; k < e->n_degrades; ++k) {
-        ores* rs = res_get(e, (uint32_t)grp[k]);
         rs->degrade = (int*)realloc(rs->degrade, sizeof(int) * (size_t)(rs->n_degrade + 1));
-        rs->degrade[rs->n_degrade++] = k;
+        rs->degrade[rs->n_degrade++] = e->n_degrades;
+        e->n_degrades++;
     }
     int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * (size_t)(e->n_degrades > 0 ? (unsigned)e->n_degrades : 1u));
     for (int k = 0; k < e->n_degrades; ++k) hs[k] = e->degrades[k].hash;
     for (uint32_t i = 0; i < e->n_res; ++i)
         if (e->res[i].n_degrade > 1) java_hashset_order(hs, e->res[i].degrade, e->res[i].n_degrade);
-    free(hs); free(grp);
+    free(hs);
     if (n_loaded) *n_loaded = (uint32_t)e->n_degrades;
     return SG_OK;
 }
@@ -1244,7 +1244,6 @@ int or_load_param_rules(or_engine* e, const sg_param_rule* r, uint32_t n, uint32
         if (n_loaded) *n_loaded = 0;
         return SG_OK;
     }
-    int* grp = (int*)malloc(sizeof(int) * n);
     for (uint32_t i = 0; i < n; ++i) {
         if (!param_valid(&r[i])) continue;
         oparam* p = &e->params[e->n_params];
@@ -1253,22 +1252,20 @@ int or_load_param_rules(or_engine* e, const sg_param_rule* r, uint32_t n, uint32
         p->src_index = (int)i;
         uint32_t rid;
         or_register(e, p->r.resource, &rid);
+        ores* rs = res_get(e, rid);
         int dup = 0;
-        for (int k = 0; k < e->n_params; ++k)
-            if (grp[k] == (int)rid && param_equals(&e->params[k], p)) { dup = 1; break; }
+        for (int k = 0; k < rs->n_param; ++k)
+            if (param_equals(&e->params[rs->param[k]], p)) { dup = 1; break; }
         if (dup) { free_param(p); memset(p, 0, sizeof(*p)); continue; }
-        grp[e->n_params++] = (int)rid;
-    }
-    for (int k = 0; k < e->n_params; ++k) {
-        ores* rs = res_get(e, (uint32_t)grp[k]);
         rs->param = (int*)realloc(rs->param, sizeof(int) * (size_t)(rs->n_param + 1));
-        rs->param[rs->n_param++] = k;
+        rs->param[rs->n_param++] = e->n_params;
+        e->n_params++;
     }
     int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * (size_t)(e->n_params > 0 ? (unsigned)e->n_params : 1u));
     for (int k = 0; k < e->n_params; ++k) hs[k] = e->params[k].hash;
     for (uint32_t i = 0; i < e->n_res; ++i)
         if (e->res[i].n_param > 1) java_hashset_order(hs, e->res[i].param, e->res[i].n_param);
-    free(hs); free(grp);
+    free(hs);
     /* clear unused hot param metrics (ParamFlowSlot.clearHotParamMetricForName) */
     for (uint32_t i = 0; i < n_res_before; ++i)
         if (had[i] && e->res[i].n_param == 0) pm_clear(&e->res[i].pm);

@@ -28,6 +28,7 @@ typedef struct or_engine or_engine;
 or_engine* or_create(const sg_config* cfg);
 void or_destroy(or_engine* e);
 int or_register(or_engine* e, const char* name, uint32_t* out_id);
+int or_register_many(or_engine* e, const char* const* names, uint32_t n);
 int or_load_flow_rules(or_engine* e, const sg_flow_rule* r, uint32_t n, uint32_t* n_loaded);
 int or_load_degrade_rules(or_engine* e, const sg_degrade_rule* r, uint32_t n, uint32_t* n_loaded);
 int or_load_param_rules(or_engine* e, const sg_param_rule* r, uint32_t n, uint32_t* n_loaded);

@@ -1,0 +1,1129 @@
+// engine.cpp -- host side of the MI355X decision engine: the C ABI of
+// include/sentinel_gpu.h, the rule managers (validation, de-duplication,
+// java.util.HashSet ordering, FlowRuleComparator sort) and the per-batch
+// launch pipeline.  All decisions are taken by the HIP kernels in kernels.hip;
+// nothing here evaluates a rule.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/sentinel_gpu.h"
+#include "dev_types.h"
+
+namespace sg {
+hipError_t launch_radix_hist(const sg_event*, const uint32_t*, uint64_t, int, uint32_t*, uint32_t, uint32_t*, uint32_t,
+                             hipStream_t);
+hipError_t launch_radix_scatter(const sg_event*, const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                uint32_t, uint32_t*, uint32_t*, hipStream_t);
+uint32_t radix_tile();
+hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
+hipError_t launch_seg(const uint32_t*, uint64_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, Seg*, uint32_t*,
+                      hipStream_t);
+hipError_t launch_seg_order(const Seg*, uint32_t, uint32_t*, uint32_t*, hipStream_t);
+hipError_t launch_chain_candidates(const sg_event*, const uint32_t*, const Seg*, uint32_t, const NodeInfo*, uint32_t*,
+                                   uint64_t*, hipStream_t);
+hipError_t launch_decide(const sg_event*, const uint32_t*, const Seg*, const uint32_t*, uint32_t, uint64_t, uint64_t,
+                         const DevState&, const DevCfg&, uint32_t*, uint32_t*, hipStream_t);
+hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                           sg_metric_node*, uint64_t, hipStream_t);
+hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, uint32_t nres, hipStream_t st);
+hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st);
+} // namespace sg
+
+using namespace sg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t _e = (x);                                                                             \
+        if (_e != hipSuccess) return fail(SG_EDEVICE, std::string(#x ": ") + hipGetErrorString(_e));    \
+    } while (0)
+
+// ----------------------------------------------------------------- Java helpers
+int32_t j_string_hash(const char* s) {
+    if (!s) return 0;
+    uint32_t h = 0;
+    const unsigned char* p = (const unsigned char*)s;
+    while (*p) {
+        uint32_t cp;
+        if (*p < 0x80) cp = *p++;
+        else if ((*p & 0xE0) == 0xC0 && p[1]) { cp = ((p[0] & 0x1Fu) << 6) | (p[1] & 0x3Fu); p += 2; }
+        else if ((*p & 0xF0) == 0xE0 && p[1] && p[2]) { cp = ((p[0] & 0x0Fu) << 12) | ((p[1] & 0x3Fu) << 6) | (p[2] & 0x3Fu); p += 3; }
+        else if (p[1] && p[2] && p[3]) { cp = ((p[0] & 0x07u) << 18) | ((p[1] & 0x3Fu) << 12) | ((p[2] & 0x3Fu) << 6) | (p[3] & 0x3Fu); p += 4; }
+        else cp = *p++;
+        if (cp >= 0x10000) {
+            cp -= 0x10000;
+            h = 31u * h + (0xD800u + (cp >> 10));
+            h = 31u * h + (0xDC00u + (cp & 0x3FFu));
+        } else {
+            h = 31u * h + cp;
+        }
+    }
+    return (int32_t)h;
+}
+inline int32_t h31(int32_t h, int32_t v) { return (int32_t)(31u * (uint32_t)h + (uint32_t)v); }
+int32_t j_double_hash(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    if (d != d) u = 0x7ff8000000000000ULL;
+    return (int32_t)(uint32_t)(u ^ (u >> 32));
+}
+uint64_t dbl_bits(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    if (d != d) u = 0x7ff8000000000000ULL;
+    return u;
+}
+int32_t long_hash(int64_t v) { return (int32_t)(uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32)); }
+bool blank(const char* s) {
+    if (!s) return true;
+    for (; *s; ++s)
+        if (*s != ' ' && *s != '\t' && *s != '\n' && *s != '\r' && *s != '\f' && *s != '\v') return false;
+    return true;
+}
+std::string sv(const char* s) { return s ? std::string(s) : std::string(); }
+// AbstractRule.limitAppEquals normal form: null, "" and "default" are interchangeable
+std::string la_norm(const char* s) { return (!s || !*s || std::strcmp(s, "default") == 0) ? "default" : std::string(s); }
+int32_t abstract_hash(const char* res, const char* la) {
+    int32_t h = res ? j_string_hash(res) : 0;
+    if (!(la == nullptr || !*la || std::strcmp(la, "default") == 0)) h = h31(h, j_string_hash(la));
+    return h;
+}
+int32_t cluster_hash(int64_t fid, int thr, int fb, int strat, int sc, int win, bool has_strat) {
+    int32_t h = fid ? long_hash(fid) : 0;
+    h = h31(h, thr);
+    h = h31(h, fb ? 1 : 0);
+    if (has_strat) h = h31(h, strat);
+    h = h31(h, sc);
+    h = h31(h, win);
+    return h;
+}
+
+// java.util.HashSet iteration order of elements inserted in `order` (see oracle Q11 note):
+// bucket index (h ^ h>>>16) & (cap-1) ascending, insertion order inside a bucket.
+void hashset_order(const std::vector<int32_t>& hashes, std::vector<int>& order) {
+    size_t n = order.size();
+    if (n <= 1) return;
+    int cap = 16;
+    for (;;) {
+        bool grown = false;
+        std::vector<int> bin(cap, 0);
+        size_t size = 0;
+        for (size_t k = 0; k < n; ++k) {
+            uint32_t h = (uint32_t)hashes[order[k]];
+            h ^= h >> 16;
+            int b = (int)(h & (uint32_t)(cap - 1));
+            if (bin[b] >= 8 && cap < 64) { cap *= 2; grown = true; break; }
+            bin[b]++;
+            if (++size > (size_t)cap * 3 / 4 && k + 1 < n) { cap *= 2; grown = true; break; }
+        }
+        if (!grown) break;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        uint32_t ha = (uint32_t)hashes[a], hb = (uint32_t)hashes[b];
+        ha ^= ha >> 16; hb ^= hb >> 16;
+        return (ha & (uint32_t)(cap - 1)) < (hb & (uint32_t)(cap - 1));
+    });
+}
+
+// ---- param value keys (ParamFlowRuleUtil.parseItemValue typing, ParamFlowRuleUtil.java:85-121)
+constexpr uint64_t KEY_MASK = 0x0FFFFFFFFFFFFFFFULL;
+uint64_t fnv64(const char* s) {
+    uint64_t h = 1469598103934665603ULL;
+    for (; *s; ++s) { h ^= (unsigned char)*s; h *= 1099511628211ULL; }
+    return h;
+}
+uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27; x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31; return x;
+}
+uint64_t tagged(uint64_t tag, uint64_t v) { return (tag << 60) | (v & KEY_MASK); }
+bool ieq(const char* a, const char* b) {
+    for (; *a && *b; ++a, ++b) if (std::tolower((unsigned char)*a) != std::tolower((unsigned char)*b)) return false;
+    return *a == *b;
+}
+uint64_t param_key(const char* v, const char* t) {
+    if (!v) return 0;
+    auto is = [&](const char* a, const char* b) { return t && (!std::strcmp(t, a) || !std::strcmp(t, b)); };
+    if (blank(t) || !std::strcmp(t, "java.lang.String") || !std::strcmp(t, "String")) return tagged(1, fnv64(v) & KEY_MASK);
+    if (is("int", "java.lang.Integer")) return tagged(2, (uint32_t)(int32_t)std::strtol(v, nullptr, 10));
+    if (is("long", "java.lang.Long")) {
+        long long x = std::strtoll(v, nullptr, 10);
+        if (x >= -(1LL << 59) && x < (1LL << 59)) return tagged(3, (uint64_t)x);
+        return tagged(3, (fnv64(v) & KEY_MASK) | (1ULL << 59));
+    }
+    if (is("double", "java.lang.Double")) {
+        double d = std::strtod(v, nullptr);
+        uint64_t u;
+        std::memcpy(&u, &d, 8);
+        return tagged(4, mix64(u));
+    }
+    if (is("float", "java.lang.Float")) {
+        float f = std::strtof(v, nullptr);
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        return tagged(5, u);
+    }
+    if (is("byte", "java.lang.Byte")) return tagged(6, (uint8_t)(int8_t)std::strtol(v, nullptr, 10));
+    if (is("short", "java.lang.Short")) return tagged(7, (uint16_t)(int16_t)std::strtol(v, nullptr, 10));
+    if (is("boolean", "java.lang.Boolean")) return tagged(8, ieq(v, "true") ? 1 : 0);
+    if (!std::strcmp(t, "char")) return tagged(9, (unsigned char)v[0]);
+    return tagged(1, fnv64(v) & KEY_MASK);
+}
+
+// ----------------------------------------------------------------- rule records
+struct FlowR {
+    sg_flow_rule r;
+    std::string res, la, ref;
+    int32_t hash;
+    std::string eqkey;  // FlowRule.equals
+};
+struct DegR {
+    sg_degrade_rule r;
+    std::string res, la;
+    int32_t hash;
+    std::string eqkey;
+};
+struct ParamItemR {
+    std::string obj, ct;
+    bool has_obj, has_ct;
+    int32_t count, has_count;
+};
+struct ParamR {
+    sg_param_rule r;
+    std::string res, la;
+    std::vector<ParamItemR> items;
+    std::vector<std::pair<uint64_t, int32_t>> hot;
+    int32_t hash;
+    std::string eqkey;
+};
+
+std::string flow_eqkey(const sg_flow_rule& r) {
+    char buf[512];
+    bool cc = r.cluster_mode || r.cluster_flow_id;
+    std::snprintf(buf, sizeof(buf), "%d|%016llx|%d|%d|%d|%d|%d|", r.grade, (unsigned long long)dbl_bits(r.count),
+                  r.strategy, r.control_behavior, r.warm_up_period_sec, r.max_queueing_time_ms, r.cluster_mode ? 1 : 0);
+    std::string k = std::string(buf) + sv(r.resource) + "\x01" + la_norm(r.limit_app) + "\x01" +
+                    (r.ref_resource ? "1" + std::string(r.ref_resource) : "0") + "\x01";
+    if (cc) {
+        std::snprintf(buf, sizeof(buf), "C%lld|%d|%d|%d|%d|%d", (long long)r.cluster_flow_id, r.cluster_threshold_type,
+                      r.cluster_fallback_to_local ? 1 : 0, r.cluster_strategy, r.cluster_sample_count,
+                      r.cluster_window_interval_ms);
+        k += buf;
+    }
+    return k;
+}
+int32_t flow_hash(const sg_flow_rule& r) {
+    int32_t h = abstract_hash(r.resource, r.limit_app && !blank(r.limit_app) ? r.limit_app : "default");
+    h = h31(h, r.grade);
+    h = h31(h, j_double_hash(r.count));
+    h = h31(h, r.strategy);
+    h = h31(h, r.ref_resource ? j_string_hash(r.ref_resource) : 0);
+    h = h31(h, r.control_behavior);
+    h = h31(h, r.warm_up_period_sec);
+    h = h31(h, r.max_queueing_time_ms);
+    h = h31(h, r.cluster_mode ? 1 : 0);
+    int32_t ch = 0;
+    if (r.cluster_mode || r.cluster_flow_id)
+        ch = cluster_hash(r.cluster_flow_id, r.cluster_threshold_type, r.cluster_fallback_to_local, r.cluster_strategy,
+                          r.cluster_sample_count, r.cluster_window_interval_ms, true);
+    return h31(h, ch);
+}
+bool flow_valid(const sg_flow_rule& r) { // FlowRuleUtil.isValidRule (FlowRuleUtil.java:174-228)
+    if (blank(r.resource) || !(r.count >= 0) || r.grade < 0 || r.strategy < 0 || r.control_behavior < 0) return false;
+    if (r.cluster_mode) {
+        if (r.cluster_flow_id <= 0) return false;
+        if (!(r.cluster_sample_count > 0 && r.cluster_window_interval_ms > 0 &&
+              r.cluster_window_interval_ms % r.cluster_sample_count == 0))
+            return false;
+        if (r.strategy != 0) return false;
+    }
+    if ((r.strategy == SG_STRATEGY_RELATE || r.strategy == SG_STRATEGY_CHAIN) && blank(r.ref_resource)) return false;
+    switch (r.control_behavior) {
+    case SG_CONTROL_BEHAVIOR_WARM_UP: return r.warm_up_period_sec > 0;
+    case SG_CONTROL_BEHAVIOR_RATE_LIMITER: return r.max_queueing_time_ms > 0;
+    case SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER: return r.warm_up_period_sec > 0 && r.max_queueing_time_ms > 0;
+    default: return true;
+    }
+}
+std::string deg_eqkey(const sg_degrade_rule& r, int uniq) {
+    char buf[256];
+    // DegradeRule.equals compares count with != (NaN never equal): give NaN rules a unique key
+    if (r.count != r.count) std::snprintf(buf, sizeof(buf), "NaN#%d|", uniq);
+    else std::snprintf(buf, sizeof(buf), "%.17g|%d|%d|", r.count == 0 ? 0.0 : r.count, r.time_window, r.grade);
+    return std::string(buf) + sv(r.resource) + "\x01" + la_norm(r.limit_app);
+}
+int32_t deg_hash(const sg_degrade_rule& r) {
+    int32_t h = abstract_hash(r.resource, r.limit_app && !blank(r.limit_app) ? r.limit_app : "default");
+    h = h31(h, j_double_hash(r.count));
+    h = h31(h, r.time_window);
+    return h31(h, r.grade);
+}
+bool param_valid(const sg_param_rule& r) { // ParamFlowRuleUtil.isValidRule (ParamFlowRuleUtil.java:32-55)
+    if (blank(r.resource) || !(r.count >= 0) || r.grade < 0 || !r.has_param_idx || r.burst_count < 0 ||
+        r.control_behavior < 0 || r.duration_in_sec <= 0 || r.max_queueing_time_ms < 0)
+        return false;
+    if (r.cluster_mode) {
+        if (!(r.cluster_sample_count > 0 && r.cluster_window_interval_ms > 0 &&
+              r.cluster_window_interval_ms % r.cluster_sample_count == 0))
+            return false;
+        if (r.cluster_flow_id <= 0) return false;
+    }
+    return true;
+}
+ParamR make_param(const sg_param_rule& s) {
+    ParamR p;
+    p.r = s;
+    p.res = sv(s.resource);
+    p.la = la_norm(s.limit_app);
+    for (int i = 0; i < s.n_items; ++i) {
+        const sg_param_item& it = s.items[i];
+        ParamItemR q;
+        q.has_obj = it.object != nullptr;
+        q.obj = sv(it.object);
+        q.has_ct = it.class_type != nullptr;
+        q.ct = sv(it.class_type);
+        q.count = it.count;
+        q.has_count = it.has_count;
+        p.items.push_back(q);
+        // ParamFlowRuleUtil.parseHotItems (ParamFlowRuleUtil.java:62-83)
+        if (!it.object || !it.has_count || it.count < 0) continue;
+        uint64_t k = param_key(it.object, it.class_type);
+        bool found = false;
+        for (auto& h : p.hot) if (h.first == k) { h.second = it.count; found = true; }
+        if (!found) p.hot.push_back({k, it.count});
+    }
+    // ParamFlowRule.hashCode (ParamFlowRule.java:218-234)
+    int32_t h = abstract_hash(s.resource, s.limit_app && !blank(s.limit_app) ? s.limit_app : "default");
+    h = h31(h, s.grade);
+    h = h31(h, s.has_param_idx ? s.param_idx : 0);
+    h = h31(h, j_double_hash(s.count));
+    h = h31(h, s.control_behavior);
+    h = h31(h, s.max_queueing_time_ms);
+    h = h31(h, s.burst_count);
+    h = h31(h, long_hash(s.duration_in_sec));
+    int32_t lh = 1;
+    for (auto& q : p.items) {
+        int32_t e = q.has_obj ? j_string_hash(q.obj.c_str()) : 0;
+        e = h31(e, q.has_count ? q.count : 0);
+        e = h31(e, q.has_ct ? j_string_hash(q.ct.c_str()) : 0);
+        lh = h31(lh, e);
+    }
+    h = h31(h, lh);
+    h = h31(h, s.cluster_mode ? 1 : 0);
+    int32_t ch = 0;
+    if (s.cluster_mode || s.cluster_flow_id)
+        ch = cluster_hash(s.cluster_flow_id, s.cluster_threshold_type, s.cluster_fallback_to_local, 0,
+                          s.cluster_sample_count, s.cluster_window_interval_ms, false);
+    p.hash = h31(h, ch);
+    // ParamFlowRule.equals
+    char buf[512];
+    std::snprintf(buf, sizeof(buf), "%d|%016llx|%d|%d|%d|%lld|%d|%d:%d|", s.grade, (unsigned long long)dbl_bits(s.count),
+                  s.control_behavior, s.max_queueing_time_ms, s.burst_count, (long long)s.duration_in_sec,
+                  s.cluster_mode ? 1 : 0, s.has_param_idx, s.has_param_idx ? s.param_idx : 0);
+    std::string k = std::string(buf) + p.res + "\x01" + p.la + "\x01";
+    for (auto& q : p.items) {
+        std::snprintf(buf, sizeof(buf), "[%d%d%d:%d]", q.has_obj, q.has_ct, q.has_count, q.has_count ? q.count : 0);
+        k += buf + q.obj + "\x02" + q.ct + "\x03";
+    }
+    if (s.cluster_mode || s.cluster_flow_id) {
+        std::snprintf(buf, sizeof(buf), "C%lld|%d|%d|%d|%d", (long long)s.cluster_flow_id, s.cluster_threshold_type,
+                      s.cluster_fallback_to_local ? 1 : 0, s.cluster_sample_count, s.cluster_window_interval_ms);
+        k += buf;
+    }
+    p.eqkey = k;
+    return p;
+}
+
+template <class T> void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+} // namespace
+
+// =====================================================================================
+struct sg_engine {
+    sg_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double last_ms[3] = {0, 0, 0};
+
+    // resources
+    std::unordered_map<std::string, uint32_t> ids;
+    std::vector<std::string> names;
+    uint32_t n_chains = 0;
+
+    // rule managers
+    bool flow_loaded = false, deg_loaded = false, par_loaded = false;
+    std::vector<std::string> last_flow, last_deg, last_par; // equality keys of the last loaded lists
+    std::vector<FlowR> flows;
+    std::vector<DegR> degs;
+    std::vector<ParamR> params;
+    std::vector<std::vector<int>> res_flow, res_deg, res_par; // compiled order per resource
+    std::map<std::string, uint32_t> psid_of;                   // "res\x00eqkey" -> param state id
+    uint32_t next_psid = 1;
+    std::vector<uint32_t> tc_epoch;                             // per resource
+    uint32_t next_epoch = 1;
+    uint32_t n_dev_rules = 0;
+
+    // device state
+    Bkt* d_sec = nullptr;
+    Bkt* d_minb = nullptr;
+    NodeInfo* d_info = nullptr;
+    Prog* d_prog = nullptr;
+    DRule* d_rules = nullptr;
+    RState* d_rstate = nullptr;
+    DHot* d_hot = nullptr;
+    PSlot* d_ptab = nullptr;
+    uint8_t* d_ring = nullptr;
+    uint32_t rules_cap = 0, hot_cap = 0;
+
+    // batch scratch
+    uint64_t cap_n = 0;
+    sg_event* d_ev = nullptr;
+    uint32_t* d_out = nullptr;
+    uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
+    uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
+    Seg* d_segs = nullptr;
+    uint32_t* d_small = nullptr;  // [0] bflags [1] nseg [2] ncand [3..34] lbucket [35..66] lcursor [67] total
+    uint64_t* d_cand = nullptr;
+    uint64_t cap_hist = 0;
+    uint64_t gbase = 0;
+    // snapshot scratch
+    uint32_t *d_snap_cnt = nullptr, *d_snap_off = nullptr;
+    sg_metric_node* d_snap_out = nullptr;
+    uint64_t snap_cap = 0;
+};
+
+namespace {
+
+int ensure_batch(sg_engine* e, uint64_t n) {
+    if (n <= e->cap_n) return SG_OK;
+    uint64_t c = std::max<uint64_t>(n, 1u << 20);
+    dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
+    dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
+    dfree(e->d_cand);
+    uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
+    e->cap_hist = nblocks * 256;
+    HIPCHK(hipMalloc(&e->d_ev, c * sizeof(sg_event)));
+    HIPCHK(hipMalloc(&e->d_out, c * 4));
+    HIPCHK(hipMalloc(&e->d_k0, c * 4));
+    HIPCHK(hipMalloc(&e->d_v0, c * 4));
+    HIPCHK(hipMalloc(&e->d_k1, c * 4));
+    HIPCHK(hipMalloc(&e->d_v1, c * 4));
+    HIPCHK(hipMalloc(&e->d_hist, e->cap_hist * 4));
+    HIPCHK(hipMalloc(&e->d_part, (e->cap_hist / 4096 + c / 4096 + 64) * 4));
+    HIPCHK(hipMalloc(&e->d_flag, c * 4));
+    HIPCHK(hipMalloc(&e->d_pos, c * 4));
+    HIPCHK(hipMalloc(&e->d_order, c * 4));
+    HIPCHK(hipMalloc(&e->d_segs, c * sizeof(Seg)));
+    HIPCHK(hipMalloc(&e->d_cand, c * 8));
+    e->cap_n = c;
+    return SG_OK;
+}
+
+// Build the device rule program of every resource from the compiled host lists.
+int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
+    uint32_t R = e->cfg.max_resources;
+    std::vector<Prog> prog(R);
+    std::vector<DRule> rules;
+    std::vector<RState> rst;
+    std::vector<DHot> hot;
+    // previous rule states to carry over when a kind was not reloaded
+    std::vector<RState> old_rst;
+    std::vector<Prog> old_prog;
+    if ((!reset_flow_state || !reset_deg_state) && e->n_dev_rules) {
+        old_rst.resize(e->n_dev_rules);
+        old_prog.resize(R);
+        HIPCHK(hipMemcpy(old_rst.data(), e->d_rstate, e->n_dev_rules * sizeof(RState), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(old_prog.data(), e->d_prog, R * sizeof(Prog), hipMemcpyDeviceToHost));
+    }
+    size_t nres = e->names.size();
+    if (e->tc_epoch.size() < nres) e->tc_epoch.resize(nres, 0);
+    for (size_t r = 0; r < nres && r < R; ++r) {
+        Prog p;
+        std::memset(&p, 0, sizeof(p));
+        p.rule_off = (uint32_t)rules.size();
+        p.tc_epoch = e->tc_epoch[r];
+        // param rules: HashSet order; only paramIdx 0 can see an argument (events carry args[0])
+        const auto& pl = r < e->res_par.size() ? e->res_par[r] : std::vector<int>();
+        for (size_t i = 0; i < pl.size(); ++i) {
+            const ParamR& q = e->params[pl[i]];
+            if (q.r.param_idx == 0) p.pflags |= PF_PARAM_IDX0;
+            if (q.r.param_idx != 0) continue; // args.length (<= 1) <= paramIdx -> always passes
+            if (q.r.cluster_mode && q.r.grade == SG_FLOW_GRADE_QPS && !q.r.cluster_fallback_to_local) continue;
+            DRule d;
+            std::memset(&d, 0, sizeof(d));
+            d.kind = RK_PARAM;
+            d.grade = (uint8_t)q.r.grade;
+            d.behavior = (uint8_t)q.r.control_behavior;
+            d.slot = (uint8_t)i;
+            d.max_queue = q.r.max_queueing_time_ms;
+            d.count = q.r.count;
+            d.burst = q.r.burst_count;
+            double c = q.r.count;
+            d.token_count = (c != c) ? 0 : c >= 2147483647.0 ? INT32_MAX : (int32_t)c;
+            d.token_count_l = (c != c) ? 0 : c >= 9.2e18 ? INT64_MAX : (int64_t)c;
+            d.duration_sec = q.r.duration_in_sec;
+            d.hot_off = (uint32_t)hot.size();
+            d.hot_n = (uint32_t)q.hot.size();
+            for (auto& h : q.hot) hot.push_back(DHot{h.first, h.second, 0});
+            d.psid = e->psid_of[q.res + std::string("\0", 1) + q.eqkey];
+            rules.push_back(d);
+            rst.push_back(RState{0, 0, 0, 0});
+            p.n_param++;
+        }
+        if (!pl.empty() && p.n_param == 0) { // metric still created (ParamFlowSlot.initHotParamMetricsFor)
+            DRule d;
+            std::memset(&d, 0, sizeof(d));
+            d.kind = RK_PARAM;
+            d.grade = 0xFF; // never blocks
+            d.psid = 0;
+            rules.push_back(d);
+            rst.push_back(RState{0, 0, 0, 0});
+            p.n_param = 1;
+        }
+        // flow rules: FlowRuleComparator order; the default context without an origin selects
+        // the ClusterNode for limitApp "default" + DIRECT (FlowRuleChecker.java:90-124)
+        const auto& fl = r < e->res_flow.size() ? e->res_flow[r] : std::vector<int>();
+        for (size_t i = 0; i < fl.size(); ++i) {
+            const FlowR& f = e->flows[fl[i]];
+            if (f.la != "default") continue;  // origin "" never matches / isOtherOrigin("") == false
+            if (f.r.strategy == SG_STRATEGY_RELATE)
+                return fail(SG_ENOTSUP, "STRATEGY_RELATE reads another resource's node: not on the device path yet");
+            if (f.r.strategy == SG_STRATEGY_CHAIN && f.ref != "sentinel_default_context") continue;
+            if (f.r.cluster_mode && !f.r.cluster_fallback_to_local) continue; // no TokenService -> pass
+            DRule d;
+            std::memset(&d, 0, sizeof(d));
+            d.kind = RK_FLOW;
+            d.grade = (uint8_t)f.r.grade;
+            d.behavior = (uint8_t)(f.r.grade == SG_FLOW_GRADE_QPS ? f.r.control_behavior : SG_CONTROL_BEHAVIOR_DEFAULT);
+            if (d.behavior > 3) d.behavior = SG_CONTROL_BEHAVIOR_DEFAULT;
+            d.slot = (uint8_t)i;
+            d.max_queue = f.r.max_queueing_time_ms;
+            d.count = f.r.count;
+            if (d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
+                // WarmUpController.construct (WarmUpController.java:100-117)
+                int cold = e->cfg.cold_factor;
+                double c = f.r.count;
+                auto d2i = [](double v) -> int32_t {
+                    if (v != v) return 0;
+                    if (v >= 2147483647.0) return INT32_MAX;
+                    if (v <= -2147483648.0) return INT32_MIN;
+                    return (int32_t)v;
+                };
+                int32_t wt = d2i(f.r.warm_up_period_sec * c) / (cold - 1);
+                int32_t mt = (int32_t)((uint32_t)wt + (uint32_t)d2i((double)(2 * f.r.warm_up_period_sec) * c / (1.0 + cold)));
+                d.warning_token = wt;
+                d.max_token = mt;
+                d.slope = (cold - 1.0) / c / (double)(mt - wt);
+                d.count_div_cold = d2i(c) / cold;
+                p.pflags |= PF_WARM;
+            }
+            rules.push_back(d);
+            rst.push_back(RState{0, 0, -1, 0});
+            p.n_flow++;
+        }
+        const auto& dl = r < e->res_deg.size() ? e->res_deg[r] : std::vector<int>();
+        for (size_t i = 0; i < dl.size(); ++i) {
+            const DegR& g = e->degs[dl[i]];
+            DRule d;
+            std::memset(&d, 0, sizeof(d));
+            d.kind = RK_DEGRADE;
+            d.grade = (uint8_t)g.r.grade;
+            d.slot = (uint8_t)i;
+            d.count = g.r.count;
+            d.time_window = g.r.time_window;
+            if (g.r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) p.pflags |= PF_EXC_COUNT;
+            rules.push_back(d);
+            rst.push_back(RState{0, 0, 0, 0});
+            p.n_degrade++;
+        }
+        if ((int)p.n_param + p.n_flow + p.n_degrade > 16)
+            return fail(SG_ENOTSUP, "more than 16 rules on one resource: " + e->names[r]);
+        // carry controller / breaker state of kinds that were not reloaded
+        if (!old_rst.empty()) {
+            const Prog& op = old_prog[r];
+            if (!reset_flow_state && op.n_flow == p.n_flow)
+                for (int i = 0; i < p.n_flow; ++i) rst[p.rule_off + p.n_param + i] = old_rst[op.rule_off + op.n_param + i];
+            if (!reset_deg_state && op.n_degrade == p.n_degrade)
+                for (int i = 0; i < p.n_degrade; ++i)
+                    rst[p.rule_off + p.n_param + p.n_flow + i] = old_rst[op.rule_off + op.n_param + op.n_flow + i];
+        }
+        prog[r] = p;
+    }
+    if (rules.size() > e->cfg.max_rules) return fail(SG_ECAPACITY, "compiled rule table exceeds max_rules");
+    if (rules.size() > e->rules_cap) {
+        dfree(e->d_rules); dfree(e->d_rstate);
+        e->rules_cap = (uint32_t)std::max<size_t>(rules.size(), 1024);
+        HIPCHK(hipMalloc(&e->d_rules, e->rules_cap * sizeof(DRule)));
+        HIPCHK(hipMalloc(&e->d_rstate, e->rules_cap * sizeof(RState)));
+    }
+    if (hot.size() > e->hot_cap) {
+        dfree(e->d_hot);
+        e->hot_cap = (uint32_t)std::max<size_t>(hot.size(), 1024);
+        HIPCHK(hipMalloc(&e->d_hot, e->hot_cap * sizeof(DHot)));
+    }
+    HIPCHK(hipDeviceSynchronize());
+    if (!rules.empty()) {
+        HIPCHK(hipMemcpy(e->d_rules, rules.data(), rules.size() * sizeof(DRule), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d_rstate, rst.data(), rst.size() * sizeof(RState), hipMemcpyHostToDevice));
+    }
+    if (!hot.empty()) HIPCHK(hipMemcpy(e->d_hot, hot.data(), hot.size() * sizeof(DHot), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_prog, prog.data(), R * sizeof(Prog), hipMemcpyHostToDevice));
+    e->n_dev_rules = (uint32_t)rules.size();
+    return SG_OK;
+}
+
+uint32_t intern(sg_engine* e, const std::string& name) {
+    auto it = e->ids.find(name);
+    if (it != e->ids.end()) return it->second;
+    uint32_t id = (uint32_t)e->names.size();
+    e->ids.emplace(name, id);
+    e->names.push_back(name);
+    return id;
+}
+
+template <class V> void resize_lists(sg_engine* e, V& v) {
+    if (v.size() < e->names.size()) v.resize(e->names.size());
+}
+
+} // namespace
+
+// =====================================================================================
+extern "C" {
+
+const char* sg_last_error(void) { return g_err.c_str(); }
+
+void sg_config_default(sg_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->sample_count = 2;
+    c->interval_ms = 1000;
+    c->statistic_max_rt = 4900;
+    c->cold_factor = 3;
+    c->occupy_timeout_ms = 500;
+    c->max_slot_chain_size = 6000;
+    c->switch_on = 1;
+    c->device = 0;
+    c->max_resources = 1u << 20;
+    c->max_rules = 1u << 21;
+    c->param_table_log2 = 22;
+    c->status_ring_log2 = 28;
+    c->max_batch_events = 1u << 25;
+    c->cluster_sample_count = 10;
+    c->cluster_interval_ms = 1000;
+    c->cluster_exceed_count = 1.0;
+    c->cluster_max_occupy_ratio = 1.0;
+    c->cluster_max_allowed_qps = 30000;
+}
+
+int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
+    if (!out) return fail(SG_EINVAL, "out is null");
+    sg_config cfg;
+    if (cfg_in) cfg = *cfg_in;
+    else sg_config_default(&cfg);
+    if (cfg.sample_count != 2 || cfg.interval_ms != 1000)
+        return fail(SG_ENOTSUP, "the device path implements SAMPLE_COUNT=2, INTERVAL=1000 (the reference defaults)");
+    if (cfg.cold_factor <= 1) return fail(SG_EINVAL, "cold factor must be > 1");
+    if (cfg.max_resources == 0 || cfg.param_table_log2 < 4 || cfg.param_table_log2 > 34 || cfg.status_ring_log2 < 10 ||
+        cfg.status_ring_log2 > 36)
+        return fail(SG_EINVAL, "bad capacity in sg_config");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SG_EDEVICE, "no HIP device visible");
+    if (cfg.device < 0 || cfg.device >= ndev) return fail(SG_EDEVICE, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg.device) != hipSuccess) return fail(SG_EDEVICE, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SG_EDEVICE, std::string("this build targets gfx950, found ") + prop.gcnArchName);
+    sg_engine* e = new sg_engine();
+    e->cfg = cfg;
+    e->device = cfg.device;
+    auto bad = [&](int rc) { sg_engine_destroy(e); return rc; };
+    if (hipSetDevice(e->device) != hipSuccess) return bad(fail(SG_EDEVICE, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+    for (auto& v : e->ev) if (hipEventCreate(&v) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
+    uint64_t R = cfg.max_resources;
+    if (hipMalloc(&e->d_sec, R * 2 * sizeof(Bkt)) != hipSuccess || hipMalloc(&e->d_minb, R * 60 * sizeof(Bkt)) != hipSuccess ||
+        hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
+        hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
+        hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess)
+        return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
+    if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_ring, 0, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
+        launch_init_state(e->d_sec, e->d_minb, e->d_info, (uint32_t)R, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        return bad(fail(SG_EDEVICE, "device initialisation failed"));
+    *out = e;
+    return SG_OK;
+}
+
+int sg_engine_destroy(sg_engine* e) {
+    if (!e) return SG_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
+    dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small);
+    dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
+    dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
+    dfree(e->d_cand); dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out);
+    for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return SG_OK;
+}
+
+int sg_register_resources(sg_engine* e, const char* const* names, uint32_t n, uint32_t* out_ids) {
+    if (!e || (n && !names)) return fail(SG_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!names[i]) return fail(SG_EINVAL, "null resource name");
+        auto it = e->ids.find(names[i]);
+        uint32_t id;
+        if (it != e->ids.end()) id = it->second;
+        else {
+            if (e->names.size() >= e->cfg.max_resources) return fail(SG_ECAPACITY, "max_resources reached");
+            id = intern(e, names[i]);
+        }
+        if (out_ids) out_ids[i] = id;
+    }
+    return SG_OK;
+}
+
+int sg_resource_id(sg_engine* e, const char* name, uint32_t* out_id) {
+    if (!e || !name || !out_id) return fail(SG_EINVAL, "null argument");
+    auto it = e->ids.find(name);
+    if (it == e->ids.end()) return fail(SG_ENOTFOUND, std::string("unknown resource ") + name);
+    *out_id = it->second;
+    return SG_OK;
+}
+
+int sg_param_key(sg_engine* e, const char* value, const char* class_type, uint64_t* out_key) {
+    (void)e;
+    if (!out_key) return fail(SG_EINVAL, "null out_key");
+    *out_key = param_key(value, class_type);
+    return SG_OK;
+}
+
+static int register_rule_resource(sg_engine* e, const char* name, uint32_t* id) {
+    auto it = e->ids.find(name);
+    if (it != e->ids.end()) { *id = it->second; return SG_OK; }
+    if (e->names.size() >= e->cfg.max_resources) return fail(SG_ECAPACITY, "max_resources reached");
+    *id = intern(e, name);
+    return SG_OK;
+}
+
+// FlowRuleManager.loadRules -> FlowRuleUtil.buildFlowRuleMap (core/slots/block/flow/FlowRuleUtil.java:89-137)
+int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    std::vector<std::string> keys(n);
+    for (uint32_t i = 0; i < n; ++i) keys[i] = flow_eqkey(rules[i]);
+    if (e->flow_loaded && keys == e->last_flow) { // DynamicSentinelProperty.updateValue: equal -> no-op
+        if (n_loaded) *n_loaded = (uint32_t)e->flows.size();
+        return SG_OK;
+    }
+    std::vector<FlowR> flows;
+    std::vector<std::vector<int>> per;
+    std::unordered_map<std::string, int> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_flow_rule& r = rules[i];
+        if (!flow_valid(r)) continue;
+        uint32_t rid;
+        int rc = register_rule_resource(e, r.resource, &rid);
+        if (rc) return rc;
+        std::string k = std::to_string(rid) + "#" + keys[i];
+        if (seen.count(k)) continue; // HashSet.add of an equal rule
+        seen[k] = 1;
+        FlowR f;
+        f.r = r;
+        f.res = r.resource;
+        f.la = la_norm(r.limit_app);
+        f.ref = sv(r.ref_resource);
+        f.hash = flow_hash(r);
+        f.eqkey = keys[i];
+        flows.push_back(f);
+        if (per.size() <= rid) per.resize(rid + 1);
+        per[rid].push_back((int)flows.size() - 1);
+    }
+    std::vector<int32_t> hs(flows.size());
+    for (size_t i = 0; i < flows.size(); ++i) hs[i] = flows[i].hash;
+    for (auto& l : per) {
+        hashset_order(hs, l);
+        // Collections.sort(rules, FlowRuleComparator) -- stable (FlowRuleComparator.java:30-55)
+        std::stable_sort(l.begin(), l.end(), [&](int a, int b) {
+            const FlowR &x = flows[a], &y = flows[b];
+            auto cmp = [](const FlowR& o1, const FlowR& o2) {
+                if (o1.r.cluster_mode && !o2.r.cluster_mode) return 1;
+                if (!o1.r.cluster_mode && o2.r.cluster_mode) return -1;
+                if (o1.la == o2.la) return 0;
+                if (o1.la == "default") return 1;
+                if (o2.la == "default") return -1;
+                return 0;
+            };
+            return cmp(x, y) < 0;
+        });
+    }
+    // publish
+    auto old_flows = std::move(e->flows);
+    auto old_per = std::move(e->res_flow);
+    e->flows = std::move(flows);
+    e->res_flow = std::move(per);
+    resize_lists(e, e->res_flow);
+    int rc = upload_rules(e, true, false);
+    if (rc) { e->flows = std::move(old_flows); e->res_flow = std::move(old_per); return rc; }
+    e->last_flow = keys;
+    e->flow_loaded = true;
+    if (n_loaded) *n_loaded = (uint32_t)e->flows.size();
+    return SG_OK;
+}
+
+// DegradeRuleManager.loadRules (core/slots/block/degrade/DegradeRuleManager.java:112-205)
+int sg_load_degrade_rules(sg_engine* e, const sg_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    std::vector<std::string> keys(n);
+    for (uint32_t i = 0; i < n; ++i) keys[i] = deg_eqkey(rules[i], (int)i);
+    bool has_nan = false;
+    for (uint32_t i = 0; i < n; ++i) has_nan |= rules[i].count != rules[i].count;
+    if (e->deg_loaded && !has_nan && keys == e->last_deg) {
+        if (n_loaded) *n_loaded = (uint32_t)e->degs.size();
+        return SG_OK;
+    }
+    std::vector<DegR> degs;
+    std::vector<std::vector<int>> per;
+    std::unordered_map<std::string, int> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_degrade_rule& r = rules[i];
+        if (blank(r.resource) || !(r.count >= 0) || r.time_window <= 0) continue; // isValidRule
+        uint32_t rid;
+        int rc = register_rule_resource(e, r.resource, &rid);
+        if (rc) return rc;
+        std::string k = std::to_string(rid) + "#" + keys[i];
+        if (seen.count(k)) continue;
+        seen[k] = 1;
+        DegR d;
+        d.r = r;
+        d.res = r.resource;
+        d.la = la_norm(r.limit_app);
+        d.hash = deg_hash(r);
+        d.eqkey = keys[i];
+        degs.push_back(d);
+        if (per.size() <= rid) per.resize(rid + 1);
+        per[rid].push_back((int)degs.size() - 1);
+    }
+    std::vector<int32_t> hs(degs.size());
+    for (size_t i = 0; i < degs.size(); ++i) hs[i] = degs[i].hash;
+    for (auto& l : per) hashset_order(hs, l);
+    auto od = std::move(e->degs);
+    auto op = std::move(e->res_deg);
+    e->degs = std::move(degs);
+    e->res_deg = std::move(per);
+    resize_lists(e, e->res_deg);
+    int rc = upload_rules(e, false, true);
+    if (rc) { e->degs = std::move(od); e->res_deg = std::move(op); return rc; }
+    e->last_deg = keys;
+    e->deg_loaded = true;
+    if (n_loaded) *n_loaded = (uint32_t)e->degs.size();
+    return SG_OK;
+}
+
+// ParamFlowRuleManager.loadRules (param/slots/block/flow/param/ParamFlowRuleManager.java:103-166)
+int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    std::vector<ParamR> all;
+    std::vector<std::string> keys;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (rules[i].n_items > 0 && !rules[i].items) return fail(SG_EINVAL, "param rule items pointer is null");
+        if (rules[i].has_param_idx && rules[i].param_idx < 0)
+            return fail(SG_ENOTSUP, "negative paramIdx is rewritten per call (ParamFlowSlot.applyRealParamIdx); "
+                                    "not on the device path yet");
+        all.push_back(make_param(rules[i]));
+        keys.push_back(all.back().eqkey);
+    }
+    if (e->par_loaded && keys == e->last_par) {
+        if (n_loaded) *n_loaded = (uint32_t)e->params.size();
+        return SG_OK;
+    }
+    std::vector<ParamR> ps;
+    std::vector<std::vector<int>> per;
+    std::unordered_map<std::string, int> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!param_valid(rules[i])) continue;
+        uint32_t rid;
+        int rc = register_rule_resource(e, rules[i].resource, &rid);
+        if (rc) return rc;
+        std::string k = std::to_string(rid) + "#" + keys[i];
+        if (seen.count(k)) continue;
+        seen[k] = 1;
+        ps.push_back(all[i]);
+        if (per.size() <= rid) per.resize(rid + 1);
+        per[rid].push_back((int)ps.size() - 1);
+    }
+    std::vector<int32_t> hs(ps.size());
+    for (size_t i = 0; i < ps.size(); ++i) hs[i] = ps[i].hash;
+    for (auto& l : per) hashset_order(hs, l);
+    // ParameterMetric lifetime: resources that had rules and now have none lose their metric
+    // (ParamFlowRuleManager.java:150-159); all metrics are cleared for an empty list.
+    if (e->tc_epoch.size() < e->names.size()) e->tc_epoch.resize(e->names.size(), 0);
+    std::vector<bool> now_has(e->names.size(), false);
+    for (size_t r = 0; r < per.size(); ++r) now_has[r] = !per[r].empty();
+    std::vector<uint64_t> clear_flags;
+    for (size_t r = 0; r < e->res_par.size(); ++r) {
+        bool had = !e->res_par[r].empty();
+        if ((had && !now_has[r]) || n == 0) {
+            e->tc_epoch[r] = e->next_epoch++;
+            for (auto it = e->psid_of.begin(); it != e->psid_of.end();) {
+                if (it->first.compare(0, e->names[r].size() + 1, e->names[r] + std::string("\0", 1)) == 0)
+                    it = e->psid_of.erase(it);
+                else ++it;
+            }
+            clear_flags.push_back(((uint64_t)(NI_PM | NI_TM0) << 32) | r);
+        }
+    }
+    for (auto& q : ps) {
+        std::string k = q.res + std::string("\0", 1) + q.eqkey;
+        if (!e->psid_of.count(k)) e->psid_of[k] = e->next_psid++;
+    }
+    auto op = std::move(e->params);
+    auto opr = std::move(e->res_par);
+    e->params = std::move(ps);
+    e->res_par = std::move(per);
+    resize_lists(e, e->res_par);
+    int rc = upload_rules(e, false, false);
+    if (rc) { e->params = std::move(op); e->res_par = std::move(opr); return rc; }
+    if (!clear_flags.empty()) {
+        uint64_t* d = nullptr;
+        HIPCHK(hipMalloc(&d, clear_flags.size() * 8));
+        HIPCHK(hipMemcpy(d, clear_flags.data(), clear_flags.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(launch_set_flags(e->d_info, d, (uint32_t)clear_flags.size(), e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        (void)hipFree(d);
+    }
+    e->last_par = keys;
+    e->par_loaded = true;
+    if (n_loaded) *n_loaded = (uint32_t)e->params.size();
+    return SG_OK;
+}
+
+static bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+    if (!e || (n && (!ev || !out))) return fail(SG_EINVAL, "null argument");
+    if (n == 0) return SG_OK;
+    if (n > e->cfg.max_batch_events || n >= (1ull << 32)) return fail(SG_EINVAL, "batch larger than max_batch_events");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = ensure_batch(e, n);
+    if (rc) return rc;
+    hipStream_t st = e->stream;
+    const sg_event* dev_ev = ev;
+    bool host_in = !is_device_ptr(ev);
+    bool host_out = !is_device_ptr(out);
+    if (host_in) {
+        HIPCHK(hipMemcpyAsync(e->d_ev, ev, n * sizeof(sg_event), hipMemcpyHostToDevice, st));
+        dev_ev = e->d_ev;
+    }
+    uint32_t* dev_out = host_out ? e->d_out : out;
+    HIPCHK(hipEventRecord(e->ev[0], st));
+    // ---- 1. group: LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
+    uint32_t R = e->cfg.max_resources;
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < R) ++bits;
+    int passes = (bits + 7) / 8;
+    uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
+    HIPCHK(hipMemsetAsync(e->d_small, 0, 256 * 4, st));
+    uint32_t *kin = nullptr, *vin = nullptr, *kout = e->d_k0, *vout = e->d_v0;
+    for (int p = 0; p < passes; ++p) {
+        const sg_event* pev = p == 0 ? dev_ev : nullptr;
+        HIPCHK(launch_radix_hist(pev, kin, n, p * 8, e->d_hist, nblocks, e->d_small + 0, R, st));
+        HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, st));
+        HIPCHK(launch_radix_scatter(pev, kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout, st));
+        kin = kout; vin = vout;
+        kout = (kin == e->d_k0) ? e->d_k1 : e->d_k0;
+        vout = (vin == e->d_v0) ? e->d_v1 : e->d_v0;
+    }
+    // ---- 2. segments
+    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_part, e->d_small + 1, e->d_segs, e->d_small + 3, st));
+    uint32_t small[68];
+    HIPCHK(hipMemcpyAsync(small, e->d_small, sizeof(small), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint32_t bflags = small[0], m = small[1];
+    if (bflags & BF_BAD_RES) return fail(SG_EINVAL, "event res_id >= max_resources");
+    if (bflags & BF_PRIORITIZED)
+        return fail(SG_ENOTSUP, "prioritized entries (StatisticNode.tryOccupyNext) are not on the device path yet");
+    if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
+    // descending length classes -> cursors
+    uint32_t cur[32];
+    uint32_t acc = 0;
+    for (int b = 31; b >= 0; --b) { cur[b] = acc; acc += small[3 + b]; }
+    HIPCHK(hipMemcpyAsync(e->d_small + 35, cur, sizeof(cur), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 35, e->d_order, st));
+    // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
+    DevCfg dc;
+    dc.max_rt = e->cfg.statistic_max_rt;
+    dc.occupy_timeout = e->cfg.occupy_timeout_ms;
+    dc.max_chain = e->cfg.max_slot_chain_size;
+    dc.switch_on = e->cfg.switch_on;
+    dc.ptab_mask = (1ull << e->cfg.param_table_log2) - 1;
+    dc.ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
+    if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
+        HIPCHK(launch_chain_candidates(dev_ev, vin, e->d_segs, m, e->d_info, e->d_small + 2, e->d_cand, st));
+        uint32_t ncand = 0;
+        HIPCHK(hipMemcpyAsync(&ncand, e->d_small + 2, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (ncand) {
+            std::vector<uint64_t> cand(ncand);
+            HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
+            std::sort(cand.begin(), cand.end()); // by batch index of the first ENTRY
+            std::vector<uint64_t> upd(ncand);
+            for (uint32_t i = 0; i < ncand; ++i) {
+                uint32_t res = (uint32_t)cand[i];
+                bool grant = e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
+                if (grant) e->n_chains++;
+                upd[i] = ((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63);
+            }
+            HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
+            HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+    }
+    HIPCHK(hipEventRecord(e->ev[1], st));
+    // ---- 3. decide
+    DevState S;
+    S.sec = e->d_sec;
+    S.minb = e->d_minb;
+    S.info = e->d_info;
+    S.prog = e->d_prog;
+    S.rules = e->d_rules;
+    S.rstate = e->d_rstate;
+    S.hot = e->d_hot;
+    S.ptab = e->d_ptab;
+    S.ring = e->d_ring;
+    HIPCHK(launch_decide(dev_ev, vin, e->d_segs, e->d_order, m, e->gbase, n, S, dc, dev_out, e->d_small + 0, st));
+    HIPCHK(hipEventRecord(e->ev[2], st));
+    if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
+    e->gbase += n;
+    return SG_OK;
+}
+
+int sg_sync(sg_engine* e) {
+    if (!e) return fail(SG_EINVAL, "null engine");
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->last_ms[0] = a;
+    if (hipEventElapsedTime(&b, e->ev[1], e->ev[2]) == hipSuccess) e->last_ms[1] = b;
+    e->last_ms[2] = e->last_ms[0] + e->last_ms[1];
+    (void)hipGetLastError();
+    uint32_t bflags = 0;
+    HIPCHK(hipMemcpy(&bflags, e->d_small, 4, hipMemcpyDeviceToHost));
+    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
+    return SG_OK;
+}
+
+int sg_submit(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+    int rc = sg_submit_async(e, ev, n, out);
+    if (rc) {
+        if (e) (void)hipStreamSynchronize(e->stream);
+        return rc;
+    }
+    return sg_sync(e);
+}
+
+int sg_last_timings(sg_engine* e, double* ms, int cap) {
+    if (!e || !ms) return 0;
+    int k = 0;
+    for (; k < cap && k < 3; ++k) ms[k] = e->last_ms[k];
+    return k;
+}
+
+int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out) {
+    (void)now_ms;
+    if (!e || !out) return fail(SG_EINVAL, "null argument");
+    if (res >= e->cfg.max_resources) return fail(SG_EINVAL, "res_id out of range");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    Bkt sec[2], mb[60];
+    NodeInfo ni;
+    HIPCHK(hipMemcpy(sec, e->d_sec + (uint64_t)res * 2, sizeof(sec), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(mb, e->d_minb + (uint64_t)res * 60, sizeof(mb), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&ni, e->d_info + res, sizeof(ni), hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof(*out));
+    auto ex = [](const Bkt& b, sg_bucket& o) {
+        if (b.ws < 0) { std::memset(&o, 0, sizeof(o)); o.window_start = -1; return; }
+        o.window_start = b.ws; o.pass = b.pass; o.block = b.block; o.exception = b.exc; o.success = b.succ;
+        o.rt = b.rt; o.occupied_pass = b.occ; o.min_rt = b.minrt;
+    };
+    for (int i = 0; i < 8; ++i) { out->second[i].window_start = -1; out->borrow[i].window_start = -1; }
+    bool chain = (ni.flags & NI_CHAIN) != 0;
+    if (chain) {
+        ex(sec[0], out->second[0]);
+        ex(sec[1], out->second[1]);
+        for (int i = 0; i < 60; ++i) ex(mb[i], out->minute[i]);
+    } else {
+        for (int i = 0; i < 60; ++i) out->minute[i].window_start = -1;
+    }
+    out->cur_thread_num = chain ? ni.thread : 0;
+    out->has_chain = chain ? 1 : 0;
+    return SG_OK;
+}
+
+int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return fail(SG_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(e->device));
+    uint32_t R = (uint32_t)std::min<size_t>(e->names.size(), e->cfg.max_resources);
+    if (R == 0) { *n = 0; return SG_OK; }
+    if (!e->d_snap_cnt) {
+        HIPCHK(hipMalloc(&e->d_snap_cnt, (uint64_t)e->cfg.max_resources * 4));
+        HIPCHK(hipMalloc(&e->d_snap_off, (uint64_t)e->cfg.max_resources * 4));
+    }
+    if (cap > e->snap_cap) {
+        dfree(e->d_snap_out);
+        HIPCHK(hipMalloc(&e->d_snap_out, std::max<uint64_t>(cap, 1) * sizeof(sg_metric_node)));
+        e->snap_cap = cap;
+    }
+    if (!e->d_part) { int rc = ensure_batch(e, 1); if (rc) return rc; }
+    HIPCHK(launch_snapshot(e->d_minb, e->d_info, R, now_ms, e->cfg.statistic_max_rt, e->d_snap_cnt, e->d_snap_off,
+                           e->d_part, e->d_small + 67, e->d_snap_out, cap, e->stream));
+    uint32_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, e->d_small + 67, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t k = std::min<uint64_t>(total, cap);
+    if (k && out) HIPCHK(hipMemcpy(out, e->d_snap_out, k * sizeof(sg_metric_node), hipMemcpyDeviceToHost));
+    *n = total;
+    return SG_OK;
+}
+
+int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected) {
+    (void)flow_id; (void)connected;
+    if (!e) return fail(SG_EINVAL, "null engine");
+    return fail(SG_ENOTSUP, "token server is not on the device path yet");
+}
+
+int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out) {
+    (void)reqs; (void)n; (void)out;
+    if (!e) return fail(SG_EINVAL, "null engine");
+    return fail(SG_ENOTSUP, "token server is not on the device path yet");
+}
+
+} // extern "C"

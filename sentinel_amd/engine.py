@@ -1,0 +1,175 @@
+"""Python binding of libsentinel_gpu.so (include/sentinel_gpu.h).
+
+The engine is the product: every decision is taken by the HIP kernels behind the
+C ABI.  There is no CPU fallback -- if the library or a gfx950 device is missing
+this module raises instead of computing anything.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
+_lib = None
+
+# every entry point declared in include/sentinel_gpu.h
+EXPORTS = (
+    "sg_config_default", "sg_engine_create", "sg_engine_destroy", "sg_register_resources", "sg_resource_id",
+    "sg_load_flow_rules", "sg_load_degrade_rules", "sg_load_param_rules", "sg_param_key", "sg_submit",
+    "sg_submit_async", "sg_sync", "sg_snapshot_metrics", "sg_cluster_set_connected_count",
+    "sg_cluster_request_tokens", "sg_read_node", "sg_last_error", "sg_last_timings",
+)
+
+
+class SentinelError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"sentinel_gpu error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SentinelError(A.SG_EDEVICE, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.sg_config_default.argtypes = [C.POINTER(A.SgConfig)]
+        L.sg_engine_create.argtypes = [C.POINTER(A.SgConfig), C.POINTER(C.c_void_p)]
+        L.sg_engine_destroy.argtypes = [P]
+        L.sg_register_resources.argtypes = [P, C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.sg_resource_id.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
+        L.sg_load_flow_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.sg_load_degrade_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.sg_load_param_rules.argtypes = [P, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.sg_param_key.argtypes = [P, C.c_char_p, C.c_char_p, C.POINTER(C.c_uint64)]
+        L.sg_submit.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_submit_async.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_sync.argtypes = [P]
+        L.sg_snapshot_metrics.argtypes = [P, C.c_int64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.sg_cluster_set_connected_count.argtypes = [P, C.c_int64, C.c_int32]
+        L.sg_cluster_request_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_read_node.argtypes = [P, C.c_uint32, C.c_int64, C.POINTER(A.SgNodeState)]
+        L.sg_last_error.restype = C.c_char_p
+        L.sg_last_timings.argtypes = [P, C.POINTER(C.c_double), C.c_int]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SentinelError(rc, (lib().sg_last_error() or b"").decode(errors="replace"))
+
+
+def default_config(**kw) -> A.SgConfig:
+    cfg = A.SgConfig()
+    lib().sg_config_default(C.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def param_key(value, class_type="java.lang.String") -> int:
+    out = C.c_uint64()
+    _check(lib().sg_param_key(None, None if value is None else str(value).encode(),
+                              None if class_type is None else class_type.encode(), C.byref(out)))
+    return out.value
+
+
+class Engine:
+    """One MI355X engine (one shard of resources on one GPU)."""
+
+    def __init__(self, **cfg):
+        self._cfg = default_config(**cfg)
+        h = C.c_void_p()
+        _check(lib().sg_engine_create(C.byref(self._cfg), C.byref(h)))
+        self.h = h
+        self.n_events = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sg_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- resources / rules
+    def register(self, name: str) -> int:
+        return self.register_many([name])[0]
+
+    def register_many(self, names) -> np.ndarray:
+        arr = (C.c_char_p * max(1, len(names)))(*[n.encode() if isinstance(n, str) else n for n in names])
+        out = np.zeros(len(names), dtype=np.uint32)
+        _check(lib().sg_register_resources(self.h, arr, len(names), out.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return out
+
+    def register_ptrs(self, names_ptr, n: int):
+        _check(lib().sg_register_resources(self.h, C.cast(names_ptr, C.POINTER(C.c_char_p)), n, None))
+
+    def resource_id(self, name: str) -> int:
+        out = C.c_uint32()
+        _check(lib().sg_resource_id(self.h, name.encode(), C.byref(out)))
+        return out.value
+
+    def _load(self, fn, rules, struct):
+        if isinstance(rules, tuple):  # (pointer, n) straight from tracegen
+            ptr, n = rules
+        else:
+            arr = (struct * max(1, len(rules)))(*rules)
+            ptr, n = C.cast(arr, C.c_void_p), len(rules)
+        out = C.c_uint32()
+        _check(fn(self.h, ptr, n, C.byref(out)))
+        return out.value
+
+    def load_flow_rules(self, rules) -> int:
+        return self._load(lib().sg_load_flow_rules, rules, A.SgFlowRule)
+
+    def load_degrade_rules(self, rules) -> int:
+        return self._load(lib().sg_load_degrade_rules, rules, A.SgDegradeRule)
+
+    def load_param_rules(self, rules) -> int:
+        return self._load(lib().sg_load_param_rules, rules, A.SgParamRule)
+
+    # ---- decisions
+    def submit(self, events: np.ndarray) -> np.ndarray:
+        ev = np.ascontiguousarray(events, dtype=A.EVENT_DTYPE)
+        out = np.zeros(len(ev), dtype=np.uint32)
+        _check(lib().sg_submit(self.h, ev.ctypes.data, len(ev), out.ctypes.data))
+        self.n_events += len(ev)
+        return out
+
+    def submit_ptr(self, ev_ptr: int, n: int, out_ptr: int, sync: bool = True):
+        """Device (or host) pointers, e.g. torch tensors' data_ptr()."""
+        if sync:
+            _check(lib().sg_submit(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr)))
+        else:
+            _check(lib().sg_submit_async(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr)))
+        self.n_events += n
+
+    def sync(self):
+        _check(lib().sg_sync(self.h))
+
+    def timings(self):
+        ms = (C.c_double * 3)()
+        k = lib().sg_last_timings(self.h, ms, 3)
+        return list(ms[:k])
+
+    def read_node(self, res: int, now: int = 0) -> dict:
+        st = A.SgNodeState()
+        _check(lib().sg_read_node(self.h, res, now, C.byref(st)))
+        return A.node_state_to_numpy(st)
+
+    def snapshot(self, now: int, cap: int = 1 << 16) -> np.ndarray:
+        out = np.zeros(cap, dtype=A.METRIC_NODE_DTYPE)
+        n = C.c_uint64()
+        _check(lib().sg_snapshot_metrics(self.h, int(now), out.ctypes.data, cap, C.byref(n)))
+        return out[: min(cap, n.value)]

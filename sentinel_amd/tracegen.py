@@ -1,0 +1,98 @@
+"""Seeded synthetic workloads, generated in C++.
+
+See sentinel_amd/csrc/tracegen.cpp for the trace model.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_trace.so")
+_lib = None
+
+SEED_BASE = 20240601  # seed 20240601 + config index
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            from . import build as _b
+            _b.build_trace()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.tg_create.restype = P
+        L.tg_create.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_double, C.c_int64, C.c_uint64]
+        L.tg_destroy.argtypes = [P]
+        L.tg_names.restype = C.c_void_p
+        L.tg_names.argtypes = [P, C.POINTER(C.c_uint32)]
+        for f in ("tg_flow_rules", "tg_degrade_rules", "tg_param_rules"):
+            getattr(L, f).restype = C.c_void_p
+            getattr(L, f).argtypes = [P, C.POINTER(C.c_uint32)]
+        L.tg_events.restype = C.c_void_p
+        L.tg_events.argtypes = [P, C.POINTER(C.c_uint64)]
+        L.tg_n_entries.restype = C.c_uint64
+        L.tg_n_entries.argtypes = [P]
+        L.tg_t_end.restype = C.c_int64
+        L.tg_t_end.argtypes = [P]
+        _lib = L
+    return _lib
+
+
+class Workload:
+    """A generated config: names, rules (as C arrays) and the event trace."""
+
+    def __init__(self, config: int, seed: int | None = None, n_res: int = 0, n_entries: int = 0, rate: float = 0.0,
+                 t0: int = 0, n_param_values: int = 0):
+        self.config = config
+        self.seed = SEED_BASE + config if seed is None else seed
+        self.h = lib().tg_create(config, self.seed, n_res, n_entries, rate, t0, n_param_values)
+        n = C.c_uint32()
+        self.names_ptr = lib().tg_names(self.h, C.byref(n))
+        self.n_res = n.value
+        self.flow = self._rules("tg_flow_rules")
+        self.degrade = self._rules("tg_degrade_rules")
+        self.param = self._rules("tg_param_rules")
+        ne = C.c_uint64()
+        ptr = lib().tg_events(self.h, C.byref(ne))
+        self.n_events = ne.value
+        if ne.value:
+            buf = (C.c_char * (ne.value * A.EVENT_DTYPE.itemsize)).from_address(ptr)
+            self.events = np.frombuffer(buf, dtype=A.EVENT_DTYPE)
+        else:
+            self.events = np.zeros(0, dtype=A.EVENT_DTYPE)
+        self.n_entries = int(lib().tg_n_entries(self.h))
+        self.t_end = int(lib().tg_t_end(self.h))
+
+    def _rules(self, fn):
+        n = C.c_uint32()
+        ptr = getattr(lib(), fn)(self.h, C.byref(n))
+        return (ptr, n.value)
+
+    def names(self):
+        arr = C.cast(self.names_ptr, C.POINTER(C.c_char_p))
+        return [arr[i].decode() for i in range(self.n_res)]
+
+    def install(self, target):
+        """Register names and load the rules into an Engine or an oracle (same calls)."""
+        target.register_ptrs(self.names_ptr, self.n_res)
+        for kind, (ptr, n) in (("flow", self.flow), ("degrade", self.degrade), ("param", self.param)):
+            if n:
+                getattr(target, "load_%s_rules" % kind)((C.c_void_p(ptr), n))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.events = None
+            lib().tg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,210 @@
+"""Parity of the HIP engine against the CPU oracle (bit-exact decisions and bucket counters).
+
+Every test replays the same seeded trace through the oracle (event-sequential CPU
+restatement) and through the C ABI on the GPU, in several batches, then compares
+the per-event decisions and the ClusterNode state of the hottest and of a random
+sample of resources field by field.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from sentinel_amd import _abi as A
+from sentinel_amd import engine as E
+from sentinel_amd import tracegen as T
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_123
+
+
+def _engine(**kw):
+    kw.setdefault("max_resources", 1 << 12)
+    kw.setdefault("param_table_log2", 18)
+    kw.setdefault("status_ring_log2", 24)
+    return E.Engine(**kw)
+
+
+def _replay(w, eng, orc, batches):
+    ev = w.events
+    cuts = np.linspace(0, len(ev), batches + 1).astype(np.int64)
+    dg, do = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        dg.append(eng.submit(ev[a:b]))
+        do.append(orc.submit(ev[a:b]))
+    return np.concatenate(dg), np.concatenate(do)
+
+
+def _assert_same_decisions(dg, do, ev):
+    bad = np.nonzero(dg != do)[0]
+    if len(bad):
+        i = bad[0]
+        raise AssertionError("decision mismatch at event %d (%s): gpu=%08x oracle=%08x; %d mismatches"
+                             % (i, ev[i], dg[i], do[i], len(bad)))
+
+
+def _compare_nodes(w, eng, orc, res_ids):
+    for r in res_ids:
+        g, o = eng.read_node(int(r)), orc.read_node(int(r))
+        assert g["has_chain"] == o["has_chain"], r
+        assert g["thread"] == o["thread"], (r, g["thread"], o["thread"])
+        np.testing.assert_array_equal(g["second"][:2], o["second"][:2], err_msg="second window of res %d" % r)
+        np.testing.assert_array_equal(g["minute"], o["minute"], err_msg="minute window of res %d" % r)
+
+
+def _sample(w, k=300, seed=0):
+    ev = w.events
+    cnt = np.bincount(ev["res_id"], minlength=w.n_res)
+    hot = np.argsort(-cnt)[:50]
+    rng = np.random.default_rng(seed)
+    touched = np.nonzero(cnt)[0]
+    rnd = rng.choice(touched, size=min(k, len(touched)), replace=False)
+    return np.unique(np.concatenate([hot, rnd]))
+
+
+def _run(config, batches=3, chain_cap=0, **kw):
+    w = T.Workload(config, **kw)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap)
+    orc = O.Oracle(max_slot_chain_size=chain_cap)
+    w.install(eng)
+    w.install(orc)
+    dg, do = _replay(w, eng, orc, batches)
+    _assert_same_decisions(dg, do, w.events)
+    _compare_nodes(w, eng, orc, _sample(w))
+    return w, eng, orc, dg
+
+
+def test_c1_flowqpsdemo():
+    # FlowQpsDemo (sentinel-demo-basic .../flow/FlowQpsDemo.java:37-66): ~20 pass/s under QPS=20
+    w, eng, orc, d = _run(1, batches=4)
+    st = d[w.events["kind"] == A.EV_ENTRY] & 0xFF
+    assert int((st == A.PASS).sum()) == 2000  # 20 pass/s for 100 s
+
+
+def test_c2_qps_default():
+    _run(2, batches=3, n_entries=400_000)
+
+
+def test_c3_mixed_controllers():
+    _run(3, batches=3, n_entries=400_000, n_res=20_000)
+
+
+def test_c4_degrade():
+    _run(4, batches=3, n_entries=400_000, n_res=50_000)
+
+
+def test_c5_param():
+    _run(5, batches=3, n_entries=400_000, n_param_values=50_000)
+
+
+def test_chain_cap_reference_default():
+    # Q1: only the first 6000 resources to enter get a slot chain (core/CtSph.java:206-227)
+    _run(2, batches=2, chain_cap=6000, n_entries=300_000)
+
+
+def test_many_small_batches_and_single_events():
+    w = T.Workload(4, n_entries=20_000, n_res=2_000)
+    eng = _engine(max_resources=w.n_res, max_slot_chain_size=0)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    ev = w.events
+    dg, do = [], []
+    i = 0
+    sizes = [1, 2, 3, 64, 65, 127, 1000, 4097]
+    k = 0
+    while i < len(ev):
+        s = sizes[k % len(sizes)]
+        dg.append(eng.submit(ev[i:i + s]))
+        do.append(orc.submit(ev[i:i + s]))
+        i += s
+        k += 1
+    dg, do = np.concatenate(dg), np.concatenate(do)
+    _assert_same_decisions(dg, do, ev)
+    _compare_nodes(w, eng, orc, _sample(w, 200))
+
+
+# ------------------------------------------------------------------ reference scenarios on the device
+def _ev(rows):
+    a = np.zeros(len(rows), dtype=A.EVENT_DTYPE)
+    for i, (ts, res, kind, count, flags, aux) in enumerate(rows):
+        a[i] = (ts, res, count, kind, flags, aux)
+    return a
+
+
+def test_flow_qps_grade_scenario():
+    # core-test/slots/block/flow/FlowPartialIntegrationTest.java:51-73 through the C ABI
+    eng = _engine()
+    rid = eng.register("testQPSGrade")
+    eng.load_flow_rules([A.flow_rule("testQPSGrade", 1)])
+    d = eng.submit(_ev([(T0, rid, A.EV_ENTRY, 1, 0, 0), (T0, rid, A.EV_EXIT, 1, 0, A.aux_exit(0, 0)),
+                        (T0, rid, A.EV_ENTRY, 1, 0, 0)]))
+    assert [x & 0xFF for x in d] == [A.PASS, A.NOT_ENTRY, A.BLOCK_FLOW]
+
+
+def test_thread_grade_scenario():
+    # FlowPartialIntegrationTest.java:75-116
+    eng = _engine()
+    rid = eng.register("testThreadGrade")
+    eng.load_flow_rules([A.flow_rule("testThreadGrade", 1, grade=A.FLOW_GRADE_THREAD)])
+    d = eng.submit(_ev([(T0, rid, A.EV_ENTRY, 1, 0, 0), (T0 + 1, rid, A.EV_ENTRY, 1, 0, 0),
+                        (T0 + 100, rid, A.EV_EXIT, 1, 0, A.aux_exit(0, 100)), (T0 + 101, rid, A.EV_ENTRY, 1, 0, 0)]))
+    assert [x & 0xFF for x in d] == [A.PASS, A.BLOCK_FLOW, A.NOT_ENTRY, A.PASS]
+    assert eng.read_node(rid)["thread"] == 1
+
+
+def test_param_burst_scenario():
+    # param-test/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:69-137 through the C ABI
+    eng = _engine()
+    rid = eng.register("burst")
+    eng.load_param_rules([A.param_rule("burst", 0, 5, burst_count=3)])
+    k = E.param_key("valueA")
+    rows, expect = [], []
+    now = T0
+    for step, npass in [(0, 8), (1002, 5), (1002, 5), (2000, 8), (1002, 5)]:
+        now += step
+        for _ in range(npass + 1):
+            rows.append((now, rid, A.EV_ENTRY, 1, A.F_HAS_ARG, k))
+        expect += [A.PASS] * npass + [A.BLOCK_PARAM]
+    d = eng.submit(_ev(rows))
+    assert [x & 0xFF for x in d] == expect
+
+
+def test_degrade_rt_scenario():
+    # DegradeRule RT breaker (core/slots/block/degrade/DegradeRule.java:181-193): 5 consecutive
+    # checks over the threshold cut the resource for timeWindow seconds.
+    eng = _engine()
+    orc = O.Oracle()
+    rows = []
+    for eng_or_orc in (eng, orc):
+        eng_or_orc.register("rt")
+        eng_or_orc.load_degrade_rules([A.degrade_rule("rt", 10, 2)])
+    gi = 0
+    t = T0
+    # one slow call, then a stream of entries
+    rows.append((t, 0, A.EV_ENTRY, 1, 0, 0))
+    rows.append((t + 50, 0, A.EV_EXIT, 1, 0, A.aux_exit(0, 50)))
+    for i in range(12):
+        rows.append((t + 60 + i, 0, A.EV_ENTRY, 1, 0, 0))
+    rows.append((t + 2100, 0, A.EV_ENTRY, 1, 0, 0))
+    rows.append((t + 3000, 0, A.EV_ENTRY, 1, 0, 0))
+    ev = _ev(rows)
+    dg, do = eng.submit(ev), orc.submit(ev)
+    np.testing.assert_array_equal(dg, do)
+    st = [x & 0xFF for x in dg]
+    assert st[2:6] == [A.PASS] * 4 and st[6] == A.BLOCK_DEGRADE
+
+
+def test_snapshot_matches_oracle():
+    w = T.Workload(2, n_entries=100_000, n_res=500)
+    eng = _engine(max_resources=w.n_res, max_slot_chain_size=0)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    eng.submit(w.events)
+    orc.submit(w.events)
+    for now in (w.t_end + 10, w.t_end + 1500, w.t_end + 70000):
+        sg = eng.snapshot(now)
+        so = orc.snapshot(now)
+        key = lambda a: np.lexsort((a["timestamp"], a["res_id"]))
+        np.testing.assert_array_equal(sg[key(sg)], so[key(so)])
