@@ -64,7 +64,7 @@ def _sample(w, k=300, seed=0):
 
 def _run(config, batches=3, chain_cap=0, **kw):
     w = T.Workload(config, **kw)
-    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap, param_table_log2=21)
     orc = O.Oracle(max_slot_chain_size=chain_cap)
     w.install(eng)
     w.install(orc)
