@@ -13,6 +13,7 @@
 // used to check it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/sentinel_gpu.h"
 #include "dev_types.h"
@@ -815,6 +816,547 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide(const sg_event* __r
     for (int i = W.lane; i < nr; i += WAVE) S.rstate[W.prog.rule_off + i] = W.rs[i];
 }
 
+
+// =================================================================================
+// 3b. decide, speculative: Jacobi rounds over the 64 staged events
+// ---------------------------------------------------------------------------------
+// Every lane evaluates the slot chain for its own event against the state it would
+// see if every earlier lane of the round had the outcome currently *guessed* for it
+// (prefix scans of the counter deltas, max-plus scans for the rate limiters,
+// run-length scans for the RT breaker).  The first lane whose evaluated outcome
+// differs from its guess is exact (all earlier guesses were right), so lanes up to
+// and including it are committed; the rest are re-guessed with their evaluated
+// outcomes and the round repeats.  A round never crosses a 500 ms bucket or a
+// breaker reset time, so bucket rotation and ResetTask stay serial points.
+// Resources with param rules take the serial path (per-value hash-table state).
+// =================================================================================
+__device__ __forceinline__ uint32_t wex_u32(uint32_t v, uint32_t lane) {
+    uint32_t x = v;
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x - v;
+}
+__device__ __forceinline__ int64_t wex_i64(int64_t v, uint32_t lane) {
+    int64_t x = v;
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x - v;
+}
+// exclusive prefix max (identity lo)
+__device__ __forceinline__ int64_t wexmax_i64(int64_t v, int64_t lo, uint32_t lane) {
+    int64_t x = v;
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x = x > y ? x : y;
+    }
+    int64_t e = __shfl_up(x, 1, 64);
+    return lane == 0 ? lo : e;
+}
+__device__ __forceinline__ int32_t wexmax_i32(int32_t v, int32_t lo, uint32_t lane) {
+    int32_t x = v;
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x = x > y ? x : y;
+    }
+    int32_t e = __shfl_up(x, 1, 64);
+    return lane == 0 ? lo : e;
+}
+__device__ __forceinline__ int64_t wsum_i64(int64_t v) {
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int64_t wmin_i64(int64_t v) {
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) { int64_t y = __shfl_xor(v, o, 64); v = v < y ? v : y; }
+    return v;
+}
+__device__ __forceinline__ int64_t wmax_i64(int64_t v) {
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) { int64_t y = __shfl_xor(v, o, 64); v = v > y ? v : y; }
+    return v;
+}
+
+#define NEG_INF64 ((int64_t)0x8000000000000000LL)
+
+// per-stage uniform info kept in registers for the round (up to MAX_RULES_PER_RES)
+struct SpecRound {
+    // base counters of the second window visible at the round's times (prev bucket + current bucket)
+    int64_t P, B, S, RT, E;
+    int64_t TH;       // thread count
+    int64_t EM;       // minute exception total (EXC_COUNT)
+    int64_t prev_pass_sec; // previous-second pass (WarmUp)
+};
+
+// evaluates every lane of the round under the guesses g; returns the lane outcome
+// (stage index that blocked, or nr for pass) and the queueing wait for entries.
+__device__ __forceinline__ uint32_t spec_eval(Wave& W, const SpecRound& R, const DRule* rules, int nr, uint32_t lane,
+                                              bool inr, bool is_entry, bool eff, uint32_t kind, int64_t t, int cnt,
+                                              int64_t rtv, uint32_t g, int64_t& wait_out, const RState* synced,
+                                              const bool* has_sync) {
+    // ---- counter prefixes under the guesses
+    bool gpass = inr && is_entry && g == (uint32_t)nr;
+    bool gblock = inr && is_entry && g != (uint32_t)nr;
+    bool eexit = inr && kind == SG_EV_EXIT && eff;
+    bool etrace = inr && kind == SG_EV_TRACE && eff && cnt > 0;
+    int64_t P = R.P + (int64_t)wex_u32(gpass ? (uint32_t)cnt : 0u, lane);
+    int64_t B = R.B + (int64_t)wex_u32(gblock ? (uint32_t)cnt : 0u, lane);
+    int64_t S = R.S + (int64_t)wex_u32(eexit ? (uint32_t)cnt : 0u, lane);
+    int64_t RT = R.RT + (int64_t)wex_u32(eexit ? (uint32_t)rtv : 0u, lane);
+    int64_t E = R.E + (int64_t)wex_u32(etrace ? (uint32_t)cnt : 0u, lane);
+    int64_t EM = R.EM + (int64_t)wex_u32(etrace ? (uint32_t)cnt : 0u, lane);
+    int32_t dth = gpass ? 1 : (eexit ? -1 : 0);
+    int64_t TH = R.TH + (int64_t)(int32_t)wex_u32((uint32_t)dth, lane);
+
+    uint32_t out = (uint32_t)nr;
+    bool alive = inr && is_entry;
+    int64_t wait = 0;
+    for (int s = 0; s < nr; ++s) {
+        const DRule r = rules[s];
+        bool reach_g = inr && is_entry && g >= (uint32_t)s;  // other lanes, by guess
+        bool pass_g = inr && is_entry && g > (uint32_t)s;
+        bool ok = true;
+        if (r.kind == RK_FLOW) {
+            switch (r.behavior) {
+            case SG_CONTROL_BEHAVIOR_WARM_UP: {
+                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                int64_t pq = P;
+                if (st.a >= r.warning_token) ok = (double)(pq + cnt) <= warm_qps(r, st.a);
+                else ok = (double)(pq + cnt) <= r.count;
+                break;
+            }
+            case SG_CONTROL_BEHAVIOR_RATE_LIMITER:
+            case SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER: {
+                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                int64_t cost;
+                if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {
+                    cost = (cnt <= 0 || r.count <= 0) ? 0 : j_round(1.0 * cnt / r.count * 1000);
+                } else {
+                    if (st.a >= r.warning_token) cost = j_round(1.0 * cnt / warm_qps(r, st.a) * 1000);
+                    else cost = j_round(1.0 * cnt / r.count * 1000);
+                }
+                bool upd = pass_g && (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || (cnt > 0 && r.count > 0));
+                int64_t C = wex_i64(upd ? cost : 0, lane);
+                int64_t M = wexmax_i64(upd ? t - (C + cost) : NEG_INF64, NEG_INF64, lane);
+                int64_t L0 = W.rs[s].c;
+                int64_t L = C + (M > L0 ? M : L0);
+                if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && cnt <= 0) { ok = true; break; }
+                if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && r.count <= 0) { ok = false; break; }
+                int64_t expected = L + cost;
+                if (expected <= t) ok = true;
+                else {
+                    int64_t w = expected - t;
+                    ok = w <= r.max_queue;
+                    if (ok && alive) wait += w;
+                }
+                break;
+            }
+            default: {
+                int32_t cur = r.grade == SG_FLOW_GRADE_THREAD ? (int32_t)TH : j_d2i((double)P);
+                ok = !((double)j_iadd(cur, cnt) > r.count);
+            }
+            }
+        } else if (r.kind == RK_DEGRADE) {
+            // lane-local check value (only meaningful where the lane checks)
+            bool bad;
+            if (r.grade == SG_DEGRADE_GRADE_RT) {
+                double avg = S == 0 ? 0.0 : (double)RT * 1.0 / (double)S;
+                bad = !(avg < r.count);
+            } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+                double exc = (double)E / 1.0, succ = (double)S / 1.0;
+                double total = (double)P / 1.0 + (double)B / 1.0;
+                if (total < 5) bad = false;
+                else if (succ - exc <= 0 && exc < 5) bad = false;
+                else bad = !(exc / succ < r.count);
+            } else {
+                bad = !((double)EM < r.count);
+            }
+            // cut before this lane: at round start, or a guessed trip of an earlier lane
+            bool trip_g = inr && is_entry && g == (uint32_t)s;
+            uint64_t trips = __ballot(trip_g);
+            uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            bool cut = W.rs[s].a != 0 || (trips & lt) != 0;
+            if (cut) { ok = false; }
+            else if (r.grade == SG_DEGRADE_GRADE_RT) {
+                // passCount before this lane: highs since the last low among checking lanes
+                bool chk = reach_g;  // lanes before the first guessed trip (later ones are cut)
+                bool low_g = chk && !bad;
+                bool high_g = chk && bad;
+                int32_t last_low = wexmax_i32(low_g ? (int32_t)lane : -1, -1, lane);
+                uint32_t highs = wex_u32(high_g ? 1u : 0u, lane);
+                int64_t pc;
+                if (last_low < 0) pc = W.rs[s].b + highs;
+                else {
+                    uint32_t h_at = __shfl(highs, last_low, 64);
+                    pc = (int64_t)(highs - h_at); // highs strictly after last_low (last_low itself is low)
+                }
+                ok = !bad || (pc + 1 < 5);
+            } else {
+                ok = !bad;
+            }
+        } else {
+            ok = true; // param rules never reach this path
+        }
+        if (alive && !ok) { out = (uint32_t)s; alive = false; }
+    }
+    wait_out = wait;
+    return out;
+}
+
+// reductions of the committed lanes into the wavefront state
+__device__ __forceinline__ void spec_commit(Wave& W, const SpecRound& R, const DRule* rules, int nr, uint32_t lane,
+                                            bool com, bool is_entry, bool eff, uint32_t kind, int64_t t, int cnt,
+                                            int64_t rtv, uint32_t g, int64_t tc0, const RState* synced,
+                                            const bool* has_sync, int64_t T) {
+    bool cpass = com && is_entry && g == (uint32_t)nr;
+    bool cblock = com && is_entry && g != (uint32_t)nr;
+    bool cexit = com && kind == SG_EV_EXIT && eff;
+    bool ctrace = com && kind == SG_EV_TRACE && eff && cnt > 0;
+    int64_t dP = wsum_i64(cpass ? cnt : 0);
+    int64_t dB = wsum_i64(cblock ? cnt : 0);
+    int64_t dS = wsum_i64(cexit ? cnt : 0);
+    int64_t dRT = wsum_i64(cexit ? rtv : 0);
+    int64_t dE = wsum_i64(ctrace ? cnt : 0);
+    int64_t dTH = wsum_i64(cpass ? 1 : (cexit ? -1 : 0));
+    int64_t mrt = wmin_i64(cexit ? rtv : INT64_MAX);
+    const bool touch = __ballot(cpass || cblock || cexit || ctrace) != 0;
+    int sl = -1;
+    if (touch) {
+        sl = sec_current(W, tc0);
+        min_current(W, tc0);
+    }
+    if (sl >= 0) {
+        Bkt& b = W.sb[sl];
+        b.pass += dP; b.block += dB; b.succ += dS; b.rt += dRT; b.exc += dE;
+        if (mrt < b.minrt) b.minrt = mrt;
+    }
+    if (touch && !W.mdetached) {
+        W.mb.pass += dP; W.mb.block += dB; W.mb.succ += dS; W.mb.rt += dRT; W.mb.exc += dE;
+        if (mrt < W.mb.minrt) W.mb.minrt = mrt;
+        if (dP | dB | dS | dRT | dE | (mrt != INT64_MAX)) W.mdirty = true;
+        if (W.exc_sum_sec == T) W.exc_sum += dE;
+    }
+    W.thread += (int32_t)dTH;
+    // rule state
+    for (int s = 0; s < nr; ++s) {
+        const DRule r = rules[s];
+        bool reach = com && is_entry && g >= (uint32_t)s;
+        bool pass = com && is_entry && g > (uint32_t)s;
+        bool any_reach = __ballot(reach) != 0;
+        if (r.kind == RK_FLOW) {
+            if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
+                if (any_reach && has_sync[s]) { W.rs[s].a = synced[s].a; W.rs[s].b = synced[s].b; }
+            }
+            if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER || r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
+                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                int64_t cost;
+                if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {
+                    cost = (cnt <= 0 || r.count <= 0) ? 0 : j_round(1.0 * cnt / r.count * 1000);
+                } else {
+                    if (st.a >= r.warning_token) cost = j_round(1.0 * cnt / warm_qps(r, st.a) * 1000);
+                    else cost = j_round(1.0 * cnt / r.count * 1000);
+                }
+                bool upd = pass && (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || (cnt > 0 && r.count > 0));
+                int64_t C = wex_i64(upd ? cost : 0, lane);
+                int64_t v = upd ? t - (C + cost) : NEG_INF64;
+                int64_t Ctot = wsum_i64(upd ? cost : 0);
+                int64_t Mall = wmax_i64(v);
+                int64_t L0 = W.rs[s].c;
+                W.rs[s].c = Ctot + (Mall > L0 ? Mall : L0);
+            }
+        } else if (r.kind == RK_DEGRADE) {
+            if (W.rs[s].a) continue; // cut for the whole round: no state change
+            bool trip = com && is_entry && g == (uint32_t)s;
+            uint64_t trips = __ballot(trip);
+            if (r.grade == SG_DEGRADE_GRADE_RT) {
+                // recompute the lanes' high/low against committed prefixes
+                int64_t S2 = R.S + (int64_t)wex_u32(cexit ? (uint32_t)cnt : 0u, lane);
+                int64_t RT2 = R.RT + (int64_t)wex_u32(cexit ? (uint32_t)rtv : 0u, lane);
+                double avg = S2 == 0 ? 0.0 : (double)RT2 * 1.0 / (double)S2;
+                bool bad = !(avg < r.count);
+                int ft = trips ? __ffsll((long long)trips) - 1 : 64;
+                bool chk = reach && (int)lane <= ft;
+                uint64_t lows = __ballot(chk && !bad);
+                uint64_t highs = __ballot(chk && bad);
+                if (lows) {
+                    int last_low = 63 - __clzll((long long)lows);
+                    uint64_t after = last_low == 63 ? 0ull : (~0ull << (last_low + 1));
+                    W.rs[s].b = __popcll(highs & after);
+                } else {
+                    W.rs[s].b += __popcll(highs);
+                }
+            }
+            if (trips) {
+                int j = __ffsll((long long)trips) - 1;
+                int64_t tj = (int64_t)rl64((uint64_t)t, j);
+                W.rs[s].a = 1;
+                W.rs[s].c = tj + (int64_t)r.time_window * 1000;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, uint32_t o, int64_t wait) {
+    if (o == (uint32_t)nr) return mk_dec(ST_PASS, 0, wait);
+    DRule r = rules[o];
+    uint32_t st = r.kind == RK_FLOW ? ST_BLOCK_FLOW : r.kind == RK_DEGRADE ? ST_BLOCK_DEGRADE : ST_BLOCK_PARAM;
+    return mk_dec(st, r.slot, 0);
+}
+
+__global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event* __restrict__ ev,
+                                                                const uint32_t* __restrict__ vals,
+                                                                const Seg* __restrict__ segs,
+                                                                const uint32_t* __restrict__ order, uint32_t m,
+                                                                uint64_t gbase, uint64_t n, DevState S, DevCfg cfg,
+                                                                uint32_t* __restrict__ out,
+                                                                uint32_t* __restrict__ bflags) {
+    __shared__ RState lds_rs[DEC_WAVES][MAX_RULES_PER_RES];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t sidx = blockIdx.x * DEC_WAVES + wv;
+    if (sidx >= m) return;
+    Wave W;
+    W.S = S;
+    W.cfg = cfg;
+    W.lane = lane_id();
+    W.bflags = bflags;
+    Seg sg = segs[order[sidx]];
+    W.res = sg.res;
+    W.prog = S.prog[W.res];
+    W.rs = lds_rs[wv];
+    const int nr = W.prog.n_param + W.prog.n_flow + W.prog.n_degrade;
+    for (int i = W.lane; i < nr; i += WAVE) W.rs[i] = S.rstate[W.prog.rule_off + i];
+    W.sb[0] = S.sec[(uint64_t)W.res * 2 + 0];
+    W.sb[1] = S.sec[(uint64_t)W.res * 2 + 1];
+    NodeInfo ni = S.info[W.res];
+    W.thread = ni.thread;
+    W.flags = ni.flags;
+    W.exc_sum_sec = ni.exc_sum_sec;
+    W.exc_sum = ni.exc_sum;
+    W.mslot = -1;
+    W.mdirty = false;
+    W.mdetached = false;
+    __builtin_amdgcn_wave_barrier();
+    const DRule* rules = S.rules + W.prog.rule_off;
+    const bool serial = W.prog.n_param > 0;
+    const uint32_t lane = W.lane;
+    uint32_t last_out = (uint32_t)nr;
+
+    // software prefetch of the next tile
+    uint32_t nidx = 0;
+    uint64_t n_ts = 0, n_w1 = 0, n_aux = 0;
+    {
+        uint32_t c1 = sg.len < WAVE ? sg.len : WAVE;
+        if (lane < c1) {
+            nidx = vals[sg.start + lane];
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(ev + nidx);
+            n_ts = p[0]; n_w1 = p[1]; n_aux = p[2];
+        }
+    }
+    for (uint32_t base = 0; base < sg.len; base += WAVE) {
+        const uint32_t cnt_t = sg.len - base < WAVE ? sg.len - base : WAVE;
+        const uint32_t idx = nidx;
+        const int64_t t = (int64_t)n_ts;
+        const uint64_t w1 = n_w1, aux = n_aux;
+        if (base + WAVE < sg.len) {
+            uint32_t c2 = sg.len - base - WAVE < WAVE ? sg.len - base - WAVE : WAVE;
+            if (lane < c2) {
+                nidx = vals[sg.start + base + WAVE + lane];
+                const uint64_t* p = reinterpret_cast<const uint64_t*>(ev + nidx);
+                n_ts = p[0]; n_w1 = p[1]; n_aux = p[2];
+            }
+        }
+        const bool valid = lane < cnt_t;
+        const int cnt = (int)((w1 >> 32) & 0xFFFFu);
+        const uint32_t kind = valid ? (uint32_t)((w1 >> 48) & 0xFF) : 0xFFu;
+        const uint8_t fl = (uint8_t)(w1 >> 56);
+        const bool is_entry = valid && kind == SG_EV_ENTRY;
+        const uint64_t gidx = gbase + idx;
+        // resolve EXIT/TRACE references: a lane of this tile, or a decided status
+        int refl = -1;
+        bool known_ok = true;
+        int64_t rtv = 0;
+        {
+            // all lanes take part in the shuffles (ds_bpermute does not read inactive lanes)
+            const bool is_ref = valid && kind != SG_EV_ENTRY;
+            const uint64_t ref = is_ref ? (aux & SG_REF_NONE) : SG_REF_NONE;
+            if (is_ref && kind == SG_EV_EXIT) {
+                int64_t raw = (int64_t)(aux >> 48);
+                rtv = raw > cfg.max_rt ? cfg.max_rt : raw;
+            }
+            const uint64_t g0 = rl64(gidx, 0);
+            const bool in_tile = ref != SG_REF_NONE && ref >= g0 && ref < gidx;
+            int lo = 0, hi = in_tile ? (int)lane : 0;  // gidx strictly increasing across the tile
+            #pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                int mid = (lo + hi) >> 1;
+                uint64_t gm = (uint64_t)__shfl((long long)gidx, mid, 64);
+                if (lo < hi) { if (gm < ref) lo = mid + 1; else hi = mid; }
+            }
+            uint64_t gl = (uint64_t)__shfl((long long)gidx, lo, 64);
+            if (in_tile) {
+                if (gl == ref) refl = lo;
+                else known_ok = false; // not an entry of this resource
+            } else if (ref != SG_REF_NONE) {
+                uint8_t st8 = S.ring[ref & cfg.ring_mask];
+                known_ok = (st8 == ST_PASS || st8 == ST_PASS_WAIT);
+            }
+        }
+        uint32_t g = is_entry ? last_out : 0u;  // outcome guesses
+        uint32_t dec = mk_dec(ST_NOT_ENTRY, 0, 0);
+        uint32_t fin = ST_NOT_ENTRY;             // final status per lane (entries)
+        int64_t lwait = 0;
+        uint32_t c0 = 0;
+        const bool chain = (W.flags & NI_CHAIN) != 0 && cfg.switch_on;
+        if (!chain) {
+            if (is_entry) { dec = mk_dec(ST_NO_CHECK, 0, 0); fin = ST_NO_CHECK; }
+            c0 = cnt_t;
+        }
+        while (c0 < cnt_t) {
+            const int64_t tc0 = (int64_t)rl64((uint64_t)t, (int)c0);
+            if (serial) {
+                // one event through the serial chain (param rules)
+                uint32_t kc0 = (uint32_t)__builtin_amdgcn_readlane((int)kind, (int)c0);
+                int cc0 = __builtin_amdgcn_readlane(cnt, (int)c0);
+                uint8_t fc0 = (uint8_t)__builtin_amdgcn_readlane((int)fl, (int)c0);
+                uint64_t ac0 = rl64(aux, (int)c0);
+                if (kc0 == SG_EV_ENTRY) {
+                    uint32_t d = do_entry(W, tc0, cc0, fc0, ac0);
+                    if (lane == c0) { dec = d; fin = d & 0xFF; }
+                } else {
+                    int rl = __builtin_amdgcn_readlane(refl, (int)c0);
+                    int ko = __builtin_amdgcn_readlane((int)known_ok, (int)c0);
+                    bool ok;
+                    if (rl >= 0) {
+                        uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)fin, rl);
+                        ok = s == ST_PASS || s == ST_PASS_WAIT;
+                    } else ok = ko != 0;
+                    if (ok) {
+                        if (kc0 == SG_EV_EXIT) do_exit(W, tc0, cc0, (int64_t)rl64((uint64_t)rtv, (int)c0));
+                        else do_trace(W, tc0, cc0);
+                    }
+                }
+                ++c0;
+                continue;
+            }
+            // breaker resets due at tc0 (ResetTask, Q12) and the next reset time
+            int64_t next_reset = INT64_MAX;
+            for (int s = W.prog.n_param + W.prog.n_flow; s < nr; ++s) {
+                if (W.rs[s].a && tc0 >= W.rs[s].c) { W.rs[s].a = 0; W.rs[s].b = 0; }
+                if (W.rs[s].a && W.rs[s].c < next_reset) next_reset = W.rs[s].c;
+            }
+            const int64_t b0 = tc0 / 500;
+            const bool inr = valid && lane >= c0 && (t / 500) == b0 && t < next_reset;
+            const uint64_t rmask = __ballot(inr);
+            const uint32_t e_end = c0 + (uint32_t)__popcll(rmask);
+            // base state of the round (buckets are only created/reset by events that write them)
+            const bool has_entry = __ballot(inr && is_entry) != 0;
+            const int64_t T = tc0 - tc0 % 1000;
+            SpecRound R;
+            {
+                const int cs = (int)(b0 & 1);
+                const Bkt& cur = W.sb[cs];
+                const Bkt& prv = W.sb[cs ^ 1];
+                bool cv = cur.ws == b0 * 500;
+                bool pv = prv.ws >= 0 && tc0 - prv.ws <= 1000 && prv.ws <= tc0;
+                R.P = (cv ? cur.pass : 0) + (pv ? prv.pass : 0);
+                R.B = (cv ? cur.block : 0) + (pv ? prv.block : 0);
+                R.S = (cv ? cur.succ : 0) + (pv ? prv.succ : 0);
+                R.RT = (cv ? cur.rt : 0) + (pv ? prv.rt : 0);
+                R.E = (cv ? cur.exc : 0) + (pv ? prv.exc : 0);
+            }
+            R.TH = W.thread;
+            R.EM = (has_entry && (W.prog.pflags & PF_EXC_COUNT)) ? min_total_exc(W, tc0) : 0;
+            RState synced[MAX_RULES_PER_RES];
+            bool has_sync[MAX_RULES_PER_RES];
+            R.prev_pass_sec = 0;
+            bool need_prev = false;
+            for (int s = 0; s < nr; ++s) {
+                has_sync[s] = false;
+                const DRule r = rules[s];
+                if (has_entry && r.kind == RK_FLOW && (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP ||
+                                                       r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)) {
+                    if (T > W.rs[s].b) {
+                        if (!need_prev) { R.prev_pass_sec = min_prev_pass(W, tc0); need_prev = true; }
+                        synced[s] = W.rs[s];
+                        warm_sync(r, synced[s], tc0, R.prev_pass_sec);
+                        has_sync[s] = true;
+                    }
+                }
+            }
+            // exits/traces: effectiveness under the guesses (referenced lane may be in this round)
+            for (;;) {
+                uint32_t gref = (uint32_t)__shfl((int)g, refl < 0 ? 0 : refl, 64);
+                uint32_t fref = (uint32_t)__shfl((int)fin, refl < 0 ? 0 : refl, 64);
+                bool eff;
+                if (refl < 0) eff = known_ok;
+                else if ((uint32_t)refl < c0) eff = (fref == ST_PASS || fref == ST_PASS_WAIT);
+                else eff = gref == (uint32_t)nr;
+                int64_t wt = 0;
+                uint32_t o = spec_eval(W, R, rules, nr, lane, inr, is_entry, eff, kind, t, cnt, rtv, g, wt, synced,
+                                       has_sync);
+                uint64_t mism = __ballot(inr && is_entry && o != g);
+                uint32_t cend = e_end;
+                if (mism) cend = (uint32_t)(__ffsll((long long)mism) - 1) + 1;
+                // Jacobi update of the guesses
+                if (inr && is_entry) g = o;
+                const bool com = inr && lane < cend;
+                // effectiveness with the final outcomes of the committed lanes
+                gref = (uint32_t)__shfl((int)g, refl < 0 ? 0 : refl, 64);
+                if (refl >= 0 && (uint32_t)refl >= c0) eff = gref == (uint32_t)nr;
+                if (com && is_entry) { dec = out_to_dec(rules, nr, o, wt); fin = dec & 0xFF; lwait = wt; }
+                spec_commit(W, R, rules, nr, lane, com, is_entry, eff, kind, t, cnt, rtv, g, tc0, synced, has_sync, T);
+                c0 = cend;
+                break;
+            }
+        }
+        // seed the next tile's guesses with the last entry's outcome
+        {
+            uint64_t em = __ballot(is_entry);
+            if (em) {
+                int lastl = 63 - __clzll((long long)em);
+                uint32_t fo = (uint32_t)__builtin_amdgcn_readlane((int)fin, lastl);
+                uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)dec, lastl);
+                if (fo == ST_PASS) last_out = (uint32_t)nr;
+                else if (fo == ST_BLOCK_FLOW || fo == ST_BLOCK_DEGRADE) {
+                    // stage index of the blocking rule
+                    uint32_t slot = (dd >> 8) & 0xFF;
+                    int base_s = fo == ST_BLOCK_FLOW ? W.prog.n_param : W.prog.n_param + W.prog.n_flow;
+                    int lim = fo == ST_BLOCK_FLOW ? W.prog.n_flow : W.prog.n_degrade;
+                    for (int k = 0; k < lim; ++k) if (rules[base_s + k].slot == slot) { last_out = (uint32_t)(base_s + k); break; }
+                }
+            }
+        }
+        (void)lwait;
+        if (valid) {
+            out[idx] = dec;
+            if (is_entry) S.ring[gidx & cfg.ring_mask] = (uint8_t)fin;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    min_flush(W);
+    if (lane == 0) {
+        S.sec[(uint64_t)W.res * 2 + 0] = W.sb[0];
+        S.sec[(uint64_t)W.res * 2 + 1] = W.sb[1];
+        NodeInfo o = ni;
+        o.thread = W.thread;
+        o.flags = W.flags;
+        o.exc_sum_sec = (W.prog.pflags & PF_EXC_COUNT) ? W.exc_sum_sec : -1;
+        o.exc_sum = W.exc_sum;
+        S.info[W.res] = o;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < nr; i += WAVE) S.rstate[W.prog.rule_off + i] = W.rs[i];
+}
+
 // =================================================================================
 // 4. per-second MetricNode snapshot (StatisticNode.metrics, StatisticNode.java:124-151)
 // =================================================================================
@@ -966,8 +1508,13 @@ hipError_t launch_decide(const sg_event* ev, const uint32_t* vals, const Seg* se
                          uint32_t* bflags, hipStream_t st) {
     if (m == 0) return hipSuccess;
     uint32_t nb = (m + DEC_WAVES - 1) / DEC_WAVES;
-    hipLaunchKernelGGL(k_decide, dim3(nb), dim3(DEC_WAVES * WAVE), 0, st, ev, vals, segs, order, m, gbase, n, S, cfg,
-                       out, bflags);
+    const char* mode = getenv("SG_DECIDE_SERIAL");
+    if (mode && mode[0] == '1')
+        hipLaunchKernelGGL(k_decide, dim3(nb), dim3(DEC_WAVES * WAVE), 0, st, ev, vals, segs, order, m, gbase, n, S,
+                           cfg, out, bflags);
+    else
+        hipLaunchKernelGGL(k_decide_spec, dim3(nb), dim3(DEC_WAVES * WAVE), 0, st, ev, vals, segs, order, m, gbase, n,
+                           S, cfg, out, bflags);
     return hipGetLastError();
 }
 hipError_t launch_snapshot(Bkt* minb, NodeInfo* info, uint32_t nres, int64_t now, int32_t max_rt, uint32_t* cnt,
