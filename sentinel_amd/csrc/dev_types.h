@@ -112,6 +112,8 @@ struct DevCfg {
     int32_t switch_on;
     uint64_t ptab_mask;
     uint64_t ring_mask;
+    uint32_t dbg_flags;  // SG_DEBUG_FLAGS experiment switches (0 in production)
+    uint32_t pad;
 };
 
 struct Seg {
@@ -131,6 +133,7 @@ struct DevState {
     const DHot* hot;
     PSlot* ptab;
     uint8_t* ring;
+    unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
 };
 
 enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8 };

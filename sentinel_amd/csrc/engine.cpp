@@ -27,12 +27,12 @@ hipError_t launch_radix_scatter(const sg_event*, const uint32_t*, const uint32_t
 uint32_t radix_tile();
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_seg(const uint32_t*, uint64_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, Seg*, uint32_t*,
-                      hipStream_t);
+                      const Prog*, hipStream_t);
 hipError_t launch_seg_order(const Seg*, uint32_t, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_chain_candidates(const sg_event*, const uint32_t*, const Seg*, uint32_t, const NodeInfo*, uint32_t*,
                                    uint64_t*, hipStream_t);
-hipError_t launch_decide(const sg_event*, const uint32_t*, const Seg*, const uint32_t*, uint32_t, uint64_t, uint64_t,
-                         const DevState&, const DevCfg&, uint32_t*, uint32_t*, hipStream_t);
+hipError_t launch_decide(const sg_event*, const uint32_t*, const Seg*, const uint32_t*, uint32_t, uint32_t, uint64_t,
+                         uint64_t, const DevState&, const DevCfg&, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                            sg_metric_node*, uint64_t, hipStream_t);
 hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, uint32_t nres, hipStream_t st);
@@ -405,8 +405,10 @@ struct sg_engine {
     uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
     uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
     Seg* d_segs = nullptr;
-    uint32_t* d_small = nullptr;  // [0] bflags [1] nseg [2] ncand [3..34] lbucket [35..66] lcursor [67] total
+    uint32_t* d_small = nullptr;  // [0] bflags [1] nseg [2] ncand [3..66] lbucket[2][32] [67..130] lcursor [131] total
     uint64_t* d_cand = nullptr;
+    unsigned long long* d_dbg = nullptr;
+    uint32_t dbg_flags = 0;
     uint64_t cap_hist = 0;
     uint64_t gbase = 0;
     // snapshot scratch
@@ -674,8 +676,20 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         launch_init_state(e->d_sec, e->d_minb, e->d_info, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
+    if (const char* d = std::getenv("SG_DEBUG")) {
+        if (d[0] == '1' && hipMalloc(&e->d_dbg, 64 * 8) == hipSuccess) (void)hipMemset(e->d_dbg, 0, 64 * 8);
+    }
+    if (const char* f = std::getenv("SG_DEBUG_FLAGS")) e->dbg_flags = (uint32_t)std::strtoul(f, nullptr, 0);
     *out = e;
     return SG_OK;
+}
+
+// hidden diagnostics export (not part of the ABI): per-batch counters of the hottest segment
+extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap) {
+    if (!e || !e->d_dbg || !out) return 0;
+    int k = cap < 64 ? cap : 64;
+    if (hipMemcpy(out, e->d_dbg, (size_t)k * 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return k;
 }
 
 int sg_engine_destroy(sg_engine* e) {
@@ -686,7 +700,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out);
+    dfree(e->d_cand); dfree(e->d_dbg); dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -964,8 +978,8 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         vout = (vin == e->d_v0) ? e->d_v1 : e->d_v0;
     }
     // ---- 2. segments
-    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_part, e->d_small + 1, e->d_segs, e->d_small + 3, st));
-    uint32_t small[68];
+    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_part, e->d_small + 1, e->d_segs, e->d_small + 3, e->d_prog, st));
+    uint32_t small[67];
     HIPCHK(hipMemcpyAsync(small, e->d_small, sizeof(small), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     uint32_t bflags = small[0], m = small[1];
@@ -973,12 +987,16 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     if (bflags & BF_PRIORITIZED)
         return fail(SG_ENOTSUP, "prioritized entries (StatisticNode.tryOccupyNext) are not on the device path yet");
     if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
-    // descending length classes -> cursors
-    uint32_t cur[32];
+    // [speculative segments | serial segments], each by descending length class -> cursors
+    uint32_t cur[64];
     uint32_t acc = 0;
-    for (int b = 31; b >= 0; --b) { cur[b] = acc; acc += small[3 + b]; }
-    HIPCHK(hipMemcpyAsync(e->d_small + 35, cur, sizeof(cur), hipMemcpyHostToDevice, st));
-    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 35, e->d_order, st));
+    for (int c = 0; c < 2; ++c)
+        for (int b = 31; b >= 0; --b) { cur[c * 32 + b] = acc; acc += small[3 + c * 32 + b]; }
+    uint32_t m_spec = 0;
+    for (int b = 0; b < 32; ++b) m_spec += small[3 + b];
+    uint32_t m_serial = m - m_spec;
+    HIPCHK(hipMemcpyAsync(e->d_small + 67, cur, sizeof(cur), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 67, e->d_order, st));
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     DevCfg dc;
     dc.max_rt = e->cfg.statistic_max_rt;
@@ -987,6 +1005,8 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     dc.switch_on = e->cfg.switch_on;
     dc.ptab_mask = (1ull << e->cfg.param_table_log2) - 1;
     dc.ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
+    dc.dbg_flags = e->dbg_flags;
+    dc.pad = 0;
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         HIPCHK(launch_chain_candidates(dev_ev, vin, e->d_segs, m, e->d_info, e->d_small + 2, e->d_cand, st));
         uint32_t ncand = 0;
@@ -1020,7 +1040,9 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.hot = e->d_hot;
     S.ptab = e->d_ptab;
     S.ring = e->d_ring;
-    HIPCHK(launch_decide(dev_ev, vin, e->d_segs, e->d_order, m, e->gbase, n, S, dc, dev_out, e->d_small + 0, st));
+    S.dbg = e->d_dbg;
+    HIPCHK(launch_decide(dev_ev, vin, e->d_segs, e->d_order, m_spec, m_serial, e->gbase, n, S, dc, dev_out,
+                         e->d_small + 0, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
     if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
     e->gbase += n;
@@ -1104,9 +1126,9 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
     }
     if (!e->d_part) { int rc = ensure_batch(e, 1); if (rc) return rc; }
     HIPCHK(launch_snapshot(e->d_minb, e->d_info, R, now_ms, e->cfg.statistic_max_rt, e->d_snap_cnt, e->d_snap_off,
-                           e->d_part, e->d_small + 67, e->d_snap_out, cap, e->stream));
+                           e->d_part, e->d_small + 131, e->d_snap_out, cap, e->stream));
     uint32_t total = 0;
-    HIPCHK(hipMemcpyAsync(&total, e->d_small + 67, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&total, e->d_small + 131, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     uint64_t k = std::min<uint64_t>(total, cap);
     if (k && out) HIPCHK(hipMemcpy(out, e->d_snap_out, k * sizeof(sg_metric_node), hipMemcpyDeviceToHost));

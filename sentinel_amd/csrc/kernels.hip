@@ -252,7 +252,8 @@ __global__ void k_seg_flags(const uint32_t* __restrict__ keys, uint64_t n, uint3
 }
 
 __global__ void k_seg_emit(const uint32_t* __restrict__ keys, uint64_t n, const uint32_t* __restrict__ flag,
-                           const uint32_t* __restrict__ pos, Seg* __restrict__ segs, uint32_t* __restrict__ lbucket) {
+                           const uint32_t* __restrict__ pos, Seg* __restrict__ segs, uint32_t* __restrict__ lbucket,
+                           const Prog* __restrict__ prog) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !flag[i]) return;
     // find the segment end
@@ -270,10 +271,10 @@ __global__ void k_seg_emit(const uint32_t* __restrict__ keys, uint64_t n, const 
     }
     (void)j;
     sg.len = (uint32_t)(lo - i);
-    sg.pad = 0;
+    sg.pad = prog[sg.res].n_param > 0 ? 1u : 0u;  // class: 1 = serial path
     segs[s] = sg;
     int b = 31 - __clz(sg.len | 1);
-    atomicAdd(&lbucket[b], 1u);
+    atomicAdd(&lbucket[sg.pad * 32 + b], 1u);
 }
 
 // order segments by descending length class so the longest start first
@@ -281,7 +282,7 @@ __global__ void k_seg_order(const Seg* __restrict__ segs, uint32_t m, uint32_t* 
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     int b = 31 - __clz(segs[i].len | 1);
-    uint32_t p = atomicAdd(&lcursor[b], 1u);
+    uint32_t p = atomicAdd(&lcursor[segs[i].pad * 32 + b], 1u);
     order[p] = i;
 }
 
@@ -370,16 +371,31 @@ struct Wave {
 
 // ---- LeapArray.currentWindow for the 2-bucket second window (LeapArray.java:117-208);
 // returns the slot, or -1 for a detached bucket (clock went back: updates are lost, Q3)
+__device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
+    b.ws = ws; b.pass = 0; b.block = 0; b.exc = 0; b.succ = 0; b.rt = 0; b.occ = 0; b.minrt = max_rt;
+}
+// (explicit branches: a runtime index into W.sb would force the wave state into scratch)
 __device__ __forceinline__ int sec_current(Wave& W, int64_t t) {
     int slot = (int)((t / 500) & 1);
     int64_t ws = t - t % 500;
-    Bkt& b = W.sb[slot];
-    if (b.ws == ws) return slot;
-    if (b.ws < ws) { // absent (-1) or deprecated: reset (the borrow array is empty on this path)
-        b.ws = ws; b.pass = 0; b.block = 0; b.exc = 0; b.succ = 0; b.rt = 0; b.occ = 0; b.minrt = W.cfg.max_rt;
-        return slot;
+    if (slot == 0) {
+        if (W.sb[0].ws == ws) return 0;
+        if (W.sb[0].ws < ws) { bkt_reset(W.sb[0], ws, W.cfg.max_rt); return 0; }
+        return -1;
     }
+    if (W.sb[1].ws == ws) return 1;
+    if (W.sb[1].ws < ws) { bkt_reset(W.sb[1], ws, W.cfg.max_rt); return 1; }
     return -1;
+}
+__device__ __forceinline__ void sec_add(Wave& W, int sl, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE,
+                                        int64_t mrt) {
+    if (sl == 0) {
+        W.sb[0].pass += dP; W.sb[0].block += dB; W.sb[0].succ += dS; W.sb[0].rt += dRT; W.sb[0].exc += dE;
+        if (mrt < W.sb[0].minrt) W.sb[0].minrt = mrt;
+    } else if (sl == 1) {
+        W.sb[1].pass += dP; W.sb[1].block += dB; W.sb[1].succ += dS; W.sb[1].rt += dRT; W.sb[1].exc += dE;
+        if (mrt < W.sb[1].minrt) W.sb[1].minrt = mrt;
+    }
 }
 // sum of one counter over values(t) (valid iff t - ws <= 1000)
 #define SEC_SUM(W, t, f) (((t) - (W).sb[0].ws <= 1000 && (W).sb[0].ws >= 0 ? (W).sb[0].f : 0) + \
@@ -397,7 +413,7 @@ __device__ __forceinline__ void min_flush(Wave& W) {
 // the buckets valid at t, i.e. window starts in [T-59000, T]).  Moves the sum to second T;
 // the minute ring in HBM must hold every bucket (cache flushed) and slot(T) must not
 // have been reset yet, so the seconds that fall out of the window are still readable.
-__device__ void exc_advance(Wave& W, int64_t T) {
+__device__ __forceinline__ void exc_advance(Wave& W, int64_t T) {
     const Bkt* mb = W.S.minb + (uint64_t)W.res * 60;
     if (W.exc_sum_sec < 0 || T - W.exc_sum_sec >= 60000) {
         int64_t s = 0;
@@ -432,7 +448,7 @@ __device__ __forceinline__ void min_current(Wave& W, int64_t t) {
     else W.mdirty = true;
 }
 // ArrayMetric.previousWindowPass on the minute window (LeapArray.getPreviousWindow, LeapArray.java:216-234)
-__device__ int64_t min_prev_pass(Wave& W, int64_t t) {
+__device__ __forceinline__ int64_t min_prev_pass(Wave& W, int64_t t) {
     min_current(W, t);
     int slot = (int)(((t - 1000) / 1000) % 60);
     Bkt b = W.S.minb[(uint64_t)W.res * 60 + slot];
@@ -441,7 +457,7 @@ __device__ int64_t min_prev_pass(Wave& W, int64_t t) {
     if (b.ws + 1000 < t - 1000) return 0;
     return b.pass;
 }
-__device__ int64_t min_total_exc(Wave& W, int64_t t) {
+__device__ __forceinline__ int64_t min_total_exc(Wave& W, int64_t t) {
     min_current(W, t);
     int64_t T = t - t % 1000;
     if (W.exc_sum_sec != T) { // rule added since the last advance: recompute (cached slot from registers)
@@ -457,7 +473,7 @@ __device__ int64_t min_total_exc(Wave& W, int64_t t) {
 }
 
 // ---- WarmUpController (core/slots/block/flow/controller/WarmUpController.java:119-174)
-__device__ void warm_sync(const DRule& r, RState& s, int64_t now, int64_t pass_qps) {
+__device__ __forceinline__ void warm_sync(const DRule& r, RState& s, int64_t now, int64_t pass_qps) {
     int64_t cur = now - now % 1000;
     if (cur <= s.b) return;
     int64_t old = s.a, nv = old;
@@ -675,13 +691,13 @@ __device__ uint32_t do_entry(Wave& W, int64_t t, int count, uint8_t eflags, uint
     min_current(W, t);
     if (status == ST_PASS) {
         W.thread++;
-        if (sl >= 0) W.sb[sl].pass += count;
+        sec_add(W, sl, count, 0, 0, 0, 0, INT64_MAX);
         if (!W.mdetached) { W.mb.pass += count; W.mdirty = true; }
         // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount
         if ((W.flags & NI_PM) && (W.flags & NI_TM0) && (eflags & SG_F_HAS_ARG) && W.lane == 0) thread_count_add(W, arg, 1);
         return mk_dec(ST_PASS, 0, wait);
     }
-    if (sl >= 0) W.sb[sl].block += count;
+    sec_add(W, sl, 0, count, 0, 0, 0, INT64_MAX);
     if (!W.mdetached) { W.mb.block += count; W.mdirty = true; }
     return mk_dec(status, slot, 0);
 }
@@ -690,11 +706,7 @@ __device__ uint32_t do_entry(Wave& W, int64_t t, int count, uint8_t eflags, uint
 __device__ void do_exit(Wave& W, int64_t t, int count, int64_t rt_raw) {
     int64_t rt = rt_raw > W.cfg.max_rt ? W.cfg.max_rt : rt_raw;
     int sl = sec_current(W, t);
-    if (sl >= 0) {
-        W.sb[sl].succ += count;
-        W.sb[sl].rt += rt;
-        if (rt < W.sb[sl].minrt) W.sb[sl].minrt = rt;
-    }
+    sec_add(W, sl, 0, 0, count, rt, 0, rt);
     min_current(W, t);
     if (!W.mdetached) {
         W.mb.succ += count;
@@ -709,7 +721,7 @@ __device__ void do_exit(Wave& W, int64_t t, int count, int64_t rt_raw) {
 __device__ void do_trace(Wave& W, int64_t t, int count) {
     if (count <= 0) return;
     int sl = sec_current(W, t);
-    if (sl >= 0) W.sb[sl].exc += count;
+    sec_add(W, sl, 0, 0, 0, 0, count, INT64_MAX);
     min_current(W, t);
     if (!W.mdetached) {
         W.mb.exc += count;
@@ -830,14 +842,22 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide(const sg_event* __r
 // breaker reset time, so bucket rotation and ResetTask stay serial points.
 // Resources with param rules take the serial path (per-value hash-table state).
 // =================================================================================
+// inclusive 64-lane prefix sum with DPP row shifts + row broadcasts (GFX9 family)
+__device__ __forceinline__ uint32_t wincl_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
 __device__ __forceinline__ uint32_t wex_u32(uint32_t v, uint32_t lane) {
-    uint32_t x = v;
-    #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    return x - v;
+    (void)lane;
+    return wincl_u32(v) - v;
+}
+__device__ __forceinline__ uint32_t wsum_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wincl_u32(v), 63);
 }
 __device__ __forceinline__ int64_t wex_i64(int64_t v, uint32_t lane) {
     int64_t x = v;
@@ -901,7 +921,7 @@ struct SpecRound {
 __device__ __forceinline__ uint32_t spec_eval(Wave& W, const SpecRound& R, const DRule* rules, int nr, uint32_t lane,
                                               bool inr, bool is_entry, bool eff, uint32_t kind, int64_t t, int cnt,
                                               int64_t rtv, uint32_t g, int64_t& wait_out, const RState* synced,
-                                              const bool* has_sync) {
+                                              uint32_t has_sync) {
     // ---- counter prefixes under the guesses
     bool gpass = inr && is_entry && g == (uint32_t)nr;
     bool gblock = inr && is_entry && g != (uint32_t)nr;
@@ -927,7 +947,7 @@ __device__ __forceinline__ uint32_t spec_eval(Wave& W, const SpecRound& R, const
         if (r.kind == RK_FLOW) {
             switch (r.behavior) {
             case SG_CONTROL_BEHAVIOR_WARM_UP: {
-                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                const RState& st = ((has_sync >> s) & 1) ? synced[s] : W.rs[s];
                 int64_t pq = P;
                 if (st.a >= r.warning_token) ok = (double)(pq + cnt) <= warm_qps(r, st.a);
                 else ok = (double)(pq + cnt) <= r.count;
@@ -935,7 +955,7 @@ __device__ __forceinline__ uint32_t spec_eval(Wave& W, const SpecRound& R, const
             }
             case SG_CONTROL_BEHAVIOR_RATE_LIMITER:
             case SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER: {
-                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                const RState& st = ((has_sync >> s) & 1) ? synced[s] : W.rs[s];
                 int64_t cost;
                 if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {
                     cost = (cnt <= 0 || r.count <= 0) ? 0 : j_round(1.0 * cnt / r.count * 1000);
@@ -1015,17 +1035,17 @@ __device__ __forceinline__ uint32_t spec_eval(Wave& W, const SpecRound& R, const
 __device__ __forceinline__ void spec_commit(Wave& W, const SpecRound& R, const DRule* rules, int nr, uint32_t lane,
                                             bool com, bool is_entry, bool eff, uint32_t kind, int64_t t, int cnt,
                                             int64_t rtv, uint32_t g, int64_t tc0, const RState* synced,
-                                            const bool* has_sync, int64_t T) {
+                                            uint32_t has_sync, int64_t T) {
     bool cpass = com && is_entry && g == (uint32_t)nr;
     bool cblock = com && is_entry && g != (uint32_t)nr;
     bool cexit = com && kind == SG_EV_EXIT && eff;
     bool ctrace = com && kind == SG_EV_TRACE && eff && cnt > 0;
-    int64_t dP = wsum_i64(cpass ? cnt : 0);
-    int64_t dB = wsum_i64(cblock ? cnt : 0);
-    int64_t dS = wsum_i64(cexit ? cnt : 0);
-    int64_t dRT = wsum_i64(cexit ? rtv : 0);
-    int64_t dE = wsum_i64(ctrace ? cnt : 0);
-    int64_t dTH = wsum_i64(cpass ? 1 : (cexit ? -1 : 0));
+    int64_t dP = wsum_u32(cpass ? (uint32_t)cnt : 0u);
+    int64_t dB = wsum_u32(cblock ? (uint32_t)cnt : 0u);
+    int64_t dS = wsum_u32(cexit ? (uint32_t)cnt : 0u);
+    int64_t dRT = wsum_u32(cexit ? (uint32_t)rtv : 0u);
+    int64_t dE = wsum_u32(ctrace ? (uint32_t)cnt : 0u);
+    int64_t dTH = (int64_t)(int32_t)wsum_u32((uint32_t)(cpass ? 1 : (cexit ? -1 : 0)));
     int64_t mrt = wmin_i64(cexit ? rtv : INT64_MAX);
     const bool touch = __ballot(cpass || cblock || cexit || ctrace) != 0;
     int sl = -1;
@@ -1033,11 +1053,7 @@ __device__ __forceinline__ void spec_commit(Wave& W, const SpecRound& R, const D
         sl = sec_current(W, tc0);
         min_current(W, tc0);
     }
-    if (sl >= 0) {
-        Bkt& b = W.sb[sl];
-        b.pass += dP; b.block += dB; b.succ += dS; b.rt += dRT; b.exc += dE;
-        if (mrt < b.minrt) b.minrt = mrt;
-    }
+    sec_add(W, sl, dP, dB, dS, dRT, dE, mrt);
     if (touch && !W.mdetached) {
         W.mb.pass += dP; W.mb.block += dB; W.mb.succ += dS; W.mb.rt += dRT; W.mb.exc += dE;
         if (mrt < W.mb.minrt) W.mb.minrt = mrt;
@@ -1053,10 +1069,10 @@ __device__ __forceinline__ void spec_commit(Wave& W, const SpecRound& R, const D
         bool any_reach = __ballot(reach) != 0;
         if (r.kind == RK_FLOW) {
             if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
-                if (any_reach && has_sync[s]) { W.rs[s].a = synced[s].a; W.rs[s].b = synced[s].b; }
+                if (any_reach && ((has_sync >> s) & 1)) { W.rs[s].a = synced[s].a; W.rs[s].b = synced[s].b; }
             }
             if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER || r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
-                const RState& st = has_sync[s] ? synced[s] : W.rs[s];
+                const RState& st = ((has_sync >> s) & 1) ? synced[s] : W.rs[s];
                 int64_t cost;
                 if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {
                     cost = (cnt <= 0 || r.count <= 0) ? 0 : j_round(1.0 * cnt / r.count * 1000);
@@ -1119,6 +1135,8 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
                                                                 uint32_t* __restrict__ out,
                                                                 uint32_t* __restrict__ bflags) {
     __shared__ RState lds_rs[DEC_WAVES][MAX_RULES_PER_RES];
+    __shared__ RState lds_sync[DEC_WAVES][MAX_RULES_PER_RES];
+    __shared__ DRule lds_rules[DEC_WAVES][MAX_RULES_PER_RES];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t sidx = blockIdx.x * DEC_WAVES + wv;
     if (sidx >= m) return;
@@ -1143,11 +1161,16 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
     W.mslot = -1;
     W.mdirty = false;
     W.mdetached = false;
+    for (int i = W.lane; i < nr; i += WAVE) lds_rules[wv][i] = S.rules[W.prog.rule_off + i];
     __builtin_amdgcn_wave_barrier();
-    const DRule* rules = S.rules + W.prog.rule_off;
-    const bool serial = W.prog.n_param > 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const DRule* rules = lds_rules[wv];
     const uint32_t lane = W.lane;
     uint32_t last_out = (uint32_t)nr;
+    const bool prof = S.dbg != nullptr && sidx == 0;
+    unsigned long long c_tiles = 0, c_rounds = 0, c_iters = 0, t_load = 0, t_ref = 0, t_round = 0, t_eval = 0, t_tail = 0;
+    unsigned long long tm0 = prof ? __builtin_amdgcn_s_memtime() : 0, tm1 = 0;
 
     // software prefetch of the next tile
     uint32_t nidx = 0;
@@ -1173,6 +1196,7 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
                 n_ts = p[0]; n_w1 = p[1]; n_aux = p[2];
             }
         }
+        if (prof) { tm1 = __builtin_amdgcn_s_memtime(); t_load += tm1 - tm0; tm0 = tm1; ++c_tiles; }
         const bool valid = lane < cnt_t;
         const int cnt = (int)((w1 >> 32) & 0xFFFFu);
         const uint32_t kind = valid ? (uint32_t)((w1 >> 48) & 0xFF) : 0xFFu;
@@ -1205,10 +1229,14 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
                 if (gl == ref) refl = lo;
                 else known_ok = false; // not an entry of this resource
             } else if (ref != SG_REF_NONE) {
-                uint8_t st8 = S.ring[ref & cfg.ring_mask];
-                known_ok = (st8 == ST_PASS || st8 == ST_PASS_WAIT);
+                if (cfg.dbg_flags & 1) known_ok = true;
+                else {
+                    uint8_t st8 = S.ring[ref & cfg.ring_mask];
+                    known_ok = (st8 == ST_PASS || st8 == ST_PASS_WAIT);
+                }
             }
         }
+        if (prof) { known_ok = __builtin_amdgcn_readfirstlane((int)known_ok) ? known_ok : known_ok; tm1 = __builtin_amdgcn_s_memtime(); t_ref += tm1 - tm0; tm0 = tm1; }
         uint32_t g = is_entry ? last_out : 0u;  // outcome guesses
         uint32_t dec = mk_dec(ST_NOT_ENTRY, 0, 0);
         uint32_t fin = ST_NOT_ENTRY;             // final status per lane (entries)
@@ -1221,31 +1249,6 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
         }
         while (c0 < cnt_t) {
             const int64_t tc0 = (int64_t)rl64((uint64_t)t, (int)c0);
-            if (serial) {
-                // one event through the serial chain (param rules)
-                uint32_t kc0 = (uint32_t)__builtin_amdgcn_readlane((int)kind, (int)c0);
-                int cc0 = __builtin_amdgcn_readlane(cnt, (int)c0);
-                uint8_t fc0 = (uint8_t)__builtin_amdgcn_readlane((int)fl, (int)c0);
-                uint64_t ac0 = rl64(aux, (int)c0);
-                if (kc0 == SG_EV_ENTRY) {
-                    uint32_t d = do_entry(W, tc0, cc0, fc0, ac0);
-                    if (lane == c0) { dec = d; fin = d & 0xFF; }
-                } else {
-                    int rl = __builtin_amdgcn_readlane(refl, (int)c0);
-                    int ko = __builtin_amdgcn_readlane((int)known_ok, (int)c0);
-                    bool ok;
-                    if (rl >= 0) {
-                        uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)fin, rl);
-                        ok = s == ST_PASS || s == ST_PASS_WAIT;
-                    } else ok = ko != 0;
-                    if (ok) {
-                        if (kc0 == SG_EV_EXIT) do_exit(W, tc0, cc0, (int64_t)rl64((uint64_t)rtv, (int)c0));
-                        else do_trace(W, tc0, cc0);
-                    }
-                }
-                ++c0;
-                continue;
-            }
             // breaker resets due at tc0 (ResetTask, Q12) and the next reset time
             int64_t next_reset = INT64_MAX;
             for (int s = W.prog.n_param + W.prog.n_flow; s < nr; ++s) {
@@ -1262,8 +1265,8 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
             SpecRound R;
             {
                 const int cs = (int)(b0 & 1);
-                const Bkt& cur = W.sb[cs];
-                const Bkt& prv = W.sb[cs ^ 1];
+                const Bkt cur = cs ? W.sb[1] : W.sb[0];
+                const Bkt prv = cs ? W.sb[0] : W.sb[1];
                 bool cv = cur.ws == b0 * 500;
                 bool pv = prv.ws >= 0 && tc0 - prv.ws <= 1000 && prv.ws <= tc0;
                 R.P = (cv ? cur.pass : 0) + (pv ? prv.pass : 0);
@@ -1274,25 +1277,27 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
             }
             R.TH = W.thread;
             R.EM = (has_entry && (W.prog.pflags & PF_EXC_COUNT)) ? min_total_exc(W, tc0) : 0;
-            RState synced[MAX_RULES_PER_RES];
-            bool has_sync[MAX_RULES_PER_RES];
+            RState* synced = lds_sync[wv];
+            uint32_t has_sync = 0;
             R.prev_pass_sec = 0;
             bool need_prev = false;
             for (int s = 0; s < nr; ++s) {
-                has_sync[s] = false;
                 const DRule r = rules[s];
                 if (has_entry && r.kind == RK_FLOW && (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP ||
                                                        r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)) {
                     if (T > W.rs[s].b) {
                         if (!need_prev) { R.prev_pass_sec = min_prev_pass(W, tc0); need_prev = true; }
-                        synced[s] = W.rs[s];
-                        warm_sync(r, synced[s], tc0, R.prev_pass_sec);
-                        has_sync[s] = true;
+                        RState tmp = W.rs[s];
+                        warm_sync(r, tmp, tc0, R.prev_pass_sec);
+                        synced[s] = tmp;
+                        has_sync |= 1u << s;
                     }
                 }
             }
+            if (prof) { tm1 = __builtin_amdgcn_s_memtime(); t_round += tm1 - tm0; tm0 = tm1; ++c_rounds; }
             // exits/traces: effectiveness under the guesses (referenced lane may be in this round)
             for (;;) {
+                if (prof) ++c_iters;
                 uint32_t gref = (uint32_t)__shfl((int)g, refl < 0 ? 0 : refl, 64);
                 uint32_t fref = (uint32_t)__shfl((int)fin, refl < 0 ? 0 : refl, 64);
                 bool eff;
@@ -1314,6 +1319,7 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
                 if (com && is_entry) { dec = out_to_dec(rules, nr, o, wt); fin = dec & 0xFF; lwait = wt; }
                 spec_commit(W, R, rules, nr, lane, com, is_entry, eff, kind, t, cnt, rtv, g, tc0, synced, has_sync, T);
                 c0 = cend;
+                if (prof) { tm1 = __builtin_amdgcn_s_memtime(); t_eval += tm1 - tm0; tm0 = tm1; }
                 break;
             }
         }
@@ -1341,6 +1347,11 @@ __global__ __launch_bounds__(DEC_WAVES * WAVE) void k_decide_spec(const sg_event
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (prof) { tm1 = __builtin_amdgcn_s_memtime(); t_tail += tm1 - tm0; tm0 = tm1; }
+    }
+    if (prof && lane == 0) {
+        S.dbg[0] = sg.len; S.dbg[1] = c_tiles; S.dbg[2] = c_rounds; S.dbg[3] = c_iters;
+        S.dbg[4] = t_load; S.dbg[5] = t_ref; S.dbg[6] = t_round; S.dbg[7] = t_eval; S.dbg[8] = t_tail;
     }
     min_flush(W);
     if (lane == 0) {
@@ -1484,12 +1495,12 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* 
 }
 
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, uint32_t* part, uint32_t* nseg,
-                      Seg* segs, uint32_t* lbucket, hipStream_t st) {
+                      Seg* segs, uint32_t* lbucket, const Prog* prog, hipStream_t st) {
     uint32_t nb = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_seg_flags, dim3(nb), dim3(256), 0, st, keys, n, flag);
     hipError_t e = launch_scan(flag, pos, n, part, nseg, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seg_emit, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs, lbucket);
+    hipLaunchKernelGGL(k_seg_emit, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs, lbucket, prog);
     return hipGetLastError();
 }
 hipError_t launch_seg_order(const Seg* segs, uint32_t m, uint32_t* lcursor, uint32_t* order, hipStream_t st) {
@@ -1503,18 +1514,23 @@ hipError_t launch_chain_candidates(const sg_event* ev, const uint32_t* vals, con
     hipLaunchKernelGGL(k_chain_candidates, dim3((m + 255) / 256), dim3(256), 0, st, ev, vals, segs, m, info, ncand, cand);
     return hipGetLastError();
 }
-hipError_t launch_decide(const sg_event* ev, const uint32_t* vals, const Seg* segs, const uint32_t* order, uint32_t m,
-                         uint64_t gbase, uint64_t n, const DevState& S, const DevCfg& cfg, uint32_t* out,
-                         uint32_t* bflags, hipStream_t st) {
-    if (m == 0) return hipSuccess;
-    uint32_t nb = (m + DEC_WAVES - 1) / DEC_WAVES;
+hipError_t launch_decide(const sg_event* ev, const uint32_t* vals, const Seg* segs, const uint32_t* order, uint32_t m_spec,
+                         uint32_t m_serial, uint64_t gbase, uint64_t n, const DevState& S, const DevCfg& cfg,
+                         uint32_t* out, uint32_t* bflags, hipStream_t st) {
     const char* mode = getenv("SG_DECIDE_SERIAL");
-    if (mode && mode[0] == '1')
-        hipLaunchKernelGGL(k_decide, dim3(nb), dim3(DEC_WAVES * WAVE), 0, st, ev, vals, segs, order, m, gbase, n, S,
-                           cfg, out, bflags);
-    else
-        hipLaunchKernelGGL(k_decide_spec, dim3(nb), dim3(DEC_WAVES * WAVE), 0, st, ev, vals, segs, order, m, gbase, n,
-                           S, cfg, out, bflags);
+    bool all_serial = mode && mode[0] == '1';
+    uint32_t m = m_spec + m_serial;
+    if (all_serial) {
+        if (m) hipLaunchKernelGGL(k_decide, dim3((m + DEC_WAVES - 1) / DEC_WAVES), dim3(DEC_WAVES * WAVE), 0, st, ev, vals,
+                                  segs, order, m, gbase, n, S, cfg, out, bflags);
+        return hipGetLastError();
+    }
+    if (m_spec)
+        hipLaunchKernelGGL(k_decide_spec, dim3((m_spec + DEC_WAVES - 1) / DEC_WAVES), dim3(DEC_WAVES * WAVE), 0, st, ev,
+                           vals, segs, order, m_spec, gbase, n, S, cfg, out, bflags);
+    if (m_serial)
+        hipLaunchKernelGGL(k_decide, dim3((m_serial + DEC_WAVES - 1) / DEC_WAVES), dim3(DEC_WAVES * WAVE), 0, st, ev, vals,
+                           segs, order + m_spec, m_serial, gbase, n, S, cfg, out, bflags);
     return hipGetLastError();
 }
 hipError_t launch_snapshot(Bkt* minb, NodeInfo* info, uint32_t nres, int64_t now, int32_t max_rt, uint32_t* cnt,
