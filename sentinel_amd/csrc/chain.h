@@ -1,0 +1,352 @@
+// chain.h -- lane-local device restatement of one resource's slot chain
+// (StatisticSlot -> FlowSlot -> DegradeSlot) over its ClusterNode windows.
+//
+// Every function here runs on ONE lane and touches only the state passed in:
+// the per-lane serial kernel calls them per event, the cooperative (Jacobi)
+// kernels call them from a single leader/pivot lane at round boundaries.
+// Semantics follow the Java cited at each function (paths as in SURVEY.md §0.1);
+// oracle/sentinel_oracle.c is the independent CPU restatement they are checked
+// against.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sentinel_gpu.h"
+#include "dev_types.h"
+
+namespace sg {
+
+// ---------------------------------------------------------------- Java arithmetic
+__device__ __forceinline__ int64_t j_d2l(double d) {  // (long) d
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+__device__ __forceinline__ int32_t j_d2i(double d) {  // (int) d
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return INT32_MAX;
+    if (d <= -2147483648.0) return INT32_MIN;
+    return (int32_t)d;
+}
+__device__ __forceinline__ int32_t j_iadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+// java.lang.Math.round(double)
+__device__ __forceinline__ int64_t j_round(double a) {
+    int64_t bits = __double_as_longlong(a);
+    int64_t biased = (bits & 0x7ff0000000000000LL) >> 52;
+    int64_t shift = (52 - 1 + 1023) - biased;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000fffffffffffffLL) | (0x000fffffffffffffLL + 1);
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    return j_d2l(a);
+}
+// java.lang.Math.nextUp(double)
+__device__ __forceinline__ double j_next_up(double d) {
+    if (d != d || d == __longlong_as_double(0x7ff0000000000000LL)) return d;
+    if (d == 0.0) return __longlong_as_double(1LL);
+    int64_t b = __double_as_longlong(d);
+    b += (d > 0.0) ? 1 : -1;
+    return __longlong_as_double(b);
+}
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27; x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31; return x;
+}
+__device__ __forceinline__ uint32_t mk_dec(uint32_t status, uint32_t slot, int64_t wait) {
+    if (wait < 0) wait = 0;
+    if (wait > 0xFFFF) wait = 0xFFFF;
+    return status | ((slot & 0xFFu) << 8) | ((uint32_t)wait << 16);
+}
+__device__ __forceinline__ bool st_passed(uint32_t st) { return st == ST_PASS || st == ST_PASS_WAIT; }
+
+// ---------------------------------------------------------------- node state
+enum : uint32_t { MS_DIRTY = 1u, MS_DETACHED = 2u };
+
+// ClusterNode of one resource: the 2 x 500 ms second window, the cached current
+// minute bucket (60 x 1000 ms ring in HBM), curThreadNum and bookkeeping.
+struct Node {
+    Bkt sb[2];
+    Bkt mb;
+    int32_t mslot;       // slot of mb, -1 = none cached
+    uint32_t mst;        // MS_*
+    int32_t thread;
+    uint32_t flags;      // NI_*
+    int64_t exc_sum_sec; // see NodeInfo
+    int64_t exc_sum;
+};
+
+__device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t res) {
+    N.sb[0] = S.sec[(uint64_t)res * 2 + 0];
+    N.sb[1] = S.sec[(uint64_t)res * 2 + 1];
+    NodeInfo ni = S.info[res];
+    N.thread = ni.thread;
+    N.flags = ni.flags;
+    N.exc_sum_sec = ni.exc_sum_sec;
+    N.exc_sum = ni.exc_sum;
+    N.mslot = -1;
+    N.mst = 0;
+}
+
+__device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
+    b.ws = ws; b.pass = 0; b.block = 0; b.exc = 0; b.succ = 0; b.rt = 0; b.occ = 0; b.minrt = max_rt;
+}
+
+// LeapArray.currentWindow for the 2-bucket second window (core/slots/statistic/base/LeapArray.java:117-208):
+// returns the slot, or -1 for a detached bucket (clock went back: the update is lost).
+// Explicit branches keep sb[] in registers (a runtime index would force it to scratch).
+__device__ __forceinline__ int sec_current(Node& N, int64_t t, int32_t max_rt) {
+    int slot = (int)((t / 500) & 1);
+    int64_t ws = t - t % 500;
+    if (slot == 0) {
+        if (N.sb[0].ws == ws) return 0;
+        if (N.sb[0].ws < ws) { bkt_reset(N.sb[0], ws, max_rt); return 0; }
+        return -1;
+    }
+    if (N.sb[1].ws == ws) return 1;
+    if (N.sb[1].ws < ws) { bkt_reset(N.sb[1], ws, max_rt); return 1; }
+    return -1;
+}
+__device__ __forceinline__ void bkt_add(Bkt& b, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE, int64_t mrt) {
+    b.pass += dP; b.block += dB; b.succ += dS; b.rt += dRT; b.exc += dE;
+    if (mrt < b.minrt) b.minrt = mrt;
+}
+__device__ __forceinline__ void sec_add(Node& N, int sl, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE,
+                                        int64_t mrt) {
+    if (sl == 0) bkt_add(N.sb[0], dP, dB, dS, dRT, dE, mrt);
+    else if (sl == 1) bkt_add(N.sb[1], dP, dB, dS, dRT, dE, mrt);
+}
+// sum of one counter over LeapArray.values(t): a bucket is valid unless t - ws > 1000 (strict, Q4)
+#define SEC_SUM(N, t, f) ((((t) - (N).sb[0].ws <= 1000 && (N).sb[0].ws >= 0) ? (N).sb[0].f : 0) + \
+                          (((t) - (N).sb[1].ws <= 1000 && (N).sb[1].ws >= 0) ? (N).sb[1].f : 0))
+
+// write the cached minute bucket back to HBM
+__device__ __forceinline__ void min_flush(Node& N, Bkt* minb) {
+    if (N.mslot >= 0 && (N.mst & MS_DIRTY) && !(N.mst & MS_DETACHED)) minb[N.mslot] = N.mb;
+    N.mst &= ~MS_DIRTY;
+}
+// StatisticNode.totalException = minute EXCEPTION sum over buckets valid at t (window starts in
+// [T-59000, T]), kept as a running sum.  Moves the sum to second T; HBM must hold every bucket
+// (cache flushed) and slot(T) must not have been reset yet, so the seconds that fall out of the
+// window are still readable.
+__device__ __forceinline__ void exc_advance(Node& N, const Bkt* minb, int64_t T) {
+    if (N.exc_sum_sec < 0 || T - N.exc_sum_sec >= 60000) {
+        int64_t s = 0;
+        for (int k = 0; k < 60; ++k) {
+            Bkt b = minb[k];
+            if (b.ws >= T - 59000 && b.ws <= T) s += b.exc;
+        }
+        N.exc_sum = s;
+    } else {
+        for (int64_t x = N.exc_sum_sec - 59000; x <= T - 60000; x += 1000) {
+            Bkt b = minb[(x / 1000) % 60];
+            if (b.ws == x) N.exc_sum -= b.exc;
+        }
+    }
+    N.exc_sum_sec = T;
+}
+// minute-window currentWindow(t) (LeapArray.java:117-208): caches the bucket of second T in N.mb
+__device__ __forceinline__ void min_current(Node& N, Bkt* minb, int64_t t, int32_t max_rt, uint32_t pflags) {
+    int slot = (int)((t / 1000) % 60);
+    int64_t ws = t - t % 1000;
+    if (N.mslot == slot && N.mb.ws == ws) return;
+    min_flush(N, minb);
+    if ((pflags & PF_EXC_COUNT) && N.exc_sum_sec < ws) exc_advance(N, minb, ws);
+    Bkt b = minb[slot];
+    N.mslot = slot;
+    N.mst = 0;
+    if (b.ws == ws) { N.mb = b; return; }
+    bool back = b.ws > ws;
+    bkt_reset(b, ws, max_rt);
+    N.mb = b;
+    N.mst = back ? MS_DETACHED : MS_DIRTY;  // clock went back: a detached bucket (Q3)
+}
+// ArrayMetric.previousWindowPass on the minute window (LeapArray.getPreviousWindow, LeapArray.java:216-234)
+__device__ __forceinline__ int64_t min_prev_pass(Node& N, Bkt* minb, int64_t t, int32_t max_rt, uint32_t pflags) {
+    min_current(N, minb, t, max_rt, pflags);
+    int slot = (int)(((t - 1000) / 1000) % 60);
+    Bkt b = minb[slot];
+    if (b.ws < 0) return 0;
+    if (t - b.ws > 60000) return 0;
+    if (b.ws + 1000 < t - 1000) return 0;
+    return b.pass;
+}
+__device__ __forceinline__ int64_t min_total_exc(Node& N, Bkt* minb, int64_t t, int32_t max_rt, uint32_t pflags) {
+    min_current(N, minb, t, max_rt, pflags);
+    int64_t T = t - t % 1000;
+    if (N.exc_sum_sec != T) {  // rule added since the last advance: recompute (cached slot from registers)
+        int64_t s = 0;
+        for (int k = 0; k < 60; ++k) {
+            Bkt b = (k == N.mslot) ? N.mb : minb[k];
+            if (b.ws >= T - 59000 && b.ws <= T) s += b.exc;
+        }
+        N.exc_sum = s;
+        N.exc_sum_sec = T;
+    }
+    return N.exc_sum;
+}
+__device__ __forceinline__ void min_add(Node& N, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE, int64_t mrt) {
+    if (N.mst & MS_DETACHED) return;
+    bkt_add(N.mb, dP, dB, dS, dRT, dE, mrt);
+    N.mst |= MS_DIRTY;
+}
+
+// ---------------------------------------------------------------- controllers
+// WarmUpController.syncToken / coolDownTokens (core/slots/block/flow/controller/WarmUpController.java:141-174)
+__device__ __forceinline__ void warm_sync(const DRule& r, RState& s, int64_t now, int64_t pass_qps) {
+    int64_t cur = now - now % 1000;
+    if (cur <= s.b) return;
+    int64_t old = s.a, nv = old;
+    if (old < r.warning_token) {
+        nv = j_d2l((double)old + (double)(cur - s.b) * r.count / 1000);
+    } else if (old > r.warning_token) {
+        if (pass_qps < r.count_div_cold) nv = j_d2l((double)old + (double)(cur - s.b) * r.count / 1000);
+    }
+    if (nv > r.max_token) nv = r.max_token;
+    int64_t v = nv - pass_qps;
+    s.a = v < 0 ? 0 : v;
+    s.b = cur;
+}
+// WarmUpController.canPass warningQps (WarmUpController.java:123-131)
+__device__ __forceinline__ double warm_qps(const DRule& r, int64_t rest) {
+    int64_t above = rest - r.warning_token;
+    return j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+}
+// RateLimiterController / WarmUpRateLimiterController queueing (RateLimiterController.java:46-91);
+// the sleep becomes wait_ms in the decision (Q10)
+__device__ __forceinline__ bool rl_admit(int64_t& latest, int64_t cost, int64_t now, int32_t maxq, int64_t& wait) {
+    int64_t expected = cost + latest;
+    if (expected <= now) { latest = now; return true; }
+    int64_t w = cost + latest - now;
+    if (w > maxq) return false;
+    latest += cost;
+    w = latest - now;
+    if (w > maxq) { latest -= cost; return false; }
+    if (w > 0) wait += w;
+    return true;
+}
+// cost of one RateLimiter / WarmUpRateLimiter admission at the state s
+__device__ __forceinline__ int64_t rl_cost(const DRule& r, const RState& s, int acquire) {
+    if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {
+        if (acquire <= 0 || r.count <= 0) return 0;
+        return j_round(1.0 * acquire / r.count * 1000);
+    }
+    if (s.a >= r.warning_token) return j_round(1.0 * acquire / warm_qps(r, s.a) * 1000);
+    return j_round(1.0 * acquire / r.count * 1000);
+}
+
+struct Ctx {  // per-resource constants
+    Bkt* minb;     // the resource's 60 minute buckets
+    int32_t max_rt;
+    uint32_t pflags;
+};
+
+// TrafficShapingController.canPass on the resource's ClusterNode (FlowRuleChecker.passLocalCheck,
+// core/slots/block/flow/FlowRuleChecker.java:52-66)
+__device__ __forceinline__ bool flow_can_pass(Node& N, const Ctx& C, const DRule& r, RState& s, int64_t t, int acquire,
+                                              int64_t& wait) {
+    switch (r.behavior) {
+    case SG_CONTROL_BEHAVIOR_WARM_UP: {
+        sec_current(N, t, C.max_rt);
+        int64_t pass_qps = SEC_SUM(N, t, pass);                               // (long) node.passQps()
+        int64_t prev = min_prev_pass(N, C.minb, t, C.max_rt, C.pflags);       // (long) node.previousPassQps()
+        warm_sync(r, s, t, prev);
+        int64_t rest = s.a;
+        if (rest >= r.warning_token) return (double)(pass_qps + acquire) <= warm_qps(r, rest);
+        return (double)(pass_qps + acquire) <= r.count;
+    }
+    case SG_CONTROL_BEHAVIOR_RATE_LIMITER: {
+        if (acquire <= 0) return true;
+        if (r.count <= 0) return false;
+        return rl_admit(s.c, rl_cost(r, s, acquire), t, r.max_queue, wait);
+    }
+    case SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER: {
+        int64_t prev = min_prev_pass(N, C.minb, t, C.max_rt, C.pflags);
+        warm_sync(r, s, t, prev);
+        return rl_admit(s.c, rl_cost(r, s, acquire), t, r.max_queue, wait);
+    }
+    default: {  // DefaultController (DefaultController.java:49-81)
+        int32_t cur;
+        if (r.grade == SG_FLOW_GRADE_THREAD) cur = N.thread;
+        else { sec_current(N, t, C.max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
+        return !((double)j_iadd(cur, acquire) > r.count);
+    }
+    }
+}
+
+// DegradeRule.passCheck (core/slots/block/degrade/DegradeRule.java:172-223); the ResetTask fires at
+// cut_until = t_cut + timeWindow*1000 (Q12).  RState: a = cut, b = passCount, c = cut_until.
+__device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DRule& r, RState& s, int64_t t) {
+    if (s.a && t >= s.c) { s.a = 0; s.b = 0; }
+    if (s.a) return false;
+    if (r.grade == SG_DEGRADE_GRADE_RT) {
+        sec_current(N, t, C.max_rt);
+        int64_t succ = SEC_SUM(N, t, succ);
+        double avg = succ == 0 ? 0.0 : (double)SEC_SUM(N, t, rt) * 1.0 / (double)succ;
+        if (avg < r.count) { s.b = 0; return true; }
+        if (++s.b < 5) return true;
+    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+        sec_current(N, t, C.max_rt);
+        double exc = (double)SEC_SUM(N, t, exc) / 1.0;
+        double succ = (double)SEC_SUM(N, t, succ) / 1.0;
+        double total = (double)SEC_SUM(N, t, pass) / 1.0 + (double)SEC_SUM(N, t, block) / 1.0;
+        if (total < 5) return true;
+        double real = succ - exc;
+        if (real <= 0 && exc < 5) return true;
+        if (exc / succ < r.count) return true;
+    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) {
+        double e = (double)min_total_exc(N, C.minb, t, C.max_rt, C.pflags);
+        if (e < r.count) return true;
+    }
+    s.a = 1;
+    s.c = t + (int64_t)r.time_window * 1000;
+    return false;
+}
+
+// StatisticSlot.entry bookkeeping after the checks (core/slots/statistic/StatisticSlot.java:54-133)
+__device__ __forceinline__ void stat_entry(Node& N, const Ctx& C, int64_t t, int count, bool passed) {
+    int sl = sec_current(N, t, C.max_rt);
+    min_current(N, C.minb, t, C.max_rt, C.pflags);
+    if (passed) {
+        N.thread++;
+        sec_add(N, sl, count, 0, 0, 0, 0, INT64_MAX);
+        min_add(N, count, 0, 0, 0, 0, INT64_MAX);
+    } else {
+        sec_add(N, sl, 0, count, 0, 0, 0, INT64_MAX);
+        min_add(N, 0, count, 0, 0, 0, INT64_MAX);
+    }
+}
+// StatisticSlot.exit (StatisticSlot.java:136-173) for an entry that passed; rt already clipped
+__device__ __forceinline__ void stat_exit(Node& N, const Ctx& C, int64_t t, int count, int64_t rt) {
+    int sl = sec_current(N, t, C.max_rt);
+    sec_add(N, sl, 0, 0, count, rt, 0, rt);
+    min_current(N, C.minb, t, C.max_rt, C.pflags);
+    min_add(N, 0, 0, count, rt, 0, rt);
+    N.thread--;
+}
+// ClusterNode.trace (core/node/ClusterNode.java:99-106)
+__device__ __forceinline__ void stat_trace(Node& N, const Ctx& C, int64_t t, int count) {
+    if (count <= 0) return;
+    int sl = sec_current(N, t, C.max_rt);
+    sec_add(N, sl, 0, 0, 0, 0, count, INT64_MAX);
+    min_current(N, C.minb, t, C.max_rt, C.pflags);
+    if (!(N.mst & MS_DETACHED)) {
+        min_add(N, 0, 0, 0, 0, count, INT64_MAX);
+        if (N.exc_sum_sec == t - t % 1000) N.exc_sum += count;
+    }
+}
+
+__device__ __forceinline__ void node_store(const Node& N, const DevState& S, uint32_t res, uint32_t pflags) {
+    S.sec[(uint64_t)res * 2 + 0] = N.sb[0];
+    S.sec[(uint64_t)res * 2 + 1] = N.sb[1];
+    NodeInfo o = S.info[res];
+    o.thread = N.thread;
+    o.flags = N.flags;
+    o.exc_sum_sec = (pflags & PF_EXC_COUNT) ? N.exc_sum_sec : -1;
+    o.exc_sum = N.exc_sum;
+    S.info[res] = o;
+}
+
+} // namespace sg

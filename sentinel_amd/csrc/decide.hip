@@ -1,0 +1,1216 @@
+// decide.hip -- per-batch decision kernels of the MI355X Sentinel engine.
+//
+// Pipeline position (engine.cpp sg_submit_async):
+//   sort (kernels.hip) -> k_seg_* (segments + bins) -> k_posof/k_prep (16-byte sorted records,
+//   EXIT/TRACE references resolved) -> k_chain -> decide kernels by bin -> k_post (scatter the
+//   decisions back to submission order and into the status ring).
+//
+// A segment is one resource's events of the batch, in event order.  Every resource's slot chain
+// is a sequential state machine, so a segment is decided by exactly one owner:
+//   * k_lane : one LANE per segment runs the chain event by event (chain.h) -- the Zipf tail,
+//              every resource with param rules, and anything outside the cooperative limits;
+//   * k_jac  : one wavefront / 256-lane / 1024-lane workgroup per segment (Zipf body and head).
+//              Lanes take consecutive events and decide them speculatively: each lane evaluates
+//              the chain against the state it would see if every earlier lane had the outcome
+//              currently guessed for it (block-wide prefix sums of the counter deltas, max-plus
+//              scans for rate limiters, a segmented scan for the RT breaker's passCount).  The
+//              first lane whose evaluated outcome differs from its guess is exact, so everything
+//              up to it commits; later lanes are re-guessed with their evaluated outcomes
+//              (Jacobi iteration).  In the steady states of a hot resource (all pass, or all
+//              blocked once its quota is spent) one iteration commits the whole tile.
+//              A round never crosses a 500 ms bucket or a breaker reset, so bucket rotation,
+//              WarmUp token sync and the ResetTask stay serial points handled by one leader lane.
+// No MFMA: nothing here is a dense contraction; the kernels are bound by latency of the
+// per-resource dependency chain and by HBM traffic of the event stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "chain.h"
+
+using namespace sg;
+
+#define WAVE 64
+#define MAXR 16          // rules per resource (engine.cpp enforces)
+#define JMAX_FLOW 4      // cooperative kernels: flow stages
+#define JMAX_DEG 4       //                      degrade stages
+#define JMAX_RL 2        //                      rate-limiter stages
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    uint32_t l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// wave-aggregated atomicAdd of 1 per active lane into ctr[bin]; returns the lane's slot.
+// Must be called by the whole (converged) wavefront.
+__device__ __forceinline__ uint32_t agg_slot(uint32_t* ctr, uint32_t bin, bool active) {
+    uint32_t res = 0;
+    uint64_t todo = __ballot(active);
+    while (todo) {
+        int leader = __ffsll((long long)todo) - 1;
+        uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bin, leader);
+        uint64_t peers = __ballot(active && bin == lb);
+        uint32_t base = 0;
+        if ((int)lane_id() == leader) base = atomicAdd(&ctr[lb], (uint32_t)__popcll(peers));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+        if (active && bin == lb) res = base + (uint32_t)__popcll(peers & lanemask_lt());
+        todo &= ~peers;
+    }
+    return res;
+}
+
+// =================================================================================
+// segments: starts, lengths, bins, bin-ordered dispatch list
+// =================================================================================
+__global__ void k_seg_flags(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ flag) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+__global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const uint32_t* __restrict__ flag,
+                            const uint32_t* __restrict__ pos, Seg* __restrict__ segs) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    Seg s;
+    s.res = keys[i];
+    s.start = (uint32_t)i;
+    s.len = 0;
+    s.bin = 0;
+    segs[pos[i]] = s;
+}
+// lengths + bins + per-bin counts.  Bins (dev_types.h BIN_*): cooperative kernels for long
+// segments of resources inside their limits, one lane per segment for everything else.
+__global__ void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n, const Prog* __restrict__ prog,
+                          uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane,
+                          uint32_t* __restrict__ bin_cnt) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    bool act = s < m;
+    uint32_t bin = 0;
+    if (act) {
+        Seg sg = segs[s];
+        uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
+        sg.len = end - sg.start;
+        Prog p = prog[sg.res];
+        int nr = p.n_param + p.n_flow + p.n_degrade;
+        bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max;
+        if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
+        else {
+            int lb = 31 - __clz(sg.len | 1);
+            if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
+            bin = (nr <= 4 ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
+        }
+        sg.bin = bin;
+        segs[s] = sg;
+    }
+    (void)agg_slot(bin_cnt, bin, act);
+}
+__global__ void k_seg_order(const Seg* __restrict__ segs, uint32_t m, uint32_t* __restrict__ cursor,
+                            uint32_t* __restrict__ order) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    bool act = s < m;
+    uint32_t bin = act ? segs[s].bin : 0;
+    uint32_t p = agg_slot(cursor, bin, act);
+    if (act) order[p] = s;
+}
+
+// =================================================================================
+// sorted records
+// =================================================================================
+__global__ void k_posof(const uint32_t* __restrict__ vals, uint64_t n, uint32_t* __restrict__ pos_of) {
+    uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) pos_of[vals[p]] = (uint32_t)p;
+}
+
+// One 16-byte record per event in sorted order.  EXIT/TRACE references are resolved here, in a
+// fully parallel pass, so the decide kernels never chase the status ring:
+//   - ENTRY earlier in this batch            -> RC_BATCH + its sorted position
+//   - ENTRY of an earlier batch (status ring)-> RC_PASSED / RC_NOT; unknown -> as if no reference
+// (or_submit in the oracle applies the same rules: an unknown reference means "the caller asserts
+// the entry passed" for an EXIT and "no entry" for a TRACE).
+__global__ void k_prep(const sg_event* __restrict__ ev, const uint32_t* __restrict__ vals, uint64_t n,
+                       const uint32_t* __restrict__ pos_of, uint64_t gbase, const uint8_t* __restrict__ ring,
+                       uint64_t ring_mask, int32_t max_rt, SEv* __restrict__ recs, uint32_t* __restrict__ bflags) {
+    uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int64_t t0 = ev[0].ts;
+    const uint32_t idx = vals[p];
+    const sg_event e = ev[idx];
+    uint32_t fl = 0;
+    SEv r;
+    int64_t dt = e.ts - t0;
+    if (dt < 0 || dt > 0x7FFFFFFFLL) fl |= (dt < 0 ? BF_BACKWARD : BF_TSPAN);
+    if (idx > 0 && ev[idx - 1].ts > e.ts) fl |= BF_BACKWARD;  // ABI: non-decreasing ts
+    r.dt = (int32_t)dt;
+    r.x = 0;
+    r.cnt = e.count;
+    r.rt = 0;
+    r.kind = e.kind;
+    r.flags = e.flags;
+    r.code = RC_NONE;
+    r.pad = 0;
+    if (e.kind == SG_EV_ENTRY) {
+        if (e.flags & SG_F_PRIORITIZED) fl |= BF_PRIORITIZED;
+    } else {
+        if (e.kind == SG_EV_EXIT) {
+            if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
+            int64_t raw = (int64_t)(e.aux >> 48);
+            r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
+        }
+        const uint64_t ref = e.aux & SG_REF_NONE;
+        if (ref != SG_REF_NONE) {
+            if (ref >= gbase) {
+                uint64_t ri = ref - gbase;
+                if (ri >= idx) fl |= BF_BAD_REF;  // an EXIT/TRACE must follow its ENTRY
+                else {
+                    const sg_event en = ev[ri];
+                    if (en.kind != SG_EV_ENTRY || en.res_id != e.res_id) fl |= BF_BAD_REF;
+                    else { r.code = RC_BATCH; r.x = pos_of[ri]; }
+                }
+            } else {
+                uint8_t st = ring[ref & ring_mask];
+                if (st == ST_NOT_ENTRY) r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+                else r.code = st_passed(st) ? RC_PASSED : RC_NOT;
+            }
+        }
+    }
+    recs[p] = r;
+    if (fl) atomicOr(bflags, fl);
+}
+
+// decisions back to submission order; the status ring keeps every event's status for
+// references from later batches (0xFF = not an ENTRY)
+__global__ void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ dec, uint64_t n,
+                       uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask, uint32_t* __restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t d = dec[pos_of[i]];
+    out[i] = d;
+    ring[(gbase + i) & ring_mask] = (uint8_t)(d & 0xFF);
+}
+
+// CtSph.lookProcessChain (core/CtSph.java:206-227): resources touched by this batch with neither a
+// chain nor a rejection.  Unbounded cap: grant in place.  Bounded: emit (batch index of the first
+// ENTRY, res) candidates for the host, which grants in first-ENTRY order up to the cap.
+__global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                        uint32_t m, NodeInfo* __restrict__ info, uint32_t grant_all, uint32_t* __restrict__ ncand,
+                        uint64_t* __restrict__ cand) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= m) return;
+    Seg sg = segs[s];
+    uint32_t f = info[sg.res].flags;
+    if (f & (NI_CHAIN | NI_REJECTED)) return;
+    for (uint32_t j = 0; j < sg.len; ++j) {
+        if (recs[sg.start + j].kind == SG_EV_ENTRY) {
+            if (grant_all) info[sg.res].flags = f | NI_CHAIN;
+            else cand[atomicAdd(ncand, 1u)] = ((uint64_t)vals[sg.start + j] << 32) | sg.res;
+            return;
+        }
+    }
+}
+
+// =================================================================================
+// ParamFlowChecker (param/slots/block/flow/param/ParamFlowChecker.java:101-248), lane-local.
+// Every (rule, value) key is owned by exactly one resource, i.e. by one lane at a time; only
+// probing crosses owners (insertion is a CAS on the key word).
+// =================================================================================
+__device__ PSlot* ptab_lookup(PSlot* tab, uint64_t mask, uint64_t khi, uint64_t kval, bool insert, bool* is_new,
+                              uint32_t* bflags) {
+    uint64_t h = mix64(khi * 0x9e3779b97f4a7c15ULL ^ kval) & mask;
+    *is_new = false;
+    for (uint32_t probe = 0; probe <= 4096; ++probe) {
+        PSlot* s = &tab[h];
+        uint64_t k = __hip_atomic_load(&s->khi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == khi && s->kval == kval) return s;
+        if (k == 0) {
+            if (!insert) return nullptr;
+            unsigned long long expect = 0;
+            if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s->khi, &expect, (unsigned long long)khi,
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                s->kval = kval;
+                s->v0 = 0;
+                s->v1 = 0;
+                *is_new = true;
+                return s;
+            }
+            // lost the race to another owner: this slot now holds a different key, keep probing
+        }
+        h = (h + 1) & mask;
+    }
+    atomicOr(bflags, BF_PTAB_FULL);
+    return nullptr;
+}
+__device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool* found) {
+    for (uint32_t i = 0; i < r.hot_n; ++i) {
+        DHot h = S.hot[r.hot_off + i];
+        if (h.key == v) { *found = true; return h.count; }
+    }
+    *found = false;
+    return 0;
+}
+__device__ __forceinline__ uint64_t tc_key(uint32_t epoch, uint32_t res) {
+    return (2ULL << 62) | ((uint64_t)(epoch & 0x3FFFFFFF) << 32) | res;
+}
+// ParameterMetric thread-count map of paramIdx 0 (ParameterMetric.java:167-199)
+__device__ int64_t thread_count_get(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint64_t v,
+                                    uint32_t* bflags) {
+    bool nw;
+    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res), v, false, &nw, bflags);
+    return s ? s->v0 : 0;
+}
+__device__ void thread_count_add(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint64_t v,
+                                 int64_t d, uint32_t* bflags) {
+    bool nw;
+    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res), v, true, &nw, bflags);
+    if (!s) return;
+    int64_t c = s->v0 + d;
+    if (d < 0 && nw) c = 0;  // putIfAbsent(value, new AtomicInteger()) without a decrement
+    s->v0 = c < 0 ? 0 : c;
+}
+__device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, const DRule& r,
+                            int acquire, uint64_t v, int64_t t, int64_t& wait, uint32_t* bflags) {
+    if (r.grade == SG_FLOW_GRADE_QPS) {
+        bool hf;
+        int32_t hc = hot_count(S, r, v, &hf);
+        uint64_t khi = (1ULL << 62) | r.psid;
+        if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {  // passThrottleLocalCheck (:198-248)
+            int64_t token_count = hf ? (int64_t)hc : r.token_count_l;
+            if (token_count == 0) return false;
+            int64_t cost = j_round(1.0 * 1000 * acquire * (double)r.duration_sec / (double)token_count);
+            bool nw;
+            PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, khi, v, true, &nw, bflags);
+            if (!s) return true;
+            if (nw) { s->v0 = t; return true; }
+            int64_t expected = s->v0 + cost;
+            if (expected <= t || expected - t < r.max_queue) {
+                s->v0 = t;
+                int64_t w = expected - t;
+                if (w > 0) { s->v0 = expected; wait += w; }
+                return true;
+            }
+            return false;
+        }
+        // passDefaultLocalCheck (:121-196)
+        int32_t token_count = hf ? hc : r.token_count;
+        if (token_count == 0) return false;
+        int32_t max_count = j_iadd(token_count, r.burst);
+        if (acquire > max_count) return false;
+        bool nw;
+        PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, khi, v, true, &nw, bflags);
+        if (!s) return true;
+        if (nw) { s->v0 = t; s->v1 = j_iadd(max_count, -acquire); return true; }
+        int64_t pass_time = t - s->v0;
+        if (pass_time > r.duration_sec * 1000) {
+            int32_t rest = (int32_t)s->v1;
+            int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
+            int32_t sum = j_iadd(rest, to_add);
+            int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
+            if (nq < 0) return false;
+            s->v1 = nq;
+            s->v0 = t;
+            return true;
+        }
+        int32_t ov = (int32_t)s->v1;
+        if (j_iadd(ov, -acquire) >= 0) { s->v1 = j_iadd(ov, -acquire); return true; }
+        return false;
+    } else if (r.grade == SG_FLOW_GRADE_THREAD) {  // passSingleValueCheck THREAD (:101-119)
+        int64_t tc = thread_count_get(S, cfg, res, epoch, v, bflags);
+        bool hf;
+        int32_t hc = hot_count(S, r, v, &hf);
+        if (hf) return ++tc <= hc;
+        int64_t threshold = j_d2l(r.count);
+        return ++tc <= threshold;
+    }
+    return true;
+}
+
+// =================================================================================
+// k_lane: one lane per segment, event by event
+// =================================================================================
+// One ENTRY through StatisticSlot -> ParamFlowSlot -> FlowSlot -> DegradeSlot
+// (param/slots/HotParamSlotChainBuilder.java:38-51, StatisticSlot.entry StatisticSlot.java:54-133).
+// rs[] is indexed only with unrolled constants, so for NRMAX <= 4 it stays in registers.
+template <int NRMAX>
+__device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg,
+                                               const Prog& pg, RState (&rs)[NRMAX], uint32_t res, int64_t t, int cnt,
+                                               uint32_t fl, uint64_t arg, uint32_t* bflags) {
+    const DRule* rules = S.rules + pg.rule_off;
+    const int np = pg.n_param, nfl = np + pg.n_flow, nr = nfl + pg.n_degrade;
+    uint32_t status = ST_PASS, slot = 0;
+    int64_t wait = 0;
+    if (np) {  // ParamFlowSlot.checkFlow (ParamFlowSlot.java:77-101): metric maps exist from now on
+        N.flags |= NI_PM;
+        if (pg.pflags & PF_PARAM_IDX0) N.flags |= NI_TM0;
+    }
+#pragma unroll
+    for (int s = 0; s < NRMAX; ++s) {
+        if (s < nr && status == ST_PASS) {
+            const DRule r = rules[s];
+            if (s < np) {
+                if (fl & SG_F_HAS_ARG) {
+                    int64_t w = 0;
+                    if (!param_check(S, cfg, res, pg.tc_epoch, r, cnt, arg, t, w, bflags)) { status = ST_BLOCK_PARAM; slot = r.slot; }
+                    else wait += w;
+                }
+            } else if (s < nfl) {  // FlowSlot.checkFlow (FlowSlot.java:146-158)
+                if (!flow_can_pass(N, C, r, rs[s], t, cnt, wait)) { status = ST_BLOCK_FLOW; slot = r.slot; }
+            } else {  // DegradeRuleManager.checkDegrade (DegradeRuleManager.java:72-85)
+                if (!degrade_pass(N, C, r, rs[s], t)) { status = ST_BLOCK_DEGRADE; slot = r.slot; }
+            }
+        }
+    }
+    const bool passed = status == ST_PASS;
+    stat_entry(N, C, t, cnt, passed);
+    // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount
+    if (passed && (N.flags & NI_PM) && (N.flags & NI_TM0) && (fl & SG_F_HAS_ARG))
+        thread_count_add(S, cfg, res, pg.tc_epoch, arg, 1, bflags);
+    return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
+}
+
+template <int NRMAX>
+__global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                              const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const Seg sg = segs[order[i]];
+    const uint32_t res = sg.res;
+    const Prog pg = S.prog[res];
+    const int nr = pg.n_param + pg.n_flow + pg.n_degrade;
+    Node N;
+    node_load(N, S, res);
+    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    RState rs[NRMAX];
+#pragma unroll
+    for (int s = 0; s < NRMAX; ++s) if (s < nr) rs[s] = S.rstate[pg.rule_off + s];
+    const bool has_chain = (N.flags & NI_CHAIN) != 0;
+    const bool chain = has_chain && cfg.switch_on;
+    if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
+        atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
+    uint64_t pm = 0;  // passed bits of the segment's first 64 positions
+    for (uint32_t j = 0; j < sg.len; ++j) {
+        const SEv r = recs[sg.start + j];
+        const int64_t t = t0 + r.dt;
+        uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+        if (r.kind == SG_EV_ENTRY) {
+            if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
+            else {
+                uint64_t arg = (r.flags & SG_F_HAS_ARG) ? ev[vals[sg.start + j]].aux : 0;
+                d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
+            }
+            if (j < 64 && st_passed(d & 0xFF)) pm |= 1ull << j;
+        } else {
+            bool eff;
+            if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
+            else if (r.code == RC_PASSED) eff = true;
+            else if (r.code == RC_NOT) eff = false;
+            else {
+                uint32_t rel = r.x - sg.start;
+                eff = rel < 64 ? ((pm >> rel) & 1) != 0 : st_passed(dec[r.x] & 0xFF);
+            }
+            if (eff) {
+                if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
+                else stat_trace(N, C, t, r.cnt);
+            }
+        }
+        dec[sg.start + j] = d;
+    }
+    min_flush(N, C.minb);
+    node_store(N, S, res, pg.pflags);
+#pragma unroll
+    for (int s = 0; s < NRMAX; ++s) if (s < nr) S.rstate[pg.rule_off + s] = rs[s];
+}
+
+// =================================================================================
+// k_jac: cooperative speculative decide of one segment by NW wavefronts
+// =================================================================================
+// inclusive wave scan with DPP row shifts + row broadcasts (GFX9 family, wave64)
+#define DPP_STEP(v, ident, ctrl, rmask, OP) \
+    v = OP((uint32_t)__builtin_amdgcn_update_dpp((int)(ident), (int)(v), ctrl, rmask, 0xf, false), v)
+#define WAVE_SCAN(v, ident, OP)              \
+    do {                                      \
+        DPP_STEP(v, ident, 0x111, 0xf, OP);   \
+        DPP_STEP(v, ident, 0x112, 0xf, OP);   \
+        DPP_STEP(v, ident, 0x114, 0xf, OP);   \
+        DPP_STEP(v, ident, 0x118, 0xf, OP);   \
+        DPP_STEP(v, ident, 0x142, 0xa, OP);   \
+        DPP_STEP(v, ident, 0x143, 0xc, OP);   \
+    } while (0)
+__device__ __forceinline__ uint32_t op_add(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t op_min(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// segmented count: bit31 = "reset here", low bits = count since the last reset; a is the earlier element
+__device__ __forceinline__ uint32_t op_seg(uint32_t a, uint32_t b) {
+    return (b & 0x80000000u) ? b : ((a & 0x80000000u) | ((a + b) & 0x7fffffffu));
+}
+__device__ __forceinline__ uint32_t shr1(uint32_t incl, uint32_t ident) {  // exclusive from inclusive
+    uint32_t v = (uint32_t)__shfl_up((int)incl, 1, 64);
+    return lane_id() == 0 ? ident : v;
+}
+__device__ __forceinline__ int64_t wscan_i64_add(int64_t x) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ int64_t wscan_i64_max(int64_t x) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x = x > y ? x : y;
+    }
+    return x;
+}
+#define NEG_INF64 ((int64_t)0x8000000000000000LL)
+
+#define NO_LANE 0xFFFFFFFFu
+
+// u32 quantities scanned block-wide in one Jacobi iteration (counts <= 1024 are packed in halves)
+enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR /* trip counts, 2 per word */ };
+
+template <int NW, int MF, int MD>
+struct JacSh {
+    Node node;
+    DRule rules[MF + MD];
+    RState rs[MF + MD];
+    RState syn[MF];  // WarmUp state synced at the round's second
+    // round base: the node's window sums at the round's bucket
+    int64_t bP, bB, bS, bRT, bE, bEM, bTH;
+    int64_t bkt0, next_reset, tnext;
+    // committed inside the round (folded into the node by the leader at round end)
+    int64_t cP, cB, cS, cRT, cE, cTH;
+    uint32_t cminrt, ctouch;
+    uint32_t has_sync, warm_reach;
+    uint32_t c0, last_out, round_open, pad;
+    uint32_t part[NW][Q_TR + (MD + 1) / 2];
+    uint32_t pseg[NW][MD];
+    int64_t prl[NW][4];
+    uint32_t mism[2][NW];
+};
+
+// leader: fold the round's committed deltas into the node (StatisticSlot bookkeeping of every
+// committed event, as one bucket update) and persist WarmUp syncs that some entry reached
+template <class SH>
+__device__ void round_fold(SH& sh, const Ctx& C, int nf) {
+    if (!sh.round_open) return;
+    Node& N = sh.node;
+    const int64_t tc = sh.bkt0 * 500;
+    if (sh.ctouch) {
+        int sl = sec_current(N, tc, C.max_rt);
+        const int64_t mrt = sh.cminrt == NO_LANE ? INT64_MAX : (int64_t)sh.cminrt;
+        sec_add(N, sl, sh.cP, sh.cB, sh.cS, sh.cRT, sh.cE, mrt);
+        min_current(N, C.minb, tc, C.max_rt, C.pflags);
+        if (!(N.mst & MS_DETACHED)) {
+            min_add(N, sh.cP, sh.cB, sh.cS, sh.cRT, sh.cE, mrt);
+            if (N.exc_sum_sec == tc - tc % 1000) N.exc_sum += sh.cE;
+        }
+    }
+    N.thread += (int32_t)sh.cTH;
+    for (int s = 0; s < nf; ++s)
+        if ((sh.has_sync >> s) & 1 & (sh.warm_reach >> s)) { sh.rs[s].a = sh.syn[s].a; sh.rs[s].b = sh.syn[s].b; }
+    sh.round_open = 0;
+}
+// leader: open the round of the 500 ms bucket holding tn.  Side-effect free in Java terms: bucket
+// resets happen at fold time, only if a committed event touched the windows.
+template <class SH>
+__device__ void round_setup(SH& sh, const Ctx& C, int nf, int nd, int64_t tn) {
+    Node& N = sh.node;
+    const int64_t b0 = tn / 500, T = tn - tn % 1000;
+    min_flush(N, C.minb);  // HBM holds the current minute bucket from here on
+    int64_t next_reset = INT64_MAX;
+    for (int k = 0; k < nd; ++k) {  // ResetTask due (Q12)
+        RState& s = sh.rs[nf + k];
+        if (s.a && tn >= s.c) { s.a = 0; s.b = 0; }
+        if (s.a && s.c < next_reset) next_reset = s.c;
+    }
+    const Bkt& cur = (b0 & 1) ? N.sb[1] : N.sb[0];
+    const Bkt& prv = (b0 & 1) ? N.sb[0] : N.sb[1];
+    const bool cv = cur.ws >= b0 * 500;  // else currentWindow resets it before any read
+    const bool pv = prv.ws >= 0 && tn - prv.ws <= 1000;
+    sh.bP = (cv ? cur.pass : 0) + (pv ? prv.pass : 0);
+    sh.bB = (cv ? cur.block : 0) + (pv ? prv.block : 0);
+    sh.bS = (cv ? cur.succ : 0) + (pv ? prv.succ : 0);
+    sh.bRT = (cv ? cur.rt : 0) + (pv ? prv.rt : 0);
+    sh.bE = (cv ? cur.exc : 0) + (pv ? prv.exc : 0);
+    sh.bTH = N.thread;
+    sh.bEM = 0;
+    if (C.pflags & PF_EXC_COUNT) {  // StatisticNode.totalException at T
+        if (N.exc_sum_sec < T) exc_advance(N, C.minb, T);
+        if (N.exc_sum_sec != T) {
+            int64_t s = 0;
+            for (int k = 0; k < 60; ++k) {
+                Bkt b = C.minb[k];
+                if (b.ws >= T - 59000 && b.ws <= T) s += b.exc;
+            }
+            N.exc_sum = s;
+            N.exc_sum_sec = T;
+        }
+        sh.bEM = N.exc_sum;
+    }
+    sh.has_sync = 0;
+    for (int s = 0; s < nf; ++s) {  // WarmUpController.syncToken at this second (persisted if reached)
+        const DRule& r = sh.rules[s];
+        if ((r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) &&
+            T > sh.rs[s].b) {
+            const int slot = (int)(((tn - 1000) / 1000) % 60);
+            const Bkt b = C.minb[slot];
+            int64_t prev = 0;
+            if (!(b.ws < 0 || tn - b.ws > 60000 || b.ws + 1000 < tn - 1000)) prev = b.pass;
+            RState tmp = sh.rs[s];
+            warm_sync(r, tmp, tn, prev);
+            sh.syn[s] = tmp;
+            sh.has_sync |= 1u << s;
+        }
+    }
+    sh.warm_reach = 0;
+    sh.bkt0 = b0;
+    sh.next_reset = next_reset;
+    sh.cP = sh.cB = sh.cS = sh.cRT = sh.cE = sh.cTH = 0;
+    sh.cminrt = NO_LANE;
+    sh.ctouch = 0;
+    sh.round_open = 1;
+}
+
+__device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, int nf, uint32_t o, int64_t wait) {
+    if (o == (uint32_t)nr) return mk_dec(ST_PASS, 0, wait);
+    return mk_dec((int)o < nf ? ST_BLOCK_FLOW : ST_BLOCK_DEGRADE, rules[o].slot, 0);
+}
+
+template <int NW, int WINLOG, int MF, int MD, bool RL>
+__global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                                const uint32_t* __restrict__ order, uint32_t m, DevState S,
+                                                DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec,
+                                                uint32_t* __restrict__ bflags) {
+    constexpr uint32_t HW = NW * 64;
+    constexpr uint32_t WIN = 1u << WINLOG;
+    constexpr int NQ = Q_TR + (MD + 1) / 2;
+    static_assert(WIN >= 2 * HW, "status window must hold two tiles");
+    __shared__ JacSh<NW, MF, MD> sh;
+    __shared__ uint8_t win[WIN];
+    if (blockIdx.x >= m) return;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t lane = tid & 63;
+    const Seg sg = segs[order[blockIdx.x]];
+    const uint32_t res = sg.res;
+    const Prog pg = S.prog[res];
+    const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
+    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    if (tid == 0) {
+        node_load(sh.node, S, res);
+        sh.round_open = 0;
+        sh.c0 = 0;
+        sh.last_out = (uint32_t)nr;
+    }
+    if ((int)tid < nr) {
+        sh.rules[tid] = S.rules[pg.rule_off + tid];
+        sh.rs[tid] = S.rstate[pg.rule_off + tid];
+    }
+    __syncthreads();
+    const bool chain = (sh.node.flags & NI_CHAIN) != 0;  // host routes switch_on == 0 to k_lane
+    if (!chain) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted
+        for (uint32_t p = tid; p < sg.len; p += HW)
+            dec[sg.start + p] = recs[sg.start + p].kind == SG_EV_ENTRY ? mk_dec(ST_NO_CHECK, 0, 0)
+                                                                        : mk_dec(ST_NOT_ENTRY, 0, 0);
+        return;
+    }
+    if (tid == 0) {
+        const int64_t tf = t0 + recs[sg.start].dt;
+        if (tf < (sh.node.sb[0].ws > sh.node.sb[1].ws ? sh.node.sb[0].ws : sh.node.sb[1].ws))
+            atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
+    }
+    int rl_s0 = -1, rl_s1 = -1;  // rate-limiter stages (uniform)
+    if (RL) {
+        for (int s = 0; s < nf; ++s) {
+            uint8_t b = sh.rules[s].behavior;
+            if (b == SG_CONTROL_BEHAVIOR_RATE_LIMITER || b == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
+                if (rl_s0 < 0) rl_s0 = s; else rl_s1 = s;
+            }
+        }
+    }
+    const bool has_rt = (pg.pflags & PF_RT) != 0;
+    const bool frozen_prog = (pg.pflags & PF_FROZEN) != 0;
+
+    // diagnostics (SG_DEBUG=1): per-bin iteration counters, phase cycles of the bin's first segment
+    const bool prof = S.dbg != nullptr;
+    const bool prof0 = prof && blockIdx.x == 0 && tid == 0;
+    unsigned long long n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0;
+    unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[6] = {0, 0, 0, 0, 0, 0};
+#define PROF_MARK(k)                                          \
+    if (prof0) {                                              \
+        unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+        tph[k] += _n - tmA;                                   \
+        tmA = _n;                                             \
+    }
+
+    // ---- per-lane tile state
+    uint32_t tbase = 0;
+    SEv cur, nxt;
+    cur.kind = 0xFF;
+    nxt.kind = 0xFF;
+    if (tid < sg.len) cur = recs[sg.start + tid];
+    if (HW + tid < sg.len) nxt = recs[sg.start + HW + tid];
+    bool valid = false, eff_win = false, eff_val = false;
+    uint32_t winidx = 0, refrel = 0, kind = 0xFF, cnt = 0, rtv = 0;
+    int64_t t = 0, tb = 0;
+    auto decode = [&](const SEv& r, uint32_t pos) {
+        valid = pos < sg.len;
+        kind = valid ? r.kind : 0xFFu;
+        t = t0 + (valid ? r.dt : 0);
+        tb = t / 500;
+        cnt = r.cnt;
+        rtv = r.rt;
+        eff_win = false;
+        eff_val = false;
+        refrel = NO_LANE;
+        if (valid && kind != SG_EV_ENTRY) {
+            if (r.code == RC_NONE || r.code == RC_PASSED) eff_val = true;  // the chain exists here
+            else if (r.code == RC_BATCH) {
+                refrel = r.x - sg.start;
+                if (refrel + WIN >= tbase + HW) { eff_win = true; winidx = refrel & (WIN - 1); }
+                else eff_val = st_passed(dec[r.x] & 0xFF);  // decided >= WIN-HW positions ago
+            }
+        }
+    };
+    auto advance = [&]() {  // next tile (uniform)
+        tbase += HW;
+        cur = nxt;
+        nxt.kind = 0xFF;
+        if (tbase + HW + tid < sg.len) nxt = recs[sg.start + tbase + HW + tid];
+        decode(cur, tbase + tid);
+        ++n_tile;
+    };
+    decode(cur, tid);
+    uint32_t g = (uint32_t)nr;  // outcome guess: index of the blocking stage, nr = pass
+    if (valid) win[tid & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
+    if (tid == 0) sh.tnext = t;
+    __syncthreads();
+    uint32_t mb = 0;  // mism double-buffer index
+
+    for (;;) {
+        uint32_t c0 = sh.c0;
+        const uint32_t cnt_t = sg.len - tbase < HW ? sg.len - tbase : HW;
+        if (c0 >= cnt_t) {  // tile done: advance (uniform)
+            if (tbase + HW >= sg.len) break;
+            advance();
+            g = sh.last_out;
+            if (valid) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
+            __syncthreads();  // everyone has read sh.last_out / sh.c0
+            if (tid == 0) { sh.c0 = 0; sh.tnext = t; }
+            __syncthreads();
+            c0 = 0;
+        }
+        ++n_it;
+        PROF_MARK(0)
+        {  // round check on the event at c0 (uniform)
+            const int64_t tn = sh.tnext;
+            const bool need = !sh.round_open || (tn / 500) != sh.bkt0 || tn >= sh.next_reset;
+            if (need) {
+                if (tid == 0) {
+                    round_fold(sh, C, nf);
+                    round_setup(sh, C, nf, nd, tn);
+                }
+                __syncthreads();
+                ++n_round;
+            }
+        }
+        const int64_t bkt0 = sh.bkt0, next_reset = sh.next_reset;
+
+        // ================= frozen stretch =================
+        // All flow stages are QPS DefaultControllers and either one of them is already saturated
+        // for acquire >= 1, or the first breaker is cut: until the round ends no ENTRY can pass, so
+        // the pass count and every rule state stay fixed, each verdict is a pure function of the
+        // event, and the rest of the round is a map + reduction (one barrier per tile).
+        if (frozen_prog) {
+            const int64_t Pfix = sh.bP + sh.cP;
+            const int32_t pint = j_d2i((double)Pfix);
+            const bool cutk0 = nd > 0 && sh.rs[nf].a != 0;
+            bool sat = false;
+#pragma unroll
+            for (int s = 0; s < MF; ++s)
+                if (s < nf) sat |= (double)j_iadd(pint, 1) > sh.rules[s].count;
+            if (sat || cutk0) {
+                const uint32_t fpos0 = tbase + c0;  // stretch start (segment position)
+                uint32_t aB = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aMin = NO_LANE, aTH = 0;
+                for (;;) {
+                    const uint32_t ct = sg.len - tbase < HW ? sg.len - tbase : HW;
+                    const bool inr = valid && tid >= c0 && tb == bkt0 && t < next_reset;
+                    uint32_t of = (uint32_t)nr;
+                    bool ok = true;
+                    if (inr && kind == SG_EV_ENTRY) {
+                        of = NO_LANE;
+#pragma unroll
+                        for (int s = 0; s < MF; ++s)
+                            if (s < nf && of == NO_LANE && (double)j_iadd(pint, (int)cnt) > sh.rules[s].count)
+                                of = (uint32_t)s;
+                        if (of == NO_LANE && cutk0) of = (uint32_t)nf;
+                        ok = of != NO_LANE;
+                    }
+                    const uint64_t stop = __ballot(valid && tid >= c0 && (!inr || !ok));
+                    if (lane == 0) sh.mism[mb][wv] = stop ? wv * 64 + (uint32_t)(__ffsll((long long)stop) - 1) : NO_LANE;
+                    __syncthreads();
+                    uint32_t f = NO_LANE;
+                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    mb ^= 1;
+                    const uint32_t fend = f != NO_LANE ? f : ct;
+                    ++n_frz;
+                    if (inr && tid < fend) {
+                        const uint32_t pos = tbase + tid;
+                        uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                        if (kind == SG_EV_ENTRY) {
+                            d = out_to_dec(sh.rules, nr, nf, of, 0);
+                            win[pos & (WIN - 1)] = 0;
+                            aB += cnt;
+                            aTI += 1;
+                        } else {
+                            bool eff = eff_win ? (refrel >= fpos0 ? false : win[winidx] != 0) : eff_val;
+                            if (eff && kind == SG_EV_EXIT) {
+                                aS += cnt; aRT += rtv; aTH -= 1; aMin = op_min(aMin, rtv); aTI += 1;
+                            } else if (eff && kind == SG_EV_TRACE && cnt > 0) {
+                                aE += cnt; aTI += 1;
+                            }
+                        }
+                        dec[sg.start + pos] = d;
+                    }
+                    if (f != NO_LANE || tbase + HW >= sg.len) { c0 = fend; break; }
+                    advance();  // the whole tile was frozen: the stretch goes on
+                    c0 = 0;
+                }
+                // stretch end: reduce the lane accumulators into the round's committed totals
+                WAVE_SCAN(aB, 0u, op_add);
+                WAVE_SCAN(aS, 0u, op_add);
+                WAVE_SCAN(aRT, 0u, op_add);
+                WAVE_SCAN(aE, 0u, op_add);
+                WAVE_SCAN(aTI, 0u, op_add);
+                WAVE_SCAN(aTH, 0u, op_add);
+                WAVE_SCAN(aMin, NO_LANE, op_min);
+                if (lane == 63) {
+                    sh.part[wv][0] = aB; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
+                    sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin;
+                }
+                // guesses of the lanes after the stretch: the frozen verdict
+                g = (cutk0 && !sat) ? (uint32_t)nf : 0u;
+                const uint32_t ct = sg.len - tbase < HW ? sg.len - tbase : HW;
+                if (valid && tid >= c0) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
+                if (c0 < ct && tid == c0) sh.tnext = t;
+                __syncthreads();
+                if (tid == 0) {
+                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                        sh.cB += sh.part[w][0]; sh.cS += sh.part[w][1]; sh.cRT += sh.part[w][2]; sh.cE += sh.part[w][3];
+                        sh.ctouch += sh.part[w][4]; sh.cTH += (int32_t)sh.part[w][5];
+                        sh.cminrt = op_min(sh.cminrt, sh.part[w][6]);
+                    }
+                    sh.last_out = g;
+                    sh.c0 = c0;
+                }
+                __syncthreads();
+                continue;
+            }
+        }
+
+        // ================= Jacobi iteration =================
+        const bool inr = valid && tid >= c0 && tb == bkt0 && t < next_reset;
+        const bool ent = inr && kind == SG_EV_ENTRY;
+        const bool eff = eff_win ? (win[winidx] != 0) : eff_val;
+        const bool xe = inr && kind == SG_EV_EXIT && eff;
+        const bool te = inr && kind == SG_EV_TRACE && eff && cnt > 0;
+        const uint32_t has_sync = sh.has_sync;
+
+        // ---- phase B: counter deltas under the guesses, wave scans
+        uint32_t ex[NQ];
+        {
+            const bool gp = ent && g == (uint32_t)nr;
+            uint32_t q[NQ];
+            q[Q_P] = gp ? cnt : 0u;
+            q[Q_B] = (ent && !gp) ? cnt : 0u;
+            q[Q_S] = xe ? cnt : 0u;
+            q[Q_RT] = xe ? rtv : 0u;
+            q[Q_E] = te ? cnt : 0u;
+            q[Q_TH] = gp ? 1u : (xe ? 0xFFFFFFFFu : 0u);
+            q[Q_MIN] = xe ? rtv : NO_LANE;
+            q[Q_TI] = ((ent || xe || te) ? 1u : 0u) | (inr ? 0x10000u : 0u);
+#pragma unroll
+            for (int k = 0; k < (MD + 1) / 2; ++k) {
+                uint32_t w = 0;
+                if (ent && g == (uint32_t)(nf + 2 * k)) w |= 1u;
+                if (ent && g == (uint32_t)(nf + 2 * k + 1)) w |= 0x10000u;
+                q[Q_TR + k] = w;
+            }
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                uint32_t v = q[k];
+                if (k == Q_MIN) {
+                    WAVE_SCAN(v, NO_LANE, op_min);
+                    ex[k] = shr1(v, NO_LANE);
+                } else {
+                    WAVE_SCAN(v, 0u, op_add);
+                    ex[k] = v - q[k];
+                }
+                if (lane == 63) sh.part[wv][k] = v;
+            }
+        }
+        // rate limiters: exclusive prefix of the costs (C) and the max-plus term (M) of updating lanes
+        int64_t rl_cost_l[2] = {0, 0}, rl_C[2] = {0, 0}, rl_M[2] = {NEG_INF64, NEG_INF64};
+        if (RL) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int s = k == 0 ? rl_s0 : rl_s1;
+                if (s >= 0) {
+                    const DRule& r = sh.rules[s];
+                    const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                    const int64_t cost = rl_cost(r, st, (int)cnt);
+                    const bool upd = ent && g > (uint32_t)s &&
+                                     (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || ((int)cnt > 0 && r.count > 0));
+                    const int64_t ci = wscan_i64_add(upd ? cost : 0);
+                    const int64_t mi = wscan_i64_max(upd ? t - ci : NEG_INF64);
+                    if (lane == 63) { sh.prl[wv][2 * k] = ci; sh.prl[wv][2 * k + 1] = mi; }
+                    rl_cost_l[k] = cost;
+                    rl_C[k] = ci - (upd ? cost : 0);
+                    const int64_t me = __shfl_up(mi, 1, 64);
+                    rl_M[k] = lane == 0 ? NEG_INF64 : me;
+                }
+            }
+        }
+        PROF_MARK(1)
+        __syncthreads();  // B2
+        PROF_MARK(2)
+        uint32_t inr_total = 0;
+        {
+            // block-wide: lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const uint32_t ident = k == Q_MIN ? NO_LANE : 0u;
+                uint32_t v = lane < (uint32_t)NW ? sh.part[lane][k] : ident;
+                uint32_t incl = v;
+                if (k == Q_MIN) WAVE_SCAN(incl, NO_LANE, op_min);
+                else WAVE_SCAN(incl, 0u, op_add);
+                const uint32_t pre = wv == 0 ? ident : (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)wv - 1);
+                ex[k] = k == Q_MIN ? op_min(pre, ex[k]) : ex[k] + pre;
+                if (k == Q_TI) inr_total = (uint32_t)__builtin_amdgcn_readlane((int)incl, NW - 1) >> 16;
+            }
+        }
+        if (RL) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int s = k == 0 ? rl_s0 : rl_s1;
+                if (s >= 0) {
+                    int64_t cb = 0, mbx = NEG_INF64;
+                    for (uint32_t w = 0; w < wv; ++w) {
+                        const int64_t cw = sh.prl[w][2 * k], mw = sh.prl[w][2 * k + 1];
+                        if (mw != NEG_INF64 && mw - cb > mbx) mbx = mw - cb;
+                        cb += cw;
+                    }
+                    const int64_t ml = rl_M[k] == NEG_INF64 ? NEG_INF64 : rl_M[k] - cb;
+                    rl_M[k] = ml > mbx ? ml : mbx;
+                    rl_C[k] += cb;
+                }
+            }
+        }
+        // lane views (base + committed-in-round + prefix)
+        const int64_t vP = sh.bP + sh.cP + ex[Q_P];
+        const int64_t vS = sh.bS + sh.cS + ex[Q_S];
+        const int64_t vRT = sh.bRT + sh.cRT + ex[Q_RT];
+
+        // ---- phase C: RT breaker passCount (segmented scan over the lanes that check it)
+        uint32_t badm = 0, cutm = 0;  // per degrade stage bits
+        int32_t bbefore[MD];
+#pragma unroll
+        for (int k = 0; k < MD; ++k) {
+            bbefore[k] = 0;
+            if (k < nd) {
+                const DRule& r = sh.rules[nf + k];
+                if (sh.rs[nf + k].a) cutm |= 1u << k;
+                if (r.grade == SG_DEGRADE_GRADE_RT) {
+                    const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
+                    if (!(avg < r.count)) badm |= 1u << k;
+                }
+            }
+        }
+        if (has_rt) {
+            uint32_t segx[MD];
+#pragma unroll
+            for (int k = 0; k < MD; ++k) {
+                segx[k] = 0;
+                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                    const bool chk = ent && g >= (uint32_t)(nf + k);
+                    const uint32_t el = chk ? (((badm >> k) & 1) ? 1u : 0x80000000u) : 0u;
+                    uint32_t v = el;
+                    WAVE_SCAN(v, 0u, op_seg);
+                    segx[k] = shr1(v, 0u);
+                    if (lane == 63) sh.pseg[wv][k] = v;
+                }
+            }
+            __syncthreads();  // B3
+#pragma unroll
+            for (int k = 0; k < MD; ++k) {
+                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                    uint32_t pre = 0;
+                    for (uint32_t w = 0; w < wv; ++w) pre = op_seg(pre, sh.pseg[w][k]);
+                    const uint32_t x = op_seg(pre, segx[k]);
+                    const int32_t c = (int32_t)(x & 0x7fffffffu);
+                    bbefore[k] = (x & 0x80000000u) ? c : (int32_t)sh.rs[nf + k].b + c;
+                }
+            }
+        }
+
+        // ---- evaluation of every lane's chain under its view
+        uint32_t o = (uint32_t)nr;
+        int64_t wait = 0;
+#pragma unroll
+        for (int s = 0; s < MF; ++s) {
+            if (s < nf) {
+                const DRule& r = sh.rules[s];
+                bool ok = true;
+                int64_t w = 0;
+                if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP) {
+                    const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                    if (st.a >= r.warning_token) ok = (double)(vP + (int)cnt) <= warm_qps(r, st.a);
+                    else ok = (double)(vP + (int)cnt) <= r.count;
+                } else if (RL && (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
+                                  r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)) {
+                    const int k = (s == rl_s0) ? 0 : 1;
+                    const int64_t L0 = sh.rs[s].c;
+                    const int64_t cexcl = k == 0 ? rl_C[0] : rl_C[1];
+                    const int64_t mexcl = k == 0 ? rl_M[0] : rl_M[1];
+                    const int64_t cost = k == 0 ? rl_cost_l[0] : rl_cost_l[1];
+                    const int64_t L = cexcl + (mexcl > L0 ? mexcl : L0);
+                    if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && (int)cnt <= 0) ok = true;
+                    else if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && r.count <= 0) ok = false;
+                    else {
+                        const int64_t expected = L + cost;
+                        if (expected <= t) ok = true;
+                        else { w = expected - t; ok = w <= r.max_queue; }
+                    }
+                } else {  // DefaultController
+                    const int32_t curv = r.grade == SG_FLOW_GRADE_THREAD
+                                             ? (int32_t)(sh.bTH + sh.cTH + (int64_t)(int32_t)ex[Q_TH])
+                                             : j_d2i((double)vP);
+                    ok = !((double)j_iadd(curv, (int)cnt) > r.count);
+                }
+                if (o == (uint32_t)nr) {
+                    if (!ok) o = (uint32_t)s;
+                    else if (w > 0) wait += w;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < MD; ++k) {
+            if (k < nd) {
+                const DRule& r = sh.rules[nf + k];
+                const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
+                bool ok;
+                if (((cutm >> k) & 1) || trip_ex > 0) ok = false;
+                else if (r.grade == SG_DEGRADE_GRADE_RT) ok = !((badm >> k) & 1) || (bbefore[k] + 1 < 5);
+                else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+                    const double exc = (double)(sh.bE + sh.cE + ex[Q_E]) / 1.0, succ = (double)vS / 1.0;
+                    const double total = (double)vP / 1.0 + (double)(sh.bB + sh.cB + ex[Q_B]) / 1.0;
+                    if (total < 5) ok = true;
+                    else if (succ - exc <= 0 && exc < 5) ok = true;
+                    else ok = exc / succ < r.count;
+                } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT)
+                    ok = (double)(sh.bEM + sh.cE + ex[Q_E]) < r.count;
+                else ok = true;
+                if (o == (uint32_t)nr && !ok) o = (uint32_t)(nf + k);
+            }
+        }
+        {
+            const uint64_t mm = __ballot(ent && o != g);
+            if (lane == 0) sh.mism[mb][wv] = mm ? wv * 64 + (uint32_t)(__ffsll((long long)mm) - 1) : NO_LANE;
+        }
+        PROF_MARK(3)
+        __syncthreads();  // B4
+        uint32_t f = NO_LANE;
+        for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+        mb ^= 1;
+        if (f != NO_LANE) ++n_mm;
+        const uint32_t e_end = c0 + inr_total;
+        const uint32_t cend = f != NO_LANE ? f + 1 : e_end;
+
+        // ---- phase D: commit [c0, cend), re-guess the rest
+        const bool com = inr && tid < cend;
+        const uint32_t fo = (tid == f) ? o : g;
+        const uint32_t pos = tbase + tid;
+        if (com) {
+            const uint32_t d = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wait) : mk_dec(ST_NOT_ENTRY, 0, 0);
+            dec[sg.start + pos] = d;
+            win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
+            g = fo;
+        } else if (ent) {
+            g = o;
+            win[pos & (WIN - 1)] = (o == (uint32_t)nr) ? 1 : 0;
+        }
+        // the first blocking degrade verdict of a committed lane trips the breaker (DegradeRule.passCheck cut)
+#pragma unroll
+        for (int k = 0; k < MD; ++k) {
+            const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
+            if (k < nd && com && kind == SG_EV_ENTRY && fo == (uint32_t)(nf + k) && !((cutm >> k) & 1) && trip_ex == 0) {
+                const DRule& r = sh.rules[nf + k];
+                RState& s = sh.rs[nf + k];
+                if (r.grade == SG_DEGRADE_GRADE_RT) s.b = bbefore[k] + 1;
+                s.a = 1;
+                s.c = t + (int64_t)r.time_window * 1000;
+            }
+        }
+        if (has_sync) {
+            for (int s = 0; s < nf; ++s) {
+                if ((has_sync >> s) & 1) {
+                    const uint64_t rb = __ballot(com && kind == SG_EV_ENTRY && fo >= (uint32_t)s);
+                    if (lane == 0 && rb) atomicOr(&sh.warm_reach, 1u << s);
+                }
+            }
+        }
+        if (tid == cend - 1) {  // pivot: the last committed lane carries the committed totals
+            const bool ce = kind == SG_EV_ENTRY;
+            const bool cp = ce && fo == (uint32_t)nr;
+            sh.cP += ex[Q_P] + (cp ? cnt : 0);
+            sh.cB += ex[Q_B] + ((ce && !cp) ? cnt : 0);
+            sh.cS += ex[Q_S] + (xe ? cnt : 0);
+            sh.cRT += ex[Q_RT] + (xe ? rtv : 0);
+            sh.cE += ex[Q_E] + (te ? cnt : 0);
+            sh.cTH += (int64_t)(int32_t)ex[Q_TH] + (cp ? 1 : (xe ? -1 : 0));
+            sh.ctouch += (ex[Q_TI] & 0xFFFFu) + ((ce || xe || te) ? 1 : 0);
+            sh.cminrt = op_min(sh.cminrt, op_min(ex[Q_MIN], xe ? rtv : NO_LANE));
+            if (RL) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int s = k == 0 ? rl_s0 : rl_s1;
+                    if (s >= 0) {
+                        const DRule& r = sh.rules[s];
+                        const int64_t L0 = sh.rs[s].c;
+                        const int64_t cexcl = k == 0 ? rl_C[0] : rl_C[1];
+                        const int64_t mexcl = k == 0 ? rl_M[0] : rl_M[1];
+                        const int64_t cost = k == 0 ? rl_cost_l[0] : rl_cost_l[1];
+                        int64_t L = cexcl + (mexcl > L0 ? mexcl : L0);
+                        const bool upd = ce && fo > (uint32_t)s &&
+                                         (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || ((int)cnt > 0 && r.count > 0));
+                        if (upd) L = (t > L + cost) ? t : L + cost;
+                        sh.rs[s].c = L;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < MD; ++k) {
+                const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
+                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT && !((cutm >> k) & 1) && trip_ex == 0 &&
+                    !(ce && fo == (uint32_t)(nf + k))) {
+                    int32_t b = bbefore[k];
+                    if (ce && fo > (uint32_t)(nf + k)) b = ((badm >> k) & 1) ? b + 1 : 0;
+                    sh.rs[nf + k].b = b;
+                }
+            }
+            if (ce) sh.last_out = fo;
+            sh.c0 = cend;
+        }
+        {
+            const uint32_t cnt_now = sg.len - tbase < HW ? sg.len - tbase : HW;
+            if (tid == cend && cend < cnt_now) sh.tnext = t;
+        }
+        PROF_MARK(4)
+        __syncthreads();  // B1
+        PROF_MARK(5)
+    }
+    if (prof && tid == 0) {
+        atomicAdd(&S.dbg[0], n_it);
+        atomicAdd(&S.dbg[1], n_round);
+        atomicAdd(&S.dbg[2], n_tile);
+        atomicAdd(&S.dbg[3], n_mm);
+        atomicAdd(&S.dbg[4], 1ull);
+        atomicAdd(&S.dbg[6], n_frz);
+        if (blockIdx.x == 0) {
+            S.dbg[5] = sg.len;
+            for (int k = 0; k < 6; ++k) S.dbg[8 + k] = tph[k];
+        }
+    }
+#undef PROF_MARK
+    // end of segment: fold the last round, write the node and rule states back
+    if (tid == 0) {
+        round_fold(sh, C, nf);
+        min_flush(sh.node, C.minb);
+        node_store(sh.node, S, res, pg.pflags);
+    }
+    __syncthreads();
+    if ((int)tid < nr) S.rstate[pg.rule_off + tid] = sh.rs[tid];
+}
+
+// =================================================================================
+// host-callable launch wrappers
+// =================================================================================
+namespace sg {
+
+hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
+                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                      uint32_t* part, uint32_t* nseg) {
+    uint32_t nb = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_seg_flags, dim3(nb), dim3(256), 0, st, keys, n, flag);
+    hipError_t e = scan(flag, pos, n, part, nseg, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_start, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs);
+    return hipGetLastError();
+}
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
+                          uint32_t j4_max, uint32_t force_lane, uint32_t* bin_cnt, hipStream_t st) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_bin, dim3((m + 255) / 256), dim3(256), 0, st, segs, m, n, prog, lane_max, j1_max, j4_max,
+                       force_lane, bin_cnt);
+    return hipGetLastError();
+}
+hipError_t launch_seg_order(const Seg* segs, uint32_t m, uint32_t* cursor, uint32_t* order, hipStream_t st) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_order, dim3((m + 255) / 256), dim3(256), 0, st, segs, m, cursor, order);
+    return hipGetLastError();
+}
+hipError_t launch_prep(const sg_event* ev, const uint32_t* vals, uint64_t n, uint32_t* pos_of, uint64_t gbase,
+                       const uint8_t* ring, uint64_t ring_mask, int32_t max_rt, SEv* recs, uint32_t* bflags,
+                       hipStream_t st) {
+    uint32_t nb = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_posof, dim3(nb), dim3(256), 0, st, vals, n, pos_of);
+    hipLaunchKernelGGL(k_prep, dim3(nb), dim3(256), 0, st, ev, vals, n, pos_of, gbase, ring, ring_mask, max_rt, recs,
+                       bflags);
+    return hipGetLastError();
+}
+hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
+                       uint64_t ring_mask, uint32_t* out, hipStream_t st) {
+    uint32_t nb = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_post, dim3(nb), dim3(256), 0, st, pos_of, dec, n, gbase, ring, ring_mask, out);
+    return hipGetLastError();
+}
+hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
+                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, hipStream_t st) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_chain, dim3((m + 255) / 256), dim3(256), 0, st, recs, vals, segs, m, info, grant_all, ncand,
+                       cand);
+    return hipGetLastError();
+}
+// bin = BIN_J16 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16
+hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                             const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
+                             uint32_t* dec, uint32_t* bflags, hipStream_t st) {
+    if (!m) return hipSuccess;
+    switch (bin) {
+    case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter
+        hipLaunchKernelGGL((k_jac<16, 15, 2, 2, false>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
+                           dec, bflags);
+        break;
+    case BIN_J4:
+        hipLaunchKernelGGL((k_jac<4, 14, JMAX_FLOW, JMAX_DEG, true>), dim3(m), dim3(256), 0, st, recs, segs, order, m, S,
+                           cfg, t0, dec, bflags);
+        break;
+    case BIN_J1:
+        hipLaunchKernelGGL((k_jac<1, 12, JMAX_FLOW, JMAX_DEG, true>), dim3(m), dim3(64), 0, st, recs, segs, order, m, S,
+                           cfg, t0, dec, bflags);
+        break;
+    case BIN_LANE:
+        hipLaunchKernelGGL(k_lane<4>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg,
+                           t0, dec, bflags);
+        break;
+    default:
+        hipLaunchKernelGGL(k_lane<MAXR>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S,
+                           cfg, t0, dec, bflags);
+        break;
+    }
+    return hipGetLastError();
+}
+
+} // namespace sg

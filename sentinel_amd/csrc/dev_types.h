@@ -45,7 +45,18 @@ struct NodeInfo {
 };
 static_assert(sizeof(NodeInfo) == 32, "NodeInfo must be 32 B");
 
-enum : uint8_t { PF_EXC_COUNT = 1, PF_WARM = 2, PF_PARAM_IDX0 = 4 };
+// Prog.pflags: what the decide kernels need to know about a resource's rule program
+enum : uint8_t {
+    PF_EXC_COUNT = 1,   // has an EXCEPTION_COUNT breaker (minute exception running sum)
+    PF_WARM = 2,        // has a WarmUp / WarmUpRateLimiter controller
+    PF_PARAM_IDX0 = 4,  // has a param rule on args[0]
+    PF_SERIAL = 8,      // outside the cooperative (Jacobi) kernels' limits: per-lane serial kernel only
+    PF_RL = 16,         // has a RateLimiter / WarmUpRateLimiter controller
+    PF_RT = 32,         // has an RT breaker
+    PF_FROZEN = 64,     // every flow stage is a QPS DefaultController: saturated / cut stretches are pure
+                        // reductions (decide.hip k_jac frozen stretch)
+    PF_J16 = 128        // fits the 1024-lane kernel's shape: <= 2 flow, <= 2 degrade stages, no rate limiter
+};
 
 struct Prog {
     uint32_t rule_off;
@@ -116,11 +127,12 @@ struct DevCfg {
     uint32_t pad;
 };
 
+// one resource's events inside a batch: sorted positions [start, start+len)
 struct Seg {
     uint32_t res;
     uint32_t start;
     uint32_t len;
-    uint32_t pad;
+    uint32_t bin;    // BIN_*
 };
 
 struct DevState {
@@ -136,6 +148,39 @@ struct DevState {
     unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
 };
 
-enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8 };
+enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
+                  BF_BACKWARD = 32, BF_TSPAN = 64 };
+
+// One event in resource-sorted order (16 B), built by k_prep from the caller's 24-byte
+// sg_event so that every decide kernel streams its segment with coalesced loads.
+struct SEv {
+    int32_t dt;      // ts - t0 (t0 = ts of the batch's first event)
+    uint32_t x;      // EXIT/TRACE with code RC_BATCH: sorted position of the referenced ENTRY
+    uint16_t cnt;    // acquire / exit / trace count
+    uint16_t rt;     // EXIT: response time clipped to statistic_max_rt (StatisticSlot.exit)
+    uint8_t kind;    // SG_EV_*
+    uint8_t flags;   // SG_F_*
+    uint8_t code;    // EXIT/TRACE: RC_*
+    uint8_t pad;
+};
+static_assert(sizeof(SEv) == 16, "SEv must be 16 B");
+// how an EXIT/TRACE's ENTRY reference resolved
+enum : uint8_t {
+    RC_NONE = 0,    // no reference (or unknown entry): effective iff the resource has a chain
+    RC_BATCH = 1,   // ENTRY earlier in this batch, same resource: effective iff it passed
+    RC_PASSED = 2,  // ENTRY of an earlier batch that passed
+    RC_NOT = 3      // ENTRY that did not pass (blocked / no chain), or a TRACE of an unknown entry
+};
+
+// decide-kernel bins of a segment (Seg.pad); order[] is laid out bin by bin
+enum : uint32_t {
+    BIN_J16 = 0,           // one 1024-lane workgroup per segment (Zipf head)
+    BIN_J4 = 1,            // one 256-lane workgroup per segment
+    BIN_J1 = 2,            // one wavefront per segment
+    BIN_LANE = 3,          // one lane per segment, nr <= 4: bins 3..3+LANE_BINS-1 by descending log2(len)
+    LANE_BINS = 20,
+    BIN_LANE16 = BIN_LANE + LANE_BINS,  // one lane per segment, nr > 4 (rule state in scratch)
+    N_BINS = BIN_LANE16 + LANE_BINS
+};
 
 } // namespace sg

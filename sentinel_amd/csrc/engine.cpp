@@ -20,23 +20,34 @@
 #include "dev_types.h"
 
 namespace sg {
+// kernels.hip
 hipError_t launch_radix_hist(const sg_event*, const uint32_t*, uint64_t, int, uint32_t*, uint32_t, uint32_t*, uint32_t,
                              hipStream_t);
 hipError_t launch_radix_scatter(const sg_event*, const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
                                 uint32_t, uint32_t*, uint32_t*, hipStream_t);
 uint32_t radix_tile();
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
-hipError_t launch_seg(const uint32_t*, uint64_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, Seg*, uint32_t*,
-                      const Prog*, hipStream_t);
-hipError_t launch_seg_order(const Seg*, uint32_t, uint32_t*, uint32_t*, hipStream_t);
-hipError_t launch_chain_candidates(const sg_event*, const uint32_t*, const Seg*, uint32_t, const NodeInfo*, uint32_t*,
-                                   uint64_t*, hipStream_t);
-hipError_t launch_decide(const sg_event*, const uint32_t*, const Seg*, const uint32_t*, uint32_t, uint32_t, uint64_t,
-                         uint64_t, const DevState&, const DevCfg&, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                            sg_metric_node*, uint64_t, hipStream_t);
 hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, uint32_t nres, hipStream_t st);
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st);
+// decide.hip
+hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
+                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                      uint32_t* part, uint32_t* nseg);
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
+                          uint32_t j4_max, uint32_t force_lane, uint32_t* bin_cnt, hipStream_t st);
+hipError_t launch_seg_order(const Seg* segs, uint32_t m, uint32_t* cursor, uint32_t* order, hipStream_t st);
+hipError_t launch_prep(const sg_event* ev, const uint32_t* vals, uint64_t n, uint32_t* pos_of, uint64_t gbase,
+                       const uint8_t* ring, uint64_t ring_mask, int32_t max_rt, SEv* recs, uint32_t* bflags,
+                       hipStream_t st);
+hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
+                       uint64_t ring_mask, uint32_t* out, hipStream_t st);
+hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
+                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, hipStream_t st);
+hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                             const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
+                             uint32_t* dec, uint32_t* bflags, hipStream_t st);
 } // namespace sg
 
 using namespace sg;
@@ -404,13 +415,21 @@ struct sg_engine {
     uint32_t* d_out = nullptr;
     uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
     uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
+    uint32_t *d_posof = nullptr, *d_dec = nullptr;
+    SEv* d_recs = nullptr;
     Seg* d_segs = nullptr;
-    uint32_t* d_small = nullptr;  // [0] bflags [1] nseg [2] ncand [3..66] lbucket[2][32] [67..130] lcursor [131] total
+    // d_small: [0] bflags [1] nseg [2] ncand [3] snapshot total [8..8+N_BINS) bin counts
+    //          [64..64+N_BINS) bin cursors
+    uint32_t* d_small = nullptr;
     uint64_t* d_cand = nullptr;
-    unsigned long long* d_dbg = nullptr;
     uint32_t dbg_flags = 0;
+    unsigned long long* d_dbg = nullptr;  // SG_DEBUG=1: [0..63] counters of the J16 bin
     uint64_t cap_hist = 0;
     uint64_t gbase = 0;
+    // decide bins run concurrently: one stream per cooperative bin, the lane bins on the main stream
+    hipStream_t bin_stream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+    uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     // snapshot scratch
     uint32_t *d_snap_cnt = nullptr, *d_snap_off = nullptr;
     sg_metric_node* d_snap_out = nullptr;
@@ -424,7 +443,7 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     uint64_t c = std::max<uint64_t>(n, 1u << 20);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand);
+    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs);
     uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
     e->cap_hist = nblocks * 256;
     HIPCHK(hipMalloc(&e->d_ev, c * sizeof(sg_event)));
@@ -440,6 +459,9 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_order, c * 4));
     HIPCHK(hipMalloc(&e->d_segs, c * sizeof(Seg)));
     HIPCHK(hipMalloc(&e->d_cand, c * 8));
+    HIPCHK(hipMalloc(&e->d_posof, c * 4));
+    HIPCHK(hipMalloc(&e->d_dec, c * 4));
+    HIPCHK(hipMalloc(&e->d_recs, c * sizeof(SEv)));
     e->cap_n = c;
     return SG_OK;
 }
@@ -557,12 +579,29 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
             d.count = g.r.count;
             d.time_window = g.r.time_window;
             if (g.r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) p.pflags |= PF_EXC_COUNT;
+            if (g.r.grade == SG_DEGRADE_GRADE_RT) p.pflags |= PF_RT;
             rules.push_back(d);
             rst.push_back(RState{0, 0, 0, 0});
             p.n_degrade++;
         }
         if ((int)p.n_param + p.n_flow + p.n_degrade > 16)
             return fail(SG_ENOTSUP, "more than 16 rules on one resource: " + e->names[r]);
+        {  // limits of the cooperative decide kernels (decide.hip JMAX_*); else one lane decides it
+            int n_rl = 0;
+            for (int i = 0; i < p.n_flow; ++i) {
+                uint8_t b = rules[p.rule_off + p.n_param + i].behavior;
+                if (b == SG_CONTROL_BEHAVIOR_RATE_LIMITER || b == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) ++n_rl;
+            }
+            if (n_rl) p.pflags |= PF_RL;
+            if (p.n_param || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2) p.pflags |= PF_SERIAL;
+            bool all_default_qps = true;
+            for (int i = 0; i < p.n_flow; ++i) {
+                const DRule& d = rules[p.rule_off + p.n_param + i];
+                if (d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || d.grade != SG_FLOW_GRADE_QPS) all_default_qps = false;
+            }
+            if (all_default_qps) p.pflags |= PF_FROZEN;
+            if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
+        }
         // carry controller / breaker state of kinds that were not reloaded
         if (!old_rst.empty()) {
             const Prog& op = old_prog[r];
@@ -672,22 +711,33 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_ring, 0, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
         launch_init_state(e->d_sec, e->d_minb, e->d_info, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
+    for (auto& s : e->bin_stream)
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+    if (hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
+    for (auto& v : e->join)
+        if (hipEventCreateWithFlags(&v, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
     if (const char* d = std::getenv("SG_DEBUG")) {
         if (d[0] == '1' && hipMalloc(&e->d_dbg, 64 * 8) == hipSuccess) (void)hipMemset(e->d_dbg, 0, 64 * 8);
     }
     if (const char* f = std::getenv("SG_DEBUG_FLAGS")) e->dbg_flags = (uint32_t)std::strtoul(f, nullptr, 0);
+    // decide-bin thresholds (segment lengths); tuning knobs, the defaults are the measured best
+    if (const char* v = std::getenv("SG_LANE_MAX")) e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0);
+    if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
+    if (const char* v = std::getenv("SG_J4_MAX")) e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0);
     *out = e;
     return SG_OK;
 }
 
-// hidden diagnostics export (not part of the ABI): per-batch counters of the hottest segment
+// diagnostics export (not part of the ABI): SG_DEBUG=1 counters of the cooperative J16 bin,
+// accumulated over batches (see decide.hip k_jac)
 extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap) {
     if (!e || !e->d_dbg || !out) return 0;
     int k = cap < 64 ? cap : 64;
+    if (hipDeviceSynchronize() != hipSuccess) return 0;
     if (hipMemcpy(out, e->d_dbg, (size_t)k * 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return k;
 }
@@ -700,8 +750,12 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_dbg); dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out);
+    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs);
+    dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+    for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
+    if (e->fork) (void)hipEventDestroy(e->fork);
+    for (auto& s : e->bin_stream) if (s) (void)hipStreamDestroy(s);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return SG_OK;
@@ -946,7 +1000,7 @@ static bool is_device_ptr(const void* p) {
 int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
     if (!e || (n && (!ev || !out))) return fail(SG_EINVAL, "null argument");
     if (n == 0) return SG_OK;
-    if (n > e->cfg.max_batch_events || n >= (1ull << 32)) return fail(SG_EINVAL, "batch larger than max_batch_events");
+    if (n > e->cfg.max_batch_events || n >= (1ull << 31)) return fail(SG_EINVAL, "batch larger than max_batch_events");
     HIPCHK(hipSetDevice(e->device));
     int rc = ensure_batch(e, n);
     if (rc) return rc;
@@ -959,8 +1013,9 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         dev_ev = e->d_ev;
     }
     uint32_t* dev_out = host_out ? e->d_out : out;
+    const uint64_t ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
     HIPCHK(hipEventRecord(e->ev[0], st));
-    // ---- 1. group: LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
+    // ---- 1. group: stable LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
     uint32_t R = e->cfg.max_resources;
     int bits = 1;
     while (bits < 32 && (1ull << bits) < R) ++bits;
@@ -977,60 +1032,72 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         kout = (kin == e->d_k0) ? e->d_k1 : e->d_k0;
         vout = (vin == e->d_v0) ? e->d_v1 : e->d_v0;
     }
-    // ---- 2. segments
-    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_part, e->d_small + 1, e->d_segs, e->d_small + 3, e->d_prog, st));
-    uint32_t small[67];
+    // ---- 2. segments + 16-byte sorted records (references resolved against the status ring)
+    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, st, launch_scan, e->d_part, e->d_small + 1));
+    HIPCHK(launch_prep(dev_ev, vin, n, e->d_posof, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt,
+                       e->d_recs, e->d_small + 0, st));
+    uint32_t m = 0;
+    HIPCHK(hipMemcpyAsync(&m, e->d_small + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
+    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
+                          e->d_small + 8, st));
+    uint32_t small[8 + N_BINS];
     HIPCHK(hipMemcpyAsync(small, e->d_small, sizeof(small), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    uint32_t bflags = small[0], m = small[1];
+    uint32_t bflags = small[0];
     if (bflags & BF_BAD_RES) return fail(SG_EINVAL, "event res_id >= max_resources");
+    if (bflags & BF_BAD_REF)
+        return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
+    if (bflags & BF_TSPAN) return fail(SG_EINVAL, "a batch must span less than 2^31 ms");
+    if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
     if (bflags & BF_PRIORITIZED)
         return fail(SG_ENOTSUP, "prioritized entries (StatisticNode.tryOccupyNext) are not on the device path yet");
     if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
-    // [speculative segments | serial segments], each by descending length class -> cursors
-    uint32_t cur[64];
-    uint32_t acc = 0;
-    for (int c = 0; c < 2; ++c)
-        for (int b = 31; b >= 0; --b) { cur[c * 32 + b] = acc; acc += small[3 + c * 32 + b]; }
-    uint32_t m_spec = 0;
-    for (int b = 0; b < 32; ++b) m_spec += small[3 + b];
-    uint32_t m_serial = m - m_spec;
-    HIPCHK(hipMemcpyAsync(e->d_small + 67, cur, sizeof(cur), hipMemcpyHostToDevice, st));
-    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 67, e->d_order, st));
+    // bin-ordered dispatch list
+    uint32_t cursor[N_BINS], off[N_BINS + 1];
+    off[0] = 0;
+    for (int b = 0; b < N_BINS; ++b) { cursor[b] = off[b]; off[b + 1] = off[b] + small[8 + b]; }
+    HIPCHK(hipMemcpyAsync(e->d_small + 64, cursor, sizeof(cursor), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 64, e->d_order, st));
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
+    if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
+        const bool grant_all = e->cfg.max_slot_chain_size <= 0;
+        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_small + 2, e->d_cand, st));
+        if (!grant_all) {
+            uint32_t ncand = 0;
+            HIPCHK(hipMemcpyAsync(&ncand, e->d_small + 2, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (ncand) {
+                std::vector<uint64_t> cand(ncand);
+                HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
+                std::sort(cand.begin(), cand.end());  // by batch index of the first ENTRY
+                std::vector<uint64_t> upd(ncand);
+                for (uint32_t i = 0; i < ncand; ++i) {
+                    uint32_t res = (uint32_t)cand[i];
+                    bool grant = e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
+                    if (grant) e->n_chains++;
+                    upd[i] = ((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63);
+                }
+                HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
+                HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+        }
+    }
+    HIPCHK(hipEventRecord(e->ev[1], st));
+    // ---- 3. decide: cooperative bins on their own streams, lane bins on the main stream
     DevCfg dc;
+    std::memset(&dc, 0, sizeof(dc));
     dc.max_rt = e->cfg.statistic_max_rt;
     dc.occupy_timeout = e->cfg.occupy_timeout_ms;
     dc.max_chain = e->cfg.max_slot_chain_size;
     dc.switch_on = e->cfg.switch_on;
     dc.ptab_mask = (1ull << e->cfg.param_table_log2) - 1;
-    dc.ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
+    dc.ring_mask = ring_mask;
     dc.dbg_flags = e->dbg_flags;
-    dc.pad = 0;
-    if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
-        HIPCHK(launch_chain_candidates(dev_ev, vin, e->d_segs, m, e->d_info, e->d_small + 2, e->d_cand, st));
-        uint32_t ncand = 0;
-        HIPCHK(hipMemcpyAsync(&ncand, e->d_small + 2, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        if (ncand) {
-            std::vector<uint64_t> cand(ncand);
-            HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
-            std::sort(cand.begin(), cand.end()); // by batch index of the first ENTRY
-            std::vector<uint64_t> upd(ncand);
-            for (uint32_t i = 0; i < ncand; ++i) {
-                uint32_t res = (uint32_t)cand[i];
-                bool grant = e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
-                if (grant) e->n_chains++;
-                upd[i] = ((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63);
-            }
-            HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
-            HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
-            HIPCHK(hipStreamSynchronize(st));
-        }
-    }
-    HIPCHK(hipEventRecord(e->ev[1], st));
-    // ---- 3. decide
     DevState S;
+    std::memset(&S, 0, sizeof(S));
     S.sec = e->d_sec;
     S.minb = e->d_minb;
     S.info = e->d_info;
@@ -1040,10 +1107,29 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.hot = e->d_hot;
     S.ptab = e->d_ptab;
     S.ring = e->d_ring;
-    S.dbg = e->d_dbg;
-    HIPCHK(launch_decide(dev_ev, vin, e->d_segs, e->d_order, m_spec, m_serial, e->gbase, n, S, dc, dev_out,
-                         e->d_small + 0, st));
+    int64_t t0 = 0;
+    HIPCHK(hipMemcpy(&t0, &dev_ev[0].ts, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipEventRecord(e->fork, st));
+    const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
+    for (int k = 0; k < 3; ++k) {
+        const int b = coop[k];
+        if (!small[8 + b]) continue;
+        DevState Sb = S;
+        Sb.dbg = (k == 0 && e->d_dbg) ? e->d_dbg : nullptr;
+        HIPCHK(hipStreamWaitEvent(e->bin_stream[k], e->fork, 0));
+        HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], small[8 + b], Sb, dc, t0,
+                                 e->d_dec, e->d_small + 0, e->bin_stream[k]));
+        HIPCHK(hipEventRecord(e->join[k], e->bin_stream[k]));
+    }
+    HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
+                             off[BIN_LANE + LANE_BINS] - off[BIN_LANE], S, dc, t0, e->d_dec, e->d_small + 0, st));
+    HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
+                             off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_small + 0, st));
+    for (int k = 0; k < 3; ++k)
+        if (small[8 + coop[k]]) HIPCHK(hipStreamWaitEvent(st, e->join[k], 0));
     HIPCHK(hipEventRecord(e->ev[2], st));
+    // ---- 4. decisions back to submission order + status ring
+    HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
     if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
     e->gbase += n;
     return SG_OK;
@@ -1126,9 +1212,9 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
     }
     if (!e->d_part) { int rc = ensure_batch(e, 1); if (rc) return rc; }
     HIPCHK(launch_snapshot(e->d_minb, e->d_info, R, now_ms, e->cfg.statistic_max_rt, e->d_snap_cnt, e->d_snap_off,
-                           e->d_part, e->d_small + 131, e->d_snap_out, cap, e->stream));
+                           e->d_part, e->d_small + 3, e->d_snap_out, cap, e->stream));
     uint32_t total = 0;
-    HIPCHK(hipMemcpyAsync(&total, e->d_small + 131, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&total, e->d_small + 3, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     uint64_t k = std::min<uint64_t>(total, cap);
     if (k && out) HIPCHK(hipMemcpy(out, e->d_snap_out, k * sizeof(sg_metric_node), hipMemcpyDeviceToHost));

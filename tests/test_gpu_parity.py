@@ -62,6 +62,23 @@ def _sample(w, k=300, seed=0):
     return np.unique(np.concatenate([hot, rnd]))
 
 
+# decide-bin modes: the engine reads its bin thresholds at creation (engine.cpp sg_engine_create)
+BIN_MODES = {
+    "default": {},
+    # every eligible segment through the cooperative kernels, all three widths exercised
+    "coop": {"SG_LANE_MAX": "0", "SG_J1_MAX": "40", "SG_J4_MAX": "400"},
+    # every segment through the one-lane-per-segment kernel
+    "lane": {"SG_DEBUG_FLAGS": "2"},
+}
+
+
+@pytest.fixture(params=sorted(BIN_MODES))
+def bin_mode(request, monkeypatch):
+    for k, v in BIN_MODES[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
 def _run(config, batches=3, chain_cap=0, **kw):
     w = T.Workload(config, **kw)
     eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap, param_table_log2=21)
@@ -74,26 +91,26 @@ def _run(config, batches=3, chain_cap=0, **kw):
     return w, eng, orc, dg
 
 
-def test_c1_flowqpsdemo():
+def test_c1_flowqpsdemo(bin_mode):
     # FlowQpsDemo (sentinel-demo-basic .../flow/FlowQpsDemo.java:37-66): ~20 pass/s under QPS=20
     w, eng, orc, d = _run(1, batches=4)
     st = d[w.events["kind"] == A.EV_ENTRY] & 0xFF
     assert int((st == A.PASS).sum()) == 2000  # 20 pass/s for 100 s
 
 
-def test_c2_qps_default():
+def test_c2_qps_default(bin_mode):
     _run(2, batches=3, n_entries=400_000)
 
 
-def test_c3_mixed_controllers():
+def test_c3_mixed_controllers(bin_mode):
     _run(3, batches=3, n_entries=400_000, n_res=20_000)
 
 
-def test_c4_degrade():
+def test_c4_degrade(bin_mode):
     _run(4, batches=3, n_entries=400_000, n_res=50_000)
 
 
-def test_c5_param():
+def test_c5_param(bin_mode):
     _run(5, batches=3, n_entries=400_000, n_param_values=50_000)
 
 
@@ -102,7 +119,7 @@ def test_chain_cap_reference_default():
     _run(2, batches=2, chain_cap=6000, n_entries=300_000)
 
 
-def test_many_small_batches_and_single_events():
+def test_many_small_batches_and_single_events(bin_mode):
     w = T.Workload(4, n_entries=20_000, n_res=2_000)
     eng = _engine(max_resources=w.n_res, max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)

@@ -1,4 +1,7 @@
-"""Diagnostics: per-stage cycle split of the hottest segment in k_decide_spec (SG_DEBUG=1)."""
+"""Diagnostics: counters of the cooperative J16 bin (SG_DEBUG=1) on a C4 batch.
+
+usage: python tools/hotprobe.py [config] [n_entries] [batches]
+"""
 import ctypes as C
 import os
 import sys
@@ -12,24 +15,33 @@ from sentinel_amd import engine as E  # noqa: E402
 from sentinel_amd import tracegen as T  # noqa: E402
 
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-n_entries = int(sys.argv[2]) if len(sys.argv) > 2 else 8_000_000
-w = T.Workload(cfg, n_entries=n_entries)
+n_entries = int(sys.argv[2]) if len(sys.argv) > 2 else 16_400_000
+nb = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+t = time.time()
+w = T.Workload(cfg, n_entries=n_entries, n_res=1_000_000 if cfg == 4 else 0)
+print("generated %d events in %.1f s" % (w.n_events, time.time() - t), flush=True)
 eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=22, status_ring_log2=28,
                max_batch_events=1 << 25)
 w.install(eng)
 ev = w.events
-B = min(len(ev), 1 << 24)
-for i in range(2):
+B = min(len(ev) // nb, 1 << 25)
+L = E.lib()
+L.sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+prev = np.zeros(16, dtype=np.uint64)
+for i in range(nb):
+    print("submit batch", i, flush=True)
     t = time.time()
-    d = eng.submit(ev[i * B:(i + 1) * B])
+    eng.submit(ev[i * B:(i + 1) * B])
     tm = eng.timings()
     buf = (C.c_ulonglong * 16)()
-    E.lib().sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-    E.lib().sgx_debug_counters(eng.h, buf, 16)
-    v = list(buf)
-    names = ["len", "tiles", "rounds", "iters", "load", "ref", "roundsetup", "eval", "tail"]
-    print("batch", i, "wall %.1f ms" % ((time.time() - t) * 1e3), "group %.2f decide %.2f ms" % (tm[0], tm[1]))
-    print({k: v[j] for j, k in enumerate(names)})
-    tot = sum(v[4:9]) or 1
-    print({k: "%.1f%%" % (100.0 * v[4 + j] / tot) for j, k in enumerate(names[4:])},
-          "cycles/tile %.0f" % (tot / max(1, v[1])), "rounds/tile %.2f" % (v[2] / max(1, v[1])))
+    L.sgx_debug_counters(eng.h, buf, 16)
+    v = np.array(list(buf), dtype=np.uint64)
+    d = v - prev
+    prev = v
+    print("batch %d: %d events, wall %.1f ms, group %.2f ms, decide %.2f ms" % (i, B, (time.time() - t) * 1e3, tm[0], tm[1]))
+    print("  J16 bin: segs %d iterations %d rounds %d tiles %d mismatched-iterations %d" % (d[4], d[0], d[1], d[2], d[3]))
+    ph = v[8:14].astype(np.float64)
+    tot = ph.sum() or 1
+    print("  block0 (len %d) phase cycles:" % v[5], {k: "%.1f%%" % (100 * ph[j] / tot) for j, k in
+                                                     enumerate(["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait"])},
+          "total %.3g, per-iteration %.0f" % (tot, tot / max(1, d[0] / max(1, d[4]))))
