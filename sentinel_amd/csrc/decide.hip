@@ -387,8 +387,13 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
         atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
     uint64_t pm = 0;  // passed bits of the segment's first 64 positions
+    SEv rn[2];        // software prefetch, two events ahead
+    rn[0] = recs[sg.start];
+    if (sg.len > 1) rn[1] = recs[sg.start + 1];
     for (uint32_t j = 0; j < sg.len; ++j) {
-        const SEv r = recs[sg.start + j];
+        const SEv r = rn[0];
+        rn[0] = rn[1];
+        if (j + 2 < sg.len) rn[1] = recs[sg.start + j + 2];
         const int64_t t = t0 + r.dt;
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
         if (r.kind == SG_EV_ENTRY) {
@@ -466,6 +471,15 @@ __device__ __forceinline__ int64_t wscan_i64_max(int64_t x) {
 #define NEG_INF64 ((int64_t)0x8000000000000000LL)
 
 #define NO_LANE 0xFFFFFFFFu
+
+// Workgroup barrier that only drains LDS traffic.  __syncthreads() is a release/acquire fence over
+// global memory as well, i.e. it waits for every outstanding vector load -- including the next tile
+// prefetched into registers -- so each tile would pay a full HBM round trip.  All cross-wave data
+// of k_jac lives in LDS; the only cross-wave global data are decisions read back as old references,
+// and those are ordered by the full __syncthreads() every FULL_FENCE_TILES tiles plus an L1-bypassing
+// (agent-scope) load.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#define FULL_FENCE_TILES 8
 
 // u32 quantities scanned block-wide in one Jacobi iteration (counts <= 1024 are packed in halves)
 enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR /* trip counts, 2 per word */ };
@@ -633,17 +647,22 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     const bool has_rt = (pg.pflags & PF_RT) != 0;
     const bool frozen_prog = (pg.pflags & PF_FROZEN) != 0;
 
-    // diagnostics (SG_DEBUG=1): per-bin iteration counters, phase cycles of the bin's first segment
+    // diagnostics (SG_DEBUG=1): per-bin iteration counters; phase cycles of the bin's first segment
+    // only in builds with -DSG_KPROF (the timers cost registers the 1024-lane kernel does not have)
     const bool prof = S.dbg != nullptr;
+    uint32_t n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0;
+#ifdef SG_KPROF
     const bool prof0 = prof && blockIdx.x == 0 && tid == 0;
-    unsigned long long n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0;
-    unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define PROF_MARK(k)                                          \
     if (prof0) {                                              \
         unsigned long long _n = __builtin_amdgcn_s_memtime(); \
         tph[k] += _n - tmA;                                   \
         tmA = _n;                                             \
     }
+#else
+#define PROF_MARK(k)
+#endif
 
     // ---- per-lane tile state
     uint32_t tbase = 0;
@@ -654,12 +673,11 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     if (HW + tid < sg.len) nxt = recs[sg.start + HW + tid];
     bool valid = false, eff_win = false, eff_val = false;
     uint32_t winidx = 0, refrel = 0, kind = 0xFF, cnt = 0, rtv = 0;
-    int64_t t = 0, tb = 0;
+    int32_t dt = 0;  // event time relative to t0 (the absolute time is t0 + dt)
     auto decode = [&](const SEv& r, uint32_t pos) {
         valid = pos < sg.len;
         kind = valid ? r.kind : 0xFFu;
-        t = t0 + (valid ? r.dt : 0);
-        tb = t / 500;
+        dt = valid ? r.dt : 0;
         cnt = r.cnt;
         rtv = r.rt;
         eff_win = false;
@@ -670,22 +688,27 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             else if (r.code == RC_BATCH) {
                 refrel = r.x - sg.start;
                 if (refrel + WIN >= tbase + HW) { eff_win = true; winidx = refrel & (WIN - 1); }
-                else eff_val = st_passed(dec[r.x] & 0xFF);  // decided >= WIN-HW positions ago
+                else  // decided >= WIN-HW positions ago, i.e. before >= 1 full fence
+                    eff_val = st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
             }
         }
     };
+    static_assert(WIN - HW >= (FULL_FENCE_TILES + 1) * HW, "old references must be older than one full fence");
     auto advance = [&]() {  // next tile (uniform)
         tbase += HW;
         cur = nxt;
+        // decode first: a (rare) old-reference load must not queue behind the prefetch below,
+        // vmcnt retires in order
+        decode(cur, tbase + tid);
         nxt.kind = 0xFF;
         if (tbase + HW + tid < sg.len) nxt = recs[sg.start + tbase + HW + tid];
-        decode(cur, tbase + tid);
         ++n_tile;
+        if ((tbase / HW) % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
     };
     decode(cur, tid);
     uint32_t g = (uint32_t)nr;  // outcome guess: index of the blocking stage, nr = pass
     if (valid) win[tid & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
-    if (tid == 0) sh.tnext = t;
+    if (tid == 0) sh.tnext = t0 + dt;
     __syncthreads();
     uint32_t mb = 0;  // mism double-buffer index
 
@@ -697,9 +720,9 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             advance();
             g = sh.last_out;
             if (valid) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
-            __syncthreads();  // everyone has read sh.last_out / sh.c0
-            if (tid == 0) { sh.c0 = 0; sh.tnext = t; }
-            __syncthreads();
+            lds_barrier();  // everyone has read sh.last_out / sh.c0
+            if (tid == 0) { sh.c0 = 0; sh.tnext = t0 + dt; }
+            lds_barrier();
             c0 = 0;
         }
         ++n_it;
@@ -708,15 +731,20 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             const int64_t tn = sh.tnext;
             const bool need = !sh.round_open || (tn / 500) != sh.bkt0 || tn >= sh.next_reset;
             if (need) {
+                PROF_MARK(0)
+                lds_barrier();  // every wave has read the round state before the leader rewrites it
                 if (tid == 0) {
                     round_fold(sh, C, nf);
                     round_setup(sh, C, nf, nd, tn);
                 }
-                __syncthreads();
+                lds_barrier();
                 ++n_round;
+                PROF_MARK(6)
             }
         }
-        const int64_t bkt0 = sh.bkt0, next_reset = sh.next_reset;
+        // the round's events: relative times in [dlo, dhi) (its 500 ms bucket, before the next reset)
+        const int64_t dlo = sh.bkt0 * 500 - t0;
+        const int64_t dhi = (sh.next_reset - t0 < dlo + 500) ? sh.next_reset - t0 : dlo + 500;
 
         // ================= frozen stretch =================
         // All flow stages are QPS DefaultControllers and either one of them is already saturated
@@ -732,52 +760,105 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             for (int s = 0; s < MF; ++s)
                 if (s < nf) sat |= (double)j_iadd(pint, 1) > sh.rules[s].count;
             if (sat || cutk0) {
-                const uint32_t fpos0 = tbase + c0;  // stretch start (segment position)
-                uint32_t aB = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aMin = NO_LANE, aTH = 0;
-                for (;;) {
-                    const uint32_t ct = sg.len - tbase < HW ? sg.len - tbase : HW;
-                    const bool inr = valid && tid >= c0 && tb == bkt0 && t < next_reset;
-                    uint32_t of = (uint32_t)nr;
-                    bool ok = true;
-                    if (inr && kind == SG_EV_ENTRY) {
-                        of = NO_LANE;
+                constexpr uint32_t EPL = 4, ST = EPL * HW;  // events per lane, positions per super-tile
+                static_assert(WIN - ST >= (FULL_FENCE_TILES + 1) * (ST + HW), "old references must precede a full fence");
+                __syncthreads();  // full fence at every stretch start (see lds_barrier)
+                const uint32_t fpos0 = tbase + c0;        // stretch start (segment position)
+                double fcount[MF];                        // flow thresholds and verdict words, hoisted
+                uint32_t fdec[MF];
 #pragma unroll
-                        for (int s = 0; s < MF; ++s)
-                            if (s < nf && of == NO_LANE && (double)j_iadd(pint, (int)cnt) > sh.rules[s].count)
-                                of = (uint32_t)s;
-                        if (of == NO_LANE && cutk0) of = (uint32_t)nf;
-                        ok = of != NO_LANE;
+                for (int s = 0; s < MF; ++s) {
+                    fcount[s] = s < nf ? sh.rules[s].count : 0.0;
+                    fdec[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, sh.rules[s].slot, 0) : 0u;
+                }
+                const uint32_t cdec = nd > 0 ? mk_dec(ST_BLOCK_DEGRADE, sh.rules[nf].slot, 0) : 0u;
+                const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
+                uint32_t aB = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aMin = NO_LANE, aTH = 0;
+                uint4 rr[EPL], rn[EPL];
+                uint32_t sb = fpos0, fend, nst = 0;
+                // loads are unconditional (clamped index): predicated loads would make the compiler's
+                // waitcnt analysis drain the prefetch (vmcnt(0)) before the current tile is touched
+                const uint32_t qmax = sg.len - 1;
+#pragma unroll
+                for (int k = 0; k < (int)EPL; ++k) {
+                    const uint32_t q = sb + k * HW + tid;
+                    rr[k] = r4[q < qmax ? q : qmax];
+                }
+                for (;;) {
+#pragma unroll
+                    for (int k = 0; k < (int)EPL; ++k) {  // prefetch the next super-tile
+                        const uint32_t q = sb + ST + k * HW + tid;
+                        rn[k] = r4[q < qmax ? q : qmax];
                     }
-                    const uint64_t stop = __ballot(valid && tid >= c0 && (!inr || !ok));
-                    if (lane == 0) sh.mism[mb][wv] = stop ? wv * 64 + (uint32_t)(__ffsll((long long)stop) - 1) : NO_LANE;
-                    __syncthreads();
+                    // first position of this lane that cannot be decided frozen
+                    uint32_t mystop = NO_LANE;
+                    uint32_t fdv[EPL];
+#pragma unroll
+                    for (int k = 0; k < (int)EPL; ++k) {
+                        const uint32_t q = sb + k * HW + tid;
+                        const int32_t edt = (int32_t)rr[k].x;
+                        const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu;
+                        const bool in = q < sg.len && edt >= dlo && edt < dhi;
+                        const double curv = (double)j_iadd(pint, (int)ec);
+                        uint32_t fd = 0;
+#pragma unroll
+                        for (int s = MF - 1; s >= 0; --s)
+                            if (s < nf && curv > fcount[s]) fd = fdec[s];
+                        if (fd == 0 && cutk0) fd = cdec;
+                        fdv[k] = fd;
+                        const bool stop = q < sg.len && (!in || (ek == SG_EV_ENTRY && fd == 0));
+                        if (stop && q < mystop) mystop = q;
+                    }
+                    uint32_t wmin = mystop;
+                    WAVE_SCAN(wmin, NO_LANE, op_min);
+                    if (lane == 63) sh.mism[mb][wv] = wmin;
+                    lds_barrier();
                     uint32_t f = NO_LANE;
                     for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
                     mb ^= 1;
-                    const uint32_t fend = f != NO_LANE ? f : ct;
                     ++n_frz;
-                    if (inr && tid < fend) {
-                        const uint32_t pos = tbase + tid;
-                        uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
-                        if (kind == SG_EV_ENTRY) {
-                            d = out_to_dec(sh.rules, nr, nf, of, 0);
-                            win[pos & (WIN - 1)] = 0;
-                            aB += cnt;
-                            aTI += 1;
-                        } else {
-                            bool eff = eff_win ? (refrel >= fpos0 ? false : win[winidx] != 0) : eff_val;
-                            if (eff && kind == SG_EV_EXIT) {
-                                aS += cnt; aRT += rtv; aTH -= 1; aMin = op_min(aMin, rtv); aTI += 1;
-                            } else if (eff && kind == SG_EV_TRACE && cnt > 0) {
-                                aE += cnt; aTI += 1;
+                    // commit every position before the stop.  The decision stores are unconditional
+                    // (masked-off lanes write a per-lane sink word) so vmcnt stays countable.
+#pragma unroll
+                    for (int k = 0; k < (int)EPL; ++k) {
+                        const uint32_t q = sb + k * HW + tid;
+                        const bool cm = q < f && q < sg.len;
+                        uint32_t d = 0;
+                        if (cm) {
+                            const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
+                            const uint32_t code = (rr[k].w >> 16) & 0xFFu;
+                            d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                            if (ek == SG_EV_ENTRY) {
+                                d = fdv[k];
+                                win[q & (WIN - 1)] = 0;
+                                aB += ec;
+                                aTI += 1;
+                            } else {
+                                bool eff = code == RC_NONE || code == RC_PASSED;
+                                if (code == RC_BATCH) {
+                                    const uint32_t rel = rr[k].y - sg.start;
+                                    if (rel >= fpos0) eff = false;  // an ENTRY of this stretch: blocked
+                                    else if (rel + WIN >= sb + ST) eff = win[rel & (WIN - 1)] != 0;
+                                    else eff = st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
+                                                                           __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                                }
+                                if (eff && ek == SG_EV_EXIT) {
+                                    aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1;
+                                } else if (eff && ek == SG_EV_TRACE && ec > 0) {
+                                    aE += ec; aTI += 1;
+                                }
                             }
                         }
-                        dec[sg.start + pos] = d;
+                        *(cm ? &dec[sg.start + q] : &S.sink[tid]) = d;
                     }
-                    if (f != NO_LANE || tbase + HW >= sg.len) { c0 = fend; break; }
-                    advance();  // the whole tile was frozen: the stretch goes on
-                    c0 = 0;
+                    if (f != NO_LANE) { fend = f; break; }
+                    sb += ST;
+                    if (sb >= sg.len) { fend = sg.len; break; }
+#pragma unroll
+                    for (int k = 0; k < (int)EPL; ++k) rr[k] = rn[k];
+                    if (++nst % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
                 }
+                PROF_MARK(7)
                 // stretch end: reduce the lane accumulators into the round's committed totals
                 WAVE_SCAN(aB, 0u, op_add);
                 WAVE_SCAN(aS, 0u, op_add);
@@ -790,11 +871,17 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     sh.part[wv][0] = aB; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
                     sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin;
                 }
-                // guesses of the lanes after the stretch: the frozen verdict
+                // re-enter the tile machinery at the stop position; guesses = the frozen verdict
+                tbase = fend / HW * HW;
+                c0 = fend - tbase;
+                cur.kind = 0xFF;
+                nxt.kind = 0xFF;
+                if (tbase + tid < sg.len) cur = recs[sg.start + tbase + tid];
+                if (tbase + HW + tid < sg.len) nxt = recs[sg.start + tbase + HW + tid];
+                decode(cur, tbase + tid);
                 g = (cutk0 && !sat) ? (uint32_t)nf : 0u;
-                const uint32_t ct = sg.len - tbase < HW ? sg.len - tbase : HW;
                 if (valid && tid >= c0) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
-                if (c0 < ct && tid == c0) sh.tnext = t;
+                if (valid && tid == c0) sh.tnext = t0 + dt;
                 __syncthreads();
                 if (tid == 0) {
                     for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
@@ -805,14 +892,16 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     sh.last_out = g;
                     sh.c0 = c0;
                 }
-                __syncthreads();
+                lds_barrier();
+                PROF_MARK(8)
                 continue;
             }
         }
 
         // ================= Jacobi iteration =================
-        const bool inr = valid && tid >= c0 && tb == bkt0 && t < next_reset;
+        const bool inr = valid && tid >= c0 && dt >= dlo && dt < dhi;
         const bool ent = inr && kind == SG_EV_ENTRY;
+        const int64_t t = t0 + dt;
         const bool eff = eff_win ? (win[winidx] != 0) : eff_val;
         const bool xe = inr && kind == SG_EV_EXIT && eff;
         const bool te = inr && kind == SG_EV_TRACE && eff && cnt > 0;
@@ -874,7 +963,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             }
         }
         PROF_MARK(1)
-        __syncthreads();  // B2
+        lds_barrier();  // B2
         PROF_MARK(2)
         uint32_t inr_total = 0;
         {
@@ -942,7 +1031,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     if (lane == 63) sh.pseg[wv][k] = v;
                 }
             }
-            __syncthreads();  // B3
+            lds_barrier();  // B3
 #pragma unroll
             for (int k = 0; k < MD; ++k) {
                 if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
@@ -1020,7 +1109,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             if (lane == 0) sh.mism[mb][wv] = mm ? wv * 64 + (uint32_t)(__ffsll((long long)mm) - 1) : NO_LANE;
         }
         PROF_MARK(3)
-        __syncthreads();  // B4
+        lds_barrier();  // B4
         uint32_t f = NO_LANE;
         for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
         mb ^= 1;
@@ -1105,23 +1194,24 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         }
         {
             const uint32_t cnt_now = sg.len - tbase < HW ? sg.len - tbase : HW;
-            if (tid == cend && cend < cnt_now) sh.tnext = t;
+            if (tid == cend && cend < cnt_now) sh.tnext = t0 + dt;
         }
         PROF_MARK(4)
-        __syncthreads();  // B1
+        lds_barrier();  // B1
         PROF_MARK(5)
     }
     if (prof && tid == 0) {
-        atomicAdd(&S.dbg[0], n_it);
-        atomicAdd(&S.dbg[1], n_round);
-        atomicAdd(&S.dbg[2], n_tile);
-        atomicAdd(&S.dbg[3], n_mm);
+        atomicAdd(&S.dbg[0], (unsigned long long)n_it);
+        atomicAdd(&S.dbg[1], (unsigned long long)n_round);
+        atomicAdd(&S.dbg[2], (unsigned long long)n_tile);
+        atomicAdd(&S.dbg[3], (unsigned long long)n_mm);
         atomicAdd(&S.dbg[4], 1ull);
-        atomicAdd(&S.dbg[6], n_frz);
-        if (blockIdx.x == 0) {
-            S.dbg[5] = sg.len;
-            for (int k = 0; k < 6; ++k) S.dbg[8 + k] = tph[k];
-        }
+        atomicAdd(&S.dbg[6], (unsigned long long)n_frz);
+        if (blockIdx.x == 0) S.dbg[5] = sg.len;
+#ifdef SG_KPROF
+        if (blockIdx.x == 0)
+            for (int k = 0; k < 10; ++k) S.dbg[8 + k] = tph[k];
+#endif
     }
 #undef PROF_MARK
     // end of segment: fold the last round, write the node and rule states back
@@ -1189,8 +1279,9 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
                              uint32_t* dec, uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
     switch (bin) {
-    case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter
-        hipLaunchKernelGGL((k_jac<16, 15, 2, 2, false>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
+    case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
+                   // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS
+        hipLaunchKernelGGL((k_jac<16, 17, 2, 2, false>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
                            dec, bflags);
         break;
     case BIN_J4:

@@ -146,6 +146,7 @@ struct DevState {
     PSlot* ptab;
     uint8_t* ring;
     unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
+    uint32_t* sink;           // >= 1024 scratch words: target of masked-off unconditional stores
 };
 
 enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,

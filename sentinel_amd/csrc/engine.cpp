@@ -421,6 +421,7 @@ struct sg_engine {
     // d_small: [0] bflags [1] nseg [2] ncand [3] snapshot total [8..8+N_BINS) bin counts
     //          [64..64+N_BINS) bin cursors
     uint32_t* d_small = nullptr;
+    uint32_t* d_sink = nullptr;  // 1024 words, DevState.sink
     uint64_t* d_cand = nullptr;
     uint32_t dbg_flags = 0;
     unsigned long long* d_dbg = nullptr;  // SG_DEBUG=1: [0..63] counters of the J16 bin
@@ -707,7 +708,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (hipMalloc(&e->d_sec, R * 2 * sizeof(Bkt)) != hipSuccess || hipMalloc(&e->d_minb, R * 60 * sizeof(Bkt)) != hipSuccess ||
         hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
         hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
-        hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess)
+        hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
+        hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
@@ -747,7 +749,7 @@ int sg_engine_destroy(sg_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
-    dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small);
+    dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
     dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs);
@@ -1107,6 +1109,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.hot = e->d_hot;
     S.ptab = e->d_ptab;
     S.ring = e->d_ring;
+    S.sink = e->d_sink;
     int64_t t0 = 0;
     HIPCHK(hipMemcpy(&t0, &dev_ev[0].ts, 8, hipMemcpyDeviceToHost));
     HIPCHK(hipEventRecord(e->fork, st));

@@ -27,21 +27,21 @@ ev = w.events
 B = min(len(ev) // nb, 1 << 25)
 L = E.lib()
 L.sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-prev = np.zeros(16, dtype=np.uint64)
+prev = np.zeros(24, dtype=np.uint64)
 for i in range(nb):
     print("submit batch", i, flush=True)
     t = time.time()
     eng.submit(ev[i * B:(i + 1) * B])
     tm = eng.timings()
-    buf = (C.c_ulonglong * 16)()
-    L.sgx_debug_counters(eng.h, buf, 16)
+    buf = (C.c_ulonglong * 24)()
+    L.sgx_debug_counters(eng.h, buf, 24)
     v = np.array(list(buf), dtype=np.uint64)
     d = v - prev
     prev = v
     print("batch %d: %d events, wall %.1f ms, group %.2f ms, decide %.2f ms" % (i, B, (time.time() - t) * 1e3, tm[0], tm[1]))
     print("  J16 bin: segs %d iterations %d rounds %d tiles %d mismatched-iterations %d" % (d[4], d[0], d[1], d[2], d[3]))
-    ph = v[8:14].astype(np.float64)
+    ph = v[8:18].astype(np.float64)
     tot = ph.sum() or 1
-    print("  block0 (len %d) phase cycles:" % v[5], {k: "%.1f%%" % (100 * ph[j] / tot) for j, k in
-                                                     enumerate(["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait"])},
-          "total %.3g, per-iteration %.0f" % (tot, tot / max(1, d[0] / max(1, d[4]))))
+    names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
+    print("  block0 (len %d) phase cycles:" % v[5], {k: "%.0f" % ph[j] for j, k in enumerate(names)})
+    print("  frozen tiles (all J16 segments):", d[6])

@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py: kernel-trace stats, then FETCH_SIZE and WRITE_SIZE in separate
+# --pmc passes (MI355X_MICROARCH.md: they cannot share a pass).  Every GPU step has its own limit.
+set -e
+export TMPDIR=/tmp
+TAG=${1:-prof}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
+echo profile done
