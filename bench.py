@@ -99,16 +99,14 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    decide_ms, group_ms = [], []
+    stage_ms = []  # per timed step: [group, decide, post, total] device ms (HIP events, engine stream)
     for i in range(warmup):
         eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value)
     barrier()
     t_start = time.perf_counter()
     for i in range(warmup, warmup + steps):
         eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value)
-        tm = eng.timings()
-        group_ms.append(tm[0])
-        decide_ms.append(tm[1])
+        stage_ms.append(eng.timings())
     barrier()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
@@ -122,12 +120,24 @@ def main():
     else:
         entries_total = float(sum(entries_per_batch[warmup:warmup + steps]))
 
-    # roofline of the dominant kernel (k_decide): algorithmic bytes per launch / its mean duration
+    # Roofline of the dominant stage: the decide kernels (k_jac<16>/<4>/<1> and k_lane, forked over
+    # four streams and joined; HIP events bracket the fork and the join on the engine stream).
+    # Algorithmic bytes per launch: every event record read once (24 B), every
+    # decision word written once (4 B), every resource touched by the batch reads (352 B) and writes
+    # (256 B) its state once.  Sorting/grouping/re-reads are implementation cost, not counted.
     sel = range(warmup, warmup + steps)
     alg_bytes = np.mean([args.batch_events * (EVENT_B + DECISION_B) + res_per_batch[i] * STATE_RW_B for i in sel])
-    dec_s = np.mean(decide_ms) / 1e3
-    achieved = alg_bytes / dec_s / 1e9
-
+    sm = np.array(stage_ms)
+    decide_ms = float(sm[:, 1].mean())
+    achieved = alg_bytes / (decide_ms / 1e3) / 1e9
+    pipe_ms = elapsed / steps * 1e3
+    pipe_achieved = alg_bytes / (pipe_ms / 1e3) / 1e9
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command (tools/profile.sh)
+        with open(pmc) as f:
+            pj = json.load(f)
+        traffic, traffic_src = pj.get("decide_stage_traffic_bytes"), "profiles/pmc_latest.json"
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(w, args.cpu_sample_events)
@@ -152,9 +162,12 @@ def main():
                        "resources_touched_per_step": float(np.mean([res_per_batch[i] for i in sel])),
                        "parallelism": "resource-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_decide", "kernel_ms": float(np.mean(decide_ms)),
-                         "group_ms": float(np.mean(group_ms)), "alg_bytes_per_launch": float(alg_bytes)},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "decide stage: k_jac<16,17,2,2> | k_jac<4,..> | k_jac<1,..> | k_lane<4> (concurrent streams)",
+                         "kernel_ms": decide_ms, "alg_bytes_per_launch": float(alg_bytes)},
+            "pipeline": {"achieved_GBs": pipe_achieved, "frac": pipe_achieved / HBM_PEAK_GBS,
+                         "group_ms": float(sm[:, 0].mean()), "decide_ms": decide_ms, "post_ms": float(sm[:, 2].mean()),
+                         "device_ms": float(sm[:, 3].mean()), "wall_ms": pipe_ms},
             "cpu_baseline": cpu,
             "gen_s": gen_s,
         }

@@ -314,8 +314,10 @@ int sg_read_node(sg_engine* e, uint32_t res_id, int64_t now_ms, sg_node_state* o
 /* Last error message of the calling thread ("" if none). */
 const char* sg_last_error(void);
 
-/* Timing of the most recent sg_submit's kernels (HIP events), in ms: [0] group,
- * [1] decide, [2] total device time; returns the number of values written. */
+/* Timing of the most recent sg_submit's device stages (HIP events on the engine
+ * stream), in ms: [0] group (sort, segments, records, chain grants), [1] decide
+ * (every decide kernel, forked over streams and joined), [2] post (decisions back
+ * to submission order), [3] their sum; returns the number of values written. */
 int sg_last_timings(sg_engine* e, double* ms, int cap);
 
 #ifdef __cplusplus

@@ -377,7 +377,7 @@ struct sg_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    double last_ms[3] = {0, 0, 0};
+    double last_ms[4] = {0, 0, 0, 0};
 
     // resources
     std::unordered_map<std::string, uint32_t> ids;
@@ -1133,6 +1133,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(hipEventRecord(e->ev[2], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
+    HIPCHK(hipEventRecord(e->ev[3], st));
     if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
     e->gbase += n;
     return SG_OK;
@@ -1141,10 +1142,11 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
 int sg_sync(sg_engine* e) {
     if (!e) return fail(SG_EINVAL, "null engine");
     HIPCHK(hipStreamSynchronize(e->stream));
-    float a = 0, b = 0;
+    float a = 0, b = 0, c = 0;
     if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->last_ms[0] = a;
     if (hipEventElapsedTime(&b, e->ev[1], e->ev[2]) == hipSuccess) e->last_ms[1] = b;
-    e->last_ms[2] = e->last_ms[0] + e->last_ms[1];
+    if (hipEventElapsedTime(&c, e->ev[2], e->ev[3]) == hipSuccess) e->last_ms[2] = c;
+    e->last_ms[3] = e->last_ms[0] + e->last_ms[1] + e->last_ms[2];
     (void)hipGetLastError();
     uint32_t bflags = 0;
     HIPCHK(hipMemcpy(&bflags, e->d_small, 4, hipMemcpyDeviceToHost));
@@ -1164,7 +1166,7 @@ int sg_submit(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
 int sg_last_timings(sg_engine* e, double* ms, int cap) {
     if (!e || !ms) return 0;
     int k = 0;
-    for (; k < cap && k < 3; ++k) ms[k] = e->last_ms[k];
+    for (; k < cap && k < 4; ++k) ms[k] = e->last_ms[k];
     return k;
 }
 

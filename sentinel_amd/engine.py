@@ -159,8 +159,9 @@ class Engine:
         _check(lib().sg_sync(self.h))
 
     def timings(self):
-        ms = (C.c_double * 3)()
-        k = lib().sg_last_timings(self.h, ms, 3)
+        """Device time of the last submit in ms: [group, decide, post, total] (sg_last_timings)."""
+        ms = (C.c_double * 4)()
+        k = lib().sg_last_timings(self.h, ms, 4)
         return list(ms[:k])
 
     def read_node(self, res: int, now: int = 0) -> dict:
