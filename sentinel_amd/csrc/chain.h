@@ -132,7 +132,11 @@ __device__ __forceinline__ void min_flush(Node& N, Bkt* minb) {
 // (cache flushed) and slot(T) must not have been reset yet, so the seconds that fall out of the
 // window are still readable.
 __device__ __forceinline__ void exc_advance(Node& N, const Bkt* minb, int64_t T) {
-    if (N.exc_sum_sec < 0 || T - N.exc_sum_sec >= 60000) {
+    if (N.exc_sum_sec >= 0 && T - N.exc_sum_sec >= 60000) {
+        // every bucket was written at or before exc_sum_sec (the sum is advanced on every minute
+        // write while the rule exists), so none is valid at T: nothing to read
+        N.exc_sum = 0;
+    } else if (N.exc_sum_sec < 0) {
         int64_t s = 0;
         for (int k = 0; k < 60; ++k) {
             Bkt b = minb[k];

@@ -1,9 +1,10 @@
 // decide.hip -- per-batch decision kernels of the MI355X Sentinel engine.
 //
 // Pipeline position (engine.cpp sg_submit_async):
-//   sort (kernels.hip) -> k_seg_* (segments + bins) -> k_posof/k_prep (16-byte sorted records,
-//   EXIT/TRACE references resolved) -> k_chain -> decide kernels by bin -> k_post (scatter the
-//   decisions back to submission order and into the status ring).
+//   record build + sort (kernels.hip k_rs_first, k_radix_*) -> k_seg_* (segments + bins) ->
+//   k_gather (16-byte sorted records, same-batch EXIT/TRACE references mapped to sorted positions)
+//   -> k_chain -> decide kernels by bin -> k_post (decisions back to submission order and into
+//   the status ring).
 //
 // A segment is one resource's events of the batch, in event order.  Every resource's slot chain
 // is a sequential state machine, so a segment is decided by exactly one owner:
@@ -41,24 +42,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
-// wave-aggregated atomicAdd of 1 per active lane into ctr[bin]; returns the lane's slot.
-// Must be called by the whole (converged) wavefront.
-__device__ __forceinline__ uint32_t agg_slot(uint32_t* ctr, uint32_t bin, bool active) {
-    uint32_t res = 0;
-    uint64_t todo = __ballot(active);
-    while (todo) {
-        int leader = __ffsll((long long)todo) - 1;
-        uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bin, leader);
-        uint64_t peers = __ballot(active && bin == lb);
-        uint32_t base = 0;
-        if ((int)lane_id() == leader) base = atomicAdd(&ctr[lb], (uint32_t)__popcll(peers));
-        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-        if (active && bin == lb) res = base + (uint32_t)__popcll(peers & lanemask_lt());
-        todo &= ~peers;
-    }
-    return res;
-}
-
 // =================================================================================
 // segments: starts, lengths, bins, bin-ordered dispatch list
 // =================================================================================
@@ -77,103 +60,74 @@ __global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const
     s.bin = 0;
     segs[pos[i]] = s;
 }
-// lengths + bins + per-bin counts.  Bins (dev_types.h BIN_*): cooperative kernels for long
-// segments of resources inside their limits, one lane per segment for everything else.
-__global__ void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n, const Prog* __restrict__ prog,
-                          uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane,
-                          uint32_t* __restrict__ bin_cnt) {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    bool act = s < m;
-    uint32_t bin = 0;
-    if (act) {
+// lengths + bins.  Bins (dev_types.h BIN_*): cooperative kernels for long segments of resources
+// inside their limits, one lane per segment for everything else.  Per-block bin counts go to
+// blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
+// in Seg.bin's upper bits until k_seg_order places the segment.
+__global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n,
+                                                 const Prog* __restrict__ prog, uint32_t lane_max, uint32_t j1_max,
+                                                 uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
+                                                 uint32_t nblk) {
+    __shared__ uint32_t cnt[N_BINS];
+    for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < m) {
         Seg sg = segs[s];
-        uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
+        const uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
         sg.len = end - sg.start;
-        Prog p = prog[sg.res];
-        int nr = p.n_param + p.n_flow + p.n_degrade;
-        bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max;
+        const Prog p = prog[sg.res];
+        const int nr = p.n_param + p.n_flow + p.n_degrade;
+        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max;
+        uint32_t bin;
         if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
             bin = (nr <= 4 ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
         }
-        sg.bin = bin;
+        const uint32_t rank = atomicAdd(&cnt[bin], 1u);
+        sg.bin = bin | (rank << 8);
         segs[s] = sg;
     }
-    (void)agg_slot(bin_cnt, bin, act);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) blkcnt[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
 }
-__global__ void k_seg_order(const Seg* __restrict__ segs, uint32_t m, uint32_t* __restrict__ cursor,
-                            uint32_t* __restrict__ order) {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    bool act = s < m;
-    uint32_t bin = act ? segs[s].bin : 0;
-    uint32_t p = agg_slot(cursor, bin, act);
-    if (act) order[p] = s;
+// bin-major dispatch list: order[off[bin][block] + rank] = segment
+__global__ __launch_bounds__(256) void k_seg_order(Seg* __restrict__ segs, uint32_t m, const uint32_t* __restrict__ off,
+                                                   uint32_t nblk, uint32_t* __restrict__ order) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= m) return;
+    const uint32_t v = segs[s].bin, bin = v & 0xFF;
+    order[off[(uint64_t)bin * nblk + blockIdx.x] + (v >> 8)] = s;
+    segs[s].bin = bin;
+}
+// per-bin first offsets (+ total) for the host: out[b] = off[b][0], out[N_BINS] = m
+__global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, uint32_t m, uint32_t* __restrict__ out) {
+    const uint32_t b = threadIdx.x;
+    if (b < N_BINS) out[b] = off[(uint64_t)b * nblk];
+    if (b == N_BINS) out[b] = m;
 }
 
 // =================================================================================
 // sorted records
 // =================================================================================
-__global__ void k_posof(const uint32_t* __restrict__ vals, uint64_t n, uint32_t* __restrict__ pos_of) {
-    uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < n) pos_of[vals[p]] = (uint32_t)p;
-}
-
-// One 16-byte record per event in sorted order.  EXIT/TRACE references are resolved here, in a
-// fully parallel pass, so the decide kernels never chase the status ring:
-//   - ENTRY earlier in this batch            -> RC_BATCH + its sorted position
-//   - ENTRY of an earlier batch (status ring)-> RC_PASSED / RC_NOT; unknown -> as if no reference
-// (or_submit in the oracle applies the same rules: an unknown reference means "the caller asserts
-// the entry passed" for an EXIT and "no entry" for a TRACE).
-__global__ void k_prep(const sg_event* __restrict__ ev, const uint32_t* __restrict__ vals, uint64_t n,
-                       const uint32_t* __restrict__ pos_of, uint64_t gbase, const uint8_t* __restrict__ ring,
-                       uint64_t ring_mask, int32_t max_rt, SEv* __restrict__ recs, uint32_t* __restrict__ bflags) {
-    uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Sorted-order records: a 16-byte gather of the record built in submission order (kernels.hip
+// k_rs_first), plus the mapping of same-batch references to the ENTRY's sorted position through
+// the inverse permutation written by the last radix pass (bit 31 = the referenced event is an
+// ENTRY).  A reference to a non-ENTRY resolves like an unknown entry in or_submit: an EXIT is then
+// taken as the caller asserting the entry passed, a TRACE as not counted.
+__global__ void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restrict__ vals, uint64_t n,
+                         const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
-    const int64_t t0 = ev[0].ts;
-    const uint32_t idx = vals[p];
-    const sg_event e = ev[idx];
-    uint32_t fl = 0;
-    SEv r;
-    int64_t dt = e.ts - t0;
-    if (dt < 0 || dt > 0x7FFFFFFFLL) fl |= (dt < 0 ? BF_BACKWARD : BF_TSPAN);
-    if (idx > 0 && ev[idx - 1].ts > e.ts) fl |= BF_BACKWARD;  // ABI: non-decreasing ts
-    r.dt = (int32_t)dt;
-    r.x = 0;
-    r.cnt = e.count;
-    r.rt = 0;
-    r.kind = e.kind;
-    r.flags = e.flags;
-    r.code = RC_NONE;
-    r.pad = 0;
-    if (e.kind == SG_EV_ENTRY) {
-        if (e.flags & SG_F_PRIORITIZED) fl |= BF_PRIORITIZED;
-    } else {
-        if (e.kind == SG_EV_EXIT) {
-            if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
-            int64_t raw = (int64_t)(e.aux >> 48);
-            r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
-        }
-        const uint64_t ref = e.aux & SG_REF_NONE;
-        if (ref != SG_REF_NONE) {
-            if (ref >= gbase) {
-                uint64_t ri = ref - gbase;
-                if (ri >= idx) fl |= BF_BAD_REF;  // an EXIT/TRACE must follow its ENTRY
-                else {
-                    const sg_event en = ev[ri];
-                    if (en.kind != SG_EV_ENTRY || en.res_id != e.res_id) fl |= BF_BAD_REF;
-                    else { r.code = RC_BATCH; r.x = pos_of[ri]; }
-                }
-            } else {
-                uint8_t st = ring[ref & ring_mask];
-                if (st == ST_NOT_ENTRY) r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-                else r.code = st_passed(st) ? RC_PASSED : RC_NOT;
-            }
-        }
+    SEv r = rec_o[vals[p] & 0x7FFFFFFFu];
+    if (r.code == RC_BATCH) {
+        const uint32_t po = pos_of[r.x];
+        if (po & 0x80000000u) r.x = po & 0x7FFFFFFFu;
+        else r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
     }
     recs[p] = r;
-    if (fl) atomicOr(bflags, fl);
 }
 
 // decisions back to submission order; the status ring keeps every event's status for
@@ -182,7 +136,7 @@ __global__ void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __re
                        uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask, uint32_t* __restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t d = dec[pos_of[i]];
+    uint32_t d = dec[pos_of[i] & 0x7FFFFFFFu];
     out[i] = d;
     ring[(gbase + i) & ring_mask] = (uint8_t)(d & 0xFF);
 }
@@ -201,7 +155,7 @@ __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict
     for (uint32_t j = 0; j < sg.len; ++j) {
         if (recs[sg.start + j].kind == SG_EV_ENTRY) {
             if (grant_all) info[sg.res].flags = f | NI_CHAIN;
-            else cand[atomicAdd(ncand, 1u)] = ((uint64_t)vals[sg.start + j] << 32) | sg.res;
+            else cand[atomicAdd(ncand, 1u)] = ((uint64_t)(vals[sg.start + j] & 0x7FFFFFFFu) << 32) | sg.res;
             return;
         }
     }
@@ -399,7 +353,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
         if (r.kind == SG_EV_ENTRY) {
             if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
             else {
-                uint64_t arg = (r.flags & SG_F_HAS_ARG) ? ev[vals[sg.start + j]].aux : 0;
+                uint64_t arg = (r.flags & SG_F_HAS_ARG) ? ev[vals[sg.start + j] & 0x7FFFFFFFu].aux : 0;
                 d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
             }
             if (j < 64 && st_passed(d & 0xFF)) pm |= 1ull << j;
@@ -410,7 +364,8 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
             else if (r.code == RC_NOT) eff = false;
             else {
                 uint32_t rel = r.x - sg.start;
-                eff = rel < 64 ? ((pm >> rel) & 1) != 0 : st_passed(dec[r.x] & 0xFF);
+                if (rel >= j) { atomicOr(bflags, BF_BAD_REF); eff = false; }  // not an earlier ENTRY of this resource
+                else eff = rel < 64 ? ((pm >> rel) & 1) != 0 : st_passed(dec[r.x] & 0xFF);
             }
             if (eff) {
                 if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
@@ -687,6 +642,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             if (r.code == RC_NONE || r.code == RC_PASSED) eff_val = true;  // the chain exists here
             else if (r.code == RC_BATCH) {
                 refrel = r.x - sg.start;
+                if (refrel >= pos) { atomicOr(bflags, BF_BAD_REF); refrel = 0; }  // not an earlier ENTRY of this resource
                 if (refrel + WIN >= tbase + HW) { eff_win = true; winidx = refrel & (WIN - 1); }
                 else  // decided >= WIN-HW positions ago, i.e. before >= 1 full fence
                     eff_val = st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
@@ -837,11 +793,13 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                                 bool eff = code == RC_NONE || code == RC_PASSED;
                                 if (code == RC_BATCH) {
                                     const uint32_t rel = rr[k].y - sg.start;
-                                    if (rel >= fpos0) eff = false;  // an ENTRY of this stretch: blocked
+                                    if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+                                    else if (rel >= fpos0) eff = false;  // an ENTRY of this stretch: blocked
                                     else if (rel + WIN >= sb + ST) eff = win[rel & (WIN - 1)] != 0;
                                     else eff = st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
                                                                            __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
                                 }
+                                win[q & (WIN - 1)] = 0;
                                 if (eff && ek == SG_EV_EXIT) {
                                     aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1;
                                 } else if (eff && ek == SG_EV_TRACE && ec > 0) {
@@ -1240,24 +1198,25 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
     return hipGetLastError();
 }
 hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
-                          uint32_t j4_max, uint32_t force_lane, uint32_t* bin_cnt, hipStream_t st) {
+                          uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st) {
     if (!m) return hipSuccess;
-    hipLaunchKernelGGL(k_seg_bin, dim3((m + 255) / 256), dim3(256), 0, st, segs, m, n, prog, lane_max, j1_max, j4_max,
-                       force_lane, bin_cnt);
+    const uint32_t nblk = (m + 255) / 256;
+    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, lane_max, j1_max, j4_max, force_lane,
+                       blkcnt, nblk);
     return hipGetLastError();
 }
-hipError_t launch_seg_order(const Seg* segs, uint32_t m, uint32_t* cursor, uint32_t* order, hipStream_t st) {
-    if (!m) return hipSuccess;
-    hipLaunchKernelGGL(k_seg_order, dim3((m + 255) / 256), dim3(256), 0, st, segs, m, cursor, order);
+// off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]
+hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
+                            hipStream_t st) {
+    const uint32_t nblk = (m + 255) / 256;
+    if (m) hipLaunchKernelGGL(k_seg_order, dim3(nblk), dim3(256), 0, st, segs, m, off, nblk, order);
+    hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(64), 0, st, off, nblk ? nblk : 1, m, bin_off);
     return hipGetLastError();
 }
-hipError_t launch_prep(const sg_event* ev, const uint32_t* vals, uint64_t n, uint32_t* pos_of, uint64_t gbase,
-                       const uint8_t* ring, uint64_t ring_mask, int32_t max_rt, SEv* recs, uint32_t* bflags,
-                       hipStream_t st) {
+hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
+                         hipStream_t st) {
     uint32_t nb = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_posof, dim3(nb), dim3(256), 0, st, vals, n, pos_of);
-    hipLaunchKernelGGL(k_prep, dim3(nb), dim3(256), 0, st, ev, vals, n, pos_of, gbase, ring, ring_mask, max_rt, recs,
-                       bflags);
+    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs);
     return hipGetLastError();
 }
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,

@@ -21,10 +21,13 @@
 
 namespace sg {
 // kernels.hip
-hipError_t launch_radix_hist(const sg_event*, const uint32_t*, uint64_t, int, uint32_t*, uint32_t, uint32_t*, uint32_t,
-                             hipStream_t);
-hipError_t launch_radix_scatter(const sg_event*, const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                uint32_t, uint32_t*, uint32_t*, hipStream_t);
+hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
+                           uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, hipStream_t st);
+hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
+                             hipStream_t st);
+hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
+                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
 uint32_t radix_tile();
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
@@ -36,11 +39,11 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
 hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
-                          uint32_t j4_max, uint32_t force_lane, uint32_t* bin_cnt, hipStream_t st);
-hipError_t launch_seg_order(const Seg* segs, uint32_t m, uint32_t* cursor, uint32_t* order, hipStream_t st);
-hipError_t launch_prep(const sg_event* ev, const uint32_t* vals, uint64_t n, uint32_t* pos_of, uint64_t gbase,
-                       const uint8_t* ring, uint64_t ring_mask, int32_t max_rt, SEv* recs, uint32_t* bflags,
-                       hipStream_t st);
+                          uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st);
+hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
+                            hipStream_t st);
+hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
+                         hipStream_t st);
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
@@ -415,8 +418,8 @@ struct sg_engine {
     uint32_t* d_out = nullptr;
     uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
     uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
-    uint32_t *d_posof = nullptr, *d_dec = nullptr;
-    SEv* d_recs = nullptr;
+    uint32_t *d_posof = nullptr, *d_dec = nullptr, *d_blkcnt = nullptr;
+    SEv *d_recs = nullptr, *d_rec_o = nullptr;
     Seg* d_segs = nullptr;
     // d_small: [0] bflags [1] nseg [2] ncand [3] snapshot total [8..8+N_BINS) bin counts
     //          [64..64+N_BINS) bin cursors
@@ -444,7 +447,7 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     uint64_t c = std::max<uint64_t>(n, 1u << 20);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs);
+    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
     uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
     e->cap_hist = nblocks * 256;
     HIPCHK(hipMalloc(&e->d_ev, c * sizeof(sg_event)));
@@ -463,6 +466,8 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_posof, c * 4));
     HIPCHK(hipMalloc(&e->d_dec, c * 4));
     HIPCHK(hipMalloc(&e->d_recs, c * sizeof(SEv)));
+    HIPCHK(hipMalloc(&e->d_rec_o, c * sizeof(SEv)));
+    HIPCHK(hipMalloc(&e->d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));
     e->cap_n = c;
     return SG_OK;
 }
@@ -752,7 +757,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs);
+    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
     for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
@@ -1017,37 +1022,35 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     uint32_t* dev_out = host_out ? e->d_out : out;
     const uint64_t ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
     HIPCHK(hipEventRecord(e->ev[0], st));
-    // ---- 1. group: stable LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
+    // ---- 1. group: records + stable LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
     uint32_t R = e->cfg.max_resources;
     int bits = 1;
     while (bits < 32 && (1ull << bits) < R) ++bits;
     int passes = (bits + 7) / 8;
     uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
     HIPCHK(hipMemsetAsync(e->d_small, 0, 256 * 4, st));
-    uint32_t *kin = nullptr, *vin = nullptr, *kout = e->d_k0, *vout = e->d_v0;
+    int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_small + 4);  // [4..5]
+    HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
+                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, st));
+    uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
-        const sg_event* pev = p == 0 ? dev_ev : nullptr;
-        HIPCHK(launch_radix_hist(pev, kin, n, p * 8, e->d_hist, nblocks, e->d_small + 0, R, st));
+        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
         HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, st));
-        HIPCHK(launch_radix_scatter(pev, kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout, st));
-        kin = kout; vin = vout;
-        kout = (kin == e->d_k0) ? e->d_k1 : e->d_k0;
-        vout = (vin == e->d_v0) ? e->d_v1 : e->d_v0;
+        HIPCHK(launch_radix_scatter(kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout,
+                                    p == passes - 1 ? e->d_posof : nullptr, st));
+        std::swap(kin, kout);
+        std::swap(vin, vout);
     }
-    // ---- 2. segments + 16-byte sorted records (references resolved against the status ring)
+    // ---- 2. segments + 16-byte sorted records
     HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, st, launch_scan, e->d_part, e->d_small + 1));
-    HIPCHK(launch_prep(dev_ev, vin, n, e->d_posof, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt,
-                       e->d_recs, e->d_small + 0, st));
-    uint32_t m = 0;
-    HIPCHK(hipMemcpyAsync(&m, e->d_small + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, st));
+    uint32_t head[6];
+    HIPCHK(hipMemcpyAsync(head, e->d_small, sizeof(head), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
-    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
-                          e->d_small + 8, st));
-    uint32_t small[8 + N_BINS];
-    HIPCHK(hipMemcpyAsync(small, e->d_small, sizeof(small), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    uint32_t bflags = small[0];
+    const uint32_t m = head[1];
+    int64_t t0 = 0;
+    std::memcpy(&t0, head + 4, 8);
+    uint32_t bflags = head[0];
     if (bflags & BF_BAD_RES) return fail(SG_EINVAL, "event res_id >= max_resources");
     if (bflags & BF_BAD_REF)
         return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
@@ -1056,12 +1059,18 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     if (bflags & BF_PRIORITIZED)
         return fail(SG_ENOTSUP, "prioritized entries (StatisticNode.tryOccupyNext) are not on the device path yet");
     if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
-    // bin-ordered dispatch list
-    uint32_t cursor[N_BINS], off[N_BINS + 1];
-    off[0] = 0;
-    for (int b = 0; b < N_BINS; ++b) { cursor[b] = off[b]; off[b + 1] = off[b] + small[8 + b]; }
-    HIPCHK(hipMemcpyAsync(e->d_small + 64, cursor, sizeof(cursor), hipMemcpyHostToDevice, st));
-    HIPCHK(launch_seg_order(e->d_segs, m, e->d_small + 64, e->d_order, st));
+    // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
+    const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
+    const uint32_t nblk = (m + 255) / 256;
+    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
+                          e->d_blkcnt, st));
+    HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, st));
+    HIPCHK(launch_seg_order(e->d_segs, m, e->d_blkcnt, e->d_order, e->d_small + 8, st));
+    uint32_t off[N_BINS + 1];
+    HIPCHK(hipMemcpyAsync(off, e->d_small + 8, sizeof(off), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint32_t bin_n[N_BINS];
+    for (int b = 0; b < N_BINS; ++b) bin_n[b] = off[b + 1] - off[b];
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
@@ -1110,17 +1119,15 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.ptab = e->d_ptab;
     S.ring = e->d_ring;
     S.sink = e->d_sink;
-    int64_t t0 = 0;
-    HIPCHK(hipMemcpy(&t0, &dev_ev[0].ts, 8, hipMemcpyDeviceToHost));
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
     for (int k = 0; k < 3; ++k) {
         const int b = coop[k];
-        if (!small[8 + b]) continue;
+        if (!bin_n[b]) continue;
         DevState Sb = S;
         Sb.dbg = (k == 0 && e->d_dbg) ? e->d_dbg : nullptr;
         HIPCHK(hipStreamWaitEvent(e->bin_stream[k], e->fork, 0));
-        HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], small[8 + b], Sb, dc, t0,
+        HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sb, dc, t0,
                                  e->d_dec, e->d_small + 0, e->bin_stream[k]));
         HIPCHK(hipEventRecord(e->join[k], e->bin_stream[k]));
     }
@@ -1129,7 +1136,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
                              off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_small + 0, st));
     for (int k = 0; k < 3; ++k)
-        if (small[8 + coop[k]]) HIPCHK(hipStreamWaitEvent(st, e->join[k], 0));
+        if (bin_n[coop[k]]) HIPCHK(hipStreamWaitEvent(st, e->join[k], 0));
     HIPCHK(hipEventRecord(e->ev[2], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));

@@ -26,41 +26,93 @@ using namespace sg;
 #define RS_TILE (RS_THREADS * RS_ITEMS)
 #define RS_BINS 256
 
-// batch flags + key extraction happen on the first histogram pass
-__global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const sg_event* __restrict__ ev, const uint32_t* __restrict__ keys,
-                                                        uint64_t n, int shift, uint32_t* __restrict__ ghist,
-                                                        uint32_t nblocks, uint32_t* __restrict__ bflags, uint32_t max_res) {
+// First pass over the caller's events, in submission order (coalesced): validates the batch,
+// builds the 16-byte decide record of every event (references to ENTRYs of earlier batches are
+// resolved against the status ring here; same-batch references keep the ENTRY's batch index and
+// are mapped to its sorted position after the sort), writes the sort keys/values (value bit 31 =
+// "is an ENTRY", so the inverse permutation also says whether a reference hits an ENTRY) and the
+// histogram of the first radix digit.
+__global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
+                                                      uint64_t gbase, const uint8_t* __restrict__ ring,
+                                                      uint64_t ring_mask, int32_t max_rt, SEv* __restrict__ rec_o,
+                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                      uint32_t* __restrict__ ghist, uint32_t nblocks,
+                                                      uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out) {
     __shared__ uint32_t h[RS_BINS];
     for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
     __syncthreads();
-    uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const int64_t t0 = ev[0].ts;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *t0_out = t0;
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
     uint32_t fl = 0;
     for (int it = 0; it < RS_ITEMS; ++it) {
-        uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
-        if (i < n) {
-            uint32_t k;
-            if (ev) {
-                const sg_event& e = ev[i];
-                k = e.res_id;
-                if (e.kind == SG_EV_ENTRY && (e.flags & SG_F_PRIORITIZED)) fl |= BF_PRIORITIZED;
-                if (e.kind == SG_EV_EXIT && (e.flags & SG_F_EXIT_ARGS)) fl |= BF_EXIT_ARGS;
-                if (k >= max_res) fl |= BF_BAD_RES;
-            } else {
-                k = keys[i];
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        if (i >= n) continue;
+        const sg_event e = ev[i];
+        if (e.res_id >= max_res) fl |= BF_BAD_RES;
+        const int64_t dt = e.ts - t0;
+        if (dt < 0 || dt > 0x7FFFFFFFLL) fl |= (dt < 0 ? BF_BACKWARD : BF_TSPAN);
+        if (i > 0 && ev[i - 1].ts > e.ts) fl |= BF_BACKWARD;  // ABI: non-decreasing ts
+        SEv r;
+        r.dt = (int32_t)dt;
+        r.x = 0;
+        r.cnt = e.count;
+        r.rt = 0;
+        r.kind = e.kind;
+        r.flags = e.flags;
+        r.code = RC_NONE;
+        r.pad = 0;
+        if (e.kind == SG_EV_ENTRY) {
+            if (e.flags & SG_F_PRIORITIZED) fl |= BF_PRIORITIZED;
+        } else {
+            if (e.kind == SG_EV_EXIT) {
+                if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
+                const int64_t raw = (int64_t)(e.aux >> 48);
+                r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
             }
-            atomicAdd(&h[(k >> shift) & (RS_BINS - 1)], 1u);
+            const uint64_t ref = e.aux & SG_REF_NONE;
+            if (ref != SG_REF_NONE) {
+                if (ref >= gbase) {
+                    if (ref - gbase >= i) fl |= BF_BAD_REF;  // an EXIT/TRACE must follow its ENTRY
+                    else { r.code = RC_BATCH; r.x = (uint32_t)(ref - gbase); }
+                } else {  // an ENTRY of an earlier batch: its status from the ring (0xFF = not an ENTRY)
+                    const uint8_t st = ring[ref & ring_mask];
+                    if (st == ST_NOT_ENTRY) r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+                    else r.code = (st == ST_PASS || st == ST_PASS_WAIT) ? RC_PASSED : RC_NOT;
+                }
+            }
         }
+        rec_o[i] = r;
+        keys[i] = e.res_id;
+        vals[i] = (uint32_t)i | (e.kind == SG_EV_ENTRY ? 0x80000000u : 0u);
+        atomicAdd(&h[e.res_id & (RS_BINS - 1)], 1u);
     }
-    if (ev && fl) atomicOr(bflags, fl);
+    if (fl) atomicOr(bflags, fl);
     __syncthreads();
     for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// stable scatter: items of a tile are ranked in (round, wave, lane) order == input order
-__global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const sg_event* __restrict__ ev, const uint32_t* __restrict__ keys_in,
+__global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, uint64_t n, int shift,
+                                                        uint32_t* __restrict__ ghist, uint32_t nblocks) {
+    __shared__ uint32_t h[RS_BINS];
+    for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    for (int it = 0; it < RS_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RS_BINS - 1)], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
+}
+
+// stable scatter: items of a tile are ranked in (round, wave, lane) order == input order.  The last
+// pass also writes the inverse permutation pos_of[idx] = sorted position | ENTRY bit.
+__global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
-                                                           uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out) {
+                                                           uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                           uint32_t* __restrict__ pos_of) {
     __shared__ uint32_t wcnt[4][RS_BINS];
     __shared__ uint32_t woff[4][RS_BINS];
     __shared__ uint32_t run[RS_BINS];
@@ -76,10 +128,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const sg_event* __
         uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
         bool valid = i < n;
         uint32_t k = 0, v = 0;
-        if (valid) {
-            if (ev) { k = ev[i].res_id; v = (uint32_t)i; }
-            else { k = keys_in[i]; v = vals_in[i]; }
-        }
+        if (valid) { k = keys_in[i]; v = vals_in[i]; }
         uint32_t d = (k >> shift) & (RS_BINS - 1);
         // peers: lanes with the same digit (8 ballots)
         uint64_t peers = __ballot(valid);
@@ -104,6 +153,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const sg_event* __
             uint32_t dst = woff[w][d] + rank;
             keys_out[dst] = k;
             vals_out[dst] = v;
+            if (pos_of) pos_of[v & 0x7FFFFFFFu] = dst | (v & 0x80000000u);
         }
         __syncthreads();
     }
@@ -273,16 +323,22 @@ __global__ void k_set_flags(NodeInfo* __restrict__ info, const uint64_t* __restr
 // =================================================================================
 namespace sg {
 
-hipError_t launch_radix_hist(const sg_event* ev, const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist,
-                             uint32_t nblocks, uint32_t* bflags, uint32_t max_res, hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, keys, n, shift, ghist, nblocks, bflags,
-                       max_res);
+hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
+                           uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, hipStream_t st) {
+    hipLaunchKernelGGL(k_rs_first, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask, max_rt,
+                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out);
     return hipGetLastError();
 }
-hipError_t launch_radix_scatter(const sg_event* ev, const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift,
-                                const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, kin, vin, n, shift, goff, nblocks,
-                       kout, vout);
+hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
+    return hipGetLastError();
+}
+hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
+                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks, kout,
+                       vout, pos_of);
     return hipGetLastError();
 }
 uint32_t radix_tile() { return RS_TILE; }
