@@ -1107,7 +1107,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     dc.ptab_mask = (1ull << e->cfg.param_table_log2) - 1;
     dc.ring_mask = ring_mask;
     dc.dbg_flags = e->dbg_flags;
-    DevState S;
+    DevState S{};
     std::memset(&S, 0, sizeof(S));
     S.sec = e->d_sec;
     S.minb = e->d_minb;

@@ -14,7 +14,8 @@ import numpy as np
 from . import _abi as A
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
+# SG_LIB_PATH: diagnostics only (e.g. a -DSG_KPROF build for tools/hotprobe.py)
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsentinel_gpu.so")
 _lib = None
 
 # every entry point declared in include/sentinel_gpu.h
