@@ -433,6 +433,15 @@ __device__ __forceinline__ int64_t wscan_i64_max(int64_t x) {
 // of k_jac lives in LDS; the only cross-wave global data are decisions read back as old references,
 // and those are ordered by the full __syncthreads() every FULL_FENCE_TILES tiles plus an L1-bypassing
 // (agent-scope) load.
+// LDS-broadcast values that steer control flow around barriers are read through readfirstlane:
+// provably uniform, they become scalar branches, and the compiler cannot restructure a loop whose
+// exit it would otherwise believe divergent into one where lanes of a wave run different numbers
+// of barriers.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    const uint32_t lo = uni((uint32_t)(uint64_t)v), hi = uni((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 #define FULL_FENCE_TILES 8
 
@@ -669,7 +678,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     uint32_t mb = 0;  // mism double-buffer index
 
     for (;;) {
-        uint32_t c0 = sh.c0;
+        uint32_t c0 = uni(sh.c0);
         const uint32_t cnt_t = sg.len - tbase < HW ? sg.len - tbase : HW;
         if (c0 >= cnt_t) {  // tile done: advance (uniform)
             if (tbase + HW >= sg.len) break;
@@ -684,8 +693,8 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         ++n_it;
         PROF_MARK(0)
         {  // round check on the event at c0 (uniform)
-            const int64_t tn = sh.tnext;
-            const bool need = !sh.round_open || (tn / 500) != sh.bkt0 || tn >= sh.next_reset;
+            const int64_t tn = uni64(sh.tnext);
+            const bool need = !uni(sh.round_open) || (tn / 500) != uni64(sh.bkt0) || tn >= uni64(sh.next_reset);
             if (need) {
                 PROF_MARK(0)
                 lds_barrier();  // every wave has read the round state before the leader rewrites it
@@ -699,8 +708,9 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             }
         }
         // the round's events: relative times in [dlo, dhi) (its 500 ms bucket, before the next reset)
-        const int64_t dlo = sh.bkt0 * 500 - t0;
-        const int64_t dhi = (sh.next_reset - t0 < dlo + 500) ? sh.next_reset - t0 : dlo + 500;
+        const int64_t dlo = uni64(sh.bkt0) * 500 - t0;
+        const int64_t nrs = uni64(sh.next_reset) - t0;
+        const int64_t dhi = (nrs < dlo + 500) ? nrs : dlo + 500;
 
         // ================= frozen stretch =================
         // All flow stages are QPS DefaultControllers and either one of them is already saturated
@@ -708,13 +718,14 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         // the pass count and every rule state stay fixed, each verdict is a pure function of the
         // event, and the rest of the round is a map + reduction (one barrier per tile).
         if (frozen_prog) {
-            const int64_t Pfix = sh.bP + sh.cP;
+            const int64_t Pfix = uni64(sh.bP + sh.cP);
             const int32_t pint = j_d2i((double)Pfix);
-            const bool cutk0 = nd > 0 && sh.rs[nf].a != 0;
+            const bool cutk0 = nd > 0 && uni(sh.rs[nf].a != 0);
             bool sat = false;
 #pragma unroll
             for (int s = 0; s < MF; ++s)
                 if (s < nf) sat |= (double)j_iadd(pint, 1) > sh.rules[s].count;
+            sat = uni(sat) != 0;
             if (sat || cutk0) {
                 constexpr uint32_t EPL = 4, ST = EPL * HW;  // events per lane, positions per super-tile
                 static_assert(WIN - ST >= (FULL_FENCE_TILES + 1) * (ST + HW), "old references must precede a full fence");
@@ -771,6 +782,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     lds_barrier();
                     uint32_t f = NO_LANE;
                     for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    f = uni(f);
                     mb ^= 1;
                     ++n_frz;
                     // commit every position before the stop.  The decision stores are unconditional
@@ -1070,6 +1082,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         lds_barrier();  // B4
         uint32_t f = NO_LANE;
         for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    f = uni(f);
         mb ^= 1;
         if (f != NO_LANE) ++n_mm;
         const uint32_t e_end = c0 + inr_total;
