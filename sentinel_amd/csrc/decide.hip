@@ -616,7 +616,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     const bool prof = S.dbg != nullptr;
     uint32_t n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0;
 #ifdef SG_KPROF
-    const bool prof0 = prof && blockIdx.x == 0 && tid == 0;
+    const bool prof0 = prof && tid == 0;  // every block times itself; the longest segment reports
     unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define PROF_MARK(k)                                          \
     if (prof0) {                                              \
@@ -1178,10 +1178,11 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         atomicAdd(&S.dbg[3], (unsigned long long)n_mm);
         atomicAdd(&S.dbg[4], 1ull);
         atomicAdd(&S.dbg[6], (unsigned long long)n_frz);
-        if (blockIdx.x == 0) S.dbg[5] = sg.len;
 #ifdef SG_KPROF
-        if (blockIdx.x == 0)
+        if (atomicMax(&S.dbg[5], (unsigned long long)sg.len) < sg.len)  // longest segment so far
             for (int k = 0; k < 10; ++k) S.dbg[8 + k] = tph[k];
+#else
+        if (blockIdx.x == 0) S.dbg[5] = sg.len;
 #endif
     }
 #undef PROF_MARK

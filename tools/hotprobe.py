@@ -43,5 +43,5 @@ for i in range(nb):
     ph = v[8:18].astype(np.float64)
     tot = ph.sum() or 1
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
-    print("  block0 (len %d) phase cycles:" % v[5], {k: "%.0f" % ph[j] for j, k in enumerate(names)})
+    print("  longest segment (len %d) phase cycles:" % v[5], {k: "%.0f" % ph[j] for j, k in enumerate(names)})
     print("  frozen tiles (all J16 segments):", d[6])
