@@ -786,7 +786,9 @@ typedef struct {
 
 typedef struct {
     int64_t flow_id;
-    int rule_index;            /* into cl_rules */
+    double count;              /* FlowRule.count of the rule now mapped to this flowId */
+    int32_t threshold_type;    /* ClusterFlowConfig.thresholdType */
+    int live;                  /* still named by the loaded list */
     oleap metric;              /* ClusterMetricLeapArray (7 events) */
     int64_t occupy_pass, occupy_pass_req;
     int has_occupied;
@@ -1044,22 +1046,35 @@ int or_load_flow_rules(or_engine* e, const sg_flow_rule* r, uint32_t n, uint32_t
     free(hs);
     if (n_loaded) *n_loaded = (uint32_t)e->n_flows;
 
-    /* token server view: ClusterFlowRuleManager keeps cluster-mode rules by flowId */
-    for (int k = 0; k < e->n_flows; ++k) {
-        oflow* f = &e->flows[k];
-        if (!f->r.cluster_mode) continue;
+    /* token server view: ClusterFlowRuleManager.applyClusterFlowRule (csrv/flow/rule/
+     * ClusterFlowRuleManager.java:323-363) walks the list in order; cluster-mode rules that pass
+     * FlowRuleUtil.isValidRule; ruleMap.put -> the last rule of a flowId wins; putMetricIfAbsent keeps
+     * an existing metric (window shape included); clearAndResetRulesConditional drops the others. */
+    for (int j = 0; j < e->n_cl; ++j) e->cl[j].live = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_flow_rule* q = &r[i];
+        if (!q->cluster_mode || !flow_valid(q)) continue;
         int found = -1;
-        for (int j = 0; j < e->n_cl; ++j) if (e->cl[j].flow_id == f->r.cluster_flow_id) found = j;
-        if (found < 0) { /* ClusterMetricStatistics.putMetricIfAbsent */
+        for (int j = 0; j < e->n_cl; ++j) if (e->cl[j].flow_id == q->cluster_flow_id) found = j;
+        if (found < 0) {
             e->cl = (ocluster*)realloc(e->cl, sizeof(ocluster) * (size_t)(e->n_cl + 1));
             ocluster* c = &e->cl[e->n_cl++];
             memset(c, 0, sizeof(*c));
-            c->flow_id = f->r.cluster_flow_id;
-            leap_init(&c->metric, LEAP_PLAIN, f->r.cluster_sample_count, f->r.cluster_window_interval_ms, e->c.max_rt);
-            c->connected = 0;
+            c->flow_id = q->cluster_flow_id;
+            leap_init(&c->metric, LEAP_PLAIN, q->cluster_sample_count, q->cluster_window_interval_ms, e->c.max_rt);
             found = e->n_cl - 1;
         }
-        e->cl[found].rule_index = k;
+        e->cl[found].count = q->count;
+        e->cl[found].threshold_type = q->cluster_threshold_type;
+        e->cl[found].live = 1;
+    }
+    {
+        int w = 0;
+        for (int j = 0; j < e->n_cl; ++j) {
+            if (e->cl[j].live) e->cl[w++] = e->cl[j];
+            else leap_free(&e->cl[j].metric);
+        }
+        e->n_cl = w;
     }
     return SG_OK;
 }
@@ -2019,10 +2034,9 @@ int or_cluster_request_tokens(or_engine* e, const sg_token_req* reqs, uint64_t n
         ocluster* c = NULL;
         for (int k = 0; k < e->n_cl; ++k) if (e->cl[k].flow_id == q->flow_id) c = &e->cl[k];
         if (!c) { o->status = SG_TOKEN_NO_RULE_EXISTS; continue; }
-        oflow* rule = &e->flows[c->rule_index];
         int64_t now = q->ts;
         /* GlobalRequestLimiter.tryPass (limit/GlobalRequestLimiter.java:46-54, RequestLimiter.java:72-87) */
-        {
+        if (e->max_allowed_qps >= 0) {  /* a negative qpsAllowed: no limiter registered -> tryPass true */
             obucket* w = leap_current(&e->ns_limiter, now);
             int64_t s = leap_sum(&e->ns_limiter, now, EV_PASS);
             if (!((double)s / (e->ns_limiter.interval / 1000.0) + 1 <= e->max_allowed_qps)) {
@@ -2031,8 +2045,7 @@ int or_cluster_request_tokens(or_engine* e, const sg_token_req* reqs, uint64_t n
             if (w) w->c[EV_PASS] += 1;
         }
         double latest_qps = cl_avg(c, now, CF_PASS_REQ);
-        double thr = rule->r.cluster_threshold_type == SG_CLUSTER_THRESHOLD_GLOBAL ? rule->r.count
-                                                                                   : rule->r.count * c->connected;
+        double thr = c->threshold_type == SG_CLUSTER_THRESHOLD_GLOBAL ? c->count : c->count * c->connected;
         double global_threshold = thr * e->exceed_count;
         double next_remaining = global_threshold - latest_qps - q->acquire_count;
         if (next_remaining >= 0) {

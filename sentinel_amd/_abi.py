@@ -333,3 +333,8 @@ def param_rule(resource, param_idx, count, grade=FLOW_GRADE_QPS, duration_in_sec
     r.cluster_sample_count = 10
     r.cluster_window_interval_ms = 1000
     return r
+
+
+# numpy views of sg_token_req / sg_token_result for bulk calls
+TOKEN_REQ_DTYPE = np.dtype([("ts", "<i8"), ("flow_id", "<i8"), ("acquire_count", "<i4"), ("prioritized", "<i4")])
+TOKEN_RES_DTYPE = np.dtype([("status", "<i4"), ("remaining", "<i4"), ("wait_in_ms", "<i4"), ("reserved", "<i4")])

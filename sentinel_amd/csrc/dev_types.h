@@ -135,6 +135,34 @@ struct Seg {
     uint32_t bin;    // BIN_*
 };
 
+// ---- token server (cluster.hip): ClusterMetric per flowId + the namespace GlobalRequestLimiter
+enum { CF_PASS = 0, CF_BLOCK, CF_PASS_REQ, CF_BLOCK_REQ, CF_OCC_PASS, CF_OCC_BLOCK, CF_WAITING, CF_N };  // ClusterFlowEvent
+struct CBkt {          // ClusterMetricBucket in a LeapArray slot; ws < 0: slot never created
+    int64_t ws;
+    int64_t c[CF_N];
+};
+struct CFlow {         // one flowId: rule view + ClusterMetricLeapArray bookkeeping
+    int64_t flow_id;
+    double count;                  // FlowRule.count
+    int32_t thr_type;              // ClusterFlowConfig.thresholdType
+    int32_t n, interval;           // sampleCount, windowIntervalMs of the metric (fixed at creation)
+    int32_t connected;             // ConnectionManager.getConnectedCount (AVG_LOCAL)
+    uint32_t boff;                 // first bucket in the bucket array
+    uint32_t has_occ;              // ClusterMetricLeapArray.hasOccupied
+    int64_t occ_pass, occ_req;     // occupyCounter[PASS], occupyCounter[PASS_REQUEST]
+};
+struct CSlot {         // flowId -> flow index (open addressing, idx 0xFFFFFFFF = empty)
+    int64_t key;
+    uint32_t idx, pad;
+};
+#define NS_BUCKETS 10   // RequestLimiter: UnaryLeapArray(10, 1000)
+#define NS_WLEN 100
+#define NS_INTERVAL 1000
+struct NsLimiter {
+    int64_t ws[NS_BUCKETS];   // < 0: never created
+    int64_t cnt[NS_BUCKETS];
+};
+
 struct DevState {
     Bkt* sec;
     Bkt* minb;

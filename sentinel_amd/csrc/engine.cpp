@@ -51,6 +51,15 @@ hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, 
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st);
+// cluster.hip
+hipError_t launch_tok_classify(const sg_token_req* req, uint64_t n, const CSlot* tab, uint32_t mask, uint32_t* fidx,
+                               sg_token_result* res, uint32_t* flags, hipStream_t st);
+hipError_t launch_tok_limiter(const sg_token_req* req, uint64_t n, const uint32_t* fidx, uint32_t nflows,
+                              NsLimiter* lim, double allowed, uint32_t* keys, uint32_t* vals, sg_token_result* res,
+                              hipStream_t st);
+hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_token_req* req,
+                           CFlow* flows, uint32_t nflows, CBkt* bkts, double exceed, double max_occ_ratio,
+                           sg_token_result* res, hipStream_t st);
 } // namespace sg
 
 using namespace sg;
@@ -434,6 +443,20 @@ struct sg_engine {
     hipStream_t bin_stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
+    // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
+    // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
+    std::vector<CFlow> cflows;                    // host copy of the config part (state lives on the device)
+    std::unordered_map<int64_t, uint32_t> cmap;   // flowId -> flow index
+    CFlow* d_cflow = nullptr;
+    CBkt* d_cbkt = nullptr;
+    CSlot* d_ctab = nullptr;
+    uint32_t ctab_mask = 0;
+    uint64_t ncbkt = 0;
+    NsLimiter* d_nslim = nullptr;
+    sg_token_req* d_treq = nullptr;
+    sg_token_result* d_tres = nullptr;
+    uint32_t* d_tfidx = nullptr;
+    uint64_t tcap = 0;
     // snapshot scratch
     uint32_t *d_snap_cnt = nullptr, *d_snap_off = nullptr;
     sg_metric_node* d_snap_out = nullptr;
@@ -758,6 +781,8 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
     dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
+    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim);
+    dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
     for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
@@ -808,6 +833,86 @@ static int register_rule_resource(sg_engine* e, const char* name, uint32_t* id) 
 }
 
 // FlowRuleManager.loadRules -> FlowRuleUtil.buildFlowRuleMap (core/slots/block/flow/FlowRuleUtil.java:89-137)
+// ClusterFlowRuleManager.applyClusterFlowRule (csrv/flow/rule/ClusterFlowRuleManager.java:323-363): the
+// cluster-mode rules of the list, in list order, FlowRuleUtil.isValidRule; a later rule with the same
+// flowId replaces an earlier one (ruleMap.put).  ClusterMetricStatistics.putMetricIfAbsent keeps the
+// metric (and its window shape) of a flowId that stays; clearAndResetRulesConditional drops the rest.
+static uint64_t tab_hash_h(int64_t k) {  // same mix as cluster.hip tab_hash
+    uint64_t z = (uint64_t)k + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static int rebuild_cluster(sg_engine* e, const sg_flow_rule* rules, uint32_t n) {
+    std::vector<int64_t> order;                       // flowIds in first-appearance order
+    std::unordered_map<int64_t, const sg_flow_rule*> rule_of;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_flow_rule& r = rules[i];
+        if (!r.cluster_mode || !flow_valid(r)) continue;
+        if (!rule_of.count(r.cluster_flow_id)) order.push_back(r.cluster_flow_id);
+        rule_of[r.cluster_flow_id] = &r;
+    }
+    // current device state of the flows that stay
+    const uint32_t nold = (uint32_t)e->cflows.size();
+    std::vector<CFlow> old_f(nold);
+    std::vector<CBkt> old_b(e->ncbkt);
+    if (nold) HIPCHK(hipMemcpy(old_f.data(), e->d_cflow, nold * sizeof(CFlow), hipMemcpyDeviceToHost));
+    if (e->ncbkt) HIPCHK(hipMemcpy(old_b.data(), e->d_cbkt, e->ncbkt * sizeof(CBkt), hipMemcpyDeviceToHost));
+    std::vector<CFlow> nf;
+    std::vector<CBkt> nb;
+    std::unordered_map<int64_t, uint32_t> nmap;
+    for (int64_t fid : order) {
+        const sg_flow_rule& r = *rule_of[fid];
+        CFlow f;
+        std::memset(&f, 0, sizeof(f));
+        auto it = e->cmap.find(fid);
+        if (it != e->cmap.end()) {  // metric kept, rule replaced
+            f = old_f[it->second];
+            const uint32_t ob = f.boff;
+            f.boff = (uint32_t)nb.size();
+            for (int k = 0; k < f.n; ++k) nb.push_back(old_b[ob + k]);
+        } else {
+            f.flow_id = fid;
+            f.n = r.cluster_sample_count;
+            f.interval = r.cluster_window_interval_ms;
+            f.boff = (uint32_t)nb.size();
+            CBkt z;
+            std::memset(&z, 0, sizeof(z));
+            z.ws = -1;
+            for (int k = 0; k < f.n; ++k) nb.push_back(z);
+        }
+        f.count = r.count;
+        f.thr_type = r.cluster_threshold_type;
+        nmap[fid] = (uint32_t)nf.size();
+        nf.push_back(f);
+    }
+    uint32_t cap = 16;
+    while (cap < 2 * nf.size() + 2) cap <<= 1;
+    std::vector<CSlot> tab(cap);
+    for (auto& t : tab) { t.key = 0; t.idx = 0xFFFFFFFFu; t.pad = 0; }
+    for (uint32_t i = 0; i < nf.size(); ++i) {
+        uint64_t h = tab_hash_h(nf[i].flow_id) & (cap - 1);
+        while (tab[h].idx != 0xFFFFFFFFu) h = (h + 1) & (cap - 1);
+        tab[h].key = nf[i].flow_id;
+        tab[h].idx = i;
+    }
+    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab);
+    e->d_cflow = nullptr; e->d_cbkt = nullptr; e->d_ctab = nullptr;
+    if (!nf.empty()) {
+        HIPCHK(hipMalloc(&e->d_cflow, nf.size() * sizeof(CFlow)));
+        HIPCHK(hipMemcpy(e->d_cflow, nf.data(), nf.size() * sizeof(CFlow), hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_cbkt, nb.size() * sizeof(CBkt)));
+        HIPCHK(hipMemcpy(e->d_cbkt, nb.data(), nb.size() * sizeof(CBkt), hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMalloc(&e->d_ctab, cap * sizeof(CSlot)));
+    HIPCHK(hipMemcpy(e->d_ctab, tab.data(), cap * sizeof(CSlot), hipMemcpyHostToDevice));
+    e->ctab_mask = cap - 1;
+    e->cflows = std::move(nf);
+    e->ncbkt = nb.size();
+    e->cmap = std::move(nmap);
+    return SG_OK;
+}
+
 int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
     std::vector<std::string> keys(n);
@@ -867,6 +972,8 @@ int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint
     if (rc) { e->flows = std::move(old_flows); e->res_flow = std::move(old_per); return rc; }
     e->last_flow = keys;
     e->flow_loaded = true;
+    rc = rebuild_cluster(e, rules, n);
+    if (rc) return rc;
     if (n_loaded) *n_loaded = (uint32_t)e->flows.size();
     return SG_OK;
 }
@@ -1235,15 +1342,73 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
 }
 
 int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected) {
-    (void)flow_id; (void)connected;
     if (!e) return fail(SG_EINVAL, "null engine");
-    return fail(SG_ENOTSUP, "token server is not on the device path yet");
+    auto it = e->cmap.find(flow_id);
+    if (it == e->cmap.end()) return fail(SG_ENOTFOUND, "no cluster flow rule with this flowId");
+    e->cflows[it->second].connected = connected;
+    HIPCHK(hipMemcpy(&e->d_cflow[it->second].connected, &connected, sizeof(int32_t), hipMemcpyHostToDevice));
+    return SG_OK;
 }
 
+// Batched DefaultTokenService.requestToken (see cluster.hip for the device steps).
 int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out) {
-    (void)reqs; (void)n; (void)out;
-    if (!e) return fail(SG_EINVAL, "null engine");
-    return fail(SG_ENOTSUP, "token server is not on the device path yet");
+    if (!e || (n && (!reqs || !out))) return fail(SG_EINVAL, "null argument");
+    if (!n) return SG_OK;
+    if (n > 0x7FFFFFFFull) return fail(SG_EINVAL, "too many token requests in one call");
+    hipStream_t st = e->stream;
+    int rc = ensure_batch(e, n);  // radix-sort scratch
+    if (rc) return rc;
+    if (n > e->tcap) {
+        dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
+        uint64_t c = std::max<uint64_t>(n, 1u << 16);
+        HIPCHK(hipMalloc(&e->d_treq, c * sizeof(sg_token_req)));
+        HIPCHK(hipMalloc(&e->d_tres, c * sizeof(sg_token_result)));
+        HIPCHK(hipMalloc(&e->d_tfidx, c * 4));
+        e->tcap = c;
+    }
+    if (!e->d_nslim) {
+        HIPCHK(hipMalloc(&e->d_nslim, sizeof(NsLimiter)));
+        NsLimiter z;
+        for (int k = 0; k < NS_BUCKETS; ++k) { z.ws[k] = -1; z.cnt[k] = 0; }
+        HIPCHK(hipMemcpy(e->d_nslim, &z, sizeof(z), hipMemcpyHostToDevice));
+    }
+    if (!e->d_ctab) {  // no cluster rule loaded yet: an empty table
+        CSlot t[16];
+        for (auto& x : t) { x.key = 0; x.idx = 0xFFFFFFFFu; x.pad = 0; }
+        HIPCHK(hipMalloc(&e->d_ctab, sizeof(t)));
+        HIPCHK(hipMemcpy(e->d_ctab, t, sizeof(t), hipMemcpyHostToDevice));
+        e->ctab_mask = 15;
+    }
+    const uint32_t nflows = (uint32_t)e->cflows.size();
+    HIPCHK(hipMemcpyAsync(e->d_treq, reqs, n * sizeof(sg_token_req), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(e->d_small, 0, 4, st));
+    HIPCHK(launch_tok_classify(e->d_treq, n, e->d_ctab, e->ctab_mask, e->d_tfidx, e->d_tres, e->d_small, st));
+    uint32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, e->d_small, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flags & 1) return fail(SG_EINVAL, "token requests must be ordered by ts (the replay clock)");
+    // GlobalRequestLimiter: a negative qpsAllowed stands for "no limiter registered" (tryPass -> true)
+    const double allowed = e->cfg.cluster_max_allowed_qps < 0 ? 1.0 / 0.0 : (double)e->cfg.cluster_max_allowed_qps;
+    HIPCHK(launch_tok_limiter(e->d_treq, n, e->d_tfidx, nflows, e->d_nslim, allowed, e->d_k0, e->d_v0, e->d_tres, st));
+    if (nflows) {
+        int bits = 1;
+        while (bits < 32 && (1ull << bits) <= nflows) ++bits;  // keys 0..nflows (nflows = not for a flow)
+        const int passes = (bits + 7) / 8;
+        const uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
+        uint32_t *kin = e->d_k0, *vin = e->d_v0, *kout = e->d_k1, *vout = e->d_v1;
+        for (int p = 0; p < passes; ++p) {
+            HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
+            HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, st));
+            HIPCHK(launch_radix_scatter(kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout, nullptr, st));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        HIPCHK(launch_tok_flow(kin, vin, n, e->d_treq, e->d_cflow, nflows, e->d_cbkt, e->cfg.cluster_exceed_count,
+                               e->cfg.cluster_max_occupy_ratio, e->d_tres, st));
+    }
+    HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return SG_OK;
 }
 
 } // extern "C"

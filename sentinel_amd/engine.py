@@ -175,3 +175,22 @@ class Engine:
         n = C.c_uint64()
         _check(lib().sg_snapshot_metrics(self.h, int(now), out.ctypes.data, cap, C.byref(n)))
         return out[: min(cap, n.value)]
+
+    # ---- token server (sg_cluster_*; DefaultTokenService.requestToken, csrv/flow/DefaultTokenService.java:37-48)
+    def cluster_set_connected(self, flow_id: int, n: int):
+        _check(lib().sg_cluster_set_connected_count(self.h, int(flow_id), int(n)))
+
+    def cluster_request_array(self, reqs: np.ndarray) -> np.ndarray:
+        """reqs: A.TOKEN_REQ_DTYPE array (time-ordered) -> A.TOKEN_RES_DTYPE array."""
+        reqs = np.ascontiguousarray(reqs, dtype=A.TOKEN_REQ_DTYPE)
+        out = np.zeros(len(reqs), dtype=A.TOKEN_RES_DTYPE)
+        _check(lib().sg_cluster_request_tokens(self.h, reqs.ctypes.data, len(reqs), out.ctypes.data))
+        return out
+
+    def cluster_request(self, reqs):
+        """reqs: list of (ts, flow_id, acquire, prioritized) -> list of (status, remaining, wait)."""
+        arr = np.zeros(len(reqs), dtype=A.TOKEN_REQ_DTYPE)
+        for i, (ts, fid, acq, pr) in enumerate(reqs):
+            arr[i] = (ts, fid, acq, int(pr))
+        out = self.cluster_request_array(arr)
+        return [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in out]

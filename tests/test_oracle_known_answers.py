@@ -498,3 +498,69 @@ def test_token_service_bad_request_and_no_rule():
     assert o.cluster_request([(T0, 0, 1, False)])[0][0] == A.TOKEN_BAD_REQUEST
     assert o.cluster_request([(T0, 5, 0, False)])[0][0] == A.TOKEN_BAD_REQUEST
     assert o.cluster_request([(T0, 5, 1, False)])[0][0] == A.TOKEN_NO_RULE_EXISTS
+
+
+def _cluster_rule(fid, count, **kw):
+    kw.setdefault("cluster_threshold_type", A.CLUSTER_THRESHOLD_GLOBAL)
+    return A.flow_rule("abc", count, cluster_mode=True, cluster_flow_id=fid, **kw)
+
+
+def test_cluster_rule_map_last_rule_wins_and_metric_kept():
+    # ClusterFlowRuleManager.applyClusterFlowRule (csrv/flow/rule/ClusterFlowRuleManager.java:323-363):
+    # list order, ruleMap.put -> the later rule of a flowId wins; putMetricIfAbsent keeps the metric
+    o = O.Oracle()
+    o.register("abc")
+    o.load_flow_rules([_cluster_rule(7, 2), _cluster_rule(7, 3)])
+    t = T0 - T0 % 1000
+    st = [s for s, _, _ in o.cluster_request([(t, 7, 1, False)] * 4)]
+    assert st == [A.TOKEN_OK] * 3 + [A.TOKEN_BLOCKED]
+    # a new list with count 5 and another window shape: the metric (3 passes, 10 x 100 ms) stays
+    o.load_flow_rules([_cluster_rule(7, 5, cluster_sample_count=2)])
+    st = [s for s, _, _ in o.cluster_request([(t + 10, 7, 1, False)] * 3)]
+    assert st == [A.TOKEN_OK, A.TOKEN_OK, A.TOKEN_BLOCKED]
+    # remaining = (int)(threshold - passQps - acquire)
+    o.load_flow_rules([_cluster_rule(7, 9.5)])
+    assert o.cluster_request([(t + 20, 7, 2, False)])[0] == (A.TOKEN_OK, 2, 0)
+
+
+def test_cluster_dropped_flow_id_and_fresh_metric():
+    o = O.Oracle()
+    o.register("abc")
+    o.load_flow_rules([_cluster_rule(7, 1), _cluster_rule(8, 1)])
+    t = T0 - T0 % 1000
+    assert [s for s, _, _ in o.cluster_request([(t, 7, 1, False), (t, 7, 1, False)])] == [A.TOKEN_OK, A.TOKEN_BLOCKED]
+    o.load_flow_rules([_cluster_rule(8, 1)])  # clearAndResetRulesConditional drops flowId 7
+    assert o.cluster_request([(t + 1, 7, 1, False)])[0][0] == A.TOKEN_NO_RULE_EXISTS
+    o.load_flow_rules([_cluster_rule(7, 1), _cluster_rule(8, 1)])  # a fresh metric
+    assert o.cluster_request([(t + 2, 7, 1, False)])[0][0] == A.TOKEN_OK
+
+
+def test_global_request_limiter():
+    # RequestLimiter.tryPass (csrv/flow/statistic/limit/RequestLimiter.java:72-87): qps + 1 <= allowed over
+    # 10 x 100 ms; requests refused here never reach the flow's metric
+    o = O.Oracle(cluster_max_allowed_qps=3)
+    o.register("abc")
+    o.load_flow_rules([_cluster_rule(7, 100)])
+    t = T0 - T0 % 1000
+    st = [s for s, _, _ in o.cluster_request([(t, 7, 1, False)] * 5)]
+    assert st == [A.TOKEN_OK] * 3 + [A.TOKEN_TOO_MANY_REQUEST] * 2
+    st = [s for s, _, _ in o.cluster_request([(t + 999, 7, 1, False), (t + 1000, 7, 1, False)])]
+    assert st == [A.TOKEN_TOO_MANY_REQUEST, A.TOKEN_OK]
+    # BAD_REQUEST / NO_RULE_EXISTS are answered before the limiter and do not consume it
+    o2 = O.Oracle(cluster_max_allowed_qps=1)
+    o2.register("abc")
+    o2.load_flow_rules([_cluster_rule(7, 100)])
+    st = [s for s, _, _ in o2.cluster_request([(t, 9, 1, False), (t, 7, 0, False), (t, 7, 1, False)])]
+    assert st == [A.TOKEN_NO_RULE_EXISTS, A.TOKEN_BAD_REQUEST, A.TOKEN_OK]
+
+
+def test_cluster_avg_local_threshold():
+    # calcGlobalThreshold: AVG_LOCAL -> count * connectedCount (csrv/flow/ClusterFlowChecker.java:38-48)
+    o = O.Oracle()
+    o.register("abc")
+    o.load_flow_rules([_cluster_rule(7, 2, cluster_threshold_type=A.CLUSTER_THRESHOLD_AVG_LOCAL)])
+    t = T0 - T0 % 1000
+    assert o.cluster_request([(t, 7, 1, False)])[0][0] == A.TOKEN_BLOCKED  # no client connected
+    assert o.cluster_set_connected(7, 3) == 0
+    st = [s for s, _, _ in o.cluster_request([(t, 7, 1, False)] * 7)]
+    assert st == [A.TOKEN_OK] * 6 + [A.TOKEN_BLOCKED]
