@@ -1,0 +1,153 @@
+"""Multi-process paths of sentinel_amd.dist on gloo, world size 2.
+
+CPU: resource sharding, the MetricNode all-gather and token routing to the server rank, with the
+oracle deciding at the server.  GPU (-m gpu): the same routing with the HIP token server on cuda:0
+behind rank 0 (rank 1 stays on the CPU), so the device path is what the ranks exchange with.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+T0 = 1_700_000_000_000
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    for p in (ROOT, os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    return dist
+
+
+def _cluster_rules(A, fids):
+    return [A.flow_rule("r%d" % f, float(5 + (f * 37) % 30), cluster_mode=True, cluster_flow_id=f,
+                        cluster_threshold_type=A.CLUSTER_THRESHOLD_GLOBAL, cluster_sample_count=5)
+            for f in fids]
+
+
+PLAN = [[300, 250], [0, 120]]  # PLAN[round][rank]: batch sizes (an empty batch on rank 0 in round 1)
+
+
+def _batch(A, rank, rnd):
+    n = PLAN[rnd][rank]
+    rng = np.random.default_rng(1000 * rnd + 7 + rank)
+    out = np.zeros(n, dtype=A.TOKEN_REQ_DTYPE)
+    out["ts"] = T0 + 10_000 * rnd + np.cumsum(rng.integers(0, 12, n))  # > 1 s: the window head fills
+    out["flow_id"] = rng.integers(11, 19, n)
+    out["acquire_count"] = 1  # PASS tokens == PASS_REQUEST: the occupy path (SHOULD_WAIT) is reachable
+    out["prioritized"] = rng.random(n) < 0.25
+    return out
+
+
+def _oracle_decider(O, A, fids, **cfg):
+    o = O.Oracle(**cfg)
+    o.load_flow_rules(_cluster_rules(A, fids))
+
+    def decide(q):
+        r = o.cluster_request([tuple(int(v) for v in x) for x in q])
+        out = np.zeros(len(q), dtype=A.TOKEN_RES_DTYPE)
+        for i, (s, rem, w) in enumerate(r):
+            out[i] = (s, rem, w, 0)
+        return out
+    return decide
+
+
+def _w_tokens(rank, world, port, use_gpu):
+    dist = _init(rank, world, port)
+    import pyoracle as O
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    fids = list(range(11, 19))
+    decide = None
+    if rank == 0:
+        if use_gpu:
+            from sentinel_amd import engine as E
+            eng = E.Engine(max_resources=64, cluster_max_allowed_qps=250)
+            eng.load_flow_rules(_cluster_rules(A, fids))
+            decide = eng.cluster_request_array
+        else:
+            decide = _oracle_decider(O, A, fids, cluster_max_allowed_qps=250)
+    ref = _oracle_decider(O, A, fids, cluster_max_allowed_qps=250)  # one server on the merged stream
+    seen = {s: 0 for s in (A.TOKEN_OK, A.TOKEN_BLOCKED, A.TOKEN_SHOULD_WAIT, A.TOKEN_TOO_MANY_REQUEST)}
+    for rnd in range(len(PLAN)):
+        got = D.request_tokens(_batch(A, rank, rnd), decide)
+        allq = [_batch(A, r, rnd) for r in range(world)]
+        cat = np.concatenate(allq)
+        src = np.concatenate([np.full(len(q), r) for r, q in enumerate(allq)])
+        loc = np.concatenate([np.arange(len(q)) for q in allq])
+        order = np.lexsort((loc, src, cat["ts"]))
+        res = np.zeros(len(cat), dtype=A.TOKEN_RES_DTYPE)
+        res[order] = ref(cat[order])
+        off = sum(len(q) for q in allq[:rank])
+        assert np.array_equal(got, res[off: off + len(got)]), (rank, rnd)
+        for s in res["status"]:
+            seen[int(s)] = seen.get(int(s), 0) + 1
+    assert all(v > 0 for v in seen.values()), seen  # every outcome is exercised by the merged stream
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _w_metrics(rank, world, port):
+    dist = _init(rank, world, port)
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    n = [3, 0][rank]
+    rows = np.zeros(n, dtype=A.METRIC_NODE_DTYPE)
+    rows["timestamp"] = T0 + 1000 * np.arange(n)
+    rows["res_id"] = 10 + np.arange(n)
+    rows["pass_qps"] = 100 + rank
+    g = D.gather_metrics(rows)
+    assert len(g) == 3 and (g["reserved"] == 0).all()
+    rows2 = np.zeros(2 + rank, dtype=A.METRIC_NODE_DTYPE)
+    rows2["timestamp"] = T0
+    rows2["res_id"] = np.arange(2 + rank)[::-1]
+    rows2["pass_qps"] = rank
+    g = D.gather_metrics(rows2)
+    assert len(g) == 5
+    assert list(g["reserved"]) == [0, 0, 1, 1, 1] and list(g["res_id"]) == [0, 1, 0, 1, 2]
+    assert list(g["pass_qps"]) == [0, 0, 1, 1, 1]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_and_route_events():
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    rng = np.random.default_rng(3)
+    ev = np.zeros(5000, dtype=A.EVENT_DTYPE)
+    ev["ts"] = T0 + np.sort(rng.integers(0, 10_000, len(ev)))
+    ev["res_id"] = rng.integers(0, 1000, len(ev))
+    parts, pos = D.route_events(ev, 4)
+    assert sorted(np.concatenate(pos).tolist()) == list(range(len(ev)))
+    for r, (p, q) in enumerate(zip(parts, pos)):
+        assert (D.shard_of(p["res_id"], 4) == r).all()
+        assert (np.diff(q) > 0).all() and (np.diff(p["ts"]) >= 0).all()
+    # splitmix64 known values (Vigna's reference generator, state 0 -> first output)
+    assert int(D.splitmix64(0)) == 0xE220A8397B1DCDAF
+
+
+def test_gather_metrics_gloo():
+    mp.spawn(_w_metrics, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_request_tokens_gloo():
+    mp.spawn(_w_tokens, args=(2, _port(), False), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
+def test_request_tokens_gpu_server():
+    mp.spawn(_w_tokens, args=(2, _port(), True), nprocs=2, join=True)
