@@ -76,6 +76,7 @@ struct Node {
     uint32_t flags;      // NI_*
     int64_t exc_sum_sec; // see NodeInfo
     int64_t exc_sum;
+    int64_t* bor;        // borrow ring {ws, pass} x 2 in HBM when NI_BORROW, else null
 };
 
 __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t res) {
@@ -88,6 +89,7 @@ __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t r
     N.exc_sum = ni.exc_sum;
     N.mslot = -1;
     N.mst = 0;
+    N.bor = (ni.flags & NI_BORROW) && S.borrow ? S.borrow + (uint64_t)res * 4 : nullptr;
 }
 
 __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
@@ -97,16 +99,31 @@ __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
 // LeapArray.currentWindow for the 2-bucket second window (core/slots/statistic/base/LeapArray.java:117-208):
 // returns the slot, or -1 for a detached bucket (clock went back: the update is lost).
 // Explicit branches keep sb[] in registers (a runtime index would force it to scratch).
+// With a live borrow ring (NI_BORROW) a new or reset bucket starts with the pass the borrow bucket of
+// t holds (OccupiableBucketLeapArray.newEmptyBucket copies every event, resetWindowTo the pass only,
+// OccupiableBucketLeapArray.java:39-64 -- the borrow bucket only ever holds pass, so both are this).
+__device__ __forceinline__ void bkt_borrow(Bkt& b, const int64_t* bor, int slot, int64_t t) {
+    const int64_t bws = bor[2 * slot];
+    if (bws >= 0 && bws <= t && t < bws + 500) b.pass = bor[2 * slot + 1];  // getWindowValue(t)
+}
 __device__ __forceinline__ int sec_current(Node& N, int64_t t, int32_t max_rt) {
     int slot = (int)((t / 500) & 1);
     int64_t ws = t - t % 500;
     if (slot == 0) {
         if (N.sb[0].ws == ws) return 0;
-        if (N.sb[0].ws < ws) { bkt_reset(N.sb[0], ws, max_rt); return 0; }
+        if (N.sb[0].ws < ws) {
+            bkt_reset(N.sb[0], ws, max_rt);
+            if (N.bor) bkt_borrow(N.sb[0], N.bor, 0, t);
+            return 0;
+        }
         return -1;
     }
     if (N.sb[1].ws == ws) return 1;
-    if (N.sb[1].ws < ws) { bkt_reset(N.sb[1], ws, max_rt); return 1; }
+    if (N.sb[1].ws < ws) {
+        bkt_reset(N.sb[1], ws, max_rt);
+        if (N.bor) bkt_borrow(N.sb[1], N.bor, 1, t);
+        return 1;
+    }
     return -1;
 }
 __device__ __forceinline__ void bkt_add(Bkt& b, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE, int64_t mrt) {
@@ -307,6 +324,77 @@ __device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DRule&
     s.a = 1;
     s.c = t + (int64_t)r.time_window * 1000;
     return false;
+}
+
+// ---------------------------------------------------------------- prioritized entries (k_lane only)
+// FutureBucketLeapArray.currentWindow(t) on the borrow ring (LeapArray.java:117-208): slot, or -1
+// for a detached bucket (t before the slot's window)
+__device__ __forceinline__ int bor_current(int64_t* bor, int64_t t) {
+    const int slot = (int)((t / 500) & 1);
+    const int64_t ws = t - t % 500;
+    const int64_t old = bor[2 * slot];
+    if (old < 0 || ws > old) { bor[2 * slot] = ws; bor[2 * slot + 1] = 0; return slot; }
+    return ws == old ? slot : -1;
+}
+// OccupiableBucketLeapArray.currentWaiting: future buckets only (FutureBucketLeapArray.isWindowDeprecated
+// is t >= windowStart, FutureBucketLeapArray.java:48-52)
+__device__ __forceinline__ int64_t bor_waiting(int64_t* bor, int64_t t) {
+    bor_current(bor, t);
+    int64_t s = 0;
+    if (bor[0] >= 0 && !(t >= bor[0])) s += bor[1];
+    if (bor[2] >= 0 && !(t >= bor[2])) s += bor[3];
+    return s;
+}
+// ArrayMetric.getWindowPass(t) of the second window: the bucket whose window holds t (LeapArray.getWindowValue)
+__device__ __forceinline__ int64_t sec_window_pass(const Node& N, int64_t t) {
+    if (t < 0) return 0;
+    const Bkt& b = ((t / 500) & 1) ? N.sb[1] : N.sb[0];
+    if (b.ws < 0 || !(b.ws <= t && t < b.ws + 500)) return 0;
+    return b.pass;
+}
+// StatisticNode.tryOccupyNext (core/node/StatisticNode.java:293-325); INTERVAL = 1000, 2 buckets
+__device__ __forceinline__ int64_t try_occupy_next(Node& N, const Ctx& C, int64_t now, int acquire, double threshold,
+                                                   int32_t occupy_timeout) {
+    const double max_count = threshold * 1000 / 1000;
+    const int64_t cur_borrow = bor_waiting(N.bor, now);
+    if ((double)cur_borrow >= max_count) return occupy_timeout;
+    const int64_t wlen = 500;
+    int64_t earliest = now - now % wlen + wlen - 1000;
+    int64_t idx = 0;
+    sec_current(N, now, C.max_rt);
+    int64_t cur_pass = SEC_SUM(N, now, pass);
+    while (earliest < now) {
+        const int64_t wait = idx * wlen + wlen - now % wlen;
+        if (wait >= occupy_timeout) break;
+        const int64_t wp = sec_window_pass(N, earliest);
+        if ((double)(cur_pass + cur_borrow + acquire - wp) <= max_count) return wait;
+        earliest += wlen;
+        cur_pass -= wp;
+        ++idx;
+    }
+    return occupy_timeout;
+}
+// DefaultController.canPass with prioritized = true (DefaultController.java:49-81): 1 pass, 0 block,
+// 2 PriorityWaitException after addWaitingRequest + addOccupiedPass (wait = waitInMs)
+__device__ __forceinline__ int default_can_pass_prio(Node& N, const Ctx& C, const DRule& r, int64_t t, int acquire,
+                                                     int32_t occupy_timeout, int64_t& wait) {
+    int32_t cur;
+    if (r.grade == SG_FLOW_GRADE_THREAD) cur = N.thread;
+    else { sec_current(N, t, C.max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
+    if (!((double)j_iadd(cur, acquire) > r.count)) return 1;
+    if (r.grade != SG_FLOW_GRADE_QPS || !N.bor) return 0;
+    const int64_t w = try_occupy_next(N, C, t, acquire, r.count, occupy_timeout);
+    if (w >= occupy_timeout) return 0;
+    const int bs = bor_current(N.bor, t + w);  // addWaitingRequest: borrowArray.currentWindow(t + wait).addPass
+    if (bs >= 0) N.bor[2 * bs + 1] += acquire;
+    min_current(N, C.minb, t, C.max_rt, C.pflags);  // addOccupiedPass: minute window OCCUPIED_PASS + PASS
+    if (!(N.mst & MS_DETACHED)) {
+        N.mb.occ += acquire;
+        N.mb.pass += acquire;
+        N.mst |= MS_DIRTY;
+    }
+    wait = w;
+    return 2;
 }
 
 // StatisticSlot.entry bookkeeping after the checks (core/slots/statistic/StatisticSlot.java:54-133)

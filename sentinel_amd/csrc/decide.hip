@@ -65,7 +65,8 @@ __global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
 __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n,
-                                                 const Prog* __restrict__ prog, uint32_t lane_max, uint32_t j1_max,
+                                                 const Prog* __restrict__ prog, const NodeInfo* __restrict__ info,
+                                                 uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
                                                  uint32_t nblk) {
     __shared__ uint32_t cnt[N_BINS];
@@ -78,7 +79,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
         sg.len = end - sg.start;
         const Prog p = prog[sg.res];
         const int nr = p.n_param + p.n_flow + p.n_degrade;
-        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max;
+        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
+                          !(info[sg.res].flags & NI_BORROW);
         uint32_t bin;
         if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
@@ -305,11 +307,22 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                     else wait += w;
                 }
             } else if (s < nfl) {  // FlowSlot.checkFlow (FlowSlot.java:146-158)
-                if (!flow_can_pass(N, C, r, rs[s], t, cnt, wait)) { status = ST_BLOCK_FLOW; slot = r.slot; }
+                if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
+                    int64_t w = 0;
+                    const int rc = default_can_pass_prio(N, C, r, t, cnt, cfg.occupy_timeout, w);
+                    if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
+                    else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }  // PriorityWaitException
+                } else if (!flow_can_pass(N, C, r, rs[s], t, cnt, wait)) { status = ST_BLOCK_FLOW; slot = r.slot; }
             } else {  // DegradeRuleManager.checkDegrade (DegradeRuleManager.java:72-85)
                 if (!degrade_pass(N, C, r, rs[s], t)) { status = ST_BLOCK_DEGRADE; slot = r.slot; }
             }
         }
+    }
+    if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
+        N.thread++;
+        if ((N.flags & NI_PM) && (N.flags & NI_TM0) && (fl & SG_F_HAS_ARG))
+            thread_count_add(S, cfg, res, pg.tc_epoch, arg, 1, bflags);
+        return mk_dec(ST_PASS_WAIT, slot, wait);
     }
     const bool passed = status == ST_PASS;
     stat_entry(N, C, t, cnt, passed);
@@ -1211,11 +1224,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
     hipLaunchKernelGGL(k_seg_start, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs);
     return hipGetLastError();
 }
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const NodeInfo* info, uint32_t lane_max,
+                          uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st) {
     if (!m) return hipSuccess;
     const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, lane_max, j1_max, j4_max, force_lane,
+    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, info, lane_max, j1_max, j4_max, force_lane,
                        blkcnt, nblk);
     return hipGetLastError();
 }

@@ -34,6 +34,8 @@ enum : uint32_t {
     NI_REJECTED = 2u,    // lookProcessChain returned null once the cap was reached
     NI_PM = 4u,          // ParamFlowSlot.metricsMap has a ParameterMetric for it
     NI_TM0 = 8u,         // ... with a thread-count map for paramIdx 0
+    NI_BORROW = 16u,     // a prioritized ENTRY was seen: the second window's borrow ring
+                         // (OccupiableBucketLeapArray.borrowArray) is live; decided by k_lane only
 };
 
 struct NodeInfo {
@@ -165,6 +167,7 @@ struct NsLimiter {
 
 struct DevState {
     Bkt* sec;
+    int64_t* borrow;          // [res][2 slots] x {ws, pass}: FutureBucketLeapArray of the second window
     Bkt* minb;
     NodeInfo* info;
     const Prog* prog;

@@ -23,7 +23,8 @@ namespace sg {
 // kernels.hip
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, hipStream_t st);
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, NodeInfo* info,
+                           hipStream_t st);
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
@@ -32,13 +33,14 @@ uint32_t radix_tile();
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                            sg_metric_node*, uint64_t, hipStream_t);
-hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, uint32_t nres, hipStream_t st);
+hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borrow, uint32_t nres, hipStream_t st);
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st);
 // decide.hip
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, uint32_t lane_max, uint32_t j1_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const NodeInfo* info, uint32_t lane_max,
+                          uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st);
 hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
                             hipStream_t st);
@@ -434,6 +436,7 @@ struct sg_engine {
     //          [64..64+N_BINS) bin cursors
     uint32_t* d_small = nullptr;
     uint32_t* d_sink = nullptr;  // 1024 words, DevState.sink
+    int64_t* d_borrow = nullptr;  // [res][2]{ws, pass}: second-window borrow rings (prioritized entries)
     uint64_t* d_cand = nullptr;
     uint32_t dbg_flags = 0;
     unsigned long long* d_dbg = nullptr;  // SG_DEBUG=1: [0..63] counters of the J16 bin
@@ -737,12 +740,12 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
         hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
         hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
-        hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess)
+        hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
-        launch_init_state(e->d_sec, e->d_minb, e->d_info, (uint32_t)R, e->stream) != hipSuccess ||
+        launch_init_state(e->d_sec, e->d_minb, e->d_info, e->d_borrow, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
     for (auto& s : e->bin_stream)
@@ -781,7 +784,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
     dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
-    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim);
+    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -1138,7 +1141,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(hipMemsetAsync(e->d_small, 0, 256 * 4, st));
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_small + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, st));
+                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, e->d_info, st));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
         if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
@@ -1163,13 +1166,11 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
     if (bflags & BF_TSPAN) return fail(SG_EINVAL, "a batch must span less than 2^31 ms");
     if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
-    if (bflags & BF_PRIORITIZED)
-        return fail(SG_ENOTSUP, "prioritized entries (StatisticNode.tryOccupyNext) are not on the device path yet");
     if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
     const uint32_t nblk = (m + 255) / 256;
-    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
+    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->d_info, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
                           e->d_blkcnt, st));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, st));
     HIPCHK(launch_seg_order(e->d_segs, m, e->d_blkcnt, e->d_order, e->d_small + 8, st));
@@ -1226,6 +1227,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.ptab = e->d_ptab;
     S.ring = e->d_ring;
     S.sink = e->d_sink;
+    S.borrow = e->d_borrow;
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
     for (int k = 0; k < 3; ++k) {
@@ -1291,7 +1293,9 @@ int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out)
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     Bkt sec[2], mb[60];
+    int64_t bor[4];
     NodeInfo ni;
+    HIPCHK(hipMemcpy(bor, e->d_borrow + (uint64_t)res * 4, sizeof(bor), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sec, e->d_sec + (uint64_t)res * 2, sizeof(sec), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(mb, e->d_minb + (uint64_t)res * 60, sizeof(mb), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&ni, e->d_info + res, sizeof(ni), hipMemcpyDeviceToHost));
@@ -1307,6 +1311,12 @@ int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out)
         ex(sec[0], out->second[0]);
         ex(sec[1], out->second[1]);
         for (int i = 0; i < 60; ++i) ex(mb[i], out->minute[i]);
+        for (int i = 0; i < 2; ++i)  // FutureBucketLeapArray buckets: pass only (min_rt as created)
+            if (bor[2 * i] >= 0) {
+                out->borrow[i].window_start = bor[2 * i];
+                out->borrow[i].pass = bor[2 * i + 1];
+                out->borrow[i].min_rt = e->cfg.statistic_max_rt;
+            }
     } else {
         for (int i = 0; i < 60; ++i) out->minute[i].window_start = -1;
     }

@@ -37,7 +37,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                                                       uint64_t ring_mask, int32_t max_rt, SEv* __restrict__ rec_o,
                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                       uint32_t* __restrict__ ghist, uint32_t nblocks,
-                                                      uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out) {
+                                                      uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out,
+                                                      NodeInfo* __restrict__ info) {
     __shared__ uint32_t h[RS_BINS];
     for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
     __syncthreads();
@@ -63,7 +64,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         r.code = RC_NONE;
         r.pad = 0;
         if (e.kind == SG_EV_ENTRY) {
-            if (e.flags & SG_F_PRIORITIZED) fl |= BF_PRIORITIZED;
+            // a prioritized ENTRY makes the resource's borrow ring live: its segments go to k_lane
+            if ((e.flags & SG_F_PRIORITIZED) && e.res_id < max_res && !(info[e.res_id].flags & NI_BORROW))
+                atomicOr(&info[e.res_id].flags, NI_BORROW);
         } else {
             if (e.kind == SG_EV_EXIT) {
                 if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
@@ -295,12 +298,17 @@ __global__ void k_snap_emit(const Bkt* __restrict__ minb, NodeInfo* __restrict__
 // =================================================================================
 // state initialisation / flag updates
 // =================================================================================
-__global__ void k_init_state(Bkt* __restrict__ sec, Bkt* __restrict__ minb, NodeInfo* __restrict__ info, uint32_t nres) {
+__global__ void k_init_state(Bkt* __restrict__ sec, Bkt* __restrict__ minb, NodeInfo* __restrict__ info,
+                             int64_t* __restrict__ borrow, uint32_t nres) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     Bkt z;
     z.ws = -1; z.pass = 0; z.block = 0; z.exc = 0; z.succ = 0; z.rt = 0; z.occ = 0; z.minrt = 0;
     if (i < (uint64_t)nres * 60) minb[i] = z;
-    if (i < (uint64_t)nres * 2) sec[i] = z;
+    if (i < (uint64_t)nres * 2) {
+        sec[i] = z;
+        borrow[2 * i] = -1;  // borrow slot never created
+        borrow[2 * i + 1] = 0;
+    }
     if (i < nres) {
         NodeInfo n;
         n.thread = 0; n.flags = 0; n.exc_sum_sec = -1; n.exc_sum = 0; n.last_fetch = -1;
@@ -325,9 +333,10 @@ namespace sg {
 
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, hipStream_t st) {
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, NodeInfo* info,
+                           hipStream_t st) {
     hipLaunchKernelGGL(k_rs_first, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask, max_rt,
-                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out);
+                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, info);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
@@ -343,9 +352,9 @@ hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64
 }
 uint32_t radix_tile() { return RS_TILE; }
 
-hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, uint32_t nres, hipStream_t st) {
+hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borrow, uint32_t nres, hipStream_t st) {
     uint64_t tot = (uint64_t)nres * 60;
-    hipLaunchKernelGGL(k_init_state, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, sec, minb, info, nres);
+    hipLaunchKernelGGL(k_init_state, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, st, sec, minb, info, borrow, nres);
     return hipGetLastError();
 }
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st) {

@@ -225,3 +225,42 @@ def test_snapshot_matches_oracle():
         so = orc.snapshot(now)
         key = lambda a: np.lexsort((a["timestamp"], a["res_id"]))
         np.testing.assert_array_equal(sg[key(sg)], so[key(so)])
+
+
+# ---------------------------------------------------------------- prioritized entries (A11/A12)
+def _run_prioritized(config, frac, batches, **kw):
+    """A workload with a fraction of its ENTRYs prioritized: DefaultController.canPass ->
+    StatisticNode.tryOccupyNext / addWaitingRequest / addOccupiedPass -> PriorityWaitException
+    (core/slots/block/flow/controller/DefaultController.java:49-81, core/node/StatisticNode.java:293-341),
+    with the OccupiableBucketLeapArray borrow transfer on window creation and reset (Q6)."""
+    w = T.Workload(config, **kw)
+    ev = w.events
+    rng = np.random.default_rng(11 + config)
+    ent = ev["kind"] == A.EV_ENTRY
+    pick = ent & (rng.random(len(ev)) < frac)
+    ev["flags"] = np.where(pick, ev["flags"] | A.F_PRIORITIZED, ev["flags"])
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    dg, do = _replay(w, eng, orc, batches)
+    _assert_same_decisions(dg, do, ev)
+    res = _sample(w)
+    _compare_nodes(w, eng, orc, res)
+    for r in res:
+        np.testing.assert_array_equal(eng.read_node(int(r))["borrow"][:2], orc.read_node(int(r))["borrow"][:2],
+                                      err_msg="borrow ring of res %d" % r)
+    return dg, w  # w owns the event buffer
+
+
+def test_prioritized_flowqps(bin_mode):
+    dg, w = _run_prioritized(1, 0.3, 4)
+    ent = w.events["kind"] == A.EV_ENTRY
+    st = dg[ent] & 0xFF
+    assert (st == A.PASS_WAIT).sum() > 0  # the occupy path is exercised
+    wait = dg[ent][st == A.PASS_WAIT] >> 16
+    assert (wait > 0).all() and (wait < 500).all()
+
+
+def test_prioritized_zipf(bin_mode):
+    _run_prioritized(2, 0.2, 3, n_entries=200_000)
