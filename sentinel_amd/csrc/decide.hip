@@ -381,8 +381,21 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
                 else eff = rel < 64 ? ((pm >> rel) & 1) != 0 : st_passed(dec[r.x] & 0xFF);
             }
             if (eff) {
-                if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
-                else stat_trace(N, C, t, r.cnt);
+                if (r.kind == SG_EV_EXIT) {
+                    stat_exit(N, C, t, r.cnt, r.rt);
+                    // exit(count, args): ParamFlowStatisticExitCallback.onExit -> ParameterMetric.decreaseThreadCount
+                    // with the ENTRY's args (param/slots/statistic/ParamFlowStatisticExitCallback.java:31-38, Q14)
+                    if ((r.flags & SG_F_EXIT_ARGS) && S.key_ring && (N.flags & NI_PM) && (N.flags & NI_TM0) &&
+                        r.code != RC_NONE) {
+                        const uint64_t ref = r.code == RC_BATCH
+                                                 ? S.gbase + (vals[r.x] & 0x7FFFFFFFu)
+                                                 : (ev[vals[sg.start + j] & 0x7FFFFFFFu].aux & SG_REF_NONE);
+                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
+                        if (key != NO_KEY) thread_count_add(S, cfg, res, pg.tc_epoch, key, -1, bflags);
+                    }
+                } else {
+                    stat_trace(N, C, t, r.cnt);
+                }
             }
         }
         dec[sg.start + j] = d;

@@ -29,6 +29,8 @@ struct Bkt {
 };
 static_assert(sizeof(Bkt) == 64, "Bkt must be 64 B");
 
+#define NO_KEY 0xFFFFFFFFFFFFFFFFull  // key-ring value of an ENTRY without an argument
+
 enum : uint32_t {
     NI_CHAIN = 1u,       // CtSph chainMap holds this resource (and its ClusterNode exists)
     NI_REJECTED = 2u,    // lookProcessChain returned null once the cap was reached
@@ -168,6 +170,9 @@ struct NsLimiter {
 struct DevState {
     Bkt* sec;
     int64_t* borrow;          // [res][2 slots] x {ws, pass}: FutureBucketLeapArray of the second window
+    uint64_t* key_ring;       // arg key of every ENTRY by global event index (ring like the status ring),
+                              // NO_KEY if it had none; null until param rules exist
+    uint64_t gbase;           // global index of the batch's first event
     Bkt* minb;
     NodeInfo* info;
     const Prog* prog;

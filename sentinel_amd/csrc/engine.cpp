@@ -24,7 +24,7 @@ namespace sg {
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, NodeInfo* info,
-                           hipStream_t st);
+                           uint64_t* key_ring, hipStream_t st);
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
@@ -437,6 +437,7 @@ struct sg_engine {
     uint32_t* d_small = nullptr;
     uint32_t* d_sink = nullptr;  // 1024 words, DevState.sink
     int64_t* d_borrow = nullptr;  // [res][2]{ws, pass}: second-window borrow rings (prioritized entries)
+    uint64_t* d_keyring = nullptr;  // ENTRY arg keys by global index (exit(count, args)); once param rules exist
     uint64_t* d_cand = nullptr;
     uint32_t dbg_flags = 0;
     unsigned long long* d_dbg = nullptr;  // SG_DEBUG=1: [0..63] counters of the J16 bin
@@ -784,7 +785,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
     dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
     dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
-    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow);
+    dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -1104,6 +1105,11 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     }
     e->last_par = keys;
     e->par_loaded = true;
+    if (!e->params.empty() && !e->d_keyring) {  // thread counts can exist from now on: remember ENTRY keys
+        const uint64_t nk = 1ull << e->cfg.status_ring_log2;
+        HIPCHK(hipMalloc(&e->d_keyring, nk * sizeof(uint64_t)));
+        HIPCHK(hipMemset(e->d_keyring, 0xFF, nk * sizeof(uint64_t)));  // NO_KEY
+    }
     if (n_loaded) *n_loaded = (uint32_t)e->params.size();
     return SG_OK;
 }
@@ -1141,7 +1147,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(hipMemsetAsync(e->d_small, 0, 256 * 4, st));
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_small + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, e->d_info, st));
+                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, e->d_info, e->d_keyring, st));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
         if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
@@ -1166,7 +1172,6 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
     if (bflags & BF_TSPAN) return fail(SG_EINVAL, "a batch must span less than 2^31 ms");
     if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
-    if (bflags & BF_EXIT_ARGS) return fail(SG_ENOTSUP, "Entry.exit(count, args) is not on the device path yet");
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
     const uint32_t nblk = (m + 255) / 256;
@@ -1228,6 +1233,8 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.ring = e->d_ring;
     S.sink = e->d_sink;
     S.borrow = e->d_borrow;
+    S.key_ring = e->d_keyring;
+    S.gbase = e->gbase;
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
     for (int k = 0; k < 3; ++k) {

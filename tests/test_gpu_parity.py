@@ -264,3 +264,29 @@ def test_prioritized_flowqps(bin_mode):
 
 def test_prioritized_zipf(bin_mode):
     _run_prioritized(2, 0.2, 3, n_entries=200_000)
+
+
+# ---------------------------------------------------------------- exit(count, args) (A25, Q14)
+def test_exit_with_args_thread_params(bin_mode):
+    """THREAD-grade param rules: onPass increments the value's thread count
+    (ParamFlowStatisticEntryCallback.java:33-40) and only exit(count, args) decrements it
+    (ParamFlowStatisticExitCallback.java:31-38, core/Entry.java:78-80), so with 70 % of the EXITs
+    carrying args the counts -- and the THREAD verdicts -- depend on the exits."""
+    w = T.Workload(5, n_entries=150_000, n_res=200, n_param_values=300)
+    ev = w.events
+    rng = np.random.default_rng(5)
+    ex = (ev["kind"] == A.EV_EXIT) & (rng.random(len(ev)) < 0.7)
+    ev["flags"] = np.where(ex, ev["flags"] | A.F_EXIT_ARGS, ev["flags"])
+    names = ["res-%d" % i for i in range(w.n_res)]
+    rules = [A.param_rule(nm, 0, 2 + i % 4, grade=A.FLOW_GRADE_THREAD) if i % 2 == 0 else
+             A.param_rule(nm, 0, 20 + i % 30) for i, nm in enumerate(names)]
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for x in (eng, orc):
+        w.install(x)
+        x.load_param_rules(rules)
+    dg, do = _replay(w, eng, orc, 3)
+    _assert_same_decisions(dg, do, ev)
+    _compare_nodes(w, eng, orc, _sample(w))
+    st = dg[ev["kind"] == A.EV_ENTRY] & 0xFF
+    assert (st == A.BLOCK_PARAM).sum() > 0 and (st == A.PASS).sum() > 0
