@@ -99,16 +99,21 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    stage_ms = []  # per timed step: [group, decide, post, total] device ms (HIP events, engine stream)
+    # Batches go through the engine's two-stage pipeline (sg_submit_async): the group stage of batch
+    # k+1 runs while batch k is being decided; sg_sync at the end of the timed region waits for the
+    # last decision.  Per-batch stage times come from HIP events on the engine's streams.
     for i in range(warmup):
-        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value)
+        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value, sync=False)
+    eng.sync()
+    eng.timing_log()
     barrier()
     t_start = time.perf_counter()
     for i in range(warmup, warmup + steps):
-        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value)
-        stage_ms.append(eng.timings())
+        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value, sync=False)
+    eng.sync()
     barrier()
     elapsed = time.perf_counter() - t_start
+    stage_ms = eng.timing_log()  # per timed step: [group, decide, post, total] device ms
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], device="cuda")

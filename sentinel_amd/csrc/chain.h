@@ -76,7 +76,7 @@ struct Node {
     uint32_t flags;      // NI_*
     int64_t exc_sum_sec; // see NodeInfo
     int64_t exc_sum;
-    int64_t* bor;        // borrow ring {ws, pass} x 2 in HBM when NI_BORROW, else null
+    int64_t* bor;        // borrow ring {ws, pass} x 2 in HBM once a prioritized ENTRY was seen, else null
 };
 
 __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t res) {
@@ -89,7 +89,7 @@ __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t r
     N.exc_sum = ni.exc_sum;
     N.mslot = -1;
     N.mst = 0;
-    N.bor = (ni.flags & NI_BORROW) && S.borrow ? S.borrow + (uint64_t)res * 4 : nullptr;
+    N.bor = S.prio && S.prio[res] ? S.borrow + (uint64_t)res * 4 : nullptr;
 }
 
 __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
@@ -99,7 +99,7 @@ __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
 // LeapArray.currentWindow for the 2-bucket second window (core/slots/statistic/base/LeapArray.java:117-208):
 // returns the slot, or -1 for a detached bucket (clock went back: the update is lost).
 // Explicit branches keep sb[] in registers (a runtime index would force it to scratch).
-// With a live borrow ring (NI_BORROW) a new or reset bucket starts with the pass the borrow bucket of
+// With a live borrow ring (DevState.prio) a new or reset bucket starts with the pass the borrow bucket of
 // t holds (OccupiableBucketLeapArray.newEmptyBucket copies every event, resetWindowTo the pass only,
 // OccupiableBucketLeapArray.java:39-64 -- the borrow bucket only ever holds pass, so both are this).
 __device__ __forceinline__ void bkt_borrow(Bkt& b, const int64_t* bor, int slot, int64_t t) {

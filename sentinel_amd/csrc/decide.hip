@@ -65,7 +65,7 @@ __global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
 __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n,
-                                                 const Prog* __restrict__ prog, const NodeInfo* __restrict__ info,
+                                                 const Prog* __restrict__ prog, const uint8_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
                                                  uint32_t nblk) {
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
         const Prog p = prog[sg.res];
         const int nr = p.n_param + p.n_flow + p.n_degrade;
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
-                          !(info[sg.res].flags & NI_BORROW);
+                          !prio[sg.res];
         uint32_t bin;
         if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
@@ -120,7 +120,8 @@ __global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, u
 // ENTRY).  A reference to a non-ENTRY resolves like an unknown entry in or_submit: an EXIT is then
 // taken as the caller asserting the entry passed, a TRACE as not counted.
 __global__ void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restrict__ vals, uint64_t n,
-                         const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs) {
+                         const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs, uint32_t* __restrict__ prev,
+                         uint32_t* __restrict__ nprev) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     SEv r = rec_o[vals[p] & 0x7FFFFFFFu];
@@ -128,8 +129,23 @@ __global__ void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restri
         const uint32_t po = pos_of[r.x];
         if (po & 0x80000000u) r.x = po & 0x7FFFFFFFu;
         else r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+    } else if (r.code == RC_PREV) {
+        prev[atomicAdd(nprev, 1u)] = (uint32_t)p;
     }
     recs[p] = r;
+}
+// references into earlier batches, once those are decided: the ENTRY's status from the ring
+// (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
+__global__ void k_resolve(const uint32_t* __restrict__ prev, uint32_t np, const uint8_t* __restrict__ ring,
+                          SEv* __restrict__ recs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    SEv r = recs[prev[i]];
+    const uint8_t st = ring[r.x];
+    if (st == ST_NOT_ENTRY) r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+    else r.code = (st == ST_PASS || st == ST_PASS_WAIT) ? RC_PASSED : RC_NOT;
+    r.x = 0;
+    recs[prev[i]] = r;
 }
 
 // decisions back to submission order; the status ring keeps every event's status for
@@ -1237,12 +1253,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
     hipLaunchKernelGGL(k_seg_start, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs);
     return hipGetLastError();
 }
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const NodeInfo* info, uint32_t lane_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint8_t* prio, uint32_t lane_max,
                           uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st) {
     if (!m) return hipSuccess;
     const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, info, lane_max, j1_max, j4_max, force_lane,
+    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
                        blkcnt, nblk);
     return hipGetLastError();
 }
@@ -1255,9 +1271,14 @@ hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t
     return hipGetLastError();
 }
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         hipStream_t st) {
+                         uint32_t* prev, uint32_t* nprev, hipStream_t st) {
     uint32_t nb = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs);
+    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev);
+    return hipGetLastError();
+}
+hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st) {
+    if (!np) return hipSuccess;
+    hipLaunchKernelGGL(k_resolve, dim3((np + 255) / 256), dim3(256), 0, st, prev, np, ring, recs);
     return hipGetLastError();
 }
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,

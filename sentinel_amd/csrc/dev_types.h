@@ -36,8 +36,6 @@ enum : uint32_t {
     NI_REJECTED = 2u,    // lookProcessChain returned null once the cap was reached
     NI_PM = 4u,          // ParamFlowSlot.metricsMap has a ParameterMetric for it
     NI_TM0 = 8u,         // ... with a thread-count map for paramIdx 0
-    NI_BORROW = 16u,     // a prioritized ENTRY was seen: the second window's borrow ring
-                         // (OccupiableBucketLeapArray.borrowArray) is live; decided by k_lane only
 };
 
 struct NodeInfo {
@@ -170,6 +168,7 @@ struct NsLimiter {
 struct DevState {
     Bkt* sec;
     int64_t* borrow;          // [res][2 slots] x {ws, pass}: FutureBucketLeapArray of the second window
+    const uint8_t* prio;      // [res] sticky: a prioritized ENTRY was seen, the borrow ring is live (k_lane only)
     uint64_t* key_ring;       // arg key of every ENTRY by global event index (ring like the status ring),
                               // NO_KEY if it had none; null until param rules exist
     uint64_t gbase;           // global index of the batch's first event
@@ -206,7 +205,9 @@ enum : uint8_t {
     RC_NONE = 0,    // no reference (or unknown entry): effective iff the resource has a chain
     RC_BATCH = 1,   // ENTRY earlier in this batch, same resource: effective iff it passed
     RC_PASSED = 2,  // ENTRY of an earlier batch that passed
-    RC_NOT = 3      // ENTRY that did not pass (blocked / no chain), or a TRACE of an unknown entry
+    RC_NOT = 3,     // ENTRY that did not pass (blocked / no chain), or a TRACE of an unknown entry
+    RC_PREV = 4     // ENTRY of an earlier batch, status not read yet (x = status-ring index): resolved to
+                    // RC_NONE / RC_PASSED / RC_NOT by k_resolve once the earlier batches are decided
 };
 
 // decide-kernel bins of a segment (Seg.pad); order[] is laid out bin by bin

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -23,7 +24,7 @@ namespace sg {
 // kernels.hip
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, NodeInfo* info,
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
                            uint64_t* key_ring, hipStream_t st);
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st);
@@ -39,13 +40,14 @@ hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hip
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const NodeInfo* info, uint32_t lane_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint8_t* prio, uint32_t lane_max,
                           uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st);
 hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
                             hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         hipStream_t st);
+                         uint32_t* prev, uint32_t* nprev, hipStream_t st);
+hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st);
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
@@ -390,7 +392,6 @@ struct sg_engine {
     sg_config cfg;
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     double last_ms[4] = {0, 0, 0, 0};
 
     // resources
@@ -423,7 +424,29 @@ struct sg_engine {
     uint8_t* d_ring = nullptr;
     uint32_t rules_cap = 0, hot_cap = 0;
 
-    // batch scratch
+    // batch scratch: two slots, so that the group stage of batch k+1 (on gstream) runs while the
+    // decide stage of batch k (on stream) is still in flight.  The d_* fields below alias the slot
+    // being filled (activate()).
+    struct BatchSlot {
+        sg_event* d_ev = nullptr;
+        uint32_t* d_out = nullptr;
+        uint32_t *d_k0 = nullptr, *d_v0 = nullptr, *d_k1 = nullptr, *d_v1 = nullptr;
+        uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
+        uint32_t *d_posof = nullptr, *d_dec = nullptr, *d_blkcnt = nullptr, *d_prev = nullptr;
+        SEv *d_recs = nullptr, *d_rec_o = nullptr;
+        Seg* d_segs = nullptr;
+        uint64_t* d_cand = nullptr;
+        uint32_t* d_bsmall = nullptr;  // [0] bflags [1] nseg [2] ncand [3] nprev [4..5] t0 [8..8+N_BINS] bin offsets
+        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // group start/end, decide start/end, post end
+        bool pending = false;  // decide enqueued, not yet collected (timings, flags)
+    } slot[2];
+    int cur = 0;                 // slot of the next batch
+    int last = -1;               // slot of the last batch submitted
+    hipStream_t gstream = nullptr;
+    std::vector<std::array<double, 4>> tlog;  // per batch [group, decide, post, total] ms, by collect()
+    uint8_t* d_prio = nullptr;   // [res] sticky prioritized-ENTRY mark (DevState.prio)
+    uint32_t* d_prev = nullptr;
+    uint32_t* d_bsmall = nullptr;
     uint64_t cap_n = 0;
     sg_event* d_ev = nullptr;
     uint32_t* d_out = nullptr;
@@ -444,8 +467,12 @@ struct sg_engine {
     uint64_t cap_hist = 0;
     uint64_t gbase = 0;
     // decide bins run concurrently: one stream per cooperative bin, the lane bins on the main stream
-    hipStream_t bin_stream[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+    // decide streams: J16 on bin_stream[0], J4 then J1 on bin_stream[1] (together shorter than J16), the
+    // lane bins on stream; with gstream that is four streams for the four hardware queues a process
+    // gets (GPU_MAX_HW_QUEUES): a fifth stream would share a queue and serialise behind another's kernels
+    hipStream_t bin_stream[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    bool pipeline = false;  // SG_PIPELINE=1: the group stage of batch k+1 overlaps the decide stage of batch k
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -469,35 +496,91 @@ struct sg_engine {
 
 namespace {
 
+static void activate(sg_engine* e, int k) {
+    auto& B = e->slot[k];
+    e->d_ev = B.d_ev; e->d_out = B.d_out;
+    e->d_k0 = B.d_k0; e->d_v0 = B.d_v0; e->d_k1 = B.d_k1; e->d_v1 = B.d_v1;
+    e->d_hist = B.d_hist; e->d_part = B.d_part; e->d_flag = B.d_flag; e->d_pos = B.d_pos; e->d_order = B.d_order;
+    e->d_posof = B.d_posof; e->d_dec = B.d_dec; e->d_blkcnt = B.d_blkcnt; e->d_prev = B.d_prev;
+    e->d_recs = B.d_recs; e->d_rec_o = B.d_rec_o; e->d_segs = B.d_segs; e->d_cand = B.d_cand;
+    e->d_bsmall = B.d_bsmall;
+}
+static void free_slot(sg_engine::BatchSlot& B) {
+    dfree(B.d_ev); dfree(B.d_out); dfree(B.d_k0); dfree(B.d_v0); dfree(B.d_k1); dfree(B.d_v1);
+    dfree(B.d_hist); dfree(B.d_part); dfree(B.d_flag); dfree(B.d_pos); dfree(B.d_order); dfree(B.d_segs);
+    dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
+    dfree(B.d_prev); dfree(B.d_bsmall);
+    B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
+    B.d_hist = B.d_part = B.d_flag = B.d_pos = B.d_order = nullptr;
+    B.d_posof = B.d_dec = B.d_blkcnt = B.d_prev = B.d_bsmall = nullptr;
+    B.d_recs = B.d_rec_o = nullptr; B.d_segs = nullptr; B.d_cand = nullptr;
+}
 int ensure_batch(sg_engine* e, uint64_t n) {
     if (n <= e->cap_n) return SG_OK;
     uint64_t c = std::max<uint64_t>(n, 1u << 20);
-    dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
-    dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
+    HIPCHK(hipStreamSynchronize(e->stream));  // no batch may use the old buffers
     uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
     e->cap_hist = nblocks * 256;
-    HIPCHK(hipMalloc(&e->d_ev, c * sizeof(sg_event)));
-    HIPCHK(hipMalloc(&e->d_out, c * 4));
-    HIPCHK(hipMalloc(&e->d_k0, c * 4));
-    HIPCHK(hipMalloc(&e->d_v0, c * 4));
-    HIPCHK(hipMalloc(&e->d_k1, c * 4));
-    HIPCHK(hipMalloc(&e->d_v1, c * 4));
-    HIPCHK(hipMalloc(&e->d_hist, e->cap_hist * 4));
-    HIPCHK(hipMalloc(&e->d_part, (e->cap_hist / 4096 + c / 4096 + 64) * 4));
-    HIPCHK(hipMalloc(&e->d_flag, c * 4));
-    HIPCHK(hipMalloc(&e->d_pos, c * 4));
-    HIPCHK(hipMalloc(&e->d_order, c * 4));
-    HIPCHK(hipMalloc(&e->d_segs, c * sizeof(Seg)));
-    HIPCHK(hipMalloc(&e->d_cand, c * 8));
-    HIPCHK(hipMalloc(&e->d_posof, c * 4));
-    HIPCHK(hipMalloc(&e->d_dec, c * 4));
-    HIPCHK(hipMalloc(&e->d_recs, c * sizeof(SEv)));
-    HIPCHK(hipMalloc(&e->d_rec_o, c * sizeof(SEv)));
-    HIPCHK(hipMalloc(&e->d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));
+    for (auto& B : e->slot) {
+        free_slot(B);
+        HIPCHK(hipMalloc(&B.d_ev, c * sizeof(sg_event)));
+        HIPCHK(hipMalloc(&B.d_out, c * 4));
+        HIPCHK(hipMalloc(&B.d_k0, c * 4));
+        HIPCHK(hipMalloc(&B.d_v0, c * 4));
+        HIPCHK(hipMalloc(&B.d_k1, c * 4));
+        HIPCHK(hipMalloc(&B.d_v1, c * 4));
+        HIPCHK(hipMalloc(&B.d_hist, e->cap_hist * 4));
+        HIPCHK(hipMalloc(&B.d_part, (e->cap_hist / 4096 + c / 4096 + 64) * 4));
+        HIPCHK(hipMalloc(&B.d_flag, c * 4));
+        HIPCHK(hipMalloc(&B.d_pos, c * 4));
+        HIPCHK(hipMalloc(&B.d_order, c * 4));
+        HIPCHK(hipMalloc(&B.d_segs, c * sizeof(Seg)));
+        HIPCHK(hipMalloc(&B.d_cand, c * 8));
+        HIPCHK(hipMalloc(&B.d_posof, c * 4));
+        HIPCHK(hipMalloc(&B.d_dec, c * 4));
+        HIPCHK(hipMalloc(&B.d_recs, c * sizeof(SEv)));
+        HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));
+        HIPCHK(hipMalloc(&B.d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));
+        HIPCHK(hipMalloc(&B.d_prev, c * 4));
+        HIPCHK(hipMalloc(&B.d_bsmall, 256 * 4));
+        HIPCHK(hipMemset(B.d_bsmall, 0, 256 * 4));
+    }
     e->cap_n = c;
+    activate(e, e->cur);
     return SG_OK;
 }
+
+// The slot's batch: wait for its decide stage, record its stage times and check its device flags.
+static int collect(sg_engine* e, int k) {
+    auto& B = e->slot[k];
+    if (!B.pending) return SG_OK;
+    B.pending = false;
+    HIPCHK(hipEventSynchronize(B.ev[4]));
+    float g = 0, d = 0, p = 0;
+    (void)hipEventElapsedTime(&g, B.ev[0], B.ev[1]);
+    (void)hipEventElapsedTime(&d, B.ev[2], B.ev[3]);
+    (void)hipEventElapsedTime(&p, B.ev[3], B.ev[4]);
+    (void)hipGetLastError();
+    e->last_ms[0] = g; e->last_ms[1] = d; e->last_ms[2] = p; e->last_ms[3] = (double)g + d + p;
+    e->tlog.push_back({(double)g, (double)d, (double)p, (double)g + d + p});
+    if (e->tlog.size() > 4096) e->tlog.erase(e->tlog.begin(), e->tlog.begin() + 2048);
+    uint32_t bflags = 0;  // on gstream: a null-stream copy could share a queue with a decide kernel
+    HIPCHK(hipMemcpyAsync(&bflags, B.d_bsmall, 4, hipMemcpyDeviceToHost, e->gstream));
+    HIPCHK(hipStreamSynchronize(e->gstream));
+    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
+    return SG_OK;
+}
+// every batch in flight done (called by the API functions that read or write engine state)
+static int drain(sg_engine* e) {
+    int rc = SG_OK;
+    for (int i = 0; i < 2; ++i) {  // oldest first
+        int r = collect(e, (e->cur + i) & 1);
+        if (r && !rc) rc = r;
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return rc;
+}
+
 
 // Build the device rule program of every resource from the compiled host lists.
 int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
@@ -735,17 +818,21 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     auto bad = [&](int rc) { sg_engine_destroy(e); return rc; };
     if (hipSetDevice(e->device) != hipSuccess) return bad(fail(SG_EDEVICE, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
-    for (auto& v : e->ev) if (hipEventCreate(&v) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
+    if (hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+    for (auto& B : e->slot)
+        for (auto& v : B.ev) if (hipEventCreate(&v) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
     uint64_t R = cfg.max_resources;
     if (hipMalloc(&e->d_sec, R * 2 * sizeof(Bkt)) != hipSuccess || hipMalloc(&e->d_minb, R * 60 * sizeof(Bkt)) != hipSuccess ||
         hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
         hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
         hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
-        hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess)
+        hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&e->d_prio, R) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_prio, 0, R, e->stream) != hipSuccess ||
         launch_init_state(e->d_sec, e->d_minb, e->d_info, e->d_borrow, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
@@ -762,12 +849,24 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_LANE_MAX")) e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J4_MAX")) e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0);
+    if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     *out = e;
     return SG_OK;
 }
 
 // diagnostics export (not part of the ABI): SG_DEBUG=1 counters of the cooperative J16 bin,
 // accumulated over batches (see decide.hip k_jac)
+// diagnostics export (not part of the ABI): stage times of the batches collected since the last call,
+// 4 doubles each ([group, decide, post, total] ms); returns the number of batches written
+extern "C" int sgx_timing_log(sg_engine* e, double* out, int cap) {
+    if (!e || !out) return 0;
+    (void)drain(e);
+    int k = 0;
+    for (; k < cap && k < (int)e->tlog.size(); ++k)
+        for (int j = 0; j < 4; ++j) out[4 * k + j] = e->tlog[k][j];
+    e->tlog.clear();
+    return k;
+}
 extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap) {
     if (!e || !e->d_dbg || !out) return 0;
     int k = cap < 64 ? cap : 64;
@@ -780,15 +879,18 @@ int sg_engine_destroy(sg_engine* e) {
     if (!e) return SG_OK;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
-    dfree(e->d_ev); dfree(e->d_out); dfree(e->d_k0); dfree(e->d_v0); dfree(e->d_k1); dfree(e->d_v1);
-    dfree(e->d_hist); dfree(e->d_part); dfree(e->d_flag); dfree(e->d_pos); dfree(e->d_order); dfree(e->d_segs);
-    dfree(e->d_cand); dfree(e->d_posof); dfree(e->d_dec); dfree(e->d_recs); dfree(e->d_rec_o); dfree(e->d_blkcnt);
+    if (e->gstream) (void)hipStreamSynchronize(e->gstream);
+    for (auto& B : e->slot) free_slot(B);
+    dfree(e->d_prio);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
-    for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+    for (auto& B : e->slot)
+        for (auto& v : B.ev) if (v) (void)hipEventDestroy(v);
+    if (e->gstream) (void)hipStreamDestroy(e->gstream);
     for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
     if (e->fork) (void)hipEventDestroy(e->fork);
     for (auto& s : e->bin_stream) if (s) (void)hipStreamDestroy(s);
@@ -799,6 +901,7 @@ int sg_engine_destroy(sg_engine* e) {
 
 int sg_register_resources(sg_engine* e, const char* const* names, uint32_t n, uint32_t* out_ids) {
     if (!e || (n && !names)) return fail(SG_EINVAL, "null argument");
+    if (int rc = drain(e)) return rc;
     for (uint32_t i = 0; i < n; ++i) {
         if (!names[i]) return fail(SG_EINVAL, "null resource name");
         auto it = e->ids.find(names[i]);
@@ -919,6 +1022,7 @@ static int rebuild_cluster(sg_engine* e, const sg_flow_rule* rules, uint32_t n) 
 
 int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    if (int rc = drain(e)) return rc;  // no batch in flight while the rule tables change
     std::vector<std::string> keys(n);
     for (uint32_t i = 0; i < n; ++i) keys[i] = flow_eqkey(rules[i]);
     if (e->flow_loaded && keys == e->last_flow) { // DynamicSentinelProperty.updateValue: equal -> no-op
@@ -985,6 +1089,7 @@ int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint
 // DegradeRuleManager.loadRules (core/slots/block/degrade/DegradeRuleManager.java:112-205)
 int sg_load_degrade_rules(sg_engine* e, const sg_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    if (int rc = drain(e)) return rc;  // no batch in flight while the rule tables change
     std::vector<std::string> keys(n);
     for (uint32_t i = 0; i < n; ++i) keys[i] = deg_eqkey(rules[i], (int)i);
     bool has_nan = false;
@@ -1034,6 +1139,7 @@ int sg_load_degrade_rules(sg_engine* e, const sg_degrade_rule* rules, uint32_t n
 // ParamFlowRuleManager.loadRules (param/slots/block/flow/param/ParamFlowRuleManager.java:103-166)
 int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
+    if (int rc = drain(e)) return rc;  // no batch in flight while the rule tables change
     std::vector<ParamR> all;
     std::vector<std::string> keys;
     for (uint32_t i = 0; i < n; ++i) {
@@ -1120,6 +1226,10 @@ static bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Batch pipeline: the group stage (records, sort, segments, bins) of this batch runs on gstream and
+// the host waits for it only; the decide stage (reference resolution, chain grants, decide kernels,
+// post) is enqueued on stream behind the previous batch's and the call returns.  So batch k+1's
+// group stage overlaps batch k's decide stage.  Buffers must stay valid until sg_sync.
 int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
     if (!e || (n && (!ev || !out))) return fail(SG_EINVAL, "null argument");
     if (n == 0) return SG_OK;
@@ -1127,43 +1237,54 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(hipSetDevice(e->device));
     int rc = ensure_batch(e, n);
     if (rc) return rc;
-    hipStream_t st = e->stream;
+    const int k = e->cur;
+    rc = collect(e, k);  // the batch that last used this slot (two batches ago) is decided
+    if (rc) return rc;
+    activate(e, k);
+    auto& B = e->slot[k];
+    hipStream_t gs = e->gstream, st = e->stream;
     const sg_event* dev_ev = ev;
     bool host_in = !is_device_ptr(ev);
     bool host_out = !is_device_ptr(out);
     if (host_in) {
-        HIPCHK(hipMemcpyAsync(e->d_ev, ev, n * sizeof(sg_event), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->d_ev, ev, n * sizeof(sg_event), hipMemcpyHostToDevice, gs));
         dev_ev = e->d_ev;
     }
     uint32_t* dev_out = host_out ? e->d_out : out;
     const uint64_t ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
-    HIPCHK(hipEventRecord(e->ev[0], st));
+    // Overlapping this group stage with the previous batch's decide stage is only a win when the
+    // bandwidth-bound sort does not slow the latency-bound decide kernels more than it hides; measured
+    // on MI355X it does (k_jac<16> 3.6 -> 6-8 ms), so by default the stages run back to back.
+    if (!e->pipeline && e->last >= 0 && e->slot[e->last].pending)
+        HIPCHK(hipStreamWaitEvent(gs, e->slot[e->last].ev[4], 0));
+    HIPCHK(hipEventRecord(B.ev[0], gs));
     // ---- 1. group: records + stable LSD radix sort on res_id (8-bit digits over the bits of max_resources-1)
     uint32_t R = e->cfg.max_resources;
     int bits = 1;
     while (bits < 32 && (1ull << bits) < R) ++bits;
     int passes = (bits + 7) / 8;
     uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
-    HIPCHK(hipMemsetAsync(e->d_small, 0, 256 * 4, st));
-    int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_small + 4);  // [4..5]
+    HIPCHK(hipMemsetAsync(e->d_bsmall, 0, 256 * 4, gs));
+    int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_small + 0, d_t0, e->d_info, e->d_keyring, st));
+                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, gs));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
-        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
-        HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, st));
+        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, gs));
+        HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, gs));
         HIPCHK(launch_radix_scatter(kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout,
-                                    p == passes - 1 ? e->d_posof : nullptr, st));
+                                    p == passes - 1 ? e->d_posof : nullptr, gs));
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
     // ---- 2. segments + 16-byte sorted records
-    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, st, launch_scan, e->d_part, e->d_small + 1));
-    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, st));
+    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, gs, launch_scan, e->d_part, e->d_bsmall + 1));
+    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, gs));
     uint32_t head[6];
-    HIPCHK(hipMemcpyAsync(head, e->d_small, sizeof(head), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
+    HIPCHK(hipStreamSynchronize(gs));
     const uint32_t m = head[1];
+    const uint32_t nprev = head[3];
     int64_t t0 = 0;
     std::memcpy(&t0, head + 4, 8);
     uint32_t bflags = head[0];
@@ -1175,22 +1296,26 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
     const uint32_t nblk = (m + 255) / 256;
-    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->d_info, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
-                          e->d_blkcnt, st));
-    HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, st));
-    HIPCHK(launch_seg_order(e->d_segs, m, e->d_blkcnt, e->d_order, e->d_small + 8, st));
+    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->d_prio, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
+                          e->d_blkcnt, gs));
+    HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
+    HIPCHK(launch_seg_order(e->d_segs, m, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     uint32_t off[N_BINS + 1];
-    HIPCHK(hipMemcpyAsync(off, e->d_small + 8, sizeof(off), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyAsync(off, e->d_bsmall + 8, sizeof(off), hipMemcpyDeviceToHost, gs));
+    HIPCHK(hipEventRecord(B.ev[1], gs));
+    HIPCHK(hipStreamSynchronize(gs));
     uint32_t bin_n[N_BINS];
     for (int b = 0; b < N_BINS; ++b) bin_n[b] = off[b + 1] - off[b];
+    // ---- decide stage, in order after the previous batch's: references into earlier batches first
+    HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
+    HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, st));
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
-        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_small + 2, e->d_cand, st));
+        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand, st));
         if (!grant_all) {
             uint32_t ncand = 0;
-            HIPCHK(hipMemcpyAsync(&ncand, e->d_small + 2, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&ncand, e->d_bsmall + 2, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             if (ncand) {
                 std::vector<uint64_t> cand(ncand);
@@ -1209,7 +1334,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
             }
         }
     }
-    HIPCHK(hipEventRecord(e->ev[1], st));
+    HIPCHK(hipEventRecord(B.ev[2], st));
     // ---- 3. decide: cooperative bins on their own streams, lane bins on the main stream
     DevCfg dc;
     std::memset(&dc, 0, sizeof(dc));
@@ -1233,54 +1358,50 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.ring = e->d_ring;
     S.sink = e->d_sink;
     S.borrow = e->d_borrow;
+    S.prio = e->d_prio;
     S.key_ring = e->d_keyring;
     S.gbase = e->gbase;
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
-    for (int k = 0; k < 3; ++k) {
-        const int b = coop[k];
+    for (int c = 0; c < 3; ++c) {
+        const int b = coop[c];
         if (!bin_n[b]) continue;
         DevState Sb = S;
-        Sb.dbg = (k == 0 && e->d_dbg) ? e->d_dbg : nullptr;
-        HIPCHK(hipStreamWaitEvent(e->bin_stream[k], e->fork, 0));
+        Sb.dbg = (c == 0 && e->d_dbg) ? e->d_dbg : nullptr;
+        const int q = c == 0 ? 0 : 1;
+        HIPCHK(hipStreamWaitEvent(e->bin_stream[q], e->fork, 0));
         HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sb, dc, t0,
-                                 e->d_dec, e->d_small + 0, e->bin_stream[k]));
-        HIPCHK(hipEventRecord(e->join[k], e->bin_stream[k]));
+                                 e->d_dec, e->d_bsmall + 0, e->bin_stream[q]));
+        HIPCHK(hipEventRecord(e->join[q], e->bin_stream[q]));
     }
     HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
-                             off[BIN_LANE + LANE_BINS] - off[BIN_LANE], S, dc, t0, e->d_dec, e->d_small + 0, st));
+                             off[BIN_LANE + LANE_BINS] - off[BIN_LANE], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
     HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
-                             off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_small + 0, st));
-    for (int k = 0; k < 3; ++k)
-        if (bin_n[coop[k]]) HIPCHK(hipStreamWaitEvent(st, e->join[k], 0));
-    HIPCHK(hipEventRecord(e->ev[2], st));
+                             off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    for (int c = 0; c < 3; ++c)
+        if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c == 0 ? 0 : 1], 0));
+    HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
-    HIPCHK(hipEventRecord(e->ev[3], st));
     if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(B.ev[4], st));
+    B.pending = true;
+    e->last = k;
+    e->cur = k ^ 1;
     e->gbase += n;
     return SG_OK;
 }
 
 int sg_sync(sg_engine* e) {
     if (!e) return fail(SG_EINVAL, "null engine");
-    HIPCHK(hipStreamSynchronize(e->stream));
-    float a = 0, b = 0, c = 0;
-    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->last_ms[0] = a;
-    if (hipEventElapsedTime(&b, e->ev[1], e->ev[2]) == hipSuccess) e->last_ms[1] = b;
-    if (hipEventElapsedTime(&c, e->ev[2], e->ev[3]) == hipSuccess) e->last_ms[2] = c;
-    e->last_ms[3] = e->last_ms[0] + e->last_ms[1] + e->last_ms[2];
-    (void)hipGetLastError();
-    uint32_t bflags = 0;
-    HIPCHK(hipMemcpy(&bflags, e->d_small, 4, hipMemcpyDeviceToHost));
-    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
-    return SG_OK;
+    HIPCHK(hipSetDevice(e->device));
+    return drain(e);
 }
 
 int sg_submit(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
     int rc = sg_submit_async(e, ev, n, out);
     if (rc) {
-        if (e) (void)hipStreamSynchronize(e->stream);
+        if (e) (void)drain(e);
         return rc;
     }
     return sg_sync(e);
@@ -1297,6 +1418,7 @@ int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out)
     (void)now_ms;
     if (!e || !out) return fail(SG_EINVAL, "null argument");
     if (res >= e->cfg.max_resources) return fail(SG_EINVAL, "res_id out of range");
+    if (int rc = drain(e)) return rc;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     Bkt sec[2], mb[60];
@@ -1335,6 +1457,7 @@ int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out)
 int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n) {
     if (!e || !n) return fail(SG_EINVAL, "null argument");
     HIPCHK(hipSetDevice(e->device));
+    if (int rc = drain(e)) return rc;
     uint32_t R = (uint32_t)std::min<size_t>(e->names.size(), e->cfg.max_resources);
     if (R == 0) { *n = 0; return SG_OK; }
     if (!e->d_snap_cnt) {
@@ -1360,6 +1483,7 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
 
 int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected) {
     if (!e) return fail(SG_EINVAL, "null engine");
+    if (int rc = drain(e)) return rc;
     auto it = e->cmap.find(flow_id);
     if (it == e->cmap.end()) return fail(SG_ENOTFOUND, "no cluster flow rule with this flowId");
     e->cflows[it->second].connected = connected;
@@ -1372,6 +1496,7 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
     if (!e || (n && (!reqs || !out))) return fail(SG_EINVAL, "null argument");
     if (!n) return SG_OK;
     if (n > 0x7FFFFFFFull) return fail(SG_EINVAL, "too many token requests in one call");
+    if (int rc = drain(e)) return rc;
     hipStream_t st = e->stream;
     int rc = ensure_batch(e, n);  // radix-sort scratch
     if (rc) return rc;

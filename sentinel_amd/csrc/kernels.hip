@@ -38,7 +38,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                       uint32_t* __restrict__ ghist, uint32_t nblocks,
                                                       uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out,
-                                                      NodeInfo* __restrict__ info, uint64_t* __restrict__ key_ring) {
+                                                      uint8_t* __restrict__ prio, uint64_t* __restrict__ key_ring) {
     __shared__ uint32_t h[RS_BINS];
     for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
     __syncthreads();
@@ -66,9 +66,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         if (e.kind == SG_EV_ENTRY) {
             // the arg an exit(count, args) of this ENTRY will decrement (ParamFlowStatisticExitCallback)
             if (key_ring) key_ring[(gbase + i) & ring_mask] = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
-            // a prioritized ENTRY makes the resource's borrow ring live: its segments go to k_lane
-            if ((e.flags & SG_F_PRIORITIZED) && e.res_id < max_res && !(info[e.res_id].flags & NI_BORROW))
-                atomicOr(&info[e.res_id].flags, NI_BORROW);
+            // a prioritized ENTRY makes the resource's borrow ring live: its segments go to k_lane (a
+            // separate byte array: this stage may run while the previous batch's decide stores NodeInfo)
+            if ((e.flags & SG_F_PRIORITIZED) && e.res_id < max_res && !prio[e.res_id]) prio[e.res_id] = 1;
         } else {
             if (e.kind == SG_EV_EXIT) {
                 const int64_t raw = (int64_t)(e.aux >> 48);
@@ -79,10 +79,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                 if (ref >= gbase) {
                     if (ref - gbase >= i) fl |= BF_BAD_REF;  // an EXIT/TRACE must follow its ENTRY
                     else { r.code = RC_BATCH; r.x = (uint32_t)(ref - gbase); }
-                } else {  // an ENTRY of an earlier batch: its status from the ring (0xFF = not an ENTRY)
-                    const uint8_t st = ring[ref & ring_mask];
-                    if (st == ST_NOT_ENTRY) r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-                    else r.code = (st == ST_PASS || st == ST_PASS_WAIT) ? RC_PASSED : RC_NOT;
+                } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve,
+                          // after the earlier batches are decided (this stage overlaps the previous decide)
+                    r.code = RC_PREV;
+                    r.x = (uint32_t)(ref & ring_mask);
                 }
             }
         }
@@ -334,10 +334,10 @@ namespace sg {
 
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, NodeInfo* info,
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
                            uint64_t* key_ring, hipStream_t st) {
     hipLaunchKernelGGL(k_rs_first, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask, max_rt,
-                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, info, key_ring);
+                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,

@@ -165,6 +165,16 @@ class Engine:
         k = lib().sg_last_timings(self.h, ms, 4)
         return list(ms[:k])
 
+    def timing_log(self, cap: int = 4096) -> np.ndarray:
+        """Stage times of every batch decided since the last call, [n, 4] ms (group, decide, post,
+        total); diagnostics export sgx_timing_log, drains the pipeline first."""
+        buf = (C.c_double * (4 * cap))()
+        fn = lib().sgx_timing_log
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        k = fn(self.h, buf, cap)
+        return np.frombuffer(buf, dtype=np.float64, count=4 * k).reshape(k, 4).copy()
+
     def read_node(self, res: int, now: int = 0) -> dict:
         st = A.SgNodeState()
         _check(lib().sg_read_node(self.h, res, now, C.byref(st)))

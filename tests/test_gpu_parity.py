@@ -290,3 +290,27 @@ def test_exit_with_args_thread_params(bin_mode):
     _compare_nodes(w, eng, orc, _sample(w))
     st = dg[ev["kind"] == A.EV_ENTRY] & 0xFF
     assert (st == A.BLOCK_PARAM).sum() > 0 and (st == A.PASS).sum() > 0
+
+
+# ---------------------------------------------------------------- batch pipeline (sg_submit_async)
+@pytest.mark.parametrize("config,kw", [(4, {"n_entries": 300_000, "n_res": 5_000}), (3, {"n_entries": 300_000, "n_res": 20_000})])
+def test_async_pipeline(config, kw):
+    """Batches submitted back to back with sg_submit_async: the group stage of batch k+1 runs while
+    batch k is decided, and references into earlier batches are resolved in the decide stage."""
+    w = T.Workload(config, **kw)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    ev = w.events
+    cuts = np.linspace(0, len(ev), 7).astype(np.int64)
+    parts = [np.ascontiguousarray(ev[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    outs = [np.zeros(len(p), dtype=np.uint32) for p in parts]
+    for p, o in zip(parts, outs):
+        eng.submit_ptr(p.ctypes.data, len(p), o.ctypes.data, sync=False)
+    eng.sync()
+    dg = np.concatenate(outs)
+    do = np.concatenate([orc.submit(p) for p in parts])
+    _assert_same_decisions(dg, do, ev)
+    _compare_nodes(w, eng, orc, _sample(w))
+    assert len(eng.timing_log()) == len(parts)
