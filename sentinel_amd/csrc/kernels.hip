@@ -110,56 +110,100 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __res
     for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// stable scatter: items of a tile are ranked in (round, wave, lane) order == input order.  The last
-// pass also writes the inverse permutation pos_of[idx] = sorted position | ENTRY bit.
+// Stable scatter of one 8-bit digit.  A tile's items are ranked in (round, wave, lane) order ==
+// input order and placed, digit-sorted, in LDS first; the tile then leaves in digit runs, so the
+// writes of a run are consecutive addresses (a direct scatter would send each round's 256 items to
+// up to 256 different places).  The last pass also writes the inverse permutation
+// pos_of[idx] = sorted position | ENTRY bit.
 __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                            uint32_t* __restrict__ pos_of) {
+    __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
     __shared__ uint32_t wcnt[4][RS_BINS];
     __shared__ uint32_t woff[4][RS_BINS];
-    __shared__ uint32_t run[RS_BINS];
+    __shared__ uint32_t run[RS_BINS];   // local cursor of each digit
+    __shared__ int64_t gdst[RS_BINS];   // global position of local position 0 of each digit's run
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint32_t cnt_tile = (uint32_t)((n - base) < RS_TILE ? (n - base) : RS_TILE);
+    uint32_t kk[RS_ITEMS], vv[RS_ITEMS];
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {  // striped loads: coalesced
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        kk[it] = i < n ? keys_in[i] : 0u;
+        vv[it] = i < n ? vals_in[i] : 0u;
+    }
     for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) {
-        run[i] = goff[(uint64_t)i * nblocks + blockIdx.x];
+        run[i] = 0;
         wcnt[0][i] = wcnt[1][i] = wcnt[2][i] = wcnt[3][i] = 0;
     }
     __syncthreads();
-    const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
-    uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    // local digit histogram -> local offsets (exclusive scan over 256 bins by wave 0)
+#pragma unroll
     for (int it = 0; it < RS_ITEMS; ++it) {
-        uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
-        bool valid = i < n;
-        uint32_t k = 0, v = 0;
-        if (valid) { k = keys_in[i]; v = vals_in[i]; }
-        uint32_t d = (k >> shift) & (RS_BINS - 1);
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&run[(kk[it] >> shift) & (RS_BINS - 1)], 1u);
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t c[4], t = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { c[j] = run[4 * l + j]; t += c[j]; }
+        uint32_t x = t;  // inclusive wave scan of the per-lane totals
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (l >= o) x += y;
+        }
+        uint32_t acc = x - t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * l + j;
+            gdst[d] = (int64_t)goff[(uint64_t)d * nblocks + blockIdx.x] - (int64_t)acc;
+            run[d] = acc;
+            acc += c[j];
+        }
+    }
+    __syncthreads();
+    const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t k = kk[it];
+        const uint32_t d = (k >> shift) & (RS_BINS - 1);
         // peers: lanes with the same digit (8 ballots)
         uint64_t peers = __ballot(valid);
-        #pragma unroll
+#pragma unroll
         for (int b = 0; b < 8; ++b) {
-            uint64_t bb = __ballot((d >> b) & 1);
+            const uint64_t bb = __ballot((d >> b) & 1);
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
-        uint32_t rank = __popcll(peers & lt_mask);
-        uint32_t cnt = __popcll(peers);
-        bool leader = valid && rank == 0;
-        if (leader) wcnt[w][d] = cnt;
+        const uint32_t rank = __popcll(peers & lt_mask);
+        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
         __syncthreads();
         for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) {
             uint32_t acc = run[b];
-            #pragma unroll
-            for (int ww = 0; ww < 4; ++ww) { uint32_t c = wcnt[ww][b]; woff[ww][b] = acc; acc += c; wcnt[ww][b] = 0; }
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) { const uint32_t c = wcnt[ww][b]; woff[ww][b] = acc; acc += c; wcnt[ww][b] = 0; }
             run[b] = acc;
         }
         __syncthreads();
         if (valid) {
-            uint32_t dst = woff[w][d] + rank;
-            keys_out[dst] = k;
-            vals_out[dst] = v;
-            if (pos_of) pos_of[v & 0x7FFFFFFFu] = dst | (v & 0x80000000u);
+            const uint32_t lp = woff[w][d] + rank;
+            sk[lp] = k;
+            sv[lp] = vv[it];
         }
-        __syncthreads();
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < cnt_tile; p += RS_THREADS) {  // digit runs: consecutive addresses
+        const uint32_t k = sk[p], v = sv[p];
+        const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (RS_BINS - 1)] + (int64_t)p);
+        keys_out[dst] = k;
+        vals_out[dst] = v;
+        if (pos_of) pos_of[v & 0x7FFFFFFFu] = (uint32_t)dst | (v & 0x80000000u);
     }
 }
 
