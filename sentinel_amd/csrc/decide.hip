@@ -78,9 +78,9 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
         const uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
         sg.len = end - sg.start;
         const Prog p = prog[sg.res];
-        const int nr = p.n_param + p.n_flow + p.n_degrade;
+        const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // members decided with 16-rule lanes
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
-                          !prio[sg.res];
+                          !prio[sg.res] && !p.multi;
         uint32_t bin;
         if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
@@ -164,10 +164,22 @@ __global__ void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __re
 // ENTRY, res) candidates for the host, which grants in first-ENTRY order up to the cap.
 __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                         uint32_t m, NodeInfo* __restrict__ info, uint32_t grant_all, uint32_t* __restrict__ ncand,
-                        uint64_t* __restrict__ cand) {
+                        uint64_t* __restrict__ cand, const sg_event* __restrict__ ev, const Prog* __restrict__ prog) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= m) return;
     Seg sg = segs[s];
+    if (prog[sg.res].multi) {  // a STRATEGY_RELATE component: every member's first ENTRY
+        for (uint32_t j = 0; j < sg.len; ++j) {
+            if (recs[sg.start + j].kind != SG_EV_ENTRY) continue;
+            const uint32_t vi = vals[sg.start + j] & 0x7FFFFFFFu;
+            const uint32_t res = ev[vi].res_id;
+            const uint32_t fr = info[res].flags;
+            if (fr & (NI_CHAIN | NI_REJECTED)) continue;
+            if (grant_all) info[res].flags = fr | NI_CHAIN;
+            else cand[atomicAdd(ncand, 1u)] = ((uint64_t)vi << 32) | res;  // the host keeps the first per resource
+        }
+        return;
+    }
     uint32_t f = info[sg.res].flags;
     if (f & (NI_CHAIN | NI_REJECTED)) return;
     for (uint32_t j = 0; j < sg.len; ++j) {
@@ -300,7 +312,31 @@ __device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, 
 // One ENTRY through StatisticSlot -> ParamFlowSlot -> FlowSlot -> DegradeSlot
 // (param/slots/HotParamSlotChainBuilder.java:38-51, StatisticSlot.entry StatisticSlot.java:54-133).
 // rs[] is indexed only with unrolled constants, so for NRMAX <= 4 it stays in registers.
-template <int NRMAX>
+// FlowRuleChecker.selectReferenceNode for STRATEGY_RELATE (FlowRuleChecker.java:67-88): the controller
+// runs on the ClusterNode of ref (ClusterBuilderSlot.getClusterNode: null until an ENTRY of ref was
+// processed with a chain -> pass), with its side effects on that node (currentWindow resets)
+__device__ int relate_check(const DevState& S, const DevCfg& cfg, const DRule& r, RState& s, int64_t t, int cnt,
+                            uint32_t fl, int64_t& wait) {
+    const uint32_t b = r.ref;
+    if (!(S.info[b].flags & NI_TOUCHED)) return 1;
+    Node NB;
+    node_load(NB, S, b);
+    const Prog pb = S.prog[b];
+    const Ctx CB{S.minb + (uint64_t)b * 60, cfg.max_rt, pb.pflags};
+    int rc;
+    if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
+        int64_t w = 0;
+        rc = default_can_pass_prio(NB, CB, r, t, cnt, cfg.occupy_timeout, w);
+        if (rc == 2) wait += w;
+    } else {
+        rc = flow_can_pass(NB, CB, r, s, t, cnt, wait) ? 1 : 0;
+    }
+    min_flush(NB, CB.minb);
+    node_store(NB, S, b, pb.pflags);
+    return rc;
+}
+
+template <int NRMAX, bool MULTI = false>
 __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg,
                                                const Prog& pg, RState (&rs)[NRMAX], uint32_t res, int64_t t, int cnt,
                                                uint32_t fl, uint64_t arg, uint32_t* bflags) {
@@ -323,7 +359,13 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                     else wait += w;
                 }
             } else if (s < nfl) {  // FlowSlot.checkFlow (FlowSlot.java:146-158)
-                if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
+                if (MULTI && r.ref != NO_REF) {
+                    int64_t w = 0;
+                    const int rc = relate_check(S, cfg, r, rs[s], t, cnt, fl, w);
+                    if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
+                    else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }
+                    else wait += w;
+                } else if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
                     int64_t w = 0;
                     const int rc = default_can_pass_prio(N, C, r, t, cnt, cfg.occupy_timeout, w);
                     if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
@@ -348,6 +390,69 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
     return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
 }
 
+// A STRATEGY_RELATE component (one segment, members in event order): each event runs on its own
+// resource's node, rules and states, loaded and stored per event -- the flow check of a member may
+// read and rotate another member's ClusterNode in between.
+template <int NRMAX>
+__device__ void lane_multi(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                           const uint32_t* __restrict__ vals, const Seg& sg, const DevState& S, const DevCfg& cfg,
+                           int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    for (uint32_t j = 0; j < sg.len; ++j) {
+        const SEv r = recs[sg.start + j];
+        const sg_event& E = ev[vals[sg.start + j] & 0x7FFFFFFFu];
+        const uint32_t res = E.res_id;
+        const int64_t t = t0 + r.dt;
+        const Prog pg = S.prog[res];
+        const int nr = pg.n_param + pg.n_flow + pg.n_degrade;
+        Node N;
+        node_load(N, S, res);
+        const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+        RState rs[NRMAX];
+#pragma unroll
+        for (int s = 0; s < NRMAX; ++s) if (s < nr) rs[s] = S.rstate[pg.rule_off + s];
+        const bool has_chain = (N.flags & NI_CHAIN) != 0;
+        const bool chain = has_chain && cfg.switch_on;
+        uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+        if (r.kind == SG_EV_ENTRY) {
+            if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
+            else {
+                N.flags |= NI_TOUCHED;  // ClusterBuilderSlot runs before the checks
+                const uint64_t arg = (r.flags & SG_F_HAS_ARG) ? E.aux : 0;
+                d = lane_entry<NRMAX, true>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
+            }
+        } else {
+            bool eff;
+            if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
+            else if (r.code == RC_PASSED) eff = true;
+            else if (r.code == RC_NOT) eff = false;
+            else {
+                const uint32_t rel = r.x - sg.start;
+                if (rel >= j) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+                else eff = st_passed(dec[r.x] & 0xFF);  // written by this lane
+            }
+            if (eff) {
+                if (r.kind == SG_EV_EXIT) {
+                    stat_exit(N, C, t, r.cnt, r.rt);
+                    if ((r.flags & SG_F_EXIT_ARGS) && S.key_ring && (N.flags & NI_PM) && (N.flags & NI_TM0) &&
+                        r.code != RC_NONE) {
+                        const uint64_t ref = r.code == RC_BATCH ? S.gbase + (vals[r.x] & 0x7FFFFFFFu)
+                                                                : (E.aux & SG_REF_NONE);
+                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
+                        if (key != NO_KEY) thread_count_add(S, cfg, res, pg.tc_epoch, key, -1, bflags);
+                    }
+                } else {
+                    stat_trace(N, C, t, r.cnt);
+                }
+            }
+        }
+        dec[sg.start + j] = d;
+        min_flush(N, C.minb);
+        node_store(N, S, res, pg.pflags);
+#pragma unroll
+        for (int s = 0; s < NRMAX; ++s) if (s < nr) S.rstate[pg.rule_off + s] = rs[s];
+    }
+}
+
 template <int NRMAX>
 __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
                                               const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
@@ -358,6 +463,10 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     const Seg sg = segs[order[i]];
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
+    if (NRMAX >= 16 && pg.multi) {
+        lane_multi<NRMAX>(recs, ev, vals, sg, S, cfg, t0, dec, bflags);
+        return;
+    }
     const int nr = pg.n_param + pg.n_flow + pg.n_degrade;
     Node N;
     node_load(N, S, res);
@@ -1288,10 +1397,11 @@ hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, 
     return hipGetLastError();
 }
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
-                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, hipStream_t st) {
+                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, const sg_event* ev, const Prog* prog,
+                        hipStream_t st) {
     if (!m) return hipSuccess;
     hipLaunchKernelGGL(k_chain, dim3((m + 255) / 256), dim3(256), 0, st, recs, vals, segs, m, info, grant_all, ncand,
-                       cand);
+                       cand, ev, prog);
     return hipGetLastError();
 }
 // bin = BIN_J16 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16

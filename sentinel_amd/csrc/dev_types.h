@@ -36,6 +36,8 @@ enum : uint32_t {
     NI_REJECTED = 2u,    // lookProcessChain returned null once the cap was reached
     NI_PM = 4u,          // ParamFlowSlot.metricsMap has a ParameterMetric for it
     NI_TM0 = 8u,         // ... with a thread-count map for paramIdx 0
+    NI_TOUCHED = 32u,    // ClusterBuilderSlot created its ClusterNode (an ENTRY with a chain was processed);
+                         // kept exact for resources in a STRATEGY_RELATE component (ClusterBuilderSlot.getClusterNode)
 };
 
 struct NodeInfo {
@@ -64,7 +66,7 @@ struct Prog {
     uint32_t rule_off;
     uint8_t n_param, n_flow, n_degrade, pflags;
     uint32_t tc_epoch;   // epoch of this resource's param thread-count keys
-    uint32_t pad;
+    uint32_t multi;      // representative of a STRATEGY_RELATE component (its members share one segment)
 };
 static_assert(sizeof(Prog) == 16, "Prog must be 16 B");
 
@@ -89,8 +91,9 @@ struct DRule {
     int64_t token_count_l; // param (long)count (throttle)
     uint32_t hot_off, hot_n;   // hot items
     uint32_t psid;       // param state id (ParameterMetric maps keyed by rule equality)
-    uint32_t pad;
+    uint32_t ref;        // flow STRATEGY_RELATE: the resource whose ClusterNode is checked (NO_REF: none)
 };
+#define NO_REF 0xFFFFFFFFu
 static_assert(sizeof(DRule) == 80, "DRule must be 80 B");
 
 struct DHot {

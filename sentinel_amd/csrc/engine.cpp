@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -25,7 +26,7 @@ namespace sg {
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
-                           uint64_t* key_ring, hipStream_t st);
+                           uint64_t* key_ring, const uint32_t* comp, hipStream_t st);
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
@@ -51,7 +52,8 @@ hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
-                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, hipStream_t st);
+                        uint32_t grant_all, uint32_t* ncand, uint64_t* cand, const sg_event* ev, const Prog* prog,
+                        hipStream_t st);
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st);
@@ -445,6 +447,7 @@ struct sg_engine {
     hipStream_t gstream = nullptr;
     std::vector<std::array<double, 4>> tlog;  // per batch [group, decide, post, total] ms, by collect()
     uint8_t* d_prio = nullptr;   // [res] sticky prioritized-ENTRY mark (DevState.prio)
+    uint32_t* d_comp = nullptr;  // [res] STRATEGY_RELATE component representative (sort key); null: none
     uint32_t* d_prev = nullptr;
     uint32_t* d_bsmall = nullptr;
     uint64_t cap_n = 0;
@@ -600,6 +603,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
     }
     size_t nres = e->names.size();
     if (e->tc_epoch.size() < nres) e->tc_epoch.resize(nres, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> relate;  // (resource, referenced resource) of RELATE rules
     for (size_t r = 0; r < nres && r < R; ++r) {
         Prog p;
         std::memset(&p, 0, sizeof(p));
@@ -649,8 +653,6 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
         for (size_t i = 0; i < fl.size(); ++i) {
             const FlowR& f = e->flows[fl[i]];
             if (f.la != "default") continue;  // origin "" never matches / isOtherOrigin("") == false
-            if (f.r.strategy == SG_STRATEGY_RELATE)
-                return fail(SG_ENOTSUP, "STRATEGY_RELATE reads another resource's node: not on the device path yet");
             if (f.r.strategy == SG_STRATEGY_CHAIN && f.ref != "sentinel_default_context") continue;
             if (f.r.cluster_mode && !f.r.cluster_fallback_to_local) continue; // no TokenService -> pass
             DRule d;
@@ -662,6 +664,12 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
             d.slot = (uint8_t)i;
             d.max_queue = f.r.max_queueing_time_ms;
             d.count = f.r.count;
+            d.ref = NO_REF;
+            if (f.r.strategy == SG_STRATEGY_RELATE) {  // another resource's ClusterNode (same node if itself)
+                auto it = e->ids.find(f.ref);
+                const uint32_t b = it == e->ids.end() ? NO_REF : it->second;
+                if (b != NO_REF && b != (uint32_t)r && b < R) { d.ref = b; relate.emplace_back((uint32_t)r, b); }
+            }
             if (d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
                 // WarmUpController.construct (WarmUpController.java:100-117)
                 int cold = e->cfg.cold_factor;
@@ -729,6 +737,36 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
         }
         prog[r] = p;
     }
+    // STRATEGY_RELATE components (co-locate the rule graph's connected components):
+    // union-find over the references; every member sorts under the representative, one segment
+    std::vector<uint32_t> comp;
+    if (!relate.empty()) {
+        comp.resize(R);
+        for (uint32_t x = 0; x < R; ++x) comp[x] = x;
+        std::function<uint32_t(uint32_t)> find = [&](uint32_t x) { return comp[x] == x ? x : comp[x] = find(comp[x]); };
+        for (auto& pr : relate) {
+            uint32_t a = find(pr.first), b = find(pr.second);
+            if (a != b) comp[std::max(a, b)] = std::min(a, b);
+        }
+        for (uint32_t x = 0; x < R; ++x) comp[x] = find(x);
+        std::vector<uint32_t> members;
+        for (uint32_t x = 0; x < R; ++x)
+            if (comp[x] != x) { members.push_back(x); members.push_back(comp[x]); }
+        std::sort(members.begin(), members.end());
+        members.erase(std::unique(members.begin(), members.end()), members.end());
+        for (uint32_t x : members) {
+            if (comp[x] == x) { prog[x].multi = 1; prog[x].pflags |= PF_SERIAL; }
+        }
+        // ClusterNode existence of the members from here on: NI_TOUCHED (a chain grant means an ENTRY of
+        // the resource was decided in a finished batch: no batch is in flight during a rule load)
+        std::vector<NodeInfo> ni(members.size());
+        for (size_t k = 0; k < members.size(); ++k)
+            HIPCHK(hipMemcpy(&ni[k], e->d_info + members[k], sizeof(NodeInfo), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < members.size(); ++k) {
+            if (ni[k].flags & NI_CHAIN) ni[k].flags |= NI_TOUCHED;
+            HIPCHK(hipMemcpy(e->d_info + members[k], &ni[k], sizeof(NodeInfo), hipMemcpyHostToDevice));
+        }
+    }
     if (rules.size() > e->cfg.max_rules) return fail(SG_ECAPACITY, "compiled rule table exceeds max_rules");
     if (rules.size() > e->rules_cap) {
         dfree(e->d_rules); dfree(e->d_rstate);
@@ -749,6 +787,13 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
     if (!hot.empty()) HIPCHK(hipMemcpy(e->d_hot, hot.data(), hot.size() * sizeof(DHot), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->d_prog, prog.data(), R * sizeof(Prog), hipMemcpyHostToDevice));
     e->n_dev_rules = (uint32_t)rules.size();
+    if (comp.empty()) {
+        dfree(e->d_comp);
+        e->d_comp = nullptr;
+    } else {
+        if (!e->d_comp) HIPCHK(hipMalloc(&e->d_comp, (uint64_t)R * 4));
+        HIPCHK(hipMemcpy(e->d_comp, comp.data(), (uint64_t)R * 4, hipMemcpyHostToDevice));
+    }
     return SG_OK;
 }
 
@@ -884,7 +929,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
-    dfree(e->d_prio);
+    dfree(e->d_prio); dfree(e->d_comp);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
@@ -1038,6 +1083,11 @@ int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint
         uint32_t rid;
         int rc = register_rule_resource(e, r.resource, &rid);
         if (rc) return rc;
+        if (r.strategy == SG_STRATEGY_RELATE && r.ref_resource && *r.ref_resource) {  // its ClusterNode is read
+            uint32_t ref;
+            rc = register_rule_resource(e, r.ref_resource, &ref);
+            if (rc) return rc;
+        }
         std::string k = std::to_string(rid) + "#" + keys[i];
         if (seen.count(k)) continue; // HashSet.add of an equal rule
         seen[k] = 1;
@@ -1267,7 +1317,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     HIPCHK(hipMemsetAsync(e->d_bsmall, 0, 256 * 4, gs));
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, gs));
+                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, e->d_comp, gs));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
         if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, gs));
@@ -1312,7 +1362,8 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
-        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand, st));
+        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand,
+                            dev_ev, e->d_prog, st));
         if (!grant_all) {
             uint32_t ncand = 0;
             HIPCHK(hipMemcpyAsync(&ncand, e->d_bsmall + 2, 4, hipMemcpyDeviceToHost, st));
@@ -1321,13 +1372,16 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
                 std::vector<uint64_t> cand(ncand);
                 HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
                 std::sort(cand.begin(), cand.end());  // by batch index of the first ENTRY
-                std::vector<uint64_t> upd(ncand);
+                std::vector<uint64_t> upd;
+                std::unordered_map<uint32_t, int> seen;  // RELATE components list every ENTRY
                 for (uint32_t i = 0; i < ncand; ++i) {
                     uint32_t res = (uint32_t)cand[i];
+                    if (!seen.emplace(res, 1).second) continue;
                     bool grant = e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
                     if (grant) e->n_chains++;
-                    upd[i] = ((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63);
+                    upd.push_back(((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63));
                 }
+                ncand = (uint32_t)upd.size();
                 HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
                 HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
                 HIPCHK(hipStreamSynchronize(st));

@@ -38,7 +38,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                       uint32_t* __restrict__ ghist, uint32_t nblocks,
                                                       uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out,
-                                                      uint8_t* __restrict__ prio, uint64_t* __restrict__ key_ring) {
+                                                      uint8_t* __restrict__ prio, uint64_t* __restrict__ key_ring,
+                                                      const uint32_t* __restrict__ comp) {
     __shared__ uint32_t h[RS_BINS];
     for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
     __syncthreads();
@@ -87,9 +88,11 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             }
         }
         rec_o[i] = r;
-        keys[i] = e.res_id;
+        // sort key: the resource, or its STRATEGY_RELATE component's representative (one segment)
+        const uint32_t key = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
+        keys[i] = key;
         vals[i] = (uint32_t)i | (e.kind == SG_EV_ENTRY ? 0x80000000u : 0u);
-        atomicAdd(&h[e.res_id & (RS_BINS - 1)], 1u);
+        atomicAdd(&h[key & (RS_BINS - 1)], 1u);
     }
     if (fl) atomicOr(bflags, fl);
     __syncthreads();
@@ -379,9 +382,9 @@ namespace sg {
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
-                           uint64_t* key_ring, hipStream_t st) {
+                           uint64_t* key_ring, const uint32_t* comp, hipStream_t st) {
     hipLaunchKernelGGL(k_rs_first, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask, max_rt,
-                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring);
+                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,

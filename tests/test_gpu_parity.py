@@ -314,3 +314,32 @@ def test_async_pipeline(config, kw):
     _assert_same_decisions(dg, do, ev)
     _compare_nodes(w, eng, orc, _sample(w))
     assert len(eng.timing_log()) == len(parts)
+
+
+# ---------------------------------------------------------------- STRATEGY_RELATE (A13)
+def test_relate_components(bin_mode):
+    """FlowRuleChecker.selectReferenceNode RELATE (core/slots/block/flow/FlowRuleChecker.java:67-88): the
+    rule of A is checked against the ClusterNode of B; A's and B's events are decided in one sequence.
+    Pairs, a 3-chain, a self reference (the resource's own node) and a reference to a resource that is
+    never entered (no ClusterNode: pass)."""
+    w = T.Workload(2, n_entries=200_000, n_res=3_000)
+    names = ["res-%d" % i for i in range(w.n_res)]
+    rules = [A.flow_rule(nm, 15 + (i * 7) % 300) for i, nm in enumerate(names)]
+    cnt = np.bincount(w.events["res_id"], minlength=w.n_res)
+    hot = [int(x) for x in np.argsort(-cnt)[:40]]
+    for k in range(0, 30, 2):  # pairs among hot resources: a.relate(b)
+        a, b = hot[k], hot[k + 1]
+        rules.append(A.flow_rule(names[a], 20 + k, strategy=A.STRATEGY_RELATE, ref_resource=names[b]))
+    a, b, c = hot[30], hot[31], hot[32]  # chain a -> b -> c
+    rules.append(A.flow_rule(names[a], 25, strategy=A.STRATEGY_RELATE, ref_resource=names[b]))
+    rules.append(A.flow_rule(names[b], 40, strategy=A.STRATEGY_RELATE, ref_resource=names[c]))
+    rules.append(A.flow_rule(names[hot[33]], 30, strategy=A.STRATEGY_RELATE, ref_resource=names[hot[33]]))
+    rules.append(A.flow_rule(names[hot[34]], 1, strategy=A.STRATEGY_RELATE, ref_resource="never-entered"))
+    eng = _engine(max_resources=max(64, w.n_res + 8), max_slot_chain_size=0, param_table_log2=21)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for x in (eng, orc):
+        w.install(x)
+        x.load_flow_rules(rules)
+    dg, do = _replay(w, eng, orc, 3)
+    _assert_same_decisions(dg, do, w.events)
+    _compare_nodes(w, eng, orc, np.unique(np.concatenate([_sample(w), np.asarray(hot[:35])])))
