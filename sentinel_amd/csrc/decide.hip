@@ -86,7 +86,9 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
         else {
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
-            bin = (nr <= 4 ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
+            // k_lite: no param rules, <= 2 DefaultController flow stages (QPS or thread), <= 2 breakers
+            const bool lite = p.n_param == 0 && !p.multi && !prio[sg.res] && (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
+            bin = (lite ? BIN_LITE : nr <= 4 ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
         }
         const uint32_t rank = atomicAdd(&cnt[bin], 1u);
         sg.bin = bin | (rank << 8);
@@ -119,20 +121,52 @@ __global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, u
 // the inverse permutation written by the last radix pass (bit 31 = the referenced event is an
 // ENTRY).  A reference to a non-ENTRY resolves like an unknown entry in or_submit: an EXIT is then
 // taken as the caller asserting the entry passed, a TRACE as not counted.
-__global__ void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restrict__ vals, uint64_t n,
-                         const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs, uint32_t* __restrict__ prev,
-                         uint32_t* __restrict__ nprev) {
+// Side tables for frozen-stretch skipping (k_jac<..., SKIP>): the forward link of every referenced
+// ENTRY (an atomic exchange detects a second EXIT/TRACE naming the same ENTRY), and per 1024-position
+// block the ENTRY count sum plus a flag for EXIT/TRACEs that count without a same-batch link.
+__global__ __launch_bounds__(256) void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restrict__ vals,
+                                                uint64_t n, const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
+                                                uint32_t* __restrict__ prev, uint32_t* __restrict__ nprev,
+                                                Link* __restrict__ link, uint32_t* __restrict__ bst, uint32_t epoch,
+                                                uint32_t* __restrict__ bflags) {
+    __shared__ uint32_t wsum[4];
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    SEv r = rec_o[vals[p] & 0x7FFFFFFFu];
-    if (r.code == RC_BATCH) {
-        const uint32_t po = pos_of[r.x];
-        if (po & 0x80000000u) r.x = po & 0x7FFFFFFFu;
-        else r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-    } else if (r.code == RC_PREV) {
-        prev[atomicAdd(nprev, 1u)] = (uint32_t)p;
+    uint32_t ecnt = 0;
+    bool stat = false;
+    if (p < n) {
+        SEv r = rec_o[vals[p] & 0x7FFFFFFFu];
+        if (r.code == RC_BATCH) {
+            const uint32_t po = pos_of[r.x];
+            if (po & 0x80000000u) r.x = po & 0x7FFFFFFFu;
+            else r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+        } else if (r.code == RC_PREV) {
+            prev[atomicAdd(nprev, 1u)] = (uint32_t)p;
+        }
+        if (r.kind == SG_EV_ENTRY) {
+            ecnt = r.cnt;
+            if (r.cnt == 0) atomicOr(bflags, BF_ZERO_CNT);
+        } else if (r.code == RC_BATCH) {
+            unsigned long long* dst = reinterpret_cast<unsigned long long*>(
+                r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
+            const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
+            if ((uint32_t)(old >> 32) == epoch) atomicOr(bflags, BF_MULTI_LINK);
+        } else if (r.code == RC_NONE || r.code == RC_PREV) {
+            stat = true;
+        }
+        recs[p] = r;
     }
-    recs[p] = r;
+    // the block's 256 positions lie in one 1024-position block: one atomic per workgroup
+    uint32_t v = ecnt;
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    const bool st = __ballot(stat) != 0;
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v | (st ? BST_STATIC : 0u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0, fl = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { sum += wsum[w] & BST_CNT; fl |= wsum[w] & BST_STATIC; }
+        if (sum) atomicAdd(&bst[p >> 10], sum);
+        if (fl) atomicOr(&bst[p >> 10], fl);
+    }
 }
 // references into earlier batches, once those are decided: the ENTRY's status from the ring
 // (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
@@ -157,6 +191,43 @@ __global__ void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __re
     uint32_t d = dec[pos_of[i] & 0x7FFFFFFFu];
     out[i] = d;
     ring[(gbase + i) & ring_mask] = (uint8_t)(d & 0xFF);
+}
+
+// Verdicts of the frozen spans recorded by k_jac<..., SKIP> (the map half of a frozen stretch, spread
+// over the whole chip): every ENTRY blocks exactly as in k_jac's streaming frozen path.
+__global__ __launch_bounds__(256) void k_fill(const Span* __restrict__ spans, const uint32_t* __restrict__ nspan,
+                                              uint32_t cap, const SEv* __restrict__ recs, const Prog* __restrict__ prog,
+                                              const DRule* __restrict__ rules, uint32_t* __restrict__ dec) {
+    const uint32_t ns = *nspan < cap ? *nspan : cap;
+    for (uint32_t k = blockIdx.x; k < ns; k += gridDim.x) {
+        const Span sp = spans[k];
+        if (sp.e <= sp.s) continue;
+        const uint32_t res = sp.res & 0x7FFFFFFFu;
+        const bool cut = (sp.res >> 31) != 0;
+        const Prog pg = prog[res];
+        const int nf = pg.n_flow < 4 ? pg.n_flow : 4;
+        double fc[4];
+        uint32_t fd[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            fc[s] = s < nf ? rules[pg.rule_off + s].count : 0.0;
+            fd[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, rules[pg.rule_off + s].slot, 0) : 0u;
+        }
+        const uint32_t cdec = (cut && pg.n_degrade) ? mk_dec(ST_BLOCK_DEGRADE, rules[pg.rule_off + pg.n_flow].slot, 0) : 0u;
+        for (uint32_t p = sp.s + threadIdx.x; p < sp.e; p += blockDim.x) {
+            const uint4 r = reinterpret_cast<const uint4*>(recs)[p];
+            uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+            if ((r.w & 0xFFu) == SG_EV_ENTRY) {
+                const double curv = (double)j_iadd(sp.pint, (int)(r.z & 0xFFFFu));
+                uint32_t v = 0;
+#pragma unroll
+                for (int s = 3; s >= 0; --s)
+                    if (s < nf && curv > fc[s]) v = fd[s];
+                d = v ? v : cdec;
+            }
+            dec[p] = d;
+        }
+    }
 }
 
 // CtSph.lookProcessChain (core/CtSph.java:206-227): resources touched by this batch with neither a
@@ -468,6 +539,18 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
         return;
     }
     const int nr = pg.n_param + pg.n_flow + pg.n_degrade;
+#ifdef SG_KPROF
+    const bool kp = S.dbg && i == 0;  // the longest segment of the launch
+    unsigned long long kt0 = kp ? __builtin_amdgcn_s_memtime() : 0, kta = 0, ktb = 0, ktc = 0;
+#define LPROF(acc)                                                \
+    if (kp) {                                                     \
+        unsigned long long _n = __builtin_amdgcn_s_memtime();     \
+        acc += _n - kt0;                                          \
+        kt0 = _n;                                                 \
+    }
+#else
+#define LPROF(acc)
+#endif
     Node N;
     node_load(N, S, res);
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
@@ -482,6 +565,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     SEv rn[2];        // software prefetch, two events ahead
     rn[0] = recs[sg.start];
     if (sg.len > 1) rn[1] = recs[sg.start + 1];
+    LPROF(kta)
     for (uint32_t j = 0; j < sg.len; ++j) {
         const SEv r = rn[0];
         rn[0] = rn[1];
@@ -495,6 +579,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
                 d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
             }
             if (j < 64 && st_passed(d & 0xFF)) pm |= 1ull << j;
+            LPROF(ktb)
         } else {
             bool eff;
             if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
@@ -522,6 +607,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
                     stat_trace(N, C, t, r.cnt);
                 }
             }
+            LPROF(ktc)
         }
         dec[sg.start + j] = d;
     }
@@ -529,6 +615,123 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     node_store(N, S, res, pg.pflags);
 #pragma unroll
     for (int s = 0; s < NRMAX; ++s) if (s < nr) S.rstate[pg.rule_off + s] = rs[s];
+#ifdef SG_KPROF
+    if (kp) {
+        S.dbg[32] += kta; S.dbg[33] += ktb; S.dbg[34] += ktc; S.dbg[35] += sg.len; S.dbg[36] += 1;
+    }
+#endif
+#undef LPROF
+}
+
+// =================================================================================
+// k_lite: one lane per segment for the common rule shape -- DefaultController flow stages (QPS or
+// thread grade, FlowSlot.java:146-158 + DefaultController.java:49-81) and DegradeRule breakers, no
+// param rules, no prioritized entries, no STRATEGY_RELATE.  Same chain.h semantics as k_lane, but the
+// rules are read once per segment (not per event), the passed bits of the first 256 positions stay in
+// registers (EXITs of them never re-read dec[]), and the kernel carries none of the param / warm-up /
+// rate-limiter / borrow code, so its code fits the instruction cache and its state fits in VGPRs.
+// =================================================================================
+__global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const Seg sg = segs[order[i]];
+    const uint32_t res = sg.res;
+    const Prog pg = S.prog[res];
+    const int nf = pg.n_flow, nd = pg.n_degrade;  // <= 2 each (PF_J16)
+    const DRule* rules = S.rules + pg.rule_off;
+    // per-segment rule constants: flow thresholds, degrade grades/thresholds/windows
+    double fcnt[2] = {0.0, 0.0};
+    bool fthr[2] = {false, false};
+    uint32_t fslot[2] = {0, 0};
+    DRule dr[2];
+    RState ds[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k < nf) {
+            const DRule r = rules[k];
+            fcnt[k] = r.count;
+            fthr[k] = r.grade == SG_FLOW_GRADE_THREAD;
+            fslot[k] = r.slot;
+        }
+        if (k < nd) {
+            dr[k] = rules[nf + k];
+            ds[k] = S.rstate[pg.rule_off + nf + k];
+        }
+    }
+    Node N;
+    node_load(N, S, res);
+    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    const bool has_chain = (N.flags & NI_CHAIN) != 0;
+    const bool chain = has_chain && cfg.switch_on;
+    if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
+        atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
+    uint64_t pm0 = 0, pm1 = 0, pm2 = 0, pm3 = 0;  // passed bits of positions 0..255
+    SEv rn[3];  // software prefetch, three events ahead
+    rn[0] = recs[sg.start];
+    if (sg.len > 1) rn[1] = recs[sg.start + 1];
+    if (sg.len > 2) rn[2] = recs[sg.start + 2];
+    for (uint32_t j = 0; j < sg.len; ++j) {
+        const SEv r = rn[0];
+        rn[0] = rn[1];
+        rn[1] = rn[2];
+        if (j + 3 < sg.len) rn[2] = recs[sg.start + j + 3];
+        const int64_t t = t0 + r.dt;
+        uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+        if (r.kind == SG_EV_ENTRY) {
+            if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
+            else {
+                uint32_t status = ST_PASS, slot = 0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {  // FlowSlot: DefaultController on the ClusterNode
+                    if (k < nf && status == ST_PASS) {
+                        int32_t cur;
+                        if (fthr[k]) cur = N.thread;
+                        else { sec_current(N, t, C.max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
+                        if ((double)j_iadd(cur, (int)r.cnt) > fcnt[k]) { status = ST_BLOCK_FLOW; slot = fslot[k]; }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {  // DegradeSlot
+                    if (k < nd && status == ST_PASS && !degrade_pass(N, C, dr[k], ds[k], t)) {
+                        status = ST_BLOCK_DEGRADE;
+                        slot = dr[k].slot;
+                    }
+                }
+                const bool passed = status == ST_PASS;
+                stat_entry(N, C, t, r.cnt, passed);
+                d = passed ? mk_dec(ST_PASS, 0, 0) : mk_dec(status, slot, 0);
+                if (passed && j < 256) {
+                    const uint64_t b = 1ull << (j & 63);
+                    if (j < 64) pm0 |= b; else if (j < 128) pm1 |= b; else if (j < 192) pm2 |= b; else pm3 |= b;
+                }
+            }
+        } else {
+            bool eff;
+            if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
+            else if (r.code == RC_PASSED) eff = true;
+            else if (r.code == RC_NOT) eff = false;
+            else {
+                const uint32_t rel = r.x - sg.start;
+                if (rel >= j) { atomicOr(bflags, BF_BAD_REF); eff = false; }  // not an earlier ENTRY of this resource
+                else if (rel < 256) {
+                    const uint64_t w = rel < 64 ? pm0 : rel < 128 ? pm1 : rel < 192 ? pm2 : pm3;
+                    eff = ((w >> (rel & 63)) & 1) != 0;
+                } else eff = st_passed(dec[r.x] & 0xFF);  // written by this lane
+            }
+            if (eff) {
+                if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
+                else stat_trace(N, C, t, r.cnt);
+            }
+        }
+        dec[sg.start + j] = d;
+    }
+    min_flush(N, C.minb);
+    node_store(N, S, res, pg.pflags);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (k < nd) S.rstate[pg.rule_off + nf + k] = ds[k];
 }
 
 // =================================================================================
@@ -599,6 +802,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // u32 quantities scanned block-wide in one Jacobi iteration (counts <= 1024 are packed in halves)
 enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR /* trip counts, 2 per word */ };
 
+#define NSPAN 64        // skipped spans per segment (LDS list for references into them)
+
 template <int NW, int MF, int MD>
 struct JacSh {
     Node node;
@@ -617,6 +822,13 @@ struct JacSh {
     uint32_t pseg[NW][MD];
     int64_t prl[NW][4];
     uint32_t mism[2][NW];
+    // frozen-stretch skipping
+    uint32_t npend;            // live entries of the pending-pass list pend[start, start + npend)
+    uint32_t nsp;              // spans of this segment decided by k_fill (their dec[] words are not written yet)
+    uint32_t skip_go;
+    uint32_t pad2;
+    uint2 spn[NSPAN];          // [s, e) relative positions
+    unsigned long long fl[NW]; // flagged-block ballots
 };
 
 // leader: fold the round's committed deltas into the node (StatisticSlot bookkeeping of every
@@ -707,7 +919,7 @@ __device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, int n
     return mk_dec((int)o < nf ? ST_BLOCK_FLOW : ST_BLOCK_DEGRADE, rules[o].slot, 0);
 }
 
-template <int NW, int WINLOG, int MF, int MD, bool RL>
+template <int NW, int WINLOG, int MF, int MD, bool RL, bool SKIP>
 __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                                 const uint32_t* __restrict__ order, uint32_t m, DevState S,
                                                 DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec,
@@ -717,7 +929,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     constexpr int NQ = Q_TR + (MD + 1) / 2;
     static_assert(WIN >= 2 * HW, "status window must hold two tiles");
     __shared__ JacSh<NW, MF, MD> sh;
-    __shared__ uint8_t win[WIN];
+    __shared__ __attribute__((aligned(16))) uint8_t win[WIN];
     if (blockIdx.x >= m) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -732,6 +944,8 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         sh.round_open = 0;
         sh.c0 = 0;
         sh.last_out = (uint32_t)nr;
+        sh.npend = 0;
+        sh.nsp = 0;
     }
     if ((int)tid < nr) {
         sh.rules[tid] = S.rules[pg.rule_off + tid];
@@ -788,6 +1002,15 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
     if (HW + tid < sg.len) nxt = recs[sg.start + HW + tid];
     bool valid = false, eff_win = false, eff_val = false;
     uint32_t winidx = 0, refrel = 0, kind = 0xFF, cnt = 0, rtv = 0;
+    const bool skip_on = SKIP && S.skip_ok && (pg.pflags & PF_FROZEN);
+    // positions of skipped spans: blocked ENTRYs whose dec[] words k_fill writes after this kernel
+    auto in_span = [&](uint32_t rel) -> bool {
+        if (!SKIP) return false;
+        const uint32_t ns = sh.nsp;
+        for (uint32_t i = 0; i < ns; ++i)
+            if (rel >= sh.spn[i].x && rel < sh.spn[i].y) return true;
+        return false;
+    };
     int32_t dt = 0;  // event time relative to t0 (the absolute time is t0 + dt)
     auto decode = [&](const SEv& r, uint32_t pos) {
         valid = pos < sg.len;
@@ -805,7 +1028,8 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                 if (refrel >= pos) { atomicOr(bflags, BF_BAD_REF); refrel = 0; }  // not an earlier ENTRY of this resource
                 if (refrel + WIN >= tbase + HW) { eff_win = true; winidx = refrel & (WIN - 1); }
                 else  // decided >= WIN-HW positions ago, i.e. before >= 1 full fence
-                    eff_val = st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                    eff_val = !in_span(refrel) &&
+                              st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
             }
         }
     };
@@ -890,10 +1114,172 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     fdec[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, sh.rules[s].slot, 0) : 0u;
                 }
                 const uint32_t cdec = nd > 0 ? mk_dec(ST_BLOCK_DEGRADE, sh.rules[nf].slot, 0) : 0u;
-                const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
                 uint32_t aB = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aMin = NO_LANE, aTH = 0;
+                uint32_t fend = 0;
+                bool skipped = false;
+                // ---- skip: a long stretch is not streamed through this CU.  Its end is found by a
+                // block-wide search over event times, its ENTRY counts come from per-block sums (k_gather),
+                // its effective EXIT/TRACEs are the same-batch EXIT/TRACEs of the passes this owner
+                // committed (pending list + forward links) plus the few that count without a link
+                // (streamed), and k_fill writes its verdicts after the decide kernels.
+                if (skip_on && sg.len - fpos0 > S.skip_min && uni(sh.nsp) < NSPAN) {
+                    if (tid == 0) sh.skip_go = (int64_t)recs[sg.start + fpos0 + S.skip_min].dt < dhi ? 1u : 0u;
+                    lds_barrier();
+                    if (uni(sh.skip_go)) {
+                        // (1) stretch end E = first position with dt >= dhi (dt is non-decreasing); dt[lo] < dhi
+                        uint32_t lo = fpos0, hi = sg.len;
+                        while (hi - lo > 1) {
+                            const uint32_t step = (hi - lo + HW - 1) / HW;
+                            const uint32_t q = lo + (tid + 1) * step;
+                            const bool pr = q < hi && (int64_t)recs[sg.start + q].dt >= dhi;
+                            const uint64_t bm = __ballot(pr);
+                            if (lane == 0) sh.mism[mb][wv] = bm ? wv * 64 + (uint32_t)(__ffsll((long long)bm) - 1) : NO_LANE;
+                            lds_barrier();
+                            uint32_t f = NO_LANE;
+                            for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                            f = uni(f);
+                            mb ^= 1;
+                            if (f == NO_LANE) {
+                                uint32_t kl = (hi - 1 - lo) / step;
+                                if (kl > HW) kl = HW;
+                                lo += kl * step;
+                            } else {
+                                hi = lo + (f + 1) * step;
+                                lo = lo + f * step;
+                            }
+                        }
+                        const uint32_t E = hi;
+                        const uint32_t A = sg.start + fpos0, B = sg.start + E;  // absolute positions
+                        const uint32_t nch = (B - A + SPAN_CHUNK - 1) / SPAN_CHUNK;
+                        // (2) span slots for k_fill; on overflow stream instead (slots already taken are voided)
+                        if (tid == 0) {
+                            const uint32_t base = atomicAdd(S.nspan, nch);
+                            sh.skip_go = base + nch <= S.span_cap ? base : NO_LANE;
+                            if (base < S.span_cap && base + nch > S.span_cap)
+                                for (uint32_t k = base; k < S.span_cap; ++k) S.spans[k] = Span{0u, 0u, 0u, 0};
+                        }
+                        lds_barrier();
+                        const uint32_t sbase = uni(sh.skip_go);
+                        if (sbase != NO_LANE) {
+                            skipped = true;
+                            fend = E;
+                            for (uint32_t c = tid; c < nch; c += HW) {
+                                Span sp;
+                                sp.s = A + c * SPAN_CHUNK;
+                                sp.e = B - sp.s < SPAN_CHUNK ? B : sp.s + SPAN_CHUNK;
+                                sp.res = res | (cutk0 ? 0x80000000u : 0u);
+                                sp.pint = pint;
+                                S.spans[sbase + c] = sp;
+                            }
+                            // (3) ENTRY counts and link-free EXIT/TRACEs: edge blocks and flagged blocks are
+                            // streamed, the other whole blocks contribute their k_gather count sums
+                            auto stat_ev = [&](uint32_t p) {
+                                const uint4 r = reinterpret_cast<const uint4*>(recs)[p];
+                                const uint32_t ek = r.w & 0xFFu, ec = r.z & 0xFFFFu, ert = r.z >> 16;
+                                const uint32_t code = (r.w >> 16) & 0xFFu;
+                                if (ek == SG_EV_ENTRY) { aB += ec; aTI += 1; }
+                                else if (code == RC_NONE || code == RC_PASSED) {
+                                    if (ek == SG_EV_EXIT) { aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1; }
+                                    else if (ec > 0) { aE += ec; aTI += 1; }
+                                }
+                            };
+                            const uint32_t fb = (A + 1023) >> 10, lb = B >> 10;
+                            if (fb >= lb) {
+                                for (uint32_t p = A + tid; p < B; p += HW) stat_ev(p);
+                            } else {
+                                for (uint32_t p = A + tid; p < (fb << 10); p += HW) stat_ev(p);
+                                for (uint32_t p = (lb << 10) + tid; p < B; p += HW) stat_ev(p);
+                                for (uint32_t k0 = fb; k0 < lb; k0 += HW) {
+                                    const uint32_t k = k0 + tid;
+                                    const uint32_t w = k < lb ? S.bst[k] : 0u;
+                                    const bool flg = (w & BST_STATIC) != 0;
+                                    if (!flg && (w & BST_CNT)) { aB += w & BST_CNT; aTI += 1; }
+                                    const uint64_t bm = __ballot(flg);
+                                    if (lane == 0) sh.fl[wv] = bm;
+                                    lds_barrier();
+                                    for (uint32_t w2 = 0; w2 < (uint32_t)NW; ++w2) {
+                                        uint64_t m2 = (uint64_t)uni64((int64_t)sh.fl[w2]);
+                                        while (m2) {
+                                            const uint32_t b = (uint32_t)(__ffsll((long long)m2) - 1);
+                                            m2 &= m2 - 1;
+                                            const uint32_t blk = k0 + w2 * 64 + b;
+                                            for (uint32_t p = (blk << 10) + tid; p < ((blk + 1) << 10); p += HW) stat_ev(p);
+                                        }
+                                    }
+                                    lds_barrier();  // sh.fl is rewritten by the next chunk
+                                }
+                            }
+                            // (4) pending passes: EXIT/TRACEs inside [A, B) count, those beyond B stay pending
+                            const uint32_t np = uni(sh.npend);
+                            uint32_t kept = 0;
+                            for (uint32_t k0 = 0; k0 < np; k0 += HW) {
+                                const uint32_t k = k0 + tid;
+                                bool keep = false;
+                                uint32_t item = 0;
+                                if (k < np) {
+                                    item = S.pend[sg.start + k];
+                                    const Link L = S.link[sg.start + item];
+                                    const uint32_t me = sg.start + item;
+                                    if ((uint32_t)(L.exit_l >> 32) == S.epoch) {
+                                        const uint32_t x = (uint32_t)L.exit_l;
+                                        if (x >= B) keep = true;
+                                        else if (x >= A) {
+                                            const SEv r = recs[x];
+                                            if (r.code == RC_BATCH && r.x == me && r.kind == SG_EV_EXIT) {
+                                                aS += r.cnt; aRT += r.rt; aTH -= 1; aMin = op_min(aMin, (uint32_t)r.rt); aTI += 1;
+                                            }
+                                        }
+                                    }
+                                    if ((uint32_t)(L.trace_l >> 32) == S.epoch) {
+                                        const uint32_t x = (uint32_t)L.trace_l;
+                                        if (x >= B) keep = true;
+                                        else if (x >= A) {
+                                            const SEv r = recs[x];
+                                            if (r.code == RC_BATCH && r.x == me && r.kind == SG_EV_TRACE && r.cnt > 0) {
+                                                aE += r.cnt; aTI += 1;
+                                            }
+                                        }
+                                    }
+                                }
+                                const uint64_t km = __ballot(keep);
+                                if (lane == 0) sh.mism[mb][wv] = (uint32_t)__popcll(km);
+                                lds_barrier();
+                                uint32_t before = 0, tot = 0;
+                                for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                                    const uint32_t c = sh.mism[mb][w];
+                                    if (w < wv) before += c;
+                                    tot += c;
+                                }
+                                mb ^= 1;
+                                if (keep) S.pend[sg.start + kept + before + (uint32_t)__popcll(km & lanemask_lt())] = item;
+                                kept += uni(tot);
+                            }
+                            // (5) statuses of the span's ENTRYs as later EXITs see them: blocked
+                            {
+                                const uint32_t lo2 = (E > WIN && E - WIN > fpos0) ? E - WIN : fpos0;
+                                const uint32_t a4 = (lo2 + 3) & ~3u, b4 = E & ~3u;
+                                if (a4 <= b4) {
+                                    if (tid < a4 - lo2) win[(lo2 + tid) & (WIN - 1)] = 0;
+                                    if (tid < E - b4) win[(b4 + tid) & (WIN - 1)] = 0;
+                                    uint32_t* w32 = reinterpret_cast<uint32_t*>(win);
+                                    for (uint32_t q = a4 / 4 + tid; q < b4 / 4; q += HW) w32[q & (WIN / 4 - 1)] = 0;
+                                } else if (tid < E - lo2) {
+                                    win[(lo2 + tid) & (WIN - 1)] = 0;
+                                }
+                            }
+                            lds_barrier();  // every wave has read sh.npend / sh.nsp
+                            if (tid == 0) {
+                                sh.npend = kept;
+                                sh.spn[sh.nsp] = make_uint2(fpos0, E);
+                                sh.nsp += 1;
+                            }
+                        }
+                    }
+                }
+                if (!skipped) {
+                const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
                 uint4 rr[EPL], rn[EPL];
-                uint32_t sb = fpos0, fend, nst = 0;
+                uint32_t sb = fpos0, nst = 0;
                 // loads are unconditional (clamped index): predicated loads would make the compiler's
                 // waitcnt analysis drain the prefetch (vmcnt(0)) before the current tile is touched
                 const uint32_t qmax = sg.len - 1;
@@ -959,7 +1345,8 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                                     if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
                                     else if (rel >= fpos0) eff = false;  // an ENTRY of this stretch: blocked
                                     else if (rel + WIN >= sb + ST) eff = win[rel & (WIN - 1)] != 0;
-                                    else eff = st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
+                                    else eff = !in_span(rel) &&
+                                               st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
                                                                            __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
                                 }
                                 win[q & (WIN - 1)] = 0;
@@ -979,6 +1366,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     for (int k = 0; k < (int)EPL; ++k) rr[k] = rn[k];
                     if (++nst % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
                 }
+                }  // !skipped
                 PROF_MARK(7)
                 // stretch end: reduce the lane accumulators into the round's committed totals
                 WAVE_SCAN(aB, 0u, op_add);
@@ -1243,6 +1631,16 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         const bool com = inr && tid < cend;
         const uint32_t fo = (tid == f) ? o : g;
         const uint32_t pos = tbase + tid;
+        if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
+            const bool app = com && kind == SG_EV_ENTRY && fo == (uint32_t)nr;
+            const uint64_t am = __ballot(app);
+            if (am) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&sh.npend, (uint32_t)__popcll(am));
+                base = (uint32_t)__shfl((int)base, 0, 64);
+                if (app) S.pend[sg.start + base + (uint32_t)__popcll(am & lanemask_lt())] = pos;
+            }
+        }
         if (com) {
             const uint32_t d = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wait) : mk_dec(ST_NOT_ENTRY, 0, 0);
             dec[sg.start + pos] = d;
@@ -1380,9 +1778,18 @@ hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t
     return hipGetLastError();
 }
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         uint32_t* prev, uint32_t* nprev, hipStream_t st) {
+                         uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst, uint32_t epoch, uint32_t* bflags,
+                         hipStream_t st) {
     uint32_t nb = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev);
+    hipError_t e = hipMemsetAsync(bst, 0, ((n + 1023) / 1024) * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev, link, bst, epoch,
+                       bflags);
+    return hipGetLastError();
+}
+hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,
+                       const DRule* rules, uint32_t* dec, hipStream_t st) {
+    hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, st, spans, nspan, cap, recs, prog, rules, dec);
     return hipGetLastError();
 }
 hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st) {
@@ -1412,16 +1819,19 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     switch (bin) {
     case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
                    // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS
-        hipLaunchKernelGGL((k_jac<16, 17, 2, 2, false>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
+        hipLaunchKernelGGL((k_jac<16, 17, 2, 2, false, true>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
                            dec, bflags);
         break;
     case BIN_J4:
-        hipLaunchKernelGGL((k_jac<4, 14, JMAX_FLOW, JMAX_DEG, true>), dim3(m), dim3(256), 0, st, recs, segs, order, m, S,
+        hipLaunchKernelGGL((k_jac<4, 14, JMAX_FLOW, JMAX_DEG, true, true>), dim3(m), dim3(256), 0, st, recs, segs, order, m, S,
                            cfg, t0, dec, bflags);
         break;
     case BIN_J1:
-        hipLaunchKernelGGL((k_jac<1, 12, JMAX_FLOW, JMAX_DEG, true>), dim3(m), dim3(64), 0, st, recs, segs, order, m, S,
+        hipLaunchKernelGGL((k_jac<1, 12, JMAX_FLOW, JMAX_DEG, true, false>), dim3(m), dim3(64), 0, st, recs, segs, order, m, S,
                            cfg, t0, dec, bflags);
+        break;
+    case BIN_LITE:
+        hipLaunchKernelGGL(k_lite, dim3((m + 255) / 256), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
         break;
     case BIN_LANE:
         hipLaunchKernelGGL(k_lane<4>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg,

@@ -168,6 +168,23 @@ struct NsLimiter {
     int64_t cnt[NS_BUCKETS];
 };
 
+// Forward links of one ENTRY (k_gather): (epoch << 32) | sorted position of the EXIT / TRACE of the same
+// batch whose reference names it.  A tag from another batch means "no link".
+struct Link {
+    uint64_t exit_l;
+    uint64_t trace_l;
+};
+// A frozen span [s, e) of sorted positions (<= SPAN_CHUNK of them) whose verdicts k_fill writes: every
+// ENTRY blocks on the first flow stage its count exceeds at pass count pint, else on the first degrade
+// stage when that breaker was cut (res bit 31).
+struct Span {
+    uint32_t s, e, res;
+    int32_t pint;
+};
+#define SPAN_CHUNK 8192u
+#define BST_STATIC 0x80000000u  // bst[] flag: the block holds an EXIT/TRACE that is effective without a link
+#define BST_CNT 0x7FFFFFFFu
+
 struct DevState {
     Bkt* sec;
     int64_t* borrow;          // [res][2 slots] x {ws, pass}: FutureBucketLeapArray of the second window
@@ -185,10 +202,22 @@ struct DevState {
     uint8_t* ring;
     unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
     uint32_t* sink;           // >= 1024 scratch words: target of masked-off unconditional stores
+    // frozen-stretch skipping (decide.hip k_jac<..., SKIP>): side tables of the batch built by k_gather
+    const Link* link;         // [sorted pos of an ENTRY] -> the EXIT / TRACE of this batch that references it
+    const uint32_t* bst;      // [pos >> 10] ENTRY count sum of the 1024-position block | BST_STATIC
+    uint32_t* pend;           // [sorted pos] per-segment list of the owner's committed passes (relative positions)
+    Span* spans;              // frozen spans whose verdicts k_fill writes after the decide kernels
+    uint32_t* nspan;          // span counter (may exceed span_cap: overflow falls back to streaming)
+    uint32_t span_cap;
+    uint32_t epoch;           // tag of this batch's links
+    uint32_t skip_ok;         // 0: no skipping this batch (links not unique / zero-count ENTRYs / SG_DEBUG_FLAGS & 4)
+    uint32_t skip_min;        // a stretch is skipped only if it holds more positions than this (SG_SKIP_MIN)
 };
 
 enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
-                  BF_BACKWARD = 32, BF_TSPAN = 64 };
+                  BF_BACKWARD = 32, BF_TSPAN = 64,
+                  BF_MULTI_LINK = 128,  // an ENTRY is referenced by two EXITs (or two TRACEs) of the batch
+                  BF_ZERO_CNT = 256 };  // an ENTRY acquires 0 (it may pass inside a saturated stretch)
 
 // One event in resource-sorted order (16 B), built by k_prep from the caller's 24-byte
 // sg_event so that every decide kernel streams its segment with coalesced loads.
@@ -221,7 +250,8 @@ enum : uint32_t {
     BIN_LANE = 3,          // one lane per segment, nr <= 4: bins 3..3+LANE_BINS-1 by descending log2(len)
     LANE_BINS = 20,
     BIN_LANE16 = BIN_LANE + LANE_BINS,  // one lane per segment, nr > 4 (rule state in scratch)
-    N_BINS = BIN_LANE16 + LANE_BINS
+    BIN_LITE = BIN_LANE16 + LANE_BINS,  // one lane per segment, DefaultController flows + breakers only (k_lite)
+    N_BINS = BIN_LITE + LANE_BINS       // <= 63: k_bin_offsets runs one 64-lane wave
 };
 
 } // namespace sg

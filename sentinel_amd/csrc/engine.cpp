@@ -47,7 +47,10 @@ hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, c
 hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
                             hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         uint32_t* prev, uint32_t* nprev, hipStream_t st);
+                         uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst, uint32_t epoch, uint32_t* bflags,
+                         hipStream_t st);
+hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,
+                       const DRule* rules, uint32_t* dec, hipStream_t st);
 hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st);
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
@@ -439,6 +442,10 @@ struct sg_engine {
         Seg* d_segs = nullptr;
         uint64_t* d_cand = nullptr;
         uint32_t* d_bsmall = nullptr;  // [0] bflags [1] nseg [2] ncand [3] nprev [4..5] t0 [8..8+N_BINS] bin offsets
+                                       // [120] frozen spans recorded
+        Link* d_link = nullptr;        // frozen-stretch skipping side tables (DevState.link/bst/pend/spans)
+        uint32_t *d_bst = nullptr, *d_pend = nullptr;
+        Span* d_spans = nullptr;
         hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // group start/end, decide start/end, post end
         bool pending = false;  // decide enqueued, not yet collected (timings, flags)
     } slot[2];
@@ -450,6 +457,12 @@ struct sg_engine {
     uint32_t* d_comp = nullptr;  // [res] STRATEGY_RELATE component representative (sort key); null: none
     uint32_t* d_prev = nullptr;
     uint32_t* d_bsmall = nullptr;
+    Link* d_link = nullptr;
+    uint32_t *d_bst = nullptr, *d_pend = nullptr;
+    Span* d_spans = nullptr;
+    uint32_t span_cap = 0;
+    uint32_t epoch = 0;          // link tag of the batch being grouped
+    uint64_t spans_total = 0;    // frozen span slots taken by the cooperative kernels (diagnostics)
     uint64_t cap_n = 0;
     sg_event* d_ev = nullptr;
     uint32_t* d_out = nullptr;
@@ -477,6 +490,7 @@ struct sg_engine {
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     bool pipeline = false;  // SG_PIPELINE=1: the group stage of batch k+1 overlaps the decide stage of batch k
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
+    uint32_t skip_min = 12288;  // frozen stretches shorter than this are streamed, not skipped
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
     std::vector<CFlow> cflows;                    // host copy of the config part (state lives on the device)
@@ -507,12 +521,15 @@ static void activate(sg_engine* e, int k) {
     e->d_posof = B.d_posof; e->d_dec = B.d_dec; e->d_blkcnt = B.d_blkcnt; e->d_prev = B.d_prev;
     e->d_recs = B.d_recs; e->d_rec_o = B.d_rec_o; e->d_segs = B.d_segs; e->d_cand = B.d_cand;
     e->d_bsmall = B.d_bsmall;
+    e->d_link = B.d_link; e->d_bst = B.d_bst; e->d_pend = B.d_pend; e->d_spans = B.d_spans;
 }
 static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_ev); dfree(B.d_out); dfree(B.d_k0); dfree(B.d_v0); dfree(B.d_k1); dfree(B.d_v1);
     dfree(B.d_hist); dfree(B.d_part); dfree(B.d_flag); dfree(B.d_pos); dfree(B.d_order); dfree(B.d_segs);
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
     dfree(B.d_prev); dfree(B.d_bsmall);
+    dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans);
+    B.d_link = nullptr; B.d_bst = B.d_pend = nullptr; B.d_spans = nullptr;
     B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
     B.d_hist = B.d_part = B.d_flag = B.d_pos = B.d_order = nullptr;
     B.d_posof = B.d_dec = B.d_blkcnt = B.d_prev = B.d_bsmall = nullptr;
@@ -547,7 +564,13 @@ int ensure_batch(sg_engine* e, uint64_t n) {
         HIPCHK(hipMalloc(&B.d_prev, c * 4));
         HIPCHK(hipMalloc(&B.d_bsmall, 256 * 4));
         HIPCHK(hipMemset(B.d_bsmall, 0, 256 * 4));
+        HIPCHK(hipMalloc(&B.d_link, c * sizeof(Link)));
+        HIPCHK(hipMemset(B.d_link, 0, c * sizeof(Link)));  // tag 0 is never a batch's epoch
+        HIPCHK(hipMalloc(&B.d_bst, ((c + 1023) / 1024 + 1) * 4));
+        HIPCHK(hipMalloc(&B.d_pend, c * 4));
+        HIPCHK(hipMalloc(&B.d_spans, (c / SPAN_CHUNK + 65536) * sizeof(Span)));
     }
+    e->span_cap = (uint32_t)(c / SPAN_CHUNK + 65536);
     e->cap_n = c;
     activate(e, e->cur);
     return SG_OK;
@@ -569,7 +592,10 @@ static int collect(sg_engine* e, int k) {
     if (e->tlog.size() > 4096) e->tlog.erase(e->tlog.begin(), e->tlog.begin() + 2048);
     uint32_t bflags = 0;  // on gstream: a null-stream copy could share a queue with a decide kernel
     HIPCHK(hipMemcpyAsync(&bflags, B.d_bsmall, 4, hipMemcpyDeviceToHost, e->gstream));
+    uint32_t nspan = 0;
+    HIPCHK(hipMemcpyAsync(&nspan, B.d_bsmall + 120, 4, hipMemcpyDeviceToHost, e->gstream));
     HIPCHK(hipStreamSynchronize(e->gstream));
+    e->spans_total += nspan;
     if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
     return SG_OK;
 }
@@ -895,6 +921,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J4_MAX")) e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
+    if (const char* v = std::getenv("SG_SKIP_MIN")) e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
     *out = e;
     return SG_OK;
 }
@@ -911,6 +938,12 @@ extern "C" int sgx_timing_log(sg_engine* e, double* out, int cap) {
         for (int j = 0; j < 4; ++j) out[4 * k + j] = e->tlog[k][j];
     e->tlog.clear();
     return k;
+}
+// diagnostics export (not part of the ABI): frozen span slots recorded by the cooperative kernels so far
+extern "C" unsigned long long sgx_spans_total(sg_engine* e) {
+    if (!e) return 0;
+    (void)drain(e);
+    return e->spans_total;
 }
 extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap) {
     if (!e || !e->d_dbg || !out) return 0;
@@ -1329,7 +1362,9 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     }
     // ---- 2. segments + 16-byte sorted records
     HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, gs, launch_scan, e->d_part, e->d_bsmall + 1));
-    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, gs));
+    if (++e->epoch == 0) e->epoch = 1;
+    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link, e->d_bst,
+                         e->epoch, e->d_bsmall + 0, gs));
     uint32_t head[6];
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
     HIPCHK(hipStreamSynchronize(gs));
@@ -1415,6 +1450,15 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.prio = e->d_prio;
     S.key_ring = e->d_keyring;
     S.gbase = e->gbase;
+    S.link = e->d_link;
+    S.bst = e->d_bst;
+    S.pend = e->d_pend;
+    S.spans = e->d_spans;
+    S.nspan = e->d_bsmall + 120;
+    S.span_cap = e->span_cap;
+    S.epoch = e->epoch;
+    S.skip_ok = !(bflags & (BF_MULTI_LINK | BF_ZERO_CNT)) && !(e->dbg_flags & 4) ? 1u : 0u;
+    S.skip_min = e->skip_min;
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
     for (int c = 0; c < 3; ++c) {
@@ -1428,12 +1472,21 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
                                  e->d_dec, e->d_bsmall + 0, e->bin_stream[q]));
         HIPCHK(hipEventRecord(e->join[q], e->bin_stream[q]));
     }
-    HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
-                             off[BIN_LANE + LANE_BINS] - off[BIN_LANE], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    {
+        DevState Sl = S;
+        Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..36]
+        HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
+                                 off[BIN_LANE + LANE_BINS] - off[BIN_LANE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    }
     HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
                              off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
+                             off[BIN_LITE + LANE_BINS] - off[BIN_LITE], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
     for (int c = 0; c < 3; ++c)
         if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c == 0 ? 0 : 1], 0));
+    // verdicts of the frozen spans the cooperative kernels skipped
+    if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J4]))
+        HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));

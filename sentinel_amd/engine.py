@@ -175,6 +175,13 @@ class Engine:
         k = fn(self.h, buf, cap)
         return np.frombuffer(buf, dtype=np.float64, count=4 * k).reshape(k, 4).copy()
 
+    def spans_total(self) -> int:
+        """Frozen span slots the cooperative kernels recorded so far (diagnostics export sgx_spans_total)."""
+        fn = lib().sgx_spans_total
+        fn.restype = C.c_ulonglong
+        fn.argtypes = [C.c_void_p]
+        return int(fn(self.h))
+
     def read_node(self, res: int, now: int = 0) -> dict:
         st = A.SgNodeState()
         _check(lib().sg_read_node(self.h, res, now, C.byref(st)))

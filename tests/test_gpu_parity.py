@@ -69,6 +69,8 @@ BIN_MODES = {
     "coop": {"SG_LANE_MAX": "0", "SG_J1_MAX": "40", "SG_J4_MAX": "400"},
     # every segment through the one-lane-per-segment kernel
     "lane": {"SG_DEBUG_FLAGS": "2"},
+    # cooperative kernels skipping every frozen stretch longer than 16 positions (k_fill writes the verdicts)
+    "skip": {"SG_LANE_MAX": "0", "SG_J1_MAX": "40", "SG_J4_MAX": "400", "SG_SKIP_MIN": "16"},
 }
 
 
@@ -343,3 +345,15 @@ def test_relate_components(bin_mode):
     dg, do = _replay(w, eng, orc, 3)
     _assert_same_decisions(dg, do, w.events)
     _compare_nodes(w, eng, orc, np.unique(np.concatenate([_sample(w), np.asarray(hot[:35])])))
+
+
+@pytest.mark.parametrize("skip_min", ["16", "1000"])
+@pytest.mark.parametrize("config", [2, 4])
+def test_frozen_skip_hot_resources(config, skip_min, monkeypatch):
+    # a few very hot resources: long saturated / breaker-cut stretches that the cooperative kernels
+    # skip (stretch end by search, block count sums, pending passes + forward links, k_fill verdicts),
+    # with EXITs referencing entries before, inside and after the skipped spans, across batches
+    for k, v in {"SG_LANE_MAX": "0", "SG_J1_MAX": "40", "SG_J4_MAX": "2000", "SG_SKIP_MIN": skip_min}.items():
+        monkeypatch.setenv(k, v)
+    w, eng, orc, d = _run(config, batches=3, n_entries=300_000, n_res=12)
+    assert eng.spans_total() > 0  # the skip path ran

@@ -27,14 +27,14 @@ ev = w.events
 B = min(len(ev) // nb, 1 << 25)
 L = E.lib()
 L.sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-prev = np.zeros(24, dtype=np.uint64)
+prev = np.zeros(64, dtype=np.uint64)
 for i in range(nb):
     print("submit batch", i, flush=True)
     t = time.time()
     eng.submit(ev[i * B:(i + 1) * B])
     tm = eng.timings()
-    buf = (C.c_ulonglong * 24)()
-    L.sgx_debug_counters(eng.h, buf, 24)
+    buf = (C.c_ulonglong * 64)()
+    L.sgx_debug_counters(eng.h, buf, 64)
     v = np.array(list(buf), dtype=np.uint64)
     d = v - prev
     prev = v
@@ -45,3 +45,6 @@ for i in range(nb):
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
     print("  longest segment (len %d) phase cycles:" % v[5], {k: "%.0f" % ph[j] for j, k in enumerate(names)})
     print("  frozen tiles (all J16 segments):", d[6])
+    if d[36]:
+        print("  k_lane longest segment: len %d, cycles start %d entries %d exits %d (per event %.0f)" %
+              (d[35], d[32], d[33], d[34], (d[32] + d[33] + d[34]) / max(1, d[35])))
