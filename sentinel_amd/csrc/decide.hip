@@ -822,6 +822,7 @@ struct JacSh {
     uint32_t pseg[NW][MD];
     int64_t prl[NW][4];
     uint32_t mism[2][NW];
+    uint32_t mo[2][NW];        // evaluated outcome of each wave's first mismatching lane
     // frozen-stretch skipping
     uint32_t npend;            // live entries of the pending-pass list pend[start, start + npend)
     uint32_t nsp;              // spans of this segment decided by k_fill (their dec[] words are not written yet)
@@ -983,6 +984,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
 #ifdef SG_KPROF
     const bool prof0 = prof && tid == 0;  // every block times itself; the longest segment reports
     unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long tm_start = tmA;
 #define PROF_MARK(k)                                          \
     if (prof0) {                                              \
         unsigned long long _n = __builtin_amdgcn_s_memtime(); \
@@ -1616,14 +1618,28 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         {
             const uint64_t mm = __ballot(ent && o != g);
             if (lane == 0) sh.mism[mb][wv] = mm ? wv * 64 + (uint32_t)(__ffsll((long long)mm) - 1) : NO_LANE;
+            if (mm && lane == (uint32_t)(__ffsll((long long)mm) - 1)) sh.mo[mb][wv] = o;
         }
         PROF_MARK(3)
         lds_barrier();  // B4
         uint32_t f = NO_LANE;
         for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
-                    f = uni(f);
+        f = uni(f);
+        // the pivot's true outcome: the re-guess of every later ENTRY of the round.  Their own evaluated
+        // outcomes saw the pivot's wrong guess (e.g. a guessed breaker trip blocks everything after it),
+        // while a state change at the pivot (reset breaker, spent quota, trip) mostly holds for the rest.
+        const uint32_t of = f != NO_LANE ? uni(sh.mo[mb][f >> 6]) : 0u;
         mb ^= 1;
         if (f != NO_LANE) ++n_mm;
+#ifdef SG_KPROF
+        if (prof && tid == f) {  // what the first mismatching lane guessed and evaluated (0 pass, 1 flow, 2 degrade)
+            const uint32_t gc = g == (uint32_t)nr ? 0u : g < (uint32_t)nf ? 1u : 2u;
+            const uint32_t oc = o == (uint32_t)nr ? 0u : o < (uint32_t)nf ? 1u : 2u;
+            atomicAdd(&S.dbg[40 + 3 * gc + oc], 1ull);
+            if (f > c0) atomicAdd(&S.dbg[49], 1ull);  // the mismatch is not at the first uncommitted lane
+            atomicAdd(&S.dbg[50], (unsigned long long)(f - c0));
+        }
+#endif
         const uint32_t e_end = c0 + inr_total;
         const uint32_t cend = f != NO_LANE ? f + 1 : e_end;
 
@@ -1647,8 +1663,8 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
             win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
             g = fo;
         } else if (ent) {
-            g = o;
-            win[pos & (WIN - 1)] = (o == (uint32_t)nr) ? 1 : 0;
+            g = f != NO_LANE ? of : o;
+            win[pos & (WIN - 1)] = (g == (uint32_t)nr) ? 1 : 0;
         }
         // the first blocking degrade verdict of a committed lane trips the breaker (DegradeRule.passCheck cut)
 #pragma unroll
@@ -1728,8 +1744,20 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         atomicAdd(&S.dbg[4], 1ull);
         atomicAdd(&S.dbg[6], (unsigned long long)n_frz);
 #ifdef SG_KPROF
-        if (atomicMax(&S.dbg[5], (unsigned long long)sg.len) < sg.len)  // longest segment so far
+        const unsigned long long tm_end = __builtin_amdgcn_s_memtime(), tot = tm_end - tm_start;
+        if (atomicMax(&S.dbg[18], tot) < tot) {  // slowest segment so far: its phases, length, rounds
             for (int k = 0; k < 10; ++k) S.dbg[8 + k] = tph[k];
+            S.dbg[5] = sg.len;
+            S.dbg[19] = n_round;
+            S.dbg[23] = n_it;
+            S.dbg[24] = n_mm;
+            S.dbg[25] = pg.pflags | (nf << 8) | (nd << 12) | ((nd ? sh.rules[nf].grade : 0xF) << 16);
+            S.dbg[26] = (unsigned long long)sh.rules[0].count;
+            S.dbg[27] = n_frz;
+        }
+        atomicMin(&S.dbg[20], tm_start);  // block start spread (waiting for a CU) and last end
+        atomicMax(&S.dbg[21], tm_start);
+        atomicMax(&S.dbg[22], tm_end);
 #else
         if (blockIdx.x == 0) S.dbg[5] = sg.len;
 #endif

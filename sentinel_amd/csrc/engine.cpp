@@ -945,6 +945,14 @@ extern "C" unsigned long long sgx_spans_total(sg_engine* e) {
     (void)drain(e);
     return e->spans_total;
 }
+// diagnostics export: zero the SG_DEBUG counters ([20] is a running minimum)
+extern "C" int sgx_debug_reset(sg_engine* e) {
+    if (!e || !e->d_dbg) return 0;
+    (void)drain(e);
+    unsigned long long z[64] = {0};
+    z[20] = ~0ull;
+    return hipMemcpy(e->d_dbg, z, sizeof(z), hipMemcpyHostToDevice) == hipSuccess ? 1 : 0;
+}
 extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap) {
     if (!e || !e->d_dbg || !out) return 0;
     int k = cap < 64 ? cap : 64;

@@ -27,23 +27,29 @@ ev = w.events
 B = min(len(ev) // nb, 1 << 25)
 L = E.lib()
 L.sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+L.sgx_debug_reset.argtypes = [C.c_void_p]
 prev = np.zeros(64, dtype=np.uint64)
 for i in range(nb):
     print("submit batch", i, flush=True)
     t = time.time()
+    L.sgx_debug_reset(eng.h)
     eng.submit(ev[i * B:(i + 1) * B])
     tm = eng.timings()
     buf = (C.c_ulonglong * 64)()
     L.sgx_debug_counters(eng.h, buf, 64)
     v = np.array(list(buf), dtype=np.uint64)
-    d = v - prev
-    prev = v
+    d = v
     print("batch %d: %d events, wall %.1f ms, group %.2f ms, decide %.2f ms" % (i, B, (time.time() - t) * 1e3, tm[0], tm[1]))
     print("  J16 bin: segs %d iterations %d rounds %d tiles %d mismatched-iterations %d" % (d[4], d[0], d[1], d[2], d[3]))
     ph = v[8:18].astype(np.float64)
     tot = ph.sum() or 1
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
-    print("  longest segment (len %d) phase cycles:" % v[5], {k: "%.0f" % ph[j] for j, k in enumerate(names)})
+    print("  slowest segment (len %d, %d rounds, %d cycles) phase cycles:" % (v[5], v[19], v[18]),
+          {k: "%.0f" % ph[j] for j, k in enumerate(names)})
+    print("  slowest: iterations %d mismatched %d frozen-tiles %d prog %#x flow count %d" % (v[23], v[24], v[27], v[25], v[26]))
+    mm = d[40:49].reshape(3, 3)
+    print("  mismatch (guess row: pass/flow/degrade -> evaluated col):", mm.tolist(), "not-first", d[49], "sum(f-c0)", d[50])
+    print("  J16 block starts spread %d cycles, first start -> last end %d cycles" % (v[21] - v[20], v[22] - v[20]))
     print("  frozen tiles (all J16 segments):", d[6])
     if d[36]:
         print("  k_lane longest segment: len %d, cycles start %d entries %d exits %d (per event %.0f)" %
