@@ -168,7 +168,7 @@ def main():
                        "parallelism": "resource-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "decide stage: k_jac<16,17,2,2> | k_jac<4,..> | k_jac<1,..> | k_lane<4> (concurrent streams)",
+                         "kernel": "decide stage: k_jac<16,..> | k_jac<4,..> then k_jac<1,..> | k_lite + k_lane (concurrent streams), then k_fill",
                          "kernel_ms": decide_ms, "alg_bytes_per_launch": float(alg_bytes)},
             "pipeline": {"achieved_GBs": pipe_achieved, "frac": pipe_achieved / HBM_PEAK_GBS,
                          "group_ms": float(sm[:, 0].mean()), "decide_ms": decide_ms, "post_ms": float(sm[:, 2].mean()),

@@ -1124,8 +1124,9 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                 // its effective EXIT/TRACEs are the same-batch EXIT/TRACEs of the passes this owner
                 // committed (pending list + forward links) plus the few that count without a link
                 // (streamed), and k_fill writes its verdicts after the decide kernels.
-                if (skip_on && sg.len - fpos0 > S.skip_min && uni(sh.nsp) < NSPAN) {
-                    if (tid == 0) sh.skip_go = (int64_t)recs[sg.start + fpos0 + S.skip_min].dt < dhi ? 1u : 0u;
+                const uint32_t skip_min = S.skip_min * NW / 16 > 0 ? S.skip_min * NW / 16 : 1u;  // scaled to the owner's width
+                if (skip_on && sg.len - fpos0 > skip_min && uni(sh.nsp) < NSPAN) {
+                    if (tid == 0) sh.skip_go = (int64_t)recs[sg.start + fpos0 + skip_min].dt < dhi ? 1u : 0u;
                     lds_barrier();
                     if (uni(sh.skip_go)) {
                         // (1) stretch end E = first position with dt >= dhi (dt is non-decreasing); dt[lo] < dhi

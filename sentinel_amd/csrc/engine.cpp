@@ -488,9 +488,9 @@ struct sg_engine {
     // gets (GPU_MAX_HW_QUEUES): a fifth stream would share a queue and serialise behind another's kernels
     hipStream_t bin_stream[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
-    bool pipeline = false;  // SG_PIPELINE=1: the group stage of batch k+1 overlaps the decide stage of batch k
+    bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
-    uint32_t skip_min = 12288;  // frozen stretches shorter than this are streamed, not skipped
+    uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
     std::vector<CFlow> cflows;                    // host copy of the config part (state lives on the device)
@@ -1343,9 +1343,9 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     }
     uint32_t* dev_out = host_out ? e->d_out : out;
     const uint64_t ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
-    // Overlapping this group stage with the previous batch's decide stage is only a win when the
-    // bandwidth-bound sort does not slow the latency-bound decide kernels more than it hides; measured
-    // on MI355X it does (k_jac<16> 3.6 -> 6-8 ms), so by default the stages run back to back.
+    // Overlapping this group stage with the previous batch's decide stage wins once the decide kernels
+    // no longer stream frozen stretches through single CUs (C4 on MI355X: 6.45 -> 5.45 ms per batch);
+    // SG_PIPELINE=0 runs the stages back to back.
     if (!e->pipeline && e->last >= 0 && e->slot[e->last].pending)
         HIPCHK(hipStreamWaitEvent(gs, e->slot[e->last].ev[4], 0));
     HIPCHK(hipEventRecord(B.ev[0], gs));

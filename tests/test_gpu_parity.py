@@ -295,10 +295,15 @@ def test_exit_with_args_thread_params(bin_mode):
 
 
 # ---------------------------------------------------------------- batch pipeline (sg_submit_async)
-@pytest.mark.parametrize("config,kw", [(4, {"n_entries": 300_000, "n_res": 5_000}), (3, {"n_entries": 300_000, "n_res": 20_000})])
-def test_async_pipeline(config, kw):
+@pytest.mark.parametrize("pipeline", ["0", "1"])
+@pytest.mark.parametrize("config,kw", [(4, {"n_entries": 300_000, "n_res": 5_000}), (3, {"n_entries": 300_000, "n_res": 20_000}),
+                                       (4, {"n_entries": 300_000, "n_res": 40})])
+def test_async_pipeline(config, kw, pipeline, monkeypatch):
     """Batches submitted back to back with sg_submit_async: the group stage of batch k+1 runs while
-    batch k is decided, and references into earlier batches are resolved in the decide stage."""
+    batch k is decided (SG_PIPELINE=1, the default), and references into earlier batches are resolved
+    in the decide stage.  The 40-resource case keeps the cooperative kernels skipping frozen stretches."""
+    monkeypatch.setenv("SG_PIPELINE", pipeline)
+    monkeypatch.setenv("SG_SKIP_MIN", "64")
     w = T.Workload(config, **kw)
     eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
     orc = O.Oracle(max_slot_chain_size=0)

@@ -12,7 +12,7 @@ import json
 import sys
 from collections import defaultdict
 
-DECIDE = ("k_jac", "k_lane")
+DECIDE = ("k_jac", "k_lane", "k_lite", "k_fill", "k_resolve")
 
 
 def load(path, counter):
