@@ -77,6 +77,11 @@ struct Node {
     int64_t exc_sum_sec; // see NodeInfo
     int64_t exc_sum;
     int64_t* bor;        // borrow ring {ws, pass} x 2 in HBM once a prioritized ENTRY was seen, else null
+    // prefetched HBM copy of the minute bucket of the second after mb's (k_lite): -2 = prefetching off,
+    // -1 = nothing prefetched.  Only this lane writes the resource's minute buckets, and only mb's slot,
+    // so the copy stays exact until mb moves onto its slot.
+    int32_t pfslot;
+    Bkt pf;
 };
 
 __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t res) {
@@ -88,6 +93,7 @@ __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t r
     N.exc_sum_sec = ni.exc_sum_sec;
     N.exc_sum = ni.exc_sum;
     N.mslot = -1;
+    N.pfslot = -2;
     N.mst = 0;
     N.bor = S.prio && S.prio[res] ? S.borrow + (uint64_t)res * 4 : nullptr;
 }
@@ -106,34 +112,46 @@ __device__ __forceinline__ void bkt_borrow(Bkt& b, const int64_t* bor, int slot,
     const int64_t bws = bor[2 * slot];
     if (bws >= 0 && bws <= t && t < bws + 500) b.pass = bor[2 * slot + 1];  // getWindowValue(t)
 }
+// Both buckets are updated by value selects, never through a pointer chosen by the slot: a selected
+// pointer into N.sb makes the compiler keep the node on the stack (scratch), and every scratch access
+// then waits for all outstanding memory operations of the lane.
+__device__ __forceinline__ void bkt_reset_if(Bkt& b, bool c, int64_t ws, int32_t max_rt) {
+    b.ws = c ? ws : b.ws;
+    b.pass = c ? 0 : b.pass;
+    b.block = c ? 0 : b.block;
+    b.exc = c ? 0 : b.exc;
+    b.succ = c ? 0 : b.succ;
+    b.rt = c ? 0 : b.rt;
+    b.occ = c ? 0 : b.occ;
+    b.minrt = c ? (int64_t)max_rt : b.minrt;
+}
 __device__ __forceinline__ int sec_current(Node& N, int64_t t, int32_t max_rt) {
-    int slot = (int)((t / 500) & 1);
-    int64_t ws = t - t % 500;
-    if (slot == 0) {
-        if (N.sb[0].ws == ws) return 0;
-        if (N.sb[0].ws < ws) {
-            bkt_reset(N.sb[0], ws, max_rt);
-            if (N.bor) bkt_borrow(N.sb[0], N.bor, 0, t);
-            return 0;
-        }
-        return -1;
+    const int slot = (int)((t / 500) & 1);
+    const int64_t ws = t - t % 500;
+    const int64_t cws = slot ? N.sb[1].ws : N.sb[0].ws;
+    if (cws == ws) return slot;
+    if (cws > ws) return -1;
+    bkt_reset_if(N.sb[0], slot == 0, ws, max_rt);
+    bkt_reset_if(N.sb[1], slot == 1, ws, max_rt);
+    if (N.bor) {
+        if (slot == 0) bkt_borrow(N.sb[0], N.bor, 0, t);
+        else bkt_borrow(N.sb[1], N.bor, 1, t);
     }
-    if (N.sb[1].ws == ws) return 1;
-    if (N.sb[1].ws < ws) {
-        bkt_reset(N.sb[1], ws, max_rt);
-        if (N.bor) bkt_borrow(N.sb[1], N.bor, 1, t);
-        return 1;
-    }
-    return -1;
+    return slot;
 }
 __device__ __forceinline__ void bkt_add(Bkt& b, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE, int64_t mrt) {
     b.pass += dP; b.block += dB; b.succ += dS; b.rt += dRT; b.exc += dE;
     if (mrt < b.minrt) b.minrt = mrt;
 }
+__device__ __forceinline__ void bkt_add_if(Bkt& b, bool c, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE,
+                                           int64_t mrt) {
+    b.pass += c ? dP : 0; b.block += c ? dB : 0; b.succ += c ? dS : 0; b.rt += c ? dRT : 0; b.exc += c ? dE : 0;
+    b.minrt = (c && mrt < b.minrt) ? mrt : b.minrt;
+}
 __device__ __forceinline__ void sec_add(Node& N, int sl, int64_t dP, int64_t dB, int64_t dS, int64_t dRT, int64_t dE,
                                         int64_t mrt) {
-    if (sl == 0) bkt_add(N.sb[0], dP, dB, dS, dRT, dE, mrt);
-    else if (sl == 1) bkt_add(N.sb[1], dP, dB, dS, dRT, dE, mrt);
+    bkt_add_if(N.sb[0], sl == 0, dP, dB, dS, dRT, dE, mrt);
+    bkt_add_if(N.sb[1], sl == 1, dP, dB, dS, dRT, dE, mrt);
 }
 // sum of one counter over LeapArray.values(t): a bucket is valid unless t - ws > 1000 (strict, Q4)
 #define SEC_SUM(N, t, f) ((((t) - (N).sb[0].ws <= 1000 && (N).sb[0].ws >= 0) ? (N).sb[0].f : 0) + \
@@ -162,7 +180,8 @@ __device__ __forceinline__ void exc_advance(Node& N, const Bkt* minb, int64_t T)
         N.exc_sum = s;
     } else {
         for (int64_t x = N.exc_sum_sec - 59000; x <= T - 60000; x += 1000) {
-            Bkt b = minb[(x / 1000) % 60];
+            const int sl = (int)((x / 1000) % 60);
+            const Bkt b = sl == N.pfslot ? N.pf : minb[sl];
             if (b.ws == x) N.exc_sum -= b.exc;
         }
     }
@@ -175,9 +194,13 @@ __device__ __forceinline__ void min_current(Node& N, Bkt* minb, int64_t t, int32
     if (N.mslot == slot && N.mb.ws == ws) return;
     min_flush(N, minb);
     if ((pflags & PF_EXC_COUNT) && N.exc_sum_sec < ws) exc_advance(N, minb, ws);
-    Bkt b = minb[slot];
+    Bkt b = slot == N.pfslot ? N.pf : minb[slot];
     N.mslot = slot;
     N.mst = 0;
+    if (N.pfslot >= -1) {  // prefetch the next second's bucket (its load overlaps the events until then)
+        N.pfslot = (slot + 1) % 60;
+        N.pf = minb[N.pfslot];
+    }
     if (b.ws == ws) { N.mb = b; return; }
     bool back = b.ws > ws;
     bkt_reset(b, ws, max_rt);

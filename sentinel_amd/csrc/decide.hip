@@ -660,23 +660,56 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
             ds[k] = S.rstate[pg.rule_off + nf + k];
         }
     }
+#ifdef SG_KPROF
+    const bool kp = S.dbg && i == 0;  // the longest segment of the launch
+    unsigned long long kt0 = kp ? __builtin_amdgcn_s_memtime() : 0, kta = 0, ktb = 0, ktc = 0, ktd = 0, ktf = 0, ktg = 0, kth = 0;
+#define LPROF(acc)                                                \
+    if (kp) {                                                     \
+        unsigned long long _n = __builtin_amdgcn_s_memtime();     \
+        acc += _n - kt0;                                          \
+        kt0 = _n;                                                 \
+    }
+#else
+#define LPROF(acc)
+#endif
     Node N;
     node_load(N, S, res);
+    N.pfslot = -1;  // minute-bucket prefetch on
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
     const bool has_chain = (N.flags & NI_CHAIN) != 0;
     const bool chain = has_chain && cfg.switch_on;
     if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
         atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
     uint64_t pm0 = 0, pm1 = 0, pm2 = 0, pm3 = 0;  // passed bits of positions 0..255
-    SEv rn[3];  // software prefetch, three events ahead
-    rn[0] = recs[sg.start];
-    if (sg.len > 1) rn[1] = recs[sg.start + 1];
-    if (sg.len > 2) rn[2] = recs[sg.start + 2];
-    for (uint32_t j = 0; j < sg.len; ++j) {
-        const SEv r = rn[0];
-        rn[0] = rn[1];
-        rn[1] = rn[2];
-        if (j + 3 < sg.len) rn[2] = recs[sg.start + j + 3];
+    // records in chunks of 4 with the next chunk in flight: one memory round trip per 4 events (the
+    // loads are unconditional with a clamped index, so the compiler's vmcnt waits cannot serialise them)
+    constexpr uint32_t CH = 4;
+    const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
+    const uint32_t qmax = sg.len ? sg.len - 1 : 0;
+    uint4 cur[CH], nxt[CH];
+#pragma unroll
+    for (uint32_t k = 0; k < CH; ++k) cur[k] = r4[k < qmax ? k : qmax];
+    LPROF(kta)
+    for (uint32_t j0 = 0; j0 < sg.len; j0 += CH) {
+#pragma unroll
+    for (uint32_t k = 0; k < CH; ++k) nxt[k] = r4[j0 + CH + k < qmax ? j0 + CH + k : qmax];
+#pragma unroll 1
+    for (uint32_t k = 0; k < CH; ++k) {
+        const uint4 rw = cur[0];
+        cur[0] = cur[1];
+        cur[1] = cur[2];
+        cur[2] = cur[3];
+        const uint32_t j = j0 + k;
+        if (j >= sg.len) break;
+        SEv r;
+        r.dt = (int32_t)rw.x;
+        r.x = rw.y;
+        r.cnt = (uint16_t)(rw.z & 0xFFFFu);
+        r.rt = (uint16_t)(rw.z >> 16);
+        r.kind = (uint8_t)(rw.w & 0xFFu);
+        r.flags = (uint8_t)((rw.w >> 8) & 0xFFu);
+        r.code = (uint8_t)((rw.w >> 16) & 0xFFu);
+        r.pad = 0;
         const int64_t t = t0 + r.dt;
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
         if (r.kind == SG_EV_ENTRY) {
@@ -692,6 +725,7 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                         if ((double)j_iadd(cur, (int)r.cnt) > fcnt[k]) { status = ST_BLOCK_FLOW; slot = fslot[k]; }
                     }
                 }
+                LPROF(ktf)
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {  // DegradeSlot
                     if (k < nd && status == ST_PASS && !degrade_pass(N, C, dr[k], ds[k], t)) {
@@ -699,14 +733,17 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                         slot = dr[k].slot;
                     }
                 }
+                LPROF(ktg)
                 const bool passed = status == ST_PASS;
                 stat_entry(N, C, t, r.cnt, passed);
+                LPROF(kth)
                 d = passed ? mk_dec(ST_PASS, 0, 0) : mk_dec(status, slot, 0);
                 if (passed && j < 256) {
                     const uint64_t b = 1ull << (j & 63);
                     if (j < 64) pm0 |= b; else if (j < 128) pm1 |= b; else if (j < 192) pm2 |= b; else pm3 |= b;
                 }
             }
+            LPROF(ktb)
         } else {
             bool eff;
             if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
@@ -724,14 +761,25 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                 if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
                 else stat_trace(N, C, t, r.cnt);
             }
+            LPROF(ktc)
         }
         dec[sg.start + j] = d;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < CH; ++k) cur[k] = nxt[k];
     }
     min_flush(N, C.minb);
     node_store(N, S, res, pg.pflags);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
         if (k < nd) S.rstate[pg.rule_off + nf + k] = ds[k];
+    LPROF(ktd)
+#ifdef SG_KPROF
+    if (kp) {
+        S.dbg[32] += kta; S.dbg[33] += ktb; S.dbg[34] += ktc; S.dbg[35] += sg.len; S.dbg[36] += 1; S.dbg[37] += ktd; S.dbg[38] += ktf; S.dbg[39] += ktg; S.dbg[51] += kth;
+    }
+#endif
+#undef LPROF
 }
 
 // =================================================================================

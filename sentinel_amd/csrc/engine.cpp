@@ -1488,8 +1488,12 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     }
     HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
                              off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
-    HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
-                             off[BIN_LITE + LANE_BINS] - off[BIN_LITE], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    {
+        DevState Sl = S;
+        Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..37]
+        HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
+                                 off[BIN_LITE + LANE_BINS] - off[BIN_LITE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    }
     for (int c = 0; c < 3; ++c)
         if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c == 0 ? 0 : 1], 0));
     // verdicts of the frozen spans the cooperative kernels skipped

@@ -52,5 +52,6 @@ for i in range(nb):
     print("  J16 block starts spread %d cycles, first start -> last end %d cycles" % (v[21] - v[20], v[22] - v[20]))
     print("  frozen tiles (all J16 segments):", d[6])
     if d[36]:
-        print("  k_lane longest segment: len %d, cycles start %d entries %d exits %d (per event %.0f)" %
-              (d[35], d[32], d[33], d[34], (d[32] + d[33] + d[34]) / max(1, d[35])))
+        print("  lane kernel longest segment: len %d, cycles start %d entries %d exits %d end %d (per event %.0f)" %
+              (d[35], d[32], d[33], d[34], d[37], (d[32] + d[33] + d[34]) / max(1, d[35])))
+        print("    entry split: flow %d degrade %d stat_entry %d after %d" % (d[38], d[39], d[51], d[33]))
