@@ -888,8 +888,14 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     e->device = cfg.device;
     auto bad = [&](int rc) { sg_engine_destroy(e); return rc; };
     if (hipSetDevice(e->device) != hipSuccess) return bad(fail(SG_EDEVICE, "hipSetDevice failed"));
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
-    if (hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+    // The decide streams (latency-bound per-resource chains) get the highest priority so that their
+    // workgroups are dispatched ahead of the overlapping group stage's bandwidth-bound sort
+    // (SG_STREAM_PRIO=0: default priorities).
+    int prio_lo = 0, prio_hi = 0;
+    const char* sp = std::getenv("SG_STREAM_PRIO");
+    if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+    if (hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, prio_lo) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
     for (auto& B : e->slot)
         for (auto& v : B.ev) if (hipEventCreate(&v) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
     uint64_t R = cfg.max_resources;
@@ -908,7 +914,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
     for (auto& s : e->bin_stream)
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
+        if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
     if (hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
     for (auto& v : e->join)
         if (hipEventCreateWithFlags(&v, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
