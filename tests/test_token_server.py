@@ -1,0 +1,156 @@
+"""Wire-compatible token server front-end (sentinel_amd/token_server.py).
+
+CPU tests: byte layouts of the reference's Netty codecs (NettyTransportServer framing,
+DefaultRequestEntityDecoder, FlowRequestDataDecoder, PingRequestDataDecoder,
+DefaultResponseEntityWriter, FlowResponseDataWriter), and the asyncio server with a recording
+stub service (batching, ping/connected counts, BAD for types without a processor, oversize frames).
+GPU test: real clients against the server on the device engine; every response equals the
+oracle's TokenService answer for the same requests at the same times.
+"""
+import asyncio
+import struct
+
+import numpy as np
+import pytest
+
+from sentinel_amd import _abi as A
+from sentinel_amd import token_server as S
+
+
+def test_flow_request_bytes():
+    b = S.encode_flow_request(7, 0x0102030405060708, 3, True)
+    # u16 length 18 | int xid | byte type 1 | long flowId | int count | bool priority
+    assert b == bytes.fromhex("0012" "00000007" "01" "0102030405060708" "00000003" "01")
+    req = S.decode_request(b[2:])
+    assert (req.xid, req.type, req.data) == (7, S.MSG_TYPE_FLOW, S.FlowRequest(0x0102030405060708, 3, True))
+    # priority byte absent -> false (FlowRequestDataDecoder.java:36-40); short body -> null data
+    assert S.decode_request(b[2:-1]).data == S.FlowRequest(0x0102030405060708, 3, False)
+    assert S.decode_request(b[2:12]).data is None
+    assert S.decode_request(b[2:6]) is None  # < 5 bytes
+    assert S.decode_request(struct.pack(">ib", 1, 9)) is None  # unknown type
+
+
+def test_ping_and_response_bytes():
+    b = S.encode_ping_request(-2, "app-ns")
+    req = S.decode_request(b[2:])
+    assert (req.xid, req.type, req.data) == (-2, S.MSG_TYPE_PING, "app-ns")
+    assert S.decode_request(struct.pack(">ibi", 1, 0, 0)).data is None
+    assert S.encode_flow_response(5, A.TOKEN_SHOULD_WAIT, 0, 200) == bytes.fromhex("000e" "00000005" "01" "02" "00000000" "000000c8")
+    assert S.encode_ping_response(5, 3) == bytes.fromhex("0007" "00000005" "00" "00" "03")
+    assert S.encode_bad_response(5, 2) == bytes.fromhex("0006" "00000005" "02" "ff")
+    assert S.decode_response(S.encode_flow_response(9, A.TOKEN_BLOCKED, -1, 0)[2:]) == (9, 1, A.TOKEN_BLOCKED, (-1, 0))
+
+
+def test_frame_decoder_split_and_oversize():
+    d = S.FrameDecoder()
+    stream = S.encode_flow_request(1, 10, 1, False) + S.encode_ping_request(2, "ns")
+    got = []
+    for i in range(len(stream)):
+        got += d.feed(stream[i:i + 1])
+    assert [S.decode_request(g).xid for g in got] == [1, 2]
+    with pytest.raises(ValueError):
+        S.FrameDecoder().feed(struct.pack(">H", 1023))
+
+
+class _Stub:
+    """Records what reaches the device boundary; answers OK with remaining = flowId + count."""
+
+    def __init__(self):
+        self.connected = {}
+
+    def cluster_set_connected(self, fid, n):
+        self.connected[fid] = n
+
+    def cluster_request_array(self, reqs):
+        out = np.zeros(len(reqs), dtype=A.TOKEN_RES_DTYPE)
+        out["status"] = A.TOKEN_OK
+        out["remaining"] = reqs["flow_id"] + reqs["acquire_count"]
+        out["wait_in_ms"] = reqs["prioritized"]
+        return out
+
+
+async def _client(port, frames, n_resp):
+    r, w = await asyncio.open_connection("127.0.0.1", port)
+    w.write(b"".join(frames))
+    await w.drain()
+    dec, out = S.FrameDecoder(), []
+    while len(out) < n_resp:
+        data = await asyncio.wait_for(r.read(65536), 10)
+        assert data
+        out += [S.decode_response(b) for b in dec.feed(data)]
+    return r, w, out
+
+
+def test_server_batches_and_pings():
+    async def run():
+        stub = _Stub()
+        srv = S.TokenServer(stub, flow_namespaces={11: "ns-a", 12: "ns-b"}, clock=lambda: 1000)
+        port = await srv.start(port=0)
+        r1, w1, a = await _client(port, [S.encode_ping_request(1, "ns-a")] +
+                                  [S.encode_flow_request(10 + i, 11, i + 1, i % 2 == 1) for i in range(50)], 51)
+        assert a[0] == (1, S.MSG_TYPE_PING, S.RESPONSE_STATUS_OK, 1)
+        assert sorted(a[1:]) == [(10 + i, 1, A.TOKEN_OK, (12 + i, i % 2)) for i in range(50)]
+        assert stub.connected == {11: 1}
+        r2, w2, b = await _client(port, [S.encode_ping_request(3, "ns-a"), S.encode_ping_request(4, " "),
+                                         S.frame(struct.pack(">ib", 5, S.MSG_TYPE_PARAM_FLOW))], 3)
+        assert b == [(3, 0, 0, 2), (4, 0, S.RESPONSE_STATUS_BAD, None), (5, S.MSG_TYPE_PARAM_FLOW, S.RESPONSE_STATUS_BAD, None)]
+        assert stub.connected == {11: 2}
+        w2.close()
+        await asyncio.sleep(0.05)
+        assert stub.connected == {11: 1}
+        # far fewer device calls than requests: frames that arrive together are decided together
+        assert sum(srv.batches) == 50 and len(srv.batches) < 50
+        w1.close()
+        await srv.stop()
+
+    asyncio.run(run())
+
+
+@pytest.mark.gpu
+def test_server_on_device_matches_oracle():
+    import pyoracle as O
+    from sentinel_amd import engine as E
+
+    T0 = 1_700_000_000_000
+    rules = [A.flow_rule("abc", c, cluster_mode=True, cluster_flow_id=fid,
+                         cluster_threshold_type=A.CLUSTER_THRESHOLD_GLOBAL)
+             for fid, c in ((101, 20), (102, 5), (103, 50))]
+    eng = E.Engine(max_resources=64)
+    eng.register("abc")
+    eng.load_flow_rules(rules)
+    tick = [T0]
+
+    def clock():
+        tick[0] += 37
+        return tick[0]
+
+    async def run():
+        srv = S.TokenServer(eng, clock=clock, record=True)
+        port = await srv.start(port=0)
+        rng = np.random.default_rng(3)
+        clients = []
+        for c in range(4):
+            frames = [S.encode_flow_request(c * 1000 + i, int(rng.choice([101, 102, 103, 999])),
+                                            int(rng.integers(1, 4)), bool(rng.random() < 0.2)) for i in range(300)]
+            clients.append(_client(port, frames, 300))
+        res = await asyncio.gather(*clients)
+        for _, w, _ in res:
+            w.close()
+        await srv.stop()
+        return srv, [x for _, _, out in res for x in out]
+
+    srv, got = asyncio.run(run())
+    orc = O.Oracle()
+    orc.register("abc")
+    orc.load_flow_rules(rules)
+    by_xid = {}
+    for xids, reqs, res in srv.submitted:
+        want = orc.cluster_request([(int(r["ts"]), int(r["flow_id"]), int(r["acquire_count"]),
+                                     bool(r["prioritized"])) for r in reqs])
+        dev = [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in res]
+        assert dev == want
+        by_xid.update(zip(xids, dev))
+    assert len(got) == 1200 and len(by_xid) == 1200 and len(srv.batches) < 1200
+    for xid, typ, st, data in got:
+        assert (st,) + tuple(data) == by_xid[xid]
+    assert {s for s, _, _ in by_xid.values()} >= {A.TOKEN_OK, A.TOKEN_NO_RULE_EXISTS}
