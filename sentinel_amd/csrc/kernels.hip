@@ -113,71 +113,44 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __res
     for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// Stable scatter of one 8-bit digit.  A tile's items are ranked in (round, wave, lane) order ==
-// input order and placed, digit-sorted, in LDS first; the tile then leaves in digit runs, so the
-// writes of a run are consecutive addresses (a direct scatter would send each round's 256 items to
-// up to 256 different places).  The last pass also writes the inverse permutation
-// pos_of[idx] = sorted position | ENTRY bit.
+// Stable scatter of one 8-bit digit.  Wave w of a tile owns the contiguous quarter
+// [base + w*1024, base + (w+1)*1024) and walks it in 16 coalesced rounds of 64, so input order is
+// (wave, round, lane): every wave ranks its own items against a wave-private digit counter
+// (peers by 8 ballots, no block barrier per round), one block-wide scan turns the four waves'
+// counts into digit-run offsets, and the tile is placed digit-sorted in LDS.  It then leaves in
+// digit runs, so the writes of a run are consecutive addresses.  The last pass also writes the
+// inverse permutation pos_of[idx] = sorted position | ENTRY bit.  (The per-block digit histograms
+// of k_rs_first / k_radix_hist count the same 4096-item tile, in any order.)
 __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                            uint32_t* __restrict__ pos_of) {
+    static_assert(RS_BINS == RS_THREADS, "one digit per thread in the offset scan");
     __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
-    __shared__ uint32_t wcnt[4][RS_BINS];
-    __shared__ uint32_t woff[4][RS_BINS];
-    __shared__ uint32_t run[RS_BINS];   // local cursor of each digit
-    __shared__ int64_t gdst[RS_BINS];   // global position of local position 0 of each digit's run
+    __shared__ uint32_t wcnt[4][RS_BINS];   // per-wave digit counts, then per-wave digit offsets
+    __shared__ int64_t gdst[RS_BINS];       // global position of local position 0 of each digit's run
+    __shared__ uint32_t wtot[4];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t wbase = base + (uint64_t)w * (RS_TILE / 4);
     const uint32_t cnt_tile = (uint32_t)((n - base) < RS_TILE ? (n - base) : RS_TILE);
-    uint32_t kk[RS_ITEMS], vv[RS_ITEMS];
+    uint32_t kk[RS_ITEMS], vv[RS_ITEMS], rk[RS_ITEMS];
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; ++it) {  // striped loads: coalesced
-        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+    for (int it = 0; it < RS_ITEMS; ++it) {  // per-wave rounds of 64 consecutive items: coalesced
+        const uint64_t i = wbase + (uint64_t)it * WAVE + l;
         kk[it] = i < n ? keys_in[i] : 0u;
         vv[it] = i < n ? vals_in[i] : 0u;
     }
-    for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) {
-        run[i] = 0;
-        wcnt[0][i] = wcnt[1][i] = wcnt[2][i] = wcnt[3][i] = 0;
-    }
-    __syncthreads();
-    // local digit histogram -> local offsets (exclusive scan over 256 bins by wave 0)
-#pragma unroll
-    for (int it = 0; it < RS_ITEMS; ++it) {
-        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&run[(kk[it] >> shift) & (RS_BINS - 1)], 1u);
-    }
-    __syncthreads();
-    if (w == 0) {
-        uint32_t c[4], t = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { c[j] = run[4 * l + j]; t += c[j]; }
-        uint32_t x = t;  // inclusive wave scan of the per-lane totals
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (l >= o) x += y;
-        }
-        uint32_t acc = x - t;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int d = 4 * l + j;
-            gdst[d] = (int64_t)goff[(uint64_t)d * nblocks + blockIdx.x] - (int64_t)acc;
-            run[d] = acc;
-            acc += c[j];
-        }
-    }
+    for (int i = threadIdx.x; i < 4 * RS_BINS; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+    uint32_t* myc = wcnt[w];
 #pragma unroll
     for (int it = 0; it < RS_ITEMS; ++it) {
-        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        const uint64_t i = wbase + (uint64_t)it * WAVE + l;
         const bool valid = i < n;
-        const uint32_t k = kk[it];
-        const uint32_t d = (k >> shift) & (RS_BINS - 1);
-        // peers: lanes with the same digit (8 ballots)
+        const uint32_t d = (kk[it] >> shift) & (RS_BINS - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -185,18 +158,40 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
         const uint32_t rank = __popcll(peers & lt_mask);
-        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
-        __syncthreads();
-        for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) {
-            uint32_t acc = run[b];
+        // every lane of the wave reads the digit's count before its first peer (rank 0) bumps it;
+        // LDS instructions of one wave execute in order
+        const uint32_t old = valid ? myc[d] : 0u;
+        rk[it] = old + rank;
+        if (valid && rank == 0) myc[d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {   // digit b = thread b: run offsets (exclusive scan over digits), then the waves in order
+        const int b = threadIdx.x;
+        const uint32_t c0 = wcnt[0][b], c1 = wcnt[1][b], c2 = wcnt[2][b], c3 = wcnt[3][b];
+        const uint32_t t = c0 + c1 + c2 + c3;
+        uint32_t x = t;
 #pragma unroll
-            for (int ww = 0; ww < 4; ++ww) { const uint32_t c = wcnt[ww][b]; woff[ww][b] = acc; acc += c; wcnt[ww][b] = 0; }
-            run[b] = acc;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (l >= o) x += y;
         }
+        if (l == 63) wtot[w] = x;
         __syncthreads();
-        if (valid) {
-            const uint32_t lp = woff[w][d] + rank;
-            sk[lp] = k;
+        uint32_t acc = x - t;
+        for (int ww = 0; ww < w; ++ww) acc += wtot[ww];
+        gdst[b] = (int64_t)goff[(uint64_t)b * nblocks + blockIdx.x] - (int64_t)acc;
+        wcnt[0][b] = acc;
+        wcnt[1][b] = acc + c0;
+        wcnt[2][b] = acc + c0 + c1;
+        wcnt[3][b] = acc + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {
+        const uint64_t i = wbase + (uint64_t)it * WAVE + l;
+        if (i < n) {
+            const uint32_t lp = myc[(kk[it] >> shift) & (RS_BINS - 1)] + rk[it];
+            sk[lp] = kk[it];
             sv[lp] = vv[it];
         }
     }
