@@ -233,6 +233,14 @@ typedef struct sg_token_req {
     int32_t prioritized;
 } sg_token_req;
 
+typedef struct sg_param_token_req { /* ParamFlowRequestData (flowId, count, params) */
+    int64_t ts;
+    int64_t flow_id;
+    int32_t acquire_count;
+    uint32_t n_values;
+    uint64_t value_off;
+} sg_param_token_req;
+
 enum { /* TokenResultStatus (sentinel-core .../cluster/TokenResultStatus.java) */
     SG_TOKEN_BAD_REQUEST = -4,
     SG_TOKEN_TOO_MANY_REQUEST = -2,
@@ -307,6 +315,15 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
  * loaded with cluster_mode=1 (the ClusterFlowRuleManager role). */
 int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected);
 int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out);
+
+/* Batched TokenService.requestParamToken (core/cluster/TokenService.java:37-46,
+ * csrv/flow/DefaultTokenService.java:50-61 -> csrv/flow/ClusterParamFlowChecker.java:42-88).
+ * Rules come from the param rules loaded with cluster_mode=1 (the ClusterParamFlowRuleManager role,
+ * csrv/flow/rule/ClusterParamFlowRuleManager.java:318-369).  Request i names its parameter values
+ * as values[value_off, value_off + n_values): interned 64-bit keys (sg_param_key).  Requests are
+ * time-ordered and share the namespace's GlobalRequestLimiter with sg_cluster_request_tokens. */
+int sg_cluster_request_param_tokens(sg_engine* e, const sg_param_token_req* reqs, uint64_t n, const uint64_t* values,
+                                    uint64_t n_values, sg_token_result* out);
 
 /* Node read-back for parity tests: the ClusterNode of res_id. */
 int sg_read_node(sg_engine* e, uint32_t res_id, int64_t now_ms, sg_node_state* out);

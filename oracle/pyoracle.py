@@ -59,6 +59,7 @@ def lib():
         L.or_param_set_thread_count.argtypes = [P, C.c_uint32, C.c_int32, C.c_uint64, C.c_int64]
         L.or_cluster_set_connected_count.argtypes = [P, C.c_int64, C.c_int32]
         L.or_cluster_request_tokens.argtypes = [P, C.POINTER(A.SgTokenReq), C.c_uint64, C.POINTER(A.SgTokenResult)]
+        L.or_cluster_request_param_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.or_ctrl_new.restype = P
         L.or_ctrl_new.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int]
         L.or_ctrl_free.argtypes = [P]
@@ -235,6 +236,15 @@ class Oracle:
         out = (A.SgTokenResult * max(1, len(reqs)))()
         assert lib().or_cluster_request_tokens(self.h, arr, len(reqs), out) == 0
         return [(out[i].status, out[i].remaining, out[i].wait_in_ms) for i in range(len(reqs))]
+
+    def cluster_request_param(self, reqs):
+        """reqs: list of (ts, flow_id, acquire, [value keys]) -> list of (status, remaining, wait)."""
+        arr, vals = A.param_token_arrays(reqs)
+        out = np.zeros(max(1, len(reqs)), dtype=A.TOKEN_RES_DTYPE)
+        vp = vals.ctypes.data if len(vals) else None
+        assert lib().or_cluster_request_param_tokens(self.h, arr.ctypes.data, len(reqs), vp, len(vals),
+                                                     out.ctypes.data) == 0
+        return [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in out[:len(reqs)]]
 
 
 class Controller:

@@ -795,6 +795,27 @@ typedef struct {
     int32_t connected;
 } ocluster;
 
+/* token server view of a cluster-mode ParamFlowRule (ClusterParamFlowRuleManager) and its
+ * ClusterParamMetric: a ClusterParameterLeapArray(sampleCount, windowIntervalMs) of per-bucket
+ * value -> LongAdder maps (csrv/flow/statistic/metric/ClusterParamMetric.java:36-91,
+ * ClusterParameterLeapArray.java:30-58).  A value's count in bucket j is live while its stamp equals
+ * the bucket's window start (resetWindowTo clears the map).  Exact tables: the reference's CLHM
+ * capacity of 4000 values per bucket (ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY) is not
+ * modelled -- parity unpinned beyond it. */
+typedef struct { uint64_t key; int64_t* ws; int64_t* cnt; } ocpval;
+typedef struct {
+    int64_t flow_id;
+    double count;
+    int32_t threshold_type;
+    int32_t connected;
+    ohot* hot; int n_hot;
+    int n; int64_t interval, wlen;
+    int64_t* fws;               /* bucket window starts, -1 = never created */
+    ocpval* vals; int n_vals;
+    int live;
+} ocparam;
+static void cp_apply(void* e, const sg_param_rule* r, uint32_t n);
+
 typedef struct {
     int64_t ts;
     uint8_t status;
@@ -830,6 +851,7 @@ struct or_engine {
     u64map ev2ent;         /* global event index -> entry record */
     /* token server */
     ocluster* cl; int n_cl;
+    ocparam* cp; int n_cp;
     oleap ns_limiter;      /* GlobalRequestLimiter (UnaryLeapArray(10, 1000)) */
     double max_allowed_qps;
     int cl_sample_count, cl_interval;
@@ -900,6 +922,8 @@ void or_destroy(or_engine* e) {
     for (int i = 0; i < e->n_cl; ++i) leap_free(&e->cl[i].metric);
     free(e->cl);
     leap_free(&e->ns_limiter);
+    cp_apply(e, NULL, 0);
+    free(e->cp);
     free(e->ents);
     m_free(&e->ev2ent);
     st_free(&e->names); st_free(&e->ctx_names); st_free(&e->origin_names);
@@ -1252,6 +1276,7 @@ int or_load_param_rules(or_engine* e, const sg_param_rule* r, uint32_t n, uint32
     e->n_params = 0;
     e->param_loaded = 1;
     for (uint32_t i = 0; i < e->n_res; ++i) { free(e->res[i].param); e->res[i].param = NULL; e->res[i].n_param = 0; }
+    cp_apply(e, r, n);  /* ClusterParamFlowRuleManager: the same list, its cluster-mode rules */
     if (n == 0) {
         /* "No parameter flow rules, so clear all the metrics" */
         for (uint32_t i = 0; i < e->n_res; ++i) pm_clear(&e->res[i].pm);
@@ -2019,9 +2044,143 @@ static int64_t cl_sum(ocluster* c, int64_t now, int ev) {
 static double cl_avg(ocluster* c, int64_t now, int ev) { return cl_sum(c, now, ev) / (c->metric.interval / 1000.0); }
 static void cl_add(ocluster* c, int64_t now, int ev, int64_t v) { *cf_slot(cl_current(c, now), ev) += v; }
 
+/* ClusterParamFlowRuleManager.applyClusterParamRules (csrv/flow/rule/ClusterParamFlowRuleManager.java:318-369):
+ * cluster-mode rules passing ParamFlowRuleUtil.isValidRule, in list order; ruleMap.put -> the last rule of
+ * a flowId wins; putMetricIfAbsent keeps an existing ClusterParamMetric (window shape included);
+ * metrics of flowIds no longer named are removed. */
+static void cp_free_one(ocparam* c) {
+    for (int i = 0; i < c->n_vals; ++i) { free(c->vals[i].ws); free(c->vals[i].cnt); }
+    free(c->vals); free(c->fws); free(c->hot);
+    memset(c, 0, sizeof(*c));
+}
+static void cp_apply(void* ev, const sg_param_rule* r, uint32_t n) {
+    or_engine* e = (or_engine*)ev;
+    for (int j = 0; j < e->n_cp; ++j) e->cp[j].live = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_param_rule* q = &r[i];
+        if (!q->cluster_mode || !param_valid(q)) continue;
+        int found = -1;
+        for (int j = 0; j < e->n_cp; ++j) if (e->cp[j].flow_id == q->cluster_flow_id) found = j;
+        if (found < 0) {
+            e->cp = (ocparam*)realloc(e->cp, sizeof(ocparam) * (size_t)(e->n_cp + 1));
+            ocparam* c = &e->cp[e->n_cp++];
+            memset(c, 0, sizeof(*c));
+            c->flow_id = q->cluster_flow_id;
+            c->n = q->cluster_sample_count;
+            c->interval = q->cluster_window_interval_ms;
+            c->wlen = c->interval / c->n;
+            c->fws = (int64_t*)malloc(sizeof(int64_t) * (size_t)c->n);
+            for (int k = 0; k < c->n; ++k) c->fws[k] = -1;
+            found = e->n_cp - 1;
+        }
+        ocparam* c = &e->cp[found];
+        c->count = q->count;
+        c->threshold_type = q->cluster_threshold_type;
+        /* ParamFlowRuleUtil.fillExceptionFlowItems: the parsed hot items of this rule */
+        oparam tmp;
+        copy_param(&tmp, q);
+        free(c->hot);
+        c->hot = (ohot*)calloc((size_t)(tmp.n_hot > 0 ? tmp.n_hot : 1), sizeof(ohot));
+        memcpy(c->hot, tmp.hot, sizeof(ohot) * (size_t)tmp.n_hot);
+        c->n_hot = tmp.n_hot;
+        free_param(&tmp);
+        c->live = 1;
+    }
+    int w = 0;
+    for (int j = 0; j < e->n_cp; ++j) {
+        if (e->cp[j].live) e->cp[w++] = e->cp[j];
+        else cp_free_one(&e->cp[j]);
+    }
+    e->n_cp = w;
+}
+/* LeapArray.currentWindow of the ClusterParameterLeapArray: create / reset (map cleared) */
+static int cp_current(ocparam* c, int64_t now) {
+    int idx = (int)((now / c->wlen) % c->n);
+    int64_t ws = now - now % c->wlen;
+    if (c->fws[idx] < 0 || ws > c->fws[idx]) c->fws[idx] = ws;
+    return idx;  /* requests are time-ordered: ws < fws (a detached bucket) cannot occur */
+}
+static ocpval* cp_val(ocparam* c, uint64_t key, int create) {
+    for (int i = 0; i < c->n_vals; ++i) if (c->vals[i].key == key) return &c->vals[i];
+    if (!create) return NULL;
+    c->vals = (ocpval*)realloc(c->vals, sizeof(ocpval) * (size_t)(c->n_vals + 1));
+    ocpval* v = &c->vals[c->n_vals++];
+    v->key = key;
+    v->ws = (int64_t*)malloc(sizeof(int64_t) * (size_t)c->n);
+    v->cnt = (int64_t*)calloc((size_t)c->n, sizeof(int64_t));
+    for (int k = 0; k < c->n; ++k) v->ws[k] = -1;
+    return v;
+}
+/* ClusterParamMetric.getSum: currentWindow(), then the value's count over the valid buckets */
+static int64_t cp_sum(ocparam* c, int64_t now, uint64_t key) {
+    cp_current(c, now);
+    ocpval* v = cp_val(c, key, 0);
+    if (!v) return 0;
+    int64_t s = 0;
+    for (int j = 0; j < c->n; ++j) {
+        if (c->fws[j] < 0 || now - c->fws[j] > c->interval) continue;  /* isWindowDeprecated (strict >) */
+        if (v->ws[j] == c->fws[j]) s += v->cnt[j];
+    }
+    return s;
+}
+static void cp_add(ocparam* c, int64_t now, uint64_t key, int64_t count) {
+    int idx = cp_current(c, now);
+    ocpval* v = cp_val(c, key, 1);
+    if (v->ws[idx] != c->fws[idx]) { v->ws[idx] = c->fws[idx]; v->cnt[idx] = 0; }
+    v->cnt[idx] += count;
+}
+/* GlobalRequestLimiter.tryPass (limit/GlobalRequestLimiter.java:46-54, RequestLimiter.java:72-87) */
+static int ns_try_pass(or_engine* e, int64_t now) {
+    if (e->max_allowed_qps < 0) return 1;  /* no limiter registered -> tryPass true */
+    obucket* w = leap_current(&e->ns_limiter, now);
+    int64_t s = leap_sum(&e->ns_limiter, now, EV_PASS);
+    if (!((double)s / (e->ns_limiter.interval / 1000.0) + 1 <= e->max_allowed_qps)) return 0;
+    if (w) w->c[EV_PASS] += 1;
+    return 1;
+}
+
+/* DefaultTokenService.requestParamToken (csrv/flow/DefaultTokenService.java:50-61) ->
+ * ClusterParamFlowChecker.acquireClusterToken (csrv/flow/ClusterParamFlowChecker.java:42-88) */
+int or_cluster_request_param_tokens(or_engine* e, const sg_param_token_req* reqs, uint64_t n, const uint64_t* values,
+                                    uint64_t n_values, sg_token_result* out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const sg_param_token_req* q = &reqs[i];
+        sg_token_result* o = &out[i];
+        memset(o, 0, sizeof(*o));
+        if (q->value_off + q->n_values > n_values) return SG_EINVAL;
+        if (q->flow_id <= 0 || q->acquire_count <= 0 || q->n_values == 0) { o->status = SG_TOKEN_BAD_REQUEST; continue; }
+        ocparam* c = NULL;
+        for (int k = 0; k < e->n_cp; ++k) if (e->cp[k].flow_id == q->flow_id) c = &e->cp[k];
+        if (!c) { o->status = SG_TOKEN_NO_RULE_EXISTS; continue; }
+        const int64_t now = q->ts;
+        if (!ns_try_pass(e, now)) { o->status = SG_TOKEN_TOO_MANY_REQUEST; continue; }
+        const uint64_t* v = values + q->value_off;
+        double remaining = -1;
+        int passed = 1;
+        for (uint32_t k = 0; k < q->n_values; ++k) {
+            double latest = (double)cp_sum(c, now, v[k]) / (c->interval / 1000.0);  /* getAvg */
+            double raw = c->count;                                                     /* getRawThreshold */
+            for (int h = 0; h < c->n_hot; ++h) if (c->hot[h].key == v[k]) { raw = c->hot[h].count; break; }
+            double thr = c->threshold_type == SG_CLUSTER_THRESHOLD_GLOBAL ? raw : raw * c->connected;
+            double next = thr - latest - q->acquire_count;
+            remaining = next;
+            if (next < 0) { passed = 0; break; }
+        }
+        if (passed)
+            for (uint32_t k = 0; k < q->n_values; ++k) cp_add(c, now, v[k], q->acquire_count);
+        if (q->n_values > 1) remaining = -1;  /* "Remaining field is unsupported for multi-values" */
+        if (passed) { o->status = SG_TOKEN_OK; o->remaining = j_d2i(remaining); }
+        else o->status = SG_TOKEN_BLOCKED;
+    }
+    return SG_OK;
+}
+
 int or_cluster_set_connected_count(or_engine* e, int64_t flow_id, int32_t connected) {
-    for (int i = 0; i < e->n_cl; ++i) if (e->cl[i].flow_id == flow_id) { e->cl[i].connected = connected; return SG_OK; }
-    return SG_ENOTFOUND;
+    /* ClusterFlowRuleManager / ClusterParamFlowRuleManager.getConnectedCount: the namespace's count */
+    int hit = 0;
+    for (int i = 0; i < e->n_cl; ++i) if (e->cl[i].flow_id == flow_id) { e->cl[i].connected = connected; hit = 1; }
+    for (int i = 0; i < e->n_cp; ++i) if (e->cp[i].flow_id == flow_id) { e->cp[i].connected = connected; hit = 1; }
+    return hit ? SG_OK : SG_ENOTFOUND;
 }
 
 int or_cluster_request_tokens(or_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out) {
@@ -2035,15 +2194,7 @@ int or_cluster_request_tokens(or_engine* e, const sg_token_req* reqs, uint64_t n
         for (int k = 0; k < e->n_cl; ++k) if (e->cl[k].flow_id == q->flow_id) c = &e->cl[k];
         if (!c) { o->status = SG_TOKEN_NO_RULE_EXISTS; continue; }
         int64_t now = q->ts;
-        /* GlobalRequestLimiter.tryPass (limit/GlobalRequestLimiter.java:46-54, RequestLimiter.java:72-87) */
-        if (e->max_allowed_qps >= 0) {  /* a negative qpsAllowed: no limiter registered -> tryPass true */
-            obucket* w = leap_current(&e->ns_limiter, now);
-            int64_t s = leap_sum(&e->ns_limiter, now, EV_PASS);
-            if (!((double)s / (e->ns_limiter.interval / 1000.0) + 1 <= e->max_allowed_qps)) {
-                o->status = SG_TOKEN_TOO_MANY_REQUEST; continue;
-            }
-            if (w) w->c[EV_PASS] += 1;
-        }
+        if (!ns_try_pass(e, now)) { o->status = SG_TOKEN_TOO_MANY_REQUEST; continue; }
         double latest_qps = cl_avg(c, now, CF_PASS_REQ);
         double thr = c->threshold_type == SG_CLUSTER_THRESHOLD_GLOBAL ? c->count : c->count * c->connected;
         double global_threshold = thr * e->exceed_count;

@@ -67,6 +67,8 @@ int or_param_set_thread_count(or_engine* e, uint32_t res, int32_t param_idx, uin
 /* ---- token server -------------------------------------------------------- */
 int or_cluster_set_connected_count(or_engine* e, int64_t flow_id, int32_t connected);
 int or_cluster_request_tokens(or_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out);
+int or_cluster_request_param_tokens(or_engine* e, const sg_param_token_req* reqs, uint64_t n, const uint64_t* values,
+                                    uint64_t n_values, sg_token_result* out);
 
 /* ---- unit-level hooks (mocked Node values, as the reference tests do) ---- */
 typedef struct or_ctrl or_ctrl;

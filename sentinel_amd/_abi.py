@@ -299,7 +299,8 @@ def degrade_rule(resource, count, time_window, grade=DEGRADE_GRADE_RT, limit_app
 
 def param_rule(resource, param_idx, count, grade=FLOW_GRADE_QPS, duration_in_sec=1, burst_count=0,
                control_behavior=CONTROL_BEHAVIOR_DEFAULT, max_queueing_time_ms=0, items=(), limit_app=None,
-               cluster_mode=False, cluster_flow_id=0, cluster_fallback_to_local=False):
+               cluster_mode=False, cluster_flow_id=0, cluster_fallback_to_local=False,
+               cluster_threshold_type=0, cluster_sample_count=10, cluster_window_interval_ms=1000):
     """A ParamFlowRule (param/slots/block/flow/param/ParamFlowRule.java:40-70).
 
     items: iterable of (object_str, class_type, count) hot items.
@@ -328,13 +329,25 @@ def param_rule(resource, param_idx, count, grade=FLOW_GRADE_QPS, duration_in_sec
     r.items = C.cast(arr, C.POINTER(SgParamItem))
     r._items = arr  # keep alive
     r.cluster_flow_id = cluster_flow_id
-    r.cluster_threshold_type = 0
+    r.cluster_threshold_type = cluster_threshold_type  # ParamFlowClusterConfig default: AVG_LOCAL (0)
     r.cluster_fallback_to_local = int(bool(cluster_fallback_to_local))
-    r.cluster_sample_count = 10
-    r.cluster_window_interval_ms = 1000
+    r.cluster_sample_count = cluster_sample_count
+    r.cluster_window_interval_ms = cluster_window_interval_ms
     return r
 
 
 # numpy views of sg_token_req / sg_token_result for bulk calls
 TOKEN_REQ_DTYPE = np.dtype([("ts", "<i8"), ("flow_id", "<i8"), ("acquire_count", "<i4"), ("prioritized", "<i4")])
+PARAM_TOKEN_REQ_DTYPE = np.dtype([("ts", "<i8"), ("flow_id", "<i8"), ("acquire_count", "<i4"), ("n_values", "<u4"),
+                                  ("value_off", "<u8")])
 TOKEN_RES_DTYPE = np.dtype([("status", "<i4"), ("remaining", "<i4"), ("wait_in_ms", "<i4"), ("reserved", "<i4")])
+
+
+def param_token_arrays(reqs):
+    """[(ts, flow_id, acquire, [value keys])] -> (PARAM_TOKEN_REQ_DTYPE array, uint64 values)."""
+    arr = np.zeros(len(reqs), dtype=PARAM_TOKEN_REQ_DTYPE)
+    vals = []
+    for i, (ts, fid, acq, vs) in enumerate(reqs):
+        arr[i] = (ts, fid, acq, len(vs), len(vals))
+        vals += [int(v) for v in vs]
+    return arr, np.array(vals, dtype=np.uint64)

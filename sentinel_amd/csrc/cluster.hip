@@ -270,4 +270,104 @@ hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_
     return hipGetLastError();
 }
 
+// ---- ClusterParamFlowChecker.acquireClusterToken (csrv/flow/ClusterParamFlowChecker.java:42-88)
+// One lane per param flow over its requests in time order (sorted positions), like k_tok_flow.  The
+// flow's ClusterParameterLeapArray keeps per-bucket value maps; here a value's counts live in a PVal
+// slot of an open-addressing table shared by all flows (claimed by CAS on PVal.flow; a lane only ever
+// looks up its own flow's values, which it inserted itself, so a lookup never races an insert it needs).
+__device__ __forceinline__ int pf_current(PFlow& F, int64_t now) {  // LeapArray.currentWindow (create / reset)
+    const int64_t wlen = F.interval / F.n;
+    const int idx = (int)((now / wlen) % F.n);
+    const int64_t ws = now - now % wlen;
+    if (F.fws[idx] < 0 || ws > F.fws[idx]) F.fws[idx] = ws;  // resetWindowTo clears the map: stamps differ
+    return idx;
+}
+__device__ PVal* pv_find(PVal* __restrict__ tab, uint32_t mask, uint32_t f, uint64_t key, bool create,
+                         uint32_t* __restrict__ flags) {
+    uint64_t h = tab_hash((int64_t)(key ^ ((uint64_t)f * 0xD6E8FEB86659FD93ull))) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        PVal* s = &tab[h];
+        uint32_t owner = __hip_atomic_load(&s->flow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (owner == PV_EMPTY) {
+            if (!create) return nullptr;
+            owner = atomicCAS(&s->flow, PV_EMPTY, f);
+            if (owner == PV_EMPTY) {  // claimed: a fresh (flow, value) entry
+                s->key = key;
+                for (int j = 0; j < CP_MAXN; ++j) { s->ws[j] = -1; s->cnt[j] = 0; }
+                return s;
+            }
+        }
+        if (owner == f && s->key == key) return s;
+        h = (h + 1) & mask;
+    }
+    atomicOr(flags, 2u);  // table full
+    return nullptr;
+}
+__global__ void k_ptok_flow(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals, uint64_t n,
+                            const sg_param_token_req* __restrict__ req, const uint64_t* __restrict__ values,
+                            PFlow* __restrict__ flows, uint32_t nflows, const PHot* __restrict__ hot,
+                            PVal* __restrict__ tab, uint32_t mask, sg_token_result* __restrict__ res,
+                            uint32_t* __restrict__ flags) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nflows) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) { const uint64_t mid = (lo + hi) / 2; if (skeys[mid] < f) lo = mid + 1; else hi = mid; }
+    uint64_t e = lo, h2 = n;
+    while (e < h2) { const uint64_t mid = (e + h2) / 2; if (skeys[mid] <= f) e = mid + 1; else h2 = mid; }
+    if (lo == e) return;
+    PFlow F = flows[f];
+    const double isec = F.interval / 1000.0;  // LeapArray.getIntervalInSecond
+    for (uint64_t p = lo; p < e; ++p) {
+        const uint32_t i = svals[p];
+        const sg_param_token_req q = req[i];
+        const int64_t now = q.ts;
+        const uint64_t* v = values + q.value_off;
+        double remaining = -1.0;
+        bool passed = true;
+        for (uint32_t k = 0; k < q.n_values; ++k) {
+            pf_current(F, now);  // ClusterParamMetric.getSum -> metric.currentWindow()
+            int64_t sum = 0;
+            const PVal* pv = pv_find(tab, mask, f, v[k], false, flags);
+            if (pv) {
+                for (int j = 0; j < F.n; ++j) {
+                    if (F.fws[j] < 0 || now - F.fws[j] > F.interval) continue;  // isWindowDeprecated (strict >)
+                    if (pv->ws[j] == F.fws[j]) sum += pv->cnt[j];
+                }
+            }
+            double raw = F.count;  // getRawThreshold: the exclusive item count, else rule.count
+            for (uint32_t hh = 0; hh < F.nhot; ++hh)
+                if (hot[F.hoff + hh].key == v[k]) { raw = (double)hot[F.hoff + hh].count; break; }
+            const double thr = F.thr_type == SG_CLUSTER_THRESHOLD_GLOBAL ? raw : raw * (double)F.connected;
+            const double next = thr - (double)sum / isec - (double)q.acquire_count;
+            remaining = next;
+            if (next < 0) { passed = false; break; }
+        }
+        sg_token_result o;
+        o.status = SG_TOKEN_BLOCKED; o.remaining = 0; o.wait_in_ms = 0; o.reserved = 0;
+        if (passed) {
+            for (uint32_t k = 0; k < q.n_values; ++k) {  // addValue to the current bucket of every value
+                const int idx = pf_current(F, now);
+                PVal* pv = pv_find(tab, mask, f, v[k], true, flags);
+                if (!pv) break;
+                if (pv->ws[idx] != F.fws[idx]) { pv->ws[idx] = F.fws[idx]; pv->cnt[idx] = 0; }
+                pv->cnt[idx] += q.acquire_count;
+            }
+            if (q.n_values > 1) remaining = -1.0;  // multi-value remaining is unsupported
+            o.status = SG_TOKEN_OK;
+            o.remaining = j_d2i(remaining);
+        }
+        res[i] = o;
+    }
+    flows[f] = F;
+}
+
+hipError_t launch_ptok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_param_token_req* req,
+                            const uint64_t* values, PFlow* flows, uint32_t nflows, const PHot* hot, PVal* tab,
+                            uint32_t mask, sg_token_result* res, uint32_t* flags, hipStream_t st) {
+    if (!n || !nflows) return hipSuccess;
+    hipLaunchKernelGGL(k_ptok_flow, dim3((nflows + 255) / 256), dim3(256), 0, st, skeys, svals, n, req, values, flows,
+                       nflows, hot, tab, mask, res, flags);
+    return hipGetLastError();
+}
+
 } // namespace sg

@@ -160,6 +160,29 @@ struct CSlot {         // flowId -> flow index (open addressing, idx 0xFFFFFFFF 
     int64_t key;
     uint32_t idx, pad;
 };
+// token server view of a cluster-mode ParamFlowRule + its ClusterParamMetric
+// (csrv/flow/statistic/metric/ClusterParamMetric.java:36-91, ClusterParameterLeapArray.java:30-58)
+#define CP_MAXN 16      // sampleCount bound of the device window (SG_ENOTSUP above)
+struct PFlow {
+    int64_t flow_id;
+    double count;                  // ParamFlowRule.count
+    int32_t thr_type;              // ParamFlowClusterConfig.thresholdType
+    int32_t n, interval;           // sampleCount, windowIntervalMs (fixed at creation)
+    int32_t connected;             // connected count of the namespace (AVG_LOCAL)
+    uint32_t hoff, nhot;           // parsed hot items: PHot[hoff, hoff + nhot)
+    int64_t fws[CP_MAXN];          // bucket window starts; < 0: never created
+};
+struct PHot {
+    uint64_t key;
+    int32_t count, pad;
+};
+#define PV_EMPTY 0xFFFFFFFFu
+struct PVal {                      // (flow, value) counts; live in bucket j while ws[j] == PFlow.fws[j]
+    uint64_t key;
+    uint32_t flow, pad;            // flow == PV_EMPTY: free slot (claimed by CAS)
+    int64_t ws[CP_MAXN];
+    int64_t cnt[CP_MAXN];
+};
 #define NS_BUCKETS 10   // RequestLimiter: UnaryLeapArray(10, 1000)
 #define NS_WLEN 100
 #define NS_INTERVAL 1000

@@ -69,6 +69,9 @@ hipError_t launch_tok_limiter(const sg_token_req* req, uint64_t n, const uint32_
 hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_token_req* req,
                            CFlow* flows, uint32_t nflows, CBkt* bkts, double exceed, double max_occ_ratio,
                            sg_token_result* res, hipStream_t st);
+hipError_t launch_ptok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_param_token_req* req,
+                            const uint64_t* values, PFlow* flows, uint32_t nflows, const PHot* hot, PVal* tab,
+                            uint32_t mask, sg_token_result* res, uint32_t* flags, hipStream_t st);
 } // namespace sg
 
 using namespace sg;
@@ -505,6 +508,18 @@ struct sg_engine {
     sg_token_result* d_tres = nullptr;
     uint32_t* d_tfidx = nullptr;
     uint64_t tcap = 0;
+    // cluster param flows (ClusterParamFlowRuleManager / ClusterParamMetricStatistics roles)
+    std::vector<PFlow> pflows;                    // host copy of the config part
+    std::unordered_map<int64_t, uint32_t> pmap;   // flowId -> param flow index
+    PFlow* d_pflow = nullptr;
+    PHot* d_phot = nullptr;
+    CSlot* d_pftab = nullptr;
+    uint32_t pftab_mask = 0;
+    PVal* d_pvtab = nullptr;                      // (flow, value) counts, 2^PV_LOG2 slots
+    uint32_t pv_mask = 0;
+    sg_param_token_req* d_preq = nullptr;
+    uint64_t* d_pvals = nullptr;
+    uint64_t pcap = 0, pvcap = 0;
     // snapshot scratch
     uint32_t *d_snap_cnt = nullptr, *d_snap_off = nullptr;
     sg_metric_node* d_snap_out = nullptr;
@@ -977,6 +992,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp);
+    dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
@@ -1234,6 +1250,100 @@ int sg_load_degrade_rules(sg_engine* e, const sg_degrade_rule* rules, uint32_t n
 }
 
 // ParamFlowRuleManager.loadRules (param/slots/block/flow/param/ParamFlowRuleManager.java:103-166)
+// ClusterParamFlowRuleManager.applyClusterParamRules (csrv/flow/rule/ClusterParamFlowRuleManager.java:318-369):
+// cluster-mode rules passing ParamFlowRuleUtil.isValidRule, in list order; the last rule of a flowId wins;
+// putMetricIfAbsent keeps the metric (window shape and value counts) of a flowId that stays; the metrics of
+// the others are dropped (their value slots leave the table).
+#define PV_LOG2 17
+static int rebuild_cluster_param(sg_engine* e, const sg_param_rule* rules, const std::vector<ParamR>& all, uint32_t n) {
+    std::vector<int64_t> order;
+    std::unordered_map<int64_t, uint32_t> rule_of;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_param_rule& r = rules[i];
+        if (!r.cluster_mode || !param_valid(r)) continue;
+        if (r.cluster_sample_count > CP_MAXN)
+            return fail(SG_ENOTSUP, "cluster param rules with sampleCount > 16 are not on the device path");
+        if (!rule_of.count(r.cluster_flow_id)) order.push_back(r.cluster_flow_id);
+        rule_of[r.cluster_flow_id] = i;
+    }
+    const uint32_t nold = (uint32_t)e->pflows.size();
+    std::vector<PFlow> old_f(nold);
+    if (nold) HIPCHK(hipMemcpy(old_f.data(), e->d_pflow, nold * sizeof(PFlow), hipMemcpyDeviceToHost));
+    std::vector<PFlow> nf;
+    std::vector<PHot> nh;
+    std::unordered_map<int64_t, uint32_t> nmap;
+    std::vector<uint32_t> remap(nold, PV_EMPTY);  // old flow index -> new (value slots that stay)
+    for (int64_t fid : order) {
+        const uint32_t ri = rule_of[fid];
+        const sg_param_rule& r = rules[ri];
+        PFlow f;
+        std::memset(&f, 0, sizeof(f));
+        auto it = e->pmap.find(fid);
+        if (it != e->pmap.end()) {
+            f = old_f[it->second];
+            remap[it->second] = (uint32_t)nf.size();
+        } else {
+            f.flow_id = fid;
+            f.n = r.cluster_sample_count;
+            f.interval = r.cluster_window_interval_ms;
+            for (int k = 0; k < CP_MAXN; ++k) f.fws[k] = -1;
+        }
+        f.count = r.count;
+        f.thr_type = r.cluster_threshold_type;
+        f.hoff = (uint32_t)nh.size();
+        f.nhot = (uint32_t)all[ri].hot.size();  // ParamFlowRuleUtil.fillExceptionFlowItems
+        for (auto& h : all[ri].hot) { PHot x; x.key = h.first; x.count = h.second; x.pad = 0; nh.push_back(x); }
+        nmap[fid] = (uint32_t)nf.size();
+        nf.push_back(f);
+    }
+    const uint32_t cap_v = 1u << PV_LOG2;
+    const bool need_v = !nf.empty() || e->d_pvtab;  // no table until a cluster param rule exists
+    std::vector<PVal> vt(need_v ? cap_v : 0);
+    if (!need_v) {}
+    else if (e->d_pvtab) HIPCHK(hipMemcpy(vt.data(), e->d_pvtab, cap_v * sizeof(PVal), hipMemcpyDeviceToHost));
+    else for (auto& v : vt) v.flow = PV_EMPTY;
+    // re-insert the value slots of the flows that stay, under their new flow index (same probe as pv_find)
+    std::vector<PVal> keep;
+    for (auto& v : vt) if (v.flow != PV_EMPTY && v.flow < nold && remap[v.flow] != PV_EMPTY) { keep.push_back(v); keep.back().flow = remap[v.flow]; }
+    for (auto& v : vt) { v.flow = PV_EMPTY; v.key = 0; }
+    for (auto& v : keep) {
+        uint64_t h = tab_hash_h((int64_t)(v.key ^ ((uint64_t)v.flow * 0xD6E8FEB86659FD93ull))) & (cap_v - 1);
+        while (vt[h].flow != PV_EMPTY) h = (h + 1) & (cap_v - 1);
+        vt[h] = v;
+    }
+    uint32_t cap = 16;
+    while (cap < 2 * nf.size() + 2) cap <<= 1;
+    std::vector<CSlot> tab(cap);
+    for (auto& t : tab) { t.key = 0; t.idx = 0xFFFFFFFFu; t.pad = 0; }
+    for (uint32_t i = 0; i < nf.size(); ++i) {
+        uint64_t h = tab_hash_h(nf[i].flow_id) & (cap - 1);
+        while (tab[h].idx != 0xFFFFFFFFu) h = (h + 1) & (cap - 1);
+        tab[h].key = nf[i].flow_id;
+        tab[h].idx = i;
+    }
+    dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab);
+    e->d_pflow = nullptr; e->d_phot = nullptr; e->d_pftab = nullptr;
+    if (!nf.empty()) {
+        HIPCHK(hipMalloc(&e->d_pflow, nf.size() * sizeof(PFlow)));
+        HIPCHK(hipMemcpy(e->d_pflow, nf.data(), nf.size() * sizeof(PFlow), hipMemcpyHostToDevice));
+    }
+    if (!nh.empty()) {
+        HIPCHK(hipMalloc(&e->d_phot, nh.size() * sizeof(PHot)));
+        HIPCHK(hipMemcpy(e->d_phot, nh.data(), nh.size() * sizeof(PHot), hipMemcpyHostToDevice));
+    }
+    if (need_v) {
+        if (!e->d_pvtab) HIPCHK(hipMalloc(&e->d_pvtab, cap_v * sizeof(PVal)));
+        HIPCHK(hipMemcpy(e->d_pvtab, vt.data(), cap_v * sizeof(PVal), hipMemcpyHostToDevice));
+        e->pv_mask = cap_v - 1;
+    }
+    HIPCHK(hipMalloc(&e->d_pftab, cap * sizeof(CSlot)));
+    HIPCHK(hipMemcpy(e->d_pftab, tab.data(), cap * sizeof(CSlot), hipMemcpyHostToDevice));
+    e->pftab_mask = cap - 1;
+    e->pflows = std::move(nf);
+    e->pmap = std::move(nmap);
+    return SG_OK;
+}
+
 int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
     if (int rc = drain(e)) return rc;  // no batch in flight while the rule tables change
@@ -1251,6 +1361,7 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
         if (n_loaded) *n_loaded = (uint32_t)e->params.size();
         return SG_OK;
     }
+    if (int rc = rebuild_cluster_param(e, rules, all, n)) return rc;
     std::vector<ParamR> ps;
     std::vector<std::vector<int>> per;
     std::unordered_map<std::string, int> seen;
@@ -1609,10 +1720,18 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
 int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected) {
     if (!e) return fail(SG_EINVAL, "null engine");
     if (int rc = drain(e)) return rc;
+    // ClusterFlowRuleManager / ClusterParamFlowRuleManager.getConnectedCount: the namespace's count
     auto it = e->cmap.find(flow_id);
-    if (it == e->cmap.end()) return fail(SG_ENOTFOUND, "no cluster flow rule with this flowId");
-    e->cflows[it->second].connected = connected;
-    HIPCHK(hipMemcpy(&e->d_cflow[it->second].connected, &connected, sizeof(int32_t), hipMemcpyHostToDevice));
+    auto pt = e->pmap.find(flow_id);
+    if (it == e->cmap.end() && pt == e->pmap.end()) return fail(SG_ENOTFOUND, "no cluster rule with this flowId");
+    if (it != e->cmap.end()) {
+        e->cflows[it->second].connected = connected;
+        HIPCHK(hipMemcpy(&e->d_cflow[it->second].connected, &connected, sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (pt != e->pmap.end()) {
+        e->pflows[pt->second].connected = connected;
+        HIPCHK(hipMemcpy(&e->d_pflow[pt->second].connected, &connected, sizeof(int32_t), hipMemcpyHostToDevice));
+    }
     return SG_OK;
 }
 
@@ -1675,6 +1794,93 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
     }
     HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    return SG_OK;
+}
+
+// Batched DefaultTokenService.requestParamToken: the flow path's classify and namespace limiter steps on a
+// derived sg_token_req view (n_values == 0 -> acquire 0 -> BAD_REQUEST), then k_ptok_flow per param flow.
+int sg_cluster_request_param_tokens(sg_engine* e, const sg_param_token_req* reqs, uint64_t n, const uint64_t* values,
+                                    uint64_t n_values, sg_token_result* out) {
+    if (!e || (n && (!reqs || !out)) || (n_values && !values)) return fail(SG_EINVAL, "null argument");
+    if (!n) return SG_OK;
+    if (n > 0x7FFFFFFFull) return fail(SG_EINVAL, "too many token requests in one call");
+    for (uint64_t i = 0; i < n; ++i)
+        if (reqs[i].value_off > n_values || reqs[i].n_values > n_values - reqs[i].value_off)
+            return fail(SG_EINVAL, "param token request values out of range");
+    if (int rc = drain(e)) return rc;
+    hipStream_t st = e->stream;
+    int rc = ensure_batch(e, n);
+    if (rc) return rc;
+    if (n > e->tcap) {
+        dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
+        uint64_t c = std::max<uint64_t>(n, 1u << 16);
+        HIPCHK(hipMalloc(&e->d_treq, c * sizeof(sg_token_req)));
+        HIPCHK(hipMalloc(&e->d_tres, c * sizeof(sg_token_result)));
+        HIPCHK(hipMalloc(&e->d_tfidx, c * 4));
+        e->tcap = c;
+    }
+    if (n > e->pcap) {
+        dfree(e->d_preq);
+        e->pcap = std::max<uint64_t>(n, 1u << 16);
+        HIPCHK(hipMalloc(&e->d_preq, e->pcap * sizeof(sg_param_token_req)));
+    }
+    if (n_values > e->pvcap) {
+        dfree(e->d_pvals);
+        e->pvcap = std::max<uint64_t>(n_values, 1u << 16);
+        HIPCHK(hipMalloc(&e->d_pvals, e->pvcap * sizeof(uint64_t)));
+    }
+    if (!e->d_nslim) {
+        HIPCHK(hipMalloc(&e->d_nslim, sizeof(NsLimiter)));
+        NsLimiter z;
+        for (int k = 0; k < NS_BUCKETS; ++k) { z.ws[k] = -1; z.cnt[k] = 0; }
+        HIPCHK(hipMemcpy(e->d_nslim, &z, sizeof(z), hipMemcpyHostToDevice));
+    }
+    if (!e->d_pftab) {  // no cluster param rule loaded yet: an empty table
+        CSlot t[16];
+        for (auto& x : t) { x.key = 0; x.idx = 0xFFFFFFFFu; x.pad = 0; }
+        HIPCHK(hipMalloc(&e->d_pftab, sizeof(t)));
+        HIPCHK(hipMemcpy(e->d_pftab, t, sizeof(t), hipMemcpyHostToDevice));
+        e->pftab_mask = 15;
+    }
+    std::vector<sg_token_req> tq(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        tq[i].ts = reqs[i].ts;
+        tq[i].flow_id = reqs[i].flow_id;
+        tq[i].acquire_count = reqs[i].n_values ? reqs[i].acquire_count : 0;  // empty params -> badRequest
+        tq[i].prioritized = 0;
+    }
+    const uint32_t nflows = (uint32_t)e->pflows.size();
+    HIPCHK(hipMemcpyAsync(e->d_treq, tq.data(), n * sizeof(sg_token_req), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->d_preq, reqs, n * sizeof(sg_param_token_req), hipMemcpyHostToDevice, st));
+    if (n_values) HIPCHK(hipMemcpyAsync(e->d_pvals, values, n_values * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(e->d_small, 0, 4, st));
+    HIPCHK(launch_tok_classify(e->d_treq, n, e->d_pftab, e->pftab_mask, e->d_tfidx, e->d_tres, e->d_small, st));
+    uint32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, e->d_small, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flags & 1) return fail(SG_EINVAL, "token requests must be ordered by ts (the replay clock)");
+    const double allowed = e->cfg.cluster_max_allowed_qps < 0 ? 1.0 / 0.0 : (double)e->cfg.cluster_max_allowed_qps;
+    HIPCHK(launch_tok_limiter(e->d_treq, n, e->d_tfidx, nflows, e->d_nslim, allowed, e->d_k0, e->d_v0, e->d_tres, st));
+    if (nflows) {
+        int bits = 1;
+        while (bits < 32 && (1ull << bits) <= nflows) ++bits;
+        const int passes = (bits + 7) / 8;
+        const uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
+        uint32_t *kin = e->d_k0, *vin = e->d_v0, *kout = e->d_k1, *vout = e->d_v1;
+        for (int p = 0; p < passes; ++p) {
+            HIPCHK(launch_radix_hist(kin, n, p * 8, e->d_hist, nblocks, st));
+            HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks * 256, e->d_part, nullptr, st));
+            HIPCHK(launch_radix_scatter(kin, vin, n, p * 8, e->d_hist, nblocks, kout, vout, nullptr, st));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        HIPCHK(launch_ptok_flow(kin, vin, n, e->d_preq, e->d_pvals, e->d_pflow, nflows, e->d_phot, e->d_pvtab,
+                                e->pv_mask, e->d_tres, e->d_small, st));
+    }
+    HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&flags, e->d_small, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flags & 2) return fail(SG_ENOMEM, "cluster param value table is full");
     return SG_OK;
 }
 

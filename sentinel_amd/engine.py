@@ -23,7 +23,7 @@ EXPORTS = (
     "sg_config_default", "sg_engine_create", "sg_engine_destroy", "sg_register_resources", "sg_resource_id",
     "sg_load_flow_rules", "sg_load_degrade_rules", "sg_load_param_rules", "sg_param_key", "sg_submit",
     "sg_submit_async", "sg_sync", "sg_snapshot_metrics", "sg_cluster_set_connected_count",
-    "sg_cluster_request_tokens", "sg_read_node", "sg_last_error", "sg_last_timings",
+    "sg_cluster_request_tokens", "sg_cluster_request_param_tokens", "sg_read_node", "sg_last_error", "sg_last_timings",
 )
 
 
@@ -55,6 +55,7 @@ def lib():
         L.sg_snapshot_metrics.argtypes = [P, C.c_int64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.sg_cluster_set_connected_count.argtypes = [P, C.c_int64, C.c_int32]
         L.sg_cluster_request_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_cluster_request_param_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.sg_read_node.argtypes = [P, C.c_uint32, C.c_int64, C.POINTER(A.SgNodeState)]
         L.sg_last_error.restype = C.c_char_p
         L.sg_last_timings.argtypes = [P, C.POINTER(C.c_double), C.c_int]
@@ -210,4 +211,20 @@ class Engine:
         for i, (ts, fid, acq, pr) in enumerate(reqs):
             arr[i] = (ts, fid, acq, int(pr))
         out = self.cluster_request_array(arr)
+        return [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in out]
+
+    # ---- TokenService.requestParamToken (csrv/flow/DefaultTokenService.java:50-61)
+    def cluster_request_param_array(self, reqs: np.ndarray, values: np.ndarray) -> np.ndarray:
+        """reqs: A.PARAM_TOKEN_REQ_DTYPE (time-ordered), values: uint64 keys -> A.TOKEN_RES_DTYPE array."""
+        reqs = np.ascontiguousarray(reqs, dtype=A.PARAM_TOKEN_REQ_DTYPE)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.zeros(len(reqs), dtype=A.TOKEN_RES_DTYPE)
+        _check(lib().sg_cluster_request_param_tokens(self.h, reqs.ctypes.data, len(reqs), values.ctypes.data,
+                                                     len(values), out.ctypes.data))
+        return out
+
+    def cluster_request_param(self, reqs):
+        """reqs: list of (ts, flow_id, acquire, [value keys]) -> list of (status, remaining, wait)."""
+        arr, vals = A.param_token_arrays(reqs)
+        out = self.cluster_request_param_array(arr, vals)
         return [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in out]

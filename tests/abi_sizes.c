@@ -14,6 +14,7 @@ int main(void) {
     printf("sg_node_state %zu\n", sizeof(sg_node_state));
     printf("sg_token_req %zu\n", sizeof(sg_token_req));
     printf("sg_token_result %zu\n", sizeof(sg_token_result));
+    printf("sg_param_token_req %zu\n", sizeof(sg_param_token_req));
     printf("ev.aux %zu\n", offsetof(sg_event, aux));
     printf("cfg.cluster_exceed_count %zu\n", offsetof(sg_config, cluster_exceed_count));
     printf("param.items %zu\n", offsetof(sg_param_rule, items));

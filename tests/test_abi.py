@@ -52,6 +52,7 @@ def test_struct_layouts_match_header(tmp_path):
     assert got["sg_node_state"] == C.sizeof(A.SgNodeState)
     assert got["sg_token_req"] == C.sizeof(A.SgTokenReq)
     assert got["sg_token_result"] == C.sizeof(A.SgTokenResult)
+    assert got["sg_param_token_req"] == A.PARAM_TOKEN_REQ_DTYPE.itemsize
     assert got["ev.aux"] == A.EVENT_DTYPE.fields["aux"][1]
     assert got["cfg.cluster_exceed_count"] == A.SgConfig.cluster_exceed_count.offset
     assert got["param.items"] == A.SgParamRule.items.offset
