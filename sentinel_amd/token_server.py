@@ -19,8 +19,12 @@ Reference (csrv/ = sentinel-cluster/sentinel-cluster-server-default/src/main/jav
   csrv/processor/FlowRequestProcessor.java:33-52             TokenResult -> (status, remaining, wait)
   cluster/ClusterConstants.java:24-40 (sentinel-cluster-common-default)  message types, status codes
 
-Not on the device: MSG_TYPE_PARAM_FLOW (ClusterParamFlowChecker) is answered with
-RESPONSE_STATUS_BAD, exactly what TokenServerHandler writes for a type without a processor.
+  csrv/server/codec/data/ParamFlowRequestDataDecoder.java:33-90  long flowId, int count, int amount,
+                                                   typed params (ClusterConstants.PARAM_TYPE_*)
+  csrv/processor/ParamFlowRequestProcessor.java:33-52        requestParamToken -> (status, remaining, 0)
+
+PARAM_FLOW requests of a tick are decided in one `sg_cluster_request_param_tokens` call; their
+typed values are interned with the same 64-bit keys as the rules' hot items (`sg_param_key`).
 """
 from __future__ import annotations
 
@@ -49,6 +53,22 @@ class ClusterRequest:
     xid: int
     type: int
     data: object  # FlowRequest, str (ping namespace) or None
+
+
+PARAM_TYPE_INTEGER, PARAM_TYPE_LONG, PARAM_TYPE_BYTE, PARAM_TYPE_DOUBLE = 0, 1, 2, 3
+PARAM_TYPE_FLOAT, PARAM_TYPE_SHORT, PARAM_TYPE_BOOLEAN, PARAM_TYPE_STRING = 4, 5, 6, 7
+# wire type -> (struct format, Java class of the decoded object, as sg_param_key names it)
+_PARAM_WIRE = {PARAM_TYPE_INTEGER: (">i", "java.lang.Integer"), PARAM_TYPE_LONG: (">q", "java.lang.Long"),
+               PARAM_TYPE_BYTE: (">b", "java.lang.Byte"), PARAM_TYPE_DOUBLE: (">d", "java.lang.Double"),
+               PARAM_TYPE_FLOAT: (">f", "java.lang.Float"), PARAM_TYPE_SHORT: (">h", "java.lang.Short"),
+               PARAM_TYPE_BOOLEAN: (">?", "java.lang.Boolean")}
+
+
+@dataclass
+class ParamFlowRequest:
+    flow_id: int
+    count: int
+    params: list  # [(java class, value)]
 
 
 @dataclass
@@ -80,8 +100,58 @@ def decode_request(body: bytes) -> Optional[ClusterRequest]:
                 data = rest[4:4 + n].decode("utf-8", "replace")
         return ClusterRequest(xid, typ, data)
     if typ == MSG_TYPE_PARAM_FLOW:
-        return ClusterRequest(xid, typ, None)  # decoded only far enough to answer BAD
+        return ClusterRequest(xid, typ, decode_param_flow(rest) if rest else None)
     return None  # "Unknown type of request data decoder": dropped
+
+
+def decode_param_flow(b: bytes) -> Optional[ParamFlowRequest]:
+    """ParamFlowRequestDataDecoder.decode: None unless >= 16 bytes and amount > 0.  An unknown param type
+    stops decoding (the reference skips the value without consuming its bytes)."""
+    if len(b) < 16:
+        return None
+    fid, cnt, amount = struct.unpack_from(">qii", b, 0)
+    if amount <= 0:
+        return None
+    off, params = 16, []
+    try:
+        for _ in range(amount):
+            t = struct.unpack_from(">b", b, off)[0]
+            off += 1
+            if t == PARAM_TYPE_STRING:
+                n = struct.unpack_from(">i", b, off)[0]
+                params.append(("java.lang.String", b[off + 4:off + 4 + n].decode("utf-8", "replace")))
+                off += 4 + n
+            elif t in _PARAM_WIRE:
+                fmt, cls = _PARAM_WIRE[t]
+                v = struct.unpack_from(fmt, b, off)[0]
+                params.append((cls, v))
+                off += struct.calcsize(fmt)
+            else:
+                break
+    except struct.error:
+        pass
+    return ParamFlowRequest(fid, cnt, params)
+
+
+def encode_param_flow_request(xid: int, flow_id: int, count: int, params) -> bytes:
+    """Client side (ParamFlowRequestDataWriter): params = [(PARAM_TYPE_*, value)]."""
+    body = struct.pack(">ibqii", xid, MSG_TYPE_PARAM_FLOW, flow_id, count, len(params))
+    for t, v in params:
+        if t == PARAM_TYPE_STRING:
+            raw = v.encode("utf-8")
+            body += struct.pack(">bi", t, len(raw)) + raw
+        else:
+            body += struct.pack(">b", t) + struct.pack(_PARAM_WIRE[t][0], v)
+    return frame(body)
+
+
+def param_value_text(cls: str, v) -> str:
+    """Text of a decoded value as sg_param_key parses it (Java's toString for the boxed types)."""
+    if cls == "java.lang.Boolean":
+        return "true" if v else "false"
+    if cls in ("java.lang.Double", "java.lang.Float"):
+        return repr(float(v))
+    return str(v)
 
 
 def encode_flow_request(xid: int, flow_id: int, count: int, priority: bool) -> bytes:
@@ -103,6 +173,11 @@ def encode_ping_response(xid: int, connected: int) -> bytes:
     return frame(struct.pack(">ibbB", xid, MSG_TYPE_PING, RESPONSE_STATUS_OK, connected & 0xFF))
 
 
+def encode_param_flow_response(xid: int, status: int, remaining: int) -> bytes:
+    """ParamFlowRequestProcessor.toResponse + FlowResponseDataWriter (waitInMs is always 0)."""
+    return frame(struct.pack(">ibbii", xid, MSG_TYPE_PARAM_FLOW, status, remaining, 0))
+
+
 def encode_bad_response(xid: int, typ: int) -> bytes:
     return frame(struct.pack(">ibb", xid, typ, RESPONSE_STATUS_BAD))
 
@@ -111,7 +186,7 @@ def decode_response(body: bytes) -> Tuple[int, int, int, object]:
     """Client side (DefaultResponseEntityDecoder): (xid, type, status, data)."""
     xid, typ, st = struct.unpack_from(">ibb", body, 0)
     rest = body[6:]
-    if typ == MSG_TYPE_FLOW and len(rest) >= 8:
+    if typ in (MSG_TYPE_FLOW, MSG_TYPE_PARAM_FLOW) and len(rest) >= 8:
         return xid, typ, st, struct.unpack_from(">ii", rest, 0)
     if typ == MSG_TYPE_PING and len(rest) >= 1:
         return xid, typ, st, struct.unpack_from(">b", rest, 0)[0]
@@ -173,7 +248,8 @@ class TokenServer:
     (TimeUtil.currentTimeMillis); tests inject a replay clock.  `max_batch` bounds one device call."""
 
     def __init__(self, service, flow_namespaces: Optional[Dict[int, str]] = None,
-                 clock: Optional[Callable[[], int]] = None, max_batch: int = 65536, record: bool = False):
+                 clock: Optional[Callable[[], int]] = None, max_batch: int = 65536, record: bool = False,
+                 param_key: Optional[Callable[[str, str], int]] = None):
         self.service = service
         self.flow_ns = dict(flow_namespaces or {})
         self.clock = clock or (lambda: int(time.time() * 1000))
@@ -181,6 +257,8 @@ class TokenServer:
         self.record = record
         self.conns = ConnectionManager()
         self._pending: List[Tuple[asyncio.StreamWriter, int, FlowRequest]] = []
+        self._ppending: List[Tuple[asyncio.StreamWriter, int, ParamFlowRequest]] = []
+        self.param_key = param_key  # (text, java class) -> interned 64-bit key
         self._wake = asyncio.Event()
         self._server = None
         self._batcher = None
@@ -233,6 +311,10 @@ class TokenServer:
                         if req.data is not None:  # the reference's processor NPEs on a null body
                             self._pending.append((writer, req.xid, req.data))
                             self._wake.set()
+                    elif req.type == MSG_TYPE_PARAM_FLOW and self.param_key is not None:
+                        if req.data is not None:  # the reference's processor NPEs on a null body
+                            self._ppending.append((writer, req.xid, req.data))
+                            self._wake.set()
                     else:
                         writer.write(encode_bad_response(req.xid, req.type))
         except (ValueError, ConnectionError):
@@ -250,6 +332,9 @@ class TokenServer:
             while self._pending:
                 batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
                 self._decide(batch)
+            while self._ppending:
+                batch, self._ppending = self._ppending[: self.max_batch], self._ppending[self.max_batch:]
+                self._decide_param(batch)
 
     def _decide(self, batch):
         now = self.clock()
@@ -265,3 +350,18 @@ class TokenServer:
         for (w, xid, _), o in zip(batch, res):
             if not w.is_closing():
                 w.write(encode_flow_response(xid, int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])))
+
+    def _decide_param(self, batch):
+        now = self.clock()
+        reqs = np.zeros(len(batch), dtype=A.PARAM_TOKEN_REQ_DTYPE)
+        vals: List[int] = []
+        for j, (_, _, r) in enumerate(batch):
+            reqs[j] = (now, r.flow_id, r.count, len(r.params), len(vals))
+            vals += [self.param_key(param_value_text(c, v), c) for c, v in r.params]
+        res = self.service.cluster_request_param_array(reqs, np.array(vals, dtype=np.uint64))
+        self.batches.append(len(batch))
+        if self.record:
+            self.submitted.append(([x for _, x, _ in batch], (reqs, vals), res))
+        for (w, xid, _), o in zip(batch, res):
+            if not w.is_closing():
+                w.write(encode_param_flow_response(xid, int(o["status"]), int(o["remaining"])))
