@@ -22,9 +22,27 @@ using namespace sg;
 // 1. grouping: stable LSD radix sort on res_id
 // =================================================================================
 #define RS_THREADS 256
+#ifndef RS_ITEMS
 #define RS_ITEMS 16
+#endif
 #define RS_TILE (RS_THREADS * RS_ITEMS)
 #define RS_BINS 256
+
+// Per-block digit histogram in LDS with one atomic per group of equal digits in a wave (DB
+// ballots find the peers): Zipf-hot resources put most of a wave on one digit, which would
+// otherwise serialise 64 LDS atomics on one address.
+template <int DB>
+__device__ __forceinline__ void hist_add(uint32_t* h, uint32_t d, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < DB; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int l = threadIdx.x & 63;
+    const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
+    if (valid && (peers & lt) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+}
 
 // First pass over the caller's events, in submission order (coalesced): validates the batch,
 // builds the 16-byte decide record of every event (references to ENTRYs of earlier batches are
@@ -32,6 +50,7 @@ using namespace sg;
 // are mapped to its sorted position after the sort), writes the sort keys/values (value bit 31 =
 // "is an ENTRY", so the inverse permutation also says whether a reference hits an ENTRY) and the
 // histogram of the first radix digit.
+template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
                                                       uint64_t gbase, const uint8_t* __restrict__ ring,
                                                       uint64_t ring_mask, int32_t max_rt, SEv* __restrict__ rec_o,
@@ -40,15 +59,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                                                       uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out,
                                                       uint8_t* __restrict__ prio, uint64_t* __restrict__ key_ring,
                                                       const uint32_t* __restrict__ comp) {
-    __shared__ uint32_t h[RS_BINS];
-    for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
+    constexpr int NB = 1 << DB;
+    __shared__ uint32_t h[NB];
+    for (int i = threadIdx.x; i < NB; i += RS_THREADS) h[i] = 0;
     __syncthreads();
     const int64_t t0 = ev[0].ts;
     if (blockIdx.x == 0 && threadIdx.x == 0) *t0_out = t0;
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
     uint32_t fl = 0;
+    uint32_t hkey[RS_ITEMS];
+#pragma unroll
     for (int it = 0; it < RS_ITEMS; ++it) {
         const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        hkey[it] = 0;
         if (i >= n) continue;
         const sg_event e = ev[i];
         if (e.res_id >= max_res) fl |= BF_BAD_RES;
@@ -92,44 +115,56 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         const uint32_t key = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
         keys[i] = key;
         vals[i] = (uint32_t)i | (e.kind == SG_EV_ENTRY ? 0x80000000u : 0u);
-        atomicAdd(&h[key & (RS_BINS - 1)], 1u);
+        hkey[it] = key;
+    }
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
+        hist_add<DB>(h, hkey[it] & (NB - 1), i < n);
     }
     if (fl) atomicOr(bflags, fl);
     __syncthreads();
-    for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
+    for (int b = threadIdx.x; b < NB; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
+template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, uint64_t n, int shift,
                                                         uint32_t* __restrict__ ghist, uint32_t nblocks) {
-    __shared__ uint32_t h[RS_BINS];
-    for (int i = threadIdx.x; i < RS_BINS; i += RS_THREADS) h[i] = 0;
+    constexpr int NB = 1 << DB;
+    __shared__ uint32_t h[NB];
+    for (int i = threadIdx.x; i < NB; i += RS_THREADS) h[i] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll
     for (int it = 0; it < RS_ITEMS; ++it) {
         const uint64_t i = base + (uint64_t)it * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RS_BINS - 1)], 1u);
+        hist_add<DB>(h, i < n ? (keys[i] >> shift) & (NB - 1) : 0u, i < n);
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < RS_BINS; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
+    for (int b = threadIdx.x; b < NB; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// Stable scatter of one 8-bit digit.  Wave w of a tile owns the contiguous quarter
+// Stable scatter of one DB-bit digit (8 or 10).  Wave w of a tile owns the contiguous quarter
 // [base + w*1024, base + (w+1)*1024) and walks it in 16 coalesced rounds of 64, so input order is
 // (wave, round, lane): every wave ranks its own items against a wave-private digit counter
-// (peers by 8 ballots, no block barrier per round), one block-wide scan turns the four waves'
+// (peers by DB ballots, no block barrier per round), one block-wide scan turns the four waves'
 // counts into digit-run offsets, and the tile is placed digit-sorted in LDS.  It then leaves in
 // digit runs, so the writes of a run are consecutive addresses.  The last pass also writes the
 // inverse permutation pos_of[idx] = sorted position | ENTRY bit.  (The per-block digit histograms
-// of k_rs_first / k_radix_hist count the same 4096-item tile, in any order.)
+// of k_rs_first / k_radix_hist count the same 4096-item tile, in any order.)  10-bit digits sort
+// 20-bit keys (1M resources) in two passes instead of three.
+template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                            uint32_t* __restrict__ pos_of) {
-    static_assert(RS_BINS == RS_THREADS, "one digit per thread in the offset scan");
+    constexpr int NB = 1 << DB;
+    constexpr int DPT = NB / RS_THREADS;  // digits per thread in the offset scan
+    static_assert(NB % RS_THREADS == 0, "whole digits per thread");
     __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
-    __shared__ uint32_t wcnt[4][RS_BINS];   // per-wave digit counts, then per-wave digit offsets
-    __shared__ int64_t gdst[RS_BINS];       // global position of local position 0 of each digit's run
+    __shared__ uint32_t wcnt[4][NB];   // per-wave digit counts, then per-wave digit offsets
+    __shared__ int64_t gdst[NB];       // global position of local position 0 of each digit's run
     __shared__ uint32_t wtot[4];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
@@ -142,7 +177,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
         kk[it] = i < n ? keys_in[i] : 0u;
         vv[it] = i < n ? vals_in[i] : 0u;
     }
-    for (int i = threadIdx.x; i < 4 * RS_BINS; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 4 * NB; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
     uint32_t* myc = wcnt[w];
@@ -150,10 +185,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
     for (int it = 0; it < RS_ITEMS; ++it) {
         const uint64_t i = wbase + (uint64_t)it * WAVE + l;
         const bool valid = i < n;
-        const uint32_t d = (kk[it] >> shift) & (RS_BINS - 1);
+        const uint32_t d = (kk[it] >> shift) & (NB - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < DB; ++b) {
             const uint64_t bb = __ballot((d >> b) & 1);
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
@@ -165,10 +200,14 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
         if (valid && rank == 0) myc[d] = old + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    {   // digit b = thread b: run offsets (exclusive scan over digits), then the waves in order
-        const int b = threadIdx.x;
-        const uint32_t c0 = wcnt[0][b], c1 = wcnt[1][b], c2 = wcnt[2][b], c3 = wcnt[3][b];
-        const uint32_t t = c0 + c1 + c2 + c3;
+    {   // thread t owns digits [t*DPT, (t+1)*DPT): run offsets (exclusive scan over digits), then the waves
+        uint32_t c[DPT][4], t = 0;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int d = threadIdx.x * DPT + j;
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) { c[j][ww] = wcnt[ww][d]; t += c[j][ww]; }
+        }
         uint32_t x = t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -179,18 +218,20 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
         __syncthreads();
         uint32_t acc = x - t;
         for (int ww = 0; ww < w; ++ww) acc += wtot[ww];
-        gdst[b] = (int64_t)goff[(uint64_t)b * nblocks + blockIdx.x] - (int64_t)acc;
-        wcnt[0][b] = acc;
-        wcnt[1][b] = acc + c0;
-        wcnt[2][b] = acc + c0 + c1;
-        wcnt[3][b] = acc + c0 + c1 + c2;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int d = threadIdx.x * DPT + j;
+            gdst[d] = (int64_t)goff[(uint64_t)d * nblocks + blockIdx.x] - (int64_t)acc;
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) { wcnt[ww][d] = acc; acc += c[j][ww]; }
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < RS_ITEMS; ++it) {
         const uint64_t i = wbase + (uint64_t)it * WAVE + l;
         if (i < n) {
-            const uint32_t lp = myc[(kk[it] >> shift) & (RS_BINS - 1)] + rk[it];
+            const uint32_t lp = myc[(kk[it] >> shift) & (NB - 1)] + rk[it];
             sk[lp] = kk[it];
             sv[lp] = vv[it];
         }
@@ -198,7 +239,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < cnt_tile; p += RS_THREADS) {  // digit runs: consecutive addresses
         const uint32_t k = sk[p], v = sv[p];
-        const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (RS_BINS - 1)] + (int64_t)p);
+        const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (NB - 1)] + (int64_t)p);
         keys_out[dst] = k;
         vals_out[dst] = v;
         if (pos_of) pos_of[v & 0x7FFFFFFFu] = (uint32_t)dst | (v & 0x80000000u);
@@ -377,20 +418,29 @@ namespace sg {
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
-                           uint64_t* key_ring, const uint32_t* comp, hipStream_t st) {
-    hipLaunchKernelGGL(k_rs_first, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask, max_rt,
-                       rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
+                           uint64_t* key_ring, const uint32_t* comp, int db, hipStream_t st) {
+    if (db == 10)
+        hipLaunchKernelGGL(k_rs_first<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
+                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
+    else
+        hipLaunchKernelGGL(k_rs_first<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
+                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
+                             hipStream_t st, int db) {
+    if (db == 10) hipLaunchKernelGGL(k_radix_hist<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
+    else hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
     return hipGetLastError();
 }
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
-                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks, kout,
-                       vout, pos_of);
+                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st, int db) {
+    if (db == 10)
+        hipLaunchKernelGGL(k_radix_scatter<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
+                           kout, vout, pos_of);
+    else
+        hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
+                           kout, vout, pos_of);
     return hipGetLastError();
 }
 uint32_t radix_tile() { return RS_TILE; }

@@ -112,6 +112,11 @@ def test_c4_degrade(bin_mode):
     _run(4, batches=3, n_entries=400_000, n_res=50_000)
 
 
+def test_c4_wide_keys_two_10bit_passes():
+    # 200k resources: 18-bit keys sort in two 10-bit radix passes (the 1M-resource bench layout)
+    _run(4, batches=2, n_entries=600_000, n_res=200_000)
+
+
 def test_c5_param(bin_mode):
     _run(5, batches=3, n_entries=400_000, n_param_values=50_000)
 
