@@ -61,6 +61,82 @@ __global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const
     s.bin = 0;
     segs[pos[i]] = s;
 }
+// Fused segment detection (the default; SG_SEG_FUSED=0 keeps flags + n-wide scan + k_seg_start):
+// a tile of 4096 sorted keys per workgroup, 16 consecutive keys per lane (4 x 16-byte loads);
+// k_seg_count writes the tile's segment-start count, a scan over tiles gives the offsets, and
+// k_seg_emit recounts and writes each Seg at its offset.  Reads the keys twice instead of
+// writing and re-reading an n-wide flag and position array.
+#define SEG_ITEMS 16
+#define SEG_TILE (256 * SEG_ITEMS)
+__device__ __forceinline__ uint32_t seg_flags16(const uint32_t* __restrict__ keys, uint64_t n, uint64_t i0,
+                                                uint32_t* kout) {
+    uint32_t f = 0;
+    if (i0 >= n) return 0;
+    uint32_t prev = i0 == 0 ? 0xFFFFFFFFu : keys[i0 - 1];
+    if (i0 + SEG_ITEMS <= n) {
+        const uint4* v = reinterpret_cast<const uint4*>(keys + i0);
+#pragma unroll
+        for (int q = 0; q < SEG_ITEMS / 4; ++q) {
+            const uint4 w = v[q];
+            kout[4 * q] = w.x; kout[4 * q + 1] = w.y; kout[4 * q + 2] = w.z; kout[4 * q + 3] = w.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < SEG_ITEMS; ++j) kout[j] = (i0 + j < n) ? keys[i0 + j] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        const bool valid = i0 + j < n;
+        const bool st = valid && (i0 + j == 0 || kout[j] != prev);
+        f |= (st ? 1u : 0u) << j;
+        prev = kout[j];
+    }
+    return f;
+}
+__device__ __forceinline__ uint32_t seg_block_excl_scan(uint32_t v, uint32_t* total) {
+    __shared__ uint32_t ws[4];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (l >= o) x += y;
+    }
+    if (l == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { if (k < w) pre += ws[k]; tot += ws[k]; }
+    *total = tot;
+    return pre + x - v;
+}
+__global__ __launch_bounds__(256) void k_seg_count(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ cnt) {
+    uint32_t kk[SEG_ITEMS];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SEG_TILE + (uint64_t)threadIdx.x * SEG_ITEMS;
+    const uint32_t f = seg_flags16(keys, n, i0, kk);
+    uint32_t tot;
+    (void)seg_block_excl_scan((uint32_t)__popc(f), &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ keys, uint64_t n,
+                                                  const uint32_t* __restrict__ off, Seg* __restrict__ segs) {
+    uint32_t kk[SEG_ITEMS];
+    const uint64_t i0 = (uint64_t)blockIdx.x * SEG_TILE + (uint64_t)threadIdx.x * SEG_ITEMS;
+    uint32_t f = seg_flags16(keys, n, i0, kk);
+    uint32_t tot;
+    uint32_t pos = off[blockIdx.x] + seg_block_excl_scan((uint32_t)__popc(f), &tot);
+#pragma unroll
+    for (int j = 0; j < SEG_ITEMS; ++j) {
+        if ((f >> j) & 1u) {
+            Seg sg;
+            sg.res = kk[j];
+            sg.start = (uint32_t)(i0 + j);
+            sg.len = 0;
+            sg.bin = 0;
+            segs[pos++] = sg;
+        }
+    }
+}
 // lengths + bins.  Bins (dev_types.h BIN_*): cooperative kernels for long segments of resources
 // inside their limits, one lane per segment for everything else.  Per-block bin counts go to
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
@@ -1886,6 +1962,15 @@ namespace sg {
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg) {
+    static const bool fused = [] { const char* v = std::getenv("SG_SEG_FUSED"); return !(v && v[0] == '0'); }();
+    if (fused) {  // flag/pos are scratch of >= n words: tile counts in flag, their offsets in pos
+        const uint32_t nt = (uint32_t)((n + SEG_TILE - 1) / SEG_TILE);
+        hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag);
+        hipError_t e = scan(flag, pos, nt, part, nseg, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs);
+        return hipGetLastError();
+    }
     uint32_t nb = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_seg_flags, dim3(nb), dim3(256), 0, st, keys, n, flag);
     hipError_t e = scan(flag, pos, n, part, nseg, st);
