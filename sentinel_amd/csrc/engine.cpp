@@ -912,6 +912,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     int prio_lo = 0, prio_hi = 0;
     const char* sp = std::getenv("SG_STREAM_PRIO");
     if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (sp && sp[0] == '2') std::swap(prio_lo, prio_hi);  // SG_STREAM_PRIO=2: the group stage first
     if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
     // SG_GROUP_CU_QUARTERS=q (1..3): the group stream runs on q of every 4 CUs (an even spread over
     // the XCDs), leaving the rest to the latency-bound decide kernels it overlaps (experiment knob).
