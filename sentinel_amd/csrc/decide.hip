@@ -267,18 +267,18 @@ __global__ __launch_bounds__(256) void k_scatter_rec(const SEv* __restrict__ rec
     }
     if (r.kind == SG_EV_ENTRY) {
         if (r.cnt == 0) atomicOr(bflags, BF_ZERO_CNT);
-    } else if (r.code == RC_BATCH) {
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(
-            r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
-        const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | p);
-        if ((uint32_t)(old >> 32) == epoch) atomicOr(bflags, BF_MULTI_LINK);
     } else if (r.code == RC_NONE || r.code == RC_PREV) {
         atomicOr(&bst[p >> 10], BST_STATIC);
     }
-    recs[p] = r;
+    recs[p] = r;  // same-batch forward links are set by k_block_sums, in sorted order (local atomics)
 }
-// ENTRY count sum of every 1024 sorted positions (one workgroup each, 4 positions per lane)
-__global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, uint64_t n, uint32_t* __restrict__ bst) {
+// ENTRY count sum of every 1024 sorted positions (one workgroup each, 4 positions per lane), and the
+// forward link of every same-batch referenced ENTRY: walked in sorted order, an EXIT/TRACE and its
+// ENTRY sit in the same segment a few positions apart, so the link atomics stay in cache (an atomic
+// exchange detects a second EXIT/TRACE naming the same ENTRY).
+__global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, uint64_t n, uint32_t* __restrict__ bst,
+                                                    Link* __restrict__ link, uint32_t epoch,
+                                                    uint32_t* __restrict__ bflags) {
     __shared__ uint32_t wsum[4];
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
     uint32_t v = 0;
@@ -290,6 +290,12 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
             SEv r;
             __builtin_memcpy(&r, &w, sizeof(r));
             if (r.kind == SG_EV_ENTRY) v += r.cnt;
+            else if (r.code == RC_BATCH) {
+                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
+                    r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
+                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
+                if ((uint32_t)(old >> 32) == epoch) atomicOr(bflags, BF_MULTI_LINK);
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
@@ -2006,7 +2012,8 @@ hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, con
     if (scatter) {
         hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
                            epoch, bflags);
-        hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst);
+        hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst, link, epoch,
+                           bflags);
     } else {
         hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev, link, bst,
                            epoch, bflags);
