@@ -322,13 +322,28 @@ __global__ void k_resolve(const uint32_t* __restrict__ prev, uint32_t np, const 
 
 // decisions back to submission order; the status ring keeps every event's status for
 // references from later batches (0xFF = not an ENTRY)
-__global__ void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ dec, uint64_t n,
-                       uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask, uint32_t* __restrict__ out) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t d = dec[pos_of[i] & 0x7FFFFFFFu];
-    out[i] = d;
-    ring[(gbase + i) & ring_mask] = (uint8_t)(d & 0xFF);
+// (POST_ITEMS items per lane, all random loads issued before any use: more of them in flight)
+#define POST_ITEMS 4
+__global__ __launch_bounds__(256) void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ dec,
+                                              uint64_t n, uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask,
+                                              uint32_t* __restrict__ out) {
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * POST_ITEMS) + threadIdx.x;
+    uint32_t po[POST_ITEMS], d[POST_ITEMS];
+#pragma unroll
+    for (int k = 0; k < POST_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256;
+        po[k] = i < n ? pos_of[i] & 0x7FFFFFFFu : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < POST_ITEMS; ++k) d[k] = (base + (uint64_t)k * 256 < n) ? dec[po[k]] : 0u;
+#pragma unroll
+    for (int k = 0; k < POST_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256;
+        if (i < n) {
+            out[i] = d[k];
+            ring[(gbase + i) & ring_mask] = (uint8_t)(d[k] & 0xFF);
+        }
+    }
 }
 
 // Verdicts of the frozen spans recorded by k_jac<..., SKIP> (the map half of a frozen stretch, spread
@@ -2032,7 +2047,7 @@ hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring
 }
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st) {
-    uint32_t nb = (uint32_t)((n + 255) / 256);
+    uint32_t nb = (uint32_t)((n + 256 * POST_ITEMS - 1) / (256 * POST_ITEMS));
     hipLaunchKernelGGL(k_post, dim3(nb), dim3(256), 0, st, pos_of, dec, n, gbase, ring, ring_mask, out);
     return hipGetLastError();
 }
