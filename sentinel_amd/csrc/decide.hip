@@ -290,11 +290,9 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
             SEv r;
             __builtin_memcpy(&r, &w, sizeof(r));
             if (r.kind == SG_EV_ENTRY) v += r.cnt;
-            else if (r.code == RC_BATCH) {
-                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
-                    r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
-                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
-                if ((uint32_t)(old >> 32) == epoch) atomicOr(bflags, BF_MULTI_LINK);
+            else if (r.code == RC_BATCH) {  // plain store; k_link_verify detects a second EXIT/TRACE
+                uint64_t* dst = r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l;
+                *dst = ((uint64_t)epoch << 32) | (uint32_t)p;
             }
         }
     }
@@ -305,6 +303,28 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
         const uint32_t sum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         if (sum) atomicAdd(&bst[blockIdx.x], sum);
     }
+}
+// Every same-batch EXIT/TRACE must find its own position in its ENTRY's link after k_block_sums'
+// plain stores: a mismatch means a second EXIT (or TRACE) named the same ENTRY.
+__global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ recs, uint64_t n,
+                                                     const Link* __restrict__ link, uint32_t epoch,
+                                                     uint32_t* __restrict__ bflags) {
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    bool multi = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
+        if (p < n) {
+            const uint4 w = reinterpret_cast<const uint4*>(recs)[p];
+            SEv r;
+            __builtin_memcpy(&r, &w, sizeof(r));
+            if (r.kind != SG_EV_ENTRY && r.code == RC_BATCH) {
+                const uint64_t v = r.kind == SG_EV_EXIT ? link[r.x].exit_l : link[r.x].trace_l;
+                if (v != (((uint64_t)epoch << 32) | (uint32_t)p)) multi = true;
+            }
+        }
+    }
+    if (__ballot(multi) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_MULTI_LINK);
 }
 // references into earlier batches, once those are decided: the ENTRY's status from the ring
 // (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
@@ -2028,6 +2048,8 @@ hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, con
         hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
                            epoch, bflags);
         hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst, link, epoch,
+                           bflags);
+        hipLaunchKernelGGL(k_link_verify, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, link, epoch,
                            bflags);
     } else {
         hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev, link, bst,

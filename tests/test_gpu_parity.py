@@ -367,3 +367,26 @@ def test_frozen_skip_hot_resources(config, skip_min, monkeypatch):
         monkeypatch.setenv(k, v)
     w, eng, orc, d = _run(config, batches=3, n_entries=300_000, n_res=12)
     assert eng.spans_total() > 0  # the skip path ran
+
+
+def test_duplicate_exits_disable_skipping(monkeypatch):
+    # Two EXITs naming the same ENTRY in one batch: the forward-link check (k_link_verify) must flag
+    # the batch so the cooperative kernels decide it without frozen-stretch skipping; decisions and
+    # node state still equal the oracle's.  A control batch without duplicates does skip.
+    for k, v in {"SG_LANE_MAX": "0", "SG_J1_MAX": "40", "SG_J4_MAX": "2000", "SG_SKIP_MIN": "16"}.items():
+        monkeypatch.setenv(k, v)
+    w = T.Workload(4, n_entries=200_000, n_res=12)
+    ev = w.events
+    exits = np.nonzero((ev["kind"] == A.EV_EXIT) & ((ev["aux"] & np.uint64(0xFFFFFFFFFFFF)) != np.uint64(0xFFFFFFFFFFFF)))[0]
+    rng = np.random.default_rng(11)
+    dup = ev[np.sort(rng.choice(exits, 500, replace=False))].copy()
+    dup["ts"] = ev["ts"][-1]
+    for events, expect_skip in ((ev, True), (np.concatenate([ev, dup]), False)):
+        eng = _engine(max_resources=64, max_slot_chain_size=0, param_table_log2=21)
+        orc = O.Oracle(max_slot_chain_size=0)
+        w.install(eng)
+        w.install(orc)
+        dg, do = eng.submit(events), orc.submit(events)
+        _assert_same_decisions(dg, do, events)
+        _compare_nodes(w, eng, orc, range(w.n_res))
+        assert (eng.spans_total() > 0) == expect_skip
