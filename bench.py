@@ -1,22 +1,34 @@
 #!/usr/bin/env python3
 """Bench: decided entries/sec (whole node) at 1M resources; % of HBM roofline.
 
-Workload = SURVEY.md §8(d) config C4 (the metric's "1M resources" config): 1M
-resources, each with a QPS DefaultController flow rule and one DegradeRule
-(1/3 RT 50 ms, 1/3 exception ratio 0.2, 1/3 exception count 20; timeWindow 10 s),
-Zipf(1.1) popularity, 10^6 entries per trace-second, every entry followed by an
-EXIT at t+RT (RT ~ Exp(20 ms), clipped at 4900) and a TRACE with p = 0.05, chain
-cap lifted (max_slot_chain_size = 0).  A "step" is one sg_submit of one batch of
---batch-events events already resident in HBM.  Synthetic data (no network).
+Workload = SURVEY.md §8(d) config C4 (the metric's "1M resources" config): 1M resources, each with
+a QPS DefaultController flow rule and one DegradeRule (1/3 RT 50 ms, 1/3 exception ratio 0.2, 1/3
+exception count 20; timeWindow 10 s), Zipf(1.1) popularity, 10^6 entries per trace-second, every
+entry followed by an EXIT at t+RT (RT ~ Exp(20 ms), clipped at 4900) and a TRACE with p = 0.05,
+chain cap lifted (max_slot_chain_size = 0).  Synthetic data (no network).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-resources are hash-sharded -- each rank owns an independent 1M-resource shard
-with its own seeded trace, decides with no data-path collective, and the step
-time is the max over ranks (weak scaling).
+Batches: the trace is cut into global batches of --batch-events events (2^25).  --base-batches of
+them are generated on the host; later batches are time-shifted copies built on the device before
+the timed region (timestamps + k x the trace span, EXIT/TRACE references + k x the events of the
+trace), so every batch is fresh to the engine -- time only moves forward, windows roll, breakers
+trip and reset -- and nothing is replayed.  A step is --sub-batches consecutive global batches
+submitted back to back through the engine's two-stage pipeline (sg_submit_async: the group stage of
+batch k+1 overlaps the decide stage of batch k); the default sizes it so the timed region is long
+(~1 s) while the inputs of all timed steps fit in HBM, and is printed in config.  Inputs are
+resident in HBM when the timed region starts.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): ONE C4 trace,
+resources sharded by splitmix64(res_id) % N (strong scaling).  Every rank generates the same trace
+and keeps its shard (EXIT/TRACE references rewritten to its own numbering); global batch k of the
+trace is rank r's k-th batch (its share of it), so all ranks advance through trace time together.
+The decision path has no collective; the per-second MetricNode all-gather (RCCL) runs inside the
+timed region once per wall-clock second.  The step time is the max over ranks and value = every
+rank's entries / that time.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -28,10 +40,12 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Algorithmic bytes: every event record is read once (24 B), every
-# decision word written once (4 B), and every resource touched by a batch reads its
-# state once (S_r = 352 B) and writes it once (S_w = 256 B).
+# Algorithmic bytes: every event record is read once (24 B), every ENTRY's decision
+# word written once (4 B), and every resource touched by a batch reads its state once (S_r = 352 B)
+# and writes it once (S_w = 256 B).
 EVENT_B, DECISION_B, STATE_RW_B = 24, 4, 352 + 256
+REF_MASK = 0xFFFFFFFFFFFF
+EPE = 2.05  # C4 events per entry (entry + exit + 5 % traces)
 
 
 def parse():
@@ -39,12 +53,56 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch-events", type=int, default=1 << 25)
+    p.add_argument("--batch-events", type=int, default=1 << 25, help="events per global batch")
+    p.add_argument("--base-batches", type=int, default=8, help="global batches generated on the host")
+    p.add_argument("--sub-batches", type=int, default=0, help="global batches per step (0: auto)")
+    p.add_argument("--max-sub-batches", type=int, default=12)
+    p.add_argument("--hbm-budget", type=float, default=0.6, help="fraction of free HBM for step inputs")
     p.add_argument("--resources", type=int, default=1_000_000)
-    p.add_argument("--cpu-sample-events", type=int, default=4_000_000)
+    p.add_argument("--cpu-threads", type=int, default=0, help="partitioned oracle threads (0: min(16, cores))")
+    p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
+    p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-out", default="")
     return p.parse_args()
+
+
+def src_sha() -> str:
+    """Content hash of the product sources (the GPU box has no .git): profiles/ files carry it, and
+    bench.py only reports PMC traffic measured on these exact sources."""
+    h = hashlib.sha256()
+    for d, exts in (("sentinel_amd/csrc", (".hip", ".cpp", ".h")), ("include", (".h",))):
+        for f in sorted(os.listdir(os.path.join(ROOT, d))):
+            if f.endswith(exts):
+                h.update(f.encode())
+                with open(os.path.join(ROOT, d, f), "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def make_trace(n_res: int, batch_events: int, base_batches: int, seed: int):
+    """The C4 trace, cut to base_batches whole global batches (the Workload owns the memory)."""
+    from sentinel_amd import tracegen as T
+    need = batch_events * base_batches
+    n_entries = int(need / EPE * 1.01) + 1000
+    while True:
+        w = T.Workload(4, seed=seed, n_res=n_res, n_entries=n_entries)
+        if len(w.events) >= need:
+            return w, w.events[:need]
+        n_entries = int(n_entries * 1.05)
+        w.close()
+
+
+def shifted_batch(base64, a: int, e: int, copy: int, tspan: int, n_base: int, out64):
+    """Global-batch copy `copy` of base rows [a, e) into out64 (torch int64 [n, 3] views of sg_event
+    records: ts | res_id,count,kind,flags | aux): ts + copy*tspan, references + copy*n_base."""
+    import torch
+    src = base64[a:e]
+    out64.copy_(src)
+    if copy:
+        out64[:, 0] += copy * tspan
+        kind = (src[:, 1] >> 48) & 0xFF
+        isref = (kind != 0) & ((src[:, 2] & REF_MASK) != REF_MASK)
+        out64[:, 2] += torch.where(isref, copy * n_base, 0)
 
 
 def main():
@@ -52,128 +110,194 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
 
+    from sentinel_amd import dist as D
     from sentinel_amd import engine as E
     from sentinel_amd import tracegen as T
 
-    steps, warmup = args.steps, args.warmup
-    nb = steps + warmup
-    # ---- synthetic trace: enough entries for warmup + timed batches
-    per_entry_events = 2.05
-    n_entries = int(args.batch_events * nb / per_entry_events) + 1
-    t0 = time.time()
-    w = T.Workload(4, seed=T.SEED_BASE + 4 + 1000 * rank, n_res=args.resources, n_entries=n_entries)
-    gen_s = time.time() - t0
-    ev = w.events
-    n_batches = min(nb, len(ev) // args.batch_events)
-    if n_batches < nb:
-        steps = max(1, n_batches - warmup)
-    eng = E.Engine(device=local if world > 1 else 0, max_resources=1 << 20, max_slot_chain_size=0,
-                   param_table_log2=16, status_ring_log2=28, max_batch_events=args.batch_events)
+    steps, warmup, gb, B = args.steps, args.warmup, args.batch_events, args.base_batches
+    # ---- one trace for the whole node; this rank's shard of it
+    t_gen = time.time()
+    w, ev = make_trace(args.resources, gb, B, T.SEED_BASE + 4)
+    gen_s = time.time() - t_gen
+    tspan = int(ev["ts"][-1] - ev["ts"][0]) + 1000  # copy k starts a second after copy k-1 ends
+    if world > 1:
+        mine, pos = D.shard_stream(ev, world, rank)
+        cuts = np.searchsorted(pos, np.arange(B + 1, dtype=np.int64) * gb)
+    else:
+        mine, cuts = ev, np.arange(B + 1, dtype=np.int64) * gb
+    n_base = len(mine)
+    sizes = np.diff(cuts)
+    ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(B)])
+    res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(B)])
+
+    eng = E.Engine(device=local, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
+                   status_ring_log2=28, max_batch_events=int(sizes.max()))
     w.install(eng)
 
-    # ---- events resident in HBM before the timed region
-    import ctypes as C
-    hip = C.CDLL("libamdhip64.so")
-    dptr = C.c_void_p()
-    total = n_batches * args.batch_events
-    assert hip.hipSetDevice(local if world > 1 else 0) == 0
-    assert hip.hipMalloc(C.byref(dptr), C.c_size_t(total * 24)) == 0
-    assert hip.hipMemcpy(dptr, C.c_void_p(ev.ctypes.data), C.c_size_t(total * 24), 1) == 0
-    optr = C.c_void_p()
-    assert hip.hipMalloc(C.byref(optr), C.c_size_t(args.batch_events * 4)) == 0
-    kinds = ev["kind"][:total].reshape(n_batches, args.batch_events)
-    entries_per_batch = (kinds == 0).sum(axis=1)
-    res_per_batch = [len(np.unique(ev["res_id"][i * args.batch_events:(i + 1) * args.batch_events]))
-                     for i in range(n_batches)]
+    # ---- the shard's base batches into HBM (pinned host -> device; the PCIe rate is reported, never value)
+    host = torch.from_numpy(np.ascontiguousarray(mine).view(np.uint8)).pin_memory()
+    base = torch.empty(host.numel(), dtype=torch.uint8, device=dev)
+    h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h0.record()
+    base.copy_(host, non_blocking=True)
+    h1.record()
+    torch.cuda.synchronize()
+    h2d_ms = h0.elapsed_time(h1)
+    del host
+    base64 = base.view(torch.int64).view(-1, 3)
+
+    # ---- sub-batches per step: the inputs of all timed steps in HBM at once (they are rebuilt between
+    # the warmup and the timed region), after the engine's two batch slots (~120 B per event each)
+    free = torch.cuda.mem_get_info(dev)[0]
+    mean_b = float(sizes.mean()) * 24
+    snap_cap = min(60 * args.resources // world + 4096, 1 << 26)
+    reserve = 2 * 120 * int(sizes.max()) + snap_cap * 64
+    S = args.sub_batches or int(max(1, min(args.max_sub_batches,
+                                         args.hbm_budget * (free - reserve) // (max(steps, warmup) * mean_b * 1.15))))
+    if dist is not None:
+        t = torch.tensor([S], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        S = int(t.item())
+    nbat = max(steps, warmup) * S
+    gidx = lambda i: (i % B, i // B)  # global batch i -> (base batch, copy)
+    max_ev = max(int(sum(sizes[gidx(i)[0]] for i in range(g0, g0 + n))) for g0, n in ((0, warmup * S), (warmup * S, steps * S)))
+    buf = torch.empty((max_ev, 3), dtype=torch.int64, device=dev)
+    out = torch.empty(int(sizes.max()), dtype=torch.int32, device=dev)
+    snap = torch.empty(snap_cap * 64, dtype=torch.uint8, device=dev) if dist is not None else None
+
+    def build(g0, n):
+        """Global batches g0..g0+n-1 of this rank into buf: [(row offset, rows, entries, touched)]."""
+        plan, off = [], 0
+        for g in range(g0, g0 + n):
+            b, k = gidx(g)
+            m = int(sizes[b])
+            shifted_batch(base64, int(cuts[b]), int(cuts[b + 1]), k, tspan, n_base, buf[off:off + m])
+            plan.append((off, m, int(ent_b[b]), int(res_b[b]), int(ev["ts"][min(len(ev) - 1, (b + 1) * gb - 1)]) + k * tspan))
+            off += m
+        torch.cuda.synchronize()
+        return plan
 
     def barrier():
+        torch.cuda.synchronize()
         if dist is not None:
-            import torch
-            torch.cuda.synchronize()
             dist.barrier()
 
-    # Batches go through the engine's two-stage pipeline (sg_submit_async): the group stage of batch
-    # k+1 runs while batch k is being decided; sg_sync at the end of the timed region waits for the
-    # last decision.  Per-batch stage times come from HIP events on the engine's streams.
-    for i in range(warmup):
-        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value, sync=False)
+    def gather_metrics(now):
+        """MetricTimerListener across the node: every rank's MetricNode rows, device to device."""
+        n = eng.snapshot_to(now, snap.data_ptr(), snap_cap)
+        n = min(n, snap_cap)
+        cnt = torch.tensor([n], device=dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        width = int(max(c.item() for c in cnts)) * 64
+        if width:
+            outs = [torch.empty(width, dtype=torch.uint8, device=dev) for _ in range(world)]
+            dist.all_gather(outs, snap[:width])
+        return sum(int(c.item()) for c in cnts)
+
+    base_ptr = buf.data_ptr()
+    # ---- warmup (untimed): the first W steps of the stream
+    plan = build(0, warmup * S)
+    for off, m, _, _, _ in plan:
+        eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
     eng.sync()
     eng.timing_log()
+    if dist is not None:  # the first fetch (lastFetchTime = -1) outside the timed region
+        gather_metrics(plan[-1][4])
+    # ---- timed: the next K steps (fresh, time-shifted batches)
+    plan = build(warmup * S, steps * S)
+    n_gather, rows_gathered = 0, 0
     barrier()
     t_start = time.perf_counter()
-    for i in range(warmup, warmup + steps):
-        eng.submit_ptr(dptr.value + i * args.batch_events * 24, args.batch_events, optr.value, sync=False)
+    t_last = t_start
+    for s in range(steps):
+        for off, m, _, _, _ in plan[s * S:(s + 1) * S]:
+            eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
+        if dist is not None and (s == steps // 2 or time.perf_counter() - t_last >= 1.0):
+            rows_gathered += gather_metrics(plan[(s + 1) * S - 1][4])  # drains this rank's pipeline
+            n_gather += 1
+            t_last = time.perf_counter()
     eng.sync()
     barrier()
     elapsed = time.perf_counter() - t_start
-    stage_ms = eng.timing_log()  # per timed step: [group, decide, post, total] device ms
+    stage_ms = np.array(eng.timing_log())  # per timed batch: [group, decide, post, total] device ms
+    entries = float(sum(p[2] for p in plan))
+    touched = float(sum(p[3] for p in plan))
+    events = float(sum(p[1] for p in plan))
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], device="cuda")
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        e = torch.tensor([float(sum(entries_per_batch[warmup:warmup + steps]))], device="cuda", dtype=torch.float64)
-        dist.all_reduce(e)
-        entries_total = float(e.item())
-    else:
-        entries_total = float(sum(entries_per_batch[warmup:warmup + steps]))
+        t = torch.tensor([entries, touched, events], device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        entries, touched, events = (float(x) for x in t.tolist())
 
-    # Roofline of the dominant stage: the decide kernels (k_jac<16>/<4>/<1> and k_lane, forked over
-    # four streams and joined; HIP events bracket the fork and the join on the engine stream).
-    # Algorithmic bytes per launch: every event record read once (24 B), every
-    # decision word written once (4 B), every resource touched by the batch reads (352 B) and writes
-    # (256 B) its state once.  Sorting/grouping/re-reads are implementation cost, not counted.
-    sel = range(warmup, warmup + steps)
-    alg_bytes = np.mean([args.batch_events * (EVENT_B + DECISION_B) + res_per_batch[i] * STATE_RW_B for i in sel])
-    sm = np.array(stage_ms)
-    decide_ms = float(sm[:, 1].mean())
-    achieved = alg_bytes / (decide_ms / 1e3) / 1e9
-    pipe_ms = elapsed / steps * 1e3
-    pipe_achieved = alg_bytes / (pipe_ms / 1e3) / 1e9
-    traffic, traffic_src = None, None
+    nb = steps * S  # global batches timed
+    batch_ms = elapsed / nb * 1e3
+    # algorithmic bytes per global batch (all ranks), SURVEY.md §8(d)
+    alg = (events * EVENT_B + entries * DECISION_B + touched * STATE_RW_B) / nb
+    achieved = alg / (batch_ms / 1e3) / 1e9
+    decide_ms = float(stage_ms[:, 1].mean())
+    dec_alg = alg / world  # this rank's share, over its own decide-stage time
+    traffic, tnote = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command (tools/profile.sh)
+    sha = src_sha()
+    if os.path.exists(pmc):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh) on these sources
         with open(pmc) as f:
             pj = json.load(f)
-        traffic, traffic_src = pj.get("decide_stage_traffic_bytes"), "profiles/pmc_latest.json"
+        if pj.get("src_sha") == sha and pj.get("batch_events") == gb and world == 1:
+            traffic = pj.get("traffic_bytes_per_batch")
+            tnote = "profiles/pmc_latest.json (src_sha %s, git %s)" % (sha, pj.get("git_head"))
+        else:
+            tnote = "profiles/pmc_latest.json is for other sources/config (src_sha %s != %s): not used" % (
+                pj.get("src_sha"), sha)
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(w, args.cpu_sample_events)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, ev, args)
 
     if rank == 0:
         line = {
             "metric": "decided entries/sec (whole node) at 1M resources; % of HBM roofline",
-            "value": entries_total / elapsed,
+            "value": entries / elapsed,
             "unit": "entries/s",
             "n_gpus": world,
             "steps": steps,
             "warmup": warmup,
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "int64/f64",
-            "data": "synthetic (seeded C4 trace: Zipf(1.1), RT~Exp(20ms), 5% traces)",
+            "data": "synthetic (seeded C4 trace: Zipf(1.1), RT~Exp(20ms), 5% traces; time-shifted fresh batches)",
             "config": {"workload": "C4: 1M resources, QPS DefaultController + DegradeRule (RT/ratio/count)",
-                       "resources_per_gpu": args.resources, "batch_events": args.batch_events,
-                       "entries_per_step": float(np.mean(entries_per_batch[warmup:warmup + steps])),
-                       "resources_touched_per_step": float(np.mean([res_per_batch[i] for i in sel])),
-                       "parallelism": "resource-sharded x%d" % world},
+                       "resources": args.resources, "batch_events": gb, "sub_batches_per_step": S,
+                       "events_per_step": events / steps, "entries_per_step": entries / steps,
+                       "resources_touched_per_batch": touched / nb, "base_batches": B,
+                       "parallelism": "resource-sharded x%d (splitmix64(res_id) %% %d)" % (world, world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "decide stage: k_jac<16,..> | k_jac<4,..> then k_jac<1,..> | k_lite + k_lane (concurrent streams), then k_fill",
-                         "kernel_ms": decide_ms, "alg_bytes_per_launch": float(alg_bytes)},
-            "pipeline": {"achieved_GBs": pipe_achieved, "frac": pipe_achieved / HBM_PEAK_GBS,
-                         "group_ms": float(sm[:, 0].mean()), "decide_ms": decide_ms, "post_ms": float(sm[:, 2].mean()),
-                         "device_ms": float(sm[:, 3].mean()), "wall_ms": pipe_ms},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
+                         "kernel": "one global batch through the whole pipeline (sort/group, decide, post)",
+                         "batch_ms": batch_ms, "alg_bytes_per_batch": alg,
+                         "decide_stage": {"ms": decide_ms, "achieved": dec_alg / (decide_ms / 1e3) / 1e9,
+                                          "frac": dec_alg / (decide_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                          "kernels": "k_jac<16>|k_jac<4>,k_jac<1>|k_lite,k_lane (streams), k_fill"}},
+            "pipeline": {"group_ms": float(stage_ms[:, 0].mean()), "decide_ms": decide_ms,
+                         "post_ms": float(stage_ms[:, 2].mean()), "device_ms": float(stage_ms[:, 3].mean()),
+                         "wall_ms_per_batch": batch_ms},
+            "h2d": {"GBps": n_base * 24 / (h2d_ms / 1e3) / 1e9, "pcie_inclusive_entries_per_s":
+                    entries / (elapsed + h2d_ms / 1e3 * events / max(1, n_base) / world),
+                    "note": "pinned host -> HBM copy of the events, measured on the base trace; not in value"},
+            "metric_gathers": {"count": n_gather, "rows": rows_gathered} if world > 1 else None,
             "cpu_baseline": cpu,
+            "src_sha": sha,
             "gen_s": gen_s,
         }
         print(json.dumps(line), flush=True)
@@ -181,19 +305,42 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(w, n_events):
-    """The oracle (C restatement of the Java path, 1 thread) on a bounded prefix of the same trace."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(w, ev, args):
+    """The oracle (C restatement of the Java path) on bounded prefixes of the same trace: T threads
+    partitioned by resource (SURVEY.md §8(d) CPU fallback), plus one thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
-    o = O.Oracle(max_slot_chain_size=0)
-    w.install(o)
-    ev = w.events[:n_events]
+    avail = len(os.sched_getaffinity(0))
+    T = args.cpu_threads or min(16, avail)
+    sample = ev[:args.cpu_sample_events]
+    po = O.PartitionedOracle(w, T, max_slot_chain_size=0)
+    spent = []
+    po.submit(sample, timed=spent)
+    po.close()
+    n_ent = int((sample["kind"] == 0).sum())
+    one = O.Oracle(max_slot_chain_size=0)
+    w.install(one)
+    s1 = ev[:args.cpu_single_events]
     t = time.perf_counter()
-    d = o.submit(ev)
-    dt = time.perf_counter() - t
-    n_ent = int((ev["kind"] == 0).sum())
-    return {"value": n_ent / dt, "unit": "entries/s", "cores": 1, "kind": "port",
-            "sample": "first %d events (%d entries) of the C4 trace, oracle/liboracle.so single thread" % (len(ev), n_ent)}
+    one.submit(s1)
+    dt1 = time.perf_counter() - t
+    n1 = int((s1["kind"] == 0).sum())
+    return {"value": n_ent / spent[0], "unit": "entries/s", "cores": T, "kind": "port",
+            "sample": "first %d events (%d entries) of the C4 trace, oracle/liboracle.so, %d threads partitioned "
+                      "by splitmix64(res_id) %% %d (routing excluded)" % (len(sample), n_ent, T, T),
+            "single_thread": {"value": n1 / dt1, "cores": 1, "sample": "first %d events (%d entries)" % (len(s1), n1)},
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": avail}
 
 
 if __name__ == "__main__":

@@ -247,6 +247,50 @@ class Oracle:
         return [(int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])) for o in out[:len(reqs)]]
 
 
+class PartitionedOracle:
+    """``threads`` oracles, resources partitioned by splitmix64(res_id) % threads (SURVEY.md §8(d):
+    "N threads partitioned by resource"), each deciding its shard of every batch in its own thread
+    (ctypes releases the GIL for the call).  Every decision reads and writes only its own resource's
+    state, so the merged decisions equal one oracle's -- tests/test_dist.py checks the routing.
+    Used as bench.py's multi-core CPU baseline and to replay large traces in the parity tests."""
+
+    def __init__(self, workload, threads: int, **cfg):
+        from concurrent.futures import ThreadPoolExecutor
+        from sentinel_amd import dist as D
+        self.T = threads
+        self.D = D
+        self.pool = ThreadPoolExecutor(threads)
+        self.router = D.EventRouter(threads, ring_log2=20)
+        self.orcs = [Oracle(**cfg) for _ in range(threads)]
+        owner = D.shard_of(np.arange(workload.n_res), threads)
+        subsets = [np.nonzero(owner == r)[0] for r in range(threads)]
+        list(self.pool.map(lambda r: workload.install(self.orcs[r], subsets[r]), range(threads)))
+        self.n_events = 0
+
+    def submit(self, events: np.ndarray, timed: list = None) -> np.ndarray:
+        """Decisions of one batch; with ``timed``, appends the seconds the threads spent deciding
+        (routing excluded)."""
+        import time
+        parts, pos = self.router.route(np.ascontiguousarray(events, dtype=A.EVENT_DTYPE))
+        t = time.perf_counter()
+        outs = list(self.pool.map(lambda r: self.orcs[r].submit(parts[r]), range(self.T)))
+        if timed is not None:
+            timed.append(time.perf_counter() - t)
+        out = np.zeros(len(events), dtype=np.uint32)
+        for p, o in zip(pos, outs):
+            out[p] = o
+        self.n_events += len(events)
+        return out
+
+    def read_node(self, res: int) -> dict:
+        return self.orcs[int(self.D.shard_of(res, self.T))].read_node(res)
+
+    def close(self):
+        for o in self.orcs:
+            o.close()
+        self.pool.shutdown()
+
+
 class Controller:
     """A TrafficShapingController driven with mocked Node values."""
 

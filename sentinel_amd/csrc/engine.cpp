@@ -614,6 +614,13 @@ static int collect(sg_engine* e, int k) {
     HIPCHK(hipMemcpyAsync(&nspan, B.d_bsmall + 120, 4, hipMemcpyDeviceToHost, e->gstream));
     HIPCHK(hipStreamSynchronize(e->gstream));
     e->spans_total += nspan;
+    // Flags the decide kernels raise (the group stage's own checks return before the decide stage runs):
+    // an EXIT/TRACE whose reference names an event that is not an earlier ENTRY of its resource, and a
+    // batch starting before the last window a resource already holds (the clock went back).
+    if (bflags & BF_BAD_REF)
+        return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
+    if (bflags & BF_BACKWARD)
+        return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
     return SG_OK;
 }
@@ -1723,19 +1730,24 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
         HIPCHK(hipMalloc(&e->d_snap_cnt, (uint64_t)e->cfg.max_resources * 4));
         HIPCHK(hipMalloc(&e->d_snap_off, (uint64_t)e->cfg.max_resources * 4));
     }
-    if (cap > e->snap_cap) {
+    // out may be device memory (e.g. the buffer an RCCL all-gather sends from): the kernels write it
+    // directly, no staging buffer and no host round trip
+    const bool dev_out = out && is_device_ptr(out);
+    if (!dev_out && cap > e->snap_cap) {
         dfree(e->d_snap_out);
         HIPCHK(hipMalloc(&e->d_snap_out, std::max<uint64_t>(cap, 1) * sizeof(sg_metric_node)));
         e->snap_cap = cap;
     }
     if (!e->d_part) { int rc = ensure_batch(e, 1); if (rc) return rc; }
     HIPCHK(launch_snapshot(e->d_minb, e->d_info, R, now_ms, e->cfg.statistic_max_rt, e->d_snap_cnt, e->d_snap_off,
-                           e->d_part, e->d_small + 3, e->d_snap_out, cap, e->stream));
+                           e->d_part, e->d_small + 3, dev_out ? out : e->d_snap_out, dev_out || out ? cap : 0,
+                           e->stream));
     uint32_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, e->d_small + 3, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     uint64_t k = std::min<uint64_t>(total, cap);
-    if (k && out) HIPCHK(hipMemcpy(out, e->d_snap_out, k * sizeof(sg_metric_node), hipMemcpyDeviceToHost));
+    if (k && out && !dev_out)
+        HIPCHK(hipMemcpy(out, e->d_snap_out, k * sizeof(sg_metric_node), hipMemcpyDeviceToHost));
     *n = total;
     return SG_OK;
 }

@@ -101,7 +101,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             const uint64_t ref = e.aux & SG_REF_NONE;
             if (ref != SG_REF_NONE) {
                 if (ref >= gbase) {
-                    if (ref - gbase >= i) fl |= BF_BAD_REF;  // an EXIT/TRACE must follow its ENTRY
+                    // an EXIT/TRACE must follow its ENTRY and name an event of its own resource (the
+                    // referenced record is a few RT milliseconds back: an L2 hit)
+                    if (ref - gbase >= i || ev[ref - gbase].res_id != e.res_id) fl |= BF_BAD_REF;
                     else { r.code = RC_BATCH; r.x = (uint32_t)(ref - gbase); }
                 } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve,
                           // after the earlier batches are decided (this stage overlaps the previous decide)

@@ -36,15 +36,96 @@ def shard_of(res_ids, world: int) -> np.ndarray:
     return (splitmix64(res_ids) % np.uint64(world)).astype(np.int64)
 
 
+_REF = np.uint64(A.REF_NONE)
+
+
+class EventRouter:
+    """Routes one submitting stream of sg_event batches to ``world`` engines, batch by batch.
+
+    Each rank's batch keeps the input order (a time-ordered stream stays time-ordered per shard).
+    An EXIT/TRACE names its ENTRY by the ENTRY's global index in the stream the engine receives
+    (include/sentinel_gpu.h, low 48 bits of ``aux``), so every reference is rewritten from the
+    submitting stream's numbering to the ENTRY's index in its rank's stream.  An ENTRY and its
+    EXIT/TRACE share the resource, hence the rank.  The index map is a ring of 2^ring_log2 events:
+    a reference older than that (or to a later event) cannot be mapped and is rewritten to point at
+    the referencing event itself, which the engine rejects as a bad reference (SG_EINVAL).
+    """
+
+    def __init__(self, world: int, ring_log2: int = 24):
+        self.world = world
+        self.mask = (1 << ring_log2) - 1
+        self.local = np.zeros(1 << ring_log2, dtype=np.int64)  # submitting index -> rank-local index
+        self.gin = 0                                  # submitting index of the next input event
+        self.gout = np.zeros(world, dtype=np.int64)   # rank-local index of each rank's next event
+
+    def _grow(self):
+        old, size = self.local, self.mask + 1
+        idx = np.arange(max(0, self.gin - size), self.gin, dtype=np.int64)  # the history the ring holds
+        self.mask = 2 * size - 1
+        self.local = np.zeros(2 * size, dtype=np.int64)
+        self.local[idx & self.mask] = old[idx & (size - 1)]
+
+    def route(self, events: np.ndarray):
+        """Returns (batches, positions): positions[r] are the indices of rank r's events in the
+        input batch (to put decisions back in submission order)."""
+        n = len(events)
+        while n > (self.mask + 1) // 2:  # keep room for the batch plus as much history again
+            self._grow()
+        owner = shard_of(events["res_id"], self.world)
+        order = np.argsort(owner, kind="stable")
+        cuts = np.searchsorted(owner[order], np.arange(self.world + 1))
+        pos = [order[cuts[r]:cuts[r + 1]] for r in range(self.world)]
+        gidx = self.gin + np.arange(n, dtype=np.int64)
+        loc = np.empty(n, dtype=np.int64)
+        for r, p in enumerate(pos):
+            loc[p] = self.gout[r] + np.arange(len(p), dtype=np.int64)
+            self.gout[r] += len(p)
+        self.local[gidx & self.mask] = loc
+        aux = events["aux"].astype(np.uint64)
+        isref = (events["kind"] != A.EV_ENTRY) & ((aux & _REF) != _REF)
+        ref = (aux & _REF).astype(np.int64)
+        ok = isref & (ref < gidx) & (ref >= self.gin + n - 1 - self.mask)  # ring slot not reused yet
+        bad = isref & ~ok
+        new = np.where(ok, self.local[ref & self.mask], loc)
+        aux2 = np.where(isref, (aux & ~_REF) | (new.astype(np.uint64) & _REF), aux)
+        if bad.any():  # self-reference: rejected by the engine (an EXIT/TRACE must follow its ENTRY)
+            aux2 = np.where(bad, (aux & ~_REF) | (loc.astype(np.uint64) & _REF), aux2)
+        self.gin += n
+        out = []
+        for p in pos:
+            b = events[p].copy()
+            b["aux"] = aux2[p]
+            out.append(b)
+        return out, pos
+
+
+def shard_stream(events: np.ndarray, world: int, rank: int):
+    """Rank ``rank``'s share of a whole sg_event stream that starts at global index 0 (what one
+    process of a multi-GPU run keeps of a trace every rank generates alike): its events in order,
+    with EXIT/TRACE references rewritten to the rank's numbering, and their positions in the
+    input.  O(n + m log m) for m events of the rank, no sort of the whole stream."""
+    pos = np.nonzero(shard_of(events["res_id"], world) == rank)[0]
+    mine = events[pos].copy()
+    aux = mine["aux"].astype(np.uint64)
+    isref = (mine["kind"] != A.EV_ENTRY) & ((aux & _REF) != _REF)
+    ref = (aux & _REF).astype(np.int64)
+    k = np.searchsorted(pos, ref)
+    kk = np.minimum(k, len(pos) - 1) if len(pos) else k
+    ok = isref & (k < len(pos)) & (pos[kk] == ref) & (ref < pos) if len(pos) else isref
+    own = np.arange(len(pos), dtype=np.int64)
+    new = np.where(ok, k, own)  # an unmappable reference names the event itself: rejected as bad
+    mine["aux"] = np.where(isref, (aux & ~_REF) | (new.astype(np.uint64) & _REF), aux)
+    return mine, pos
+
+
 def route_events(events: np.ndarray, world: int):
-    """Split a time-ordered sg_event batch into the per-rank batches (stable: each rank's events
-    keep their order, so each shard sees a time-ordered batch).  Returns (batches, positions) where
-    positions[r] are the indices of rank r's events in the input (to put decisions back)."""
-    owner = shard_of(events["res_id"], world)
-    order = np.argsort(owner, kind="stable")
-    cuts = np.searchsorted(owner[order], np.arange(world + 1))
-    pos = [order[cuts[r]:cuts[r + 1]] for r in range(world)]
-    return [events[p] for p in pos], pos
+    """Split a time-ordered sg_event stream that starts at global index 0 into the per-rank
+    streams, with EXIT/TRACE references rewritten to each rank's numbering (see EventRouter).
+    Returns (batches, positions)."""
+    ring = 1
+    while ring < max(2, len(events)):
+        ring <<= 1
+    return EventRouter(world, ring_log2=ring.bit_length() - 1).route(events)
 
 
 def _device(group=None):

@@ -194,6 +194,13 @@ class Engine:
         _check(lib().sg_snapshot_metrics(self.h, int(now), out.ctypes.data, cap, C.byref(n)))
         return out[: min(cap, n.value)]
 
+    def snapshot_to(self, now: int, out_ptr: int, cap: int) -> int:
+        """sg_snapshot_metrics into caller memory (a device pointer stays on the device); returns the
+        number of MetricNode rows produced (only min(n, cap) are written)."""
+        n = C.c_uint64()
+        _check(lib().sg_snapshot_metrics(self.h, int(now), C.c_void_p(out_ptr), cap, C.byref(n)))
+        return n.value
+
     # ---- token server (sg_cluster_*; DefaultTokenService.requestToken, csrv/flow/DefaultTokenService.java:37-48)
     def cluster_set_connected(self, flow_id: int, n: int):
         _check(lib().sg_cluster_set_connected_count(self.h, int(flow_id), int(n)))

@@ -105,8 +105,12 @@ def decode_request(body: bytes) -> Optional[ClusterRequest]:
 
 
 def decode_param_flow(b: bytes) -> Optional[ParamFlowRequest]:
-    """ParamFlowRequestDataDecoder.decode: None unless >= 16 bytes and amount > 0.  An unknown param type
-    stops decoding (the reference skips the value without consuming its bytes)."""
+    """ParamFlowRequestDataDecoder.decode (sentinel-cluster-server-default .../codec/data/
+    ParamFlowRequestDataDecoder.java:34-94): None unless >= 16 bytes and amount > 0.  The loop runs
+    `amount` times; decodeParam's false return for an unknown type byte is ignored, so the next byte is
+    read as the next value's type.  A read past the end of the body (ByteBuf IndexOutOfBoundsException,
+    including a string whose declared length exceeds the remaining bytes or is negative) throws out of
+    the decoder, so the request is dropped: None."""
     if len(b) < 16:
         return None
     fid, cnt, amount = struct.unpack_from(">qii", b, 0)
@@ -119,6 +123,8 @@ def decode_param_flow(b: bytes) -> Optional[ParamFlowRequest]:
             off += 1
             if t == PARAM_TYPE_STRING:
                 n = struct.unpack_from(">i", b, off)[0]
+                if n < 0 or off + 4 + n > len(b):
+                    return None
                 params.append(("java.lang.String", b[off + 4:off + 4 + n].decode("utf-8", "replace")))
                 off += 4 + n
             elif t in _PARAM_WIRE:
@@ -126,10 +132,9 @@ def decode_param_flow(b: bytes) -> Optional[ParamFlowRequest]:
                 v = struct.unpack_from(fmt, b, off)[0]
                 params.append((cls, v))
                 off += struct.calcsize(fmt)
-            else:
-                break
+            # else: unknown type, decodeParam returns false and the loop goes on
     except struct.error:
-        pass
+        return None
     return ParamFlowRequest(fid, cnt, params)
 
 
@@ -256,14 +261,15 @@ class TokenServer:
         self.max_batch = max_batch
         self.record = record
         self.conns = ConnectionManager()
-        self._pending: List[Tuple[asyncio.StreamWriter, int, FlowRequest]] = []
-        self._ppending: List[Tuple[asyncio.StreamWriter, int, ParamFlowRequest]] = []
+        # FLOW and PARAM_FLOW requests in arrival order: (writer, xid, type, request)
+        self._pending: List[Tuple[asyncio.StreamWriter, int, int, object]] = []
         self.param_key = param_key  # (text, java class) -> interned 64-bit key
         self._wake = asyncio.Event()
         self._server = None
         self._batcher = None
         self.batches: List[int] = []      # sizes of the device calls (observability)
         self.submitted: List[tuple] = []  # (xids, requests, results) of every device call, in order
+        self.errors: List[str] = []       # device-call failures answered with FAIL (observability)
 
     async def start(self, host: str = "127.0.0.1", port: int = DEFAULT_CLUSTER_SERVER_PORT):
         self._server = await asyncio.start_server(self._serve, host, port)
@@ -309,11 +315,11 @@ class TokenServer:
                             writer.write(encode_ping_response(req.xid, n))
                     elif req.type == MSG_TYPE_FLOW:
                         if req.data is not None:  # the reference's processor NPEs on a null body
-                            self._pending.append((writer, req.xid, req.data))
+                            self._pending.append((writer, req.xid, MSG_TYPE_FLOW, req.data))
                             self._wake.set()
                     elif req.type == MSG_TYPE_PARAM_FLOW and self.param_key is not None:
                         if req.data is not None:  # the reference's processor NPEs on a null body
-                            self._ppending.append((writer, req.xid, req.data))
+                            self._pending.append((writer, req.xid, MSG_TYPE_PARAM_FLOW, req.data))
                             self._wake.set()
                     else:
                         writer.write(encode_bad_response(req.xid, req.type))
@@ -325,19 +331,35 @@ class TokenServer:
             writer.close()
 
     async def _batch_loop(self):
+        """One tick = every request queued since the last one, decided with ONE clock reading, in arrival
+        order: consecutive requests of one type form one device call (FLOW and PARAM_FLOW share the
+        namespace's GlobalRequestLimiter, so the order of the calls is the order of arrival).  A device
+        error fails the requests of that call (TokenResultStatus.FAIL) and the loop keeps serving."""
         while True:
             await self._wake.wait()
             self._wake.clear()
             await asyncio.sleep(0)  # let every readable connection queue its frames first
-            while self._pending:
-                batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
-                self._decide(batch)
-            while self._ppending:
-                batch, self._ppending = self._ppending[: self.max_batch], self._ppending[self.max_batch:]
-                self._decide_param(batch)
+            if not self._pending:
+                continue
+            now = self.clock()
+            queue, self._pending = self._pending, []
+            i = 0
+            while i < len(queue):
+                typ, j = queue[i][2], i
+                while j < len(queue) and queue[j][2] == typ and j - i < self.max_batch:
+                    j += 1
+                run = [(w, x, r) for w, x, _, r in queue[i:j]]
+                try:
+                    (self._decide if typ == MSG_TYPE_FLOW else self._decide_param)(run, now)
+                except Exception as exc:  # e.g. SentinelError from the device call
+                    self.errors.append(repr(exc))
+                    for w, xid, _ in run:
+                        if not w.is_closing():
+                            w.write(encode_flow_response(xid, A.TOKEN_FAIL, 0, 0) if typ == MSG_TYPE_FLOW
+                                    else encode_param_flow_response(xid, A.TOKEN_FAIL, 0))
+                i = j
 
-    def _decide(self, batch):
-        now = self.clock()
+    def _decide(self, batch, now: int):
         reqs = np.zeros(len(batch), dtype=A.TOKEN_REQ_DTYPE)
         reqs["ts"] = now
         reqs["flow_id"] = [r.flow_id for _, _, r in batch]
@@ -351,8 +373,7 @@ class TokenServer:
             if not w.is_closing():
                 w.write(encode_flow_response(xid, int(o["status"]), int(o["remaining"]), int(o["wait_in_ms"])))
 
-    def _decide_param(self, batch):
-        now = self.clock()
+    def _decide_param(self, batch, now: int):
         reqs = np.zeros(len(batch), dtype=A.PARAM_TOKEN_REQ_DTYPE)
         vals: List[int] = []
         for j, (_, _, r) in enumerate(batch):

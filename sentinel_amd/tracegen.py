@@ -78,12 +78,36 @@ class Workload:
         arr = C.cast(self.names_ptr, C.POINTER(C.c_char_p))
         return [arr[i].decode() for i in range(self.n_res)]
 
-    def install(self, target):
-        """Register names and load the rules into an Engine or an oracle (same calls)."""
+    _STRUCTS = {"flow": A.SgFlowRule, "degrade": A.SgDegradeRule, "param": A.SgParamRule}
+
+    def install(self, target, res_ids=None):
+        """Register names and load the rules into an Engine or an oracle (same calls).  With res_ids,
+        every name is still registered (ids stay global) but only the rules of those resources are
+        loaded (a resource-partitioned shard)."""
         target.register_ptrs(self.names_ptr, self.n_res)
         for kind, (ptr, n) in (("flow", self.flow), ("degrade", self.degrade), ("param", self.param)):
-            if n:
+            if not n:
+                continue
+            if res_ids is None:
                 getattr(target, "load_%s_rules" % kind)((C.c_void_p(ptr), n))
+                continue
+            sub = self._subset(kind, ptr, n, res_ids)
+            getattr(target, "load_%s_rules" % kind)((C.c_void_p(sub.ctypes.data), len(sub)))
+            self._keep = getattr(self, "_keep", []) + [sub]
+
+    def _subset(self, kind, ptr, n, res_ids):
+        """The rules (raw struct rows, resource-name pointers kept) whose resource is in res_ids."""
+        size = C.sizeof(self._STRUCTS[kind])
+        raw = np.frombuffer((C.c_char * (n * size)).from_address(ptr), dtype=np.dtype((np.void, size)))
+        rptr = np.frombuffer((C.c_char * (n * size)).from_address(ptr), dtype=np.uint64).reshape(n, size // 8)[:, 0]
+        names = np.frombuffer((C.c_char * (8 * self.n_res)).from_address(self.names_ptr), dtype=np.uint64)
+        order = np.argsort(names)
+        k = np.searchsorted(names[order], rptr)
+        rid = order[np.minimum(k, self.n_res - 1)]
+        if not (names[rid] == rptr).all():
+            raise ValueError("a rule names a resource outside the workload's name table")
+        keep = np.isin(rid, np.asarray(res_ids))
+        return np.ascontiguousarray(raw[keep])
 
     def close(self):
         if getattr(self, "h", None):

@@ -124,6 +124,77 @@ def _w_metrics(rank, world, port):
     dist.destroy_process_group()
 
 
+def _w_routed_decisions(rank, world, port):
+    """Each rank decides its splitmix64 shard of one C4 stream (ENTRY/EXIT/TRACE, three batches) with its
+    own engine; the merged decisions and the owned resources' node states equal one engine's run over the
+    whole stream.  The oracle is the engine here (CPU), so this checks the routing: shards, order and the
+    rewriting of EXIT/TRACE references to each rank's numbering."""
+    dist = _init(rank, world, port)
+    import pyoracle as O
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    from sentinel_amd import tracegen as T
+    w = T.Workload(4, n_entries=40_000, n_res=300)
+    ev = w.events
+    mine = O.Oracle(max_slot_chain_size=0)
+    w.install(mine)
+    router = D.EventRouter(world, ring_log2=18)
+    cuts = np.linspace(0, len(ev), 4).astype(np.int64)
+    dec = np.zeros(len(ev), dtype=np.uint32)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        parts, pos = router.route(np.ascontiguousarray(ev[a:b]))
+        rows = np.zeros(len(pos[rank]), dtype=[("i", "<i8"), ("d", "<u4"), ("pad", "<u4")])
+        rows["i"] = a + pos[rank]
+        rows["d"] = mine.submit(parts[rank])
+        for got in D._all_gather_rows(rows):
+            dec[got["i"]] = got["d"]
+    whole = O.Oracle(max_slot_chain_size=0)
+    w.install(whole)
+    ref = whole.submit(ev)
+    assert np.array_equal(dec, ref), (rank, int(np.nonzero(dec != ref)[0][0]))
+    owned = np.nonzero(D.shard_of(np.arange(w.n_res), world) == rank)[0]
+    for r in owned[:60]:
+        g, o = mine.read_node(int(r)), whole.read_node(int(r))
+        assert g["thread"] == o["thread"] and np.array_equal(g["minute"], o["minute"]), r
+    st = ref[ev["kind"] == A.EV_ENTRY] & 0xFF
+    assert (st == A.BLOCK_FLOW).sum() > 0 and (st == A.BLOCK_DEGRADE).sum() > 0
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_routed_decisions_equal_single_engine_gloo():
+    mp.spawn(_w_routed_decisions, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_router_rewrites_references():
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    ev = np.zeros(6, dtype=A.EVENT_DTYPE)
+    ev["ts"] = T0 + np.arange(6)
+    ev["res_id"] = [1, 2, 1, 2, 1, 1]
+    ev["kind"] = [A.EV_ENTRY, A.EV_ENTRY, A.EV_EXIT, A.EV_EXIT, A.EV_TRACE, A.EV_EXIT]
+    ev["aux"] = [0, 0, A.aux_exit(0, 7), A.aux_exit(1, 3), 0, A.aux_exit(A.REF_NONE, 2)]
+    router = D.EventRouter(2, ring_log2=4)
+    parts, pos = router.route(ev)
+    o1, o2 = int(D.shard_of(1, 2)), int(D.shard_of(2, 2))
+    REF = np.uint64(A.REF_NONE)
+    if o1 != o2:
+        p1 = parts[o1]
+        assert list(p1["aux"] & REF) == [0, 0, 0, A.REF_NONE]  # the EXIT and TRACE name local index 0
+        assert int(p1["aux"][1]) >> 48 == 7 and int(p1["aux"][3]) >> 48 == 2  # RT bits kept
+        assert list(parts[o2]["aux"] & REF) == [0, 0]
+    # next batch: a reference into the previous batch maps through the ring; a future reference is rejected
+    ev2 = np.zeros(2, dtype=A.EVENT_DTYPE)
+    ev2["ts"] = T0 + 10
+    ev2["res_id"] = [2, 2]
+    ev2["kind"] = [A.EV_EXIT, A.EV_EXIT]
+    ev2["aux"] = [A.aux_exit(1, 1), A.aux_exit(9, 1)]
+    parts2, _ = router.route(ev2)
+    got = parts2[o2]["aux"] & REF
+    n2_before = 2 if o1 != o2 else 6
+    assert int(got[0]) == (0 if o1 != o2 else 1) and int(got[1]) == n2_before + 1
+
+
 def test_shard_and_route_events():
     from sentinel_amd import _abi as A
     from sentinel_amd import dist as D
@@ -151,3 +222,23 @@ def test_request_tokens_gloo():
 @pytest.mark.gpu
 def test_request_tokens_gpu_server():
     mp.spawn(_w_tokens, args=(2, _port(), True), nprocs=2, join=True)
+
+
+def test_partitioned_oracle_equals_one_oracle():
+    # bench.py's multi-core CPU baseline (and the large-trace parity replays): 4 resource-partitioned oracles
+    # in threads, rules installed per shard, decisions and node states equal one oracle's over 3 batches
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from sentinel_amd import tracegen as T
+    w = T.Workload(4, n_entries=60_000, n_res=2_000)
+    po = O.PartitionedOracle(w, 4, max_slot_chain_size=0)
+    one = O.Oracle(max_slot_chain_size=0)
+    w.install(one)
+    ev = w.events
+    cuts = np.linspace(0, len(ev), 4).astype(np.int64)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        assert np.array_equal(po.submit(ev[a:b]), one.submit(ev[a:b]))
+    for r in np.argsort(-np.bincount(ev["res_id"], minlength=w.n_res))[:30]:
+        g, o = po.read_node(int(r)), one.read_node(int(r))
+        assert np.array_equal(g["minute"], o["minute"]) and g["thread"] == o["thread"]
+    po.close()

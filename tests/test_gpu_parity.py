@@ -194,6 +194,35 @@ def test_param_burst_scenario():
     assert [x & 0xFF for x in d] == expect
 
 
+def test_backward_clock_across_batches_is_an_error():
+    # a resource whose next batch starts before a window it already holds (LeapArray would hand
+    # out a detached bucket).  The decide kernels flag it and sg_submit must return SG_EINVAL, not SG_OK.
+    eng = _engine()
+    rid = eng.register("back")
+    eng.load_flow_rules([A.flow_rule("back", 100)])
+    assert (eng.submit(_ev([(T0 + 5000, rid, A.EV_ENTRY, 1, 0, 0)]))[0] & 0xFF) == A.PASS
+    with pytest.raises(E.SentinelError) as ei:
+        eng.submit(_ev([(T0, rid, A.EV_ENTRY, 1, 0, 0)]))
+    assert ei.value.code == A.SG_EINVAL and "non-decreasing" in str(ei.value)
+    # the engine stays usable for time-ordered batches
+    assert (eng.submit(_ev([(T0 + 6000, rid, A.EV_ENTRY, 1, 0, 0)]))[0] & 0xFF) == A.PASS
+
+
+@pytest.mark.parametrize("kind", [A.EV_EXIT, A.EV_TRACE])
+def test_reference_to_other_resource_is_an_error(kind, bin_mode):
+    # An EXIT/TRACE naming an earlier ENTRY of another resource (the ABI requires its own resource's ENTRY):
+    # BF_BAD_REF raised by the decide kernels surfaces as SG_EINVAL from sg_submit.
+    eng = _engine()
+    a, b = eng.register("ra"), eng.register("rb")
+    eng.load_flow_rules([A.flow_rule("ra", 100), A.flow_rule("rb", 100)])
+    rows = [(T0 + i, a if i % 2 else b, A.EV_ENTRY, 1, 0, 0) for i in range(600)]
+    aux = A.aux_exit(1, 5) if kind == A.EV_EXIT else 1  # event 1 is an ENTRY of "ra"
+    rows.append((T0 + 700, b, kind, 1, 0, aux))
+    with pytest.raises(E.SentinelError) as ei:
+        eng.submit(_ev(rows))
+    assert ei.value.code == A.SG_EINVAL and "references" in str(ei.value)
+
+
 def test_degrade_rt_scenario():
     # DegradeRule RT breaker (core/slots/block/degrade/DegradeRule.java:181-193): 5 consecutive
     # checks over the threshold cut the resource for timeWindow seconds.

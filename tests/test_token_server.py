@@ -225,3 +225,69 @@ def test_server_param_flow_on_device_matches_oracle():
     for xid, typ, st, data in got:
         assert typ == S.MSG_TYPE_PARAM_FLOW and (st,) + tuple(data) == by_xid[xid]
     assert {s for s, _, _ in by_xid.values()} >= {A.TOKEN_OK, A.TOKEN_BLOCKED, A.TOKEN_NO_RULE_EXISTS}
+
+
+def test_param_flow_decoder_unknown_type_and_truncation():
+    # ParamFlowRequestDataDecoder.java:34-94: the loop runs `amount` times and ignores decodeParam's false
+    # return, so an unknown type byte is consumed and the next byte is read as the next type.
+    head = struct.pack(">ibqii", 3, 2, 77, 1, 3)
+    body = head + bytes([0x7F]) + struct.pack(">bi", S.PARAM_TYPE_INTEGER, 5) + struct.pack(">bq", S.PARAM_TYPE_LONG, 6)
+    assert S.decode_request(body).data == S.ParamFlowRequest(77, 1, [("java.lang.Integer", 5), ("java.lang.Long", 6)])
+    # a read past the end throws out of the decoder: the request is dropped (no partial param list)
+    assert S.decode_request(head + struct.pack(">bi", S.PARAM_TYPE_INTEGER, 5)).data is None
+    short_str = struct.pack(">ibqii", 3, 2, 77, 1, 1) + struct.pack(">bi", S.PARAM_TYPE_STRING, 10) + b"abc"
+    assert S.decode_request(short_str).data is None
+    neg_str = struct.pack(">ibqii", 3, 2, 77, 1, 1) + struct.pack(">bi", S.PARAM_TYPE_STRING, -1)
+    assert S.decode_request(neg_str).data is None
+    assert S.decode_request(struct.pack(">ibqii", 3, 2, 77, 1, 2) + struct.pack(">bh", S.PARAM_TYPE_SHORT, 1)).data is None
+
+
+class _MixedStub(_Stub):
+    """Records the order and clock of every device call; the first FLOW call raises."""
+
+    def __init__(self):
+        super().__init__()
+        self.calls = []
+
+    def cluster_request_array(self, reqs):
+        self.calls.append(("flow", int(reqs["ts"][0]), len(reqs)))
+        if len(self.calls) == 1:
+            raise RuntimeError("device error")
+        return super().cluster_request_array(reqs)
+
+    def cluster_request_param_array(self, reqs, vals):
+        self.calls.append(("param", int(reqs["ts"][0]), len(reqs)))
+        out = np.zeros(len(reqs), dtype=A.TOKEN_RES_DTYPE)
+        out["status"] = A.TOKEN_OK
+        return out
+
+
+def test_server_tick_order_clock_and_error_recovery():
+    # One tick: FLOW x2, PARAM x1, FLOW x1 in arrival order -> three device calls in that order, one clock
+    # reading for the whole tick.  The first call raises: its requests get FAIL, the loop keeps serving.
+    stub = _MixedStub()
+    ticks = []
+
+    def clock():
+        ticks.append(1)
+        return 1_700_000_000_000 + len(ticks)
+
+    async def run():
+        srv = S.TokenServer(stub, clock=clock, param_key=lambda text, cls: 5)
+        port = await srv.start(port=0)
+        frames = [S.encode_flow_request(1, 10, 1, False), S.encode_flow_request(2, 10, 1, False),
+                  S.encode_param_flow_request(3, 11, 1, [(S.PARAM_TYPE_INTEGER, 1)]),
+                  S.encode_flow_request(4, 10, 1, False)]
+        _, w, out = await _client(port, frames, 4)
+        _, w2, out2 = await _client(port, [S.encode_flow_request(5, 10, 2, False)], 1)
+        w.close()
+        w2.close()
+        await srv.stop()
+        return srv, out, out2
+
+    srv, out, out2 = asyncio.run(run())
+    by = {x: st for x, _, st, _ in out}
+    assert by == {1: A.TOKEN_FAIL, 2: A.TOKEN_FAIL, 3: A.TOKEN_OK, 4: A.TOKEN_OK}
+    assert [c[0] for c in stub.calls[:3]] == ["flow", "param", "flow"] and [c[2] for c in stub.calls[:3]] == [2, 1, 1]
+    assert len({c[1] for c in stub.calls[:3]}) == 1  # one clock reading per tick
+    assert out2[0][2] == A.TOKEN_OK and len(srv.errors) == 1

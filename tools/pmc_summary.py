@@ -1,44 +1,73 @@
-"""Per-launch HBM traffic of bench.py's kernels from two rocprofv3 --pmc passes.
+"""Per-batch HBM traffic and kernel time of bench.py from rocprofv3 passes (tools/profile.sh).
 
-usage: python tools/pmc_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json
+usage: python tools/pmc_summary.py FETCH.csv WRITE.csv KERNEL_STATS.csv OUT.json [git_head]
 
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
 reports half the bytes of a wide coalesced streaming read, so it is doubled here (other access
 widths are uncalibrated -- the doubled figure is an upper-bound style estimate for them).
-The decide stage's traffic is the sum over its kernels of the mean per-dispatch bytes.
+Totals are summed over every dispatch of the run and divided by the number of batches (one
+k_rs_first dispatch per batch), so kernels launched several times per batch (radix passes, scans)
+count every launch.  The JSON is stamped with bench.src_sha() of the sources it was measured on;
+bench.py reports its traffic only when that stamp matches the sources it runs.
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 
-DECIDE = ("k_jac", "k_lane", "k_lite", "k_fill", "k_resolve")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+DECIDE = ("k_jac", "k_lane", "k_lite", "k_fill", "k_resolve", "k_chain")
+SKIP = ("k_init_state", "k_snap_", "k_set_flags")
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
 
 
 def load(path, counter):
-    per = defaultdict(list)
+    tot, cnt = defaultdict(float), defaultdict(int)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        per[name].append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in per.items()}
+        n = short(r["Kernel_Name"])
+        tot[n] += float(r["Counter_Value"]) * 1024.0
+        cnt[n] += 1
+    return tot, cnt
 
 
 def main():
-    fetch = load(sys.argv[1], "FETCH_SIZE")
-    write = load(sys.argv[2], "WRITE_SIZE")
+    fetch, fcnt = load(sys.argv[1], "FETCH_SIZE")
+    write, _ = load(sys.argv[2], "WRITE_SIZE")
+    nb = max(1, sum(v for k, v in fcnt.items() if k.startswith("k_rs_first")))
     names = sorted(set(fetch) | set(write))
-    kern = {n: {"fetch_bytes_x2": 2 * fetch.get(n, 0.0), "write_bytes": write.get(n, 0.0)} for n in names}
-    for v in kern.values():
-        v["traffic_bytes"] = v["fetch_bytes_x2"] + v["write_bytes"]
-    decide = sum(v["traffic_bytes"] for n, v in kern.items() if n.startswith(DECIDE))
-    pipeline = sum(v["traffic_bytes"] for n, v in kern.items() if n.startswith("k_") and n != "k_init_state")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of `python3 bench.py --steps 3 --warmup 1`",
-           "units": "bytes per launch (mean over dispatches); FETCH_SIZE doubled per MI355X_MICROARCH.md",
-           "decide_stage_traffic_bytes": decide, "pipeline_traffic_bytes_per_step": pipeline, "kernels": kern}
-    json.dump(out, open(sys.argv[3], "w"), indent=1)
-    print(json.dumps({"decide_stage_traffic_bytes": decide, "pipeline_traffic_bytes_per_step": pipeline}))
+    kern = {}
+    for n in names:
+        if not n.startswith("k_") or n.startswith(SKIP):  # engine kernels only (no torch / rocclr setup copies)
+            continue
+        f2, wb = 2 * fetch.get(n, 0.0), write.get(n, 0.0)
+        kern[n] = {"launches_per_batch": fcnt.get(n, 0) / nb, "fetch_bytes_x2_per_batch": f2 / nb,
+                   "write_bytes_per_batch": wb / nb, "traffic_bytes_per_batch": (f2 + wb) / nb}
+    times = {}
+    if len(sys.argv) > 4 and os.path.exists(sys.argv[3]):
+        for r in csv.DictReader(open(sys.argv[3])):
+            n = short(r["Name"])
+            times[n] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                        "ms_per_batch": float(r["TotalDurationNs"]) / 1e6 / nb}
+    total = sum(v["traffic_bytes_per_batch"] for v in kern.values())
+    decide = sum(v["traffic_bytes_per_batch"] for n, v in kern.items() if n.startswith(DECIDE))
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --kernel-trace --stats passes of "
+                     "`python3 bench.py --steps 2 --warmup 1 --sub-batches 2 --no-cpu-baseline` (tools/profile.sh)",
+           "units": "bytes per global batch (sum over the batch's dispatches); FETCH_SIZE doubled per MI355X_MICROARCH.md",
+           "src_sha": bench.src_sha(), "git_head": sys.argv[5] if len(sys.argv) > 5 else None,
+           "batch_events": 1 << 25, "batches_profiled": nb,
+           "traffic_bytes_per_batch": total, "decide_traffic_bytes_per_batch": decide,
+           "kernels": kern, "kernel_times": times}
+    json.dump(out, open(sys.argv[4], "w"), indent=1)
+    print(json.dumps({k: out[k] for k in ("src_sha", "batches_profiled", "traffic_bytes_per_batch",
+                                          "decide_traffic_bytes_per_batch")}))
 
 
 if __name__ == "__main__":
