@@ -81,7 +81,10 @@ typedef struct sg_config {
     double cluster_exceed_count;      /* 1.0 */
     double cluster_max_occupy_ratio;  /* 1.0 */
     int32_t cluster_max_allowed_qps;  /* GlobalRequestLimiter default 30000 */
-    int32_t reserved[7];
+    uint32_t aux_node_capacity;       /* origin StatisticNodes + context DefaultNodes kept on the device for the
+                                         resources whose flow rules read them (origin / "other" / CHAIN rules);
+                                         ~4 KB each, default 65536 */
+    int32_t reserved[6];
 } sg_config;
 
 /* ---- rules ----------------------------------------------------------------
@@ -159,9 +162,14 @@ enum {
 };
 enum {
     SG_F_PRIORITIZED = 1u << 0, /* SphU.entryWithPriority (ENTRY) */
-    SG_F_HAS_ARG = 1u << 1,     /* args[0] present and non-null; aux = its interned 64-bit key (ENTRY) */
+    SG_F_HAS_ARG = 1u << 1,     /* args = {args[0]}, non-null; aux = its interned 64-bit key (ENTRY; sg_submit_ex
+                                   with ext.n_args > 0 takes the args from the table instead) */
     SG_F_EXIT_ARGS = 1u << 2,   /* Entry.exit(count, args): param thread counts are released (EXIT), SURVEY Q14 */
-    SG_F_ENTRY_OUT = 1u << 3    /* EntryType.OUT (ENTRY); informational (SystemSlot is out of scope) */
+    SG_F_ENTRY_OUT = 1u << 3,   /* EntryType.OUT (ENTRY); informational (SystemSlot is out of scope) */
+    SG_F_BLOCKED_UPSTREAM = 1u << 4 /* ENTRY: the caller's SystemSlot / AuthoritySlot threw.  Those slots sit between
+                                   ParamFlowSlot and FlowSlot (param/slots/HotParamSlotChainBuilder.java:39-50), so the
+                                   param checks still run (and may block first); otherwise the entry is blocked with
+                                   SG_BLOCK_UPSTREAM and StatisticSlot counts the block (StatisticSlot.java:97-117) */
 };
 /* EXIT/TRACE aux: low 48 bits = global index of the ENTRY event this refers
  * to (SG_REF_NONE = the caller asserts the entry passed); EXIT bits 48..63 =
@@ -178,6 +186,35 @@ typedef struct sg_event {
     uint64_t aux;
 } sg_event;
 
+/* ---- per-event extension (sg_submit_ex) ---------------------------------------
+ * ProcessorSlot.entry(Context, ResourceWrapper, node, count, prioritized, Object... args)
+ * (core/slotchain/ProcessorSlot.java:41-50) carries more than an sg_event: the Context -- its
+ * name and origin (core/context/Context.java, ContextUtil.enter(name, origin)) -- and every
+ * argument.  sg_submit_ex takes one sg_event_ext per event next to the events, and a flat
+ * argument table.  An EXIT/TRACE's ext names the origin and context of its ENTRY (the Entry
+ * carries its Context); an EXIT's args are those of Entry.exit(count, args). */
+enum {
+    SG_ARG_NULL = 0,   /* args[i] == null: param rules on index i pass (ParamFlowChecker.java:59-62) */
+    SG_ARG_SCALAR = 1, /* key = the interned value (sg_param_key) */
+    SG_ARG_LIST = 2    /* a Collection or an array (ParamFlowChecker.java:75-90): its element keys are
+                          args_table[key .. key + len), each an SG_ARG_SCALAR / SG_ARG_NULL entry */
+};
+#define SG_MAX_ARGS 24        /* args per event (and largest paramIdx with a thread-count map + 1) */
+#define SG_MAX_CONTEXTS 2000  /* Constants.MAX_CONTEXT_NAME_SIZE (core/Constants.java:35): context ids above it
+                                 are ContextUtil's NullContext -- no checks, no statistics (CtSph.java:120-127) */
+typedef struct sg_arg {
+    uint64_t key;
+    uint32_t kind;     /* SG_ARG_* */
+    uint32_t len;      /* SG_ARG_LIST: element count */
+} sg_arg;
+
+typedef struct sg_event_ext {
+    uint32_t origin_id;  /* sg_intern_origin; 0 = "" (no origin) */
+    uint32_t context_id; /* sg_intern_context; 0 = sentinel_default_context */
+    uint32_t arg_off;    /* args[i] = args_table[arg_off + i], i < n_args */
+    uint32_t n_args;     /* <= SG_MAX_ARGS; ENTRY: 0 with SG_F_HAS_ARG = {aux}, 0 without = an empty array */
+} sg_event_ext;
+
 /* ---- decisions --------------------------------------------------------------
  * One uint32 per submitted event: status | rule_slot << 8 | wait_ms << 16.
  * rule_slot is the index of the blocking rule inside the resource's compiled
@@ -189,7 +226,8 @@ enum {
     SG_BLOCK_FLOW = 2,    /* FlowException       core/slots/block/flow/FlowSlot.java:154 */
     SG_BLOCK_DEGRADE = 3, /* DegradeException    core/slots/block/degrade/DegradeRuleManager.java:82 */
     SG_BLOCK_PARAM = 4,   /* ParamFlowException  param/slots/block/flow/param/ParamFlowSlot.java:98 */
-    SG_NO_CHECK = 5,      /* no slot chain (MAX_SLOT_CHAIN_SIZE) or Constants.ON == false */
+    SG_NO_CHECK = 5,      /* no slot chain (MAX_SLOT_CHAIN_SIZE), NullContext, or Constants.ON == false */
+    SG_BLOCK_UPSTREAM = 6,/* SG_F_BLOCKED_UPSTREAM: SystemBlockException / AuthorityException of the caller's slots */
     SG_NOT_ENTRY = 0xFF   /* EXIT / TRACE record */
 };
 #define SG_DECISION_STATUS(d) ((d) & 0xFFu)
@@ -304,6 +342,24 @@ int sg_param_key(sg_engine* e, const char* value, const char* class_type, uint64
 int sg_submit(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out);
 int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out);
 int sg_sync(sg_engine* e);
+
+/* sg_submit with the Context and the full argument list of every event (see sg_event_ext):
+ * origin-specific and `other` flow rules select the origin's StatisticNode, STRATEGY_CHAIN rules the
+ * DefaultNode of the entry's context (FlowRuleChecker.selectNodeByRequesterAndStrategy,
+ * core/slots/block/flow/FlowRuleChecker.java:90-124); param rules check args[paramIdx] with negative
+ * indices resolved on first use and Collection/array values checked element by element
+ * (ParamFlowSlot.java:65-101, ParamFlowChecker.java:48-99).  ext may be NULL (= sg_submit); args may be
+ * NULL when no ext names any.  All pointers may be host or device memory; sync as sg_submit. */
+int sg_submit_ex(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                 uint64_t n_args, uint32_t* out);
+int sg_submit_ex_async(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                       uint64_t n_args, uint32_t* out);
+
+/* Context names and origins (ContextUtil.enter(name, origin), core/context/ContextUtil.java:118-166):
+ * dense ids, in first-intern order; the name "" interns to origin 0 and "sentinel_default_context"
+ * to context 0.  Context ids above SG_MAX_CONTEXTS are NullContexts.  Idempotent. */
+int sg_intern_origin(sg_engine* e, const char* origin, uint32_t* out_id);
+int sg_intern_context(sg_engine* e, const char* context, uint32_t* out_id);
 
 /* Per-second MetricNode export: StatisticNode.metrics() of every ClusterNode
  * (core/node/StatisticNode.java:124-151, core/node/metric/MetricTimerListener.java:39-71).

@@ -43,6 +43,9 @@ def lib():
         L.or_param_key.restype = C.c_uint64
         L.or_param_key.argtypes = [C.c_char_p, C.c_char_p]
         L.or_submit.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.or_submit_ex.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.or_intern_origin.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
+        L.or_intern_context.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
         L.or_entry_ex.restype = C.c_uint32
         L.or_entry_ex.argtypes = [P, C.c_int64, C.c_uint32, C.c_int32, C.c_int, C.c_char_p, C.c_char_p, C.c_int,
                                   C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.POINTER(C.c_uint64)),
@@ -165,6 +168,27 @@ class Oracle:
         self.n_events += len(ev)
         return out
 
+    def submit_ex(self, events: np.ndarray, ext: np.ndarray = None, args: np.ndarray = None) -> np.ndarray:
+        ev = np.ascontiguousarray(events, dtype=A.EVENT_DTYPE)
+        ex = None if ext is None else np.ascontiguousarray(ext, dtype=A.EXT_DTYPE)
+        ar = None if args is None or len(args) == 0 else np.ascontiguousarray(args, dtype=A.ARG_DTYPE)
+        out = np.zeros(len(ev), dtype=np.uint32)
+        rc = lib().or_submit_ex(self.h, ev.ctypes.data, None if ex is None else ex.ctypes.data, len(ev),
+                                None if ar is None else ar.ctypes.data, 0 if ar is None else len(ar), out.ctypes.data)
+        assert rc == 0, rc
+        self.n_events += len(ev)
+        return out
+
+    def intern_origin(self, name: str) -> int:
+        out = C.c_uint32()
+        assert lib().or_intern_origin(self.h, name.encode(), C.byref(out)) == 0
+        return out.value
+
+    def intern_context(self, name: str) -> int:
+        out = C.c_uint32()
+        assert lib().or_intern_context(self.h, name.encode(), C.byref(out)) == 0
+        return out.value
+
     def entry(self, now, res, count=1, prioritized=False, context=None, origin=None, args=None):
         """args: list of None | int key | list[int] keys (Collection/array value)."""
         args = list(args or [])
@@ -179,7 +203,7 @@ class Oracle:
                 kinds[i] = 0
             elif isinstance(a, (list, tuple)):
                 kinds[i] = 2
-                arr = (C.c_uint64 * max(1, len(a)))(*a)
+                arr = (C.c_uint64 * max(1, len(a)))(*[0xFFFFFFFFFFFFFFFF if x is None else x for x in a])
                 keep.append(arr)
                 lists[i] = C.cast(arr, C.POINTER(C.c_uint64))
                 lens[i] = len(a)

@@ -1594,7 +1594,7 @@ static int param_throttle_check(oparam_metric* pm, oparam* rule, int acquire, ui
     if (expected <= now || expected - now < rule->r.max_queueing_time_ms) {
         *rec = now;
         int64_t wait = expected - now;
-        if (wait > 0) { *rec = expected; if (wait_ms) *wait_ms = wait; }
+        if (wait > 0) { *rec = expected; if (wait_ms) *wait_ms += wait; }  /* each element's check sleeps */
         return 1;
     }
     return 0;
@@ -1615,32 +1615,40 @@ static int param_single_check(oparam_metric* pm, oparam* rule, int acquire, uint
     return 1;
 }
 
+/* The args of one call: args[i] = a[i] (SG_ARG_NULL / SCALAR / LIST); a LIST's elements are
+ * table[a[i].key .. a[i].key + a[i].len), each SCALAR or NULL (include/sentinel_gpu.h sg_arg). */
 typedef struct {
     int n;
-    const int32_t* kind;
-    const uint64_t* key;
-    const uint64_t* const* list;
-    const int32_t* len;
+    const sg_arg* a;
+    const sg_arg* table;
 } oargs;
 
-/* ParamFlowChecker.passCheck/passLocalCheck (ParamFlowChecker.java:48-99) */
+/* ParamFlowChecker.passCheck/passLocalCheck (ParamFlowChecker.java:48-99).  A null element of a
+ * Collection/array reaches passSingleValueCheck, whose map lookup throws; passLocalCheck catches
+ * Throwable and returns true, so the value passes and its later elements are not checked. */
 static int param_pass_check(oparam_metric* pm, oparam* rule, int acquire, const oargs* a, int64_t now, int64_t* wait_ms) {
     int idx = rule->r.param_idx;
     if (a->n <= idx) return 1;
-    if (a->kind[idx] == 0) return 1;
+    const sg_arg* v = &a->a[idx];
+    if (v->kind == SG_ARG_NULL) return 1;
     if (rule->r.cluster_mode && rule->r.grade == SG_FLOW_GRADE_QPS) {
         /* passClusterCheck: no TokenService -> fallbackToLocalOrPass */
         if (!rule->r.cluster_fallback_to_local) return 1;
     }
-    if (a->kind[idx] == 2) {
-        for (int i = 0; i < a->len[idx]; ++i)
-            if (!param_single_check(pm, rule, acquire, a->list[idx][i], now, wait_ms)) return 0;
+    if (v->kind == SG_ARG_LIST) {
+        for (uint32_t i = 0; i < v->len; ++i) {
+            const sg_arg* el = &a->table[v->key + i];
+            if (el->kind != SG_ARG_SCALAR) return 1;
+            if (!param_single_check(pm, rule, acquire, el->key, now, wait_ms)) return 0;
+        }
         return 1;
     }
-    return param_single_check(pm, rule, acquire, a->key[idx], now, wait_ms);
+    return param_single_check(pm, rule, acquire, v->key, now, wait_ms);
 }
 
-/* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241) */
+/* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241): every index
+ * with a thread-count map; a null element throws inside the try around the whole loop, so the
+ * remaining elements and indices are skipped. */
 static void pm_thread_one(u64map* m, uint64_t v, int add) {
     int64_t* p = m_find(m, v);
     if (add) {
@@ -1655,9 +1663,17 @@ static void pm_thread_one(u64map* m, uint64_t v, int add) {
 static void pm_thread_args(oparam_metric* pm, const oargs* a, int add) {
     for (int i = 0; i < a->n; ++i) {
         u64map* m = pm_thread_map(pm, i);
-        if (!m || a->kind[i] == 0) continue;
-        if (a->kind[i] == 2) { for (int k = 0; k < a->len[i]; ++k) pm_thread_one(m, a->list[i][k], add); }
-        else pm_thread_one(m, a->key[i], add);
+        const sg_arg* v = &a->a[i];
+        if (!m || v->kind == SG_ARG_NULL) continue;
+        if (v->kind == SG_ARG_LIST) {
+            for (uint32_t k = 0; k < v->len; ++k) {
+                const sg_arg* el = &a->table[v->key + k];
+                if (el->kind != SG_ARG_SCALAR) return;
+                pm_thread_one(m, el->key, add);
+            }
+        } else {
+            pm_thread_one(m, v->key, add);
+        }
     }
 }
 
@@ -1681,7 +1697,9 @@ static int ensure_chain(or_engine* e, ores* r) {
 
 /* CtSph.entryWithPriority -> DefaultProcessorSlotChain.entry -> ... */
 static uint32_t do_entry(or_engine* e, int64_t now, uint32_t res, int32_t count, int prioritized, uint32_t ctx,
-                         int32_t origin, const oargs* a, uint8_t* status_out) {
+                         int32_t origin, const oargs* a, int upstream, uint8_t* status_out) {
+    /* NullContext: more than MAX_CONTEXT_NAME_SIZE contexts (ContextUtil.trueEnter, CtSph.java:120-127) */
+    if (ctx > SG_MAX_CONTEXTS) { *status_out = SG_NO_CHECK; return mk_decision(SG_NO_CHECK, 0, 0); }
     if (!e->switch_on) { *status_out = SG_NO_CHECK; return mk_decision(SG_NO_CHECK, 0, 0); }
     ores* r = res_get(e, res);
     if (!ensure_chain(e, r)) { *status_out = SG_NO_CHECK; return mk_decision(SG_NO_CHECK, 0, 0); }
@@ -1711,6 +1729,8 @@ static uint32_t do_entry(or_engine* e, int64_t now, uint32_t res, int32_t count,
             else wait += w; /* the Java thread sleeps once per queueing check */
         }
     }
+    /* SystemSlot / AuthoritySlot of the caller (after ParamFlowSlot, before FlowSlot) */
+    if (status == SG_PASS && upstream) { status = SG_BLOCK_UPSTREAM; rule_slot = 0; }
     /* FlowSlot.checkFlow (FlowSlot.java:146-158) */
     if (status == SG_PASS) {
         for (int i = 0; i < r->n_flow; ++i) {
@@ -1774,21 +1794,31 @@ static oentry* new_entry(or_engine* e) {
     return en;
 }
 
-int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+/* one batch of sg_submit / sg_submit_ex (ext and args may be NULL) */
+static int submit_impl(or_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                       uint64_t n_args, uint32_t* out) {
     if (!e || (n && !ev)) return SG_EINVAL;
     for (uint64_t i = 0; i < n; ++i) {
         const sg_event* v = &ev[i];
+        const sg_event_ext* x = ext ? &ext[i] : NULL;
+        if (x && (x->n_args > SG_MAX_ARGS || (x->n_args && (!args || x->arg_off + (uint64_t)x->n_args > n_args))))
+            return SG_EINVAL;
+        uint32_t ctx = x ? x->context_id : 0;
+        int32_t origin = x && x->origin_id ? (int32_t)x->origin_id - 1 : -1;
         uint64_t gidx = e->n_events++;
         uint32_t d = SG_NOT_ENTRY;
+        sg_arg one = {v->aux, SG_ARG_SCALAR, 0};
+        oargs a = {0, NULL, args};
+        if (x && x->n_args) { a.n = (int)x->n_args; a.a = args + x->arg_off; }
         if (v->kind == SG_EV_ENTRY) {
-            int32_t kind0 = 1;
-            uint64_t key0 = v->aux;
-            oargs a = {0, NULL, NULL, NULL, NULL};
-            if (v->flags & SG_F_HAS_ARG) { a.n = 1; a.kind = &kind0; a.key = &key0; }
+            if (!(x && x->n_args) && (v->flags & SG_F_HAS_ARG)) { a.n = 1; a.a = &one; }
             oentry* en = new_entry(e);
-            en->ts = v->ts; en->res = v->res_id; en->ctx = 0; en->origin = -1; en->count = v->count;
-            en->nargs = a.n; en->key0 = key0; en->key0_kind = a.n ? 1 : 0;
-            d = do_entry(e, v->ts, v->res_id, v->count, (v->flags & SG_F_PRIORITIZED) != 0, 0, -1, &a, &en->status);
+            en->ts = v->ts; en->res = v->res_id; en->ctx = ctx; en->origin = origin; en->count = v->count;
+            en->key0_kind = a.n && a.a[0].kind == SG_ARG_SCALAR ? 1 : 0;
+            en->nargs = a.n ? 1 : 0;
+            en->key0 = en->key0_kind ? a.a[0].key : 0;
+            d = do_entry(e, v->ts, v->res_id, v->count, (v->flags & SG_F_PRIORITIZED) != 0, ctx, origin, &a,
+                         (v->flags & SG_F_BLOCKED_UPSTREAM) != 0, &en->status);
             m_put(&e->ev2ent, gidx, (int64_t)(en - e->ents));
         } else if (v->kind == SG_EV_EXIT) {
             uint64_t ref = v->aux & SG_REF_NONE;
@@ -1801,13 +1831,15 @@ int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
             if (!en) { /* caller asserts the entry passed */
                 memset(&tmp, 0, sizeof(tmp));
                 ores* r = res_get(e, v->res_id);
-                tmp.status = r->has_chain && e->switch_on ? SG_PASS : SG_NO_CHECK;
-                tmp.res = v->res_id; tmp.ctx = 0; tmp.origin = -1;
+                tmp.status = r->has_chain && e->switch_on && ctx <= SG_MAX_CONTEXTS ? SG_PASS : SG_NO_CHECK;
+                tmp.res = v->res_id; tmp.ctx = ctx; tmp.origin = origin;
                 en = &tmp;
             }
-            int32_t kind0 = en->key0_kind;
-            oargs a = {en->nargs, &kind0, &en->key0, NULL, NULL};
-            do_exit(e, v->ts, en, v->count, rt_raw, (v->flags & SG_F_EXIT_ARGS) != 0, &a);
+            /* Entry.exit(count, args): the exit's own args; without a table, the ENTRY's args[0] (Q14) */
+            sg_arg k0 = {en->key0, en->key0_kind ? SG_ARG_SCALAR : SG_ARG_NULL, 0};
+            oargs ea = a;
+            if (!(x && x->n_args)) { ea.n = en->nargs; ea.a = &k0; }
+            do_exit(e, v->ts, en, v->count, rt_raw, (v->flags & SG_F_EXIT_ARGS) != 0, &ea);
         } else if (v->kind == SG_EV_TRACE) {
             uint64_t ref = v->aux & SG_REF_NONE;
             int ok;
@@ -1815,7 +1847,7 @@ int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
                 int64_t* p = m_find(&e->ev2ent, ref);
                 ok = p && (e->ents[*p].status == SG_PASS || e->ents[*p].status == SG_PASS_WAIT);
             } else {
-                ok = v->res_id < e->n_res && e->res[v->res_id].has_chain;
+                ok = v->res_id < e->n_res && e->res[v->res_id].has_chain && ctx <= SG_MAX_CONTEXTS;
             }
             ores* r = v->res_id < e->n_res ? &e->res[v->res_id] : NULL;
             /* Tracer.traceExceptionToNode -> ClusterNode.trace (ClusterNode.java:99-106) */
@@ -1826,18 +1858,55 @@ int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
     return SG_OK;
 }
 
+int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+    return submit_impl(e, ev, NULL, n, NULL, 0, out);
+}
+
+int or_submit_ex(or_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                 uint64_t n_args, uint32_t* out) {
+    return submit_impl(e, ev, ext, n, args, n_args, out);
+}
+
+int or_intern_origin(or_engine* e, const char* origin, uint32_t* out_id) {
+    if (!e || !out_id) return SG_EINVAL;
+    *out_id = (!origin || !*origin) ? 0 : st_intern(&e->origin_names, origin) + 1;
+    return SG_OK;
+}
+
+int or_intern_context(or_engine* e, const char* context, uint32_t* out_id) {
+    if (!e || !out_id) return SG_EINVAL;
+    *out_id = st_intern(&e->ctx_names, context && *context ? context : "sentinel_default_context");
+    return SG_OK;
+}
+
 uint32_t or_entry_ex(or_engine* e, int64_t now, uint32_t res, int32_t count, int prioritized, const char* context,
                      const char* origin, int nargs, const int32_t* arg_kind, const uint64_t* arg_key,
                      const uint64_t* const* arg_list, const int32_t* arg_len, uint64_t* handle) {
     uint32_t ctx = context ? st_intern(&e->ctx_names, context) : 0;
     int32_t org = (origin && *origin) ? (int32_t)st_intern(&e->origin_names, origin) : -1;
-    oargs a = {nargs, arg_kind, arg_key, arg_list, arg_len};
+    /* the kinds/keys/lists of the call as an sg_arg table: args first, list elements after them */
+    int total = nargs;
+    for (int i = 0; i < nargs; ++i) if (arg_kind[i] == 2) total += arg_len[i];
+    sg_arg* t = (sg_arg*)calloc((size_t)(total > 0 ? total : 1), sizeof(sg_arg));
+    int off = nargs;
+    for (int i = 0; i < nargs; ++i) {
+        if (arg_kind[i] == 1) { t[i].kind = SG_ARG_SCALAR; t[i].key = arg_key[i]; }
+        else if (arg_kind[i] == 2) {
+            t[i].kind = SG_ARG_LIST; t[i].key = (uint64_t)off; t[i].len = (uint32_t)arg_len[i];
+            for (int k = 0; k < arg_len[i]; ++k, ++off) {  /* UINT64_MAX stands for a null element */
+                t[off].kind = arg_list[i][k] == UINT64_MAX ? SG_ARG_NULL : SG_ARG_SCALAR;
+                t[off].key = arg_list[i][k];
+            }
+        }
+    }
+    oargs a = {nargs, t, t};
     oentry* en = new_entry(e);
     en->ts = now; en->res = res; en->ctx = ctx; en->origin = org; en->count = count;
     en->nargs = nargs > 0 ? 1 : 0;
     en->key0_kind = nargs > 0 && arg_kind[0] == 1 ? 1 : 0;
     en->key0 = en->key0_kind ? arg_key[0] : 0;
-    uint32_t d = do_entry(e, now, res, count, prioritized, ctx, org, &a, &en->status);
+    uint32_t d = do_entry(e, now, res, count, prioritized, ctx, org, &a, 0, &en->status);
+    free(t);
     if (handle) *handle = (uint64_t)(en - e->ents);
     return d;
 }
@@ -1847,8 +1916,8 @@ int or_exit_ex(or_engine* e, int64_t now, uint64_t handle, int32_t count, int wi
     oentry* en = &e->ents[handle];
     if (en->exited) return SG_ESTATE;
     en->exited = 1;
-    int32_t kind0 = en->key0_kind;
-    oargs a = {en->nargs, &kind0, &en->key0, NULL, NULL};
+    sg_arg k0 = {en->key0, en->key0_kind ? SG_ARG_SCALAR : SG_ARG_NULL, 0};
+    oargs a = {en->nargs, &k0, &k0};
     do_exit(e, now, en, count, now - en->ts, with_args, &a);
     return SG_OK;
 }
@@ -2383,5 +2452,6 @@ void sg_config_default(sg_config* c) {
     c->cluster_exceed_count = 1.0;
     c->cluster_max_occupy_ratio = 1.0;
     c->cluster_max_allowed_qps = 30000;
+    c->aux_node_capacity = 65536;
 }
 #endif

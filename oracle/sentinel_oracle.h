@@ -37,8 +37,13 @@ int or_load_param_rules(or_engine* e, const sg_param_rule* r, uint32_t n, uint32
 int or_rule_order(or_engine* e, uint32_t res, int kind, int32_t* out, int cap);
 uint64_t or_param_key(const char* value, const char* class_type);
 
-/* Replay a batch of sg_event records (same contract as sg_submit). */
+/* Replay a batch of sg_event records (same contract as sg_submit / sg_submit_ex). */
 int or_submit(or_engine* e, const sg_event* ev, uint64_t n, uint32_t* out);
+int or_submit_ex(or_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                 uint64_t n_args, uint32_t* out);
+/* sg_intern_origin / sg_intern_context: same ids in the same first-intern order */
+int or_intern_origin(or_engine* e, const char* origin, uint32_t* out_id);
+int or_intern_context(or_engine* e, const char* context, uint32_t* out_id);
 
 /* Rich entry for integration tests: explicit context name / origin and an
  * args array.  arg_kind[i]: 0 = null, 1 = scalar key arg_key[i], 2 = a

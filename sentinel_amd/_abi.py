@@ -40,7 +40,11 @@ F_PRIORITIZED = 1 << 0
 F_HAS_ARG = 1 << 1
 F_EXIT_ARGS = 1 << 2
 F_ENTRY_OUT = 1 << 3
+F_BLOCKED_UPSTREAM = 1 << 4
 REF_NONE = 0xFFFFFFFFFFFF
+ARG_NULL, ARG_SCALAR, ARG_LIST = 0, 1, 2
+MAX_ARGS = 24
+MAX_CONTEXTS = 2000
 
 PASS = 0
 PASS_WAIT = 1
@@ -48,6 +52,7 @@ BLOCK_FLOW = 2
 BLOCK_DEGRADE = 3
 BLOCK_PARAM = 4
 NO_CHECK = 5
+BLOCK_UPSTREAM = 6
 NOT_ENTRY = 0xFF
 
 TOKEN_BAD_REQUEST = -4
@@ -95,7 +100,8 @@ class SgConfig(C.Structure):
         ("cluster_exceed_count", C.c_double),
         ("cluster_max_occupy_ratio", C.c_double),
         ("cluster_max_allowed_qps", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("aux_node_capacity", C.c_uint32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -231,6 +237,39 @@ EVENT_DTYPE = np.dtype(
     align=True,
 )
 assert EVENT_DTYPE.itemsize == 24
+
+EXT_DTYPE = np.dtype([("origin_id", "<u4"), ("context_id", "<u4"), ("arg_off", "<u4"), ("n_args", "<u4")])
+ARG_DTYPE = np.dtype([("key", "<u8"), ("kind", "<u4"), ("len", "<u4")])
+assert EXT_DTYPE.itemsize == 16 and ARG_DTYPE.itemsize == 16
+
+
+def ext_tables(n: int, args_of: dict, origin=None, context=None):
+    """sg_event_ext rows + the flat sg_arg table for n events.  args_of[i] = list of per-index values:
+    None (null), an int key (scalar) or a list/tuple of int keys / None (a Collection/array).
+    origin / context: optional length-n arrays of interned ids."""
+    ext = np.zeros(n, dtype=EXT_DTYPE)
+    if origin is not None:
+        ext["origin_id"] = origin
+    if context is not None:
+        ext["context_id"] = context
+    rows = []
+    for i in sorted(args_of):
+        vals = args_of[i]
+        ext["arg_off"][i] = len(rows)
+        ext["n_args"][i] = len(vals)
+        rows.extend([None] * len(vals))
+        base = ext["arg_off"][i]
+        for j, v in enumerate(vals):
+            if v is None:
+                rows[base + j] = (0, ARG_NULL, 0)
+            elif isinstance(v, (list, tuple)):
+                rows[base + j] = (len(rows), ARG_LIST, len(v))
+                rows.extend((0, ARG_NULL, 0) if x is None else (int(x), ARG_SCALAR, 0) for x in v)
+            else:
+                rows[base + j] = (int(v), ARG_SCALAR, 0)
+    table = np.array(rows, dtype=ARG_DTYPE) if rows else np.zeros(0, dtype=ARG_DTYPE)
+    return ext, table
+
 
 METRIC_NODE_DTYPE = np.dtype(
     [

@@ -95,7 +95,21 @@ __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t r
     N.mslot = -1;
     N.pfslot = -2;
     N.mst = 0;
-    N.bor = S.prio && S.prio[res] ? S.borrow + (uint64_t)res * 4 : nullptr;
+    N.bor = S.prio && (S.prio[res] & PM_PRIO) ? S.borrow + (uint64_t)res * 4 : nullptr;
+}
+// an origin StatisticNode / context DefaultNode (AuxNode); its borrow ring starts empty, so it is always
+// consulted (a bucket borrows only what a prioritized entry on this very node put there)
+__device__ __forceinline__ void node_load_aux(Node& N, const AuxNode* a) {
+    N.sb[0] = a->sec[0];
+    N.sb[1] = a->sec[1];
+    N.thread = a->info.thread;
+    N.flags = a->info.flags;
+    N.exc_sum_sec = -1;
+    N.exc_sum = 0;
+    N.mslot = -1;
+    N.pfslot = -2;
+    N.mst = 0;
+    N.bor = const_cast<int64_t*>(a->borrow);
 }
 
 __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
@@ -451,6 +465,12 @@ __device__ __forceinline__ void stat_trace(Node& N, const Ctx& C, int64_t t, int
         min_add(N, 0, 0, 0, 0, count, INT64_MAX);
         if (N.exc_sum_sec == t - t % 1000) N.exc_sum += count;
     }
+}
+
+__device__ __forceinline__ void node_store_aux(const Node& N, AuxNode* a) {
+    a->sec[0] = N.sb[0];
+    a->sec[1] = N.sb[1];
+    a->info.thread = N.thread;
 }
 
 __device__ __forceinline__ void node_store(const Node& N, const DevState& S, uint32_t res, uint32_t pflags) {

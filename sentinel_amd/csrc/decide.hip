@@ -2,7 +2,7 @@
 //
 // Pipeline position (engine.cpp sg_submit_async):
 //   record build + sort (kernels.hip k_rs_first, k_radix_*) -> k_seg_* (segments + bins) ->
-//   k_gather (16-byte sorted records, same-batch EXIT/TRACE references mapped to sorted positions)
+//   k_scatter_rec + k_block_sums (16-byte sorted records, same-batch references mapped to sorted positions)
 //   -> k_chain -> decide kernels by bin -> k_post (decisions back to submission order and into
 //   the status ring).
 //
@@ -46,23 +46,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // =================================================================================
 // segments: starts, lengths, bins, bin-ordered dispatch list
 // =================================================================================
-__global__ void k_seg_flags(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ flag) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
-}
-__global__ void k_seg_start(const uint32_t* __restrict__ keys, uint64_t n, const uint32_t* __restrict__ flag,
-                            const uint32_t* __restrict__ pos, Seg* __restrict__ segs) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    Seg s;
-    s.res = keys[i];
-    s.start = (uint32_t)i;
-    s.len = 0;
-    s.bin = 0;
-    segs[pos[i]] = s;
-}
-// Fused segment detection (the default; SG_SEG_FUSED=0 keeps flags + n-wide scan + k_seg_start):
-// a tile of 4096 sorted keys per workgroup, 16 consecutive keys per lane (4 x 16-byte loads);
+// Segment detection: a tile of 4096 sorted keys per workgroup, 16 consecutive keys per lane (4 x 16-byte loads);
 // k_seg_count writes the tile's segment-start count, a scan over tiles gives the offsets, and
 // k_seg_emit recounts and writes each Seg at its offset.  Reads the keys twice instead of
 // writing and re-reading an n-wide flag and position array.
@@ -142,7 +126,7 @@ __global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ k
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
 __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n,
-                                                 const Prog* __restrict__ prog, const uint8_t* __restrict__ prio,
+                                                 const Prog* __restrict__ prog, const uint32_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
                                                  uint32_t nblk) {
@@ -155,7 +139,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
         const uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
         sg.len = end - sg.start;
         const Prog p = prog[sg.res];
-        const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // members decided with 16-rule lanes
+        const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // PX_*: decided with 16-rule lanes
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
                           !prio[sg.res] && !p.multi;
         uint32_t bin;
@@ -193,62 +177,15 @@ __global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, u
 // =================================================================================
 // sorted records
 // =================================================================================
-// Sorted-order records: a 16-byte gather of the record built in submission order (kernels.hip
-// k_rs_first), plus the mapping of same-batch references to the ENTRY's sorted position through
-// the inverse permutation written by the last radix pass (bit 31 = the referenced event is an
-// ENTRY).  A reference to a non-ENTRY resolves like an unknown entry in or_submit: an EXIT is then
-// taken as the caller asserting the entry passed, a TRACE as not counted.
-// Side tables for frozen-stretch skipping (k_jac<..., SKIP>): the forward link of every referenced
-// ENTRY (an atomic exchange detects a second EXIT/TRACE naming the same ENTRY), and per 1024-position
-// block the ENTRY count sum plus a flag for EXIT/TRACEs that count without a same-batch link.
-__global__ __launch_bounds__(256) void k_gather(const SEv* __restrict__ rec_o, const uint32_t* __restrict__ vals,
-                                                uint64_t n, const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
-                                                uint32_t* __restrict__ prev, uint32_t* __restrict__ nprev,
-                                                Link* __restrict__ link, uint32_t* __restrict__ bst, uint32_t epoch,
-                                                uint32_t* __restrict__ bflags) {
-    __shared__ uint32_t wsum[4];
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t ecnt = 0;
-    bool stat = false;
-    if (p < n) {
-        SEv r = rec_o[vals[p] & 0x7FFFFFFFu];
-        if (r.code == RC_BATCH) {
-            const uint32_t po = pos_of[r.x];
-            if (po & 0x80000000u) r.x = po & 0x7FFFFFFFu;
-            else r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-        } else if (r.code == RC_PREV) {
-            prev[atomicAdd(nprev, 1u)] = (uint32_t)p;
-        }
-        if (r.kind == SG_EV_ENTRY) {
-            ecnt = r.cnt;
-            if (r.cnt == 0) atomicOr(bflags, BF_ZERO_CNT);
-        } else if (r.code == RC_BATCH) {
-            unsigned long long* dst = reinterpret_cast<unsigned long long*>(
-                r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
-            const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
-            if ((uint32_t)(old >> 32) == epoch) atomicOr(bflags, BF_MULTI_LINK);
-        } else if (r.code == RC_NONE || r.code == RC_PREV) {
-            stat = true;
-        }
-        recs[p] = r;
-    }
-    // the block's 256 positions lie in one 1024-position block: one atomic per workgroup
-    uint32_t v = ecnt;
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-    const bool st = __ballot(stat) != 0;
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v | (st ? BST_STATIC : 0u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sum = 0, fl = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { sum += wsum[w] & BST_CNT; fl |= wsum[w] & BST_STATIC; }
-        if (sum) atomicAdd(&bst[p >> 10], sum);
-        if (fl) atomicOr(&bst[p >> 10], fl);
-    }
-}
-// Scatter variant of the record build (the default; SG_GATHER=1 selects k_gather): reads the
-// submission-order records and the inverse permutation sequentially and writes each record to its
-// sorted position (random 16-byte writes instead of random 16-byte reads); the per-1024-block ENTRY
-// count sums then come from one sequential pass over the sorted records (k_block_sums).
+// Sorted-order records: reads the submission-order records built by k_rs_first and the inverse
+// permutation written by the last radix pass sequentially, maps same-batch references to the ENTRY's
+// sorted position (bit 31 of pos_of = the referenced event is an ENTRY; a reference to a non-ENTRY
+// resolves like an unknown entry: an EXIT is then the caller asserting the entry passed, a TRACE is not
+// counted) and writes each record to its sorted position (random 16-byte writes; gathering through the
+// permutation instead -- random 16-byte reads -- over-fetched whole lines, ~6 GB per C4 batch).  Side
+// tables for frozen-stretch skipping (k_jac<..., SKIP>) come from one sequential pass over the sorted
+// records (k_block_sums): per 1024 positions the ENTRY count sum plus a flag for EXIT/TRACEs that count
+// without a same-batch link, and the forward link of every referenced ENTRY.
 __global__ __launch_bounds__(256) void k_scatter_rec(const SEv* __restrict__ rec_o, uint64_t n,
                                                      const uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
                                                      uint32_t* __restrict__ prev, uint32_t* __restrict__ nprev,
@@ -305,12 +242,14 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
     }
 }
 // Every same-batch EXIT/TRACE must find its own position in its ENTRY's link after k_block_sums'
-// plain stores: a mismatch means a second EXIT (or TRACE) named the same ENTRY.
-__global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ recs, uint64_t n,
-                                                     const Link* __restrict__ link, uint32_t epoch,
+// plain stores: a mismatch means a second EXIT (or TRACE) named the same ENTRY.  It must also name an
+// ENTRY of its own resource: the two carry the same sort key (in sorted order they sit a few positions
+// apart, so the key loads hit cache; inside a STRATEGY_RELATE component the key is the component's).
+__global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ recs, const uint32_t* __restrict__ skeys,
+                                                     uint64_t n, const Link* __restrict__ link, uint32_t epoch,
                                                      uint32_t* __restrict__ bflags) {
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
-    bool multi = false;
+    bool multi = false, bad = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
@@ -321,10 +260,12 @@ __global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ rec
             if (r.kind != SG_EV_ENTRY && r.code == RC_BATCH) {
                 const uint64_t v = r.kind == SG_EV_EXIT ? link[r.x].exit_l : link[r.x].trace_l;
                 if (v != (((uint64_t)epoch << 32) | (uint32_t)p)) multi = true;
+                if (skeys[r.x] != skeys[p]) bad = true;
             }
         }
     }
     if (__ballot(multi) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_MULTI_LINK);
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_BAD_REF);
 }
 // references into earlier batches, once those are decided: the ENTRY's status from the ring
 // (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
@@ -408,13 +349,19 @@ __global__ __launch_bounds__(256) void k_fill(const Span* __restrict__ spans, co
 // ENTRY, res) candidates for the host, which grants in first-ENTRY order up to the cap.
 __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                         uint32_t m, NodeInfo* __restrict__ info, uint32_t grant_all, uint32_t* __restrict__ ncand,
-                        uint64_t* __restrict__ cand, const sg_event* __restrict__ ev, const Prog* __restrict__ prog) {
+                        uint64_t* __restrict__ cand, const sg_event* __restrict__ ev, const Prog* __restrict__ prog,
+                        const sg_event_ext* __restrict__ ext, uint32_t max_ctx) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= m) return;
     Seg sg = segs[s];
-    if (prog[sg.res].multi) {  // a STRATEGY_RELATE component: every member's first ENTRY
+    // an ENTRY in a NullContext never looks its chain up (CtSph.entryWithPriority, CtSph.java:120-127)
+    auto looks_up = [&](uint32_t j) {
+        return recs[sg.start + j].kind == SG_EV_ENTRY &&
+               (!ext || ext[vals[sg.start + j] & 0x7FFFFFFFu].context_id <= max_ctx);
+    };
+    if (prog[sg.res].multi & PX_MULTI) {  // a STRATEGY_RELATE component: every member's first ENTRY
         for (uint32_t j = 0; j < sg.len; ++j) {
-            if (recs[sg.start + j].kind != SG_EV_ENTRY) continue;
+            if (!looks_up(j)) continue;
             const uint32_t vi = vals[sg.start + j] & 0x7FFFFFFFu;
             const uint32_t res = ev[vi].res_id;
             const uint32_t fr = info[res].flags;
@@ -427,7 +374,7 @@ __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict
     uint32_t f = info[sg.res].flags;
     if (f & (NI_CHAIN | NI_REJECTED)) return;
     for (uint32_t j = 0; j < sg.len; ++j) {
-        if (recs[sg.start + j].kind == SG_EV_ENTRY) {
+        if (looks_up(j)) {
             if (grant_all) info[sg.res].flags = f | NI_CHAIN;
             else cand[atomicAdd(ncand, 1u)] = ((uint64_t)(vals[sg.start + j] & 0x7FFFFFFFu) << 32) | sg.res;
             return;
@@ -474,27 +421,29 @@ __device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool
     *found = false;
     return 0;
 }
-__device__ __forceinline__ uint64_t tc_key(uint32_t epoch, uint32_t res) {
-    return (2ULL << 62) | ((uint64_t)(epoch & 0x3FFFFFFF) << 32) | res;
+// ParameterMetric thread-count map of paramIdx idx: key (2 << 62) | idx << 54 | epoch << 32 | res
+__device__ __forceinline__ uint64_t tc_key(uint32_t epoch, uint32_t res, uint32_t idx) {
+    return (2ULL << 62) | ((uint64_t)(idx & 0xFF) << 54) | ((uint64_t)(epoch & 0x3FFFFF) << 32) | res;
 }
-// ParameterMetric thread-count map of paramIdx 0 (ParameterMetric.java:167-199)
-__device__ int64_t thread_count_get(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint64_t v,
-                                    uint32_t* bflags) {
+// ParameterMetric.getThreadCount (ParameterMetric.java:235-241)
+__device__ int64_t thread_count_get(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t idx,
+                                    uint64_t v, uint32_t* bflags) {
     bool nw;
-    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res), v, false, &nw, bflags);
+    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res, idx), v, false, &nw, bflags);
     return s ? s->v0 : 0;
 }
-__device__ void thread_count_add(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint64_t v,
-                                 int64_t d, uint32_t* bflags) {
+__device__ void thread_count_add(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t idx,
+                                 uint64_t v, int64_t d, uint32_t* bflags) {
     bool nw;
-    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res), v, true, &nw, bflags);
+    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res, idx), v, true, &nw, bflags);
     if (!s) return;
     int64_t c = s->v0 + d;
     if (d < 0 && nw) c = 0;  // putIfAbsent(value, new AtomicInteger()) without a decrement
     s->v0 = c < 0 ? 0 : c;
 }
+// ParamFlowChecker.passSingleValueCheck (ParamFlowChecker.java:101-119) of one value
 __device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, const DRule& r,
-                            int acquire, uint64_t v, int64_t t, int64_t& wait, uint32_t* bflags) {
+                            uint32_t idx, int acquire, uint64_t v, int64_t t, int64_t& wait, uint32_t* bflags) {
     if (r.grade == SG_FLOW_GRADE_QPS) {
         bool hf;
         int32_t hc = hot_count(S, r, v, &hf);
@@ -539,8 +488,8 @@ __device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, 
         int32_t ov = (int32_t)s->v1;
         if (j_iadd(ov, -acquire) >= 0) { s->v1 = j_iadd(ov, -acquire); return true; }
         return false;
-    } else if (r.grade == SG_FLOW_GRADE_THREAD) {  // passSingleValueCheck THREAD (:101-119)
-        int64_t tc = thread_count_get(S, cfg, res, epoch, v, bflags);
+    } else if (r.grade == SG_FLOW_GRADE_THREAD) {
+        int64_t tc = thread_count_get(S, cfg, res, epoch, idx, v, bflags);
         bool hf;
         int32_t hc = hot_count(S, r, v, &hf);
         if (hf) return ++tc <= hc;
@@ -550,12 +499,127 @@ __device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, 
     return true;
 }
 
+// ---- the Context and args of one event (sg_submit_ex, include/sentinel_gpu.h sg_event_ext)
+struct EvX {
+    uint32_t origin, ctx;  // interned ids (0: no origin / sentinel_default_context)
+    uint32_t n;            // args.length
+    const sg_arg* a;       // args; null with n == 1: the single key k0 (SG_F_HAS_ARG, or a key-ring key)
+    uint64_t k0;
+};
+__device__ __forceinline__ EvX evx_of(const DevState& S, uint32_t oi, uint32_t flags, uint64_t aux, bool entry) {
+    EvX x;
+    x.origin = 0; x.ctx = 0; x.n = 0; x.a = nullptr; x.k0 = aux;
+    if (S.ext) {
+        const sg_event_ext e = S.ext[oi];
+        x.origin = e.origin_id;
+        x.ctx = e.context_id;
+        if (e.n_args) { x.n = e.n_args; x.a = S.args + e.arg_off; return x; }
+    }
+    if (entry && (flags & SG_F_HAS_ARG)) x.n = 1;
+    return x;
+}
+__device__ __forceinline__ sg_arg evx_arg(const EvX& x, uint32_t i) {
+    if (x.a) return x.a[i];
+    sg_arg r;
+    r.key = x.k0; r.kind = SG_ARG_SCALAR; r.len = 0;
+    return r;
+}
+// ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241): every index with a
+// thread-count map; a null element of a Collection/array throws inside the try that wraps the whole loop,
+// so the remaining elements and indices are skipped.
+__device__ void thread_args(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t nflags,
+                            const EvX& x, int64_t d, uint32_t* bflags) {
+    for (uint32_t i = 0; i < x.n && i < SG_MAX_ARGS; ++i) {
+        if (!(nflags & ni_tm(i))) continue;
+        const sg_arg v = evx_arg(x, i);
+        if (v.kind == SG_ARG_LIST) {
+            for (uint32_t k = 0; k < v.len; ++k) {
+                const sg_arg el = S.args[v.key + k];
+                if (el.kind != SG_ARG_SCALAR) return;
+                thread_count_add(S, cfg, res, epoch, i, el.key, d, bflags);
+            }
+        } else if (v.kind == SG_ARG_SCALAR) {
+            thread_count_add(S, cfg, res, epoch, i, v.key, d, bflags);
+        }
+    }
+}
+
+// ---- origin StatisticNodes / context DefaultNodes (PX_ORIGIN / PX_CHAIN resources, k_lane<16> only)
+__device__ AuxNode* aux_get(const DevState& S, uint32_t res, uint32_t kind, uint32_t id, uint32_t* bflags) {
+    const unsigned long long key = ((unsigned long long)res << 32) | ((unsigned long long)kind << 31) | (id & 0x7FFFFFFFu);
+    uint64_t h = mix64(key) & S.aux_mask;
+    for (uint64_t probe = 0; probe <= S.aux_mask; ++probe) {
+        AuxSlot* s = &S.aux_tab[h];
+        unsigned long long k = __hip_atomic_load(&s->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == AUX_EMPTY) {
+            unsigned long long expect = AUX_EMPTY;
+            if (__hip_atomic_compare_exchange_strong(&s->key, &expect, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                // keys of a resource are inserted by its owner lane only: nobody else reads this slot's idx
+                const uint32_t idx = atomicAdd(S.aux_count, 1u);
+                if (idx >= S.aux_cap) { atomicOr(bflags, BF_AUX_FULL); s->idx = NO_ID; return nullptr; }
+                AuxNode* a = &S.aux_pool[idx];
+                Bkt z;
+                z.ws = -1; z.pass = 0; z.block = 0; z.exc = 0; z.succ = 0; z.rt = 0; z.occ = 0; z.minrt = 0;
+                a->sec[0] = z; a->sec[1] = z;
+                for (int m = 0; m < 60; ++m) a->minb[m] = z;
+                a->borrow[0] = -1; a->borrow[1] = 0; a->borrow[2] = -1; a->borrow[3] = 0;
+                NodeInfo ni;
+                ni.thread = 0; ni.flags = 0; ni.exc_sum_sec = -1; ni.exc_sum = 0; ni.last_fetch = -1;
+                a->info = ni;
+                s->idx = idx;
+                return a;
+            }
+            k = expect;
+        }
+        if (k == key) return s->idx == NO_ID ? nullptr : &S.aux_pool[s->idx];
+        h = (h + 1) & S.aux_mask;
+    }
+    atomicOr(bflags, BF_AUX_FULL);
+    return nullptr;
+}
+// the DefaultNode of (res, ctx) is kept iff a CHAIN rule of the resource names ctx
+__device__ __forceinline__ bool chain_ctx_kept(const DRule* flows, int nf, uint32_t ctx) {
+    for (int k = 0; k < nf; ++k)
+        if (flows[k].strategy == SG_STRATEGY_CHAIN && flows[k].chain_ctx == ctx) return true;
+    return false;
+}
+// StatisticSlot bookkeeping on an origin node / DefaultNode: 0 = block, 1 = pass, 2 = PriorityWait (thread only),
+// 3 = exit (rt, success, thread)
+__device__ void aux_stat(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t kind, uint32_t id, int what,
+                         int64_t t, int cnt, int64_t rt, uint32_t* bflags) {
+    AuxNode* a = aux_get(S, res, kind, id, bflags);
+    if (!a) return;
+    Node NA;
+    node_load_aux(NA, a);
+    const Ctx CA{a->minb, cfg.max_rt, 0};
+    if (what == 2) NA.thread++;
+    else if (what == 3) stat_exit(NA, CA, t, cnt, rt);
+    else stat_entry(NA, CA, t, cnt, what == 1);
+    min_flush(NA, CA.minb);
+    node_store_aux(NA, a);
+}
+
+enum { SEL_NONE = 0, SEL_CLUSTER = 1, SEL_ORIGIN = 2, SEL_DEFAULT = 3, SEL_RELATE = 4 };
+// FlowRuleChecker.selectNodeByRequesterAndStrategy / selectReferenceNode (FlowRuleChecker.java:67-124)
+__device__ __forceinline__ int flow_select(const DRule& r, const EvX& x, const DRule* flows, int nf) {
+    bool applies;
+    if (r.la_kind == LA_DEFAULT) applies = true;
+    else if (r.la_kind == LA_ORIGIN) applies = x.origin != 0 && x.origin == r.la_origin;
+    else {  // "other": FlowRuleManager.isOtherOrigin (FlowRuleManager.java:106-125)
+        applies = x.origin != 0;
+        for (int k = 0; k < nf; ++k)
+            if (flows[k].la_origin == x.origin) applies = false;
+    }
+    if (!applies) return SEL_NONE;
+    if (r.strategy == SG_STRATEGY_RELATE) return r.ref == NO_REF ? SEL_CLUSTER : SEL_RELATE;
+    if (r.strategy == SG_STRATEGY_CHAIN) return x.ctx == r.chain_ctx ? SEL_DEFAULT : SEL_NONE;
+    return r.la_kind == LA_DEFAULT ? SEL_CLUSTER : SEL_ORIGIN;
+}
+
 // =================================================================================
 // k_lane: one lane per segment, event by event
 // =================================================================================
-// One ENTRY through StatisticSlot -> ParamFlowSlot -> FlowSlot -> DegradeSlot
-// (param/slots/HotParamSlotChainBuilder.java:38-51, StatisticSlot.entry StatisticSlot.java:54-133).
-// rs[] is indexed only with unrolled constants, so for NRMAX <= 4 it stays in registers.
 // FlowRuleChecker.selectReferenceNode for STRATEGY_RELATE (FlowRuleChecker.java:67-88): the controller
 // runs on the ClusterNode of ref (ClusterBuilderSlot.getClusterNode: null until an ENTRY of ref was
 // processed with a chain -> pass), with its side effects on that node (currentWindow resets)
@@ -579,59 +643,130 @@ __device__ int relate_check(const DevState& S, const DevCfg& cfg, const DRule& r
     node_store(NB, S, b, pb.pflags);
     return rc;
 }
+// the controller of one flow rule on an origin node / DefaultNode (1 pass, 0 block, 2 PriorityWait)
+__device__ int aux_check(const DevState& S, const DevCfg& cfg, const DRule& r, RState& s, uint32_t res, uint32_t kind,
+                         uint32_t id, int64_t t, int cnt, uint32_t fl, int64_t& wait, uint32_t* bflags) {
+    AuxNode* a = aux_get(S, res, kind, id, bflags);
+    if (!a) return 1;
+    Node NA;
+    node_load_aux(NA, a);
+    const Ctx CA{a->minb, cfg.max_rt, 0};
+    int rc;
+    if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
+        int64_t w = 0;
+        rc = default_can_pass_prio(NA, CA, r, t, cnt, cfg.occupy_timeout, w);
+        if (rc == 2) wait += w;
+    } else {
+        rc = flow_can_pass(NA, CA, r, s, t, cnt, wait) ? 1 : 0;
+    }
+    min_flush(NA, CA.minb);
+    node_store_aux(NA, a);
+    return rc;
+}
 
+// One ENTRY through StatisticSlot -> ParamFlowSlot -> [caller's System/Authority] -> FlowSlot -> DegradeSlot
+// (param/slots/HotParamSlotChainBuilder.java:38-51, StatisticSlot.entry StatisticSlot.java:54-133).
+// rs[] is indexed only with unrolled constants, so for NRMAX <= 4 it stays in registers.  AUX: the
+// resource keeps origin nodes / DefaultNodes (k_lane<16> only).
 template <int NRMAX, bool MULTI = false>
 __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg,
                                                const Prog& pg, RState (&rs)[NRMAX], uint32_t res, int64_t t, int cnt,
-                                               uint32_t fl, uint64_t arg, uint32_t* bflags) {
+                                               uint32_t fl, const EvX& x, uint32_t* bflags) {
     const DRule* rules = S.rules + pg.rule_off;
     const int np = pg.n_param, nfl = np + pg.n_flow, nr = nfl + pg.n_degrade;
+    const bool aux = NRMAX >= 16 && (pg.multi & (PX_ORIGIN | PX_CHAIN));
     uint32_t status = ST_PASS, slot = 0;
     int64_t wait = 0;
-    if (np) {  // ParamFlowSlot.checkFlow (ParamFlowSlot.java:77-101): metric maps exist from now on
-        N.flags |= NI_PM;
-        if (pg.pflags & PF_PARAM_IDX0) N.flags |= NI_TM0;
-    }
 #pragma unroll
     for (int s = 0; s < NRMAX; ++s) {
         if (s < nr && status == ST_PASS) {
             const DRule r = rules[s];
-            if (s < np) {
-                if (fl & SG_F_HAS_ARG) {
-                    int64_t w = 0;
-                    if (!param_check(S, cfg, res, pg.tc_epoch, r, cnt, arg, t, w, bflags)) { status = ST_BLOCK_PARAM; slot = r.slot; }
-                    else wait += w;
+            if (s < np) {  // ParamFlowSlot.checkFlow (ParamFlowSlot.java:77-101)
+                int idx = r.param_idx;
+                if (idx < 0) {  // applyRealParamIdx mutates the rule once (RState.a = resolved index + 1)
+                    if (rs[s].a == 0) rs[s].a = 1 + ((-idx <= (int)x.n) ? (int)x.n + idx : -idx);
+                    idx = (int)rs[s].a - 1;
                 }
+                N.flags |= NI_PM;  // initHotParamMetricsFor -> ParameterMetric.initialize
+                if (idx < SG_MAX_ARGS) N.flags |= ni_tm((uint32_t)idx);
+                if (r.behavior == PB_INIT_ONLY || idx >= (int)x.n) continue;
+                const sg_arg v = evx_arg(x, (uint32_t)idx);
+                bool ok = true;
+                int64_t w = 0;
+                if (v.kind == SG_ARG_LIST) {  // Collection / array: element by element (ParamFlowChecker.java:75-90)
+                    for (uint32_t k = 0; k < v.len && ok; ++k) {
+                        const sg_arg el = S.args[v.key + k];
+                        if (el.kind != SG_ARG_SCALAR) break;  // a null element throws: passLocalCheck passes
+                        ok = param_check(S, cfg, res, pg.tc_epoch, r, (uint32_t)idx, cnt, el.key, t, w, bflags);
+                    }
+                } else if (v.kind == SG_ARG_SCALAR) {
+                    ok = param_check(S, cfg, res, pg.tc_epoch, r, (uint32_t)idx, cnt, v.key, t, w, bflags);
+                }
+                if (!ok) { status = ST_BLOCK_PARAM; slot = r.slot; }
+                else wait += w;
             } else if (s < nfl) {  // FlowSlot.checkFlow (FlowSlot.java:146-158)
-                if (MULTI && r.ref != NO_REF) {
-                    int64_t w = 0;
-                    const int rc = relate_check(S, cfg, r, rs[s], t, cnt, fl, w);
-                    if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
-                    else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }
-                    else wait += w;
-                } else if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
-                    int64_t w = 0;
-                    const int rc = default_can_pass_prio(N, C, r, t, cnt, cfg.occupy_timeout, w);
-                    if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
-                    else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }  // PriorityWaitException
-                } else if (!flow_can_pass(N, C, r, rs[s], t, cnt, wait)) { status = ST_BLOCK_FLOW; slot = r.slot; }
+                if (s == np && (fl & SG_F_BLOCKED_UPSTREAM)) { status = ST_BLOCK_UPSTREAM; slot = 0; continue; }
+                const int sel = flow_select(r, x, rules + np, pg.n_flow);
+                if (sel == SEL_NONE) continue;
+                int rc;
+                int64_t w = 0;
+                if (MULTI && sel == SEL_RELATE) rc = relate_check(S, cfg, r, rs[s], t, cnt, fl, w);
+                else if (aux && (sel == SEL_ORIGIN || sel == SEL_DEFAULT))
+                    rc = aux_check(S, cfg, r, rs[s], res, sel == SEL_ORIGIN ? AUX_ORIGIN : AUX_CONTEXT,
+                                   sel == SEL_ORIGIN ? x.origin : x.ctx, t, cnt, fl, w, bflags);
+                else if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT)
+                    rc = default_can_pass_prio(N, C, r, t, cnt, cfg.occupy_timeout, w);
+                else rc = flow_can_pass(N, C, r, rs[s], t, cnt, w) ? 1 : 0;
+                if (rc == 0) { status = ST_BLOCK_FLOW; slot = r.slot; }
+                else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }  // PriorityWaitException
+                else wait += w;
             } else {  // DegradeRuleManager.checkDegrade (DegradeRuleManager.java:72-85)
                 if (!degrade_pass(N, C, r, rs[s], t)) { status = ST_BLOCK_DEGRADE; slot = r.slot; }
             }
         }
     }
+    if (status == ST_PASS && pg.n_flow == 0 && (fl & SG_F_BLOCKED_UPSTREAM)) { status = ST_BLOCK_UPSTREAM; slot = 0; }
+    // StatisticSlot.entry (StatisticSlot.java:54-133): DefaultNode -> ClusterNode, origin node
+    const int what = status == ST_PASS ? 1 : status == ST_PASS_WAIT ? 2 : 0;
+    if (aux) {
+        if ((pg.multi & PX_ORIGIN) && x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, what, t, cnt, 0, bflags);
+        if ((pg.multi & PX_CHAIN) && chain_ctx_kept(rules + np, pg.n_flow, x.ctx))
+            aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, what, t, cnt, 0, bflags);
+    }
     if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
         N.thread++;
-        if ((N.flags & NI_PM) && (N.flags & NI_TM0) && (fl & SG_F_HAS_ARG))
-            thread_count_add(S, cfg, res, pg.tc_epoch, arg, 1, bflags);
+        if (N.flags & NI_PM) thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, 1, bflags);
         return mk_dec(ST_PASS_WAIT, slot, wait);
     }
     const bool passed = status == ST_PASS;
     stat_entry(N, C, t, cnt, passed);
-    // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount
-    if (passed && (N.flags & NI_PM) && (N.flags & NI_TM0) && (fl & SG_F_HAS_ARG))
-        thread_count_add(S, cfg, res, pg.tc_epoch, arg, 1, bflags);
+    // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount(args)
+    if (passed && (N.flags & NI_PM)) thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, 1, bflags);
     return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
+}
+
+// StatisticSlot.exit of an effective EXIT (StatisticSlot.java:136-173) + ParamFlowStatisticExitCallback.onExit:
+// Entry.exit(count, args) releases the thread counts of its args -- the EXIT's own args (sg_submit_ex), else
+// args[0] of its ENTRY from the key ring
+template <int NRMAX>
+__device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg, const Prog& pg,
+                                          uint32_t res, int64_t t, const SEv& r, const EvX& x, uint64_t ref,
+                                          uint32_t* bflags) {
+    stat_exit(N, C, t, r.cnt, r.rt);
+    if (NRMAX >= 16 && (pg.multi & (PX_ORIGIN | PX_CHAIN))) {
+        const DRule* flows = S.rules + pg.rule_off + pg.n_param;
+        if ((pg.multi & PX_ORIGIN) && x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, 3, t, r.cnt, r.rt, bflags);
+        if ((pg.multi & PX_CHAIN) && chain_ctx_kept(flows, pg.n_flow, x.ctx))
+            aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
+    }
+    if (!(r.flags & SG_F_EXIT_ARGS) || !(N.flags & NI_PM)) return;
+    if (x.n) { thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, -1, bflags); return; }
+    if (!S.key_ring || ref == SG_REF_NONE) return;
+    const uint64_t key = S.key_ring[ref & cfg.ring_mask];
+    if (key == NO_KEY) return;
+    EvX k;
+    k.origin = 0; k.ctx = 0; k.n = 1; k.a = nullptr; k.k0 = key;
+    thread_args(S, cfg, res, pg.tc_epoch, N.flags, k, -1, bflags);
 }
 
 // A STRATEGY_RELATE component (one segment, members in event order): each event runs on its own
@@ -643,7 +778,8 @@ __device__ void lane_multi(const SEv* __restrict__ recs, const sg_event* __restr
                            int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     for (uint32_t j = 0; j < sg.len; ++j) {
         const SEv r = recs[sg.start + j];
-        const sg_event& E = ev[vals[sg.start + j] & 0x7FFFFFFFu];
+        const uint32_t oi = vals[sg.start + j] & 0x7FFFFFFFu;
+        const sg_event& E = ev[oi];
         const uint32_t res = E.res_id;
         const int64_t t = t0 + r.dt;
         const Prog pg = S.prog[res];
@@ -654,15 +790,15 @@ __device__ void lane_multi(const SEv* __restrict__ recs, const sg_event* __restr
         RState rs[NRMAX];
 #pragma unroll
         for (int s = 0; s < NRMAX; ++s) if (s < nr) rs[s] = S.rstate[pg.rule_off + s];
-        const bool has_chain = (N.flags & NI_CHAIN) != 0;
+        const EvX x = evx_of(S, oi, r.flags, E.aux, r.kind == SG_EV_ENTRY);
+        const bool has_chain = (N.flags & NI_CHAIN) != 0 && x.ctx <= S.max_ctx;  // NullContext: no chain
         const bool chain = has_chain && cfg.switch_on;
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
         if (r.kind == SG_EV_ENTRY) {
             if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
             else {
                 N.flags |= NI_TOUCHED;  // ClusterBuilderSlot runs before the checks
-                const uint64_t arg = (r.flags & SG_F_HAS_ARG) ? E.aux : 0;
-                d = lane_entry<NRMAX, true>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
+                d = lane_entry<NRMAX, true>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, x, bflags);
             }
         } else {
             bool eff;
@@ -676,14 +812,9 @@ __device__ void lane_multi(const SEv* __restrict__ recs, const sg_event* __restr
             }
             if (eff) {
                 if (r.kind == SG_EV_EXIT) {
-                    stat_exit(N, C, t, r.cnt, r.rt);
-                    if ((r.flags & SG_F_EXIT_ARGS) && S.key_ring && (N.flags & NI_PM) && (N.flags & NI_TM0) &&
-                        r.code != RC_NONE) {
-                        const uint64_t ref = r.code == RC_BATCH ? S.gbase + (vals[r.x] & 0x7FFFFFFFu)
-                                                                : (E.aux & SG_REF_NONE);
-                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
-                        if (key != NO_KEY) thread_count_add(S, cfg, res, pg.tc_epoch, key, -1, bflags);
-                    }
+                    const uint64_t ref = r.code == RC_NONE ? SG_REF_NONE
+                                         : r.code == RC_BATCH ? S.gbase + (vals[r.x] & 0x7FFFFFFFu) : (E.aux & SG_REF_NONE);
+                    lane_exit<NRMAX>(N, C, S, cfg, pg, res, t, r, x, ref, bflags);
                 } else {
                     stat_trace(N, C, t, r.cnt);
                 }
@@ -707,7 +838,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     const Seg sg = segs[order[i]];
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
-    if (NRMAX >= 16 && pg.multi) {
+    if (NRMAX >= 16 && (pg.multi & PX_MULTI)) {
         lane_multi<NRMAX>(recs, ev, vals, sg, S, cfg, t0, dec, bflags);
         return;
     }
@@ -730,8 +861,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     RState rs[NRMAX];
 #pragma unroll
     for (int s = 0; s < NRMAX; ++s) if (s < nr) rs[s] = S.rstate[pg.rule_off + s];
-    const bool has_chain = (N.flags & NI_CHAIN) != 0;
-    const bool chain = has_chain && cfg.switch_on;
+    const bool has_chain_r = (N.flags & NI_CHAIN) != 0;
     if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
         atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
     uint64_t pm = 0;  // passed bits of the segment's first 64 positions
@@ -744,13 +874,18 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
         rn[0] = rn[1];
         if (j + 2 < sg.len) rn[1] = recs[sg.start + j + 2];
         const int64_t t = t0 + r.dt;
+        const uint32_t oi = vals[sg.start + j] & 0x7FFFFFFFu;
+        // the caller's record is read only for an ENTRY's argument key or an EXIT(args) of an earlier batch's ENTRY
+        const bool need_ev = (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG)) ||
+                             (r.kind == SG_EV_EXIT && r.code == RC_PASSED && (r.flags & SG_F_EXIT_ARGS));
+        const uint64_t aux = need_ev ? ev[oi].aux : 0;
+        const EvX x = evx_of(S, oi, r.flags, aux, r.kind == SG_EV_ENTRY);
+        const bool has_chain = has_chain_r && x.ctx <= S.max_ctx;  // NullContext: no chain, no statistics
+        const bool chain = has_chain && cfg.switch_on;
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
         if (r.kind == SG_EV_ENTRY) {
             if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
-            else {
-                uint64_t arg = (r.flags & SG_F_HAS_ARG) ? ev[vals[sg.start + j] & 0x7FFFFFFFu].aux : 0;
-                d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, arg, bflags);
-            }
+            else d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, x, bflags);
             if (j < 64 && st_passed(d & 0xFF)) pm |= 1ull << j;
             LPROF(ktb)
         } else {
@@ -765,17 +900,9 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
             }
             if (eff) {
                 if (r.kind == SG_EV_EXIT) {
-                    stat_exit(N, C, t, r.cnt, r.rt);
-                    // exit(count, args): ParamFlowStatisticExitCallback.onExit -> ParameterMetric.decreaseThreadCount
-                    // with the ENTRY's args (param/slots/statistic/ParamFlowStatisticExitCallback.java:31-38, Q14)
-                    if ((r.flags & SG_F_EXIT_ARGS) && S.key_ring && (N.flags & NI_PM) && (N.flags & NI_TM0) &&
-                        r.code != RC_NONE) {
-                        const uint64_t ref = r.code == RC_BATCH
-                                                 ? S.gbase + (vals[r.x] & 0x7FFFFFFFu)
-                                                 : (ev[vals[sg.start + j] & 0x7FFFFFFFu].aux & SG_REF_NONE);
-                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
-                        if (key != NO_KEY) thread_count_add(S, cfg, res, pg.tc_epoch, key, -1, bflags);
-                    }
+                    const uint64_t ref = r.code == RC_NONE ? SG_REF_NONE
+                                         : r.code == RC_BATCH ? S.gbase + (vals[r.x] & 0x7FFFFFFFu) : (aux & SG_REF_NONE);
+                    lane_exit<NRMAX>(N, C, S, cfg, pg, res, t, r, x, ref, bflags);
                 } else {
                     stat_trace(N, C, t, r.cnt);
                 }
@@ -1341,7 +1468,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                 uint32_t fend = 0;
                 bool skipped = false;
                 // ---- skip: a long stretch is not streamed through this CU.  Its end is found by a
-                // block-wide search over event times, its ENTRY counts come from per-block sums (k_gather),
+                // block-wide search over event times, its ENTRY counts come from per-block sums (k_block_sums),
                 // its effective EXIT/TRACEs are the same-batch EXIT/TRACEs of the passes this owner
                 // committed (pending list + forward links) plus the few that count without a link
                 // (streamed), and k_fill writes its verdicts after the decide kernels.
@@ -1396,7 +1523,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                                 S.spans[sbase + c] = sp;
                             }
                             // (3) ENTRY counts and link-free EXIT/TRACEs: edge blocks and flagged blocks are
-                            // streamed, the other whole blocks contribute their k_gather count sums
+                            // streamed, the other whole blocks contribute their k_block_sums count sums
                             auto stat_ev = [&](uint32_t p) {
                                 const uint4 r = reinterpret_cast<const uint4*>(recs)[p];
                                 const uint32_t ek = r.w & 0xFFu, ec = r.z & 0xFFFFu, ert = r.z >> 16;
@@ -2003,23 +2130,15 @@ namespace sg {
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg) {
-    static const bool fused = [] { const char* v = std::getenv("SG_SEG_FUSED"); return !(v && v[0] == '0'); }();
-    if (fused) {  // flag/pos are scratch of >= n words: tile counts in flag, their offsets in pos
-        const uint32_t nt = (uint32_t)((n + SEG_TILE - 1) / SEG_TILE);
-        hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag);
-        hipError_t e = scan(flag, pos, nt, part, nseg, st);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs);
-        return hipGetLastError();
-    }
-    uint32_t nb = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_seg_flags, dim3(nb), dim3(256), 0, st, keys, n, flag);
-    hipError_t e = scan(flag, pos, n, part, nseg, st);
+    // flag/pos are scratch of >= n words: tile counts in flag, their offsets in pos
+    const uint32_t nt = (uint32_t)((n + SEG_TILE - 1) / SEG_TILE);
+    hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag);
+    hipError_t e = scan(flag, pos, nt, part, nseg, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seg_start, dim3(nb), dim3(256), 0, st, keys, n, flag, pos, segs);
+    hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs);
     return hipGetLastError();
 }
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint8_t* prio, uint32_t lane_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint32_t* prio, uint32_t lane_max,
                           uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st) {
     if (!m) return hipSuccess;
@@ -2036,25 +2155,18 @@ hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t
     hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(64), 0, st, off, nblk ? nblk : 1, m, bin_off);
     return hipGetLastError();
 }
-hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst, uint32_t epoch, uint32_t* bflags,
-                         hipStream_t st) {
+hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
+                         const uint32_t* pos_of, SEv* recs, uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst,
+                         uint32_t epoch, uint32_t* bflags, hipStream_t st) {
     uint32_t nb = (uint32_t)((n + 255) / 256);
     hipError_t e = hipMemsetAsync(bst, 0, ((n + 1023) / 1024) * 4, st);
     if (e != hipSuccess) return e;
-    // scatter by default (C4 on MI355X: group stage 2.97 -> 2.76 ms standalone); SG_GATHER=1: gather
-    static const bool scatter = [] { const char* v = std::getenv("SG_GATHER"); return !(v && v[0] == '1'); }();
-    if (scatter) {
-        hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
-                           epoch, bflags);
-        hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst, link, epoch,
-                           bflags);
-        hipLaunchKernelGGL(k_link_verify, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, link, epoch,
-                           bflags);
-    } else {
-        hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, st, rec_o, vals, n, pos_of, recs, prev, nprev, link, bst,
-                           epoch, bflags);
-    }
+    hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
+                       epoch, bflags);
+    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst, link, epoch,
+                       bflags);
+    hipLaunchKernelGGL(k_link_verify, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, skeys, n, link,
+                       epoch, bflags);
     return hipGetLastError();
 }
 hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,
@@ -2075,10 +2187,10 @@ hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, 
 }
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
                         uint32_t grant_all, uint32_t* ncand, uint64_t* cand, const sg_event* ev, const Prog* prog,
-                        hipStream_t st) {
+                        const sg_event_ext* ext, uint32_t max_ctx, hipStream_t st) {
     if (!m) return hipSuccess;
     hipLaunchKernelGGL(k_chain, dim3((m + 255) / 256), dim3(256), 0, st, recs, vals, segs, m, info, grant_all, ncand,
-                       cand, ev, prog);
+                       cand, ev, prog, ext, max_ctx);
     return hipGetLastError();
 }
 // bin = BIN_J16 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16

@@ -12,7 +12,10 @@
 //   uint8   ring[2^k]     status of every ENTRY by global event index (EXIT/TRACE references)
 // All counters are int64 exactly as the Java LongAdders; RT sums are int64.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "../../include/sentinel_gpu.h"
 
 namespace sg {
 
@@ -35,9 +38,17 @@ enum : uint32_t {
     NI_CHAIN = 1u,       // CtSph chainMap holds this resource (and its ClusterNode exists)
     NI_REJECTED = 2u,    // lookProcessChain returned null once the cap was reached
     NI_PM = 4u,          // ParamFlowSlot.metricsMap has a ParameterMetric for it
-    NI_TM0 = 8u,         // ... with a thread-count map for paramIdx 0
     NI_TOUCHED = 32u,    // ClusterBuilderSlot created its ClusterNode (an ENTRY with a chain was processed);
                          // kept exact for resources in a STRATEGY_RELATE component (ClusterBuilderSlot.getClusterNode)
+    NI_TM_SHIFT = 6u     // bit NI_TM_SHIFT + i: ParameterMetric has a thread-count map for paramIdx i (i < SG_MAX_ARGS)
+};
+__host__ __device__ inline uint32_t ni_tm(uint32_t idx) { return 1u << (NI_TM_SHIFT + idx); }
+
+// sticky per-resource event marks (DevState.prio), set by the group stage: any mark sends the resource's
+// segments to the per-lane kernel
+enum : uint8_t {
+    PM_PRIO = 1,         // a prioritized ENTRY was seen: the second window's borrow ring is live
+    PM_LANE = 2          // an event only k_lane implements was seen: SG_F_BLOCKED_UPSTREAM, a NullContext
 };
 
 struct NodeInfo {
@@ -53,7 +64,6 @@ static_assert(sizeof(NodeInfo) == 32, "NodeInfo must be 32 B");
 enum : uint8_t {
     PF_EXC_COUNT = 1,   // has an EXCEPTION_COUNT breaker (minute exception running sum)
     PF_WARM = 2,        // has a WarmUp / WarmUpRateLimiter controller
-    PF_PARAM_IDX0 = 4,  // has a param rule on args[0]
     PF_SERIAL = 8,      // outside the cooperative (Jacobi) kernels' limits: per-lane serial kernel only
     PF_RL = 16,         // has a RateLimiter / WarmUpRateLimiter controller
     PF_RT = 32,         // has an RT breaker
@@ -66,17 +76,26 @@ struct Prog {
     uint32_t rule_off;
     uint8_t n_param, n_flow, n_degrade, pflags;
     uint32_t tc_epoch;   // epoch of this resource's param thread-count keys
-    uint32_t multi;      // representative of a STRATEGY_RELATE component (its members share one segment)
+    uint32_t multi;      // PX_* bits
+};
+enum : uint32_t {
+    PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)
+    PX_ORIGIN = 2,       // a flow rule reads an origin StatisticNode (limitApp = an origin / "other", DIRECT):
+                         // the resource keeps its origin nodes (ClusterNode.getOrCreateOriginNode)
+    PX_CHAIN = 4         // a STRATEGY_CHAIN rule reads the DefaultNode of its context: the resource keeps the
+                         // DefaultNodes of the contexts its CHAIN rules name (NodeSelectorSlot)
 };
 static_assert(sizeof(Prog) == 16, "Prog must be 16 B");
 
 enum : uint8_t { RK_PARAM = 0, RK_FLOW = 1, RK_DEGRADE = 2 };
 
-// compiled rule (host: engine.cpp compile_*)
+// compiled rule (host: engine.cpp upload_rules)
+enum : uint32_t { LA_DEFAULT = 0, LA_ORIGIN = 1, LA_OTHER = 2 };  // FlowRule.limitApp kinds
+#define NO_ID 0xFFFFFFFFu
 struct DRule {
     uint8_t kind;
     uint8_t grade;       // flow/param: FLOW_GRADE_*; degrade: DEGRADE_GRADE_*
-    uint8_t behavior;    // CONTROL_BEHAVIOR_* (flow, param)
+    uint8_t behavior;    // CONTROL_BEHAVIOR_* (flow, param); param: PB_INIT_ONLY = initialised, never checked
     uint8_t slot;        // index in the resource's full compiled list of this kind (decision rule_slot)
     int32_t max_queue;   // maxQueueingTimeMs
     double count;
@@ -92,9 +111,16 @@ struct DRule {
     uint32_t hot_off, hot_n;   // hot items
     uint32_t psid;       // param state id (ParameterMetric maps keyed by rule equality)
     uint32_t ref;        // flow STRATEGY_RELATE: the resource whose ClusterNode is checked (NO_REF: none)
+    int32_t param_idx;   // param: ParamFlowRule.paramIdx as loaded (< 0: resolved on first use, RState.a)
+    uint32_t la_kind;    // flow: LA_* of limitApp
+    uint32_t la_origin;  // flow: origin id of the limitApp string (NO_ID: never interned)
+    uint32_t strategy;   // flow: STRATEGY_*
+    uint32_t chain_ctx;  // flow STRATEGY_CHAIN: context id of refResource (NO_ID: never interned)
+    uint32_t pad[3];
 };
 #define NO_REF 0xFFFFFFFFu
-static_assert(sizeof(DRule) == 80, "DRule must be 80 B");
+#define PB_INIT_ONLY 0xFF
+static_assert(sizeof(DRule) == 112, "DRule must be 112 B");
 
 struct DHot {
     uint64_t key;
@@ -119,7 +145,7 @@ struct PSlot {
 };
 
 enum : uint8_t { ST_PASS = 0, ST_PASS_WAIT = 1, ST_BLOCK_FLOW = 2, ST_BLOCK_DEGRADE = 3, ST_BLOCK_PARAM = 4,
-                 ST_NO_CHECK = 5, ST_NOT_ENTRY = 0xFF };
+                 ST_NO_CHECK = 5, ST_BLOCK_UPSTREAM = 6, ST_NOT_ENTRY = 0xFF };
 
 struct DevCfg {
     int32_t max_rt;
@@ -208,10 +234,27 @@ struct Span {
 #define BST_STATIC 0x80000000u  // bst[] flag: the block holds an EXIT/TRACE that is effective without a link
 #define BST_CNT 0x7FFFFFFFu
 
+// Origin StatisticNodes and context DefaultNodes of the resources that read them (PX_ORIGIN / PX_CHAIN):
+// a pool of nodes and an open-addressing index keyed (resource, kind, id)
+struct AuxNode {
+    Bkt sec[2];
+    Bkt minb[60];
+    int64_t borrow[4];   // FutureBucketLeapArray {ws, pass} x 2 (prioritized entries on this node)
+    NodeInfo info;       // thread; flags bit 0 = borrow ring live
+};
+static_assert(sizeof(AuxNode) == 4032, "AuxNode size");
+#define AUX_EMPTY 0xFFFFFFFFFFFFFFFFull
+enum : uint32_t { AUX_ORIGIN = 0, AUX_CONTEXT = 1 };
+struct AuxSlot {
+    unsigned long long key;  // res << 32 | kind << 31 | id; AUX_EMPTY = free (claimed by CAS)
+    uint32_t idx;            // pool index, NO_ID until the claimer published it
+    uint32_t pad;
+};
+
 struct DevState {
     Bkt* sec;
     int64_t* borrow;          // [res][2 slots] x {ws, pass}: FutureBucketLeapArray of the second window
-    const uint8_t* prio;      // [res] sticky: a prioritized ENTRY was seen, the borrow ring is live (k_lane only)
+    const uint32_t* prio;     // [res] sticky PM_* marks of the group stage (PM_PRIO: the borrow ring is live)
     uint64_t* key_ring;       // arg key of every ENTRY by global event index (ring like the status ring),
                               // NO_KEY if it had none; null until param rules exist
     uint64_t gbase;           // global index of the batch's first event
@@ -235,10 +278,21 @@ struct DevState {
     uint32_t epoch;           // tag of this batch's links
     uint32_t skip_ok;         // 0: no skipping this batch (links not unique / zero-count ENTRYs / SG_DEBUG_FLAGS & 4)
     uint32_t skip_min;        // a stretch is skipped only if it holds more positions than this (SG_SKIP_MIN)
+    // sg_submit_ex: per-event context and args (null: none), origin / context nodes
+    const sg_event_ext* ext;  // [submission index]
+    const sg_arg* args;
+    AuxSlot* aux_tab;
+    AuxNode* aux_pool;
+    uint32_t* aux_count;      // nodes taken from the pool
+    uint32_t aux_cap;
+    uint32_t max_ctx;         // context ids above this are NullContexts
+    uint64_t aux_mask;
 };
 
 enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
                   BF_BACKWARD = 32, BF_TSPAN = 64,
+                  BF_BAD_ARGS = 512,    // an sg_event_ext names args outside the table, or more than SG_MAX_ARGS
+                  BF_AUX_FULL = 1024,   // the origin / context node pool is full
                   BF_MULTI_LINK = 128,  // an ENTRY is referenced by two EXITs (or two TRACEs) of the batch
                   BF_ZERO_CNT = 256 };  // an ENTRY acquires 0 (it may pass inside a saturated stretch)
 

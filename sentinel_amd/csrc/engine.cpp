@@ -25,8 +25,9 @@ namespace sg {
 // kernels.hip
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
-                           uint64_t* key_ring, const uint32_t* comp, int db, hipStream_t st);
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint32_t* prio,
+                           uint64_t* key_ring, const uint32_t* comp, const sg_event_ext* ext, const sg_arg* args,
+                           uint64_t n_args, uint32_t max_ctx, int db, hipStream_t st);
 // db = digit bits (8 or 10)
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks, hipStream_t st,
                              int db = 8);
@@ -43,14 +44,14 @@ hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hip
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint8_t* prio, uint32_t lane_max,
+hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint32_t* prio, uint32_t lane_max,
                           uint32_t j1_max,
                           uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st);
 hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
                             hipStream_t st);
-hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, uint64_t n, const uint32_t* pos_of, SEv* recs,
-                         uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst, uint32_t epoch, uint32_t* bflags,
-                         hipStream_t st);
+hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
+                         const uint32_t* pos_of, SEv* recs, uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst,
+                         uint32_t epoch, uint32_t* bflags, hipStream_t st);
 hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,
                        const DRule* rules, uint32_t* dec, hipStream_t st);
 hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st);
@@ -58,7 +59,7 @@ hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, 
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
                         uint32_t grant_all, uint32_t* ncand, uint64_t* cand, const sg_event* ev, const Prog* prog,
-                        hipStream_t st);
+                        const sg_event_ext* ext, uint32_t max_ctx, hipStream_t st);
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st);
@@ -448,6 +449,9 @@ struct sg_engine {
         uint64_t* d_cand = nullptr;
         uint32_t* d_bsmall = nullptr;  // [0] bflags [1] nseg [2] ncand [3] nprev [4..5] t0 [8..8+N_BINS] bin offsets
                                        // [120] frozen spans recorded
+        sg_event_ext* d_ext = nullptr; // sg_submit_ex host inputs staged in HBM
+        sg_arg* d_args = nullptr;
+        uint64_t ext_cap = 0, args_cap = 0;
         Link* d_link = nullptr;        // frozen-stretch skipping side tables (DevState.link/bst/pend/spans)
         uint32_t *d_bst = nullptr, *d_pend = nullptr;
         Span* d_spans = nullptr;
@@ -458,7 +462,15 @@ struct sg_engine {
     int last = -1;               // slot of the last batch submitted
     hipStream_t gstream = nullptr;
     std::vector<std::array<double, 4>> tlog;  // per batch [group, decide, post, total] ms, by collect()
-    uint8_t* d_prio = nullptr;   // [res] sticky prioritized-ENTRY mark (DevState.prio)
+    uint32_t* d_prio = nullptr;  // [res] sticky PM_* marks (DevState.prio)
+    // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
+    AuxSlot* d_auxtab = nullptr;
+    AuxNode* d_auxpool = nullptr;
+    uint32_t* d_auxcnt = nullptr;
+    uint64_t aux_mask = 0;
+    // ContextUtil names: origins (0 = "") and contexts (0 = sentinel_default_context), first-intern order
+    std::unordered_map<std::string, uint32_t> origin_ids, context_ids;
+    std::unordered_map<std::string, int> rule_names;  // limitApp / CHAIN ref strings the flow rules name
     uint32_t* d_comp = nullptr;  // [res] STRATEGY_RELATE component representative (sort key); null: none
     uint32_t* d_prev = nullptr;
     uint32_t* d_bsmall = nullptr;
@@ -495,7 +507,6 @@ struct sg_engine {
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
-    int radix_db = 0;           // radix digit bits (0: 8; SG_RADIX_DB=8|10)
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -546,7 +557,8 @@ static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_hist); dfree(B.d_part); dfree(B.d_flag); dfree(B.d_pos); dfree(B.d_order); dfree(B.d_segs);
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
     dfree(B.d_prev); dfree(B.d_bsmall);
-    dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans);
+    dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans); dfree(B.d_ext); dfree(B.d_args);
+    B.ext_cap = B.args_cap = 0;
     B.d_link = nullptr; B.d_bst = B.d_pend = nullptr; B.d_spans = nullptr;
     B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
     B.d_hist = B.d_part = B.d_flag = B.d_pos = B.d_order = nullptr;
@@ -622,6 +634,7 @@ static int collect(sg_engine* e, int k) {
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
+    if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
     return SG_OK;
 }
 // every batch in flight done (called by the API functions that read or write engine state)
@@ -637,7 +650,7 @@ static int drain(sg_engine* e) {
 
 
 // Build the device rule program of every resource from the compiled host lists.
-int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
+int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool reset_par_state) {
     uint32_t R = e->cfg.max_resources;
     std::vector<Prog> prog(R);
     std::vector<DRule> rules;
@@ -646,7 +659,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
     // previous rule states to carry over when a kind was not reloaded
     std::vector<RState> old_rst;
     std::vector<Prog> old_prog;
-    if ((!reset_flow_state || !reset_deg_state) && e->n_dev_rules) {
+    if ((!reset_flow_state || !reset_deg_state || !reset_par_state) && e->n_dev_rules) {
         old_rst.resize(e->n_dev_rules);
         old_prog.resize(R);
         HIPCHK(hipMemcpy(old_rst.data(), e->d_rstate, e->n_dev_rules * sizeof(RState), hipMemcpyDeviceToHost));
@@ -660,18 +673,18 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
         std::memset(&p, 0, sizeof(p));
         p.rule_off = (uint32_t)rules.size();
         p.tc_epoch = e->tc_epoch[r];
-        // param rules: HashSet order; only paramIdx 0 can see an argument (events carry args[0])
+        // param rules: HashSet order (ParamFlowSlot.checkFlow iterates them, ParamFlowSlot.java:84-100)
         const auto& pl = r < e->res_par.size() ? e->res_par[r] : std::vector<int>();
         for (size_t i = 0; i < pl.size(); ++i) {
             const ParamR& q = e->params[pl[i]];
-            if (q.r.param_idx == 0) p.pflags |= PF_PARAM_IDX0;
-            if (q.r.param_idx != 0) continue; // args.length (<= 1) <= paramIdx -> always passes
-            if (q.r.cluster_mode && q.r.grade == SG_FLOW_GRADE_QPS && !q.r.cluster_fallback_to_local) continue;
             DRule d;
             std::memset(&d, 0, sizeof(d));
             d.kind = RK_PARAM;
             d.grade = (uint8_t)q.r.grade;
             d.behavior = (uint8_t)q.r.control_behavior;
+            // cluster mode + QPS without fallback: passClusterCheck finds no TokenService in this process and
+            // passes -- the rule's metric is still initialised (ParamFlowSlot.initHotParamMetricsFor)
+            if (q.r.cluster_mode && q.r.grade == SG_FLOW_GRADE_QPS && !q.r.cluster_fallback_to_local) d.behavior = PB_INIT_ONLY;
             d.slot = (uint8_t)i;
             d.max_queue = q.r.max_queueing_time_ms;
             d.count = q.r.count;
@@ -684,27 +697,17 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
             d.hot_n = (uint32_t)q.hot.size();
             for (auto& h : q.hot) hot.push_back(DHot{h.first, h.second, 0});
             d.psid = e->psid_of[q.res + std::string("\0", 1) + q.eqkey];
+            d.param_idx = q.r.param_idx;
+            d.ref = NO_REF;
             rules.push_back(d);
-            rst.push_back(RState{0, 0, 0, 0});
+            rst.push_back(RState{0, 0, 0, 0});  // a: paramIdx resolved by applyRealParamIdx + 1 (0 = not yet)
             p.n_param++;
         }
-        if (!pl.empty() && p.n_param == 0) { // metric still created (ParamFlowSlot.initHotParamMetricsFor)
-            DRule d;
-            std::memset(&d, 0, sizeof(d));
-            d.kind = RK_PARAM;
-            d.grade = 0xFF; // never blocks
-            d.psid = 0;
-            rules.push_back(d);
-            rst.push_back(RState{0, 0, 0, 0});
-            p.n_param = 1;
-        }
-        // flow rules: FlowRuleComparator order; the default context without an origin selects
-        // the ClusterNode for limitApp "default" + DIRECT (FlowRuleChecker.java:90-124)
+        // flow rules: FlowRuleComparator order; limitApp and strategy pick the node each rule checks
+        // (FlowRuleChecker.selectNodeByRequesterAndStrategy, FlowRuleChecker.java:90-124)
         const auto& fl = r < e->res_flow.size() ? e->res_flow[r] : std::vector<int>();
         for (size_t i = 0; i < fl.size(); ++i) {
             const FlowR& f = e->flows[fl[i]];
-            if (f.la != "default") continue;  // origin "" never matches / isOtherOrigin("") == false
-            if (f.r.strategy == SG_STRATEGY_CHAIN && f.ref != "sentinel_default_context") continue;
             if (f.r.cluster_mode && !f.r.cluster_fallback_to_local) continue; // no TokenService -> pass
             DRule d;
             std::memset(&d, 0, sizeof(d));
@@ -716,11 +719,26 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
             d.max_queue = f.r.max_queueing_time_ms;
             d.count = f.r.count;
             d.ref = NO_REF;
+            d.la_kind = f.la == "default" ? LA_DEFAULT : f.la == "other" ? LA_OTHER : LA_ORIGIN;
+            auto oi = e->origin_ids.find(f.la);
+            d.la_origin = oi == e->origin_ids.end() ? NO_ID : oi->second;
+            d.strategy = (uint32_t)f.r.strategy;
+            d.chain_ctx = NO_ID;
             if (f.r.strategy == SG_STRATEGY_RELATE) {  // another resource's ClusterNode (same node if itself)
                 auto it = e->ids.find(f.ref);
                 const uint32_t b = it == e->ids.end() ? NO_REF : it->second;
                 if (b != NO_REF && b != (uint32_t)r && b < R) { d.ref = b; relate.emplace_back((uint32_t)r, b); }
+            } else if (f.r.strategy == SG_STRATEGY_CHAIN) {  // the DefaultNode of the context named refResource
+                if (f.ref == "sentinel_default_context") d.chain_ctx = 0;
+                else {
+                    auto ci = e->context_ids.find(f.ref);
+                    if (ci != e->context_ids.end()) d.chain_ctx = ci->second;
+                }
+                p.multi |= PX_CHAIN;
             }
+            if (d.la_kind != LA_DEFAULT && f.r.strategy == SG_STRATEGY_DIRECT) p.multi |= PX_ORIGIN;
+            if (d.la_kind != LA_DEFAULT || f.r.strategy == SG_STRATEGY_CHAIN || f.r.strategy > SG_STRATEGY_CHAIN)
+                p.pflags |= PF_SERIAL;  // node selection beyond the ClusterNode: the per-lane kernel
             if (d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP || d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) {
                 // WarmUpController.construct (WarmUpController.java:100-117)
                 int cold = e->cfg.cold_factor;
@@ -768,7 +786,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
                 if (b == SG_CONTROL_BEHAVIOR_RATE_LIMITER || b == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) ++n_rl;
             }
             if (n_rl) p.pflags |= PF_RL;
-            if (p.n_param || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2) p.pflags |= PF_SERIAL;
+            if (p.n_param || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2 || p.multi) p.pflags |= PF_SERIAL;
             bool all_default_qps = true;
             for (int i = 0; i < p.n_flow; ++i) {
                 const DRule& d = rules[p.rule_off + p.n_param + i];
@@ -780,6 +798,8 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
         // carry controller / breaker state of kinds that were not reloaded
         if (!old_rst.empty()) {
             const Prog& op = old_prog[r];
+            if (!reset_par_state && op.n_param == p.n_param)
+                for (int i = 0; i < p.n_param; ++i) rst[p.rule_off + i] = old_rst[op.rule_off + i];
             if (!reset_flow_state && op.n_flow == p.n_flow)
                 for (int i = 0; i < p.n_flow; ++i) rst[p.rule_off + p.n_param + i] = old_rst[op.rule_off + op.n_param + i];
             if (!reset_deg_state && op.n_degrade == p.n_degrade)
@@ -806,7 +826,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state) {
         std::sort(members.begin(), members.end());
         members.erase(std::unique(members.begin(), members.end()), members.end());
         for (uint32_t x : members) {
-            if (comp[x] == x) { prog[x].multi = 1; prog[x].pflags |= PF_SERIAL; }
+            if (comp[x] == x) { prog[x].multi |= PX_MULTI; prog[x].pflags |= PF_SERIAL; }
         }
         // ClusterNode existence of the members from here on: NI_TOUCHED (a chain grant means an ENTRY of
         // the resource was decided in a finished batch: no batch is in flight during a rule load)
@@ -888,6 +908,7 @@ void sg_config_default(sg_config* c) {
     c->cluster_exceed_count = 1.0;
     c->cluster_max_occupy_ratio = 1.0;
     c->cluster_max_allowed_qps = 30000;
+    c->aux_node_capacity = 65536;
 }
 
 int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
@@ -944,12 +965,24 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
         hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
         hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess ||
-        hipMalloc(&e->d_prio, R) != hipSuccess)
+        hipMalloc(&e->d_prio, R * 4) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
+    {   // origin / context node pool + its index (2 slots per node, power of two)
+        const uint64_t cap = std::max<uint32_t>(cfg.aux_node_capacity, 16u);
+        uint64_t slots = 32;
+        while (slots < 2 * cap) slots <<= 1;
+        e->aux_mask = slots - 1;
+        e->cfg.aux_node_capacity = (uint32_t)cap;
+        if (hipMalloc(&e->d_auxtab, slots * sizeof(AuxSlot)) != hipSuccess ||
+            hipMalloc(&e->d_auxpool, cap * sizeof(AuxNode)) != hipSuccess || hipMalloc(&e->d_auxcnt, 4) != hipSuccess ||
+            hipMemsetAsync(e->d_auxtab, 0xFF, slots * sizeof(AuxSlot), e->stream) != hipSuccess ||
+            hipMemsetAsync(e->d_auxcnt, 0, 4, e->stream) != hipSuccess)
+            return bad(fail(SG_ENOMEM, "device allocation of the origin/context node pool failed"));
+    }
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_prio, 0, R, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_prio, 0, R * 4, e->stream) != hipSuccess ||
         launch_init_state(e->d_sec, e->d_minb, e->d_info, e->d_borrow, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
@@ -967,7 +1000,6 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J4_MAX")) e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
-    if (const char* v = std::getenv("SG_RADIX_DB")) e->radix_db = std::atoi(v) == 10 ? 10 : std::atoi(v) == 8 ? 8 : 0;
     if (const char* v = std::getenv("SG_SKIP_MIN")) e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
     *out = e;
     return SG_OK;
@@ -1017,7 +1049,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
-    dfree(e->d_prio); dfree(e->d_comp);
+    dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt);
     dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
@@ -1215,7 +1247,12 @@ int sg_load_flow_rules(sg_engine* e, const sg_flow_rule* rules, uint32_t n, uint
     e->flows = std::move(flows);
     e->res_flow = std::move(per);
     resize_lists(e, e->res_flow);
-    int rc = upload_rules(e, true, false);
+    e->rule_names.clear();  // the origin / context names the flow rules read (sg_intern_* recompiles on first sight)
+    for (auto& f : e->flows) {
+        e->rule_names["o\x01" + f.la] = 1;
+        if (f.r.strategy == SG_STRATEGY_CHAIN) e->rule_names["c\x01" + f.ref] = 1;
+    }
+    int rc = upload_rules(e, true, false, false);
     if (rc) { e->flows = std::move(old_flows); e->res_flow = std::move(old_per); return rc; }
     e->last_flow = keys;
     e->flow_loaded = true;
@@ -1267,7 +1304,7 @@ int sg_load_degrade_rules(sg_engine* e, const sg_degrade_rule* rules, uint32_t n
     e->degs = std::move(degs);
     e->res_deg = std::move(per);
     resize_lists(e, e->res_deg);
-    int rc = upload_rules(e, false, true);
+    int rc = upload_rules(e, false, true, false);
     if (rc) { e->degs = std::move(od); e->res_deg = std::move(op); return rc; }
     e->last_deg = keys;
     e->deg_loaded = true;
@@ -1377,13 +1414,14 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     std::vector<std::string> keys;
     for (uint32_t i = 0; i < n; ++i) {
         if (rules[i].n_items > 0 && !rules[i].items) return fail(SG_EINVAL, "param rule items pointer is null");
-        if (rules[i].has_param_idx && rules[i].param_idx < 0)
-            return fail(SG_ENOTSUP, "negative paramIdx is rewritten per call (ParamFlowSlot.applyRealParamIdx); "
-                                    "not on the device path yet");
         all.push_back(make_param(rules[i]));
         keys.push_back(all.back().eqkey);
     }
-    if (e->par_loaded && keys == e->last_par) {
+    // a negative paramIdx is rewritten in the loaded rule objects (ParamFlowSlot.applyRealParamIdx), so the
+    // property's equality check never matches the list that created them: such a list always reloads
+    bool neg = false;
+    for (uint32_t i = 0; i < n; ++i) neg |= rules[i].has_param_idx && rules[i].param_idx < 0;
+    if (e->par_loaded && keys == e->last_par && !neg) {
         if (n_loaded) *n_loaded = (uint32_t)e->params.size();
         return SG_OK;
     }
@@ -1421,7 +1459,7 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
                     it = e->psid_of.erase(it);
                 else ++it;
             }
-            clear_flags.push_back(((uint64_t)(NI_PM | NI_TM0) << 32) | r);
+            clear_flags.push_back(((uint64_t)(NI_PM | (((1u << SG_MAX_ARGS) - 1) << NI_TM_SHIFT)) << 32) | r);
         }
     }
     for (auto& q : ps) {
@@ -1433,7 +1471,7 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     e->params = std::move(ps);
     e->res_par = std::move(per);
     resize_lists(e, e->res_par);
-    int rc = upload_rules(e, false, false);
+    int rc = upload_rules(e, false, false, true);
     if (rc) { e->params = std::move(op); e->res_par = std::move(opr); return rc; }
     if (!clear_flags.empty()) {
         uint64_t* d = nullptr;
@@ -1464,8 +1502,10 @@ static bool is_device_ptr(const void* p) {
 // the host waits for it only; the decide stage (reference resolution, chain grants, decide kernels,
 // post) is enqueued on stream behind the previous batch's and the call returns.  So batch k+1's
 // group stage overlaps batch k's decide stage.  Buffers must stay valid until sg_sync.
-int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                       uint64_t n_args, uint32_t* out) {
     if (!e || (n && (!ev || !out))) return fail(SG_EINVAL, "null argument");
+    if (n_args && !args) return fail(SG_EINVAL, "null args table");
     if (n == 0) return SG_OK;
     if (n > e->cfg.max_batch_events || n >= (1ull << 31)) return fail(SG_EINVAL, "batch larger than max_batch_events");
     HIPCHK(hipSetDevice(e->device));
@@ -1485,6 +1525,27 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         dev_ev = e->d_ev;
     }
     uint32_t* dev_out = host_out ? e->d_out : out;
+    // sg_submit_ex: the Context and args tables in HBM (staged per batch slot when the caller's are host memory)
+    const sg_event_ext* dev_ext = ext;
+    const sg_arg* dev_args = n_args ? args : nullptr;
+    if (ext && !is_device_ptr(ext)) {
+        if (n > B.ext_cap) {
+            dfree(B.d_ext);
+            B.ext_cap = std::max<uint64_t>(n, 1u << 16);
+            HIPCHK(hipMalloc(&B.d_ext, B.ext_cap * sizeof(sg_event_ext)));
+        }
+        HIPCHK(hipMemcpyAsync(B.d_ext, ext, n * sizeof(sg_event_ext), hipMemcpyHostToDevice, gs));
+        dev_ext = B.d_ext;
+    }
+    if (n_args && !is_device_ptr(args)) {
+        if (n_args > B.args_cap) {
+            dfree(B.d_args);
+            B.args_cap = std::max<uint64_t>(n_args, 1u << 16);
+            HIPCHK(hipMalloc(&B.d_args, B.args_cap * sizeof(sg_arg)));
+        }
+        HIPCHK(hipMemcpyAsync(B.d_args, args, n_args * sizeof(sg_arg), hipMemcpyHostToDevice, gs));
+        dev_args = B.d_args;
+    }
     const uint64_t ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
     // Overlapping this group stage with the previous batch's decide stage wins once the decide kernels
     // no longer stream frozen stretches through single CUs (C4 on MI355X: 6.45 -> 5.45 ms per batch);
@@ -1498,14 +1559,15 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     while (bits < 32 && (1ull << bits) < R) ++bits;
     // 8-bit digits: measured faster than two 10-bit passes for 1M resources on MI355X (group stage
     // 2.99 vs 3.11 ms standalone; 1024 digit runs per 4096-item tile average 4 items, too short to
-    // write coalesced).  SG_RADIX_DB=10 selects 10-bit digits.
-    const int db = e->radix_db ? e->radix_db : 8;
+    // write coalesced).
+    const int db = 8;
     int passes = (bits + db - 1) / db;
     uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
     HIPCHK(hipMemsetAsync(e->d_bsmall, 0, 256 * 4, gs));
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, e->d_comp, db, gs));
+                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, e->d_comp, dev_ext,
+                           dev_args, n_args, SG_MAX_CONTEXTS, db, gs));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
         if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * db, e->d_hist, nblocks, gs, db));
@@ -1518,7 +1580,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     // ---- 2. segments + 16-byte sorted records
     HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, gs, launch_scan, e->d_part, e->d_bsmall + 1));
     if (++e->epoch == 0) e->epoch = 1;
-    HIPCHK(launch_gather(e->d_rec_o, vin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link, e->d_bst,
+    HIPCHK(launch_gather(e->d_rec_o, vin, kin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link, e->d_bst,
                          e->epoch, e->d_bsmall + 0, gs));
     uint32_t head[6];
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
@@ -1533,6 +1595,8 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
         return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
     if (bflags & BF_TSPAN) return fail(SG_EINVAL, "a batch must span less than 2^31 ms");
     if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
+    if (bflags & BF_BAD_ARGS)
+        return fail(SG_EINVAL, "an sg_event_ext names args outside the table (or more than SG_MAX_ARGS, or a bad kind)");
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
     const uint32_t nblk = (m + 255) / 256;
@@ -1553,7 +1617,7 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
         HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand,
-                            dev_ev, e->d_prog, st));
+                            dev_ev, e->d_prog, dev_ext, SG_MAX_CONTEXTS, st));
         if (!grant_all) {
             uint32_t ncand = 0;
             HIPCHK(hipMemcpyAsync(&ncand, e->d_bsmall + 2, 4, hipMemcpyDeviceToHost, st));
@@ -1614,6 +1678,14 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     S.epoch = e->epoch;
     S.skip_ok = !(bflags & (BF_MULTI_LINK | BF_ZERO_CNT)) && !(e->dbg_flags & 4) ? 1u : 0u;
     S.skip_min = e->skip_min;
+    S.ext = dev_ext;
+    S.args = dev_args;
+    S.aux_tab = e->d_auxtab;
+    S.aux_pool = e->d_auxpool;
+    S.aux_count = e->d_auxcnt;
+    S.aux_cap = e->cfg.aux_node_capacity;
+    S.aux_mask = e->aux_mask;
+    S.max_ctx = SG_MAX_CONTEXTS;
     HIPCHK(hipEventRecord(e->fork, st));
     const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
     for (int c = 0; c < 3; ++c) {
@@ -1655,6 +1727,59 @@ int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out)
     e->last = k;
     e->cur = k ^ 1;
     e->gbase += n;
+    return SG_OK;
+}
+
+int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+    return submit_impl(e, ev, nullptr, n, nullptr, 0, out);
+}
+
+int sg_submit_ex_async(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                       uint64_t n_args, uint32_t* out) {
+    return submit_impl(e, ev, ext, n, args, n_args, out);
+}
+
+int sg_submit_ex(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                 uint64_t n_args, uint32_t* out) {
+    int rc = submit_impl(e, ev, ext, n, args, n_args, out);
+    if (rc) {
+        if (e) (void)drain(e);
+        return rc;
+    }
+    return sg_sync(e);
+}
+
+// ContextUtil.enter(name, origin) names (core/context/ContextUtil.java:118-166).  A flow rule naming an origin
+// (limitApp) or a context (STRATEGY_CHAIN refResource) before it was interned was compiled to match nothing;
+// the first intern of such a name recompiles the rule programs, keeping every controller / breaker state.
+int sg_intern_origin(sg_engine* e, const char* origin, uint32_t* out_id) {
+    if (!e || !out_id) return fail(SG_EINVAL, "null argument");
+    if (!origin || !*origin) { *out_id = 0; return SG_OK; }
+    auto it = e->origin_ids.find(origin);
+    if (it != e->origin_ids.end()) { *out_id = it->second; return SG_OK; }
+    const uint32_t id = (uint32_t)e->origin_ids.size() + 1;
+    if (id >= 0x7FFFFFFFu) return fail(SG_ECAPACITY, "too many origins");
+    e->origin_ids.emplace(origin, id);
+    *out_id = id;
+    if (e->rule_names.count(std::string("o\x01") + origin)) {
+        if (int rc = drain(e)) return rc;
+        return upload_rules(e, false, false, false);
+    }
+    return SG_OK;
+}
+
+int sg_intern_context(sg_engine* e, const char* context, uint32_t* out_id) {
+    if (!e || !out_id) return fail(SG_EINVAL, "null argument");
+    if (!context || !*context || !std::strcmp(context, "sentinel_default_context")) { *out_id = 0; return SG_OK; }
+    auto it = e->context_ids.find(context);
+    if (it != e->context_ids.end()) { *out_id = it->second; return SG_OK; }
+    const uint32_t id = (uint32_t)e->context_ids.size() + 1;
+    e->context_ids.emplace(context, id);
+    *out_id = id;
+    if (e->rule_names.count(std::string("c\x01") + context)) {
+        if (int rc = drain(e)) return rc;
+        return upload_rules(e, false, false, false);
+    }
     return SG_OK;
 }
 

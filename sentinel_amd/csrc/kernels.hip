@@ -57,8 +57,11 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                       uint32_t* __restrict__ ghist, uint32_t nblocks,
                                                       uint32_t* __restrict__ bflags, int64_t* __restrict__ t0_out,
-                                                      uint8_t* __restrict__ prio, uint64_t* __restrict__ key_ring,
-                                                      const uint32_t* __restrict__ comp) {
+                                                      uint32_t* __restrict__ prio, uint64_t* __restrict__ key_ring,
+                                                      const uint32_t* __restrict__ comp,
+                                                      const sg_event_ext* __restrict__ ext,
+                                                      const sg_arg* __restrict__ args, uint64_t n_args,
+                                                      uint32_t max_ctx) {
     constexpr int NB = 1 << DB;
     __shared__ uint32_t h[NB];
     for (int i = threadIdx.x; i < NB; i += RS_THREADS) h[i] = 0;
@@ -87,12 +90,32 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         r.flags = e.flags;
         r.code = RC_NONE;
         r.pad = 0;
+        uint32_t mark = 0;  // PM_* marks for the resource
+        uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+        if (ext) {  // sg_submit_ex: validate the event's args; a NullContext event is k_lane's
+            const sg_event_ext x = ext[i];
+            if (x.n_args > SG_MAX_ARGS || (uint64_t)x.arg_off + x.n_args > n_args) fl |= BF_BAD_ARGS;
+            else if (x.n_args) {
+                for (uint32_t k = 0; k < x.n_args; ++k) {
+                    const sg_arg a = args[x.arg_off + k];
+                    if (a.kind > SG_ARG_LIST || (a.kind == SG_ARG_LIST && (a.key > n_args || a.len > n_args - a.key)))
+                        fl |= BF_BAD_ARGS;
+                    else if (a.kind == SG_ARG_LIST)
+                        for (uint32_t q = 0; q < a.len; ++q)
+                            if (args[a.key + q].kind > SG_ARG_SCALAR) fl |= BF_BAD_ARGS;
+                }
+                const sg_arg a0 = args[x.arg_off];
+                key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+            }
+            if (x.context_id > max_ctx) mark |= PM_LANE;
+        }
         if (e.kind == SG_EV_ENTRY) {
             // the arg an exit(count, args) of this ENTRY will decrement (ParamFlowStatisticExitCallback)
-            if (key_ring) key_ring[(gbase + i) & ring_mask] = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
-            // a prioritized ENTRY makes the resource's borrow ring live: its segments go to k_lane (a
-            // separate byte array: this stage may run while the previous batch's decide stores NodeInfo)
-            if ((e.flags & SG_F_PRIORITIZED) && e.res_id < max_res && !prio[e.res_id]) prio[e.res_id] = 1;
+            if (key_ring) key_ring[(gbase + i) & ring_mask] = key0;
+            // a prioritized ENTRY makes the resource's borrow ring live; an upstream block is k_lane's (a
+            // separate mark array: this stage may run while the previous batch's decide stores NodeInfo)
+            if (e.flags & SG_F_PRIORITIZED) mark |= PM_PRIO;
+            if (e.flags & SG_F_BLOCKED_UPSTREAM) mark |= PM_LANE;
         } else {
             if (e.kind == SG_EV_EXIT) {
                 const int64_t raw = (int64_t)(e.aux >> 48);
@@ -101,9 +124,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             const uint64_t ref = e.aux & SG_REF_NONE;
             if (ref != SG_REF_NONE) {
                 if (ref >= gbase) {
-                    // an EXIT/TRACE must follow its ENTRY and name an event of its own resource (the
-                    // referenced record is a few RT milliseconds back: an L2 hit)
-                    if (ref - gbase >= i || ev[ref - gbase].res_id != e.res_id) fl |= BF_BAD_REF;
+                    // an EXIT/TRACE must follow its ENTRY (that the ENTRY is of its own resource is checked
+                    // after the sort, where the two sit a few positions apart: k_link_verify)
+                    if (ref - gbase >= i) fl |= BF_BAD_REF;
                     else { r.code = RC_BATCH; r.x = (uint32_t)(ref - gbase); }
                 } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve,
                           // after the earlier batches are decided (this stage overlaps the previous decide)
@@ -112,6 +135,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                 }
             }
         }
+        if (mark && e.res_id < max_res && (prio[e.res_id] & mark) != mark) atomicOr(&prio[e.res_id], mark);
         rec_o[i] = r;
         // sort key: the resource, or its STRATEGY_RELATE component's representative (one segment)
         const uint32_t key = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
@@ -419,14 +443,17 @@ namespace sg {
 
 hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, const uint8_t* ring,
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
-                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint8_t* prio,
-                           uint64_t* key_ring, const uint32_t* comp, int db, hipStream_t st) {
+                           uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint32_t* prio,
+                           uint64_t* key_ring, const uint32_t* comp, const sg_event_ext* ext, const sg_arg* args,
+                           uint64_t n_args, uint32_t max_ctx, int db, hipStream_t st) {
     if (db == 10)
         hipLaunchKernelGGL(k_rs_first<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
-                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
+                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp, ext, args,
+                           n_args, max_ctx);
     else
         hipLaunchKernelGGL(k_rs_first<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
-                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp);
+                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp, ext, args,
+                           n_args, max_ctx);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,

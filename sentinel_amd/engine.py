@@ -24,6 +24,7 @@ EXPORTS = (
     "sg_load_flow_rules", "sg_load_degrade_rules", "sg_load_param_rules", "sg_param_key", "sg_submit",
     "sg_submit_async", "sg_sync", "sg_snapshot_metrics", "sg_cluster_set_connected_count",
     "sg_cluster_request_tokens", "sg_cluster_request_param_tokens", "sg_read_node", "sg_last_error", "sg_last_timings",
+    "sg_submit_ex", "sg_submit_ex_async", "sg_intern_origin", "sg_intern_context",
 )
 
 
@@ -52,6 +53,10 @@ def lib():
         L.sg_submit.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
         L.sg_submit_async.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
         L.sg_sync.argtypes = [P]
+        L.sg_submit_ex.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_submit_ex_async.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_intern_origin.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
+        L.sg_intern_context.argtypes = [P, C.c_char_p, C.POINTER(C.c_uint32)]
         L.sg_snapshot_metrics.argtypes = [P, C.c_int64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.sg_cluster_set_connected_count.argtypes = [P, C.c_int64, C.c_int32]
         L.sg_cluster_request_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
@@ -148,6 +153,27 @@ class Engine:
         _check(lib().sg_submit(self.h, ev.ctypes.data, len(ev), out.ctypes.data))
         self.n_events += len(ev)
         return out
+
+    def submit_ex(self, events: np.ndarray, ext: np.ndarray = None, args: np.ndarray = None) -> np.ndarray:
+        """sg_submit_ex: ext = A.EXT_DTYPE per event (or None), args = A.ARG_DTYPE table (see A.ext_tables)."""
+        ev = np.ascontiguousarray(events, dtype=A.EVENT_DTYPE)
+        ex = None if ext is None else np.ascontiguousarray(ext, dtype=A.EXT_DTYPE)
+        ar = None if args is None or len(args) == 0 else np.ascontiguousarray(args, dtype=A.ARG_DTYPE)
+        out = np.zeros(len(ev), dtype=np.uint32)
+        _check(lib().sg_submit_ex(self.h, ev.ctypes.data, None if ex is None else ex.ctypes.data, len(ev),
+                                  None if ar is None else ar.ctypes.data, 0 if ar is None else len(ar), out.ctypes.data))
+        self.n_events += len(ev)
+        return out
+
+    def intern_origin(self, name: str) -> int:
+        out = C.c_uint32()
+        _check(lib().sg_intern_origin(self.h, name.encode(), C.byref(out)))
+        return out.value
+
+    def intern_context(self, name: str) -> int:
+        out = C.c_uint32()
+        _check(lib().sg_intern_context(self.h, name.encode(), C.byref(out)))
+        return out.value
 
     def submit_ptr(self, ev_ptr: int, n: int, out_ptr: int, sync: bool = True):
         """Device (or host) pointers, e.g. torch tensors' data_ptr()."""

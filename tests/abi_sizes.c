@@ -18,5 +18,8 @@ int main(void) {
     printf("ev.aux %zu\n", offsetof(sg_event, aux));
     printf("cfg.cluster_exceed_count %zu\n", offsetof(sg_config, cluster_exceed_count));
     printf("param.items %zu\n", offsetof(sg_param_rule, items));
+    printf("cfg.aux_node_capacity %zu\n", offsetof(sg_config, aux_node_capacity));
+    printf("sg_event_ext %zu\n", sizeof(sg_event_ext));
+    printf("sg_arg %zu\n", sizeof(sg_arg));
     return 0;
 }

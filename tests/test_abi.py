@@ -56,6 +56,8 @@ def test_struct_layouts_match_header(tmp_path):
     assert got["ev.aux"] == A.EVENT_DTYPE.fields["aux"][1]
     assert got["cfg.cluster_exceed_count"] == A.SgConfig.cluster_exceed_count.offset
     assert got["param.items"] == A.SgParamRule.items.offset
+    assert got["cfg.aux_node_capacity"] == A.SgConfig.aux_node_capacity.offset
+    assert got["sg_event_ext"] == A.EXT_DTYPE.itemsize and got["sg_arg"] == A.ARG_DTYPE.itemsize
 
 
 def test_config_defaults_are_the_reference_defaults():

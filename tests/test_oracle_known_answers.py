@@ -564,3 +564,75 @@ def test_cluster_avg_local_threshold():
     assert o.cluster_set_connected(7, 3) == 0
     st = [s for s, _, _ in o.cluster_request([(t, 7, 1, False)] * 7)]
     assert st == [A.TOKEN_OK] * 6 + [A.TOKEN_BLOCKED]
+
+
+# ---------------------------------------------------------------- args: collections, arrays, negative index
+def _param_oracle(res, **rule):
+    o = O.Oracle()
+    rid = o.register(res)
+    o.load_param_rules([A.param_rule(res, **rule)])
+    return o, rid
+
+
+def test_param_pass_local_check_for_collection():
+    # param-test/slots/block/flow/param/ParamFlowCheckerTest.java:149-166: threshold 1, list [a, B, Cc]:
+    # the first check consumes every element's token, the second blocks on the first element
+    o, rid = _param_oracle("testPassLocalCheckForCollection", param_idx=0, count=1)
+    lst = [O.param_key("a"), O.param_key("B"), O.param_key("Cc")]
+    assert o.entry(T0, rid, args=[lst])[0] & 0xFF == A.PASS
+    assert o.entry(T0, rid, args=[lst])[0] & 0xFF == A.BLOCK_PARAM
+
+
+def test_param_pass_local_check_for_array():
+    # ParamFlowCheckerTest.java:169-188: RATE_LIMITER, threshold 1, array [a, B, Cc] -> pass, then block
+    o, rid = _param_oracle("testPassLocalCheckForArray", param_idx=0, count=1,
+                           control_behavior=A.CONTROL_BEHAVIOR_RATE_LIMITER)
+    arr = [O.param_key("a"), O.param_key("B"), O.param_key("Cc")]
+    assert o.entry(T0, rid, args=[arr])[0] & 0xFF == A.PASS
+    assert o.entry(T0, rid, args=[arr])[0] & 0xFF == A.BLOCK_PARAM
+
+
+def test_param_negative_index():
+    # param-test/slots/block/flow/param/ParamFlowSlotTest.java:52-77: paramIdx -1 with 3 args resolves to 2,
+    # -100 to 100 (past the args: always passes); the rule object keeps the resolved index
+    o, rid = _param_oracle("testNegativeParamIdx", param_idx=-1, count=1)
+    k = [O.param_key(v) for v in ("abc", "def", "ghi", "xyz")]
+    assert o.entry(T0, rid, args=[k[0], k[1], k[2]])[0] & 0xFF == A.PASS
+    assert o.entry(T0, rid, args=[k[3], k[3], k[2]])[0] & 0xFF == A.BLOCK_PARAM  # args[2] = "ghi" again
+    assert o.entry(T0, rid, args=[k[2], k[2], k[3]])[0] & 0xFF == A.PASS         # "xyz" is new
+    # resolved once: a 2-arg call still checks index 2 (absent -> pass)
+    assert o.entry(T0, rid, args=[k[2], k[2]])[0] & 0xFF == A.PASS
+    o2, rid2 = _param_oracle("testNegativeParamIdx", param_idx=-100, count=1)
+    for _ in range(3):
+        assert o2.entry(T0, rid2, args=[k[0], k[1], k[2]])[0] & 0xFF == A.PASS
+
+
+def test_param_collection_with_null_element():
+    # ParamFlowChecker.passLocalCheck (ParamFlowChecker.java:73-99): a null element makes the map lookup throw;
+    # the Throwable is caught and the check passes -- elements before it have consumed their tokens
+    o, rid = _param_oracle("nullElem", param_idx=0, count=1)
+    a, b = O.param_key("a"), O.param_key("b")
+    assert o.entry(T0, rid, args=[[a, None, b]])[0] & 0xFF == A.PASS
+    assert o.entry(T0, rid, args=[[a, None, b]])[0] & 0xFF == A.BLOCK_PARAM  # a is spent
+    assert o.entry(T0, rid, args=[[b]])[0] & 0xFF == A.PASS                  # b was never checked
+
+
+def test_upstream_block_after_param_before_flow():
+    # HotParamSlotChainBuilder (param/slots/HotParamSlotChainBuilder.java:38-51): ParamFlowSlot runs before the
+    # System/Authority slots, FlowSlot after them; StatisticSlot counts the block (StatisticSlot.java:97-117)
+    o = O.Oracle()
+    rid = o.register("up")
+    o.load_param_rules([A.param_rule("up", 0, 2)])
+    o.load_flow_rules([A.flow_rule("up", 100)])
+    k = O.param_key("v")
+    ev = A.np.zeros(4, dtype=A.EVENT_DTYPE)
+    ev["ts"] = T0
+    ev["res_id"] = rid
+    ev["count"] = 1
+    ev["kind"] = A.EV_ENTRY
+    ev["flags"] = [A.F_HAS_ARG | A.F_BLOCKED_UPSTREAM, A.F_HAS_ARG, A.F_HAS_ARG | A.F_BLOCKED_UPSTREAM, A.F_HAS_ARG]
+    ev["aux"] = k
+    d = o.submit(ev) & 0xFF
+    # the upstream-blocked entry still spends a param token; the third is a param block (it comes first)
+    assert list(d) == [A.BLOCK_UPSTREAM, A.PASS, A.BLOCK_PARAM, A.BLOCK_PARAM]
+    assert o.read_node(rid)["second"][:, 2].sum() == 3 and o.read_node(rid)["second"][:, 1].sum() == 1
