@@ -682,12 +682,16 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
         if (s < nr && status == ST_PASS) {
             const DRule r = rules[s];
             if (s < np) {  // ParamFlowSlot.checkFlow (ParamFlowSlot.java:77-101)
+                N.flags |= NI_PM;  // initHotParamMetricsFor -> ParameterMetric.initialize
+                if (r.behavior == PB_INIT_ONLY && r.param_idx >= 0) {  // maps of a run of never-checked rules
+                    N.flags |= (uint32_t)r.burst << NI_TM_SHIFT;
+                    continue;
+                }
                 int idx = r.param_idx;
                 if (idx < 0) {  // applyRealParamIdx mutates the rule once (RState.a = resolved index + 1)
                     if (rs[s].a == 0) rs[s].a = 1 + ((-idx <= (int)x.n) ? (int)x.n + idx : -idx);
                     idx = (int)rs[s].a - 1;
                 }
-                N.flags |= NI_PM;  // initHotParamMetricsFor -> ParameterMetric.initialize
                 if (idx < SG_MAX_ARGS) N.flags |= ni_tm((uint32_t)idx);
                 if (r.behavior == PB_INIT_ONLY || idx >= (int)x.n) continue;
                 const sg_arg v = evx_arg(x, (uint32_t)idx);

@@ -684,11 +684,21 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             d.behavior = (uint8_t)q.r.control_behavior;
             // cluster mode + QPS without fallback: passClusterCheck finds no TokenService in this process and
             // passes -- the rule's metric is still initialised (ParamFlowSlot.initHotParamMetricsFor)
-            if (q.r.cluster_mode && q.r.grade == SG_FLOW_GRADE_QPS && !q.r.cluster_fallback_to_local) d.behavior = PB_INIT_ONLY;
+            if (q.r.cluster_mode && q.r.grade == SG_FLOW_GRADE_QPS && !q.r.cluster_fallback_to_local) {
+                d.behavior = PB_INIT_ONLY;
+                // a run of such rules with fixed indices is one pseudo-rule: the set of maps it initialises
+                if (q.r.param_idx >= 0 && p.n_param && rules.back().behavior == PB_INIT_ONLY &&
+                    rules.back().param_idx >= 0) {
+                    if (q.r.param_idx < SG_MAX_ARGS) rules.back().burst |= (int32_t)(1u << q.r.param_idx);
+                    continue;
+                }
+            }
             d.slot = (uint8_t)i;
             d.max_queue = q.r.max_queueing_time_ms;
             d.count = q.r.count;
             d.burst = q.r.burst_count;
+            if (d.behavior == PB_INIT_ONLY && q.r.param_idx >= 0)  // the pseudo-rule's map set
+                d.burst = q.r.param_idx < SG_MAX_ARGS ? (int32_t)(1u << q.r.param_idx) : 0;
             double c = q.r.count;
             d.token_count = (c != c) ? 0 : c >= 2147483647.0 ? INT32_MAX : (int32_t)c;
             d.token_count_l = (c != c) ? 0 : c >= 9.2e18 ? INT64_MAX : (int64_t)c;
