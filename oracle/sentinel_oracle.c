@@ -115,8 +115,8 @@ static char* str_dup(const char* s) {
 typedef struct {
     uint64_t* keys;
     int64_t* vals;
-    uint8_t* used;
-    uint64_t cap, n;
+    uint8_t* used;          /* 0 empty, 1 live, 2 tombstone */
+    uint64_t cap, n, tomb;
 } u64map;
 
 static uint64_t mix64(uint64_t x) {
@@ -124,7 +124,6 @@ static uint64_t mix64(uint64_t x) {
     x ^= x >> 27; x *= 0x94d049bb133111ebULL;
     x ^= x >> 31; return x;
 }
-static void m_init(u64map* m) { memset(m, 0, sizeof(*m)); }
 static void m_free(u64map* m) { free(m->keys); free(m->vals); free(m->used); memset(m, 0, sizeof(*m)); }
 static int64_t* m_find(u64map* m, uint64_t k) {
     if (!m->cap) return NULL;
@@ -135,9 +134,10 @@ static int64_t* m_find(u64map* m, uint64_t k) {
     }
     return NULL;
 }
-static void m_grow(u64map* m);
+static void m_rehash(u64map* m, uint64_t cap);
 static int64_t* m_put(u64map* m, uint64_t k, int64_t v) { /* insert or overwrite */
-    if ((m->n + 1) * 2 > m->cap) m_grow(m);
+    if ((m->n + m->tomb + 1) * 2 > m->cap) /* live + tombstones at most half: probes always end */
+        m_rehash(m, (m->n + 1) * 4 > m->cap ? (m->cap ? m->cap * 2 : 16) : m->cap);
     uint64_t i = mix64(k) & (m->cap - 1);
     while (m->used[i] == 1) {
         if (m->keys[i] == k) { m->vals[i] = v; return &m->vals[i]; }
@@ -149,6 +149,7 @@ static int64_t* m_put(u64map* m, uint64_t k, int64_t v) { /* insert or overwrite
         if (m->used[j] == 1 && m->keys[j] == k) { m->vals[j] = v; return &m->vals[j]; }
         j = (j + 1) & (m->cap - 1);
     }
+    if (m->used[i] == 2) m->tomb--;
     m->used[i] = 1; m->keys[i] = k; m->vals[i] = v; m->n++;
     return &m->vals[i];
 }
@@ -156,20 +157,102 @@ static void m_del(u64map* m, uint64_t k) {
     if (!m->cap) return;
     uint64_t i = mix64(k) & (m->cap - 1);
     while (m->used[i]) {
-        if (m->used[i] == 1 && m->keys[i] == k) { m->used[i] = 2; m->n--; return; }
+        if (m->used[i] == 1 && m->keys[i] == k) { m->used[i] = 2; m->n--; m->tomb++; return; }
         i = (i + 1) & (m->cap - 1);
     }
 }
-static void m_grow(u64map* m) {
+static void m_rehash(u64map* m, uint64_t cap) {
     u64map o = *m;
-    m->cap = o.cap ? o.cap * 2 : 16;
+    m->cap = cap;
     m->keys = (uint64_t*)calloc(m->cap, 8);
     m->vals = (int64_t*)calloc(m->cap, 8);
     m->used = (uint8_t*)calloc(m->cap, 1);
     m->n = 0;
+    m->tomb = 0;
     for (uint64_t i = 0; i < o.cap; ++i)
         if (o.used[i] == 1) m_put(m, o.keys[i], o.vals[i]);
     free(o.keys); free(o.vals); free(o.used);
+}
+
+/* ======================================================================= */
+/* CacheMap: ConcurrentLinkedHashMapWrapper(capacity) as ParameterMetric    */
+/* uses it (param/.../ParameterMetric.java:37-114).  Access order = LRU:     */
+/* get and putIfAbsent of a present key move it to the most-recently-used    */
+/* end; an insert beyond the capacity evicts the least recently used entry   */
+/* (ConcurrentLinkedHashMap's eviction deque, exact for one caller thread).  */
+/* The library itself is not in /root/reference: restated, parity unpinned  */
+/* (SURVEY Q13).                                                            */
+/* ======================================================================= */
+typedef struct {
+    u64map idx;               /* key -> node */
+    uint64_t* key;
+    int64_t* val;
+    int64_t *prev, *next;     /* -1 at the ends */
+    int64_t head, tail;       /* head = most recently used */
+    int64_t n_nodes, cap_nodes, free_head;
+    uint64_t n, cap;          /* live entries, maximum */
+} lrumap;
+
+static void lm_init(lrumap* m, uint64_t cap) { memset(m, 0, sizeof(*m)); m->head = m->tail = m->free_head = -1; m->cap = cap; }
+static void lm_free(lrumap* m) {
+    m_free(&m->idx); free(m->key); free(m->val); free(m->prev); free(m->next);
+    memset(m, 0, sizeof(*m)); m->head = m->tail = m->free_head = -1;
+}
+static void lm_unlink(lrumap* m, int64_t i) {
+    if (m->prev[i] >= 0) m->next[m->prev[i]] = m->next[i]; else m->head = m->next[i];
+    if (m->next[i] >= 0) m->prev[m->next[i]] = m->prev[i]; else m->tail = m->prev[i];
+}
+static void lm_front(lrumap* m, int64_t i) {
+    m->prev[i] = -1; m->next[i] = m->head;
+    if (m->head >= 0) m->prev[m->head] = i; else m->tail = i;
+    m->head = i;
+}
+static int64_t lm_node(lrumap* m, uint64_t k) {
+    int64_t* p = m_find(&m->idx, k);
+    return p ? *p : -1;
+}
+static void lm_drop(lrumap* m, int64_t i) {
+    lm_unlink(m, i);
+    m_del(&m->idx, m->key[i]);
+    m->next[i] = m->free_head; m->free_head = i;
+    m->n--;
+}
+/* CacheMap.get: the value (touched) or NULL */
+static int64_t* lm_get(lrumap* m, uint64_t k) {
+    int64_t i = lm_node(m, k);
+    if (i < 0) return NULL;
+    if (m->head != i) { lm_unlink(m, i); lm_front(m, i); }
+    return &m->val[i];
+}
+/* CacheMap.putIfAbsent: the present value (touched), or inserts v (*inserted = 1) and evicts beyond capacity */
+static int64_t* lm_put_absent(lrumap* m, uint64_t k, int64_t v, int* inserted) {
+    int64_t* p = lm_get(m, k);
+    if (inserted) *inserted = p == NULL;
+    if (p) return p;
+    int64_t i = m->free_head;
+    if (i >= 0) m->free_head = m->next[i];
+    else {
+        if (m->n_nodes == m->cap_nodes) {
+            m->cap_nodes = m->cap_nodes ? m->cap_nodes * 2 : 16;
+            m->key = (uint64_t*)realloc(m->key, 8 * (size_t)m->cap_nodes);
+            m->val = (int64_t*)realloc(m->val, 8 * (size_t)m->cap_nodes);
+            m->prev = (int64_t*)realloc(m->prev, 8 * (size_t)m->cap_nodes);
+            m->next = (int64_t*)realloc(m->next, 8 * (size_t)m->cap_nodes);
+        }
+        i = m->n_nodes++;
+    }
+    m->key[i] = k; m->val[i] = v;
+    m_put(&m->idx, k, i);
+    lm_front(m, i);
+    m->n++;
+    while (m->n > m->cap && m->tail >= 0 && m->tail != i) lm_drop(m, m->tail);
+    return &m->val[i];
+}
+/* CacheMap.put: insert or overwrite (touched) */
+static void lm_put(lrumap* m, uint64_t k, int64_t v) { *lm_put_absent(m, k, v, NULL) = v; }
+static void lm_remove(lrumap* m, uint64_t k) {
+    int64_t i = lm_node(m, k);
+    if (i >= 0) lm_drop(m, i);
 }
 
 /* string interning: name -> dense id */
@@ -565,13 +648,13 @@ typedef struct {
 /* per-(resource, rule) param state: ParameterMetric keeps maps keyed by rule *equality* */
 typedef struct {
     oparam rule;             /* a copy used for equality only */
-    u64map time_map;         /* ruleTimeCounters[rule] */
-    u64map token_map;        /* ruleTokenCounter[rule] */
+    lrumap time_map;         /* ruleTimeCounters[rule] */
+    lrumap token_map;        /* ruleTokenCounter[rule] */
 } oparam_state;
 
 typedef struct {
     int32_t idx;
-    u64map map;              /* threadCountMap[paramIdx] */
+    lrumap map;              /* threadCountMap[paramIdx] */
 } othread_map;
 
 typedef struct {
@@ -896,10 +979,10 @@ static void res_free(ores* r) {
     free(r->defs); free(r->origins);
     free(r->flow); free(r->degrade); free(r->param);
     for (int i = 0; i < r->pm.n_st; ++i) {
-        m_free(&r->pm.st[i].time_map); m_free(&r->pm.st[i].token_map);
+        lm_free(&r->pm.st[i].time_map); lm_free(&r->pm.st[i].token_map);
         free_param(&r->pm.st[i].rule);
     }
-    for (int i = 0; i < r->pm.n_tm; ++i) m_free(&r->pm.tm[i].map);
+    for (int i = 0; i < r->pm.n_tm; ++i) lm_free(&r->pm.tm[i].map);
     free(r->pm.st); free(r->pm.tm);
 }
 
@@ -1243,8 +1326,8 @@ static void copy_param(oparam* d, const sg_param_rule* s) {
 }
 
 static void pm_clear(oparam_metric* pm) { /* ParameterMetric removed from ParamFlowSlot.metricsMap */
-    for (int i = 0; i < pm->n_st; ++i) { m_free(&pm->st[i].time_map); m_free(&pm->st[i].token_map); free_param(&pm->st[i].rule); }
-    for (int i = 0; i < pm->n_tm; ++i) m_free(&pm->tm[i].map);
+    for (int i = 0; i < pm->n_st; ++i) { lm_free(&pm->st[i].time_map); lm_free(&pm->st[i].token_map); free_param(&pm->st[i].rule); }
+    for (int i = 0; i < pm->n_tm; ++i) lm_free(&pm->tm[i].map);
     free(pm->st); free(pm->tm);
     memset(pm, 0, sizeof(*pm));
 }
@@ -1500,7 +1583,7 @@ static oparam_state* pm_state(oparam_metric* pm, const oparam* rule) {
     for (int i = 0; i < pm->n_st; ++i) if (param_equals(&pm->st[i].rule, rule)) return &pm->st[i];
     return NULL;
 }
-static u64map* pm_thread_map(oparam_metric* pm, int32_t idx) {
+static lrumap* pm_thread_map(oparam_metric* pm, int32_t idx) {
     for (int i = 0; i < pm->n_tm; ++i) if (pm->tm[i].idx == idx) return &pm->tm[i].map;
     return NULL;
 }
@@ -1515,6 +1598,11 @@ static void pm_initialize(oparam_metric* pm, const oparam* rule) { /* ParameterM
         memset(s, 0, sizeof(*s));
         copy_param(&s->rule, &rule->r);
         s->rule.r.param_idx = rule->r.param_idx;
+        /* Math.min(BASE_PARAM_MAX_CAPACITY * durationInSec, TOTAL_MAX_CAPACITY) (ParameterMetric.java:91,100) */
+        int64_t cap = 4000 * rule->r.duration_in_sec;
+        if (cap > 200000) cap = 200000;
+        lm_init(&s->time_map, (uint64_t)cap);
+        lm_init(&s->token_map, (uint64_t)cap);
     }
     if (!pm_thread_map(pm, rule->r.param_idx)) {
         if (pm->n_tm == pm->cap_tm) {
@@ -1523,13 +1611,13 @@ static void pm_initialize(oparam_metric* pm, const oparam* rule) { /* ParameterM
         }
         othread_map* t = &pm->tm[pm->n_tm++];
         t->idx = rule->r.param_idx;
-        m_init(&t->map);
+        lm_init(&t->map, 4000);  /* THREAD_COUNT_MAX_CAPACITY (ParameterMetric.java:37) */
     }
 }
 static int64_t pm_thread_count(oparam_metric* pm, int32_t idx, uint64_t v) {
-    u64map* m = pm_thread_map(pm, idx);
+    lrumap* m = pm_thread_map(pm, idx);
     if (!m) return 0;
-    int64_t* p = m_find(m, v);
+    int64_t* p = lm_get(m, v);
     return p ? *p : 0;
 }
 static const ohot* hot_find(const oparam* p, uint64_t v) {
@@ -1547,18 +1635,17 @@ static int param_default_check(oparam_metric* pm, oparam* rule, int acquire, uin
     if (token_count == 0) return 0;
     int32_t max_count = j_iadd(token_count, rule->r.burst_count);
     if (acquire > max_count) return 0;
-    int64_t* last = m_find(&s->time_map, v);
-    if (!last) {
-        m_put(&s->time_map, v, now);
-        if (!m_find(&s->token_map, v)) m_put(&s->token_map, v, j_iadd(max_count, -acquire));
+    int ins;
+    int64_t* last = lm_put_absent(&s->time_map, v, now, &ins);  /* timeCounters.putIfAbsent(value, now) */
+    if (ins) {
+        lm_put_absent(&s->token_map, v, j_iadd(max_count, -acquire), NULL);
         return 1;
     }
     int64_t pass_time = now - *last;
     if (pass_time > rule->r.duration_in_sec * 1000) {
-        int64_t* old = m_find(&s->token_map, v);
-        if (!old) {
-            m_put(&s->token_map, v, j_iadd(max_count, -acquire));
-            *m_find(&s->time_map, v) = now;
+        int64_t* old = lm_put_absent(&s->token_map, v, j_iadd(max_count, -acquire), &ins);
+        if (ins) {
+            *last = now;
             return 1;
         }
         int32_t rest = (int32_t)*old;
@@ -1567,16 +1654,17 @@ static int param_default_check(oparam_metric* pm, oparam* rule, int acquire, uin
         int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
         if (nq < 0) return 0;
         *old = nq;
-        *m_find(&s->time_map, v) = now;
+        *last = now;
         return 1;
     }
-    int64_t* old = m_find(&s->token_map, v);
+    int64_t* old = lm_get(&s->token_map, v);
     if (old) {
         int32_t ov = (int32_t)*old;
         if (j_iadd(ov, -acquire) >= 0) { *old = j_iadd(ov, -acquire); return 1; }
         return 0;
     }
-    return 1; /* unreachable with exact maps (the Java loop would spin) */
+    return 1; /* unreachable: both maps see the same key sequence, so they hold the same keys (the Java loop
+                 would spin until the window passes) */
 }
 /* ParamFlowChecker.passThrottleLocalCheck (ParamFlowChecker.java:198-248) */
 static int param_throttle_check(oparam_metric* pm, oparam* rule, int acquire, uint64_t v, int64_t now, int64_t* wait_ms) {
@@ -1587,8 +1675,9 @@ static int param_throttle_check(oparam_metric* pm, oparam* rule, int acquire, ui
     if (h) token_count = h->count;
     if (token_count == 0) return 0;
     int64_t cost = j_round(1.0 * 1000 * acquire * (double)rule->r.duration_in_sec / (double)token_count);
-    int64_t* rec = m_find(&s->time_map, v);
-    if (!rec) { m_put(&s->time_map, v, now); return 1; }
+    int ins;
+    int64_t* rec = lm_put_absent(&s->time_map, v, now, &ins);  /* timeRecorderMap.putIfAbsent(value, now) */
+    if (ins) return 1;
     int64_t last = *rec;
     int64_t expected = last + cost;
     if (expected <= now || expected - now < rule->r.max_queueing_time_ms) {
@@ -1649,20 +1738,19 @@ static int param_pass_check(oparam_metric* pm, oparam* rule, int acquire, const 
 /* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241): every index
  * with a thread-count map; a null element throws inside the try around the whole loop, so the
  * remaining elements and indices are skipped. */
-static void pm_thread_one(u64map* m, uint64_t v, int add) {
-    int64_t* p = m_find(m, v);
+static void pm_thread_one(lrumap* m, uint64_t v, int add) {
+    int ins;
+    int64_t* p = lm_put_absent(m, v, 0, &ins);  /* putIfAbsent(value, new AtomicInteger()) */
     if (add) {
-        if (p) (*p)++;
-        else m_put(m, v, 1);
-    } else {
-        if (!p) { m_put(m, v, 0); return; } /* putIfAbsent(value, new AtomicInteger()) */
-        int64_t cur = --(*p);
-        if (cur <= 0) m_del(m, v);
+        if (ins) lm_put(m, v, 1);               /* put(value, new AtomicInteger(1)) */
+        else (*p)++;
+    } else if (!ins) {
+        if (--(*p) <= 0) lm_remove(m, v);
     }
 }
 static void pm_thread_args(oparam_metric* pm, const oargs* a, int add) {
     for (int i = 0; i < a->n; ++i) {
-        u64map* m = pm_thread_map(pm, i);
+        lrumap* m = pm_thread_map(pm, i);
         const sg_arg* v = &a->a[i];
         if (!m || v->kind == SG_ARG_NULL) continue;
         if (v->kind == SG_ARG_LIST) {
@@ -2044,7 +2132,7 @@ int or_snapshot_metrics(or_engine* e, int64_t now, sg_metric_node* out, uint64_t
 int or_param_set_thread_count(or_engine* e, uint32_t res, int32_t param_idx, uint64_t key, int64_t v) {
     if (!e || res >= e->n_res) return SG_EINVAL;
     oparam_metric* pm = &e->res[res].pm;
-    u64map* m = pm_thread_map(pm, param_idx);
+    lrumap* m = pm_thread_map(pm, param_idx);
     if (!m) {
         if (pm->n_tm == pm->cap_tm) {
             pm->cap_tm = pm->cap_tm ? pm->cap_tm * 2 : 4;
@@ -2052,10 +2140,10 @@ int or_param_set_thread_count(or_engine* e, uint32_t res, int32_t param_idx, uin
         }
         othread_map* t = &pm->tm[pm->n_tm++];
         t->idx = param_idx;
-        m_init(&t->map);
+        lm_init(&t->map, 4000);
         m = &t->map;
     }
-    m_put(m, key, v);
+    lm_put(m, key, v);
     return SG_OK;
 }
 

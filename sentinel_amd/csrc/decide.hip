@@ -383,36 +383,69 @@ __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict
 }
 
 // =================================================================================
-// ParamFlowChecker (param/slots/block/flow/param/ParamFlowChecker.java:101-248), lane-local.
-// Every (rule, value) key is owned by exactly one resource, i.e. by one lane at a time; only
-// probing crosses owners (insertion is a CAS on the key word).
+// ParameterMetric's bounded LRU maps (PMap, dev_types.h).  Every operation below is the CacheMap call the
+// reference makes, with ConcurrentLinkedHashMap's access order: get / putIfAbsent of a present key move it
+// to the MRU end, an insert into a full map evicts the LRU entry.  A map is private to its resource's lane.
 // =================================================================================
-__device__ PSlot* ptab_lookup(PSlot* tab, uint64_t mask, uint64_t khi, uint64_t kval, bool insert, bool* is_new,
-                              uint32_t* bflags) {
-    uint64_t h = mix64(khi * 0x9e3779b97f4a7c15ULL ^ kval) & mask;
-    *is_new = false;
-    for (uint32_t probe = 0; probe <= 4096; ++probe) {
-        PSlot* s = &tab[h];
-        uint64_t k = __hip_atomic_load(&s->khi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == khi && s->kval == kval) return s;
-        if (k == 0) {
-            if (!insert) return nullptr;
-            unsigned long long expect = 0;
-            if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s->khi, &expect, (unsigned long long)khi,
-                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                s->kval = kval;
-                s->v0 = 0;
-                s->v1 = 0;
-                *is_new = true;
-                return s;
-            }
-            // lost the race to another owner: this slot now holds a different key, keep probing
-        }
-        h = (h + 1) & mask;
-    }
-    atomicOr(bflags, BF_PTAB_FULL);
-    return nullptr;
+__device__ __forceinline__ uint32_t pm_home(const PMap& m, uint64_t v) {
+    return (uint32_t)(((mix64(v) >> 32) * (uint64_t)m.slots) >> 32);
 }
+__device__ __forceinline__ uint32_t pm_next(const PMap& m, uint32_t i) { return i + 1 == m.slots ? 0 : i + 1; }
+__device__ uint32_t pm_find(const PMap& m, const PSlot* R, uint64_t v) {
+    for (uint32_t i = pm_home(m, v);; i = pm_next(m, i)) {  // a region always has a free slot
+        if (!R[i].used) return PM_NIL;
+        if (R[i].kval == v) return i;
+    }
+}
+__device__ __forceinline__ void lru_unlink(PMap& m, PSlot* R, uint32_t i) {
+    const uint32_t p = R[i].prev, n = R[i].next;
+    if (p != PM_NIL) R[p].next = n; else m.head = n;
+    if (n != PM_NIL) R[n].prev = p; else m.tail = p;
+}
+__device__ __forceinline__ void lru_front(PMap& m, PSlot* R, uint32_t i) {
+    R[i].prev = PM_NIL;
+    R[i].next = m.head;
+    if (m.head != PM_NIL) R[m.head].prev = i; else m.tail = i;
+    m.head = i;
+}
+__device__ __forceinline__ void pm_touch(PMap& m, PSlot* R, uint32_t i) {
+    if (m.head != i) { lru_unlink(m, R, i); lru_front(m, R, i); }
+}
+// remove slot i: unlink it, then backward-shift the probe run behind it (linear probing keeps no tombstones)
+__device__ void pm_erase(PMap& m, PSlot* R, uint32_t i) {
+    lru_unlink(m, R, i);
+    m.count--;
+    for (uint32_t j = pm_next(m, i); R[j].used; j = pm_next(m, j)) {
+        const uint32_t k = pm_home(m, R[j].kval);
+        const bool move = i <= j ? (k <= i || k > j) : (k <= i && k > j);  // home not in (i, j] cyclically
+        if (!move) continue;
+        R[i] = R[j];
+        if (R[i].prev != PM_NIL) R[R[i].prev].next = i; else m.head = i;
+        if (R[i].next != PM_NIL) R[R[i].next].prev = i; else m.tail = i;
+        i = j;
+    }
+    R[i].used = 0;
+}
+// insert an absent key at the MRU end; a full map loses its LRU entry (CLHM evicts after the insert: same set)
+__device__ uint32_t pm_insert(PMap& m, PSlot* R, uint64_t v) {
+    if (m.count >= m.cap) pm_erase(m, R, m.tail);
+    uint32_t i = pm_home(m, v);
+    while (R[i].used) i = pm_next(m, i);
+    R[i].kval = v;
+    R[i].v0 = 0;
+    R[i].v1 = 0;
+    R[i].used = 1;
+    m.count++;
+    lru_front(m, R, i);
+    return i;
+}
+__device__ __forceinline__ void pm_store(const DevState& S, uint32_t id, const PMap& m) {
+    PMap* h = &S.pmap[id];
+    h->count = m.count;
+    h->head = m.head;
+    h->tail = m.tail;
+}
+
 __device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool* found) {
     for (uint32_t i = 0; i < r.hot_n; ++i) {
         DHot h = S.hot[r.hot_off + i];
@@ -421,75 +454,104 @@ __device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool
     *found = false;
     return 0;
 }
-// ParameterMetric thread-count map of paramIdx idx: key (2 << 62) | idx << 54 | epoch << 32 | res
-__device__ __forceinline__ uint64_t tc_key(uint32_t epoch, uint32_t res, uint32_t idx) {
-    return (2ULL << 62) | ((uint64_t)(idx & 0xFF) << 54) | ((uint64_t)(epoch & 0x3FFFFF) << 32) | res;
+__device__ __forceinline__ uint32_t tmap_of(const DevState& S, uint32_t tm_base, uint32_t idx) {
+    return tm_base == NO_ID || idx >= SG_MAX_ARGS ? NO_ID : S.tmid[tm_base + idx];
 }
-// ParameterMetric.getThreadCount (ParameterMetric.java:235-241)
-__device__ int64_t thread_count_get(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t idx,
-                                    uint64_t v, uint32_t* bflags) {
-    bool nw;
-    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res, idx), v, false, &nw, bflags);
-    return s ? s->v0 : 0;
+// ParameterMetric.getThreadCount (ParameterMetric.java:233-241): cacheMap.get(value)
+__device__ int64_t thread_count_get(const DevState& S, uint32_t tm_base, uint32_t idx, uint64_t v) {
+    const uint32_t id = tmap_of(S, tm_base, idx);
+    if (id == NO_ID) return 0;
+    PMap m = S.pmap[id];
+    PSlot* R = S.pslot + m.base;
+    const uint32_t i = pm_find(m, R, v);
+    if (i == PM_NIL) return 0;
+    pm_touch(m, R, i);
+    pm_store(S, id, m);
+    return R[i].v0;
 }
-__device__ void thread_count_add(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t idx,
-                                 uint64_t v, int64_t d, uint32_t* bflags) {
-    bool nw;
-    PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, tc_key(epoch, res, idx), v, true, &nw, bflags);
-    if (!s) return;
-    int64_t c = s->v0 + d;
-    if (d < 0 && nw) c = 0;  // putIfAbsent(value, new AtomicInteger()) without a decrement
-    s->v0 = c < 0 ? 0 : c;
+// addThreadCount / decreaseThreadCount of one value (ParameterMetric.java:117-231):
+//   add: putIfAbsent(v, 0) then increment, or put(v, 1) when it was absent;
+//   decrease: putIfAbsent(v, 0) -- an absent value stays at 0 -- else decrement, removed at <= 0
+__device__ void thread_count_add(const DevState& S, uint32_t tm_base, uint32_t idx, uint64_t v, int64_t d) {
+    const uint32_t id = tmap_of(S, tm_base, idx);
+    if (id == NO_ID) return;
+    PMap m = S.pmap[id];
+    PSlot* R = S.pslot + m.base;
+    uint32_t i = pm_find(m, R, v);
+    if (i == PM_NIL) {
+        i = pm_insert(m, R, v);
+        R[i].v0 = d > 0 ? 1 : 0;
+    } else {
+        pm_touch(m, R, i);
+        const int64_t c = R[i].v0 + (d > 0 ? 1 : -1);
+        if (c <= 0 && d < 0) pm_erase(m, R, i);
+        else R[i].v0 = c;
+    }
+    pm_store(S, id, m);
 }
 // ParamFlowChecker.passSingleValueCheck (ParamFlowChecker.java:101-119) of one value
-__device__ bool param_check(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, const DRule& r,
-                            uint32_t idx, int acquire, uint64_t v, int64_t t, int64_t& wait, uint32_t* bflags) {
+__device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r, uint32_t idx, int acquire, uint64_t v,
+                            int64_t t, int64_t& wait) {
     if (r.grade == SG_FLOW_GRADE_QPS) {
         bool hf;
         int32_t hc = hot_count(S, r, v, &hf);
-        uint64_t khi = (1ULL << 62) | r.psid;
         if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) {  // passThrottleLocalCheck (:198-248)
             int64_t token_count = hf ? (int64_t)hc : r.token_count_l;
             if (token_count == 0) return false;
             int64_t cost = j_round(1.0 * 1000 * acquire * (double)r.duration_sec / (double)token_count);
-            bool nw;
-            PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, khi, v, true, &nw, bflags);
-            if (!s) return true;
-            if (nw) { s->v0 = t; return true; }
-            int64_t expected = s->v0 + cost;
-            if (expected <= t || expected - t < r.max_queue) {
-                s->v0 = t;
-                int64_t w = expected - t;
-                if (w > 0) { s->v0 = expected; wait += w; }
-                return true;
+            PMap m = S.pmap[r.pmap];
+            PSlot* R = S.pslot + m.base;
+            uint32_t i = pm_find(m, R, v);  // timeRecorderMap.putIfAbsent(value, now)
+            bool ok = true;
+            if (i == PM_NIL) {
+                i = pm_insert(m, R, v);
+                R[i].v0 = t;
+            } else {
+                pm_touch(m, R, i);
+                const int64_t expected = R[i].v0 + cost;
+                if (expected <= t || expected - t < r.max_queue) {
+                    R[i].v0 = t;
+                    const int64_t w = expected - t;
+                    if (w > 0) { R[i].v0 = expected; wait += w; }
+                } else {
+                    ok = false;
+                }
             }
-            return false;
+            pm_store(S, r.pmap, m);
+            return ok;
         }
         // passDefaultLocalCheck (:121-196)
         int32_t token_count = hf ? hc : r.token_count;
         if (token_count == 0) return false;
         int32_t max_count = j_iadd(token_count, r.burst);
         if (acquire > max_count) return false;
-        bool nw;
-        PSlot* s = ptab_lookup(S.ptab, cfg.ptab_mask, khi, v, true, &nw, bflags);
-        if (!s) return true;
-        if (nw) { s->v0 = t; s->v1 = j_iadd(max_count, -acquire); return true; }
-        int64_t pass_time = t - s->v0;
-        if (pass_time > r.duration_sec * 1000) {
-            int32_t rest = (int32_t)s->v1;
-            int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
-            int32_t sum = j_iadd(rest, to_add);
-            int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
-            if (nq < 0) return false;
-            s->v1 = nq;
-            s->v0 = t;
-            return true;
+        PMap m = S.pmap[r.pmap];
+        PSlot* R = S.pslot + m.base;
+        uint32_t i = pm_find(m, R, v);  // timeCounters.putIfAbsent, then tokenCounters.putIfAbsent / get
+        bool ok = true;
+        if (i == PM_NIL) {
+            i = pm_insert(m, R, v);
+            R[i].v0 = t;
+            R[i].v1 = j_iadd(max_count, -acquire);
+        } else {
+            pm_touch(m, R, i);
+            const int64_t pass_time = t - R[i].v0;
+            if (pass_time > r.duration_sec * 1000) {
+                int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
+                int32_t sum = j_iadd(R[i].v1, to_add);
+                int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
+                if (nq < 0) ok = false;
+                else { R[i].v1 = nq; R[i].v0 = t; }
+            } else if (j_iadd(R[i].v1, -acquire) >= 0) {
+                R[i].v1 = j_iadd(R[i].v1, -acquire);
+            } else {
+                ok = false;
+            }
         }
-        int32_t ov = (int32_t)s->v1;
-        if (j_iadd(ov, -acquire) >= 0) { s->v1 = j_iadd(ov, -acquire); return true; }
-        return false;
+        pm_store(S, r.pmap, m);
+        return ok;
     } else if (r.grade == SG_FLOW_GRADE_THREAD) {
-        int64_t tc = thread_count_get(S, cfg, res, epoch, idx, v, bflags);
+        int64_t tc = thread_count_get(S, tm_base, idx, v);
         bool hf;
         int32_t hc = hot_count(S, r, v, &hf);
         if (hf) return ++tc <= hc;
@@ -527,8 +589,7 @@ __device__ __forceinline__ sg_arg evx_arg(const EvX& x, uint32_t i) {
 // ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241): every index with a
 // thread-count map; a null element of a Collection/array throws inside the try that wraps the whole loop,
 // so the remaining elements and indices are skipped.
-__device__ void thread_args(const DevState& S, const DevCfg& cfg, uint32_t res, uint32_t epoch, uint32_t nflags,
-                            const EvX& x, int64_t d, uint32_t* bflags) {
+__device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags, const EvX& x, int64_t d) {
     for (uint32_t i = 0; i < x.n && i < SG_MAX_ARGS; ++i) {
         if (!(nflags & ni_tm(i))) continue;
         const sg_arg v = evx_arg(x, i);
@@ -536,10 +597,10 @@ __device__ void thread_args(const DevState& S, const DevCfg& cfg, uint32_t res, 
             for (uint32_t k = 0; k < v.len; ++k) {
                 const sg_arg el = S.args[v.key + k];
                 if (el.kind != SG_ARG_SCALAR) return;
-                thread_count_add(S, cfg, res, epoch, i, el.key, d, bflags);
+                thread_count_add(S, tm_base, i, el.key, d);
             }
         } else if (v.kind == SG_ARG_SCALAR) {
-            thread_count_add(S, cfg, res, epoch, i, v.key, d, bflags);
+            thread_count_add(S, tm_base, i, v.key, d);
         }
     }
 }
@@ -614,6 +675,7 @@ __device__ __forceinline__ int flow_select(const DRule& r, const EvX& x, const D
     if (!applies) return SEL_NONE;
     if (r.strategy == SG_STRATEGY_RELATE) return r.ref == NO_REF ? SEL_CLUSTER : SEL_RELATE;
     if (r.strategy == SG_STRATEGY_CHAIN) return x.ctx == r.chain_ctx ? SEL_DEFAULT : SEL_NONE;
+    if (r.strategy != SG_STRATEGY_DIRECT) return SEL_NONE;  // selectReferenceNode: no node for other strategies
     return r.la_kind == LA_DEFAULT ? SEL_CLUSTER : SEL_ORIGIN;
 }
 
@@ -701,10 +763,10 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                     for (uint32_t k = 0; k < v.len && ok; ++k) {
                         const sg_arg el = S.args[v.key + k];
                         if (el.kind != SG_ARG_SCALAR) break;  // a null element throws: passLocalCheck passes
-                        ok = param_check(S, cfg, res, pg.tc_epoch, r, (uint32_t)idx, cnt, el.key, t, w, bflags);
+                        ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, el.key, t, w);
                     }
                 } else if (v.kind == SG_ARG_SCALAR) {
-                    ok = param_check(S, cfg, res, pg.tc_epoch, r, (uint32_t)idx, cnt, v.key, t, w, bflags);
+                    ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, v.key, t, w);
                 }
                 if (!ok) { status = ST_BLOCK_PARAM; slot = r.slot; }
                 else wait += w;
@@ -739,13 +801,13 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
     }
     if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
         N.thread++;
-        if (N.flags & NI_PM) thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, 1, bflags);
+        if (N.flags & NI_PM) thread_args(S, pg.tm_base, N.flags, x, 1);
         return mk_dec(ST_PASS_WAIT, slot, wait);
     }
     const bool passed = status == ST_PASS;
     stat_entry(N, C, t, cnt, passed);
     // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount(args)
-    if (passed && (N.flags & NI_PM)) thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, 1, bflags);
+    if (passed && (N.flags & NI_PM)) thread_args(S, pg.tm_base, N.flags, x, 1);
     return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
 }
 
@@ -764,13 +826,13 @@ __device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState&
             aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
     }
     if (!(r.flags & SG_F_EXIT_ARGS) || !(N.flags & NI_PM)) return;
-    if (x.n) { thread_args(S, cfg, res, pg.tc_epoch, N.flags, x, -1, bflags); return; }
+    if (x.n) { thread_args(S, pg.tm_base, N.flags, x, -1); return; }
     if (!S.key_ring || ref == SG_REF_NONE) return;
     const uint64_t key = S.key_ring[ref & cfg.ring_mask];
     if (key == NO_KEY) return;
     EvX k;
     k.origin = 0; k.ctx = 0; k.n = 1; k.a = nullptr; k.k0 = key;
-    thread_args(S, cfg, res, pg.tc_epoch, N.flags, k, -1, bflags);
+    thread_args(S, pg.tm_base, N.flags, k, -1);
 }
 
 // A STRATEGY_RELATE component (one segment, members in event order): each event runs on its own

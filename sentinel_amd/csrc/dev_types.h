@@ -7,8 +7,9 @@
 //   Prog    prog[R]       compiled rule program: [param..., flow..., degrade...]
 //   DRule   rules[]       compiled rule constants
 //   RState  rstate[]      controller / breaker state (one per rule)
-//   PSlot   ptab[2^k]     exact open-addressing table: (param rule state id, value) -> token bucket,
-//                         (resource, value) -> param thread count (ParameterMetric maps)
+//   PMap    pmap[]        ParameterMetric's CacheMaps: one bounded LRU map per (param rule state) and per
+//                         (resource, paramIdx) thread-count map, each a private open-addressing region of
+//   PSlot   pslot[]       the slot pool (linear probing, backward-shift deletion, doubly linked LRU list)
 //   uint8   ring[2^k]     status of every ENTRY by global event index (EXIT/TRACE references)
 // All counters are int64 exactly as the Java LongAdders; RT sums are int64.
 #pragma once
@@ -75,7 +76,7 @@ enum : uint8_t {
 struct Prog {
     uint32_t rule_off;
     uint8_t n_param, n_flow, n_degrade, pflags;
-    uint32_t tc_epoch;   // epoch of this resource's param thread-count keys
+    uint32_t tm_base;    // thread-count maps of this resource: DevState.tmid[tm_base + paramIdx] (NO_ID: none)
     uint32_t multi;      // PX_* bits
 };
 enum : uint32_t {
@@ -109,7 +110,8 @@ struct DRule {
     int64_t duration_sec;// param durationInSec
     int64_t token_count_l; // param (long)count (throttle)
     uint32_t hot_off, hot_n;   // hot items
-    uint32_t psid;       // param state id (ParameterMetric maps keyed by rule equality)
+    uint32_t pmap;       // param: its ParameterMetric time/token map (DevState.pmap index; maps are keyed by
+                         // rule equality, so an equal rule reloaded keeps its map)
     uint32_t ref;        // flow STRATEGY_RELATE: the resource whose ClusterNode is checked (NO_REF: none)
     int32_t param_idx;   // param: ParamFlowRule.paramIdx as loaded (< 0: resolved on first use, RState.a)
     uint32_t la_kind;    // flow: LA_* of limitApp
@@ -136,13 +138,33 @@ struct RState {
     int64_t d;
 };
 
-// param table slot
-struct PSlot {
-    uint64_t khi;    // 0 = empty; (1<<62)|psid for token buckets; (2<<62)|epoch<<32|res for thread counts
-    uint64_t kval;   // parameter value key
-    int64_t v0;      // token bucket: last add time / throttle last pass time; thread: count
-    int64_t v1;      // token bucket: tokens (int)
+// ParameterMetric's CacheMap (ConcurrentLinkedHashMapWrapper, param/.../ParameterMetric.java:37-114): at most
+// `cap` entries, least-recently-used evicted on insert.  A rule's ruleTimeCounters and ruleTokenCounter maps
+// see the same key sequence (every passDefaultLocalCheck touches both, time first), so they always hold the
+// same keys in the same LRU order and share one map here (v0 = time, v1 = tokens).  A map is owned by one
+// resource and only its lane touches it: no atomics.
+#define PM_NIL 0xFFFFFFFFu
+struct PMap {
+    uint64_t base;   // first slot in DevState.pslot
+    uint32_t slots;  // region size (> cap: the probe always finds a free slot)
+    uint32_t cap;    // min(4000 * durationInSec, 200000) for rule maps, 4000 for thread-count maps
+    uint32_t count;
+    uint32_t head;   // most recently used slot (region-local), PM_NIL when empty
+    uint32_t tail;   // least recently used
+    uint32_t pad;
 };
+static_assert(sizeof(PMap) == 32, "PMap must be 32 B");
+struct PSlot {
+    uint64_t kval;   // parameter value key
+    int64_t v0;      // rule map: last add time / throttle last pass time; thread map: count
+    int32_t v1;      // rule map: tokens
+    uint32_t prev;   // LRU neighbours (region-local slots, PM_NIL at the ends)
+    uint32_t next;
+    uint32_t used;
+};
+static_assert(sizeof(PSlot) == 32, "PSlot must be 32 B");
+#define PM_BASE_CAP 4000u      // ParameterMetric.BASE_PARAM_MAX_CAPACITY / THREAD_COUNT_MAX_CAPACITY
+#define PM_TOTAL_CAP 200000u   // ParameterMetric.TOTAL_MAX_CAPACITY
 
 enum : uint8_t { ST_PASS = 0, ST_PASS_WAIT = 1, ST_BLOCK_FLOW = 2, ST_BLOCK_DEGRADE = 3, ST_BLOCK_PARAM = 4,
                  ST_NO_CHECK = 5, ST_BLOCK_UPSTREAM = 6, ST_NOT_ENTRY = 0xFF };
@@ -152,7 +174,7 @@ struct DevCfg {
     int32_t occupy_timeout;
     int32_t max_chain;
     int32_t switch_on;
-    uint64_t ptab_mask;
+    uint64_t reserved0;
     uint64_t ring_mask;
     uint32_t dbg_flags;  // SG_DEBUG_FLAGS experiment switches (0 in production)
     uint32_t pad;
@@ -264,7 +286,9 @@ struct DevState {
     const DRule* rules;
     RState* rstate;
     const DHot* hot;
-    PSlot* ptab;
+    PMap* pmap;               // ParameterMetric maps (see PMap)
+    PSlot* pslot;
+    const uint32_t* tmid;     // [Prog.tm_base + paramIdx] -> thread-count map (NO_ID: none)
     uint8_t* ring;
     unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
     uint32_t* sink;           // >= 1024 scratch words: target of masked-off unconditional stores

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -40,6 +41,7 @@ hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t
                            sg_metric_node*, uint64_t, hipStream_t);
 hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borrow, uint32_t nres, hipStream_t st);
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st);
+hipError_t launch_region_copy(const PSlot* src, PSlot* dst, const uint64_t* tri, uint32_t n, hipStream_t st);
 // decide.hip
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
@@ -419,8 +421,14 @@ struct sg_engine {
     std::vector<std::vector<int>> res_flow, res_deg, res_par; // compiled order per resource
     std::map<std::string, uint32_t> psid_of;                   // "res\x00eqkey" -> param state id
     uint32_t next_psid = 1;
-    std::vector<uint32_t> tc_epoch;                             // per resource
-    uint32_t next_epoch = 1;
+    // ParameterMetric maps (dev_types.h PMap): one region per rule state (psid) and per (resource, paramIdx)
+    // thread-count map, laid out in one slot pool rebuilt whenever the set of maps changes
+    std::map<uint32_t, uint32_t> rmap_cap;                      // psid -> CacheMap capacity
+    std::set<uint64_t> tmaps;                                   // res << 8 | paramIdx
+    std::vector<uint64_t> pmap_key;                             // map index -> psid, or TMAP_KEY | res << 8 | idx
+    std::unordered_map<uint32_t, uint32_t> pmap_index;         // psid -> map index
+    std::vector<uint32_t> tm_base;                              // per resource: Prog.tm_base
+    uint64_t n_pslot = 0;
     uint32_t n_dev_rules = 0;
 
     // device state
@@ -431,7 +439,9 @@ struct sg_engine {
     DRule* d_rules = nullptr;
     RState* d_rstate = nullptr;
     DHot* d_hot = nullptr;
-    PSlot* d_ptab = nullptr;
+    PMap* d_pmap = nullptr;
+    PSlot* d_pslot = nullptr;
+    uint32_t* d_tmid = nullptr;
     uint8_t* d_ring = nullptr;
     uint32_t rules_cap = 0, hot_cap = 0;
 
@@ -633,7 +643,6 @@ static int collect(sg_engine* e, int k) {
         return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
-    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "param hash table full (raise param_table_log2)");
     if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
     return SG_OK;
 }
@@ -666,13 +675,12 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
         HIPCHK(hipMemcpy(old_prog.data(), e->d_prog, R * sizeof(Prog), hipMemcpyDeviceToHost));
     }
     size_t nres = e->names.size();
-    if (e->tc_epoch.size() < nres) e->tc_epoch.resize(nres, 0);
     std::vector<std::pair<uint32_t, uint32_t>> relate;  // (resource, referenced resource) of RELATE rules
     for (size_t r = 0; r < nres && r < R; ++r) {
         Prog p;
         std::memset(&p, 0, sizeof(p));
         p.rule_off = (uint32_t)rules.size();
-        p.tc_epoch = e->tc_epoch[r];
+        p.tm_base = r < e->tm_base.size() ? e->tm_base[r] : NO_ID;
         // param rules: HashSet order (ParamFlowSlot.checkFlow iterates them, ParamFlowSlot.java:84-100)
         const auto& pl = r < e->res_par.size() ? e->res_par[r] : std::vector<int>();
         for (size_t i = 0; i < pl.size(); ++i) {
@@ -706,7 +714,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             d.hot_off = (uint32_t)hot.size();
             d.hot_n = (uint32_t)q.hot.size();
             for (auto& h : q.hot) hot.push_back(DHot{h.first, h.second, 0});
-            d.psid = e->psid_of[q.res + std::string("\0", 1) + q.eqkey];
+            d.pmap = e->pmap_index.at(e->psid_of.at(q.res + std::string("\0", 1) + q.eqkey));
             d.param_idx = q.r.param_idx;
             d.ref = NO_REF;
             rules.push_back(d);
@@ -910,7 +918,7 @@ void sg_config_default(sg_config* c) {
     c->device = 0;
     c->max_resources = 1u << 20;
     c->max_rules = 1u << 21;
-    c->param_table_log2 = 22;
+    c->param_table_log2 = 28;
     c->status_ring_log2 = 28;
     c->max_batch_events = 1u << 25;
     c->cluster_sample_count = 10;
@@ -972,7 +980,6 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     uint64_t R = cfg.max_resources;
     if (hipMalloc(&e->d_sec, R * 2 * sizeof(Bkt)) != hipSuccess || hipMalloc(&e->d_minb, R * 60 * sizeof(Bkt)) != hipSuccess ||
         hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
-        hipMalloc(&e->d_ptab, (1ull << cfg.param_table_log2) * sizeof(PSlot)) != hipSuccess ||
         hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
         hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&e->d_prio, R * 4) != hipSuccess)
@@ -990,7 +997,6 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
             return bad(fail(SG_ENOMEM, "device allocation of the origin/context node pool failed"));
     }
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_ptab, 0, (1ull << cfg.param_table_log2) * sizeof(PSlot), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_prio, 0, R * 4, e->stream) != hipSuccess ||
         launch_init_state(e->d_sec, e->d_minb, e->d_info, e->d_borrow, (uint32_t)R, e->stream) != hipSuccess ||
@@ -1056,7 +1062,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
-    dfree(e->d_hot); dfree(e->d_ptab); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
+    dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pslot); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt);
@@ -1417,6 +1423,100 @@ static int rebuild_cluster_param(sg_engine* e, const sg_param_rule* rules, const
     return SG_OK;
 }
 
+// ---- ParameterMetric maps (dev_types.h PMap)
+#define TMAP_KEY (1ull << 63)
+// CacheMap capacity of a rule's time/token maps (ParameterMetric.initialize, ParameterMetric.java:87-104)
+static uint32_t rule_map_cap(int64_t duration_sec) {
+    const int64_t c = (int64_t)PM_BASE_CAP * std::max<int64_t>(duration_sec, 1);
+    return (uint32_t)std::min<int64_t>(c, PM_TOTAL_CAP);
+}
+// region slots: at most 2/3 full, so linear probes stay short and always meet a free slot
+static uint32_t region_slots(uint32_t cap) { return (uint32_t)((((uint64_t)cap * 3 / 2 + 1) + 63) & ~63ull); }
+
+// Lay out one region per map in a fresh slot pool, carrying the entries, counts and LRU order of the maps that
+// stay.  Everything that can fail (the capacity check, the allocations) happens before the engine changes:
+// an SG_ECAPACITY leaves the old maps in place.
+static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap, const std::set<uint64_t>& tmaps) {
+    std::vector<uint64_t> keys;
+    std::vector<PMap> hdr;
+    uint64_t total = 0;
+    auto add = [&](uint64_t key, uint32_t cap) {
+        PMap m;
+        std::memset(&m, 0, sizeof(m));
+        m.base = total;
+        m.cap = cap;
+        m.slots = region_slots(cap);
+        m.head = m.tail = PM_NIL;
+        keys.push_back(key);
+        hdr.push_back(m);
+        total += m.slots;
+    };
+    for (const auto& kv : rcap) add(kv.first, kv.second);
+    for (uint64_t t : tmaps) add(TMAP_KEY | t, PM_BASE_CAP);
+    if (total > (1ull << e->cfg.param_table_log2))
+        return fail(SG_ECAPACITY, "hot-parameter maps need " + std::to_string(total) + " slots, param_table_log2 = " +
+                                      std::to_string(e->cfg.param_table_log2) + " allows " +
+                                      std::to_string(1ull << e->cfg.param_table_log2));
+    std::vector<PMap> old(e->pmap_key.size());
+    if (!old.empty()) HIPCHK(hipMemcpy(old.data(), e->d_pmap, old.size() * sizeof(PMap), hipMemcpyDeviceToHost));
+    std::unordered_map<uint64_t, uint32_t> was;
+    for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i) was[e->pmap_key[i]] = i;
+    std::vector<uint64_t> tri;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        auto it = was.find(keys[i]);
+        if (it == was.end()) continue;
+        const PMap& o = old[it->second];
+        if (o.slots != hdr[i].slots) continue;  // cannot happen: a map's capacity is fixed by its identity
+        hdr[i].count = o.count;
+        hdr[i].head = o.head;
+        hdr[i].tail = o.tail;
+        tri.insert(tri.end(), {o.base, hdr[i].base, (uint64_t)o.slots});
+    }
+    std::vector<uint32_t> tb(e->names.size(), NO_ID), tmid;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        if (!(keys[i] & TMAP_KEY)) continue;
+        const uint32_t r = (uint32_t)(keys[i] >> 8), idx = (uint32_t)(keys[i] & 0xFF);
+        if (r >= tb.size()) tb.resize(r + 1, NO_ID);
+        if (tb[r] == NO_ID) { tb[r] = (uint32_t)tmid.size(); tmid.resize(tmid.size() + SG_MAX_ARGS, NO_ID); }
+        tmid[tb[r] + idx] = (uint32_t)i;
+    }
+    PSlot* np = nullptr;
+    PMap* nh = nullptr;
+    uint32_t* nt = nullptr;
+    uint64_t* dtri = nullptr;
+    auto release = [&]() { dfree(np); dfree(nh); dfree(nt); dfree(dtri); };
+    if ((total && hipMalloc(&np, total * sizeof(PSlot)) != hipSuccess) ||
+        (!hdr.empty() && hipMalloc(&nh, hdr.size() * sizeof(PMap)) != hipSuccess) ||
+        (!tmid.empty() && hipMalloc(&nt, tmid.size() * 4) != hipSuccess) ||
+        (!tri.empty() && hipMalloc(&dtri, tri.size() * 8) != hipSuccess)) {
+        release();
+        (void)hipGetLastError();
+        return fail(SG_ECAPACITY, "device memory for " + std::to_string(total) + " hot-parameter map slots");
+    }
+    if (total) HIPCHK(hipMemsetAsync(np, 0, total * sizeof(PSlot), e->stream));
+    if (!hdr.empty()) HIPCHK(hipMemcpyAsync(nh, hdr.data(), hdr.size() * sizeof(PMap), hipMemcpyHostToDevice, e->stream));
+    if (!tmid.empty()) HIPCHK(hipMemcpyAsync(nt, tmid.data(), tmid.size() * 4, hipMemcpyHostToDevice, e->stream));
+    if (!tri.empty()) {
+        HIPCHK(hipMemcpyAsync(dtri, tri.data(), tri.size() * 8, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(launch_region_copy(e->d_pslot, np, dtri, (uint32_t)(tri.size() / 3), e->stream));
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    dfree(dtri);
+    dfree(e->d_pslot); dfree(e->d_pmap); dfree(e->d_tmid);
+    e->d_pslot = np;
+    e->d_pmap = nh;
+    e->d_tmid = nt;
+    e->n_pslot = total;
+    e->pmap_key = keys;
+    e->pmap_index.clear();
+    for (uint32_t i = 0; i < (uint32_t)keys.size(); ++i)
+        if (!(keys[i] & TMAP_KEY)) e->pmap_index[(uint32_t)keys[i]] = i;
+    e->tm_base = tb;
+    e->rmap_cap = rcap;
+    e->tmaps = tmaps;
+    return SG_OK;
+}
+
 int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SG_EINVAL, "null argument");
     if (int rc = drain(e)) return rc;  // no batch in flight while the rule tables change
@@ -1435,7 +1535,6 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
         if (n_loaded) *n_loaded = (uint32_t)e->params.size();
         return SG_OK;
     }
-    if (int rc = rebuild_cluster_param(e, rules, all, n)) return rc;
     std::vector<ParamR> ps;
     std::vector<std::vector<int>> per;
     std::unordered_map<std::string, int> seen;
@@ -1455,27 +1554,54 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     for (size_t i = 0; i < ps.size(); ++i) hs[i] = ps[i].hash;
     for (auto& l : per) hashset_order(hs, l);
     // ParameterMetric lifetime: resources that had rules and now have none lose their metric
-    // (ParamFlowRuleManager.java:150-159); all metrics are cleared for an empty list.
-    if (e->tc_epoch.size() < e->names.size()) e->tc_epoch.resize(e->names.size(), 0);
+    // (ParamFlowRuleManager.java:150-159); all metrics are cleared for an empty list.  Work on copies: the maps
+    // are rebuilt (and may fail with SG_ECAPACITY) before anything of the engine changes.
     std::vector<bool> now_has(e->names.size(), false);
     for (size_t r = 0; r < per.size(); ++r) now_has[r] = !per[r].empty();
+    auto psid_of = e->psid_of;
+    auto rcap = e->rmap_cap;
+    auto tmaps = e->tmaps;
+    uint32_t next_psid = e->next_psid;
     std::vector<uint64_t> clear_flags;
     for (size_t r = 0; r < e->res_par.size(); ++r) {
         bool had = !e->res_par[r].empty();
         if ((had && !now_has[r]) || n == 0) {
-            e->tc_epoch[r] = e->next_epoch++;
-            for (auto it = e->psid_of.begin(); it != e->psid_of.end();) {
-                if (it->first.compare(0, e->names[r].size() + 1, e->names[r] + std::string("\0", 1)) == 0)
-                    it = e->psid_of.erase(it);
+            const std::string pre = e->names[r] + std::string("\0", 1);
+            for (auto it = psid_of.begin(); it != psid_of.end();) {
+                if (it->first.compare(0, pre.size(), pre) == 0) { rcap.erase(it->second); it = psid_of.erase(it); }
                 else ++it;
             }
+            tmaps.erase(tmaps.lower_bound((uint64_t)r << 8), tmaps.lower_bound((uint64_t)(r + 1) << 8));
             clear_flags.push_back(((uint64_t)(NI_PM | (((1u << SG_MAX_ARGS) - 1) << NI_TM_SHIFT)) << 32) | r);
         }
     }
     for (auto& q : ps) {
         std::string k = q.res + std::string("\0", 1) + q.eqkey;
-        if (!e->psid_of.count(k)) e->psid_of[k] = e->next_psid++;
+        if (!psid_of.count(k)) {
+            psid_of[k] = next_psid;
+            rcap[next_psid++] = rule_map_cap(q.r.duration_in_sec);
+        }
     }
+    // thread-count maps: ParameterMetric.initialize makes one per paramIdx a rule of the resource resolves to
+    // (a negative index resolves per call: any index); a map stays while the resource keeps a metric
+    for (size_t r = 0; r < per.size(); ++r)
+        for (int i : per[r]) {
+            const int32_t idx = ps[i].r.param_idx;
+            for (int32_t k = 0; k < SG_MAX_ARGS; ++k)
+                if (idx < 0 || idx == k) tmaps.insert(((uint64_t)r << 8) | (uint64_t)k);
+        }
+    // the capacity check first: with SG_ECAPACITY neither the cluster rules nor the maps change
+    uint64_t need = 0;
+    for (const auto& kv : rcap) need += region_slots(kv.second);
+    need += tmaps.size() * (uint64_t)region_slots(PM_BASE_CAP);
+    if (need > (1ull << e->cfg.param_table_log2))
+        return fail(SG_ECAPACITY, "hot-parameter maps need " + std::to_string(need) + " slots, param_table_log2 = " +
+                                      std::to_string(e->cfg.param_table_log2) + " allows " +
+                                      std::to_string(1ull << e->cfg.param_table_log2));
+    if (int rc = rebuild_cluster_param(e, rules, all, n)) return rc;
+    if (int rc = rebuild_pmaps(e, rcap, tmaps)) return rc;
+    e->psid_of = std::move(psid_of);
+    e->next_psid = next_psid;
     auto op = std::move(e->params);
     auto opr = std::move(e->res_par);
     e->params = std::move(ps);
@@ -1660,7 +1786,6 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     dc.occupy_timeout = e->cfg.occupy_timeout_ms;
     dc.max_chain = e->cfg.max_slot_chain_size;
     dc.switch_on = e->cfg.switch_on;
-    dc.ptab_mask = (1ull << e->cfg.param_table_log2) - 1;
     dc.ring_mask = ring_mask;
     dc.dbg_flags = e->dbg_flags;
     DevState S{};
@@ -1672,7 +1797,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.rules = e->d_rules;
     S.rstate = e->d_rstate;
     S.hot = e->d_hot;
-    S.ptab = e->d_ptab;
+    S.pmap = e->d_pmap;
+    S.pslot = e->d_pslot;
+    S.tmid = e->d_tmid;
     S.ring = e->d_ring;
     S.sink = e->d_sink;
     S.borrow = e->d_borrow;

@@ -435,6 +435,12 @@ __global__ void k_set_flags(NodeInfo* __restrict__ info, const uint64_t* __restr
     if (u >> 63) info[res].flags |= f;
     else info[res].flags &= ~f;
 }
+// the ParameterMetric map regions that survive a rule reload, moved into the new slot pool: one workgroup per
+// region, tri[3 * i] = {source base, destination base, slots}
+__global__ void k_region_copy(const PSlot* __restrict__ src, PSlot* __restrict__ dst, const uint64_t* __restrict__ tri) {
+    const uint64_t s = tri[3 * blockIdx.x], d = tri[3 * blockIdx.x + 1], n = tri[3 * blockIdx.x + 2];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[d + i] = src[s + i];
+}
 
 // =================================================================================
 // host-callable launch wrappers (engine.cpp)
@@ -482,6 +488,12 @@ hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borro
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_set_flags, dim3((n + 255) / 256), dim3(256), 0, st, info, upd, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_region_copy(const PSlot* src, PSlot* dst, const uint64_t* tri, uint32_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_region_copy, dim3(n), dim3(256), 0, st, src, dst, tri);
     return hipGetLastError();
 }
 

@@ -91,6 +91,19 @@ struct Workload {
     uint64_t n_entries = 0;
     int64_t t0 = 0, t_end = 0;
     std::string la_default = "default";
+    // hot items of the param rules (variant TG_V_HOT): the strings the sg_param_item pointers name
+    std::vector<std::string> item_text;
+    std::vector<std::vector<sg_param_item>> items;
+};
+
+// trace variants (tg_create `variant` bits), on top of the SURVEY.md configs:
+enum : uint32_t {
+    TG_V_WARM_RL = 1,   // C3: a fifth of the flow rules become WarmUpRateLimiter (control behaviour 3)
+    TG_V_HOT = 2,       // C5: every param rule gets 3 hot items (popular values, counts 0..19)
+    TG_V_THREAD = 4,    // C5: a fifth of the param rules are THREAD grade; every EXIT releases its ENTRY's
+                        // argument (Entry.exit(count, args): SG_F_EXIT_ARGS)
+    TG_V_UNIFORM = 8    // C5: half of the parameter values uniform over n_param_values, half Zipf(1.1): many
+                        // distinct values churn the maps while the popular ones repeat (and get blocked)
 };
 
 sg_flow_rule flow_default(const char* res, double count) {
@@ -193,7 +206,7 @@ void gen_c1(Workload& w, uint64_t seed, int seconds) {
 
 // C2-C5: Zipf(1.1) resources, Poisson arrivals at `rate` entries/s.
 void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n_entries, double rate,
-              uint64_t n_param_values) {
+              uint64_t n_param_values, uint32_t variant) {
     Rng rng(seed);
     w.name_store.resize(n_res);
     w.names.resize(n_res);
@@ -219,6 +232,10 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
             } else if (u < 0.8) {
                 r.control_behavior = SG_CONTROL_BEHAVIOR_WARM_UP;
                 r.warm_up_period_sec = 10;
+            } else if ((variant & TG_V_WARM_RL) && u < 0.9) {
+                r.control_behavior = SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER;
+                r.warm_up_period_sec = 10;
+                r.max_queueing_time_ms = 500;
             } else {
                 r.control_behavior = SG_CONTROL_BEHAVIOR_RATE_LIMITER;
                 r.max_queueing_time_ms = 500;
@@ -252,6 +269,11 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
                 p.control_behavior = SG_CONTROL_BEHAVIOR_RATE_LIMITER;
                 p.max_queueing_time_ms = 100;
             }
+            if ((variant & TG_V_THREAD) && rng.uniform() < 0.2) {
+                p.grade = SG_FLOW_GRADE_THREAD;
+                p.control_behavior = SG_CONTROL_BEHAVIOR_DEFAULT;
+                p.count = (double)(3 + rng.below(8));
+            }
             p.cluster_sample_count = 10;
             p.cluster_window_interval_ms = 1000;
             w.param.push_back(p);
@@ -271,7 +293,32 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
         pkey.resize(n_param_values);
         Rng kr(seed ^ 0x5eed5eedULL);
         for (uint64_t i = 0; i < n_param_values; ++i) pkey[i] = (3ULL << 60) | (kr.next() & ((1ULL << 59) - 1)); // Long keys
+        if (variant & TG_V_HOT) {  // hot items: three of the 16 most popular values, as ("<long>", "long")
+            Rng hr(seed ^ 0x407e11ULL);
+            w.items.resize(w.param.size());
+            w.item_text.reserve(w.param.size() * 3);
+            for (size_t k = 0; k < w.param.size(); ++k) {
+                for (int j = 0; j < 3; ++j) {
+                    const uint64_t v = pkey[hr.below(std::min<uint64_t>(16, n_param_values))] & ((1ULL << 59) - 1);
+                    w.item_text.push_back(std::to_string(v));
+                }
+            }
+            for (size_t k = 0; k < w.param.size(); ++k) {
+                for (int j = 0; j < 3; ++j) {
+                    sg_param_item it;
+                    std::memset(&it, 0, sizeof(it));
+                    it.object = w.item_text[3 * k + j].c_str();
+                    it.class_type = "long";
+                    it.count = (int32_t)hr.below(20);
+                    it.has_count = 1;
+                    w.items[k].push_back(it);
+                }
+                w.param[k].items = w.items[k].data();
+                w.param[k].n_items = 3;
+            }
+        }
     }
+    const uint8_t exit_flags = (config == 5 && (variant & TG_V_THREAD)) ? SG_F_EXIT_ARGS : 0;
 
     std::vector<Raw> raw;
     raw.reserve(n_entries * (config == 4 ? 21 : 20) / 10);
@@ -282,12 +329,15 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
         uint64_t ms = (uint64_t)(t_us / 1000.0);
         uint32_t res = perm[za.sample(rng)];
         Raw e{ms * 4 + 0, i, res, 1, SG_EV_ENTRY, 0, 0};
-        if (config == 5) { e.flags = SG_F_HAS_ARG; e.aux = pkey[pa.sample(rng)]; }
+        if (config == 5) {
+            e.flags = SG_F_HAS_ARG;
+            e.aux = pkey[(variant & TG_V_UNIFORM) && rng.uniform() < 0.5 ? rng.below(n_param_values) : pa.sample(rng)];
+        }
         raw.push_back(e);
         int64_t rt = exp_rt(rng);
         uint64_t xms = ms + (uint64_t)rt;
         if (config == 4 && rng.uniform() < 0.05) raw.push_back(Raw{xms * 4 + 1, i, res, 1, SG_EV_TRACE, 0, 0});
-        raw.push_back(Raw{xms * 4 + 2, i, res, 1, SG_EV_EXIT, 0, (uint64_t)rt});
+        raw.push_back(Raw{xms * 4 + 2, i, res, 1, SG_EV_EXIT, exit_flags, (uint64_t)rt});
     }
     w.n_entries = n_entries;
     w.t_end = w.t0 + (int64_t)(t_us / 1000.0) + 1;
@@ -302,7 +352,7 @@ typedef struct tg_workload tg_workload;
 
 // config 1..5; n_res/n_entries/rate = 0 pick the SURVEY.md defaults.
 tg_workload* tg_create(int config, uint64_t seed, uint32_t n_res, uint64_t n_entries, double rate, int64_t t0,
-                       uint64_t n_param_values) {
+                       uint64_t n_param_values, uint32_t variant) {
     Workload* w = new Workload();
     w->config = config;
     w->t0 = t0 ? t0 : 1700000000000LL;
@@ -311,7 +361,7 @@ tg_workload* tg_create(int config, uint64_t seed, uint32_t n_res, uint64_t n_ent
     } else {
         uint32_t dres = config == 2 ? 10000 : config == 3 ? 100000 : config == 4 ? 1000000 : 10000;
         gen_zipf(*w, config, seed, n_res ? n_res : dres, n_entries ? n_entries : 100000000ULL,
-                 rate > 0 ? rate : 1e6, n_param_values ? n_param_values : 10000000ULL);
+                 rate > 0 ? rate : 1e6, n_param_values ? n_param_values : 10000000ULL, variant);
     }
     return reinterpret_cast<tg_workload*>(w);
 }

@@ -17,6 +17,12 @@ _lib = None
 
 SEED_BASE = 20240601  # seed 20240601 + config index
 
+# tg_create variant bits (csrc/tracegen.cpp TG_V_*)
+V_WARM_RL = 1   # C3: WarmUpRateLimiter flow rules in the mix
+V_HOT = 2       # C5: hot items on every param rule
+V_THREAD = 4    # C5: THREAD-grade param rules, exits release their argument (SG_F_EXIT_ARGS)
+V_UNIFORM = 8   # C5: half the parameter values uniform (many distinct values: the param maps fill and evict)
+
 
 def lib():
     global _lib
@@ -27,7 +33,8 @@ def lib():
         L = C.CDLL(LIB_PATH)
         P = C.c_void_p
         L.tg_create.restype = P
-        L.tg_create.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_double, C.c_int64, C.c_uint64]
+        L.tg_create.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_double, C.c_int64, C.c_uint64,
+                                C.c_uint32]
         L.tg_destroy.argtypes = [P]
         L.tg_names.restype = C.c_void_p
         L.tg_names.argtypes = [P, C.POINTER(C.c_uint32)]
@@ -48,10 +55,11 @@ class Workload:
     """A generated config: names, rules (as C arrays) and the event trace."""
 
     def __init__(self, config: int, seed: int | None = None, n_res: int = 0, n_entries: int = 0, rate: float = 0.0,
-                 t0: int = 0, n_param_values: int = 0):
+                 t0: int = 0, n_param_values: int = 0, variant: int = 0):
         self.config = config
         self.seed = SEED_BASE + config if seed is None else seed
-        self.h = lib().tg_create(config, self.seed, n_res, n_entries, rate, t0, n_param_values)
+        self.variant = variant
+        self.h = lib().tg_create(config, self.seed, n_res, n_entries, rate, t0, n_param_values, variant)
         n = C.c_uint32()
         self.names_ptr = lib().tg_names(self.h, C.byref(n))
         self.n_res = n.value

@@ -55,7 +55,7 @@ def test_golden_gpu(name):
     from sentinel_amd import engine as E
     m, g = _load(name)
     w = T.Workload(m["config"], **m["kwargs"])
-    eng = E.Engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=18, status_ring_log2=24)
+    eng = E.Engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, status_ring_log2=24)
     w.install(eng)
     np.testing.assert_array_equal(_replay(eng, m, g["events"]), g["decisions"])
     _check_nodes(eng, g)

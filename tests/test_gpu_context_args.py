@@ -35,8 +35,8 @@ def _rules(n_res):
     for i in range(n_res):
         nm = "r%d" % i
         k = i % 6
-        if k == 0:
-            flow.append(A.flow_rule(nm, 25))
+        if k == 0:  # strategy 3 is a valid rule whose node is never selected: it always passes
+            flow += [A.flow_rule(nm, 25), A.flow_rule(nm, 1, strategy=3, ref_resource="ctxA")]
         elif k == 1:
             flow += [A.flow_rule(nm, 4, limit_app="appA"), A.flow_rule(nm, 30)]
         elif k == 2:
@@ -128,7 +128,7 @@ def _trace(seed, n_res, n_entries, ids_o, ids_c, null_ctx=None):
 
 
 def _pair(n_res, intern_first=True, null_ctx=False, **cfg):
-    eng = E.Engine(max_resources=max(64, n_res), max_slot_chain_size=0, param_table_log2=18, status_ring_log2=22, **cfg)
+    eng = E.Engine(max_resources=max(64, n_res), max_slot_chain_size=0, status_ring_log2=22, **cfg)
     orc = O.Oracle(max_slot_chain_size=0)
     names = ["r%d" % i for i in range(n_res)]
     ids = []

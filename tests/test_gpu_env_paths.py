@@ -1,10 +1,9 @@
 """Parity of the engine's alternative group-stage paths, selected by environment knobs that the
 library reads once per process (so each runs in a child process):
 
-  SG_GATHER=1       records gathered through the sort permutation (k_gather) instead of scattered
-  SG_SEG_FUSED=0    n-wide segment flags + scan + k_seg_start instead of the tile-fused kernels
-  SG_RADIX_DB=10    10-bit radix digits
-  SG_PIPELINE=0     group and decide stages back to back
+  SG_PIPELINE=0            group and decide stages back to back (no overlap of batch k+1's grouping)
+  SG_GROUP_CU_QUARTERS=2   the group stage confined to half of the CUs
+  SG_STREAM_PRIO=2         the group stream at the higher priority (default: the decide streams)
 
 Each child replays a seeded C4 trace (DegradeRules + QPS rules, several batches) through the HIP
 engine and the oracle and requires bit-identical decisions and node state.
@@ -27,7 +26,7 @@ import pyoracle as O
 from sentinel_amd import engine as E
 from sentinel_amd import tracegen as T
 w = T.Workload(4, n_entries=300_000, n_res=30_000)
-eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=18, status_ring_log2=24)
+eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, status_ring_log2=24)
 orc = O.Oracle(max_slot_chain_size=0)
 w.install(eng); w.install(orc)
 ev = w.events
@@ -44,7 +43,7 @@ print("ok", len(ev))
 """
 
 
-@pytest.mark.parametrize("env", ["SG_GATHER=1", "SG_SEG_FUSED=0", "SG_RADIX_DB=10", "SG_PIPELINE=0"])
+@pytest.mark.parametrize("env", ["SG_PIPELINE=0", "SG_GROUP_CU_QUARTERS=2", "SG_STREAM_PRIO=2"])
 def test_alternative_path_parity(env):
     k, v = env.split("=")
     child_env = dict(os.environ, **{k: v})

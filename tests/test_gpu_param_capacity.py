@@ -1,0 +1,106 @@
+"""The device's bounded ParameterMetric maps (dev_types.h PMap) against the oracle's (tests/test_param_capacity.py):
+LRU eviction at min(4000 * durationInSec, 200000) / 4000 values, the capacity check at rule load that leaves the
+engine unchanged (SG_ECAPACITY), and a C5 trace with more than five million distinct values through a pool sized
+by param_table_log2 = 24."""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from sentinel_amd import _abi as A
+from sentinel_amd import engine as E
+from sentinel_amd import tracegen as T
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+def _entries(rid, keys, t=T0):
+    ev = np.zeros(len(keys), dtype=A.EVENT_DTYPE)
+    ev["ts"] = t
+    ev["res_id"] = rid
+    ev["count"] = 1
+    ev["kind"] = A.EV_ENTRY
+    ev["flags"] = A.F_HAS_ARG
+    ev["aux"] = np.asarray(keys, dtype=np.uint64)
+    return ev
+
+
+def _pair(rule, **cfg):
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, **cfg)
+    orc = O.Oracle(max_slot_chain_size=0)
+    name = rule.resource.decode()
+    rid = eng.register(name)
+    assert orc.register(name) == rid
+    assert eng.load_param_rules([rule]) == 1 and orc.load_param_rules([rule]) == 1
+    return eng, orc, rid
+
+
+def _long(v):
+    return E.param_key(str(v), "java.lang.Long")
+
+
+@pytest.mark.parametrize("grade", [A.FLOW_GRADE_QPS, A.FLOW_GRADE_THREAD])
+@pytest.mark.parametrize("behavior", [A.CONTROL_BEHAVIOR_DEFAULT, A.CONTROL_BEHAVIOR_RATE_LIMITER])
+def test_eviction_sequences_match_the_oracle(grade, behavior):
+    if grade == A.FLOW_GRADE_THREAD and behavior != A.CONTROL_BEHAVIOR_DEFAULT:
+        pytest.skip("the control behaviour only applies to QPS rules")
+    eng, orc, rid = _pair(A.param_rule("capk", 0, 1, grade=grade, control_behavior=behavior, max_queueing_time_ms=0))
+    k = _long(-1)
+    seq = [k, k] + [_long(v) for v in range(3999)] + [k] + [_long(5000)] + [k, _long(0), _long(1)] + \
+          [_long(v) for v in range(6000, 12000)] + [k, _long(3000), _long(11999)]
+    ev = _entries(rid, seq)
+    for a, b in ((0, 2), (2, 4001), (4001, 4010), (4010, len(ev))):   # batches cut inside the sequences
+        dg, do = eng.submit(ev[a:b]), orc.submit(ev[a:b])
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), ("event", a + int(bad[0]), hex(dg[bad[0]]), hex(do[bad[0]]))
+
+
+def test_capacity_follows_the_duration_on_the_device():
+    eng, orc, rid = _pair(A.param_rule("capd", 0, 1, duration_in_sec=2))   # 8000 values
+    seq = [_long(-1)] + [_long(v) for v in range(7000)] + [_long(-1)] + [_long(v) for v in range(7000, 9000)] + \
+          [_long(-1), _long(0), _long(100)]
+    ev = _entries(rid, seq)
+    np.testing.assert_array_equal(eng.submit(ev), orc.submit(ev))
+
+
+def test_ecapacity_at_rule_load_leaves_the_engine_unchanged():
+    # 2^14 slots hold one resource's maps (a rule map + a thread-count map of 6016 slots each) but not two
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=14)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for n in ("a", "b"):
+        assert eng.register(n) == orc.register(n)
+    first = [A.param_rule("a", 0, 2)]
+    assert eng.load_param_rules(first) == 1 and orc.load_param_rules(first) == 1
+    ev = _entries(0, [_long(v % 7) for v in range(50)])
+    np.testing.assert_array_equal(eng.submit(ev), orc.submit(ev))
+    with pytest.raises(E.SentinelError) as ei:
+        eng.load_param_rules(first + [A.param_rule("b", 0, 1)])
+    assert ei.value.code == A.SG_ECAPACITY and "param_table_log2" in str(ei.value)
+    # the rules and the maps of "a" are what they were: the next batch still matches the oracle that never saw
+    # the failed load, including the tokens consumed before it
+    ev2 = _entries(0, [_long(v % 9) for v in range(60)], t=T0 + 500)
+    ev2 = np.concatenate([ev2, _entries(1, [_long(1)] * 3, t=T0 + 500)])
+    np.testing.assert_array_equal(eng.submit(ev2), orc.submit(ev2))
+
+
+def test_c5_five_million_distinct_values():
+    # SURVEY.md §8(d) C5 shape with churn: 14M entries over 1000 resources, half of the values uniform over 10M
+    # (5.46M distinct), hot items, THREAD-grade rules; every map fills and evicts.  The pool needs
+    # 1000 x 2 x 6016 slots, inside param_table_log2 = 24.
+    w = T.Workload(5, n_res=1000, n_entries=14_000_000, n_param_values=10_000_000,
+                   variant=T.V_UNIFORM | T.V_HOT | T.V_THREAD)
+    ev = w.events
+    assert len(np.unique(ev["aux"][ev["kind"] == A.EV_ENTRY])) >= 5_000_000
+    eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=24, status_ring_log2=26)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    cuts = np.linspace(0, len(ev), 5).astype(np.int64)
+    blocked = 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        dg, do = eng.submit(ev[a:b]), orc.submit(ev[a:b])
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), ("event", int(a + bad[0]), hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+        blocked += int(((dg & 0xFF) == A.BLOCK_PARAM).sum())
+    assert blocked > 100_000

@@ -20,7 +20,6 @@ T0 = 1_700_000_000_123
 
 def _engine(**kw):
     kw.setdefault("max_resources", 1 << 12)
-    kw.setdefault("param_table_log2", 18)
     kw.setdefault("status_ring_log2", 24)
     return E.Engine(**kw)
 
@@ -83,7 +82,7 @@ def bin_mode(request, monkeypatch):
 
 def _run(config, batches=3, chain_cap=0, **kw):
     w = T.Workload(config, **kw)
-    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap, param_table_log2=21)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=chain_cap)
     orc = O.Oracle(max_slot_chain_size=chain_cap)
     w.install(eng)
     w.install(orc)
@@ -119,6 +118,26 @@ def test_c4_wide_keys_two_10bit_passes():
 
 def test_c5_param(bin_mode):
     _run(5, batches=3, n_entries=400_000, n_param_values=50_000)
+
+
+def test_c3_warm_up_rate_limiter(bin_mode):
+    # WarmUpRateLimiterController (core/slots/block/flow/controller/WarmUpRateLimiterController.java) in the mix
+    w, *_ = _run(3, batches=3, n_entries=400_000, n_res=20_000, variant=T.V_WARM_RL)
+    assert w.variant == T.V_WARM_RL
+
+
+def test_c5_hot_items_and_thread_grade(bin_mode):
+    # local hot items (ParamFlowChecker.passDefaultLocalCheck / passThrottleLocalCheck exclusion items) and
+    # THREAD-grade param rules with exits that release their argument (ParameterMetric.decreaseThreadCount)
+    _, _, _, d = _run(5, batches=3, n_entries=400_000, n_param_values=50_000, variant=T.V_HOT | T.V_THREAD)
+    assert int(((d & 0xFF) == A.BLOCK_PARAM).sum()) > 0
+
+
+def test_c5_full_param_maps_evict(bin_mode):
+    # 16 resources, ~25k entries each over 200k values: every map fills and evicts its LRU values
+    _, _, _, d = _run(5, batches=4, n_entries=400_000, n_res=16, n_param_values=200_000,
+                      variant=T.V_UNIFORM | T.V_HOT | T.V_THREAD)
+    assert int(((d & 0xFF) == A.BLOCK_PARAM).sum()) > 0
 
 
 def test_chain_cap_reference_default():
@@ -275,7 +294,7 @@ def _run_prioritized(config, frac, batches, **kw):
     ent = ev["kind"] == A.EV_ENTRY
     pick = ent & (rng.random(len(ev)) < frac)
     ev["flags"] = np.where(pick, ev["flags"] | A.F_PRIORITIZED, ev["flags"])
-    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)
     w.install(eng)
     w.install(orc)
@@ -316,7 +335,7 @@ def test_exit_with_args_thread_params(bin_mode):
     names = ["res-%d" % i for i in range(w.n_res)]
     rules = [A.param_rule(nm, 0, 2 + i % 4, grade=A.FLOW_GRADE_THREAD) if i % 2 == 0 else
              A.param_rule(nm, 0, 20 + i % 30) for i, nm in enumerate(names)]
-    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)
     for x in (eng, orc):
         w.install(x)
@@ -339,7 +358,7 @@ def test_async_pipeline(config, kw, pipeline, monkeypatch):
     monkeypatch.setenv("SG_PIPELINE", pipeline)
     monkeypatch.setenv("SG_SKIP_MIN", "64")
     w = T.Workload(config, **kw)
-    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0, param_table_log2=21)
+    eng = _engine(max_resources=max(64, w.n_res), max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)
     w.install(eng)
     w.install(orc)
@@ -376,7 +395,7 @@ def test_relate_components(bin_mode):
     rules.append(A.flow_rule(names[b], 40, strategy=A.STRATEGY_RELATE, ref_resource=names[c]))
     rules.append(A.flow_rule(names[hot[33]], 30, strategy=A.STRATEGY_RELATE, ref_resource=names[hot[33]]))
     rules.append(A.flow_rule(names[hot[34]], 1, strategy=A.STRATEGY_RELATE, ref_resource="never-entered"))
-    eng = _engine(max_resources=max(64, w.n_res + 8), max_slot_chain_size=0, param_table_log2=21)
+    eng = _engine(max_resources=max(64, w.n_res + 8), max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)
     for x in (eng, orc):
         w.install(x)
@@ -411,7 +430,7 @@ def test_duplicate_exits_disable_skipping(monkeypatch):
     dup = ev[np.sort(rng.choice(exits, 500, replace=False))].copy()
     dup["ts"] = ev["ts"][-1]
     for events, expect_skip in ((ev, True), (np.concatenate([ev, dup]), False)):
-        eng = _engine(max_resources=64, max_slot_chain_size=0, param_table_log2=21)
+        eng = _engine(max_resources=64, max_slot_chain_size=0)
         orc = O.Oracle(max_slot_chain_size=0)
         w.install(eng)
         w.install(orc)
