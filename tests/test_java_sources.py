@@ -21,6 +21,8 @@ from sentinel_amd import engine
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 JAVA = os.path.join(ROOT, "java", "src", "main", "java", "com", "alibaba", "csp", "sentinel", "gpu")
+if not os.path.isdir(JAVA):  # the java/ sources do not travel to the GPU box (.gpurunignore)
+    pytest.skip("java/ sources absent", allow_module_level=True)
 SG = open(os.path.join(JAVA, "SentinelGpu.java")).read()
 
 _SIZE = {"JAVA_INT": 4, "JAVA_LONG": 8, "JAVA_DOUBLE": 8, "JAVA_SHORT": 2, "JAVA_BYTE": 1, "ADDRESS": 8}
