@@ -196,6 +196,46 @@ def test_thread_grade_scenario():
     assert eng.read_node(rid)["thread"] == 1
 
 
+def _submit_ctx(eng, rid, rows):
+    """rows: (ts, kind, origin, context, ref) -> decisions through sg_submit_ex (origin / context interned)."""
+    ev = np.zeros(len(rows), dtype=A.EVENT_DTYPE)
+    ext = np.zeros(len(rows), dtype=A.EXT_DTYPE)
+    for i, (ts, kind, origin, ctx, ref) in enumerate(rows):
+        aux = 0 if kind == A.EV_ENTRY else A.aux_exit(ref, 0)
+        ev[i] = (ts, rid, 1, kind, 0, aux)
+        ext[i]["origin_id"] = eng.intern_origin(origin) if origin else 0
+        ext[i]["context_id"] = eng.intern_context(ctx) if ctx else 0
+    return [int(x) & 0xFF for x in eng.submit_ex(ev, ext)]
+
+
+def test_origin_flow_rule_scenario():
+    # FlowPartialIntegrationTest.java:118-158 (testOriginFlowRule): "other" at 0 blocks app1, app2 has its own rule
+    eng = _engine()
+    rid = eng.register("testOriginFlowRule")
+    eng.load_flow_rules([A.flow_rule("testOriginFlowRule", 0, limit_app="other"),
+                         A.flow_rule("testOriginFlowRule", 1, limit_app="app2")])
+    d = _submit_ctx(eng, rid, [(T0, A.EV_ENTRY, "app1", "node1", 0), (T0, A.EV_ENTRY, "app2", "node1", 0),
+                               (T0, A.EV_EXIT, "app2", "node1", 1)])
+    assert d == [A.BLOCK_FLOW, A.PASS, A.NOT_ENTRY]
+
+
+def test_flow_rule_other_scenario():
+    # FlowPartialIntegrationTest.java:160-181 (testFlowRule_other): no origin is not an "other" origin
+    eng = _engine()
+    rid = eng.register("testOther")
+    eng.load_flow_rules([A.flow_rule("testOther", 0, limit_app="other")])
+    assert _submit_ctx(eng, rid, [(T0, A.EV_ENTRY, None, None, 0)]) == [A.PASS]
+
+
+def test_strategy_chain_scenario():
+    # FlowPartialIntegrationTest.java:224-255 (testStrategyChain): the rule reads the DefaultNode of context entry1
+    eng = _engine()
+    rid = eng.register("entry2")
+    eng.load_flow_rules([A.flow_rule("entry2", 0, strategy=A.STRATEGY_CHAIN, ref_resource="entry1")])
+    d = _submit_ctx(eng, rid, [(T0, A.EV_ENTRY, None, "entry1", 0), (T0, A.EV_ENTRY, None, "entry3", 0)])
+    assert d == [A.BLOCK_FLOW, A.PASS]
+
+
 def test_param_burst_scenario():
     # param-test/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:69-137 through the C ABI
     eng = _engine()
