@@ -111,12 +111,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # SG_BENCH_GLOO=1 rehearses the multi-rank path on a one-GPU box: gloo instead of RCCL, every rank on
+    # device local % device_count (never used for a reported number)
+    rehearse = os.environ.get("SG_BENCH_GLOO") == "1"
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev if rehearse else local)
+    dev = torch.device("cuda", local % ndev if rehearse else local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    cdev = torch.device("cpu") if rehearse else dev  # where collective tensors live
 
     from sentinel_amd import dist as D
     from sentinel_amd import engine as E
@@ -138,7 +146,7 @@ def main():
     ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(B)])
     res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(B)])
 
-    eng = E.Engine(device=local, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
+    eng = E.Engine(device=dev.index, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
                    status_ring_log2=28, max_batch_events=int(sizes.max()))
     w.install(eng)
 
@@ -163,7 +171,7 @@ def main():
     S = args.sub_batches or int(max(1, min(args.max_sub_batches,
                                          args.hbm_budget * (free - reserve) // (max(steps, warmup) * mean_b * 1.15))))
     if dist is not None:
-        t = torch.tensor([S], device=dev)
+        t = torch.tensor([S], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         S = int(t.item())
     nbat = max(steps, warmup) * S
@@ -194,13 +202,13 @@ def main():
         """MetricTimerListener across the node: every rank's MetricNode rows, device to device."""
         n = eng.snapshot_to(now, snap.data_ptr(), snap_cap)
         n = min(n, snap_cap)
-        cnt = torch.tensor([n], device=dev)
+        cnt = torch.tensor([n], device=cdev)
         cnts = [torch.zeros_like(cnt) for _ in range(world)]
         dist.all_gather(cnts, cnt)
         width = int(max(c.item() for c in cnts)) * 64
         if width:
-            outs = [torch.empty(width, dtype=torch.uint8, device=dev) for _ in range(world)]
-            dist.all_gather(outs, snap[:width])
+            outs = [torch.empty(width, dtype=torch.uint8, device=cdev) for _ in range(world)]
+            dist.all_gather(outs, snap[:width].to(cdev))
         return sum(int(c.item()) for c in cnts)
 
     base_ptr = buf.data_ptr()
@@ -233,10 +241,10 @@ def main():
     touched = float(sum(p[3] for p in plan))
     events = float(sum(p[1] for p in plan))
     if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        t = torch.tensor([entries, touched, events], device=dev, dtype=torch.float64)
+        t = torch.tensor([entries, touched, events], device=cdev, dtype=torch.float64)
         dist.all_reduce(t)
         entries, touched, events = (float(x) for x in t.tolist())
 
@@ -296,6 +304,7 @@ def main():
                     entries / (elapsed + h2d_ms / 1e3 * events / max(1, n_base) / world),
                     "note": "pinned host -> HBM copy of the events, measured on the base trace; not in value"},
             "metric_gathers": {"count": n_gather, "rows": rows_gathered} if world > 1 else None,
+            "rehearsal": "gloo, all ranks on one GPU: NOT a measurement" if rehearse else None,
             "cpu_baseline": cpu,
             "src_sha": sha,
             "gen_s": gen_s,
