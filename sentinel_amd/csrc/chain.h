@@ -336,7 +336,14 @@ __device__ __forceinline__ bool flow_can_pass(Node& N, const Ctx& C, const DRule
 
 // DegradeRule.passCheck (core/slots/block/degrade/DegradeRule.java:172-223); the ResetTask fires at
 // cut_until = t_cut + timeWindow*1000 (Q12).  RState: a = cut, b = passCount, c = cut_until.
-__device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DRule& r, RState& s, int64_t t) {
+// the DegradeRule fields the check reads (k_lite keeps only these in registers)
+struct DegParam {
+    double count;
+    int32_t time_window;
+    uint8_t grade;
+};
+__device__ __forceinline__ DegParam deg_param(const DRule& r) { return DegParam{r.count, r.time_window, r.grade}; }
+__device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DegParam& r, RState& s, int64_t t) {
     if (s.a && t >= s.c) { s.a = 0; s.b = 0; }
     if (s.a) return false;
     if (r.grade == SG_DEGRADE_GRADE_RT) {

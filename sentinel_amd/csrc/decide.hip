@@ -787,7 +787,7 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                 else if (rc == 2) { status = ST_PASS_WAIT; slot = r.slot; wait += w; }  // PriorityWaitException
                 else wait += w;
             } else {  // DegradeRuleManager.checkDegrade (DegradeRuleManager.java:72-85)
-                if (!degrade_pass(N, C, r, rs[s], t)) { status = ST_BLOCK_DEGRADE; slot = r.slot; }
+                if (!degrade_pass(N, C, deg_param(r), rs[s], t)) { status = ST_BLOCK_DEGRADE; slot = r.slot; }
             }
         }
     }
@@ -1011,18 +1011,19 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
     double fcnt[2] = {0.0, 0.0};
     bool fthr[2] = {false, false};
     uint32_t fslot[2] = {0, 0};
-    DRule dr[2];
+    DegParam dr[2];       // only the fields the checks read: the whole DRule would cost 28 VGPRs each
+    uint32_t dslot[2] = {0, 0};
     RState ds[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (k < nf) {
-            const DRule r = rules[k];
-            fcnt[k] = r.count;
-            fthr[k] = r.grade == SG_FLOW_GRADE_THREAD;
-            fslot[k] = r.slot;
+            fcnt[k] = rules[k].count;
+            fthr[k] = rules[k].grade == SG_FLOW_GRADE_THREAD;
+            fslot[k] = rules[k].slot;
         }
         if (k < nd) {
-            dr[k] = rules[nf + k];
+            dr[k] = deg_param(rules[nf + k]);
+            dslot[k] = rules[nf + k].slot;
             ds[k] = S.rstate[pg.rule_off + nf + k];
         }
     }
@@ -1096,7 +1097,7 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                 for (int k = 0; k < 2; ++k) {  // DegradeSlot
                     if (k < nd && status == ST_PASS && !degrade_pass(N, C, dr[k], ds[k], t)) {
                         status = ST_BLOCK_DEGRADE;
-                        slot = dr[k].slot;
+                        slot = dslot[k];
                     }
                 }
                 LPROF(ktg)

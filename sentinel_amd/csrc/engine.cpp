@@ -28,13 +28,12 @@ hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uin
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint32_t* prio,
                            uint64_t* key_ring, const uint32_t* comp, const sg_event_ext* ext, const sg_arg* args,
-                           uint64_t n_args, uint32_t max_ctx, int db, hipStream_t st);
+                           uint64_t n_args, uint32_t max_ctx, hipStream_t st);
 // db = digit bits (8 or 10)
-hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks, hipStream_t st,
-                             int db = 8);
+hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
+                             hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
-                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st,
-                                int db = 8);
+                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
 uint32_t radix_tile();
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
@@ -580,7 +579,7 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     uint64_t c = std::max<uint64_t>(n, 1u << 20);
     HIPCHK(hipStreamSynchronize(e->stream));  // no batch may use the old buffers
     uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
-    e->cap_hist = nblocks * 1024;  // 10-bit digits
+    e->cap_hist = nblocks * 256;  // 8-bit digit histograms
     for (auto& B : e->slot) {
         free_slot(B);
         HIPCHK(hipMalloc(&B.d_ev, c * sizeof(sg_event)));
@@ -1703,13 +1702,13 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
     HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
                            e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, e->d_comp, dev_ext,
-                           dev_args, n_args, SG_MAX_CONTEXTS, db, gs));
+                           dev_args, n_args, SG_MAX_CONTEXTS, gs));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     for (int p = 0; p < passes; ++p) {
-        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * db, e->d_hist, nblocks, gs, db));
+        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * db, e->d_hist, nblocks, gs));
         HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks << db, e->d_part, nullptr, gs));
         HIPCHK(launch_radix_scatter(kin, vin, n, p * db, e->d_hist, nblocks, kout, vout,
-                                    p == passes - 1 ? e->d_posof : nullptr, gs, db));
+                                    p == passes - 1 ? e->d_posof : nullptr, gs));
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
@@ -1824,17 +1823,18 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.aux_mask = e->aux_mask;
     S.max_ctx = SG_MAX_CONTEXTS;
     HIPCHK(hipEventRecord(e->fork, st));
-    const int coop[3] = {BIN_J16, BIN_J4, BIN_J1};
-    for (int c = 0; c < 3; ++c) {
+    // J16 and J4 on their own streams; J1 after the lane bins on the main stream (J4 + J1 in series was the
+    // longest chain of the decide stage)
+    const int coop[2] = {BIN_J16, BIN_J4};
+    for (int c = 0; c < 2; ++c) {
         const int b = coop[c];
         if (!bin_n[b]) continue;
         DevState Sb = S;
         Sb.dbg = (c == 0 && e->d_dbg) ? e->d_dbg : nullptr;
-        const int q = c == 0 ? 0 : 1;
-        HIPCHK(hipStreamWaitEvent(e->bin_stream[q], e->fork, 0));
+        HIPCHK(hipStreamWaitEvent(e->bin_stream[c], e->fork, 0));
         HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sb, dc, t0,
-                                 e->d_dec, e->d_bsmall + 0, e->bin_stream[q]));
-        HIPCHK(hipEventRecord(e->join[q], e->bin_stream[q]));
+                                 e->d_dec, e->d_bsmall + 0, e->bin_stream[c]));
+        HIPCHK(hipEventRecord(e->join[c], e->bin_stream[c]));
     }
     {
         DevState Sl = S;
@@ -1850,8 +1850,11 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
                                  off[BIN_LITE + LANE_BINS] - off[BIN_LITE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
     }
-    for (int c = 0; c < 3; ++c)
-        if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c == 0 ? 0 : 1], 0));
+    if (bin_n[BIN_J1])
+        HIPCHK(launch_decide_bin(BIN_J1, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J1], bin_n[BIN_J1], S, dc,
+                                 t0, e->d_dec, e->d_bsmall + 0, st));
+    for (int c = 0; c < 2; ++c)
+        if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));

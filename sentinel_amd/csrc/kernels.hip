@@ -177,8 +177,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __res
 // counts into digit-run offsets, and the tile is placed digit-sorted in LDS.  It then leaves in
 // digit runs, so the writes of a run are consecutive addresses.  The last pass also writes the
 // inverse permutation pos_of[idx] = sorted position | ENTRY bit.  (The per-block digit histograms
-// of k_rs_first / k_radix_hist count the same 4096-item tile, in any order.)  10-bit digits sort
-// 20-bit keys (1M resources) in two passes instead of three.
+// of k_rs_first / k_radix_hist count the same 4096-item tile, in any order.)  8-bit digits: two 10-bit
+// passes for 1M resources measured slower (1024 digit runs per 4096-item tile are too short to write
+// coalesced).
 template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
@@ -451,33 +452,24 @@ hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uin
                            uint64_t ring_mask, int32_t max_rt, SEv* rec_o, uint32_t* keys, uint32_t* vals,
                            uint32_t* ghist, uint32_t nblocks, uint32_t* bflags, int64_t* t0_out, uint32_t* prio,
                            uint64_t* key_ring, const uint32_t* comp, const sg_event_ext* ext, const sg_arg* args,
-                           uint64_t n_args, uint32_t max_ctx, int db, hipStream_t st) {
-    if (db == 10)
-        hipLaunchKernelGGL(k_rs_first<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
-                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp, ext, args,
-                           n_args, max_ctx);
-    else
-        hipLaunchKernelGGL(k_rs_first<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
-                           max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp, ext, args,
-                           n_args, max_ctx);
+                           uint64_t n_args, uint32_t max_ctx, hipStream_t st) {
+    hipLaunchKernelGGL(k_rs_first<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring, ring_mask,
+                       max_rt, rec_o, keys, vals, ghist, nblocks, bflags, t0_out, prio, key_ring, comp, ext, args,
+                       n_args, max_ctx);
     return hipGetLastError();
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
-                             hipStream_t st, int db) {
-    if (db == 10) hipLaunchKernelGGL(k_radix_hist<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
-    else hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
     return hipGetLastError();
 }
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
-                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st, int db) {
-    if (db == 10)
-        hipLaunchKernelGGL(k_radix_scatter<10>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                           kout, vout, pos_of);
-    else
-        hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                           kout, vout, pos_of);
+                                uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
+                       kout, vout, pos_of);
     return hipGetLastError();
 }
+
 uint32_t radix_tile() { return RS_TILE; }
 
 hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borrow, uint32_t nres, hipStream_t st) {
