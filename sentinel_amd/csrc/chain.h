@@ -343,7 +343,10 @@ struct DegParam {
     uint8_t grade;
 };
 __device__ __forceinline__ DegParam deg_param(const DRule& r) { return DegParam{r.count, r.time_window, r.grade}; }
-__device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DegParam& r, RState& s, int64_t t) {
+// exc_total: StatisticNode.totalException at t when the caller keeps it (k_lite), else read through the
+// node's cached minute bucket
+__device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DegParam& r, RState& s, int64_t t,
+                                             const int64_t* exc_total = nullptr) {
     if (s.a && t >= s.c) { s.a = 0; s.b = 0; }
     if (s.a) return false;
     if (r.grade == SG_DEGRADE_GRADE_RT) {
@@ -362,7 +365,7 @@ __device__ __forceinline__ bool degrade_pass(Node& N, const Ctx& C, const DegPar
         if (real <= 0 && exc < 5) return true;
         if (exc / succ < r.count) return true;
     } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) {
-        double e = (double)min_total_exc(N, C.minb, t, C.max_rt, C.pflags);
+        double e = (double)(exc_total ? *exc_total : min_total_exc(N, C.minb, t, C.max_rt, C.pflags));
         if (e < r.count) return true;
     }
     s.a = 1;

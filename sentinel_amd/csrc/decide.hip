@@ -996,7 +996,62 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
 // rules are read once per segment (not per event), the passed bits of the first 256 positions stay in
 // registers (EXITs of them never re-read dec[]), and the kernel carries none of the param / warm-up /
 // rate-limiter / borrow code, so its code fits the instruction cache and its state fits in VGPRs.
+//
+// Minute window: a lite segment is a cold resource, a few events per second, so nearly every event
+// opens a new second and the read of that second's bucket (to tell "same second, accumulate" from
+// "stale slot, reset") would be an HBM round trip on every event's critical path.  No check of a lite
+// segment reads the current second's minute bucket (the flow checks read the second window, the
+// exception-count breaker a running sum of expired seconds), so the events of a second accumulate
+// into register deltas and the bucket is read-modified-written when the segment moves on: its load is
+// issued at that second change and consumed at the next one, off the critical path.  (A bucket with a
+// later window start -- the clock went back a minute -- would need the old path's "detached" drop;
+// that only happens in a batch rejected with BF_BACKWARD.)
 // =================================================================================
+struct MinDelta {
+    int32_t p, b, s, rt, e, minrt;  // per-second deltas of a cold resource (<= 256 events) fit in int32
+};
+struct LiteMin {
+    int64_t T;      // second of the pending deltas (-1: none yet)
+    MinDelta pd;    // pending deltas of second T
+    bool fly;       // an RMW in flight: bucket fb (loaded at the last second change) + deltas fd of second fT
+    int64_t fT;
+    MinDelta fd;
+    Bkt fb;
+};
+__device__ __forceinline__ void md_zero(MinDelta& d) { d.p = d.b = d.s = d.rt = d.e = 0; d.minrt = INT32_MAX; }
+// LeapArray.currentWindow on the minute bucket of second T, then the second's additions
+__device__ __forceinline__ Bkt md_apply(Bkt b, int64_t T, const MinDelta& d, int32_t max_rt) {
+    if (b.ws > T) return b;  // detached: the additions are lost (Q3)
+    if (b.ws < T) bkt_reset(b, T, max_rt);
+    b.pass += d.p; b.block += d.b; b.succ += d.s; b.rt += d.rt; b.exc += d.e;
+    if ((int64_t)d.minrt < b.minrt) b.minrt = d.minrt;
+    return b;
+}
+__device__ __forceinline__ void lm_finish(LiteMin& L, Bkt* minb, int32_t max_rt) {
+    if (L.fly) {
+        minb[(L.fT / 1000) % 60] = md_apply(L.fb, L.fT, L.fd, max_rt);
+        L.fly = false;
+    }
+}
+// the event opens second T: the pending second goes in flight, the previous flight lands
+__device__ __forceinline__ void lm_roll(LiteMin& L, Node& N, Bkt* minb, int64_t T, int32_t max_rt, uint32_t pflags) {
+    lm_finish(L, minb, max_rt);
+    if (L.T >= 0) {
+        L.fb = minb[(L.T / 1000) % 60];  // consumed at the next second change
+        L.fT = L.T;
+        L.fd = L.pd;
+        L.fly = true;
+    }
+    L.T = T;
+    md_zero(L.pd);
+    // StatisticNode.totalException running sum (exc_advance): the seconds it reads are a minute old --
+    // never the one in flight -- except on a first full sum, which must see it
+    if ((pflags & PF_EXC_COUNT) && N.exc_sum_sec < T) {
+        if (N.exc_sum_sec < 0) lm_finish(L, minb, max_rt);
+        exc_advance(N, minb, T);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                               const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                               int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
@@ -1041,8 +1096,11 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
 #endif
     Node N;
     node_load(N, S, res);
-    N.pfslot = -1;  // minute-bucket prefetch on
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    LiteMin L;
+    L.T = -1;
+    L.fly = false;
+    md_zero(L.pd);
     const bool has_chain = (N.flags & NI_CHAIN) != 0;
     const bool chain = has_chain && cfg.switch_on;
     if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
@@ -1068,20 +1126,18 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
         cur[2] = cur[3];
         const uint32_t j = j0 + k;
         if (j >= sg.len) break;
-        SEv r;
-        r.dt = (int32_t)rw.x;
-        r.x = rw.y;
-        r.cnt = (uint16_t)(rw.z & 0xFFFFu);
-        r.rt = (uint16_t)(rw.z >> 16);
-        r.kind = (uint8_t)(rw.w & 0xFFu);
-        r.flags = (uint8_t)((rw.w >> 8) & 0xFFu);
-        r.code = (uint8_t)((rw.w >> 16) & 0xFFu);
-        r.pad = 0;
-        const int64_t t = t0 + r.dt;
+        const int32_t rdt = (int32_t)rw.x;
+        const uint32_t rx = rw.y;
+        const int cntv = (int)(rw.z & 0xFFFFu);
+        const int32_t rtv = (int32_t)(rw.z >> 16);
+        const uint32_t kind = rw.w & 0xFFu, code = (rw.w >> 16) & 0xFFu;
+        const int64_t t = t0 + rdt;
+        const int64_t T = t - t % 1000;
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
-        if (r.kind == SG_EV_ENTRY) {
+        if (kind == SG_EV_ENTRY) {
             if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
             else {
+                if (T != L.T) lm_roll(L, N, C.minb, T, C.max_rt, C.pflags);
                 uint32_t status = ST_PASS, slot = 0;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {  // FlowSlot: DefaultController on the ClusterNode
@@ -1089,20 +1145,31 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                         int32_t cur;
                         if (fthr[k]) cur = N.thread;
                         else { sec_current(N, t, C.max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
-                        if ((double)j_iadd(cur, (int)r.cnt) > fcnt[k]) { status = ST_BLOCK_FLOW; slot = fslot[k]; }
+                        if ((double)j_iadd(cur, cntv) > fcnt[k]) { status = ST_BLOCK_FLOW; slot = fslot[k]; }
                     }
                 }
                 LPROF(ktf)
+                // StatisticNode.totalException: exc_sum is at T after the roll (PF_EXC_COUNT)
+                const int64_t exc_total = N.exc_sum;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {  // DegradeSlot
-                    if (k < nd && status == ST_PASS && !degrade_pass(N, C, dr[k], ds[k], t)) {
+                    if (k < nd && status == ST_PASS && !degrade_pass(N, C, dr[k], ds[k], t, &exc_total)) {
                         status = ST_BLOCK_DEGRADE;
                         slot = dslot[k];
                     }
                 }
                 LPROF(ktg)
                 const bool passed = status == ST_PASS;
-                stat_entry(N, C, t, r.cnt, passed);
+                // StatisticSlot.entry: second window + the second's minute deltas
+                const int sl = sec_current(N, t, C.max_rt);
+                if (passed) {
+                    N.thread++;
+                    sec_add(N, sl, cntv, 0, 0, 0, 0, INT64_MAX);
+                    L.pd.p += cntv;
+                } else {
+                    sec_add(N, sl, 0, cntv, 0, 0, 0, INT64_MAX);
+                    L.pd.b += cntv;
+                }
                 LPROF(kth)
                 d = passed ? mk_dec(ST_PASS, 0, 0) : mk_dec(status, slot, 0);
                 if (passed && j < 256) {
@@ -1113,20 +1180,31 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
             LPROF(ktb)
         } else {
             bool eff;
-            if (r.code == RC_NONE) eff = r.kind == SG_EV_EXIT ? chain : has_chain;
-            else if (r.code == RC_PASSED) eff = true;
-            else if (r.code == RC_NOT) eff = false;
+            if (code == RC_NONE) eff = kind == SG_EV_EXIT ? chain : has_chain;
+            else if (code == RC_PASSED) eff = true;
+            else if (code == RC_NOT) eff = false;
             else {
-                const uint32_t rel = r.x - sg.start;
+                const uint32_t rel = rx - sg.start;
                 if (rel >= j) { atomicOr(bflags, BF_BAD_REF); eff = false; }  // not an earlier ENTRY of this resource
                 else if (rel < 256) {
                     const uint64_t w = rel < 64 ? pm0 : rel < 128 ? pm1 : rel < 192 ? pm2 : pm3;
                     eff = ((w >> (rel & 63)) & 1) != 0;
-                } else eff = st_passed(dec[r.x] & 0xFF);  // written by this lane
+                } else eff = st_passed(dec[rx] & 0xFF);  // written by this lane
             }
-            if (eff) {
-                if (r.kind == SG_EV_EXIT) stat_exit(N, C, t, r.cnt, r.rt);
-                else stat_trace(N, C, t, r.cnt);
+            if (eff && kind == SG_EV_EXIT) {  // StatisticSlot.exit
+                if (T != L.T) lm_roll(L, N, C.minb, T, C.max_rt, C.pflags);
+                const int sl = sec_current(N, t, C.max_rt);
+                sec_add(N, sl, 0, 0, cntv, rtv, 0, rtv);
+                L.pd.s += cntv;
+                L.pd.rt += rtv;
+                if (rtv < L.pd.minrt) L.pd.minrt = rtv;
+                N.thread--;
+            } else if (eff && cntv > 0) {  // ClusterNode.trace
+                if (T != L.T) lm_roll(L, N, C.minb, T, C.max_rt, C.pflags);
+                const int sl = sec_current(N, t, C.max_rt);
+                sec_add(N, sl, 0, 0, 0, 0, cntv, INT64_MAX);
+                L.pd.e += cntv;
+                if (N.exc_sum_sec == T) N.exc_sum += cntv;
             }
             LPROF(ktc)
         }
@@ -1135,7 +1213,12 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
 #pragma unroll
     for (uint32_t k = 0; k < CH; ++k) cur[k] = nxt[k];
     }
-    min_flush(N, C.minb);
+    // the last two seconds' minute buckets
+    lm_finish(L, C.minb, C.max_rt);
+    if (L.T >= 0) {
+        Bkt* b = C.minb + (L.T / 1000) % 60;
+        *b = md_apply(*b, L.T, L.pd, C.max_rt);
+    }
     node_store(N, S, res, pg.pflags);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -1336,7 +1419,7 @@ __device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, int n
 }
 
 template <int NW, int WINLOG, int MF, int MD, bool RL, bool SKIP>
-__global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? 4 : 1))) void k_jac(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                                 const uint32_t* __restrict__ order, uint32_t m, DevState S,
                                                 DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec,
                                                 uint32_t* __restrict__ bflags) {
@@ -1864,7 +1947,7 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
                     WAVE_SCAN(v, 0u, op_add);
                     ex[k] = v - q[k];
                 }
-                if (lane == 63) sh.part[wv][k] = v;
+                if (NW > 1 && lane == 63) sh.part[wv][k] = v;  // one wave: its prefixes are the block's
             }
         }
         // rate limiters: exclusive prefix of the costs (C) and the max-plus term (M) of updating lanes
@@ -1892,8 +1975,11 @@ __global__ __launch_bounds__(NW * 64) void k_jac(const SEv* __restrict__ recs, c
         PROF_MARK(1)
         lds_barrier();  // B2
         PROF_MARK(2)
-        uint32_t inr_total = 0;
-        {
+        uint32_t inr_total;
+        if (NW == 1) {  // lane 63's inclusive in-round count
+            const uint32_t own = inr ? 1u : 0u;
+            inr_total = (uint32_t)__builtin_amdgcn_readlane((int)((ex[Q_TI] >> 16) + own), 63);
+        } else {
             // block-wide: lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv
 #pragma unroll
             for (int k = 0; k < NQ; ++k) {

@@ -1826,15 +1826,18 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // J16 and J4 on their own streams; J1 after the lane bins on the main stream (J4 + J1 in series was the
     // longest chain of the decide stage)
     const int coop[2] = {BIN_J16, BIN_J4};
+    // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
+    const bool serial_bins = (e->dbg_flags & 8) != 0;
     for (int c = 0; c < 2; ++c) {
         const int b = coop[c];
         if (!bin_n[b]) continue;
         DevState Sb = S;
         Sb.dbg = (c == 0 && e->d_dbg) ? e->d_dbg : nullptr;
-        HIPCHK(hipStreamWaitEvent(e->bin_stream[c], e->fork, 0));
+        hipStream_t bs = serial_bins ? st : e->bin_stream[c];
+        if (!serial_bins) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
         HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sb, dc, t0,
-                                 e->d_dec, e->d_bsmall + 0, e->bin_stream[c]));
-        HIPCHK(hipEventRecord(e->join[c], e->bin_stream[c]));
+                                 e->d_dec, e->d_bsmall + 0, bs));
+        HIPCHK(hipEventRecord(e->join[c], bs));
     }
     {
         DevState Sl = S;
