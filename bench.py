@@ -13,9 +13,9 @@ the timed region (timestamps + k x the trace span, EXIT/TRACE references + k x t
 trace), so every batch is fresh to the engine -- time only moves forward, windows roll, breakers
 trip and reset -- and nothing is replayed.  A step is --sub-batches consecutive global batches
 submitted back to back through the engine's two-stage pipeline (sg_submit_async: the group stage of
-batch k+1 overlaps the decide stage of batch k); the default sizes it so the timed region is long
-(~1 s) while the inputs of all timed steps fit in HBM, and is printed in config.  Inputs are
-resident in HBM when the timed region starts.
+batch k+1 overlaps the decide stage of batch k); the default sizes it so that the inputs of all timed
+steps take 80 % of the free HBM (~220 global batches, a ~1 s timed region), and is printed in config.
+Inputs are resident in HBM when the timed region starts.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): ONE C4 trace,
 resources sharded by splitmix64(res_id) % N (strong scaling).  Every rank generates the same trace
@@ -56,8 +56,9 @@ def parse():
     p.add_argument("--batch-events", type=int, default=1 << 25, help="events per global batch")
     p.add_argument("--base-batches", type=int, default=8, help="global batches generated on the host")
     p.add_argument("--sub-batches", type=int, default=0, help="global batches per step (0: auto)")
-    p.add_argument("--max-sub-batches", type=int, default=12)
-    p.add_argument("--hbm-budget", type=float, default=0.6, help="fraction of free HBM for step inputs")
+    p.add_argument("--max-sub-batches", type=int, default=64)
+    p.add_argument("--hbm-budget", type=float, default=0.8,
+                   help="fraction of free HBM for the timed steps' inputs (sets the timed region's length, ~1 s)")
     p.add_argument("--resources", type=int, default=1_000_000)
     p.add_argument("--cpu-threads", type=int, default=0, help="partitioned oracle threads (0: min(16, cores))")
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)

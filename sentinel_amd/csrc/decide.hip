@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ k
 // inside their limits, one lane per segment for everything else.  Per-block bin counts go to
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
-__global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_t m, uint64_t n,
+__global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const uint32_t* __restrict__ mp, uint64_t n,
                                                  const Prog* __restrict__ prog, const uint32_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
+    const uint32_t m = *mp;  // segment count (the grid covers an upper bound: no host round trip)
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < m) {
         Seg sg = segs[s];
@@ -159,19 +160,21 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, uint32_
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) blkcnt[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
 }
 // bin-major dispatch list: order[off[bin][block] + rank] = segment
-__global__ __launch_bounds__(256) void k_seg_order(Seg* __restrict__ segs, uint32_t m, const uint32_t* __restrict__ off,
-                                                   uint32_t nblk, uint32_t* __restrict__ order) {
+__global__ __launch_bounds__(256) void k_seg_order(Seg* __restrict__ segs, const uint32_t* __restrict__ mp,
+                                                   const uint32_t* __restrict__ off, uint32_t nblk,
+                                                   uint32_t* __restrict__ order) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= m) return;
+    if (s >= *mp) return;
     const uint32_t v = segs[s].bin, bin = v & 0xFF;
     order[off[(uint64_t)bin * nblk + blockIdx.x] + (v >> 8)] = s;
     segs[s].bin = bin;
 }
 // per-bin first offsets (+ total) for the host: out[b] = off[b][0], out[N_BINS] = m
-__global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, uint32_t m, uint32_t* __restrict__ out) {
+__global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, const uint32_t* __restrict__ mp,
+                              uint32_t* __restrict__ out) {
     const uint32_t b = threadIdx.x;
     if (b < N_BINS) out[b] = off[(uint64_t)b * nblk];
-    if (b == N_BINS) out[b] = m;
+    if (b == N_BINS) out[b] = *mp;
 }
 
 // =================================================================================
@@ -2291,21 +2294,22 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
     hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs);
     return hipGetLastError();
 }
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint32_t* prio, uint32_t lane_max,
-                          uint32_t j1_max,
-                          uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st) {
-    if (!m) return hipSuccess;
-    const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, m, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
+// mp: the segment count on the device; mb: an upper bound of it (the grid)
+hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
+                          uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
+                          hipStream_t st) {
+    const uint32_t nblk = (mb + 255) / 256;
+    if (!nblk) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
                        blkcnt, nblk);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]
-hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
-                            hipStream_t st) {
-    const uint32_t nblk = (m + 255) / 256;
-    if (m) hipLaunchKernelGGL(k_seg_order, dim3(nblk), dim3(256), 0, st, segs, m, off, nblk, order);
-    hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(64), 0, st, off, nblk ? nblk : 1, m, bin_off);
+hipError_t launch_seg_order(Seg* segs, const uint32_t* mp, uint32_t mb, const uint32_t* off, uint32_t* order,
+                            uint32_t* bin_off, hipStream_t st) {
+    const uint32_t nblk = (mb + 255) / 256;
+    if (nblk) hipLaunchKernelGGL(k_seg_order, dim3(nblk), dim3(256), 0, st, segs, mp, off, nblk, order);
+    hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(64), 0, st, off, nblk ? nblk : 1, mp, bin_off);
     return hipGetLastError();
 }
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,

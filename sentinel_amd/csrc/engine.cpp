@@ -45,11 +45,11 @@ hipError_t launch_region_copy(const PSlot* src, PSlot* dst, const uint64_t* tri,
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
-hipError_t launch_seg_bin(Seg* segs, uint32_t m, uint64_t n, const Prog* prog, const uint32_t* prio, uint32_t lane_max,
-                          uint32_t j1_max,
-                          uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt, hipStream_t st);
-hipError_t launch_seg_order(Seg* segs, uint32_t m, const uint32_t* off, uint32_t* order, uint32_t* bin_off,
-                            hipStream_t st);
+hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
+                          uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
+                          hipStream_t st);
+hipError_t launch_seg_order(Seg* segs, const uint32_t* mp, uint32_t mb, const uint32_t* off, uint32_t* order,
+                            uint32_t* bin_off, hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
                          const uint32_t* pos_of, SEv* recs, uint32_t* prev, uint32_t* nprev, Link* link, uint32_t* bst,
                          uint32_t epoch, uint32_t* bflags, hipStream_t st);
@@ -1717,8 +1717,18 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (++e->epoch == 0) e->epoch = 1;
     HIPCHK(launch_gather(e->d_rec_o, vin, kin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link, e->d_bst,
                          e->epoch, e->d_bsmall + 0, gs));
-    uint32_t head[6];
+    // bins + bin-ordered dispatch list (per-block counts -> scan -> placement), sized by an upper bound of
+    // the segment count so that the group stage needs one host round trip
+    const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
+    const uint32_t mb = (uint32_t)std::min<uint64_t>(n, R);
+    const uint32_t nblk = (mb + 255) / 256;
+    HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, e->lane_max, e->j1_max, e->j4_max,
+                          force_lane ? 1 : 0, e->d_blkcnt, gs));
+    HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
+    HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
+    uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
+    HIPCHK(hipEventRecord(B.ev[1], gs));
     HIPCHK(hipStreamSynchronize(gs));
     const uint32_t m = head[1];
     const uint32_t nprev = head[3];
@@ -1732,17 +1742,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
     if (bflags & BF_BAD_ARGS)
         return fail(SG_EINVAL, "an sg_event_ext names args outside the table (or more than SG_MAX_ARGS, or a bad kind)");
-    // bins + bin-ordered dispatch list (per-block counts -> scan -> placement)
-    const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
-    const uint32_t nblk = (m + 255) / 256;
-    HIPCHK(launch_seg_bin(e->d_segs, m, n, e->d_prog, e->d_prio, e->lane_max, e->j1_max, e->j4_max, force_lane ? 1 : 0,
-                          e->d_blkcnt, gs));
-    HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
-    HIPCHK(launch_seg_order(e->d_segs, m, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
-    uint32_t off[N_BINS + 1];
-    HIPCHK(hipMemcpyAsync(off, e->d_bsmall + 8, sizeof(off), hipMemcpyDeviceToHost, gs));
-    HIPCHK(hipEventRecord(B.ev[1], gs));
-    HIPCHK(hipStreamSynchronize(gs));
+    const uint32_t* off = head + 8;
     uint32_t bin_n[N_BINS];
     for (int b = 0; b < N_BINS; ++b) bin_n[b] = off[b + 1] - off[b];
     // ---- decide stage, in order after the previous batch's: references into earlier batches first
