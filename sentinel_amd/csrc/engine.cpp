@@ -505,6 +505,7 @@ struct sg_engine {
     uint64_t* d_keyring = nullptr;  // ENTRY arg keys by global index (exit(count, args)); once param rules exist
     uint64_t* d_cand = nullptr;
     uint32_t dbg_flags = 0;
+    int prof_bin = 0;            // SG_PROF_BIN: which cooperative bin (0 J16, 1 J4, 2 J1) fills the SG_DEBUG counters
     unsigned long long* d_dbg = nullptr;  // SG_DEBUG=1: [0..63] counters of the J16 bin
     uint64_t cap_hist = 0;
     uint64_t gbase = 0;
@@ -1010,6 +1011,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         if (d[0] == '1' && hipMalloc(&e->d_dbg, 64 * 8) == hipSuccess) (void)hipMemset(e->d_dbg, 0, 64 * 8);
     }
     if (const char* f = std::getenv("SG_DEBUG_FLAGS")) e->dbg_flags = (uint32_t)std::strtoul(f, nullptr, 0);
+    if (const char* f = std::getenv("SG_PROF_BIN")) e->prof_bin = std::atoi(f);  // SG_DEBUG counters of J16/J4/J1
     // decide-bin thresholds (segment lengths); tuning knobs, the defaults are the measured best
     if (const char* v = std::getenv("SG_LANE_MAX")) e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
@@ -1832,7 +1834,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         const int b = coop[c];
         if (!bin_n[b]) continue;
         DevState Sb = S;
-        Sb.dbg = (c == 0 && e->d_dbg) ? e->d_dbg : nullptr;
+        Sb.dbg = (c == e->prof_bin && e->d_dbg) ? e->d_dbg : nullptr;
         hipStream_t bs = serial_bins ? st : e->bin_stream[c];
         if (!serial_bins) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
         HIPCHK(launch_decide_bin(b, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sb, dc, t0,
@@ -1853,9 +1855,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
                                  off[BIN_LITE + LANE_BINS] - off[BIN_LITE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
     }
-    if (bin_n[BIN_J1])
-        HIPCHK(launch_decide_bin(BIN_J1, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J1], bin_n[BIN_J1], S, dc,
+    if (bin_n[BIN_J1]) {
+        DevState Sj = S;
+        Sj.dbg = (e->prof_bin == 2 && e->d_dbg) ? e->d_dbg : nullptr;
+        HIPCHK(launch_decide_bin(BIN_J1, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J1], bin_n[BIN_J1], Sj, dc,
                                  t0, e->d_dec, e->d_bsmall + 0, st));
+    }
     for (int c = 0; c < 2; ++c)
         if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped

@@ -1,4 +1,4 @@
-"""Diagnostics: counters of the cooperative J16 bin (SG_DEBUG=1) on a C4 batch.
+"""Diagnostics: counters of one cooperative bin (SG_DEBUG=1; SG_PROF_BIN = 0 J16, 1 J4, 2 J1) on a C4 batch.
 
 usage: python tools/hotprobe.py [config] [n_entries] [batches]
 """
@@ -40,7 +40,7 @@ for i in range(nb):
     v = np.array(list(buf), dtype=np.uint64)
     d = v
     print("batch %d: %d events, wall %.1f ms, group %.2f ms, decide %.2f ms" % (i, B, (time.time() - t) * 1e3, tm[0], tm[1]))
-    print("  J16 bin: segs %d iterations %d rounds %d tiles %d mismatched-iterations %d" % (d[4], d[0], d[1], d[2], d[3]))
+    print("  bin %s: segs %d iterations %d rounds %d tiles %d mismatched-iterations %d" % (os.environ.get("SG_PROF_BIN", "0"), d[4], d[0], d[1], d[2], d[3]))
     ph = v[8:18].astype(np.float64)
     tot = ph.sum() or 1
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
