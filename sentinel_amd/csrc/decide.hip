@@ -214,44 +214,17 @@ __global__ __launch_bounds__(256) void k_scatter_rec(const SEv* __restrict__ rec
 }
 // ENTRY count sum of every 1024 sorted positions (one workgroup each, 4 positions per lane), and the
 // forward link of every same-batch referenced ENTRY: walked in sorted order, an EXIT/TRACE and its
-// ENTRY sit in the same segment a few positions apart, so the link atomics stay in cache (an atomic
-// exchange detects a second EXIT/TRACE naming the same ENTRY).
-__global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, uint64_t n, uint32_t* __restrict__ bst,
-                                                    Link* __restrict__ link, uint32_t epoch,
-                                                    uint32_t* __restrict__ bflags) {
+// ENTRY sit in the same segment a few positions apart, so the link atomics and the key loads stay in
+// cache.  The exchange returns the link's previous value: one of this batch's epoch means a second
+// EXIT (or TRACE) named the same ENTRY (BF_MULTI_LINK: frozen-stretch skipping is off for the batch).
+// A reference must also name an ENTRY of its own resource: the two carry the same sort key (inside a
+// STRATEGY_RELATE component the key is the component's).
+__global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, const uint32_t* __restrict__ skeys,
+                                                    uint64_t n, uint32_t* __restrict__ bst, Link* __restrict__ link,
+                                                    uint32_t epoch, uint32_t* __restrict__ bflags) {
     __shared__ uint32_t wsum[4];
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
     uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
-        if (p < n) {
-            const uint4 w = reinterpret_cast<const uint4*>(recs)[p];
-            SEv r;
-            __builtin_memcpy(&r, &w, sizeof(r));
-            if (r.kind == SG_EV_ENTRY) v += r.cnt;
-            else if (r.code == RC_BATCH) {  // plain store; k_link_verify detects a second EXIT/TRACE
-                uint64_t* dst = r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l;
-                *dst = ((uint64_t)epoch << 32) | (uint32_t)p;
-            }
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t sum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        if (sum) atomicAdd(&bst[blockIdx.x], sum);
-    }
-}
-// Every same-batch EXIT/TRACE must find its own position in its ENTRY's link after k_block_sums'
-// plain stores: a mismatch means a second EXIT (or TRACE) named the same ENTRY.  It must also name an
-// ENTRY of its own resource: the two carry the same sort key (in sorted order they sit a few positions
-// apart, so the key loads hit cache; inside a STRATEGY_RELATE component the key is the component's).
-__global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ recs, const uint32_t* __restrict__ skeys,
-                                                     uint64_t n, const Link* __restrict__ link, uint32_t epoch,
-                                                     uint32_t* __restrict__ bflags) {
-    const uint64_t base = (uint64_t)blockIdx.x * 1024;
     bool multi = false, bad = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -260,15 +233,25 @@ __global__ __launch_bounds__(256) void k_link_verify(const SEv* __restrict__ rec
             const uint4 w = reinterpret_cast<const uint4*>(recs)[p];
             SEv r;
             __builtin_memcpy(&r, &w, sizeof(r));
-            if (r.kind != SG_EV_ENTRY && r.code == RC_BATCH) {
-                const uint64_t v = r.kind == SG_EV_EXIT ? link[r.x].exit_l : link[r.x].trace_l;
-                if (v != (((uint64_t)epoch << 32) | (uint32_t)p)) multi = true;
+            if (r.kind == SG_EV_ENTRY) v += r.cnt;
+            else if (r.code == RC_BATCH) {
+                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
+                    r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
+                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
+                if ((uint32_t)(old >> 32) == epoch) multi = true;
                 if (skeys[r.x] != skeys[p]) bad = true;
             }
         }
     }
     if (__ballot(multi) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_MULTI_LINK);
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_BAD_REF);
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t sum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (sum) atomicAdd(&bst[blockIdx.x], sum);
+    }
 }
 // references into earlier batches, once those are decided: the ENTRY's status from the ring
 // (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
@@ -1421,15 +1404,67 @@ __device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, int n
     return mk_dec((int)o < nf ? ST_BLOCK_FLOW : ST_BLOCK_DEGRADE, rules[o].slot, 0);
 }
 
-template <int NW, int WINLOG, int MF, int MD, bool RL, bool SKIP>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? 4 : 1))) void k_jac(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
-                                                const uint32_t* __restrict__ order, uint32_t m, DevState S,
-                                                DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec,
-                                                uint32_t* __restrict__ bflags) {
+// one event of a k_jac tile, decoded once when its tile is loaded
+struct JEv {
+    int32_t dt;   // time relative to t0
+    uint32_t cz;  // count | rt << 16
+    uint32_t kf;  // kind (0xFF: no event) | JK_VALID | JK_WIN | JK_VAL
+    uint32_t wi;  // JK_WIN: status-window index of the referenced ENTRY
+};
+enum : uint32_t { JK_VALID = 0x100u, JK_WIN = 0x200u, JK_VAL = 0x400u };
+// an event's class in one Jacobi iteration: in the round, ENTRY, effective EXIT, effective TRACE
+enum : uint32_t { JC_INR = 1u, JC_ENT = 2u, JC_XE = 4u, JC_TE = 8u };
+
+// the scanned quantities (Q_*) of one event under its outcome guess g
+template <int NQ>
+__device__ __forceinline__ void jac_q(uint32_t (&q)[NQ], uint32_t c, uint32_t g, uint32_t cz, uint32_t nr, uint32_t nf) {
+    const uint32_t cnt = cz & 0xFFFFu, rtv = cz >> 16;
+    const bool ent = (c & JC_ENT) != 0, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0;
+    const bool gp = ent && g == nr;
+    q[Q_P] = gp ? cnt : 0u;
+    q[Q_B] = (ent && !gp) ? cnt : 0u;
+    q[Q_S] = xe ? cnt : 0u;
+    q[Q_RT] = xe ? rtv : 0u;
+    q[Q_E] = te ? cnt : 0u;
+    q[Q_TH] = gp ? 1u : (xe ? 0xFFFFFFFFu : 0u);
+    q[Q_MIN] = xe ? rtv : NO_LANE;
+    q[Q_TI] = ((ent || xe || te) ? 1u : 0u) | ((c & JC_INR) ? 0x10000u : 0u);
+#pragma unroll
+    for (int k = Q_TR; k < NQ; ++k) {  // guessed breaker trips, two degrade stages per word
+        const uint32_t s0 = nf + 2u * (uint32_t)(k - Q_TR);
+        q[k] = (ent && g == s0) ? 1u : (ent && g == s0 + 1u) ? 0x10000u : 0u;
+    }
+}
+template <int NQ>
+__device__ __forceinline__ void jac_acc(uint32_t (&a)[NQ], const uint32_t (&q)[NQ]) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) a[k] = k == Q_MIN ? op_min(a[k], q[k]) : a[k] + q[k];
+}
+template <int NQ>
+__device__ __forceinline__ void jac_zero(uint32_t (&a)[NQ]) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) a[k] = k == Q_MIN ? NO_LANE : 0u;
+}
+// a rate limiter's latestPassedTime moves for this ENTRY under outcome g (it passed stage s)
+__device__ __forceinline__ bool rl_upd(const DRule& r, uint32_t c, uint32_t g, int s, int cnt) {
+    return (c & JC_ENT) && g > (uint32_t)s &&
+           (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || (cnt > 0 && r.count > 0));
+}
+
+// NW wavefronts own one segment; each lane takes EP consecutive events of a tile (TILE = NW * 64 * EP
+// positions), so one chain of scans and barriers -- the latency that bounds an iteration -- decides
+// up to TILE events: a lane folds its events' quantities sequentially, the wave and block scans run on
+// the lane totals, and each event's view is the lane's exclusive prefix plus its running sum.
+template <int NW, int EP, int WINLOG, int MF, int MD, bool RL, bool SKIP>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? (EP == 1 ? 4 : 2) : (EP == 1 ? 1 : 2)))) void k_jac(
+    const SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t m,
+    DevState S, DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     constexpr uint32_t HW = NW * 64;
+    constexpr uint32_t TILE = HW * EP;  // positions per tile; lane l holds [l * EP, l * EP + EP)
     constexpr uint32_t WIN = 1u << WINLOG;
     constexpr int NQ = Q_TR + (MD + 1) / 2;
-    static_assert(WIN >= 2 * HW, "status window must hold two tiles");
+    static_assert(WIN >= 2 * TILE, "status window must hold two tiles");
+    static_assert(TILE < 0x10000u, "counts of a tile are packed in 16 bits");
     __shared__ JacSh<NW, MF, MD> sh;
     __shared__ __attribute__((aligned(16))) uint8_t win[WIN];
     if (blockIdx.x >= m) return;
@@ -1496,15 +1531,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
 #define PROF_MARK(k)
 #endif
 
-    // ---- per-lane tile state
+    // ---- per-lane tile state: EP consecutive events
     uint32_t tbase = 0;
-    SEv cur, nxt;
-    cur.kind = 0xFF;
-    nxt.kind = 0xFF;
-    if (tid < sg.len) cur = recs[sg.start + tid];
-    if (HW + tid < sg.len) nxt = recs[sg.start + HW + tid];
-    bool valid = false, eff_win = false, eff_val = false;
-    uint32_t winidx = 0, refrel = 0, kind = 0xFF, cnt = 0, rtv = 0;
+    const uint32_t lp0 = tid * EP;  // tile-relative position of the lane's first event
+    SEv nxt[EP];                    // the next tile, in flight
+    JEv ev[EP];
+    uint32_t gg[EP];  // outcome guesses: index of the blocking stage, nr = pass
     const bool skip_on = SKIP && S.skip_ok && (pg.pflags & PF_FROZEN);
     // positions of skipped spans: blocked ENTRYs whose dec[] words k_fill writes after this kernel
     auto in_span = [&](uint32_t rel) -> bool {
@@ -1514,57 +1546,75 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             if (rel >= sh.spn[i].x && rel < sh.spn[i].y) return true;
         return false;
     };
-    int32_t dt = 0;  // event time relative to t0 (the absolute time is t0 + dt)
-    auto decode = [&](const SEv& r, uint32_t pos) {
-        valid = pos < sg.len;
-        kind = valid ? r.kind : 0xFFu;
-        dt = valid ? r.dt : 0;
-        cnt = r.cnt;
-        rtv = r.rt;
-        eff_win = false;
-        eff_val = false;
-        refrel = NO_LANE;
-        if (valid && kind != SG_EV_ENTRY) {
-            if (r.code == RC_NONE || r.code == RC_PASSED) eff_val = true;  // the chain exists here
+    auto decode = [&](const SEv& r, uint32_t pos) -> JEv {
+        JEv x;
+        const bool valid = pos < sg.len;
+        x.dt = valid ? r.dt : 0;
+        x.cz = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
+        x.kf = valid ? ((uint32_t)r.kind | JK_VALID) : 0xFFu;
+        x.wi = 0;
+        if (valid && r.kind != SG_EV_ENTRY) {
+            if (r.code == RC_NONE || r.code == RC_PASSED) x.kf |= JK_VAL;  // the chain exists here
             else if (r.code == RC_BATCH) {
-                refrel = r.x - sg.start;
+                uint32_t refrel = r.x - sg.start;
                 if (refrel >= pos) { atomicOr(bflags, BF_BAD_REF); refrel = 0; }  // not an earlier ENTRY of this resource
-                if (refrel + WIN >= tbase + HW) { eff_win = true; winidx = refrel & (WIN - 1); }
-                else  // decided >= WIN-HW positions ago, i.e. before >= 1 full fence
-                    eff_val = !in_span(refrel) &&
-                              st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                if (refrel + WIN >= tbase + TILE) { x.kf |= JK_WIN; x.wi = refrel & (WIN - 1); }
+                else if (!in_span(refrel) &&  // decided >= WIN-TILE positions ago, i.e. before >= 1 full fence
+                         st_passed(__hip_atomic_load(&dec[r.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFF))
+                    x.kf |= JK_VAL;
             }
         }
+        return x;
     };
-    static_assert(WIN - HW >= (FULL_FENCE_TILES + 1) * HW, "old references must be older than one full fence");
+    auto load = [&](SEv (&dst)[EP], uint32_t tb) {
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            const uint32_t p = tb + lp0 + (uint32_t)e;
+            dst[e].kind = 0xFF;
+            if (p < sg.len) dst[e] = recs[sg.start + p];
+        }
+    };
+    // guesses g0 for the tile's events; the window statuses of those at positions >= from
+    auto guess_all = [&](uint32_t g0, uint32_t from) {
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            gg[e] = g0;
+            if ((ev[e].kf & JK_VALID) && lp0 + (uint32_t)e >= from)
+                win[(tbase + lp0 + e) & (WIN - 1)] = ((ev[e].kf & 0xFFu) == SG_EV_ENTRY && g0 == (uint32_t)nr) ? 1 : 0;
+        }
+    };
+    static_assert(WIN - TILE >= (FULL_FENCE_TILES + 1) * TILE, "old references must be older than one full fence");
     auto advance = [&]() {  // next tile (uniform)
-        tbase += HW;
-        cur = nxt;
+        tbase += TILE;
         // decode first: a (rare) old-reference load must not queue behind the prefetch below,
         // vmcnt retires in order
-        decode(cur, tbase + tid);
-        nxt.kind = 0xFF;
-        if (tbase + HW + tid < sg.len) nxt = recs[sg.start + tbase + HW + tid];
+#pragma unroll
+        for (int e = 0; e < EP; ++e) ev[e] = decode(nxt[e], tbase + lp0 + e);
+        load(nxt, tbase + TILE);
         ++n_tile;
-        if ((tbase / HW) % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
+        if ((tbase / TILE) % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
     };
-    decode(cur, tid);
-    uint32_t g = (uint32_t)nr;  // outcome guess: index of the blocking stage, nr = pass
-    if (valid) win[tid & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
-    if (tid == 0) sh.tnext = t0 + dt;
+    {
+        SEv cur[EP];
+        load(cur, 0);
+        load(nxt, TILE);
+#pragma unroll
+        for (int e = 0; e < EP; ++e) ev[e] = decode(cur[e], lp0 + e);
+    }
+    guess_all((uint32_t)nr, 0);
+    if (tid == 0) sh.tnext = t0 + ev[0].dt;
     __syncthreads();
     uint32_t mb = 0;  // mism double-buffer index
 
     for (;;) {
         uint32_t c0 = uni(sh.c0);
-        const uint32_t cnt_t = sg.len - tbase < HW ? sg.len - tbase : HW;
+        const uint32_t cnt_t = sg.len - tbase < TILE ? sg.len - tbase : TILE;
         if (c0 >= cnt_t) {  // tile done: advance (uniform)
-            if (tbase + HW >= sg.len) break;
+            if (tbase + TILE >= sg.len) break;
             advance();
-            g = sh.last_out;
-            if (valid) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
+            guess_all(sh.last_out, 0);
             lds_barrier();  // everyone has read sh.last_out / sh.c0
-            if (tid == 0) { sh.c0 = 0; sh.tnext = t0 + dt; }
+            if (tid == 0) { sh.c0 = 0; sh.tnext = t0 + ev[0].dt; }
             lds_barrier();
             c0 = 0;
         }
@@ -1885,16 +1935,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin;
                 }
                 // re-enter the tile machinery at the stop position; guesses = the frozen verdict
-                tbase = fend / HW * HW;
+                tbase = fend / TILE * TILE;
                 c0 = fend - tbase;
-                cur.kind = 0xFF;
-                nxt.kind = 0xFF;
-                if (tbase + tid < sg.len) cur = recs[sg.start + tbase + tid];
-                if (tbase + HW + tid < sg.len) nxt = recs[sg.start + tbase + HW + tid];
-                decode(cur, tbase + tid);
-                g = (cutk0 && !sat) ? (uint32_t)nf : 0u;
-                if (valid && tid >= c0) win[(tbase + tid) & (WIN - 1)] = (kind == SG_EV_ENTRY && g == (uint32_t)nr) ? 1 : 0;
-                if (valid && tid == c0) sh.tnext = t0 + dt;
+                {
+                    SEv cur[EP];
+                    load(cur, tbase);
+                    load(nxt, tbase + TILE);
+#pragma unroll
+                    for (int e = 0; e < EP; ++e) ev[e] = decode(cur[e], tbase + lp0 + e);
+                }
+                const uint32_t g = (cutk0 && !sat) ? (uint32_t)nf : 0u;
+                guess_all(g, c0);
+#pragma unroll
+                for (int e = 0; e < EP; ++e)
+                    if ((ev[e].kf & JK_VALID) && lp0 + (uint32_t)e == c0) sh.tnext = t0 + ev[e].dt;
                 __syncthreads();
                 if (tid == 0) {
                     for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
@@ -1912,49 +1966,47 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         }
 
         // ================= Jacobi iteration =================
-        const bool inr = valid && tid >= c0 && dt >= dlo && dt < dhi;
-        const bool ent = inr && kind == SG_EV_ENTRY;
-        const int64_t t = t0 + dt;
-        const bool eff = eff_win ? (win[winidx] != 0) : eff_val;
-        const bool xe = inr && kind == SG_EV_EXIT && eff;
-        const bool te = inr && kind == SG_EV_TRACE && eff && cnt > 0;
         const uint32_t has_sync = sh.has_sync;
-
-        // ---- phase B: counter deltas under the guesses, wave scans
-        uint32_t ex[NQ];
-        {
-            const bool gp = ent && g == (uint32_t)nr;
-            uint32_t q[NQ];
-            q[Q_P] = gp ? cnt : 0u;
-            q[Q_B] = (ent && !gp) ? cnt : 0u;
-            q[Q_S] = xe ? cnt : 0u;
-            q[Q_RT] = xe ? rtv : 0u;
-            q[Q_E] = te ? cnt : 0u;
-            q[Q_TH] = gp ? 1u : (xe ? 0xFFFFFFFFu : 0u);
-            q[Q_MIN] = xe ? rtv : NO_LANE;
-            q[Q_TI] = ((ent || xe || te) ? 1u : 0u) | (inr ? 0x10000u : 0u);
+        uint32_t cls[EP];  // JC_* of each event under the current guesses
 #pragma unroll
-            for (int k = 0; k < (MD + 1) / 2; ++k) {
-                uint32_t w = 0;
-                if (ent && g == (uint32_t)(nf + 2 * k)) w |= 1u;
-                if (ent && g == (uint32_t)(nf + 2 * k + 1)) w |= 0x10000u;
-                q[Q_TR + k] = w;
+        for (int e = 0; e < EP; ++e) {
+            const uint32_t kf = ev[e].kf, kind = kf & 0xFFu;
+            const bool inr = (kf & JK_VALID) && lp0 + (uint32_t)e >= c0 && ev[e].dt >= dlo && ev[e].dt < dhi;
+            const bool eff = (kf & JK_WIN) ? (win[ev[e].wi] != 0) : ((kf & JK_VAL) != 0);
+            uint32_t c = 0;
+            if (inr) {
+                c = JC_INR;
+                if (kind == SG_EV_ENTRY) c |= JC_ENT;
+                else if (kind == SG_EV_EXIT && eff) c |= JC_XE;
+                else if (kind == SG_EV_TRACE && eff && (ev[e].cz & 0xFFFFu) > 0) c |= JC_TE;
             }
-#pragma unroll
-            for (int k = 0; k < NQ; ++k) {
-                uint32_t v = q[k];
-                if (k == Q_MIN) {
-                    WAVE_SCAN(v, NO_LANE, op_min);
-                    ex[k] = shr1(v, NO_LANE);
-                } else {
-                    WAVE_SCAN(v, 0u, op_add);
-                    ex[k] = v - q[k];
-                }
-                if (NW > 1 && lane == 63) sh.part[wv][k] = v;  // one wave: its prefixes are the block's
-            }
+            cls[e] = c;
         }
-        // rate limiters: exclusive prefix of the costs (C) and the max-plus term (M) of updating lanes
-        int64_t rl_cost_l[2] = {0, 0}, rl_C[2] = {0, 0}, rl_M[2] = {NEG_INF64, NEG_INF64};
+
+        // ---- phase B: counter deltas under the guesses: lane totals, wave scans
+        uint32_t ex[NQ], tq[NQ];
+        jac_zero<NQ>(tq);
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            uint32_t q[NQ];
+            jac_q<NQ>(q, cls[e], gg[e], ev[e].cz, (uint32_t)nr, (uint32_t)nf);
+            jac_acc<NQ>(tq, q);
+        }
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            uint32_t v = tq[k];
+            if (k == Q_MIN) {
+                WAVE_SCAN(v, NO_LANE, op_min);
+                ex[k] = shr1(v, NO_LANE);
+            } else {
+                WAVE_SCAN(v, 0u, op_add);
+                ex[k] = v - tq[k];
+            }
+            if (NW > 1 && lane == 63) sh.part[wv][k] = v;  // one wave: its prefixes are the block's
+        }
+        // rate limiters: exclusive prefix of the costs (C) and the max-plus term (M) of updating events
+        // before the lane (a lane folds its own events: local cost sum, max of t - local inclusive cost)
+        int64_t rl_C[2] = {0, 0}, rl_M[2] = {NEG_INF64, NEG_INF64};
         if (RL) {
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -1962,14 +2014,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 if (s >= 0) {
                     const DRule& r = sh.rules[s];
                     const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
-                    const int64_t cost = rl_cost(r, st, (int)cnt);
-                    const bool upd = ent && g > (uint32_t)s &&
-                                     (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || ((int)cnt > 0 && r.count > 0));
-                    const int64_t ci = wscan_i64_add(upd ? cost : 0);
-                    const int64_t mi = wscan_i64_max(upd ? t - ci : NEG_INF64);
+                    int64_t cl = 0, ml = NEG_INF64;
+#pragma unroll
+                    for (int e = 0; e < EP; ++e) {
+                        const int cnt = (int)(ev[e].cz & 0xFFFFu);
+                        if (rl_upd(r, cls[e], gg[e], s, cnt)) {
+                            cl += rl_cost(r, st, cnt);
+                            const int64_t v = t0 + ev[e].dt - cl;
+                            ml = v > ml ? v : ml;
+                        }
+                    }
+                    const int64_t ci = wscan_i64_add(cl);
+                    const int64_t mi = wscan_i64_max(ml == NEG_INF64 ? NEG_INF64 : ml - (ci - cl));
                     if (lane == 63) { sh.prl[wv][2 * k] = ci; sh.prl[wv][2 * k + 1] = mi; }
-                    rl_cost_l[k] = cost;
-                    rl_C[k] = ci - (upd ? cost : 0);
+                    rl_C[k] = ci - cl;
                     const int64_t me = __shfl_up(mi, 1, 64);
                     rl_M[k] = lane == 0 ? NEG_INF64 : me;
                 }
@@ -1980,8 +2038,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         PROF_MARK(2)
         uint32_t inr_total;
         if (NW == 1) {  // lane 63's inclusive in-round count
-            const uint32_t own = inr ? 1u : 0u;
-            inr_total = (uint32_t)__builtin_amdgcn_readlane((int)((ex[Q_TI] >> 16) + own), 63);
+            inr_total = (uint32_t)__builtin_amdgcn_readlane((int)((ex[Q_TI] + tq[Q_TI]) >> 16), 63);
         } else {
             // block-wide: lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv
 #pragma unroll
@@ -2013,37 +2070,45 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 }
             }
         }
-        // lane views (base + committed-in-round + prefix)
-        const int64_t vP = sh.bP + sh.cP + ex[Q_P];
-        const int64_t vS = sh.bS + sh.cS + ex[Q_S];
-        const int64_t vRT = sh.bRT + sh.cRT + ex[Q_RT];
 
-        // ---- phase C: RT breaker passCount (segmented scan over the lanes that check it)
-        uint32_t badm = 0, cutm = 0;  // per degrade stage bits
-        int32_t bbefore[MD];
+        // ---- phase C: RT breakers' passCount (segmented scan over the events that check them).  An
+        // event's RT average (its view of succ/rt) decides whether it counts or resets: the lane walks its
+        // events for those bits, then scans its segmented total.
+        uint32_t cutm = 0;  // per degrade stage: the breaker is cut at the round's start
 #pragma unroll
-        for (int k = 0; k < MD; ++k) {
-            bbefore[k] = 0;
-            if (k < nd) {
-                const DRule& r = sh.rules[nf + k];
-                if (sh.rs[nf + k].a) cutm |= 1u << k;
-                if (r.grade == SG_DEGRADE_GRADE_RT) {
-                    const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
-                    if (!(avg < r.count)) badm |= 1u << k;
-                }
-            }
-        }
+        for (int k = 0; k < MD; ++k)
+            if (k < nd && sh.rs[nf + k].a) cutm |= 1u << k;
+        uint32_t badb = 0;   // bit e * MD + k: stage k's RT average is at its threshold in event e's view
+        uint32_t segl[MD];   // RT stages: the segmented count before the lane
+#pragma unroll
+        for (int k = 0; k < MD; ++k) segl[k] = 0;
         if (has_rt) {
-            uint32_t segx[MD];
+            uint32_t agg[MD];
+#pragma unroll
+            for (int k = 0; k < MD; ++k) agg[k] = 0;
+            uint32_t rS = 0, rRT = 0;
+#pragma unroll
+            for (int e = 0; e < EP; ++e) {
+                const int64_t vS = sh.bS + sh.cS + (int64_t)(ex[Q_S] + rS);
+                const int64_t vRT = sh.bRT + sh.cRT + (int64_t)(ex[Q_RT] + rRT);
+#pragma unroll
+                for (int k = 0; k < MD; ++k) {
+                    if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                        const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
+                        const bool bad = !(avg < sh.rules[nf + k].count);
+                        if (bad) badb |= 1u << (e * MD + k);
+                        const bool chk = (cls[e] & JC_ENT) && gg[e] >= (uint32_t)(nf + k);
+                        agg[k] = op_seg(agg[k], chk ? (bad ? 1u : 0x80000000u) : 0u);
+                    }
+                }
+                if (cls[e] & JC_XE) { rS += ev[e].cz & 0xFFFFu; rRT += ev[e].cz >> 16; }
+            }
 #pragma unroll
             for (int k = 0; k < MD; ++k) {
-                segx[k] = 0;
                 if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                    const bool chk = ent && g >= (uint32_t)(nf + k);
-                    const uint32_t el = chk ? (((badm >> k) & 1) ? 1u : 0x80000000u) : 0u;
-                    uint32_t v = el;
+                    uint32_t v = agg[k];
                     WAVE_SCAN(v, 0u, op_seg);
-                    segx[k] = shr1(v, 0u);
+                    segl[k] = shr1(v, 0u);
                     if (lane == 63) sh.pseg[wv][k] = v;
                 }
             }
@@ -2053,77 +2118,145 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
                     uint32_t pre = 0;
                     for (uint32_t w = 0; w < wv; ++w) pre = op_seg(pre, sh.pseg[w][k]);
-                    const uint32_t x = op_seg(pre, segx[k]);
-                    const int32_t c = (int32_t)(x & 0x7fffffffu);
-                    bbefore[k] = (x & 0x80000000u) ? c : (int32_t)sh.rs[nf + k].b + c;
+                    segl[k] = op_seg(pre, segl[k]);
                 }
             }
         }
 
-        // ---- evaluation of every lane's chain under its view
-        uint32_t o = (uint32_t)nr;
-        int64_t wait = 0;
+        // ---- the lane's running sums over its own events (the view of event e = block prefix + run)
+        uint32_t run[NQ], rseg[MD];
+        int64_t lc[2], lm[2];
+        auto run_reset = [&]() {
+            jac_zero<NQ>(run);
 #pragma unroll
-        for (int s = 0; s < MF; ++s) {
-            if (s < nf) {
-                const DRule& r = sh.rules[s];
-                bool ok = true;
-                int64_t w = 0;
-                if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP) {
-                    const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
-                    if (st.a >= r.warning_token) ok = (double)(vP + (int)cnt) <= warm_qps(r, st.a);
-                    else ok = (double)(vP + (int)cnt) <= r.count;
-                } else if (RL && (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
-                                  r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)) {
-                    const int k = (s == rl_s0) ? 0 : 1;
-                    const int64_t L0 = sh.rs[s].c;
-                    const int64_t cexcl = k == 0 ? rl_C[0] : rl_C[1];
-                    const int64_t mexcl = k == 0 ? rl_M[0] : rl_M[1];
-                    const int64_t cost = k == 0 ? rl_cost_l[0] : rl_cost_l[1];
-                    const int64_t L = cexcl + (mexcl > L0 ? mexcl : L0);
-                    if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && (int)cnt <= 0) ok = true;
-                    else if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && r.count <= 0) ok = false;
-                    else {
-                        const int64_t expected = L + cost;
-                        if (expected <= t) ok = true;
-                        else { w = expected - t; ok = w <= r.max_queue; }
+            for (int k = 0; k < MD; ++k) rseg[k] = 0;
+            lc[0] = lc[1] = 0;
+            lm[0] = lm[1] = NEG_INF64;
+        };
+        auto run_step = [&](int e, uint32_t g) {  // fold event e under guess g
+            uint32_t q[NQ];
+            jac_q<NQ>(q, cls[e], g, ev[e].cz, (uint32_t)nr, (uint32_t)nf);
+            jac_acc<NQ>(run, q);
+            if (has_rt) {
+#pragma unroll
+                for (int k = 0; k < MD; ++k) {
+                    if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                        const bool chk = (cls[e] & JC_ENT) && g >= (uint32_t)(nf + k);
+                        rseg[k] = op_seg(rseg[k], chk ? (((badb >> (e * MD + k)) & 1) ? 1u : 0x80000000u) : 0u);
                     }
-                } else {  // DefaultController
-                    const int32_t curv = r.grade == SG_FLOW_GRADE_THREAD
-                                             ? (int32_t)(sh.bTH + sh.cTH + (int64_t)(int32_t)ex[Q_TH])
-                                             : j_d2i((double)vP);
-                    ok = !((double)j_iadd(curv, (int)cnt) > r.count);
-                }
-                if (o == (uint32_t)nr) {
-                    if (!ok) o = (uint32_t)s;
-                    else if (w > 0) wait += w;
                 }
             }
-        }
+            if (RL) {
 #pragma unroll
-        for (int k = 0; k < MD; ++k) {
-            if (k < nd) {
-                const DRule& r = sh.rules[nf + k];
-                const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
-                bool ok;
-                if (((cutm >> k) & 1) || trip_ex > 0) ok = false;
-                else if (r.grade == SG_DEGRADE_GRADE_RT) ok = !((badm >> k) & 1) || (bbefore[k] + 1 < 5);
-                else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
-                    const double exc = (double)(sh.bE + sh.cE + ex[Q_E]) / 1.0, succ = (double)vS / 1.0;
-                    const double total = (double)vP / 1.0 + (double)(sh.bB + sh.cB + ex[Q_B]) / 1.0;
-                    if (total < 5) ok = true;
-                    else if (succ - exc <= 0 && exc < 5) ok = true;
-                    else ok = exc / succ < r.count;
-                } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT)
-                    ok = (double)(sh.bEM + sh.cE + ex[Q_E]) < r.count;
-                else ok = true;
-                if (o == (uint32_t)nr && !ok) o = (uint32_t)(nf + k);
+                for (int k = 0; k < 2; ++k) {
+                    const int s = k == 0 ? rl_s0 : rl_s1;
+                    const int cnt = (int)(ev[e].cz & 0xFFFFu);
+                    if (s >= 0 && rl_upd(sh.rules[s], cls[e], g, s, cnt)) {
+                        const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                        lc[k] += rl_cost(sh.rules[s], st, cnt);
+                        const int64_t v = t0 + ev[e].dt - lc[k];
+                        lm[k] = v > lm[k] ? v : lm[k];
+                    }
+                }
             }
+        };
+        // breaker passCount before event e (RT stage k)
+        auto bbefore_of = [&](int k) -> int32_t {
+            const uint32_t x = op_seg(segl[k], rseg[k]);
+            const int32_t c = (int32_t)(x & 0x7fffffffu);
+            return (x & 0x80000000u) ? c : (int32_t)sh.rs[nf + k].b + c;
+        };
+        // a rate limiter's latestPassedTime before event e
+        auto rl_latest = [&](int k, int s) -> int64_t {
+            const int64_t L0 = sh.rs[s].c;
+            const int64_t mx = lm[k] == NEG_INF64 ? NEG_INF64 : lm[k] - rl_C[k];
+            const int64_t me = mx > rl_M[k] ? mx : rl_M[k];
+            return rl_C[k] + lc[k] + (me > L0 ? me : L0);
+        };
+
+        // ---- evaluation of every event's chain under its view
+        uint32_t fe = NO_LANE, fo_m = 0;  // the lane's first mismatching ENTRY and its evaluated outcome
+        uint32_t wq[EP];                  // queueing waits (rate limiters)
+        run_reset();
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            const uint32_t c = cls[e];
+            const int cnt = (int)(ev[e].cz & 0xFFFFu);
+            const int64_t t = t0 + ev[e].dt;
+            const int64_t vP = sh.bP + sh.cP + (int64_t)(ex[Q_P] + run[Q_P]);
+            const int64_t vS = sh.bS + sh.cS + (int64_t)(ex[Q_S] + run[Q_S]);
+            uint32_t o = (uint32_t)nr;
+            int64_t wait = 0;
+            if (c & JC_ENT) {
+#pragma unroll
+                for (int s = 0; s < MF; ++s) {
+                    if (s < nf) {
+                        const DRule& r = sh.rules[s];
+                        bool ok = true;
+                        int64_t w = 0;
+                        if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP) {
+                            const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                            if (st.a >= r.warning_token) ok = (double)(vP + cnt) <= warm_qps(r, st.a);
+                            else ok = (double)(vP + cnt) <= r.count;
+                        } else if (RL && (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
+                                          r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)) {
+                            const int k = (s == rl_s0) ? 0 : 1;
+                            const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                            if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && cnt <= 0) ok = true;
+                            else if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER && r.count <= 0) ok = false;
+                            else {
+                                const int64_t expected = rl_latest(k, s) + rl_cost(r, st, cnt);
+                                if (expected <= t) ok = true;
+                                else { w = expected - t; ok = w <= r.max_queue; }
+                            }
+                        } else {  // DefaultController
+                            const int32_t curv = r.grade == SG_FLOW_GRADE_THREAD
+                                                     ? (int32_t)(sh.bTH + sh.cTH + (int64_t)(int32_t)(ex[Q_TH] + run[Q_TH]))
+                                                     : j_d2i((double)vP);
+                            ok = !((double)j_iadd(curv, cnt) > r.count);
+                        }
+                        if (o == (uint32_t)nr) {
+                            if (!ok) o = (uint32_t)s;
+                            else if (w > 0) wait += w;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < MD; ++k) {
+                    if (k < nd) {
+                        const DRule& r = sh.rules[nf + k];
+                        const uint32_t trip_ex = ((ex[Q_TR + k / 2] + run[Q_TR + k / 2]) >> (16 * (k & 1))) & 0xFFFFu;
+                        bool ok;
+                        if (((cutm >> k) & 1) || trip_ex > 0) ok = false;
+                        else if (r.grade == SG_DEGRADE_GRADE_RT) ok = !((badb >> (e * MD + k)) & 1) || (bbefore_of(k) + 1 < 5);
+                        else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+                            const double exc = (double)(sh.bE + sh.cE + (int64_t)(ex[Q_E] + run[Q_E])) / 1.0;
+                            const double succ = (double)vS / 1.0;
+                            const double total = (double)vP / 1.0 + (double)(sh.bB + sh.cB + (int64_t)(ex[Q_B] + run[Q_B])) / 1.0;
+                            if (total < 5) ok = true;
+                            else if (succ - exc <= 0 && exc < 5) ok = true;
+                            else ok = exc / succ < r.count;
+                        } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT)
+                            ok = (double)(sh.bEM + sh.cE + (int64_t)(ex[Q_E] + run[Q_E])) < r.count;
+                        else ok = true;
+                        if (o == (uint32_t)nr && !ok) o = (uint32_t)(nf + k);
+                    }
+                }
+                if (o != gg[e] && fe == NO_LANE) { fe = (uint32_t)e; fo_m = o; }
+            }
+            wq[e] = (uint32_t)(wait > 0xFFFF ? 0xFFFF : wait);
+            run_step(e, gg[e]);
         }
-        {
-            const uint64_t mm = __ballot(ent && o != g);
-            if (lane == 0) sh.mism[mb][wv] = mm ? wv * 64 + (uint32_t)(__ffsll((long long)mm) - 1) : NO_LANE;
-            if (mm && lane == (uint32_t)(__ffsll((long long)mm) - 1)) sh.mo[mb][wv] = o;
+        {   // the wave's first mismatching position and its evaluated outcome
+            const uint64_t mm = __ballot(fe != NO_LANE);
+            if (mm) {
+                const int fl = __ffsll((long long)mm) - 1;
+                const uint32_t fel = (uint32_t)__builtin_amdgcn_readlane((int)fe, fl);
+                const uint32_t fol = (uint32_t)__builtin_amdgcn_readlane((int)fo_m, fl);
+                if (lane == 0) { sh.mism[mb][wv] = (wv * 64 + (uint32_t)fl) * EP + fel; sh.mo[mb][wv] = fol; }
+            } else if (lane == 0) {
+                sh.mism[mb][wv] = NO_LANE;
+            }
         }
         PROF_MARK(3)
         lds_barrier();  // B4
@@ -2133,109 +2266,124 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         // the pivot's true outcome: the re-guess of every later ENTRY of the round.  Their own evaluated
         // outcomes saw the pivot's wrong guess (e.g. a guessed breaker trip blocks everything after it),
         // while a state change at the pivot (reset breaker, spent quota, trip) mostly holds for the rest.
-        const uint32_t of = f != NO_LANE ? uni(sh.mo[mb][f >> 6]) : 0u;
+        const uint32_t of = f != NO_LANE ? uni(sh.mo[mb][f / (64 * EP)]) : 0u;
         mb ^= 1;
         if (f != NO_LANE) ++n_mm;
-#ifdef SG_KPROF
-        if (prof && tid == f) {  // what the first mismatching lane guessed and evaluated (0 pass, 1 flow, 2 degrade)
-            const uint32_t gc = g == (uint32_t)nr ? 0u : g < (uint32_t)nf ? 1u : 2u;
-            const uint32_t oc = o == (uint32_t)nr ? 0u : o < (uint32_t)nf ? 1u : 2u;
-            atomicAdd(&S.dbg[40 + 3 * gc + oc], 1ull);
-            if (f > c0) atomicAdd(&S.dbg[49], 1ull);  // the mismatch is not at the first uncommitted lane
-            atomicAdd(&S.dbg[50], (unsigned long long)(f - c0));
-        }
-#endif
         const uint32_t e_end = c0 + inr_total;
         const uint32_t cend = f != NO_LANE ? f + 1 : e_end;
+        const uint32_t cnt_now = sg.len - tbase < TILE ? sg.len - tbase : TILE;
 
-        // ---- phase D: commit [c0, cend), re-guess the rest
-        const bool com = inr && tid < cend;
-        const uint32_t fo = (tid == f) ? o : g;
-        const uint32_t pos = tbase + tid;
-        if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
-            const bool app = com && kind == SG_EV_ENTRY && fo == (uint32_t)nr;
-            const uint64_t am = __ballot(app);
-            if (am) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&sh.npend, (uint32_t)__popcll(am));
-                base = (uint32_t)__shfl((int)base, 0, 64);
-                if (app) S.pend[sg.start + base + (uint32_t)__popcll(am & lanemask_lt())] = pos;
-            }
-        }
-        if (com) {
-            const uint32_t d = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wait) : mk_dec(ST_NOT_ENTRY, 0, 0);
-            dec[sg.start + pos] = d;
-            win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
-            g = fo;
-        } else if (ent) {
-            g = f != NO_LANE ? of : o;
-            win[pos & (WIN - 1)] = (g == (uint32_t)nr) ? 1 : 0;
-        }
-        // the first blocking degrade verdict of a committed lane trips the breaker (DegradeRule.passCheck cut)
+        // ---- phase D: commit [c0, cend), re-guess the rest (every in-round ENTRY after f: f exists)
+        uint32_t appm = 0;  // committed passes (pending list for frozen-stretch skipping)
+        uint32_t fmax = 0;  // 1 + the largest outcome of a committed ENTRY (WarmUp sync reach)
+        run_reset();
 #pragma unroll
-        for (int k = 0; k < MD; ++k) {
-            const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
-            if (k < nd && com && kind == SG_EV_ENTRY && fo == (uint32_t)(nf + k) && !((cutm >> k) & 1) && trip_ex == 0) {
-                const DRule& r = sh.rules[nf + k];
-                RState& s = sh.rs[nf + k];
-                if (r.grade == SG_DEGRADE_GRADE_RT) s.b = bbefore[k] + 1;
-                s.a = 1;
-                s.c = t + (int64_t)r.time_window * 1000;
+        for (int e = 0; e < EP; ++e) {
+            const uint32_t c = cls[e];
+            const uint32_t pt = lp0 + (uint32_t)e, pos = tbase + pt;
+            const uint32_t kind = ev[e].kf & 0xFFu;
+            const uint32_t g = gg[e];
+            const bool com = (c & JC_INR) && pt < cend;
+            const uint32_t fo = (pt == f) ? of : g;
+            const int cnt = (int)(ev[e].cz & 0xFFFFu);
+            const uint32_t rtv = ev[e].cz >> 16;
+            const int64_t t = t0 + ev[e].dt;
+#ifdef SG_KPROF
+            if (prof && pt == f) {  // what the first mismatching event guessed and evaluated (0 pass, 1 flow, 2 degrade)
+                const uint32_t gc = g == (uint32_t)nr ? 0u : g < (uint32_t)nf ? 1u : 2u;
+                const uint32_t oc = of == (uint32_t)nr ? 0u : of < (uint32_t)nf ? 1u : 2u;
+                atomicAdd(&S.dbg[40 + 3 * gc + oc], 1ull);
+                if (f > c0) atomicAdd(&S.dbg[49], 1ull);  // the mismatch is not at the first uncommitted event
+                atomicAdd(&S.dbg[50], (unsigned long long)(f - c0));
+            }
+#endif
+            if (com) {
+                const uint32_t d = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wq[e]) : mk_dec(ST_NOT_ENTRY, 0, 0);
+                dec[sg.start + pos] = d;
+                win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
+                gg[e] = fo;
+                if (kind == SG_EV_ENTRY) {
+                    if (fo == (uint32_t)nr) appm |= 1u << e;
+                    if (fo + 1 > fmax) fmax = fo + 1;
+                    // the first blocking degrade verdict of a committed ENTRY trips the breaker (DegradeRule.passCheck cut)
+#pragma unroll
+                    for (int k = 0; k < MD; ++k) {
+                        const uint32_t trip_ex = ((ex[Q_TR + k / 2] + run[Q_TR + k / 2]) >> (16 * (k & 1))) & 0xFFFFu;
+                        if (k < nd && fo == (uint32_t)(nf + k) && !((cutm >> k) & 1) && trip_ex == 0) {
+                            const DRule& r = sh.rules[nf + k];
+                            RState& s = sh.rs[nf + k];
+                            if (r.grade == SG_DEGRADE_GRADE_RT) s.b = bbefore_of(k) + 1;
+                            s.a = 1;
+                            s.c = t + (int64_t)r.time_window * 1000;
+                        }
+                    }
+                }
+                if (pt == cend - 1) {  // pivot: the last committed event carries the committed totals
+                    const bool ce = kind == SG_EV_ENTRY, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0;
+                    const bool cp = ce && fo == (uint32_t)nr;
+                    sh.cP += (int64_t)(ex[Q_P] + run[Q_P]) + (cp ? cnt : 0);
+                    sh.cB += (int64_t)(ex[Q_B] + run[Q_B]) + ((ce && !cp) ? cnt : 0);
+                    sh.cS += (int64_t)(ex[Q_S] + run[Q_S]) + (xe ? cnt : 0);
+                    sh.cRT += (int64_t)(ex[Q_RT] + run[Q_RT]) + (xe ? rtv : 0);
+                    sh.cE += (int64_t)(ex[Q_E] + run[Q_E]) + (te ? cnt : 0);
+                    sh.cTH += (int64_t)(int32_t)(ex[Q_TH] + run[Q_TH]) + (cp ? 1 : (xe ? -1 : 0));
+                    sh.ctouch += ((ex[Q_TI] + run[Q_TI]) & 0xFFFFu) + ((ce || xe || te) ? 1 : 0);
+                    sh.cminrt = op_min(sh.cminrt, op_min(op_min(ex[Q_MIN], run[Q_MIN]), xe ? rtv : NO_LANE));
+                    if (RL) {
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            const int s = k == 0 ? rl_s0 : rl_s1;
+                            if (s >= 0) {
+                                const DRule& r = sh.rules[s];
+                                const RState& st = ((has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                                const int64_t cost = rl_cost(r, st, cnt);
+                                int64_t L = rl_latest(k, s);
+                                if (rl_upd(r, c, fo, s, cnt)) L = (t > L + cost) ? t : L + cost;
+                                sh.rs[s].c = L;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < MD; ++k) {
+                        const uint32_t trip_ex = ((ex[Q_TR + k / 2] + run[Q_TR + k / 2]) >> (16 * (k & 1))) & 0xFFFFu;
+                        if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT && !((cutm >> k) & 1) && trip_ex == 0 &&
+                            !(ce && fo == (uint32_t)(nf + k))) {
+                            int32_t b = bbefore_of(k);
+                            if (ce && fo > (uint32_t)(nf + k)) b = ((badb >> (e * MD + k)) & 1) ? b + 1 : 0;
+                            sh.rs[nf + k].b = b;
+                        }
+                    }
+                    if (ce) sh.last_out = fo;
+                    sh.c0 = cend;
+                }
+            } else if (c & JC_ENT) {
+                gg[e] = of;
+                win[pos & (WIN - 1)] = (of == (uint32_t)nr) ? 1 : 0;
+            }
+            if (pt == cend && cend < cnt_now) sh.tnext = t0 + ev[e].dt;
+            run_step(e, g);
+        }
+        if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
+            const uint32_t na = (uint32_t)__popc(appm);
+            uint32_t incl = na;
+            WAVE_SCAN(incl, 0u, op_add);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (tot) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&sh.npend, tot);
+                base = (uint32_t)__shfl((int)base, 0, 64) + incl - na;
+#pragma unroll
+                for (int e = 0; e < EP; ++e)
+                    if ((appm >> e) & 1) S.pend[sg.start + base++] = tbase + lp0 + e;
             }
         }
         if (has_sync) {
             for (int s = 0; s < nf; ++s) {
                 if ((has_sync >> s) & 1) {
-                    const uint64_t rb = __ballot(com && kind == SG_EV_ENTRY && fo >= (uint32_t)s);
+                    const uint64_t rb = __ballot(fmax > (uint32_t)s);
                     if (lane == 0 && rb) atomicOr(&sh.warm_reach, 1u << s);
                 }
             }
-        }
-        if (tid == cend - 1) {  // pivot: the last committed lane carries the committed totals
-            const bool ce = kind == SG_EV_ENTRY;
-            const bool cp = ce && fo == (uint32_t)nr;
-            sh.cP += ex[Q_P] + (cp ? cnt : 0);
-            sh.cB += ex[Q_B] + ((ce && !cp) ? cnt : 0);
-            sh.cS += ex[Q_S] + (xe ? cnt : 0);
-            sh.cRT += ex[Q_RT] + (xe ? rtv : 0);
-            sh.cE += ex[Q_E] + (te ? cnt : 0);
-            sh.cTH += (int64_t)(int32_t)ex[Q_TH] + (cp ? 1 : (xe ? -1 : 0));
-            sh.ctouch += (ex[Q_TI] & 0xFFFFu) + ((ce || xe || te) ? 1 : 0);
-            sh.cminrt = op_min(sh.cminrt, op_min(ex[Q_MIN], xe ? rtv : NO_LANE));
-            if (RL) {
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int s = k == 0 ? rl_s0 : rl_s1;
-                    if (s >= 0) {
-                        const DRule& r = sh.rules[s];
-                        const int64_t L0 = sh.rs[s].c;
-                        const int64_t cexcl = k == 0 ? rl_C[0] : rl_C[1];
-                        const int64_t mexcl = k == 0 ? rl_M[0] : rl_M[1];
-                        const int64_t cost = k == 0 ? rl_cost_l[0] : rl_cost_l[1];
-                        int64_t L = cexcl + (mexcl > L0 ? mexcl : L0);
-                        const bool upd = ce && fo > (uint32_t)s &&
-                                         (r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER || ((int)cnt > 0 && r.count > 0));
-                        if (upd) L = (t > L + cost) ? t : L + cost;
-                        sh.rs[s].c = L;
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < MD; ++k) {
-                const uint32_t trip_ex = (ex[Q_TR + k / 2] >> (16 * (k & 1))) & 0xFFFFu;
-                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT && !((cutm >> k) & 1) && trip_ex == 0 &&
-                    !(ce && fo == (uint32_t)(nf + k))) {
-                    int32_t b = bbefore[k];
-                    if (ce && fo > (uint32_t)(nf + k)) b = ((badm >> k) & 1) ? b + 1 : 0;
-                    sh.rs[nf + k].b = b;
-                }
-            }
-            if (ce) sh.last_out = fo;
-            sh.c0 = cend;
-        }
-        {
-            const uint32_t cnt_now = sg.len - tbase < HW ? sg.len - tbase : HW;
-            if (tid == cend && cend < cnt_now) sh.tnext = t0 + dt;
         }
         PROF_MARK(4)
         lds_barrier();  // B1
@@ -2320,9 +2468,7 @@ hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
                        epoch, bflags);
-    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, n, bst, link, epoch,
-                       bflags);
-    hipLaunchKernelGGL(k_link_verify, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, skeys, n, link,
+    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, skeys, n, bst, link,
                        epoch, bflags);
     return hipGetLastError();
 }
@@ -2358,15 +2504,16 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     switch (bin) {
     case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
                    // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS
-        hipLaunchKernelGGL((k_jac<16, 17, 2, 2, false, true>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
+        hipLaunchKernelGGL((k_jac<16, 1, 17, 2, 2, false, true>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
                            dec, bflags);
         break;
-    case BIN_J4:
-        hipLaunchKernelGGL((k_jac<4, 14, JMAX_FLOW, JMAX_DEG, true, true>), dim3(m), dim3(256), 0, st, recs, segs, order, m, S,
+    case BIN_J4:  // 256 lanes, one event each: two events per lane (k_jac<4, 2, ...>) measured 22 % faster alone
+                  // but slower in the pipeline (200 VGPRs: less room for the overlapping group stage)
+        hipLaunchKernelGGL((k_jac<4, 1, 14, JMAX_FLOW, JMAX_DEG, true, true>), dim3(m), dim3(256), 0, st, recs, segs, order, m, S,
                            cfg, t0, dec, bflags);
         break;
     case BIN_J1:
-        hipLaunchKernelGGL((k_jac<1, 12, JMAX_FLOW, JMAX_DEG, true, false>), dim3(m), dim3(64), 0, st, recs, segs, order, m, S,
+        hipLaunchKernelGGL((k_jac<1, 1, 12, JMAX_FLOW, JMAX_DEG, true, false>), dim3(m), dim3(64), 0, st, recs, segs, order, m, S,
                            cfg, t0, dec, bflags);
         break;
     case BIN_LITE:

@@ -952,27 +952,15 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     e->device = cfg.device;
     auto bad = [&](int rc) { sg_engine_destroy(e); return rc; };
     if (hipSetDevice(e->device) != hipSuccess) return bad(fail(SG_EDEVICE, "hipSetDevice failed"));
-    // The decide streams (latency-bound per-resource chains) get the highest priority so that their
-    // workgroups are dispatched ahead of the overlapping group stage's bandwidth-bound sort
-    // (SG_STREAM_PRIO=0: default priorities).
+    // The group stage (the critical path of the two-slot pipeline) gets the highest stream priority,
+    // so that its short bandwidth-bound kernels are dispatched into the CUs the long decide kernels
+    // free (C4: 4.53 -> 4.34 ms per batch).  SG_STREAM_PRIO=0: default priorities; =1: decide first.
     int prio_lo = 0, prio_hi = 0;
     const char* sp = std::getenv("SG_STREAM_PRIO");
     if (!(sp && sp[0] == '0')) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (sp && sp[0] == '2') std::swap(prio_lo, prio_hi);  // SG_STREAM_PRIO=2: the group stage first
+    if (!(sp && sp[0] == '1')) std::swap(prio_lo, prio_hi);
     if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
-    // SG_GROUP_CU_QUARTERS=q (1..3): the group stream runs on q of every 4 CUs (an even spread over
-    // the XCDs), leaving the rest to the latency-bound decide kernels it overlaps (experiment knob).
-    int gq = 0;
-    if (const char* v = std::getenv("SG_GROUP_CU_QUARTERS")) gq = std::atoi(v);
-    if (gq >= 1 && gq <= 3) {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int j = 0; j < ncu; ++j)
-            if (j % 4 < gq) mask[(size_t)j / 32] |= 1u << (j % 32);
-        if (hipExtStreamCreateWithCUMask(&e->gstream, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-            return bad(fail(SG_EDEVICE, "stream (CU mask)"));
-    } else if (hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, prio_lo) != hipSuccess) {
+    if (hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, prio_lo) != hipSuccess) {
         return bad(fail(SG_EDEVICE, "stream"));
     }
     for (auto& B : e->slot)

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             if (ref != SG_REF_NONE) {
                 if (ref >= gbase) {
                     // an EXIT/TRACE must follow its ENTRY (that the ENTRY is of its own resource is checked
-                    // after the sort, where the two sit a few positions apart: k_link_verify)
+                    // after the sort, where the two sit a few positions apart: k_block_sums)
                     if (ref - gbase >= i) fl |= BF_BAD_REF;
                     else { r.code = RC_BATCH; r.x = (uint32_t)(ref - gbase); }
                 } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve,

@@ -2,8 +2,8 @@
 library reads once per process (so each runs in a child process):
 
   SG_PIPELINE=0            group and decide stages back to back (no overlap of batch k+1's grouping)
-  SG_GROUP_CU_QUARTERS=2   the group stage confined to half of the CUs
-  SG_STREAM_PRIO=2         the group stream at the higher priority (default: the decide streams)
+  SG_STREAM_PRIO=1         the decide streams at the higher priority (default: the group stream)
+  SG_STREAM_PRIO=0         default stream priorities
 
 Each child replays a seeded C4 trace (DegradeRules + QPS rules, several batches) through the HIP
 engine and the oracle and requires bit-identical decisions and node state.
@@ -43,7 +43,7 @@ print("ok", len(ev))
 """
 
 
-@pytest.mark.parametrize("env", ["SG_PIPELINE=0", "SG_GROUP_CU_QUARTERS=2", "SG_STREAM_PRIO=2"])
+@pytest.mark.parametrize("env", ["SG_PIPELINE=0", "SG_STREAM_PRIO=1", "SG_STREAM_PRIO=0"])
 def test_alternative_path_parity(env):
     k, v = env.split("=")
     child_env = dict(os.environ, **{k: v})
