@@ -269,7 +269,9 @@ __global__ void k_resolve(const uint32_t* __restrict__ prev, uint32_t np, const 
 
 // decisions back to submission order; the status ring keeps every event's status for
 // references from later batches (0xFF = not an ENTRY)
-// (POST_ITEMS items per lane, all random loads issued before any use: more of them in flight)
+// (POST_ITEMS items per lane, all random loads issued before any use: more of them in flight).  Only
+// ENTRYs are gathered (bit 31 of pos_of): every other event's word is mk_dec(ST_NOT_ENTRY, 0, 0), which
+// the decide kernels need not store.
 #define POST_ITEMS 4
 __global__ __launch_bounds__(256) void k_post(const uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ dec,
                                               uint64_t n, uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask,
@@ -279,10 +281,11 @@ __global__ __launch_bounds__(256) void k_post(const uint32_t* __restrict__ pos_o
 #pragma unroll
     for (int k = 0; k < POST_ITEMS; ++k) {
         const uint64_t i = base + (uint64_t)k * 256;
-        po[k] = i < n ? pos_of[i] & 0x7FFFFFFFu : 0u;
+        po[k] = i < n ? pos_of[i] : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < POST_ITEMS; ++k) d[k] = (base + (uint64_t)k * 256 < n) ? dec[po[k]] : 0u;
+    for (int k = 0; k < POST_ITEMS; ++k)
+        d[k] = (po[k] & 0x80000000u) ? dec[po[k] & 0x7FFFFFFFu] : mk_dec(ST_NOT_ENTRY, 0, 0);
 #pragma unroll
     for (int k = 0; k < POST_ITEMS; ++k) {
         const uint64_t i = base + (uint64_t)k * 256;
@@ -961,7 +964,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
             }
             LPROF(ktc)
         }
-        dec[sg.start + j] = d;
+        if (r.kind == SG_EV_ENTRY) dec[sg.start + j] = d;  // k_post reads ENTRY words only
     }
     min_flush(N, C.minb);
     node_store(N, S, res, pg.pflags);
@@ -1194,7 +1197,7 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
             }
             LPROF(ktc)
         }
-        dec[sg.start + j] = d;
+        if (kind == SG_EV_ENTRY) dec[sg.start + j] = d;  // k_post reads ENTRY words only
     }
 #pragma unroll
     for (uint32_t k = 0; k < CH; ++k) cur[k] = nxt[k];
