@@ -1587,12 +1587,24 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         }
     };
     static_assert(WIN - TILE >= (FULL_FENCE_TILES + 1) * TILE, "old references must be older than one full fence");
+    // Decisions committed by the Jacobi iterations wait in registers and are stored when the tile is left:
+    // vmcnt counts stores and loads in one in-order counter, so a store issued inside the iterations would
+    // make the wait for the next tile's prefetch (whose distance in vector-memory ops the compiler cannot
+    // count across the iteration loop) also wait for that store's write acknowledgement.
+    uint32_t pdec[EP], pmask = 0;
+    auto flush = [&](uint32_t tb) {
+#pragma unroll
+        for (int e = 0; e < EP; ++e)
+            if ((pmask >> e) & 1) dec[sg.start + tb + lp0 + (uint32_t)e] = pdec[e];
+        pmask = 0;
+    };
     auto advance = [&]() {  // next tile (uniform)
         tbase += TILE;
         // decode first: a (rare) old-reference load must not queue behind the prefetch below,
-        // vmcnt retires in order
+        // vmcnt retires in order; the finished tile's decisions go out between the two
 #pragma unroll
         for (int e = 0; e < EP; ++e) ev[e] = decode(nxt[e], tbase + lp0 + e);
+        flush(tbase - TILE);
         load(nxt, tbase + TILE);
         ++n_tile;
         if ((tbase / TILE) % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
@@ -1613,7 +1625,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         uint32_t c0 = uni(sh.c0);
         const uint32_t cnt_t = sg.len - tbase < TILE ? sg.len - tbase : TILE;
         if (c0 >= cnt_t) {  // tile done: advance (uniform)
-            if (tbase + TILE >= sg.len) break;
+            if (tbase + TILE >= sg.len) { flush(tbase); break; }
             advance();
             guess_all(sh.last_out, 0);
             lds_barrier();  // everyone has read sh.last_out / sh.c0
@@ -1660,6 +1672,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             if (sat || cutk0) {
                 constexpr uint32_t EPL = 4, ST = EPL * HW;  // events per lane, positions per super-tile
                 static_assert(WIN - ST >= (FULL_FENCE_TILES + 1) * (ST + HW), "old references must precede a full fence");
+                flush(tbase);     // the tile's committed decisions before the stretch
                 __syncthreads();  // full fence at every stretch start (see lds_barrier)
                 const uint32_t fpos0 = tbase + c0;        // stretch start (segment position)
                 double fcount[MF];                        // flow thresholds and verdict words, hoisted
@@ -2301,8 +2314,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             }
 #endif
             if (com) {
-                const uint32_t d = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wq[e]) : mk_dec(ST_NOT_ENTRY, 0, 0);
-                dec[sg.start + pos] = d;
+                pdec[e] = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wq[e]) : mk_dec(ST_NOT_ENTRY, 0, 0);
+                pmask |= 1u << e;
                 win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
                 gg[e] = fo;
                 if (kind == SG_EV_ENTRY) {

@@ -111,6 +111,14 @@ def test_c4_degrade(bin_mode):
     _run(4, batches=3, n_entries=400_000, n_res=50_000)
 
 
+@pytest.mark.parametrize("batches", [8, 2])
+def test_c4_minute_window_long_trace(batches, bin_mode):
+    # 2000 entries/s for ~150 s: exceptions leave the minute window while exception-count breakers read it
+    # (k_lite's running exception sum, chain.h exc_advance), in batches of ~19 s and of ~75 s (a second of
+    # the batch expires inside it).
+    _run(4, batches=batches, n_entries=300_000, n_res=3_000, rate=2000.0)
+
+
 def test_c4_wide_keys_two_10bit_passes():
     # 200k resources: 18-bit keys sort in two 10-bit radix passes (the 1M-resource bench layout)
     _run(4, batches=2, n_entries=600_000, n_res=200_000)
