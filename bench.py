@@ -266,8 +266,10 @@ def main():
             traffic = pj.get("traffic_bytes_per_batch")
             tnote = "profiles/pmc_latest.json (src_sha %s, git %s)" % (sha, pj.get("git_head"))
         else:
-            tnote = "profiles/pmc_latest.json is for other sources/config (src_sha %s != %s): not used" % (
-                pj.get("src_sha"), sha)
+            why = ("src_sha %s != %s" % (pj.get("src_sha"), sha) if pj.get("src_sha") != sha else
+                   "batch_events %s != %s" % (pj.get("batch_events"), gb) if pj.get("batch_events") != gb else
+                   "measured on one GPU, this run has %d ranks" % world)
+            tnote = "profiles/pmc_latest.json is for other sources/config (%s): not used" % why
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, ev, args)
