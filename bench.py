@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
     p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--shard", default="", metavar="R/N",
+                   help="rehearsal: run rank R's shard of an N-GPU run alone on this GPU (no collectives; "
+                        "the per-rank step time of the N-GPU run, NOT a measurement of it)")
     return p.parse_args()
 
 
@@ -137,8 +140,11 @@ def main():
     w, ev = make_trace(args.resources, gb, B, T.SEED_BASE + 4)
     gen_s = time.time() - t_gen
     tspan = int(ev["ts"][-1] - ev["ts"][0]) + 1000  # copy k starts a second after copy k-1 ends
-    if world > 1:
-        mine, pos = D.shard_stream(ev, world, rank)
+    shard = tuple(int(x) for x in args.shard.split("/")) if args.shard else None  # (R, N)
+    if shard:
+        assert world == 1 and 0 <= shard[0] < shard[1], "--shard R/N: one process, 0 <= R < N"
+    if world > 1 or shard:
+        mine, pos = D.shard_stream(ev, shard[1], shard[0]) if shard else D.shard_stream(ev, world, rank)
         cuts = np.searchsorted(pos, np.arange(B + 1, dtype=np.int64) * gb)
     else:
         mine, cuts = ev, np.arange(B + 1, dtype=np.int64) * gb
@@ -262,16 +268,17 @@ def main():
     if os.path.exists(pmc):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh) on these sources
         with open(pmc) as f:
             pj = json.load(f)
-        if pj.get("src_sha") == sha and pj.get("batch_events") == gb and world == 1:
+        if pj.get("src_sha") == sha and pj.get("batch_events") == gb and world == 1 and not shard:
             traffic = pj.get("traffic_bytes_per_batch")
             tnote = "profiles/pmc_latest.json (src_sha %s, git %s)" % (sha, pj.get("git_head"))
         else:
             why = ("src_sha %s != %s" % (pj.get("src_sha"), sha) if pj.get("src_sha") != sha else
                    "batch_events %s != %s" % (pj.get("batch_events"), gb) if pj.get("batch_events") != gb else
-                   "measured on one GPU, this run has %d ranks" % world)
+                   "measured on one GPU, this run has %d ranks" % world if world > 1 else
+                   "measured on the whole trace, this run is one shard")
             tnote = "profiles/pmc_latest.json is for other sources/config (%s): not used" % why
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not shard and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, ev, args)
 
     if rank == 0:
@@ -307,7 +314,9 @@ def main():
                     entries / (elapsed + h2d_ms / 1e3 * events / max(1, n_base) / world),
                     "note": "pinned host -> HBM copy of the events, measured on the base trace; not in value"},
             "metric_gathers": {"count": n_gather, "rows": rows_gathered} if world > 1 else None,
-            "rehearsal": "gloo, all ranks on one GPU: NOT a measurement" if rehearse else None,
+            "rehearsal": ("gloo, all ranks on one GPU: NOT a measurement" if rehearse else
+                          "rank %d of %d alone on one GPU (per-rank step of an N-GPU run): NOT a measurement" % shard
+                          if shard else None),
             "cpu_baseline": cpu,
             "src_sha": sha,
             "gen_s": gen_s,

@@ -111,6 +111,17 @@ def test_c4_degrade(bin_mode):
     _run(4, batches=3, n_entries=400_000, n_res=50_000)
 
 
+def test_c2_full_resource_count():
+    # C2 at its configured 10k resources, 4M entries (4 s of trace) in 4 batches, default bins
+    _run(2, batches=4, n_entries=4_000_000, n_res=10_000)
+
+
+def test_c3_full_resource_count():
+    # C3 at its configured 100k resources (QPS / thread / WarmUp / RateLimiter / WarmUpRateLimiter mix),
+    # 2M entries in 3 batches, default bins
+    _run(3, batches=3, n_entries=2_000_000, n_res=100_000, variant=T.V_WARM_RL)
+
+
 @pytest.mark.parametrize("batches", [8, 2])
 def test_c4_minute_window_long_trace(batches, bin_mode):
     # 2000 entries/s for ~150 s: exceptions leave the minute window while exception-count breakers read it
