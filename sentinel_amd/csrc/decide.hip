@@ -1310,6 +1310,8 @@ struct JacSh {
     int64_t prl[NW][4];
     uint32_t mism[2][NW];
     uint32_t mo[2][NW];        // evaluated outcome of each wave's first mismatching lane
+    uint32_t mu[2][NW];        // ... its in-round ENTRY acquire units up to and including it
+    int64_t mp[2][NW];         // ... and the round's pass count right after it (when it passed)
     // frozen-stretch skipping
     uint32_t npend;            // live entries of the pending-pass list pend[start, start + npend)
     uint32_t nsp;              // spans of this segment decided by k_fill (their dec[] words are not written yet)
@@ -2192,6 +2194,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
 
         // ---- evaluation of every event's chain under its view
         uint32_t fe = NO_LANE, fo_m = 0;  // the lane's first mismatching ENTRY and its evaluated outcome
+        uint32_t fu_m = 0;                // its ENTRY acquire units through it (from c0)
+        int64_t fp_m = 0;                 // the round's pass count after it
         uint32_t wq[EP];                  // queueing waits (rate limiters)
         run_reset();
 #pragma unroll
@@ -2258,7 +2262,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         if (o == (uint32_t)nr && !ok) o = (uint32_t)(nf + k);
                     }
                 }
-                if (o != gg[e] && fe == NO_LANE) { fe = (uint32_t)e; fo_m = o; }
+                if (o != gg[e] && fe == NO_LANE) {
+                    fe = (uint32_t)e;
+                    fo_m = o;
+                    fu_m = ex[Q_P] + ex[Q_B] + run[Q_P] + run[Q_B] + (uint32_t)cnt;
+                    fp_m = vP + (o == (uint32_t)nr ? cnt : 0);
+                }
             }
             wq[e] = (uint32_t)(wait > 0xFFFF ? 0xFFFF : wait);
             run_step(e, gg[e]);
@@ -2269,7 +2278,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 const int fl = __ffsll((long long)mm) - 1;
                 const uint32_t fel = (uint32_t)__builtin_amdgcn_readlane((int)fe, fl);
                 const uint32_t fol = (uint32_t)__builtin_amdgcn_readlane((int)fo_m, fl);
-                if (lane == 0) { sh.mism[mb][wv] = (wv * 64 + (uint32_t)fl) * EP + fel; sh.mo[mb][wv] = fol; }
+                const uint32_t ful = (uint32_t)__builtin_amdgcn_readlane((int)fu_m, fl);
+                const uint32_t fpl = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fp_m, fl);
+                const uint32_t fph = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)fp_m >> 32), fl);
+                if (lane == 0) {
+                    sh.mism[mb][wv] = (wv * 64 + (uint32_t)fl) * EP + fel;
+                    sh.mo[mb][wv] = fol;
+                    sh.mu[mb][wv] = ful;
+                    sh.mp[mb][wv] = (int64_t)(((uint64_t)fph << 32) | fpl);
+                }
             } else if (lane == 0) {
                 sh.mism[mb][wv] = NO_LANE;
             }
@@ -2283,6 +2300,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         // outcomes saw the pivot's wrong guess (e.g. a guessed breaker trip blocks everything after it),
         // while a state change at the pivot (reset breaker, spent quota, trip) mostly holds for the rest.
         const uint32_t of = f != NO_LANE ? uni(sh.mo[mb][f / (64 * EP)]) : 0u;
+        // Quota-aware re-guess: when the pivot passed and the first flow stage is a QPS DefaultController,
+        // a later ENTRY of the round passes that stage iff the acquire units between the pivot and it still
+        // fit the rule's count (FlowRuleChecker order, DefaultController.canPass), so the guess is "pass" for
+        // that prefix and "blocked by stage 0" after it instead of "pass" for all -- the iteration that would
+        // find the saturation point is saved.  Guesses only steer the iteration count, never a verdict.
+        bool qg = false;
+        uint32_t q_units = 0;
+        int64_t q_pass = 0;
+        double q_count = 0.0;
+        if (f != NO_LANE && of == (uint32_t)nr && nf > 0 && sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_DEFAULT &&
+            sh.rules[0].grade == SG_FLOW_GRADE_QPS) {
+            qg = true;
+            q_units = uni(sh.mu[mb][f / (64 * EP)]);
+            q_pass = uni64(sh.mp[mb][f / (64 * EP)]);
+            q_count = sh.rules[0].count;
+        }
         mb ^= 1;
         if (f != NO_LANE) ++n_mm;
         const uint32_t e_end = c0 + inr_total;
@@ -2373,8 +2406,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     sh.c0 = cend;
                 }
             } else if (c & JC_ENT) {
-                gg[e] = of;
-                win[pos & (WIN - 1)] = (of == (uint32_t)nr) ? 1 : 0;
+                uint32_t ng = of;
+                if (qg) {
+                    const uint32_t before = ex[Q_P] + ex[Q_B] + run[Q_P] + run[Q_B];  // units before this ENTRY
+                    const int64_t v = q_pass + (int64_t)(before - q_units);
+                    if ((double)j_iadd(j_d2i((double)v), cnt) > q_count) ng = 0u;
+                }
+                gg[e] = ng;
+                win[pos & (WIN - 1)] = (ng == (uint32_t)nr) ? 1 : 0;
             }
             if (pt == cend && cend < cnt_now) sh.tnext = t0 + ev[e].dt;
             run_step(e, g);

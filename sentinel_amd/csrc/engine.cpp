@@ -517,6 +517,7 @@ struct sg_engine {
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
+    bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -1001,9 +1002,9 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* f = std::getenv("SG_DEBUG_FLAGS")) e->dbg_flags = (uint32_t)std::strtoul(f, nullptr, 0);
     if (const char* f = std::getenv("SG_PROF_BIN")) e->prof_bin = std::atoi(f);  // SG_DEBUG counters of J16/J4/J1
     // decide-bin thresholds (segment lengths); tuning knobs, the defaults are the measured best
-    if (const char* v = std::getenv("SG_LANE_MAX")) e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0);
-    if (const char* v = std::getenv("SG_J1_MAX")) e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0);
-    if (const char* v = std::getenv("SG_J4_MAX")) e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0);
+    if (const char* v = std::getenv("SG_LANE_MAX")) { e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
+    if (const char* v = std::getenv("SG_J1_MAX")) { e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
+    if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_SKIP_MIN")) e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
     *out = e;
@@ -1712,7 +1713,18 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
     const uint32_t mb = (uint32_t)std::min<uint64_t>(n, R);
     const uint32_t nblk = (mb + 255) / 256;
-    HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, e->lane_max, e->j1_max, e->j4_max,
+    // Bin thresholds by batch size: a full batch (C4: 2^25 events) keeps the decide stage busy with event
+    // throughput, and wider owners for shorter segments cost more than they save (measured); in a batch of
+    // fewer than 2^24 events -- one rank's shard of a multi-GPU step -- the longest owner chains bound it
+    // instead, so segments get wider owners sooner (tools/shard_rehearsal.sh: 8-way shards of C4, mean
+    // rank step 1.70 -> 1.33 ms, slowest 1.85 -> 1.73 ms).
+    uint32_t lane_max = e->lane_max, j1_max = e->j1_max, j4_max = e->j4_max;
+    if (!e->bins_pinned && n < (1ull << 24)) {
+        lane_max = std::min<uint32_t>(lane_max, 128);
+        j1_max = std::min<uint32_t>(j1_max, 1024);
+        j4_max = std::min<uint32_t>(j4_max, 4096);
+    }
+    HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));

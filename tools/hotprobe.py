@@ -1,6 +1,6 @@
 """Diagnostics: counters of one cooperative bin (SG_DEBUG=1; SG_PROF_BIN = 0 J16, 1 J4, 2 J1) on a C4 batch.
 
-usage: python tools/hotprobe.py [config] [n_entries] [batches]
+usage: python tools/hotprobe.py [config] [n_entries] [batches] [R/N shard]
 """
 import ctypes as C
 import os
@@ -17,6 +17,7 @@ from sentinel_amd import tracegen as T  # noqa: E402
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 n_entries = int(sys.argv[2]) if len(sys.argv) > 2 else 16_400_000
 nb = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+shard = tuple(int(x) for x in sys.argv[4].split("/")) if len(sys.argv) > 4 else None  # R/N: one rank's shard
 t = time.time()
 w = T.Workload(cfg, n_entries=n_entries, n_res=1_000_000 if cfg == 4 else 0)
 print("generated %d events in %.1f s" % (w.n_events, time.time() - t), flush=True)
@@ -24,6 +25,10 @@ eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=22
                max_batch_events=1 << 25)
 w.install(eng)
 ev = w.events
+if shard:
+    from sentinel_amd import dist as D
+    ev, _ = D.shard_stream(ev, shard[1], shard[0])
+    print("shard %d/%d: %d events" % (shard[0], shard[1], len(ev)), flush=True)
 B = min(len(ev) // nb, 1 << 25)
 L = E.lib()
 L.sgx_debug_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
