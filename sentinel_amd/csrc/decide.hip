@@ -1695,31 +1695,38 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 // (streamed), and k_fill writes its verdicts after the decide kernels.
                 const uint32_t skip_min = S.skip_min * NW / 16 > 0 ? S.skip_min * NW / 16 : 1u;  // scaled to the owner's width
                 if (skip_on && sg.len - fpos0 > skip_min && uni(sh.nsp) < NSPAN) {
-                    if (tid == 0) sh.skip_go = (int64_t)recs[sg.start + fpos0 + skip_min].dt < dhi ? 1u : 0u;
-                    lds_barrier();
-                    if (uni(sh.skip_go)) {
-                        // (1) stretch end E = first position with dt >= dhi (dt is non-decreasing); dt[lo] < dhi
-                        uint32_t lo = fpos0, hi = sg.len;
-                        while (hi - lo > 1) {
-                            const uint32_t step = (hi - lo + HW - 1) / HW;
-                            const uint32_t q = lo + (tid + 1) * step;
-                            const bool pr = q < hi && (int64_t)recs[sg.start + q].dt >= dhi;
-                            const uint64_t bm = __ballot(pr);
-                            if (lane == 0) sh.mism[mb][wv] = bm ? wv * 64 + (uint32_t)(__ffsll((long long)bm) - 1) : NO_LANE;
-                            lds_barrier();
-                            uint32_t f = NO_LANE;
-                            for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
-                            f = uni(f);
-                            mb ^= 1;
-                            if (f == NO_LANE) {
-                                uint32_t kl = (hi - 1 - lo) / step;
-                                if (kl > HW) kl = HW;
-                                lo += kl * step;
-                            } else {
-                                hi = lo + (f + 1) * step;
-                                lo = lo + f * step;
-                            }
+                    // (0) the pending passes do not depend on the stretch end: their item loads are issued now and
+                    // land during the search (a memory round trip off the chain; their links are loaded later --
+                    // kept live across the span bookkeeping they would spill the 1024-lane owner's registers)
+                    // (1) stretch end E = first position with dt >= dhi (dt is non-decreasing); dt[lo] < dhi.
+                    // The first probe round also settles whether the stretch is long enough to skip.
+                    uint32_t lo = fpos0, hi = sg.len;
+                    bool go = true, first = true;
+                    while (hi - lo > 1) {
+                        const uint32_t step = (hi - lo + HW - 1) / HW;
+                        const uint32_t q = lo + (tid + 1) * step;
+                        const bool pr = q < hi && (int64_t)recs[sg.start + q].dt >= dhi;
+                        const uint64_t bm = __ballot(pr);
+                        if (lane == 0) sh.mism[mb][wv] = bm ? wv * 64 + (uint32_t)(__ffsll((long long)bm) - 1) : NO_LANE;
+                        lds_barrier();
+                        uint32_t f = NO_LANE;
+                        for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                        f = uni(f);
+                        mb ^= 1;
+                        if (f == NO_LANE) {
+                            uint32_t kl = (hi - 1 - lo) / step;
+                            if (kl > HW) kl = HW;
+                            lo += kl * step;
+                        } else {
+                            hi = lo + (f + 1) * step;
+                            lo = lo + f * step;
                         }
+                        if (first) {
+                            first = false;
+                            if (hi <= fpos0 + skip_min) { go = false; break; }  // E <= hi: too short, stream it
+                        }
+                    }
+                    if (go && hi - fpos0 > skip_min) {
                         const uint32_t E = hi;
                         const uint32_t A = sg.start + fpos0, B = sg.start + E;  // absolute positions
                         const uint32_t nch = (B - A + SPAN_CHUNK - 1) / SPAN_CHUNK;
