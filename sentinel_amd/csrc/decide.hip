@@ -1695,9 +1695,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 // (streamed), and k_fill writes its verdicts after the decide kernels.
                 const uint32_t skip_min = S.skip_min * NW / 16 > 0 ? S.skip_min * NW / 16 : 1u;  // scaled to the owner's width
                 if (skip_on && sg.len - fpos0 > skip_min && uni(sh.nsp) < NSPAN) {
-                    // (0) the pending passes do not depend on the stretch end: their item loads are issued now and
-                    // land during the search (a memory round trip off the chain; their links are loaded later --
-                    // kept live across the span bookkeeping they would spill the 1024-lane owner's registers)
                     // (1) stretch end E = first position with dt >= dhi (dt is non-decreasing); dt[lo] < dhi.
                     // The first probe round also settles whether the stretch is long enough to skip.
                     uint32_t lo = fpos0, hi = sg.len;
