@@ -50,7 +50,7 @@ __device__ __forceinline__ double j_next_up(double d) {
     b += (d > 0.0) ? 1 : -1;
     return __longlong_as_double(b);
 }
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
     x ^= x >> 27; x *= 0x94d049bb133111ebULL;
     x ^= x >> 31; return x;

@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include "chain.h"
+#include "pmap.h"
 
 using namespace sg;
 
@@ -129,11 +130,14 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  const Prog* __restrict__ prog, const uint32_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
-                                                 uint32_t nblk) {
+                                                 uint32_t nblk, uint32_t pq_ok, const uint32_t* __restrict__ bflags,
+                                                 uint32_t pq_wide) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const uint32_t m = *mp;  // segment count (the grid covers an upper bound: no host round trip)
+    // k_pq runs in batches without sg_submit_ex context/args and without EXITs that release thread counts
+    const bool pq = pq_ok && !force_lane && !(*bflags & BF_EXIT_ARGS);
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < m) {
         Seg sg = segs[s];
@@ -144,7 +148,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
                           !prio[sg.res] && !p.multi;
         uint32_t bin;
-        if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
+        if (pq && (p.pflags & PF_PQ) && !prio[sg.res]) bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
+        else if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
@@ -372,69 +377,10 @@ __global__ void k_chain(const SEv* __restrict__ recs, const uint32_t* __restrict
 }
 
 // =================================================================================
-// ParameterMetric's bounded LRU maps (PMap, dev_types.h).  Every operation below is the CacheMap call the
-// reference makes, with ConcurrentLinkedHashMap's access order: get / putIfAbsent of a present key move it
-// to the MRU end, an insert into a full map evicts the LRU entry.  A map is private to its resource's lane.
+// ParameterMetric's bounded LRU maps (pmap.h).  Every operation below is the CacheMap call the reference makes,
+// with ConcurrentLinkedHashMap's access order: get / putIfAbsent of a present key move it to the MRU end, an
+// insert into a full map evicts the LRU entry.  A map is private to its resource's owner.
 // =================================================================================
-__device__ __forceinline__ uint32_t pm_home(const PMap& m, uint64_t v) {
-    return (uint32_t)(((mix64(v) >> 32) * (uint64_t)m.slots) >> 32);
-}
-__device__ __forceinline__ uint32_t pm_next(const PMap& m, uint32_t i) { return i + 1 == m.slots ? 0 : i + 1; }
-__device__ uint32_t pm_find(const PMap& m, const PSlot* R, uint64_t v) {
-    for (uint32_t i = pm_home(m, v);; i = pm_next(m, i)) {  // a region always has a free slot
-        if (!R[i].used) return PM_NIL;
-        if (R[i].kval == v) return i;
-    }
-}
-__device__ __forceinline__ void lru_unlink(PMap& m, PSlot* R, uint32_t i) {
-    const uint32_t p = R[i].prev, n = R[i].next;
-    if (p != PM_NIL) R[p].next = n; else m.head = n;
-    if (n != PM_NIL) R[n].prev = p; else m.tail = p;
-}
-__device__ __forceinline__ void lru_front(PMap& m, PSlot* R, uint32_t i) {
-    R[i].prev = PM_NIL;
-    R[i].next = m.head;
-    if (m.head != PM_NIL) R[m.head].prev = i; else m.tail = i;
-    m.head = i;
-}
-__device__ __forceinline__ void pm_touch(PMap& m, PSlot* R, uint32_t i) {
-    if (m.head != i) { lru_unlink(m, R, i); lru_front(m, R, i); }
-}
-// remove slot i: unlink it, then backward-shift the probe run behind it (linear probing keeps no tombstones)
-__device__ void pm_erase(PMap& m, PSlot* R, uint32_t i) {
-    lru_unlink(m, R, i);
-    m.count--;
-    for (uint32_t j = pm_next(m, i); R[j].used; j = pm_next(m, j)) {
-        const uint32_t k = pm_home(m, R[j].kval);
-        const bool move = i <= j ? (k <= i || k > j) : (k <= i && k > j);  // home not in (i, j] cyclically
-        if (!move) continue;
-        R[i] = R[j];
-        if (R[i].prev != PM_NIL) R[R[i].prev].next = i; else m.head = i;
-        if (R[i].next != PM_NIL) R[R[i].next].prev = i; else m.tail = i;
-        i = j;
-    }
-    R[i].used = 0;
-}
-// insert an absent key at the MRU end; a full map loses its LRU entry (CLHM evicts after the insert: same set)
-__device__ uint32_t pm_insert(PMap& m, PSlot* R, uint64_t v) {
-    if (m.count >= m.cap) pm_erase(m, R, m.tail);
-    uint32_t i = pm_home(m, v);
-    while (R[i].used) i = pm_next(m, i);
-    R[i].kval = v;
-    R[i].v0 = 0;
-    R[i].v1 = 0;
-    R[i].used = 1;
-    m.count++;
-    lru_front(m, R, i);
-    return i;
-}
-__device__ __forceinline__ void pm_store(const DevState& S, uint32_t id, const PMap& m) {
-    PMap* h = &S.pmap[id];
-    h->count = m.count;
-    h->head = m.head;
-    h->tail = m.tail;
-}
-
 __device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool* found) {
     for (uint32_t i = 0; i < r.hot_n; ++i) {
         DHot h = S.hot[r.hot_off + i];
@@ -451,36 +397,34 @@ __device__ int64_t thread_count_get(const DevState& S, uint32_t tm_base, uint32_
     const uint32_t id = tmap_of(S, tm_base, idx);
     if (id == NO_ID) return 0;
     PMap m = S.pmap[id];
-    PSlot* R = S.pslot + m.base;
-    const uint32_t i = pm_find(m, R, v);
-    if (i == PM_NIL) return 0;
-    pm_touch(m, R, i);
+    const PRef R = pm_ref(S, m);
+    const int32_t i = pm_get(m, R, v);
     pm_store(S, id, m);
-    return R[i].v0;
+    return i < 0 ? 0 : R.D[i].v0;
 }
 // addThreadCount / decreaseThreadCount of one value (ParameterMetric.java:117-231):
 //   add: putIfAbsent(v, 0) then increment, or put(v, 1) when it was absent;
 //   decrease: putIfAbsent(v, 0) -- an absent value stays at 0 -- else decrement, removed at <= 0
-__device__ void thread_count_add(const DevState& S, uint32_t tm_base, uint32_t idx, uint64_t v, int64_t d) {
+__device__ void thread_count_add(const DevState& S, uint32_t tm_base, uint32_t idx, uint64_t v, int64_t d,
+                                 uint32_t* bflags) {
     const uint32_t id = tmap_of(S, tm_base, idx);
     if (id == NO_ID) return;
     PMap m = S.pmap[id];
-    PSlot* R = S.pslot + m.base;
-    uint32_t i = pm_find(m, R, v);
-    if (i == PM_NIL) {
-        i = pm_insert(m, R, v);
-        R[i].v0 = d > 0 ? 1 : 0;
+    const PRef R = pm_ref(S, m);
+    bool present;
+    const int32_t i = pm_put(m, R, v, &present, bflags);
+    if (!present) {
+        R.D[i].v0 = d > 0 ? 1 : 0;
     } else {
-        pm_touch(m, R, i);
-        const int64_t c = R[i].v0 + (d > 0 ? 1 : -1);
+        const int64_t c = R.D[i].v0 + (d > 0 ? 1 : -1);
         if (c <= 0 && d < 0) pm_erase(m, R, i);
-        else R[i].v0 = c;
+        else R.D[i].v0 = c;
     }
     pm_store(S, id, m);
 }
 // ParamFlowChecker.passSingleValueCheck (ParamFlowChecker.java:101-119) of one value
 __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r, uint32_t idx, int acquire, uint64_t v,
-                            int64_t t, int64_t& wait) {
+                            int64_t t, int64_t& wait, uint32_t* bflags) {
     if (r.grade == SG_FLOW_GRADE_QPS) {
         bool hf;
         int32_t hc = hot_count(S, r, v, &hf);
@@ -489,19 +433,19 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
             if (token_count == 0) return false;
             int64_t cost = j_round(1.0 * 1000 * acquire * (double)r.duration_sec / (double)token_count);
             PMap m = S.pmap[r.pmap];
-            PSlot* R = S.pslot + m.base;
-            uint32_t i = pm_find(m, R, v);  // timeRecorderMap.putIfAbsent(value, now)
+            const PRef R = pm_ref(S, m);
+            bool present;
+            const int32_t i = pm_put(m, R, v, &present, bflags);  // timeRecorderMap.putIfAbsent(value, now)
             bool ok = true;
-            if (i == PM_NIL) {
-                i = pm_insert(m, R, v);
-                R[i].v0 = t;
+            if (!present) {
+                R.D[i].v0 = t;
             } else {
-                pm_touch(m, R, i);
-                const int64_t expected = R[i].v0 + cost;
+                const int64_t last = R.D[i].v0;
+                const int64_t expected = last + cost;
                 if (expected <= t || expected - t < r.max_queue) {
-                    R[i].v0 = t;
                     const int64_t w = expected - t;
-                    if (w > 0) { R[i].v0 = expected; wait += w; }
+                    R.D[i].v0 = w > 0 ? expected : t;
+                    if (w > 0) wait += w;
                 } else {
                     ok = false;
                 }
@@ -515,24 +459,27 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
         int32_t max_count = j_iadd(token_count, r.burst);
         if (acquire > max_count) return false;
         PMap m = S.pmap[r.pmap];
-        PSlot* R = S.pslot + m.base;
-        uint32_t i = pm_find(m, R, v);  // timeCounters.putIfAbsent, then tokenCounters.putIfAbsent / get
+        const PRef R = pm_ref(S, m);
+        bool present;
+        const int32_t i = pm_put(m, R, v, &present, bflags);  // timeCounters.putIfAbsent, then tokenCounters
         bool ok = true;
-        if (i == PM_NIL) {
-            i = pm_insert(m, R, v);
-            R[i].v0 = t;
-            R[i].v1 = j_iadd(max_count, -acquire);
+        if (!present) {
+            PData d;
+            d.v0 = t;
+            d.v1 = j_iadd(max_count, -acquire);
+            d.pad = 0;
+            R.D[i] = d;
         } else {
-            pm_touch(m, R, i);
-            const int64_t pass_time = t - R[i].v0;
+            PData d = R.D[i];
+            const int64_t pass_time = t - d.v0;
             if (pass_time > r.duration_sec * 1000) {
                 int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
-                int32_t sum = j_iadd(R[i].v1, to_add);
+                int32_t sum = j_iadd(d.v1, to_add);
                 int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
                 if (nq < 0) ok = false;
-                else { R[i].v1 = nq; R[i].v0 = t; }
-            } else if (j_iadd(R[i].v1, -acquire) >= 0) {
-                R[i].v1 = j_iadd(R[i].v1, -acquire);
+                else { d.v1 = nq; d.v0 = t; R.D[i] = d; }
+            } else if (j_iadd(d.v1, -acquire) >= 0) {
+                R.D[i].v1 = j_iadd(d.v1, -acquire);
             } else {
                 ok = false;
             }
@@ -578,7 +525,8 @@ __device__ __forceinline__ sg_arg evx_arg(const EvX& x, uint32_t i) {
 // ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:126-241): every index with a
 // thread-count map; a null element of a Collection/array throws inside the try that wraps the whole loop,
 // so the remaining elements and indices are skipped.
-__device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags, const EvX& x, int64_t d) {
+__device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags, const EvX& x, int64_t d,
+                            uint32_t* bflags) {
     for (uint32_t i = 0; i < x.n && i < SG_MAX_ARGS; ++i) {
         if (!(nflags & ni_tm(i))) continue;
         const sg_arg v = evx_arg(x, i);
@@ -586,10 +534,10 @@ __device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags
             for (uint32_t k = 0; k < v.len; ++k) {
                 const sg_arg el = S.args[v.key + k];
                 if (el.kind != SG_ARG_SCALAR) return;
-                thread_count_add(S, tm_base, i, el.key, d);
+                thread_count_add(S, tm_base, i, el.key, d, bflags);
             }
         } else if (v.kind == SG_ARG_SCALAR) {
-            thread_count_add(S, tm_base, i, v.key, d);
+            thread_count_add(S, tm_base, i, v.key, d, bflags);
         }
     }
 }
@@ -752,10 +700,10 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                     for (uint32_t k = 0; k < v.len && ok; ++k) {
                         const sg_arg el = S.args[v.key + k];
                         if (el.kind != SG_ARG_SCALAR) break;  // a null element throws: passLocalCheck passes
-                        ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, el.key, t, w);
+                        ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, el.key, t, w, bflags);
                     }
                 } else if (v.kind == SG_ARG_SCALAR) {
-                    ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, v.key, t, w);
+                    ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, v.key, t, w, bflags);
                 }
                 if (!ok) { status = ST_BLOCK_PARAM; slot = r.slot; }
                 else wait += w;
@@ -790,13 +738,13 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
     }
     if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
         N.thread++;
-        if (N.flags & NI_PM) thread_args(S, pg.tm_base, N.flags, x, 1);
+        if (N.flags & NI_PM) thread_args(S, pg.tm_base, N.flags, x, 1, bflags);
         return mk_dec(ST_PASS_WAIT, slot, wait);
     }
     const bool passed = status == ST_PASS;
     stat_entry(N, C, t, cnt, passed);
     // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount(args)
-    if (passed && (N.flags & NI_PM)) thread_args(S, pg.tm_base, N.flags, x, 1);
+    if (passed && (N.flags & NI_PM)) thread_args(S, pg.tm_base, N.flags, x, 1, bflags);
     return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
 }
 
@@ -815,13 +763,13 @@ __device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState&
             aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
     }
     if (!(r.flags & SG_F_EXIT_ARGS) || !(N.flags & NI_PM)) return;
-    if (x.n) { thread_args(S, pg.tm_base, N.flags, x, -1); return; }
+    if (x.n) { thread_args(S, pg.tm_base, N.flags, x, -1, bflags); return; }
     if (!S.key_ring || ref == SG_REF_NONE) return;
     const uint64_t key = S.key_ring[ref & cfg.ring_mask];
     if (key == NO_KEY) return;
     EvX k;
     k.origin = 0; k.ctx = 0; k.n = 1; k.a = nullptr; k.k0 = key;
-    thread_args(S, pg.tm_base, N.flags, k, -1);
+    thread_args(S, pg.tm_base, N.flags, k, -1, bflags);
 }
 
 // A STRATEGY_RELATE component (one segment, members in event order): each event runs on its own
@@ -2504,11 +2452,11 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 // mp: the segment count on the device; mb: an upper bound of it (the grid)
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          hipStream_t st) {
+                          uint32_t pq_ok, const uint32_t* bflags, uint32_t pq_wide, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk);
+                       blkcnt, nblk, pq_ok, bflags, pq_wide);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

@@ -8,8 +8,9 @@
 //   DRule   rules[]       compiled rule constants
 //   RState  rstate[]      controller / breaker state (one per rule)
 //   PMap    pmap[]        ParameterMetric's CacheMaps: one bounded LRU map per (param rule state) and per
-//                         (resource, paramIdx) thread-count map, each a private open-addressing region of
-//   PSlot   pslot[]       the slot pool (linear probing, backward-shift deletion, doubly linked LRU list)
+//                         (resource, paramIdx) thread-count map, each a private region of
+//   PBucket pbkt[]        the cuckoo bucket pool (keys + access stamps), PData pdat[] their values, and
+//   uint64  pbm[]         the live-stamp rings (recency order, pmap.h)
 //   uint8   ring[2^k]     status of every ENTRY by global event index (EXIT/TRACE references)
 // All counters are int64 exactly as the Java LongAdders; RT sums are int64.
 #pragma once
@@ -65,6 +66,8 @@ static_assert(sizeof(NodeInfo) == 32, "NodeInfo must be 32 B");
 enum : uint8_t {
     PF_EXC_COUNT = 1,   // has an EXCEPTION_COUNT breaker (minute exception running sum)
     PF_WARM = 2,        // has a WarmUp / WarmUpRateLimiter controller
+    PF_PQ = 4,          // only QPS-grade param rules with a fixed paramIdx and maps of capacity <= 4080: the
+                        // cooperative param owner (param.hip k_pq) decides it in batches it is enabled for
     PF_SERIAL = 8,      // outside the cooperative (Jacobi) kernels' limits: per-lane serial kernel only
     PF_RL = 16,         // has a RateLimiter / WarmUpRateLimiter controller
     PF_RT = 32,         // has an RT breaker
@@ -142,27 +145,41 @@ struct RState {
 // `cap` entries, least-recently-used evicted on insert.  A rule's ruleTimeCounters and ruleTokenCounter maps
 // see the same key sequence (every passDefaultLocalCheck touches both, time first), so they always hold the
 // same keys in the same LRU order and share one map here (v0 = time, v1 = tokens).  A map is owned by one
-// resource and only its lane touches it: no atomics.
-#define PM_NIL 0xFFFFFFFFu
-struct PMap {
-    uint64_t base;   // first slot in DevState.pslot
-    uint32_t slots;  // region size (> cap: the probe always finds a free slot)
-    uint32_t cap;    // min(4000 * durationInSec, 200000) for rule maps, 4000 for thread-count maps
-    uint32_t count;
-    uint32_t head;   // most recently used slot (region-local), PM_NIL when empty
-    uint32_t tail;   // least recently used
-    uint32_t pad;
+// resource and only its owner (a lane of k_lane, or a k_pq workgroup) touches it.
+//
+// Representation (pmap.h): recency is a per-map access stamp, not a linked list.  Every access gives the key
+// the next stamp (clock++); the live keys are exactly the `live` largest stamps of keys not evicted or erased,
+// recorded in a ring bitmap of 2^rb_log2 bits (bit stamp mod 2^rb_log2; every live stamp lies in
+// [clock - 2^rb_log2, clock)).  The least recently used key is the lowest set bit at or after `thr`; evicting it
+// clears the bit and nothing else (its slot is dead from then on and is reused by inserts).  The recency rank of
+// a key -- how many live keys are more recent -- is a popcount over the ring, which is what lets k_pq decide a
+// whole tile of accesses at once (LRU residency = fewer than `cap` distinct keys accessed since the key's stamp).
+// Keys live in a two-choice bucketed cuckoo table: a bucket is one 128-byte line of 8 keys + their 8 stamps.
+#define PM_BKT 8
+#define PK_EMPTY 0xFFFFFFFFFFFFFFFFull  // never-used key slot (param keys are type-tagged, never all-ones)
+struct PBucket {
+    uint64_t key[PM_BKT];
+    int64_t stamp[PM_BKT];  // stamp of the key's last access (live iff its ring bit is set, see pmap.h)
 };
-static_assert(sizeof(PMap) == 32, "PMap must be 32 B");
-struct PSlot {
-    uint64_t kval;   // parameter value key
+static_assert(sizeof(PBucket) == 128, "PBucket must be one 128-byte line");
+struct PData {
     int64_t v0;      // rule map: last add time / throttle last pass time; thread map: count
     int32_t v1;      // rule map: tokens
-    uint32_t prev;   // LRU neighbours (region-local slots, PM_NIL at the ends)
-    uint32_t next;
-    uint32_t used;
+    uint32_t pad;
 };
-static_assert(sizeof(PSlot) == 32, "PSlot must be 32 B");
+static_assert(sizeof(PData) == 16, "PData must be 16 B");
+struct PMap {
+    uint64_t base;   // first bucket in DevState.pbkt (its slots' data at pdat[base * PM_BKT ...])
+    uint64_t bm;     // first word of the live-stamp ring in DevState.pbm (and of the rank scratch in pre)
+    int64_t clock;   // next stamp
+    int64_t thr;     // <= the lowest live stamp (eviction scans start here)
+    uint32_t nb;     // buckets (>= 2)
+    uint32_t cap;    // min(4000 * durationInSec, 200000) for rule maps, 4000 for thread-count maps
+    uint32_t live;   // keys in the map
+    uint32_t rb_log2;// ring bits = 2^rb_log2 >= 4 * cap
+    uint32_t pad[4];
+};
+static_assert(sizeof(PMap) == 64, "PMap must be 64 B");
 #define PM_BASE_CAP 4000u      // ParameterMetric.BASE_PARAM_MAX_CAPACITY / THREAD_COUNT_MAX_CAPACITY
 #define PM_TOTAL_CAP 200000u   // ParameterMetric.TOTAL_MAX_CAPACITY
 
@@ -287,7 +304,10 @@ struct DevState {
     RState* rstate;
     const DHot* hot;
     PMap* pmap;               // ParameterMetric maps (see PMap)
-    PSlot* pslot;
+    PBucket* pbkt;            // their key/stamp buckets
+    PData* pdat;              // their values, one per bucket slot
+    uint64_t* pbm;            // their live-stamp rings
+    uint32_t* ppre;           // per ring word: rank scratch of a lane-side compaction (pmap.h pm_compact)
     const uint32_t* tmid;     // [Prog.tm_base + paramIdx] -> thread-count map (NO_ID: none)
     uint8_t* ring;
     unsigned long long* dbg;  // optional per-batch diagnostics (SG_DEBUG=1), else null
@@ -313,7 +333,9 @@ struct DevState {
     uint64_t aux_mask;
 };
 
-enum : uint32_t { BF_PRIORITIZED = 1, BF_EXIT_ARGS = 2, BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
+enum : uint32_t { BF_PRIORITIZED = 1,
+                  BF_EXIT_ARGS = 2,     // an EXIT releases thread counts (SG_F_EXIT_ARGS): no k_pq this batch
+                  BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
                   BF_BACKWARD = 32, BF_TSPAN = 64,
                   BF_BAD_ARGS = 512,    // an sg_event_ext names args outside the table, or more than SG_MAX_ARGS
                   BF_AUX_FULL = 1024,   // the origin / context node pool is full
@@ -348,8 +370,10 @@ enum : uint32_t {
     BIN_J16 = 0,           // one 1024-lane workgroup per segment (Zipf head)
     BIN_J4 = 1,            // one 256-lane workgroup per segment
     BIN_J1 = 2,            // one wavefront per segment
-    BIN_LANE = 3,          // one lane per segment, nr <= 4: bins 3..3+LANE_BINS-1 by descending log2(len)
-    LANE_BINS = 20,
+    BIN_PQ16 = 3,          // PF_PQ segments: one 1024-lane k_pq workgroup (long segments)
+    BIN_PQ4 = 4,           //                 one 256-lane k_pq workgroup
+    BIN_LANE = 5,          // one lane per segment, nr <= 4: bins 5..5+LANE_BINS-1 by descending log2(len)
+    LANE_BINS = 19,
     BIN_LANE16 = BIN_LANE + LANE_BINS,  // one lane per segment, nr > 4 (rule state in scratch)
     BIN_LITE = BIN_LANE16 + LANE_BINS,  // one lane per segment, DefaultController flows + breakers only (k_lite)
     N_BINS = BIN_LITE + LANE_BINS       // <= 63: k_bin_offsets runs one 64-lane wave

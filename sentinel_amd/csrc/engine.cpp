@@ -40,14 +40,18 @@ hipError_t launch_snapshot(Bkt*, NodeInfo*, uint32_t, int64_t, int32_t, uint32_t
                            sg_metric_node*, uint64_t, hipStream_t);
 hipError_t launch_init_state(Bkt* sec, Bkt* minb, NodeInfo* info, int64_t* borrow, uint32_t nres, hipStream_t st);
 hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hipStream_t st);
-hipError_t launch_region_copy(const PSlot* src, PSlot* dst, const uint64_t* tri, uint32_t n, hipStream_t st);
+hipError_t launch_region_copy(const uint64_t* src, uint64_t* dst, const uint64_t* tri, uint32_t n, hipStream_t st);
 // decide.hip
 hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t* pos, Seg* segs, hipStream_t st,
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t* part, uint32_t* nseg);
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          hipStream_t st);
+                          uint32_t pq_ok, const uint32_t* bflags, uint32_t pq_wide, hipStream_t st);
+// param.hip
+hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                     const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
+                     uint32_t* bflags, hipStream_t st);
 hipError_t launch_seg_order(Seg* segs, const uint32_t* mp, uint32_t mb, const uint32_t* off, uint32_t* order,
                             uint32_t* bin_off, hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
@@ -427,7 +431,7 @@ struct sg_engine {
     std::vector<uint64_t> pmap_key;                             // map index -> psid, or TMAP_KEY | res << 8 | idx
     std::unordered_map<uint32_t, uint32_t> pmap_index;         // psid -> map index
     std::vector<uint32_t> tm_base;                              // per resource: Prog.tm_base
-    uint64_t n_pslot = 0;
+    uint64_t n_pslot = 0;                                       // bucket slots in the pool (param_table_log2 bound)
     uint32_t n_dev_rules = 0;
 
     // device state
@@ -439,7 +443,10 @@ struct sg_engine {
     RState* d_rstate = nullptr;
     DHot* d_hot = nullptr;
     PMap* d_pmap = nullptr;
-    PSlot* d_pslot = nullptr;
+    PBucket* d_pbkt = nullptr;
+    PData* d_pdat = nullptr;
+    uint64_t* d_pbm = nullptr;
+    uint32_t* d_ppre = nullptr;
     uint32_t* d_tmid = nullptr;
     uint8_t* d_ring = nullptr;
     uint32_t rules_cap = 0, hot_cap = 0;
@@ -519,6 +526,8 @@ struct sg_engine {
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
+    bool pq_on = true;          // PF_PQ segments to k_pq (SG_PQ=0: the per-lane kernel, as before round 3)
+    uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -646,6 +655,7 @@ static int collect(sg_engine* e, int k) {
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
+    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "a hot-parameter map table could not place a key");
     return SG_OK;
 }
 // every batch in flight done (called by the API functions that read or write engine state)
@@ -659,6 +669,12 @@ static int drain(sg_engine* e) {
     return rc;
 }
 
+
+// CacheMap capacity of a rule's time/token maps (ParameterMetric.initialize, ParameterMetric.java:87-104)
+static uint32_t rule_map_cap(int64_t duration_sec) {
+    const int64_t c = (int64_t)PM_BASE_CAP * std::max<int64_t>(duration_sec, 1);
+    return (uint32_t)std::min<int64_t>(c, PM_TOTAL_CAP);
+}
 
 // Build the device rule program of every resource from the compiled host lists.
 int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool reset_par_state) {
@@ -813,6 +829,15 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || d.grade != SG_FLOW_GRADE_QPS) all_default_qps = false;
             }
             if (all_default_qps) p.pflags |= PF_FROZEN;
+            // k_pq (param.hip): QPS-grade param rules with a fixed paramIdx and LDS-sized rings, nothing else
+            bool pq = p.n_param >= 1 && p.n_param <= 4 && p.n_flow == 0 && p.n_degrade == 0 && !p.multi;
+            for (int i = 0; i < p.n_param && pq; ++i) {
+                const DRule& d = rules[p.rule_off + i];
+                if (d.param_idx < 0) pq = false;
+                else if (d.behavior == PB_INIT_ONLY) continue;
+                else if (d.grade != SG_FLOW_GRADE_QPS || rule_map_cap(d.duration_sec) > 4080) pq = false;
+            }
+            if (pq) p.pflags |= PF_PQ;
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
         }
         // carry controller / breaker state of kinds that were not reloaded
@@ -1007,6 +1032,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J1_MAX")) { e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
+    if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
+    if (const char* v = std::getenv("SG_PQ_WIDE")) e->pq_wide = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_SKIP_MIN")) {
         e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
         e->skip_pinned = true;
@@ -1056,7 +1083,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
-    dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pslot); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
+    dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt);
@@ -1419,34 +1446,38 @@ static int rebuild_cluster_param(sg_engine* e, const sg_param_rule* rules, const
 
 // ---- ParameterMetric maps (dev_types.h PMap)
 #define TMAP_KEY (1ull << 63)
-// CacheMap capacity of a rule's time/token maps (ParameterMetric.initialize, ParameterMetric.java:87-104)
-static uint32_t rule_map_cap(int64_t duration_sec) {
-    const int64_t c = (int64_t)PM_BASE_CAP * std::max<int64_t>(duration_sec, 1);
-    return (uint32_t)std::min<int64_t>(c, PM_TOTAL_CAP);
+// A map's cuckoo table: two-choice buckets of PM_BKT slots at <= 50 % load; its live-stamp ring: >= 4 x cap bits
+static uint32_t map_buckets(uint32_t cap) { return std::max<uint32_t>(2u, (2u * cap + PM_BKT - 1) / PM_BKT); }
+static uint32_t region_slots(uint32_t cap) { return map_buckets(cap) * PM_BKT; }
+static uint32_t ring_log2(uint32_t cap) {
+    uint32_t k = 10;
+    while ((1ull << k) < 4ull * cap + 64) ++k;
+    return k;
 }
-// region slots: at most 2/3 full, so linear probes stay short and always meet a free slot
-static uint32_t region_slots(uint32_t cap) { return (uint32_t)((((uint64_t)cap * 3 / 2 + 1) + 63) & ~63ull); }
 
-// Lay out one region per map in a fresh slot pool, carrying the entries, counts and LRU order of the maps that
-// stay.  Everything that can fail (the capacity check, the allocations) happens before the engine changes:
-// an SG_ECAPACITY leaves the old maps in place.
+// Lay out one region per map in fresh pools, carrying the entries, stamps, rings and counters of the maps that
+// stay.  Everything that can fail (the capacity check, the allocations) happens before the engine changes: an
+// SG_ECAPACITY leaves the old maps in place.
 static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap, const std::set<uint64_t>& tmaps) {
     std::vector<uint64_t> keys;
     std::vector<PMap> hdr;
-    uint64_t total = 0;
+    uint64_t nbkt = 0, nword = 0;
     auto add = [&](uint64_t key, uint32_t cap) {
         PMap m;
         std::memset(&m, 0, sizeof(m));
-        m.base = total;
+        m.base = nbkt;
+        m.nb = map_buckets(cap);
         m.cap = cap;
-        m.slots = region_slots(cap);
-        m.head = m.tail = PM_NIL;
+        m.rb_log2 = ring_log2(cap);
+        m.bm = nword;
         keys.push_back(key);
         hdr.push_back(m);
-        total += m.slots;
+        nbkt += m.nb;
+        nword += (1ull << m.rb_log2) / 64;
     };
     for (const auto& kv : rcap) add(kv.first, kv.second);
     for (uint64_t t : tmaps) add(TMAP_KEY | t, PM_BASE_CAP);
+    const uint64_t total = nbkt * PM_BKT;
     if (total > (1ull << e->cfg.param_table_log2))
         return fail(SG_ECAPACITY, "hot-parameter maps need " + std::to_string(total) + " slots, param_table_log2 = " +
                                       std::to_string(e->cfg.param_table_log2) + " allows " +
@@ -1455,16 +1486,19 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     if (!old.empty()) HIPCHK(hipMemcpy(old.data(), e->d_pmap, old.size() * sizeof(PMap), hipMemcpyDeviceToHost));
     std::unordered_map<uint64_t, uint32_t> was;
     for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i) was[e->pmap_key[i]] = i;
-    std::vector<uint64_t> tri;
+    std::vector<uint64_t> tri_b, tri_d, tri_w;  // {source word, destination word, words} per pool
     for (size_t i = 0; i < keys.size(); ++i) {
         auto it = was.find(keys[i]);
         if (it == was.end()) continue;
         const PMap& o = old[it->second];
-        if (o.slots != hdr[i].slots) continue;  // cannot happen: a map's capacity is fixed by its identity
-        hdr[i].count = o.count;
-        hdr[i].head = o.head;
-        hdr[i].tail = o.tail;
-        tri.insert(tri.end(), {o.base, hdr[i].base, (uint64_t)o.slots});
+        if (o.nb != hdr[i].nb || o.rb_log2 != hdr[i].rb_log2) continue;  // cannot happen: fixed by the map's identity
+        hdr[i].clock = o.clock;
+        hdr[i].thr = o.thr;
+        hdr[i].live = o.live;
+        const uint64_t bw = sizeof(PBucket) / 8, dw = PM_BKT * sizeof(PData) / 8;
+        tri_b.insert(tri_b.end(), {o.base * bw, hdr[i].base * bw, (uint64_t)o.nb * bw});
+        tri_d.insert(tri_d.end(), {o.base * dw, hdr[i].base * dw, (uint64_t)o.nb * dw});
+        tri_w.insert(tri_w.end(), {o.bm, hdr[i].bm, (1ull << o.rb_log2) / 64});
     }
     std::vector<uint32_t> tb(e->names.size(), NO_ID), tmid;
     for (size_t i = 0; i < keys.size(); ++i) {
@@ -1474,30 +1508,50 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
         if (tb[r] == NO_ID) { tb[r] = (uint32_t)tmid.size(); tmid.resize(tmid.size() + SG_MAX_ARGS, NO_ID); }
         tmid[tb[r] + idx] = (uint32_t)i;
     }
-    PSlot* np = nullptr;
+    PBucket* nbk = nullptr;
+    PData* ndt = nullptr;
+    uint64_t* nbm = nullptr;
+    uint32_t* npr = nullptr;
     PMap* nh = nullptr;
     uint32_t* nt = nullptr;
     uint64_t* dtri = nullptr;
-    auto release = [&]() { dfree(np); dfree(nh); dfree(nt); dfree(dtri); };
-    if ((total && hipMalloc(&np, total * sizeof(PSlot)) != hipSuccess) ||
+    auto release = [&]() { dfree(nbk); dfree(ndt); dfree(nbm); dfree(npr); dfree(nh); dfree(nt); dfree(dtri); };
+    const size_t ntri = std::max(tri_b.size(), std::max(tri_d.size(), tri_w.size()));
+    if ((nbkt && (hipMalloc(&nbk, nbkt * sizeof(PBucket)) != hipSuccess ||
+                  hipMalloc(&ndt, total * sizeof(PData)) != hipSuccess ||
+                  hipMalloc(&nbm, nword * 8) != hipSuccess || hipMalloc(&npr, nword * 4) != hipSuccess)) ||
         (!hdr.empty() && hipMalloc(&nh, hdr.size() * sizeof(PMap)) != hipSuccess) ||
         (!tmid.empty() && hipMalloc(&nt, tmid.size() * 4) != hipSuccess) ||
-        (!tri.empty() && hipMalloc(&dtri, tri.size() * 8) != hipSuccess)) {
+        (ntri && hipMalloc(&dtri, 3 * ntri * 8) != hipSuccess)) {
         release();
         (void)hipGetLastError();
         return fail(SG_ECAPACITY, "device memory for " + std::to_string(total) + " hot-parameter map slots");
     }
-    if (total) HIPCHK(hipMemsetAsync(np, 0, total * sizeof(PSlot), e->stream));
+    if (nbkt) {
+        HIPCHK(hipMemsetAsync(nbk, 0xFF, nbkt * sizeof(PBucket), e->stream));  // PK_EMPTY keys
+        HIPCHK(hipMemsetAsync(ndt, 0, total * sizeof(PData), e->stream));
+        HIPCHK(hipMemsetAsync(nbm, 0, nword * 8, e->stream));
+    }
     if (!hdr.empty()) HIPCHK(hipMemcpyAsync(nh, hdr.data(), hdr.size() * sizeof(PMap), hipMemcpyHostToDevice, e->stream));
     if (!tmid.empty()) HIPCHK(hipMemcpyAsync(nt, tmid.data(), tmid.size() * 4, hipMemcpyHostToDevice, e->stream));
-    if (!tri.empty()) {
+    auto copy = [&](const std::vector<uint64_t>& tri, const void* src, void* dst) -> int {
+        if (tri.empty()) return SG_OK;
         HIPCHK(hipMemcpyAsync(dtri, tri.data(), tri.size() * 8, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(launch_region_copy(e->d_pslot, np, dtri, (uint32_t)(tri.size() / 3), e->stream));
-    }
+        HIPCHK(launch_region_copy(reinterpret_cast<const uint64_t*>(src), reinterpret_cast<uint64_t*>(dst), dtri,
+                                  (uint32_t)(tri.size() / 3), e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));  // dtri is reused by the next pool
+        return SG_OK;
+    };
+    if (int rc = copy(tri_b, e->d_pbkt, nbk)) { release(); return rc; }
+    if (int rc = copy(tri_d, e->d_pdat, ndt)) { release(); return rc; }
+    if (int rc = copy(tri_w, e->d_pbm, nbm)) { release(); return rc; }
     HIPCHK(hipStreamSynchronize(e->stream));
     dfree(dtri);
-    dfree(e->d_pslot); dfree(e->d_pmap); dfree(e->d_tmid);
-    e->d_pslot = np;
+    dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_pmap); dfree(e->d_tmid);
+    e->d_pbkt = nbk;
+    e->d_pdat = ndt;
+    e->d_pbm = nbm;
+    e->d_ppre = npr;
     e->d_pmap = nh;
     e->d_tmid = nt;
     e->n_pslot = total;
@@ -1729,7 +1783,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         j4_max = std::min<uint32_t>(j4_max, 4096);
     }
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
-                          force_lane ? 1 : 0, e->d_blkcnt, gs));
+                          force_lane ? 1 : 0, e->d_blkcnt, (ext || !e->pq_on) ? 0u : 1u, e->d_bsmall + 0, e->pq_wide, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets
@@ -1803,7 +1857,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.rstate = e->d_rstate;
     S.hot = e->d_hot;
     S.pmap = e->d_pmap;
-    S.pslot = e->d_pslot;
+    S.pbkt = e->d_pbkt;
+    S.pdat = e->d_pdat;
+    S.pbm = e->d_pbm;
+    S.ppre = e->d_ppre;
     S.tmid = e->d_tmid;
     S.ring = e->d_ring;
     S.sink = e->d_sink;
@@ -1847,6 +1904,16 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                                  e->d_dec, e->d_bsmall + 0, bs));
         HIPCHK(hipEventRecord(e->join[c], bs));
     }
+    // hot-parameter owners (k_pq): the wide ones beside J16, the narrow ones beside J4
+    for (int c = 0; c < 2; ++c) {
+        const int b = c == 0 ? BIN_PQ16 : BIN_PQ4;
+        if (!bin_n[b]) continue;
+        hipStream_t bs = serial_bins ? st : e->bin_stream[c];
+        if (!serial_bins && !bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
+        HIPCHK(launch_pq(c == 0, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], S, dc, t0, e->d_dec,
+                         e->d_bsmall + 0, bs));
+        HIPCHK(hipEventRecord(e->join[c], bs));
+    }
     {
         DevState Sl = S;
         Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..36]
@@ -1868,7 +1935,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                                  t0, e->d_dec, e->d_bsmall + 0, st));
     }
     for (int c = 0; c < 2; ++c)
-        if (bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
+        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4]) HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));

@@ -118,6 +118,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             if (e.flags & SG_F_BLOCKED_UPSTREAM) mark |= PM_LANE;
         } else {
             if (e.kind == SG_EV_EXIT) {
+                if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
                 const int64_t raw = (int64_t)(e.aux >> 48);
                 r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
             }
@@ -436,9 +437,9 @@ __global__ void k_set_flags(NodeInfo* __restrict__ info, const uint64_t* __restr
     if (u >> 63) info[res].flags |= f;
     else info[res].flags &= ~f;
 }
-// the ParameterMetric map regions that survive a rule reload, moved into the new slot pool: one workgroup per
-// region, tri[3 * i] = {source base, destination base, slots}
-__global__ void k_region_copy(const PSlot* __restrict__ src, PSlot* __restrict__ dst, const uint64_t* __restrict__ tri) {
+// the ParameterMetric map regions that survive a rule reload, moved into the new pools: one workgroup per
+// region, tri[3 * i] = {source word, destination word, words}
+__global__ void k_region_copy(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, const uint64_t* __restrict__ tri) {
     const uint64_t s = tri[3 * blockIdx.x], d = tri[3 * blockIdx.x + 1], n = tri[3 * blockIdx.x + 2];
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[d + i] = src[s + i];
 }
@@ -483,7 +484,7 @@ hipError_t launch_set_flags(NodeInfo* info, const uint64_t* upd, uint32_t n, hip
     return hipGetLastError();
 }
 
-hipError_t launch_region_copy(const PSlot* src, PSlot* dst, const uint64_t* tri, uint32_t n, hipStream_t st) {
+hipError_t launch_region_copy(const uint64_t* src, uint64_t* dst, const uint64_t* tri, uint32_t n, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_region_copy, dim3(n), dim3(256), 0, st, src, dst, tri);
     return hipGetLastError();

@@ -1,0 +1,776 @@
+// param.hip -- k_pq: the cooperative owner of a hot-parameter resource's segment.
+//
+// A resource whose rules are all QPS-grade ParamFlowRules (passDefaultLocalCheck / passThrottleLocalCheck with a
+// fixed paramIdx; no flow or degrade rules, engine.cpp PF_PQ) is decided by one workgroup per segment instead of
+// one lane.  The reference runs, per ENTRY (param/slots/HotParamSlotChainBuilder.java:38-51):
+//   ParamFlowSlot.checkFlow  -- every rule in order, each a CacheMap access of the rule's (time, token) map for
+//                               the argument value, first block wins (ParamFlowSlot.java:77-101,
+//                               ParamFlowChecker.java:121-248);
+//   StatisticSlot            -- pass / block counters, curThreadNum (StatisticSlot.java:54-133);
+//   ParamFlowStatisticEntryCallback.onPass -- the thread-count map's access for the value (ParameterMetric.java:126-149)
+// and per EXIT StatisticSlot.exit.  Nothing reads the node's windows (no flow / degrade rule), so the statistics
+// are a reduction per 500 ms bucket, and a value's param state depends only on the earlier checks of the same
+// (rule, value) -- SURVEY.md §8(a) P3 -- except through LRU residency: whether a value is still in its
+// capacity-bounded map depends on every value accessed since.
+//
+// Residency without a sequential walk: a map holds the `cap` most recently used keys, so an access to key v hits
+// iff v was live at the tile start with recency rank r (r live keys more recent) and fewer than cap distinct keys
+// were accessed in between:
+//     D = r + #{ first accesses j of the tile before this one : key_j was not live, or had rank > r } < cap,
+// and any repeat of a key inside the tile hits (a tile holds < cap accesses).  Ranks are popcounts over the map's
+// live-stamp ring (pmap.h), held in LDS for the whole segment.  So a tile of accesses is decided at once:
+//   sort the tile's accesses by (key, position) in LDS; group leaders probe the map (cuckoo buckets in HBM / L2);
+//   D from the leaders' ranks (an upper bound r + #earlier leaders settles nearly all); one lane per key group walks
+//   its accesses in order through the token bucket / throttle (only same-key state is involved); then the group's
+//   new stamp, values and ring bits are committed, the oldest untouched keys beyond cap evicted (their ring bits
+//   cleared) and new keys placed in free or dead slots.
+// The thread-count map of paramIdx 0 is updated the same way from the tile's passed ENTRYs (count + 1, or 1 for a
+// key that was not live).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "chain.h"
+#include "pmap.h"
+
+using namespace sg;
+
+#define PQ_MAXP 4          // param rules of a k_pq resource (engine.cpp PF_PQ)
+#define PQ_RBW 256         // ring words a map may have (2^14 bits: capacity <= 4080)
+#define PQ_EPL 2           // events per lane per tile
+#define PQ_NPEND 64        // keys waiting for a displacement walk per tile (more: BF_PTAB_FULL)
+#define PQ_CLW 128         // claim bitmap words (>= buckets * 8 / 64 for capacity <= 4080)
+#define RANK_REP (-1)      // not a first access of its key in the tile
+#define RANK_NEW 0x7FFFFFFF
+
+template <int NW>
+struct PqSh {
+    static constexpr uint32_t HW = NW * 64;
+    static constexpr uint32_t TE = HW * PQ_EPL;
+    Node node;
+    DRule rules[PQ_MAXP];
+    PMap hdr[PQ_MAXP + 1];          // rule maps, then the thread-count map of paramIdx 0
+    uint32_t mid[PQ_MAXP + 1];
+    uint64_t bm[PQ_MAXP + 1][PQ_RBW];
+    uint32_t wpre[PQ_RBW];          // live stamps before each ring word (stamp order from thr)
+    uint64_t claim[PQ_CLW];
+    uint64_t tkey[TE];              // tile event -> argument key
+    int32_t tdt[TE];                // tile event -> time - t0
+    uint32_t tcz[TE];               // tile event -> count | rt << 16
+    uint32_t tkx[TE];               // tile event -> kind | flags << 8 | code << 16 (kind 0xFF: past the segment)
+    uint32_t tx[TE];                // tile event -> SEv.x (EXIT / TRACE reference)
+    int32_t lrank[TE];              // tile event -> RANK_* or the leader's rank at the tile start
+    uint32_t tA[TE];                // tile event -> accesses of the map before it in the tile
+    uint32_t tver[TE];              // tile event -> walk verdict (by sorted position first)
+    uint32_t tdec[TE];              // tile event -> decision word (EXIT references inside the tile)
+    uint64_t skey[TE];
+    uint32_t sidx[TE];
+    uint32_t red[NW][8];
+    int64_t red64[NW][2];
+    uint32_t flags_or, npend;
+    uint64_t pend_key[PQ_NPEND];
+    int64_t pend_stamp[PQ_NPEND];
+    PData pend_dat[PQ_NPEND];
+};
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ uint64_t ld64(const void* p) {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t uni64_pq(int64_t v) {  // LDS-broadcast value as a provably uniform scalar
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t ld32(const void* p) {
+    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive block scan of one u32 per lane; *tot = block total (uniform)
+template <int NW>
+__device__ __forceinline__ uint32_t pq_scan(PqSh<NW>& sh, uint32_t v, uint32_t* tot) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    if (l == 63) sh.red[w][7] = x;
+    __syncthreads();
+    uint32_t pre = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint32_t c = sh.red[k][7];
+        if ((uint32_t)k < w) pre += c;
+        t += c;
+    }
+    __syncthreads();
+    *tot = t;
+    return pre + x - v;
+}
+
+// ring helpers on the LDS copy of map k
+__device__ __forceinline__ uint32_t ring_word(const PMap& m, int64_t s) {
+    return (uint32_t)(((uint64_t)s & (uint64_t)((1ull << m.rb_log2) - 1)) >> 6);
+}
+__device__ __forceinline__ bool ring_live(const PMap& m, const uint64_t* bm, int64_t s) {
+    if (s < m.thr || s >= m.clock) return false;
+    const uint64_t p = (uint64_t)s & (uint64_t)((1ull << m.rb_log2) - 1);
+    return ((bm[p >> 6] >> (p & 63)) & 1ull) != 0;
+}
+
+// Tighten thr to the lowest live stamp; renumber the live stamps densely (pm_compact, in parallel) when the ring
+// would otherwise wrap onto a live stamp within the next `k` stamps.
+template <int NW>
+__device__ void pq_reserve(PqSh<NW>& sh, int mk, const DevState& S, uint32_t k) {
+    PMap& m = sh.hdr[mk];
+    const int64_t RB = (int64_t)1 << m.rb_log2;
+    const uint32_t W = (uint32_t)(RB >> 6);
+    if (m.clock + (int64_t)k - m.thr <= RB - 64) return;  // uniform (LDS header)
+    __syncthreads();
+    if (threadIdx.x == 0) m.thr = pm_first_live(m, sh.bm[mk], m.thr);
+    __syncthreads();
+    if (m.clock + (int64_t)k - m.thr <= RB - 64) return;
+    // ranks of the live stamps in stamp order
+    const uint32_t w0 = ring_word(m, m.thr);
+    const uint32_t lw = threadIdx.x;
+    const uint32_t c = lw < W ? (uint32_t)__popcll(sh.bm[mk][(w0 + lw) & (W - 1)]) : 0u;
+    uint32_t tot;
+    const uint32_t pre = pq_scan<NW>(sh, c, &tot);
+    if (lw < W) sh.wpre[(w0 + lw) & (W - 1)] = pre;
+    __syncthreads();
+    const int64_t base = m.clock - (int64_t)m.live;
+    PBucket* B = S.pbkt + m.base;
+    const uint32_t nslot = m.nb * PM_BKT;
+    for (uint32_t i = threadIdx.x; i < nslot; i += PqSh<NW>::HW) {
+        const uint32_t b = i / PM_BKT, j = i % PM_BKT;
+        const uint64_t key = ld64(&B[b].key[j]);
+        const int64_t s = (int64_t)ld64(&B[b].stamp[j]);
+        if (key == PK_EMPTY) continue;
+        if (!ring_live(m, sh.bm[mk], s)) {  // a dead slot's stamp may fall in the renumbered range: retire it
+            B[b].stamp[j] = PM_DEAD;
+            continue;
+        }
+        const uint64_t p = (uint64_t)s & (uint64_t)(RB - 1);
+        const uint32_t rk = sh.wpre[p >> 6] + (uint32_t)__popcll(sh.bm[mk][p >> 6] & ((1ull << (p & 63)) - 1ull));
+        B[b].stamp[j] = base + (int64_t)rk;
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < W; w += PqSh<NW>::HW) sh.bm[mk][w] = 0;
+    __syncthreads();
+    for (int64_t s = base + threadIdx.x; s < m.clock; s += PqSh<NW>::HW) {
+        const uint64_t p = (uint64_t)s & (uint64_t)(RB - 1);
+        atomicOr(reinterpret_cast<unsigned long long*>(&sh.bm[mk][p >> 6]), 1ull << (p & 63));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) m.thr = base;
+    __syncthreads();
+}
+
+// bitonic sort of (skey, sidx) pairs [0, P) in LDS, P a power of two
+template <int NW>
+__device__ void pq_sort(PqSh<NW>& sh, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P / 2; i += PqSh<NW>::HW) {
+                const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                const bool up = (lo & k) == 0;
+                const uint64_t ka = sh.skey[lo], kb = sh.skey[hi];
+                const uint32_t ia = sh.sidx[lo], ib = sh.sidx[hi];
+                const bool gt = ka > kb || (ka == kb && ia > ib);
+                if (gt == up) {
+                    sh.skey[lo] = kb; sh.skey[hi] = ka;
+                    sh.sidx[lo] = ib; sh.sidx[hi] = ia;
+                }
+            }
+            lds_sync();
+        }
+    }
+}
+
+enum { PW_TOKEN = 0, PW_THROTTLE = 1, PW_COUNT = 2 };
+
+// One map's accesses of the tile (acc[e] for the lane's events e = tid * PQ_EPL + q): residency, the walk of
+// every key group (WALK), commit.  Verdicts of rule walks land in sh.tver[e]: 0 pass | wait << 16, 1 block.
+template <int NW>
+__device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const DRule* r, const DevState& S, int64_t t0,
+                             const bool (&acc)[PQ_EPL], uint32_t* bflags) {
+    constexpr uint32_t HW = PqSh<NW>::HW;
+    constexpr uint32_t SP = PqSh<NW>::TE / HW;  // sorted positions per lane
+    const uint32_t tid = threadIdx.x;
+    // (a) accesses before each event, in tile order
+    uint32_t la = 0;
+#pragma unroll
+    for (int q = 0; q < PQ_EPL; ++q) la += acc[q] ? 1u : 0u;
+    uint32_t na;
+    uint32_t a0 = pq_scan<NW>(sh, la, &na);
+    if (na == 0) return;  // uniform
+#pragma unroll
+    for (int q = 0; q < PQ_EPL; ++q) {
+        const uint32_t e = tid * PQ_EPL + q;
+        sh.tA[e] = a0;
+        sh.lrank[e] = RANK_REP;
+        if (acc[q]) { sh.skey[a0] = sh.tkey[e]; sh.sidx[a0] = e; ++a0; }
+    }
+    uint32_t P = 64;
+    while (P < na) P <<= 1;
+    for (uint32_t i = na + tid; i < P; i += HW) { sh.skey[i] = PK_EMPTY; sh.sidx[i] = 0xFFFFFFFFu; }
+    pq_reserve<NW>(sh, mk, S, na);
+    __syncthreads();
+    pq_sort<NW>(sh, P);
+    PMap& m = sh.hdr[mk];
+    const int64_t RB = (int64_t)1 << m.rb_log2;
+    const uint32_t W = (uint32_t)(RB >> 6);
+    const int64_t clock0 = m.clock;
+    const uint32_t live0 = m.live, cap = m.cap;
+    {   // ranks: live stamps before each ring word, in stamp order from thr
+        const uint32_t w0 = ring_word(m, m.thr);
+        const uint32_t c = tid < W ? (uint32_t)__popcll(sh.bm[mk][(w0 + tid) & (W - 1)]) : 0u;
+        uint32_t tot;
+        const uint32_t pre = pq_scan<NW>(sh, c, &tot);
+        if (tid < W) sh.wpre[(w0 + tid) & (W - 1)] = pre;
+    }
+    __syncthreads();
+    // (b) group leaders probe the map; their ranks by tile event
+    PBucket* B = S.pbkt + m.base;
+    PData* D = S.pdat + m.base * PM_BKT;
+    int32_t gslot[SP];
+    bool glive[SP], glead[SP];
+    int64_t gst[SP];
+    PData gd[SP];
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        const uint32_t s = tid + q * HW;
+        glead[q] = false; glive[q] = false; gslot[q] = -1; gst[q] = 0;
+        gd[q].v0 = 0; gd[q].v1 = 0; gd[q].pad = 0;
+        if (s >= na) continue;
+        const uint64_t key = sh.skey[s];
+        if (s > 0 && sh.skey[s - 1] == key) continue;
+        glead[q] = true;
+        uint32_t b1, b2;
+        pm_buckets(m.nb, key, b1, b2);
+        for (int j = 0; j < PM_BKT && gslot[q] < 0; ++j)
+            if (ld64(&B[b1].key[j]) == key) gslot[q] = (int32_t)(b1 * PM_BKT + j);
+        for (int j = 0; j < PM_BKT && gslot[q] < 0; ++j)
+            if (ld64(&B[b2].key[j]) == key) gslot[q] = (int32_t)(b2 * PM_BKT + j);
+        int32_t rank = RANK_NEW;
+        if (gslot[q] >= 0) {
+            gst[q] = (int64_t)ld64(&B[gslot[q] / PM_BKT].stamp[gslot[q] % PM_BKT]);
+            glive[q] = ring_live(m, sh.bm[mk], gst[q]);
+            if (glive[q]) {
+                const uint64_t p = (uint64_t)gst[q] & (uint64_t)(RB - 1);
+                const uint32_t below = sh.wpre[p >> 6] + (uint32_t)__popcll(sh.bm[mk][p >> 6] & ((1ull << (p & 63)) - 1ull));
+                rank = (int32_t)(live0 - below - 1);
+                const uint64_t* dp = reinterpret_cast<const uint64_t*>(&D[gslot[q]]);
+                gd[q].v0 = (int64_t)ld64(dp);
+                gd[q].v1 = (int32_t)(uint32_t)ld64(dp + 1);
+            }
+        }
+        sh.lrank[sh.sidx[s]] = rank;
+    }
+    __syncthreads();
+    // (c) residency of every first access: the upper bound r + (first accesses before it) settles it unless the key
+    // is near the LRU end; then the exact count of the earlier first accesses of keys older than it
+    {
+        uint32_t lf = 0;
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) lf += sh.lrank[tid * PQ_EPL + q] != RANK_REP ? 1u : 0u;
+        uint32_t nf;
+        uint32_t F = pq_scan<NW>(sh, lf, &nf);
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q;
+            const int32_t rk = sh.lrank[e];
+            if (rk == RANK_REP) continue;
+            uint32_t hit = 0;
+            if (rk != RANK_NEW) {
+                if ((uint32_t)rk + F < cap) hit = 1;
+                else {
+                    uint32_t d = (uint32_t)rk;
+                    for (uint32_t j = 0; j < e && d < cap; ++j) {
+                        const int32_t x = sh.lrank[j];
+                        if (x != RANK_REP && x > rk) ++d;
+                    }
+                    hit = d < cap ? 1u : 0u;
+                }
+            }
+            sh.tver[e] = hit;  // leader residency, read by the group's walker
+            ++F;
+        }
+    }
+    __syncthreads();
+    // (d) walks: one lane per key group, its accesses in tile order
+    uint32_t gend[SP];
+    PData gfin[SP];
+    bool ghit[SP];
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        const uint32_t s = tid + q * HW;
+        gend[q] = s;
+        gfin[q] = gd[q];
+        ghit[q] = false;
+        if (!glead[q]) continue;
+        const uint32_t e0 = sh.sidx[s];
+        ghit[q] = sh.tver[e0] != 0;
+        const uint64_t key = sh.skey[s];
+        uint32_t send = s + 1;
+        while (send < na && sh.skey[send] == key) ++send;
+        gend[q] = send;
+        PData st = gd[q];
+        int64_t tcl = 0;
+        int32_t maxc = 0;
+        if (walk != PW_COUNT) {  // the value's token count: its hot item, else (int) / (long) count
+            bool hf = false;
+            int32_t hc = 0;
+            for (uint32_t i = 0; i < r->hot_n; ++i) {
+                const DHot h = S.hot[r->hot_off + i];
+                if (h.key == key) { hf = true; hc = h.count; break; }
+            }
+            tcl = hf ? (int64_t)hc : (walk == PW_THROTTLE ? r->token_count_l : (int64_t)r->token_count);
+            maxc = j_iadd((int32_t)tcl, r->burst);
+        }
+        const int64_t dur_ms = r ? r->duration_sec * 1000 : 0;
+        bool first_miss = !ghit[q];
+        for (uint32_t p = s; p < send; ++p) {
+            const uint32_t e = sh.sidx[p];
+            const int64_t t = t0 + sh.tdt[e];
+            const int acq = (int)(sh.tcz[e] & 0xFFFFu);
+            uint32_t v = 0;
+            if (walk == PW_COUNT) {
+                st.v0 = first_miss ? 1 : st.v0 + 1;
+            } else if (walk == PW_THROTTLE) {  // passThrottleLocalCheck (ParamFlowChecker.java:198-248)
+                if (first_miss) {
+                    st.v0 = t;
+                } else {
+                    const int64_t cost = j_round(1.0 * 1000 * acq * (double)r->duration_sec / (double)tcl);
+                    const int64_t expected = st.v0 + cost;
+                    if (expected <= t || expected - t < r->max_queue) {
+                        const int64_t w = expected - t;
+                        st.v0 = w > 0 ? expected : t;
+                        if (w > 0) v = (uint32_t)(w > 0xFFFF ? 0xFFFF : w) << 16;
+                    } else {
+                        v = 1;
+                    }
+                }
+            } else {  // passDefaultLocalCheck (ParamFlowChecker.java:121-196)
+                if (first_miss) {
+                    st.v0 = t;
+                    st.v1 = j_iadd(maxc, -acq);
+                } else {
+                    const int64_t pass_time = t - st.v0;
+                    if (pass_time > dur_ms) {
+                        const int32_t to_add = (int32_t)((pass_time * tcl) / dur_ms);
+                        const int32_t sum = j_iadd(st.v1, to_add);
+                        const int32_t nq = sum > maxc ? j_iadd(maxc, -acq) : j_iadd(sum, -acq);
+                        if (nq < 0) v = 1;
+                        else { st.v1 = nq; st.v0 = t; }
+                    } else if (j_iadd(st.v1, -acq) >= 0) {
+                        st.v1 = j_iadd(st.v1, -acq);
+                    } else {
+                        v = 1;
+                    }
+                }
+            }
+            first_miss = false;
+            sh.tver[e] = v;
+        }
+        gfin[q] = st;
+    }
+    __syncthreads();
+    // (e) commit: touched keys leave their old stamp; the oldest untouched keys beyond cap are evicted
+    uint32_t nnew = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        if (!glead[q]) continue;
+        if (glive[q]) {
+            const uint64_t p = (uint64_t)gst[q] & (uint64_t)(RB - 1);
+            atomicAnd(reinterpret_cast<unsigned long long*>(&sh.bm[mk][p >> 6]), ~(1ull << (p & 63)));
+        } else {
+            ++nnew;
+        }
+    }
+    uint32_t ntot;
+    (void)pq_scan<NW>(sh, nnew, &ntot);  // (barrier: the cleared bits are in place)
+    const uint32_t E = live0 + ntot > cap ? live0 + ntot - cap : 0u;
+    if (E) {
+        const uint32_t w0 = ring_word(m, m.thr);
+        const uint32_t w = (w0 + tid) & (W - 1);
+        const uint64_t word = tid < W ? sh.bm[mk][w] : 0ull;
+        uint32_t tot;
+        const uint32_t before = pq_scan<NW>(sh, (uint32_t)__popcll(word), &tot);
+        if (tid < W && before < E && word) {
+            uint64_t x = word;
+            uint32_t k = E - before;
+            while (x && k) { x &= x - 1; --k; }  // clear the lowest E - before set bits
+            sh.bm[mk][w] = x;
+        }
+    }
+    for (uint32_t i = tid; i < PQ_CLW; i += HW) sh.claim[i] = 0;
+    __syncthreads();
+    // new stamps: the group's last access; keys with a slot (live or dead) keep it
+    bool need[SP];
+    int64_t gns[SP];
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        need[q] = false;
+        gns[q] = 0;
+        if (!glead[q]) continue;
+        gns[q] = clock0 + (int64_t)sh.tA[sh.sidx[gend[q] - 1]];
+        const uint64_t p = (uint64_t)gns[q] & (uint64_t)(RB - 1);
+        atomicOr(reinterpret_cast<unsigned long long*>(&sh.bm[mk][p >> 6]), 1ull << (p & 63));
+        if (gslot[q] >= 0) {
+            B[gslot[q] / PM_BKT].stamp[gslot[q] % PM_BKT] = gns[q];
+            D[gslot[q]] = gfin[q];
+            const uint32_t i = (uint32_t)gslot[q];
+            atomicOr(reinterpret_cast<unsigned long long*>(&sh.claim[i >> 6]), 1ull << (i & 63));
+        } else {
+            need[q] = true;
+        }
+    }
+    if (tid == 0) {
+        m.clock = clock0 + (int64_t)na;
+        m.live = live0 + ntot - E;
+        sh.npend = 0;
+    }
+    __syncthreads();
+    // keys without a slot: a free slot (never used, or dead by the ring) of the less loaded bucket, claimed in LDS
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        if (!need[q]) continue;
+        const uint64_t key = sh.skey[tid + q * HW];
+        uint32_t b1, b2;
+        pm_buckets(m.nb, key, b1, b2);
+        bool placed = false;
+        for (int attempt = 0; attempt < 4 && !placed; ++attempt) {
+            int f1 = -1, f2 = -1, n1 = 0, n2 = 0;
+            for (int j = 0; j < PM_BKT; ++j) {
+                const uint32_t i1 = b1 * PM_BKT + j, i2 = b2 * PM_BKT + j;
+                const bool c1 = (sh.claim[i1 >> 6] >> (i1 & 63)) & 1ull, c2 = (sh.claim[i2 >> 6] >> (i2 & 63)) & 1ull;
+                const bool fr1 = !c1 && (ld64(&B[b1].key[j]) == PK_EMPTY || !ring_live(m, sh.bm[mk], (int64_t)ld64(&B[b1].stamp[j])));
+                const bool fr2 = !c2 && (ld64(&B[b2].key[j]) == PK_EMPTY || !ring_live(m, sh.bm[mk], (int64_t)ld64(&B[b2].stamp[j])));
+                if (fr1) { if (f1 < 0) f1 = j; } else ++n1;
+                if (fr2) { if (f2 < 0) f2 = j; } else ++n2;
+            }
+            const bool u1 = f1 >= 0 && (f2 < 0 || n1 <= n2);
+            if (!u1 && f2 < 0) break;
+            const uint32_t i = u1 ? b1 * PM_BKT + (uint32_t)f1 : b2 * PM_BKT + (uint32_t)f2;
+            const unsigned long long old =
+                atomicOr(reinterpret_cast<unsigned long long*>(&sh.claim[i >> 6]), 1ull << (i & 63));
+            if ((old >> (i & 63)) & 1ull) continue;  // another lane took it first
+            B[i / PM_BKT].key[i % PM_BKT] = key;
+            B[i / PM_BKT].stamp[i % PM_BKT] = gns[q];
+            D[i] = gfin[q];
+            placed = true;
+        }
+        if (!placed) {
+            const uint32_t k = atomicAdd(&sh.npend, 1u);
+            if (k < PQ_NPEND) { sh.pend_key[k] = key; sh.pend_stamp[k] = gns[q]; sh.pend_dat[k] = gfin[q]; }
+            else atomicOr(bflags, BF_PTAB_FULL);
+        }
+    }
+    __syncthreads();
+    if (tid == 0 && sh.npend) {  // displacement walks (pmap.h pm_insert_new), one lane
+        const uint32_t np = sh.npend < PQ_NPEND ? sh.npend : PQ_NPEND;
+        for (uint32_t k = 0; k < np; ++k) {
+            uint64_t ck = sh.pend_key[k];
+            int64_t cs = sh.pend_stamp[k];
+            PData cd = sh.pend_dat[k];
+            uint32_t b1, b2;
+            pm_buckets(m.nb, ck, b1, b2);
+            uint32_t b = b1;
+            bool done = false;
+            for (int step = 0; step < 256 && !done; ++step) {
+                for (int j = 0; j < PM_BKT; ++j) {
+                    const uint64_t kk = ld64(&B[b].key[j]);
+                    if (kk == PK_EMPTY || !ring_live(m, sh.bm[mk], (int64_t)ld64(&B[b].stamp[j]))) {
+                        B[b].key[j] = ck; B[b].stamp[j] = cs; D[b * PM_BKT + j] = cd;
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                const int j = (int)((cs + step * 5) & 7);
+                const uint64_t nk = ld64(&B[b].key[j]);
+                const int64_t ns = (int64_t)ld64(&B[b].stamp[j]);
+                const PData nd = D[b * PM_BKT + j];
+                B[b].key[j] = ck; B[b].stamp[j] = cs; D[b * PM_BKT + j] = cd;
+                ck = nk; cs = ns; cd = nd;
+                b = pm_alt(m.nb, ck, b);
+            }
+            if (!done) atomicOr(bflags, BF_PTAB_FULL);
+        }
+        __threadfence_block();
+    }
+    __syncthreads();
+}
+
+// StatisticSlot on the ClusterNode for one tile (StatisticSlot.java:54-173, ClusterNode.trace): the events of
+// one 500 ms bucket are one bucket update (nothing reads the windows in between); an EXIT / TRACE counts iff its
+// ENTRY passed (CtSph exits a blocked entry internally: no statistics)
+template <int NW>
+__device__ __noinline__ void pq_fold(PqSh<NW>& sh, const Ctx& C, int64_t t0, uint32_t tb, uint32_t start, uint32_t len,
+                                     const uint32_t* dec, uint32_t* bflags) {
+    constexpr uint32_t TE = PqSh<NW>::TE;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ne = len - tb < TE ? len - tb : TE;
+    int64_t bcur = (t0 + sh.tdt[0]) / 500;
+    const int64_t blast = (t0 + sh.tdt[ne - 1]) / 500;
+    // effectiveness of this lane's EXIT / TRACEs (bit q)
+    uint32_t effm = 0;
+#pragma unroll
+    for (int q = 0; q < PQ_EPL; ++q) {
+        const uint32_t e = tid * PQ_EPL + q, p = tb + e;
+        if (p >= len) continue;
+        const uint32_t kx = sh.tkx[e], kind = kx & 0xFFu, code = (kx >> 16) & 0xFFu;
+        if (kind == SG_EV_ENTRY) continue;
+        bool eff;
+        if (code == RC_NONE || code == RC_PASSED) eff = true;  // the chain exists (k_pq runs only then)
+        else if (code == RC_NOT) eff = false;
+        else {
+            const uint32_t rel = sh.tx[e] - start;
+            if (rel >= p) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+            else if (rel >= tb) eff = st_passed(sh.tdec[rel - tb] & 0xFF);
+            else eff = st_passed(ld32(&dec[sh.tx[e]]) & 0xFF);
+        }
+        if (eff) effm |= 1u << q;
+    }
+    for (;;) {
+        uint32_t a[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};  // pass block succ rt exc minrt thread touched
+        int64_t nxt = INT64_MAX;
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q;
+            if (tb + e >= len) continue;
+            const int64_t bk = (t0 + sh.tdt[e]) / 500;
+            if (bk != bcur) {
+                if (bk > bcur && bk < nxt) nxt = bk;
+                continue;
+            }
+            const uint32_t kx = sh.tkx[e], kind = kx & 0xFFu, cz = sh.tcz[e], cnt = cz & 0xFFFFu, rt = cz >> 16;
+            if (kind == SG_EV_ENTRY) {
+                a[7] += 1;
+                if (st_passed(sh.tdec[e] & 0xFF)) { a[0] += cnt; a[6] += 1; }
+                else a[1] += cnt;
+            } else if ((effm >> q) & 1) {
+                if (kind == SG_EV_EXIT) {
+                    a[7] += 1;
+                    a[2] += cnt; a[3] += rt; a[5] = rt < a[5] ? rt : a[5]; a[6] -= 1;
+                } else if (cnt > 0) {
+                    a[7] += 1;
+                    a[4] += cnt;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t y = (uint32_t)__shfl_xor((int)a[k], o, 64);
+                a[k] = k == 5 ? (y < a[k] ? y : a[k]) : a[k] + y;
+            }
+            const int64_t yn = __shfl_xor(nxt, o, 64);
+            nxt = yn < nxt ? yn : nxt;
+        }
+        const uint32_t w = tid >> 6;
+        if ((tid & 63) == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sh.red[w][k] = a[k];
+            sh.red64[w][0] = nxt;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t s[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};
+            int64_t nx = INT64_MAX;
+            for (int ww = 0; ww < NW; ++ww) {
+                for (int k = 0; k < 8; ++k) s[k] = k == 5 ? (sh.red[ww][k] < s[k] ? sh.red[ww][k] : s[k]) : s[k] + sh.red[ww][k];
+                nx = sh.red64[ww][0] < nx ? sh.red64[ww][0] : nx;
+            }
+            if (s[7]) {  // the bucket's first touching event resets a stale bucket (LeapArray.currentWindow)
+                Node& N = sh.node;
+                const int64_t tc = bcur * 500;
+                const int64_t mrt = s[5] == 0xFFFFFFFFu ? INT64_MAX : (int64_t)s[5];
+                const int sl = sec_current(N, tc, C.max_rt);
+                sec_add(N, sl, s[0], s[1], s[2], s[3], s[4], mrt);
+                min_current(N, C.minb, tc, C.max_rt, C.pflags);
+                min_add(N, s[0], s[1], s[2], s[3], s[4], mrt);
+                N.thread += (int32_t)s[6];
+            }
+            sh.red64[0][1] = nx;
+        }
+        __syncthreads();
+        const int64_t nn = uni64_pq(sh.red64[0][1]);
+        if (nn == INT64_MAX || nn > blast) break;
+        bcur = nn;
+        __syncthreads();
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                                const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                                const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                                int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    constexpr uint32_t HW = PqSh<NW>::HW, TE = PqSh<NW>::TE;
+    __shared__ PqSh<NW> sh;
+    if (blockIdx.x >= m) return;
+    const uint32_t tid = threadIdx.x;
+    const Seg sg = segs[order[blockIdx.x]];
+    const uint32_t res = sg.res;
+    const Prog pg = S.prog[res];
+    const int np = pg.n_param;
+    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    if (tid == 0) {
+        node_load(sh.node, S, res);
+        sh.flags_or = 0;
+    }
+    if ((int)tid < np) sh.rules[tid] = S.rules[pg.rule_off + tid];
+    __syncthreads();
+    // the maps: rule maps (QPS rules), then the thread-count map of paramIdx 0
+    const uint32_t tm = (pg.tm_base == NO_ID) ? NO_ID : S.tmid[pg.tm_base];
+    if (tid <= PQ_MAXP) {
+        uint32_t id = NO_ID;
+        if ((int)tid < np && sh.rules[tid].behavior != PB_INIT_ONLY) id = sh.rules[tid].pmap;
+        if (tid == PQ_MAXP) id = tm;
+        sh.mid[tid] = id;
+        if (id != NO_ID) sh.hdr[tid] = S.pmap[id];
+    }
+    __syncthreads();
+    for (int k = 0; k <= PQ_MAXP; ++k) {
+        if (sh.mid[k] == NO_ID) continue;
+        const uint32_t W = 1u << (sh.hdr[k].rb_log2 - 6);
+        for (uint32_t w = tid; w < W; w += HW) sh.bm[k][w] = S.pbm[sh.hdr[k].bm + w];
+    }
+    const bool chain = (sh.node.flags & NI_CHAIN) != 0;  // the host routes switch_on == 0 to k_lane
+    if (!chain) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted, no map is touched
+        for (uint32_t p = tid; p < sg.len; p += HW)
+            if (recs[sg.start + p].kind == SG_EV_ENTRY) dec[sg.start + p] = mk_dec(ST_NO_CHECK, 0, 0);
+        return;
+    }
+    if (tid == 0 && sg.len && (t0 + recs[sg.start].dt) < (sh.node.sb[0].ws > sh.node.sb[1].ws ? sh.node.sb[0].ws : sh.node.sb[1].ws))
+        atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
+    // tm bit of paramIdx 0 for a passed ENTRY: it has visited every rule (ParamFlowSlot sets the bits of the
+    // rules it checks: ni_tm(paramIdx), or an initialise-only run's map set)
+    uint32_t all_bits = NI_PM;
+    for (int k = 0; k < np; ++k) {
+        const DRule& r = sh.rules[k];
+        if (r.behavior == PB_INIT_ONLY) all_bits |= (uint32_t)r.burst << NI_TM_SHIFT;
+        else if (r.param_idx < SG_MAX_ARGS) all_bits |= ni_tm((uint32_t)r.param_idx);
+    }
+    const bool tm_on = tm != NO_ID && ((sh.node.flags | all_bits) & ni_tm(0)) != 0;
+    __syncthreads();
+
+    for (uint32_t tb = 0; tb < sg.len; tb += TE) {
+        // ---- 1. the tile's events
+        uint32_t st[PQ_EPL], wt[PQ_EPL];  // st: 0 pending / passed, else the blocking rule + 1
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q, p = tb + e;
+            SEv r;
+            r.kind = 0xFF; r.flags = 0; r.code = 0; r.dt = 0; r.cnt = 0; r.rt = 0; r.x = 0;
+            if (p < sg.len) r = recs[sg.start + p];
+            st[q] = 0;
+            wt[q] = 0;
+            sh.tdt[e] = r.dt;
+            sh.tcz[e] = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
+            sh.tkx[e] = (uint32_t)r.kind | ((uint32_t)r.flags << 8) | ((uint32_t)r.code << 16);
+            sh.tx[e] = r.x;
+            if (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG)) sh.tkey[e] = ev[vals[sg.start + p] & 0x7FFFFFFFu].aux;
+        }
+        __syncthreads();
+        // ---- 2. ParamFlowSlot: the rules in order
+        for (int k = 0; k < np; ++k) {
+            const DRule& r = sh.rules[k];
+            bool reach = false;
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) reach |= (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY && st[q] == 0;
+            if (reach) {
+                const uint32_t bits = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
+                                      : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
+                atomicOr(&sh.flags_or, bits | NI_PM);
+            }
+            if (r.behavior == PB_INIT_ONLY || r.param_idx != 0) continue;  // no check (idx >= args.length)
+            const int walk = r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ? PW_THROTTLE : PW_TOKEN;
+            bool acc[PQ_EPL];
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t e = tid * PQ_EPL + q, kx = sh.tkx[e];
+                acc[q] = false;
+                if (!((kx & 0xFFu) == SG_EV_ENTRY && ((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0)) continue;
+                const uint64_t key = sh.tkey[e];
+                const int acq = (int)(sh.tcz[e] & 0xFFFFu);
+                bool hf = false;
+                int32_t hc = 0;
+                for (uint32_t i = 0; i < r.hot_n; ++i) {
+                    const DHot h = S.hot[r.hot_off + i];
+                    if (h.key == key) { hf = true; hc = h.count; break; }
+                }
+                // checks before any map access: a zero token count, an acquire above maxCount
+                if (walk == PW_THROTTLE) {
+                    if ((hf ? (int64_t)hc : r.token_count_l) == 0) { st[q] = (uint32_t)k + 1; continue; }
+                } else {
+                    const int32_t tc = hf ? hc : r.token_count;
+                    if (tc == 0 || acq > j_iadd(tc, r.burst)) { st[q] = (uint32_t)k + 1; continue; }
+                }
+                acc[q] = true;
+            }
+            pq_map_phase<NW>(sh, k, walk, &r, S, t0, acc, bflags);
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                if (!acc[q]) continue;
+                const uint32_t v = sh.tver[tid * PQ_EPL + q];
+                if (v & 1) st[q] = (uint32_t)k + 1;
+                else wt[q] += v >> 16;
+            }
+            __syncthreads();  // tver is rewritten by the next phase
+        }
+        // ---- 3. ParamFlowStatisticEntryCallback.onPass: the thread-count map of paramIdx 0
+        if (tm_on) {
+            bool acc[PQ_EPL];
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t kx = sh.tkx[tid * PQ_EPL + q];
+                acc[q] = (kx & 0xFFu) == SG_EV_ENTRY && ((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0;
+            }
+            pq_map_phase<NW>(sh, PQ_MAXP, PW_COUNT, nullptr, S, t0, acc, bflags);
+        }
+        // ---- 4. decisions
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q, p = tb + e;
+            uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+            if ((sh.tkx[e] & 0xFFu) == SG_EV_ENTRY) {
+                d = st[q] == 0 ? mk_dec(ST_PASS, 0, wt[q]) : mk_dec(ST_BLOCK_PARAM, sh.rules[st[q] - 1].slot, 0);
+                if (p < sg.len) dec[sg.start + p] = d;
+            }
+            sh.tdec[e] = d;
+        }
+        __syncthreads();
+        // ---- 5. StatisticSlot: one bucket update per 500 ms bucket of the tile
+        pq_fold<NW>(sh, C, t0, tb, sg.start, sg.len, dec, bflags);
+        __syncthreads();  // full fence: this tile's dec[] words are visible to the next tiles' EXIT lookups
+    }
+    // ---- segment end: node, map headers and rings back to HBM
+    if (tid == 0) {
+        Node& N = sh.node;
+        N.flags |= sh.flags_or;
+        min_flush(N, C.minb);
+        node_store(N, S, res, pg.pflags);
+    }
+    for (int k = 0; k <= PQ_MAXP; ++k) {
+        if (sh.mid[k] == NO_ID) continue;
+        const uint32_t W = 1u << (sh.hdr[k].rb_log2 - 6);
+        for (uint32_t w = tid; w < W; w += HW) S.pbm[sh.hdr[k].bm + w] = sh.bm[k][w];
+        if (tid == 0) pm_store(S, sh.mid[k], sh.hdr[k]);
+    }
+}
+
+namespace sg {
+hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                     const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
+                     uint32_t* bflags, hipStream_t st) {
+    if (!m) return hipSuccess;
+    if (wide) hipLaunchKernelGGL(k_pq<16>, dim3(m), dim3(1024), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    else hipLaunchKernelGGL(k_pq<4>, dim3(m), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    return hipGetLastError();
+}
+} // namespace sg

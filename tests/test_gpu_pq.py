@@ -1,0 +1,133 @@
+"""The cooperative hot-parameter owner (sentinel_amd/csrc/param.hip k_pq) against the oracle.
+
+k_pq decides the segments of resources whose rules are QPS-grade ParamFlowRules (PF_PQ) a tile at a time: LRU
+residency of the CacheMaps from recency ranks, one lane per value group through the token bucket / throttle,
+statistics per 500 ms bucket.  These tests replay traces in which every such segment goes through it (batches
+without sg_submit_ex context and without exit(count, args)) and compare every decision and the ClusterNode
+windows with the event-sequential oracle (ParamFlowChecker.java:121-248, ParameterMetric.java:37-241,
+StatisticSlot.java:54-173).
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from sentinel_amd import _abi as A
+from sentinel_amd import engine as E
+from sentinel_amd import tracegen as T
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+def _check(w, eng, orc, cuts, k_nodes=200):
+    ev = w.events
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        dg, do = eng.submit(ev[a:b]), orc.submit(ev[a:b])
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), ("event", int(a + bad[0]), ev[a + bad[0]], hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+    cnt = np.bincount(ev["res_id"], minlength=w.n_res)
+    hot = np.argsort(-cnt)[:40]
+    rnd = np.random.default_rng(1).choice(np.nonzero(cnt)[0], size=min(k_nodes, int((cnt > 0).sum())), replace=False)
+    for r in np.unique(np.concatenate([hot, rnd])):
+        g, o = eng.read_node(int(r)), orc.read_node(int(r))
+        assert g["thread"] == o["thread"], r
+        np.testing.assert_array_equal(g["second"][:2], o["second"][:2], err_msg="second window of res %d" % r)
+        np.testing.assert_array_equal(g["minute"], o["minute"], err_msg="minute window of res %d" % r)
+
+
+def test_pq_c5_survey_shape():
+    # 10k resources, one param rule each (count 5-50, burst 0-5, 1 s, 20 % throttle with
+    # maxQueue 100), values Zipf(1.1) over 10M keys; two batches of 2^23 events.  Every hot map fills and evicts.
+    w = T.Workload(5, n_res=10_000, n_entries=1 << 23, n_param_values=10_000_000)
+    ev = w.events
+    eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=28, status_ring_log2=26,
+                   max_batch_events=1 << 23)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    _check(w, eng, orc, [0, 1 << 23, len(ev)])
+
+
+@pytest.mark.parametrize("wide", ["0", "1073741824"])
+@pytest.mark.parametrize("variant", ["hot", "uniform"])
+def test_pq_variants(variant, wide, monkeypatch):
+    # hot items (per-value token counts, some 0: blocked without a map access) and uniform churn (a million
+    # distinct values); every segment on the 1024-lane owner (wide=0) or on the 256-lane one
+    monkeypatch.setenv("SG_PQ_WIDE", wide)
+    v = T.V_HOT if variant == "hot" else T.V_HOT | T.V_UNIFORM
+    w = T.Workload(5, n_res=2_000, n_entries=600_000, n_param_values=2_000_000, variant=v)
+    eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=26, status_ring_log2=24)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    _check(w, eng, orc, np.linspace(0, len(w.events), 4).astype(np.int64))
+
+
+def _rules():
+    return [
+        # two checked rules on index 0 (token bucket with burst, then a throttle), hot items incl. a zero count
+        A.param_rule("m0", 0, 3, burst_count=2, items=[("7", "long", 0), ("8", "long", 50)]),
+        A.param_rule("m0", 0, 20, control_behavior=A.CONTROL_BEHAVIOR_RATE_LIMITER, max_queueing_time_ms=40),
+        # a rule on index 1 (an argument the events never carry: no check, its thread map exists)
+        A.param_rule("m0", 1, 1),
+        # cluster mode without fallback: initialised, never checked
+        A.param_rule("m1", 0, 1, cluster_mode=True, cluster_flow_id=77),
+        A.param_rule("m1", 0, 2),
+        A.param_rule("m2", 0, 1, burst_count=1),
+    ]
+
+
+def _synthetic(seed, n, gbase, nres=3, nval=9000, t=T0):
+    # EXIT references name the ENTRY's global event index (batches are numbered consecutively)
+    rng = np.random.default_rng(seed)
+    ev = np.zeros(2 * n, dtype=A.EVENT_DTYPE)
+    ts = t + np.sort(rng.integers(0, 6000, n))
+    k = 0
+    pend = []
+    for i in range(n):
+        while pend and pend[0][0] <= ts[i]:
+            tx, ref, rid = pend.pop(0)
+            ev[k] = (tx, rid, 1, A.EV_EXIT, 0, A.aux_exit(ref, 3))
+            k += 1
+        rid = int(rng.integers(0, nres))
+        v = int(rng.zipf(1.3)) if rng.random() < 0.6 else int(rng.integers(0, nval))
+        flags = A.F_HAS_ARG if rng.random() < 0.97 else 0
+        cnt = int(rng.choice([1, 1, 1, 2, 0, 6]))
+        ev[k] = (ts[i], rid, cnt, A.EV_ENTRY, flags, E.param_key(str(v), "long"))
+        if rng.random() < 0.5:
+            pend.append((int(ts[i]) + int(rng.integers(0, 30)), gbase + k, rid))
+            pend.sort()
+        k += 1
+    for tx, ref, rid in pend:
+        ev[k] = (tx, rid, 1, A.EV_EXIT, 0, A.aux_exit(ref, 3))
+        k += 1
+    return ev[:k]
+
+
+def test_pq_rule_mix_and_alternating_paths():
+    # several param rules per resource, hot items, entries without an argument, zero and oversized acquires,
+    # > 4000 distinct values per resource (evictions inside and across tiles); batches alternate between k_pq and
+    # the per-lane kernel (an exit(count, args) sends a whole batch to k_lane): both work on the same maps
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=20, status_ring_log2=24)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for nm in ("m0", "m1", "m2"):
+        assert eng.register(nm) == orc.register(nm)
+    rules = _rules()
+    assert eng.load_param_rules(rules) == orc.load_param_rules(rules)
+    t, gbase = T0, 0
+    for b in range(6):
+        ev = _synthetic(100 + b, 30_000, gbase, t=t)
+        gbase += len(ev)
+        if b % 2 == 1:  # one EXIT carries exit(count, args): this batch is the lane kernel's
+            ex = np.nonzero(ev["kind"] == A.EV_EXIT)[0][0]
+            ev["flags"][ex] |= A.F_EXIT_ARGS
+        dg, do = eng.submit(ev), orc.submit(ev)
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), ("batch", b, "event", int(bad[0]), ev[bad[0]], hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+        t = int(ev["ts"].max()) + 1
+    for r in range(3):
+        g, o = eng.read_node(r), orc.read_node(r)
+        assert g["thread"] == o["thread"]
+        np.testing.assert_array_equal(g["second"][:2], o["second"][:2])
+        np.testing.assert_array_equal(g["minute"], o["minute"])
