@@ -231,18 +231,42 @@ final class GpuEngine {
         }
     }
 
-    private static int argSlots(Op op) {
+    /**
+     * The op's arguments with every Collection / array copied once: the slot count and the table fill read the same
+     * elements even if a caller's collection changes meanwhile.
+     */
+    private static Object[] argSnapshot(Op op) {
         if (op.args == null) {
-            return 0;
+            return null;
         }
         int n = Math.min(op.args.length, SentinelGpu.MAX_ARGS);
-        int slots = n;
+        Object[] a = new Object[n];
         for (int i = 0; i < n; i++) {
             Object v = op.args[i];
             if (v instanceof Collection) {
-                slots += ((Collection<?>)v).size();
+                a[i] = ((Collection<?>)v).toArray();
             } else if (v != null && v.getClass().isArray()) {
-                slots += Array.getLength(v);
+                int len = Array.getLength(v);
+                Object[] el = new Object[len];
+                for (int j = 0; j < len; j++) {
+                    el[j] = Array.get(v, j);
+                }
+                a[i] = el;
+            } else {
+                a[i] = v;
+            }
+        }
+        return a;
+    }
+
+    private static int argSlots(Object[] a) {
+        if (a == null) {
+            return 0;
+        }
+        int slots = a.length;
+        for (Object v : a) {
+            if (v instanceof Object[]) {
+                slots += ((Object[])v).length;
             }
         }
         return slots;
@@ -288,16 +312,21 @@ final class GpuEngine {
             throw new IllegalStateException("an earlier batch failed; the engine's event indices are unknown");
         }
         int n = batch.size();
+        Object[][] args = new Object[n][];
         int nArg = 0;
-        for (Op op : batch) {
-            nArg += argSlots(op);
+        for (int i = 0; i < n; i++) {
+            args[i] = argSnapshot(batch.get(i));
+            nArg += argSlots(args[i]);
         }
         ensure(n, nArg);
+        // Fill the buffers first: a caller's toString() may throw in ParamKeys.of, and then nothing of this batch
+        // reached the engine -- no event index is consumed and later batches stay valid.
         int tail = 0;
+        long ts0 = lastTs;
         for (int i = 0; i < n; i++) {
             Op op = batch.get(i);
-            long ts = Math.max(op.ts, lastTs);
-            lastTs = ts;
+            long ts = Math.max(op.ts, ts0);
+            ts0 = ts;
             long e = i * EV_SZ;
             evBuf.set(JAVA_LONG, e + EV_TS, ts);
             evBuf.set(JAVA_INT, e + EV_RES, op.resId);
@@ -305,7 +334,8 @@ final class GpuEngine {
             evBuf.set(JAVA_BYTE, e + EV_KIND, (byte)op.kind);
             evBuf.set(JAVA_BYTE, e + EV_FLAGS, (byte)op.flags);
             evBuf.set(JAVA_LONG, e + EV_AUX, op.aux);
-            int na = op.args == null ? 0 : Math.min(op.args.length, SentinelGpu.MAX_ARGS);
+            Object[] a = args[i];
+            int na = a == null ? 0 : a.length;
             long x = i * EXT_SZ;
             extBuf.set(JAVA_INT, x + X_ORIGIN, op.origin);
             extBuf.set(JAVA_INT, x + X_CONTEXT, op.context);
@@ -314,18 +344,11 @@ final class GpuEngine {
             int base = tail;
             tail += na;
             for (int k = 0; k < na; k++) {
-                Object v = op.args[k];
-                if (v instanceof Collection || (v != null && v.getClass().isArray())) {
+                Object v = a[k];
+                if (v instanceof Object[]) {
                     int start = tail;
-                    if (v instanceof Collection) {
-                        for (Object el : (Collection<?>)v) {
-                            putArg(tail++, el);
-                        }
-                    } else {
-                        int len = Array.getLength(v);
-                        for (int j = 0; j < len; j++) {
-                            putArg(tail++, Array.get(v, j));
-                        }
+                    for (Object el : (Object[])v) {
+                        putArg(tail++, el);
                     }
                     long o = (base + k) * ARG_SZ;
                     argBuf.set(JAVA_LONG, o + A_KEY, start);
@@ -335,7 +358,6 @@ final class GpuEngine {
                     putArg(base + k, v);
                 }
             }
-            op.gidx = nextGidx++;
         }
         int rc;
         synchronized (nativeLock) {
@@ -348,6 +370,12 @@ final class GpuEngine {
             poisoned = true;
             SentinelGpu.check(rc);
         }
+        // the batch is in: its events hold the next n global indices (EXIT / TRACE references name them)
+        lastTs = ts0;
+        for (int i = 0; i < n; i++) {
+            batch.get(i).gidx = nextGidx + i;
+        }
+        nextGidx += n;
         for (int i = 0; i < n; i++) {
             Op op = batch.get(i);
             if (op.waiter != null) {

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
             // k_lite: no param rules, <= 2 DefaultController flow stages (QPS or thread), <= 2 breakers
             const bool lite = p.n_param == 0 && !p.multi && !prio[sg.res] && (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
-            bin = (lite ? BIN_LITE : nr <= 4 ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
+            bin = (lite ? BIN_LITE : (nr <= 4 && !(prio[sg.res] & PM_AUX)) ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
         }
         const uint32_t rank = atomicAdd(&cnt[bin], 1u);
         sg.bin = bin | (rank << 8);
@@ -576,8 +576,11 @@ __device__ AuxNode* aux_get(const DevState& S, uint32_t res, uint32_t kind, uint
     atomicOr(bflags, BF_AUX_FULL);
     return nullptr;
 }
-// the DefaultNode of (res, ctx) is kept iff a CHAIN rule of the resource names ctx
+// NodeSelectorSlot keeps a DefaultNode per (context, resource) for every entry (NodeSelectorSlot.java:134-176);
+// the device keeps those of named contexts always, and that of the default context while a CHAIN rule of the
+// resource names it (a CHAIN rule on sentinel_default_context starts from a fresh node)
 __device__ __forceinline__ bool chain_ctx_kept(const DRule* flows, int nf, uint32_t ctx) {
+    if (ctx != 0) return true;
     for (int k = 0; k < nf; ++k)
         if (flows[k].strategy == SG_STRATEGY_CHAIN && flows[k].chain_ctx == ctx) return true;
     return false;
@@ -673,7 +676,7 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                                                uint32_t fl, const EvX& x, uint32_t* bflags) {
     const DRule* rules = S.rules + pg.rule_off;
     const int np = pg.n_param, nfl = np + pg.n_flow, nr = nfl + pg.n_degrade;
-    const bool aux = NRMAX >= 16 && (pg.multi & (PX_ORIGIN | PX_CHAIN));
+    const bool aux = NRMAX >= 16;  // origin nodes / DefaultNodes (PM_AUX resources and PX_* rules are k_lane<16>'s)
     uint32_t status = ST_PASS, slot = 0;
     int64_t wait = 0;
 #pragma unroll
@@ -731,10 +734,9 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
     if (status == ST_PASS && pg.n_flow == 0 && (fl & SG_F_BLOCKED_UPSTREAM)) { status = ST_BLOCK_UPSTREAM; slot = 0; }
     // StatisticSlot.entry (StatisticSlot.java:54-133): DefaultNode -> ClusterNode, origin node
     const int what = status == ST_PASS ? 1 : status == ST_PASS_WAIT ? 2 : 0;
-    if (aux) {
-        if ((pg.multi & PX_ORIGIN) && x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, what, t, cnt, 0, bflags);
-        if ((pg.multi & PX_CHAIN) && chain_ctx_kept(rules + np, pg.n_flow, x.ctx))
-            aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, what, t, cnt, 0, bflags);
+    if (aux) {  // ClusterBuilderSlot's origin node, NodeSelectorSlot's DefaultNode: counted whatever the rules
+        if (x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, what, t, cnt, 0, bflags);
+        if (chain_ctx_kept(rules + np, pg.n_flow, x.ctx)) aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, what, t, cnt, 0, bflags);
     }
     if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
         N.thread++;
@@ -756,11 +758,10 @@ __device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState&
                                           uint32_t res, int64_t t, const SEv& r, const EvX& x, uint64_t ref,
                                           uint32_t* bflags) {
     stat_exit(N, C, t, r.cnt, r.rt);
-    if (NRMAX >= 16 && (pg.multi & (PX_ORIGIN | PX_CHAIN))) {
+    if (NRMAX >= 16) {  // the exit runs on the nodes its entry counted on (the same origin and context)
         const DRule* flows = S.rules + pg.rule_off + pg.n_param;
-        if ((pg.multi & PX_ORIGIN) && x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, 3, t, r.cnt, r.rt, bflags);
-        if ((pg.multi & PX_CHAIN) && chain_ctx_kept(flows, pg.n_flow, x.ctx))
-            aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
+        if (x.origin) aux_stat(S, cfg, res, AUX_ORIGIN, x.origin, 3, t, r.cnt, r.rt, bflags);
+        if (chain_ctx_kept(flows, pg.n_flow, x.ctx)) aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
     }
     if (!(r.flags & SG_F_EXIT_ARGS) || !(N.flags & NI_PM)) return;
     if (x.n) { thread_args(S, pg.tm_base, N.flags, x, -1, bflags); return; }

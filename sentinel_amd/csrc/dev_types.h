@@ -50,7 +50,9 @@ __host__ __device__ inline uint32_t ni_tm(uint32_t idx) { return 1u << (NI_TM_SH
 // segments to the per-lane kernel
 enum : uint8_t {
     PM_PRIO = 1,         // a prioritized ENTRY was seen: the second window's borrow ring is live
-    PM_LANE = 2          // an event only k_lane implements was seen: SG_F_BLOCKED_UPSTREAM, a NullContext
+    PM_LANE = 2,         // an event only k_lane implements was seen: SG_F_BLOCKED_UPSTREAM, a NullContext
+    PM_AUX = 4           // an event carried an origin or a named context: the resource keeps its origin
+                         // StatisticNodes / context DefaultNodes (k_lane<16>) whatever its rules are
 };
 
 struct NodeInfo {

@@ -108,6 +108,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                 key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
             }
             if (x.context_id > max_ctx) mark |= PM_LANE;
+            // ClusterBuilderSlot / NodeSelectorSlot keep an origin node and a DefaultNode per context for every
+            // entry, whatever the rules (ClusterBuilderSlot.java:74-99, NodeSelectorSlot.java:134-176)
+            else if (x.origin_id != 0 || x.context_id != 0) mark |= PM_AUX;
         }
         if (e.kind == SG_EV_ENTRY) {
             // the arg an exit(count, args) of this ENTRY will decrement (ParamFlowStatisticExitCallback)

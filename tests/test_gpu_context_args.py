@@ -237,3 +237,34 @@ def test_bad_args_table_is_rejected():
         eng.submit_ex(ev, ext, table)
     ext["n_args"] = 0
     assert (eng.submit_ex(ev, ext, table)[0] & 0xFF) == A.PASS  # the engine is still usable
+
+
+def test_rule_reload_with_entries_in_flight():
+    # origin nodes and DefaultNodes are kept for every entry whatever the rules, so origin / CHAIN rules
+    # loaded or removed while entries are in flight see the same node history as the reference
+    # (ClusterBuilderSlot.java:74-99, NodeSelectorSlot.java:134-176): no thread count leaks or goes negative
+    n_res = 36
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, status_ring_log2=22)
+    orc = O.Oracle(max_slot_chain_size=0)
+    io = [eng.intern_origin(o) for o in ORIGINS]
+    ic = [eng.intern_context(c) for c in CONTEXTS]
+    assert io == [orc.intern_origin(o) for o in ORIGINS] and ic == [orc.intern_context(c) for c in CONTEXTS]
+    for x in (eng, orc):
+        for i in range(n_res):
+            x.register("r%d" % i)
+    flow, param, deg = _rules(n_res)
+    plain = [A.flow_rule("r%d" % i, 12) for i in range(n_res)]
+    ev, ext, table = _trace(23, n_res, 9_000, io, ic)
+    cuts = np.linspace(0, len(ev), 4).astype(np.int64)
+    stages = [plain, flow, plain]  # origin / CHAIN rules arrive after batch 1 and leave after batch 2
+    dg, do = [], []
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        for x in (eng, orc):
+            x.load_flow_rules(stages[k])
+            if k == 1:
+                x.load_param_rules(param)
+                x.load_degrade_rules(deg)
+        g, o = _replay(eng, orc, ev[a:b], ext[a:b], table, 1)
+        dg.append(g)
+        do.append(o)
+    _check(eng, orc, ev, np.concatenate(dg), np.concatenate(do), n_res)

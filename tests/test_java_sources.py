@@ -122,6 +122,26 @@ def test_service_file_names_the_builder():
     assert "new GpuDecisionSlot()" in src
 
 
+def test_init_func_makes_the_builder_deterministic():
+    # SlotChainProvider takes the first non-default builder ServiceLoader finds (core/slotchain/
+    # SlotChainProvider.java:57-68) and the param extension registers HotParamSlotChainBuilder too: an InitFunc
+    # (run from Env's static initialiser before any chain, core/init/InitExecutor.java:40-63) installs the GPU
+    # builder into the provider's resolved field and fails loudly unless a built chain holds GpuDecisionSlot
+    svc = os.path.join(ROOT, "java", "src", "main", "resources", "META-INF", "services",
+                       "com.alibaba.csp.sentinel.init.InitFunc")
+    cls = [l.strip() for l in open(svc) if l.strip() and not l.startswith("#")]
+    assert cls == ["com.alibaba.csp.sentinel.gpu.GpuChainInit"]
+    src = open(os.path.join(JAVA, "GpuChainInit.java")).read()
+    assert "class GpuChainInit implements InitFunc" in src
+    assert "@InitOrder(Integer.MIN_VALUE)" in src                     # before every other InitFunc
+    assert 'getDeclaredField("builder")' in src                       # SlotChainProvider.builder
+    ref = "/root/reference/sentinel-core/src/main/java/com/alibaba/csp/sentinel/slotchain/SlotChainProvider.java"
+    if os.path.exists(ref):  # the field the InitFunc sets is the one newSlotChain() returns from
+        txt = open(ref).read()
+        assert "private static volatile SlotChainBuilder builder" in txt and "return builder.build();" in txt
+    assert "instanceof GpuDecisionSlot" in src and "throw new IllegalStateException" in src
+
+
 def test_java_sources_are_balanced():
     for root, _, files in os.walk(os.path.join(ROOT, "java", "src")):
         for f in files:
