@@ -9,21 +9,27 @@ chain cap lifted (max_slot_chain_size = 0).  Synthetic data (no network).
 
 Batches: the trace is cut into global batches of --batch-events events (2^25).  --base-batches of
 them are generated on the host; later batches are time-shifted copies built on the device before
-the timed region (timestamps + k x the trace span, EXIT/TRACE references + k x the events of the
+each timed chunk (timestamps + k x the trace span, EXIT/TRACE references + k x the events of the
 trace), so every batch is fresh to the engine -- time only moves forward, windows roll, breakers
-trip and reset -- and nothing is replayed.  A step is --sub-batches consecutive global batches
-submitted back to back through the engine's two-stage pipeline (sg_submit_async: the group stage of
-batch k+1 overlaps the decide stage of batch k); the default sizes it so that the inputs of all timed
-steps take 80 % of the free HBM (~220 global batches, a ~1 s timed region), and is printed in config.
-Inputs are resident in HBM when the timed region starts.
+trip and reset -- and nothing is replayed.  A step is --sub-batches global batches submitted back to
+back through the engine's two-stage pipeline (sg_submit_async: the group stage of batch k+1 overlaps
+the decide stage of batch k).  The K timed steps run in chunks whose inputs fit in HBM: before each
+chunk its fresh batches are built (untimed), the chunk is bracketed by barrier + synchronize and
+timed, and the step time is the chunks' total over K.  Inputs are resident in HBM whenever a timed
+chunk starts.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): ONE C4 trace,
-resources sharded by splitmix64(res_id) % N (strong scaling).  Every rank generates the same trace
-and keeps its shard (EXIT/TRACE references rewritten to its own numbering); global batch k of the
-trace is rank r's k-th batch (its share of it), so all ranks advance through trace time together.
-The decision path has no collective; the per-second MetricNode all-gather (RCCL) runs inside the
-timed region once per wall-clock second.  The step time is the max over ranks and value = every
-rank's entries / that time.
+resources partitioned over the ranks (strong scaling).  Every rank generates the same trace and
+keeps its shard (EXIT/TRACE references rewritten to its own numbering).  The partition is a resource ->
+rank table balanced by the base trace's event counts (sentinel_amd/dist.py balanced_table; --sharding
+hash: splitmix64(res_id) % N), and each rank submits its shard in rank-local batches of ~--batch-events
+events (a step is S / N of them per rank), so the ranks advance independently: the decision path has
+no collective, and only the per-second MetricNode all-gather (RCCL) inside the timed chunks and the
+chunk barriers synchronise them.  The step time is the max over ranks and value = every rank's
+entries / that time.
+
+After the C4 line's measurement (N = 1), the same pipeline measures the other SURVEY.md §8(d) configs
+C2, C3 and C5 (bounded traces, inputs in HBM) and reports them under "configs" (--no-configs: skip).
 """
 from __future__ import annotations
 
@@ -55,12 +61,16 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch-events", type=int, default=1 << 25, help="events per global batch")
     p.add_argument("--base-batches", type=int, default=8, help="global batches generated on the host")
-    p.add_argument("--sub-batches", type=int, default=0, help="global batches per step (0: auto)")
-    p.add_argument("--max-sub-batches", type=int, default=64)
+    p.add_argument("--sub-batches", type=int, default=48, help="global batches per step (a multiple of N)")
+    p.add_argument("--max-sub-batches", type=int, default=0, help="(kept for old scripts; unused)")
     p.add_argument("--hbm-budget", type=float, default=0.8,
-                   help="fraction of free HBM for the timed steps' inputs (sets the timed region's length, ~1 s)")
+                   help="fraction of free HBM for one timed chunk's inputs")
+    p.add_argument("--sharding", choices=("balanced", "hash"), default="balanced",
+                   help="resource -> GPU partition: balanced by event counts, or splitmix64(res_id) %% N")
+    p.add_argument("--no-configs", action="store_true", help="skip the C2 / C3 / C5 sub-lines")
     p.add_argument("--resources", type=int, default=1_000_000)
-    p.add_argument("--cpu-threads", type=int, default=0, help="partitioned oracle threads (0: min(16, cores))")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="partitioned oracle threads (0: this job's CPU share -- cgroup cpu.max, else min(16, cores))")
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
     p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -135,6 +145,7 @@ def main():
     from sentinel_amd import tracegen as T
 
     steps, warmup, gb, B = args.steps, args.warmup, args.batch_events, args.base_batches
+    S = max(1, args.sub_batches)
     # ---- one trace for the whole node; this rank's shard of it
     t_gen = time.time()
     w, ev = make_trace(args.resources, gb, B, T.SEED_BASE + 4)
@@ -143,15 +154,24 @@ def main():
     shard = tuple(int(x) for x in args.shard.split("/")) if args.shard else None  # (R, N)
     if shard:
         assert world == 1 and 0 <= shard[0] < shard[1], "--shard R/N: one process, 0 <= R < N"
-    if world > 1 or shard:
-        mine, pos = D.shard_stream(ev, shard[1], shard[0]) if shard else D.shard_stream(ev, world, rank)
-        cuts = np.searchsorted(pos, np.arange(B + 1, dtype=np.int64) * gb)
+    nparts = shard[1] if shard else world
+    me = shard[0] if shard else rank
+    table = None
+    if nparts > 1:
+        if args.sharding == "balanced":  # every rank computes the same table from the same trace
+            table = D.balanced_table(np.bincount(ev["res_id"], minlength=args.resources), nparts)
+        mine, pos = D.shard_stream(ev, nparts, me, table)
     else:
-        mine, cuts = ev, np.arange(B + 1, dtype=np.int64) * gb
+        mine = ev
     n_base = len(mine)
+    # rank-local batches: the shard of the B base batches in B / N batches of ~gb events (a step is S / N of them)
+    LB = max(1, B // nparts)
+    per_step = max(1, S // nparts)
+    cuts = np.linspace(0, n_base, LB + 1).astype(np.int64)
     sizes = np.diff(cuts)
-    ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(B)])
-    res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(B)])
+    ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(LB)])
+    res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(LB)])
+    end_b = np.array([int(mine["ts"][max(cuts[b], cuts[b + 1] - 1)]) for b in range(LB)])
 
     eng = E.Engine(device=dev.index, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
                    status_ring_log2=28, max_batch_events=int(sizes.max()))
@@ -169,33 +189,31 @@ def main():
     del host
     base64 = base.view(torch.int64).view(-1, 3)
 
-    # ---- sub-batches per step: the inputs of all timed steps in HBM at once (they are rebuilt between
-    # the warmup and the timed region), after the engine's two batch slots (~120 B per event each)
+    # ---- one timed chunk's inputs in HBM at once, after the engine's two batch slots (~120 B per event each)
     free = torch.cuda.mem_get_info(dev)[0]
     mean_b = float(sizes.mean()) * 24
-    snap_cap = min(60 * args.resources // world + 4096, 1 << 26)
+    snap_cap = min(60 * args.resources // max(1, world) + 4096, 1 << 26)
     reserve = 2 * 120 * int(sizes.max()) + snap_cap * 64
-    S = args.sub_batches or int(max(1, min(args.max_sub_batches,
-                                         args.hbm_budget * (free - reserve) // (max(steps, warmup) * mean_b * 1.15))))
+    chunk_steps = int(max(1, min(steps, args.hbm_budget * (free - reserve) // (per_step * mean_b * 1.15))))
     if dist is not None:
-        t = torch.tensor([S], device=cdev)
+        t = torch.tensor([chunk_steps], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        S = int(t.item())
-    nbat = max(steps, warmup) * S
-    gidx = lambda i: (i % B, i // B)  # global batch i -> (base batch, copy)
-    max_ev = max(int(sum(sizes[gidx(i)[0]] for i in range(g0, g0 + n))) for g0, n in ((0, warmup * S), (warmup * S, steps * S)))
+        chunk_steps = int(t.item())
+    gidx = lambda i: (i % LB, i // LB)  # rank-local batch i -> (base batch, copy)
+    max_ev = max(int(sum(sizes[gidx(i)[0]] for i in range(g0, g0 + chunk_steps * per_step)))
+                 for g0 in range(0, (warmup + steps) * per_step, chunk_steps * per_step))
     buf = torch.empty((max_ev, 3), dtype=torch.int64, device=dev)
     out = torch.empty(int(sizes.max()), dtype=torch.int32, device=dev)
     snap = torch.empty(snap_cap * 64, dtype=torch.uint8, device=dev) if dist is not None else None
 
     def build(g0, n):
-        """Global batches g0..g0+n-1 of this rank into buf: [(row offset, rows, entries, touched)]."""
+        """Rank-local batches g0..g0+n-1 into buf: [(row offset, rows, entries, touched, end ts)]."""
         plan, off = [], 0
         for g in range(g0, g0 + n):
             b, k = gidx(g)
             m = int(sizes[b])
             shifted_batch(base64, int(cuts[b]), int(cuts[b + 1]), k, tspan, n_base, buf[off:off + m])
-            plan.append((off, m, int(ent_b[b]), int(res_b[b]), int(ev["ts"][min(len(ev) - 1, (b + 1) * gb - 1)]) + k * tspan))
+            plan.append((off, m, int(ent_b[b]), int(res_b[b]), int(end_b[b]) + k * tspan))
             off += m
         torch.cuda.synchronize()
         return plan
@@ -220,33 +238,45 @@ def main():
 
     base_ptr = buf.data_ptr()
     # ---- warmup (untimed): the first W steps of the stream
-    plan = build(0, warmup * S)
-    for off, m, _, _, _ in plan:
-        eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
-    eng.sync()
+    g = 0
+    for c0 in range(0, warmup, chunk_steps):
+        n = min(chunk_steps, warmup - c0) * per_step
+        for off, m, _, _, _ in build(g, n):
+            eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
+        eng.sync()
+        g += n
     eng.timing_log()
     if dist is not None:  # the first fetch (lastFetchTime = -1) outside the timed region
-        gather_metrics(plan[-1][4])
-    # ---- timed: the next K steps (fresh, time-shifted batches)
-    plan = build(warmup * S, steps * S)
+        gather_metrics(int(end_b[(g - 1) % LB]) + ((g - 1) // LB) * tspan)
+    # ---- timed: the next K steps (fresh, time-shifted batches), chunk by chunk
     n_gather, rows_gathered = 0, 0
-    barrier()
-    t_start = time.perf_counter()
-    t_last = t_start
-    for s in range(steps):
-        for off, m, _, _, _ in plan[s * S:(s + 1) * S]:
-            eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
-        if dist is not None and (s == steps // 2 or time.perf_counter() - t_last >= 1.0):
-            rows_gathered += gather_metrics(plan[(s + 1) * S - 1][4])  # drains this rank's pipeline
-            n_gather += 1
-            t_last = time.perf_counter()
-    eng.sync()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    stage_ms = np.array(eng.timing_log())  # per timed batch: [group, decide, post, total] device ms
-    entries = float(sum(p[2] for p in plan))
-    touched = float(sum(p[3] for p in plan))
-    events = float(sum(p[1] for p in plan))
+    elapsed, entries, touched, events, stage_rows = 0.0, 0.0, 0.0, 0.0, []
+    chunks = 0
+    for c0 in range(0, steps, chunk_steps):
+        ns = min(chunk_steps, steps - c0)
+        plan = build(g, ns * per_step)
+        g += ns * per_step
+        barrier()
+        t_start = time.perf_counter()
+        t_last = t_start
+        for s in range(ns):
+            for off, m, _, _, _ in plan[s * per_step:(s + 1) * per_step]:
+                eng.submit_ptr(base_ptr + off * 24, m, out.data_ptr(), sync=False)
+            if dist is not None and time.perf_counter() - t_last >= 1.0:
+                rows_gathered += gather_metrics(plan[(s + 1) * per_step - 1][4])  # drains this rank's pipeline
+                n_gather += 1
+                t_last = time.perf_counter()
+        eng.sync()
+        barrier()
+        elapsed += time.perf_counter() - t_start
+        chunks += 1
+        stage_rows += eng.timing_log()  # per timed batch: [group, decide, post, total] device ms
+        entries += float(sum(p[2] for p in plan))
+        touched += float(sum(p[3] for p in plan))
+        events += float(sum(p[1] for p in plan))
+    if dist is not None and n_gather == 0:  # at least one all-gather per run, untimed
+        rows_gathered += gather_metrics(plan[-1][4])
+    stage_ms = np.array(stage_rows)
     if dist is not None:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -254,14 +284,20 @@ def main():
         t = torch.tensor([entries, touched, events], device=cdev, dtype=torch.float64)
         dist.all_reduce(t)
         entries, touched, events = (float(x) for x in t.tolist())
+        lb = torch.tensor([float(n_base)], device=cdev, dtype=torch.float64)
+        lbs = [torch.zeros_like(lb) for _ in range(world)]
+        dist.all_gather(lbs, lb)
+        shares = [float(x.item()) for x in lbs]
+    else:
+        shares = [float(n_base)]
 
-    nb = steps * S  # global batches timed
+    nb = steps * S  # global-batch equivalents timed (all ranks)
     batch_ms = elapsed / nb * 1e3
     # algorithmic bytes per global batch (all ranks), SURVEY.md §8(d)
     alg = (events * EVENT_B + entries * DECISION_B + touched * STATE_RW_B) / nb
     achieved = alg / (batch_ms / 1e3) / 1e9
     decide_ms = float(stage_ms[:, 1].mean())
-    dec_alg = alg / world  # this rank's share, over its own decide-stage time
+    dec_alg = alg * nb / (steps * per_step) / world  # one rank-local batch's share, over its decide-stage time
     traffic, tnote = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     sha = src_sha()
@@ -277,9 +313,16 @@ def main():
                    "measured on one GPU, this run has %d ranks" % world if world > 1 else
                    "measured on the whole trace, this run is one shard")
             tnote = "profiles/pmc_latest.json is for other sources/config (%s): not used" % why
+    stream = stream_copy_gbps(dev) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not shard and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, ev, args)
+    configs = None
+    if rank == 0 and world == 1 and not shard and not args.no_configs:
+        del buf, base, base64, out
+        eng.close()
+        torch.cuda.empty_cache()
+        configs = config_lines(dev)
 
     if rank == 0:
         line = {
@@ -291,7 +334,7 @@ def main():
             "warmup": warmup,
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",   # one trace split over the ranks: total work is fixed as N grows
+            "scaling": "strong",   # one trace partitioned over the ranks: total work is fixed as N grows
             "vs_baseline": None,
             "dtype": "int64/f64",
             "data": "synthetic (seeded C4 trace: Zipf(1.1), RT~Exp(20ms), 5% traces; time-shifted fresh batches)",
@@ -299,9 +342,17 @@ def main():
                        "resources": args.resources, "batch_events": gb, "sub_batches_per_step": S,
                        "events_per_step": events / steps, "entries_per_step": entries / steps,
                        "resources_touched_per_batch": touched / nb, "base_batches": B,
-                       "parallelism": "resource-sharded x%d (splitmix64(res_id) %% %d)" % (world, world)},
+                       "timed_chunks": chunks, "rank_local_batches_per_step": per_step,
+                       "parallelism": ("resource-sharded x%d (%s)" % (world, "balanced by event counts"
+                                                                      if args.sharding == "balanced" else
+                                                                      "splitmix64(res_id) %% %d" % world))
+                                      if world > 1 else "one GPU",
+                       "rank_event_shares": [x / sum(shares) for x in shares]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
+                         "traffic_GBps": traffic / (batch_ms / 1e3) / 1e9 if traffic else None,
+                         "stream_copy_GBps": stream,
+                         "frac_of_stream_copy": achieved / stream if stream else None,
                          "kernel": "one global batch through the whole pipeline (sort/group, decide, post)",
                          "batch_ms": batch_ms, "alg_bytes_per_batch": alg,
                          "decide_stage": {"ms": decide_ms, "achieved": dec_alg / (decide_ms / 1e3) / 1e9,
@@ -318,12 +369,95 @@ def main():
                           "rank %d of %d alone on one GPU (per-rank step of an N-GPU run): NOT a measurement" % shard
                           if shard else None),
             "cpu_baseline": cpu,
+            "configs": configs,
             "src_sha": sha,
             "gen_s": gen_s,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def stream_copy_gbps(dev) -> float:
+    """Device-to-device copy bandwidth (read + write bytes / time) of a 4 GiB buffer: the attainable
+    HBM rate, the second roofline denominator."""
+    import torch
+    n = 1 << 31
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2.0 * n * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbps
+
+
+# SURVEY.md §8(d) configs besides C4, measured as bench.py measures C4 (first batch untimed, the rest back to back
+# through the pipeline, inputs in HBM): (config, entries, events per batch, engine kwargs, tracegen variant, name)
+CONFIGS = [
+    (2, 50_000_000, 1 << 25, {}, 0, "C2: 10k resources, QPS DefaultController flow rules, Zipf(1.1)"),
+    (3, 24_000_000, 1 << 24, {}, 1, "C3: 100k resources, QPS / thread / WarmUp / RateLimiter / WarmUpRateLimiter"),
+    (5, 12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
+     "C5: 10k resources, ParamFlow QPS rules (20 % throttle) over 10M Zipf values"),
+]
+
+
+def config_lines(dev):
+    import torch
+    from sentinel_amd import engine as E
+    from sentinel_amd import tracegen as T
+    rows = []
+    for cfg, n_entries, gb, kw, var, name in CONFIGS:
+        w = T.Workload(cfg, seed=T.SEED_BASE + cfg, n_entries=n_entries, variant=var)
+        ev = w.events
+        nb = (len(ev) + gb - 1) // gb
+        cuts = [min(len(ev), b * gb) for b in range(nb + 1)]
+        eng = E.Engine(device=dev.index, max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0,
+                       max_batch_events=gb, **kw)
+        w.install(eng)
+        buf = torch.from_numpy(np.ascontiguousarray(ev).view(np.uint8)).to(dev)
+        out = torch.empty(gb, dtype=torch.int32, device=dev)
+        p0 = buf.data_ptr()
+        eng.submit_ptr(p0, cuts[1], out.data_ptr(), sync=True)  # the first batch, untimed
+        eng.timing_log()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in range(1, nb):
+            eng.submit_ptr(p0 + cuts[b] * 24, cuts[b + 1] - cuts[b], out.data_ptr(), sync=False)
+        eng.sync()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        st = np.array(eng.timing_log())
+        timed = ev[cuts[1]:]
+        ent = int((timed["kind"] == 0).sum())
+        rows.append({"config": name, "value": ent / dt, "unit": "entries/s", "batches_timed": nb - 1,
+                     "batch_events": gb, "entries_timed": ent, "ms_per_batch": dt / (nb - 1) * 1e3,
+                     "stage_ms_mean": {"group": float(st[:, 0].mean()), "decide": float(st[:, 1].mean()),
+                                       "post": float(st[:, 2].mean())}, "resources": w.n_res})
+        eng.close()
+        w.close()
+        del buf, out
+        torch.cuda.empty_cache()
+    return rows
+
+
+def cpu_share() -> int:
+    """This job's CPUs: the cgroup v2 cpu.max quota (the GPU box gives a one-GPU job 16 of its host's
+    cores), else min(16, the affinity set)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return min(16, len(os.sched_getaffinity(0)))
 
 
 def cpu_model() -> str:
@@ -343,7 +477,7 @@ def cpu_baseline(w, ev, args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     avail = len(os.sched_getaffinity(0))
-    T = args.cpu_threads or min(16, avail)
+    T = args.cpu_threads or cpu_share()
     sample = ev[:args.cpu_sample_events]
     po = O.PartitionedOracle(w, T, max_slot_chain_size=0)
     spent = []
@@ -361,6 +495,10 @@ def cpu_baseline(w, ev, args):
             "sample": "first %d events (%d entries) of the C4 trace, oracle/liboracle.so, %d threads partitioned "
                       "by splitmix64(res_id) %% %d (routing excluded)" % (len(sample), n_ent, T, T),
             "single_thread": {"value": n1 / dt1, "cores": 1, "sample": "first %d events (%d entries)" % (len(s1), n1)},
+            "full_width": {"value": n_ent / spent[0] * (os.cpu_count() or T) / T, "cores": os.cpu_count(),
+                           "note": "the measured %d-thread rate scaled linearly to nproc: this job may use %d of "
+                                   "the host's %d CPUs (the box's CPU share), so nproc threads are not run" %
+                                   (T, T, os.cpu_count() or T)},
             "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": avail}
 
 

@@ -2,8 +2,11 @@
 
 One process and one engine per GPU (torch.distributed: "nccl" is RCCL over xGMI here, "gloo" on
 CPU).  Every decision reads and writes only its own resource's state, so resources shard by
-``splitmix64(res_id) % world`` and the decision path has no collective at all.  Two exchanges
-remain, and they live here:
+``splitmix64(res_id) % world`` and the decision path has no collective at all.  Under Zipf popularity a
+hash leaves the hottest resource's GPU with its share plus 1/world of the rest (C4 at 8 GPUs: 23 % of the
+events on one GPU, a 4.3x ceiling), so a ``ShardMap`` may instead place resources by their observed event
+counts (largest first onto the least loaded GPU; unseen resources by the hash): still a fixed partition of
+resources, still no data-path traffic.  Two exchanges remain, and they live here:
 
 * ``gather_metrics``: once per second every rank's ``sg_snapshot_metrics`` output is all-gathered
   (the MetricTimerListener role, core/node/metric/MetricTimerListener.java:39-56, over the whole
@@ -31,9 +34,29 @@ def splitmix64(x) -> np.ndarray:
     return z ^ (z >> np.uint64(31))
 
 
-def shard_of(res_ids, world: int) -> np.ndarray:
-    """Owning rank of each resource: splitmix64(res_id) % world."""
-    return (splitmix64(res_ids) % np.uint64(world)).astype(np.int64)
+def shard_of(res_ids, world: int, table=None) -> np.ndarray:
+    """Owning rank of each resource: table[res_id] where a ShardMap table gives one (>= 0), else
+    splitmix64(res_id) % world."""
+    h = (splitmix64(res_ids) % np.uint64(world)).astype(np.int64)
+    if table is None:
+        return h
+    r = np.asarray(res_ids, dtype=np.int64)
+    t = np.where(r < len(table), table[np.minimum(r, len(table) - 1)], -1)
+    return np.where(t >= 0, t, h)
+
+
+def balanced_table(counts, world: int) -> np.ndarray:
+    """A resource -> rank table from per-resource event counts: largest first onto the least loaded rank
+    (longest-processing-time greedy); resources with no events stay on their hash rank (-1)."""
+    counts = np.asarray(counts, dtype=np.int64)
+    table = np.full(len(counts), -1, dtype=np.int64)
+    load = np.zeros(world, dtype=np.int64)
+    seen = np.nonzero(counts)[0]
+    for r in seen[np.argsort(-counts[seen], kind="stable")]:
+        k = int(np.argmin(load))
+        table[r] = k
+        load[k] += counts[r]
+    return table
 
 
 _REF = np.uint64(A.REF_NONE)
@@ -51,10 +74,12 @@ class EventRouter:
     the referencing event itself, which the engine rejects as a bad reference (SG_EINVAL).
     """
 
-    def __init__(self, world: int, ring_log2: int = 24):
+    def __init__(self, world: int, ring_log2: int = 24, table=None):
         self.world = world
+        self.table = table
         self.mask = (1 << ring_log2) - 1
         self.local = np.zeros(1 << ring_log2, dtype=np.int64)  # submitting index -> rank-local index
+        self.owner = np.zeros(1 << ring_log2, dtype=np.int64)  # submitting index -> its rank
         self.gin = 0                                  # submitting index of the next input event
         self.gout = np.zeros(world, dtype=np.int64)   # rank-local index of each rank's next event
 
@@ -64,6 +89,9 @@ class EventRouter:
         self.mask = 2 * size - 1
         self.local = np.zeros(2 * size, dtype=np.int64)
         self.local[idx & self.mask] = old[idx & (size - 1)]
+        oown = self.owner
+        self.owner = np.zeros(2 * size, dtype=np.int64)
+        self.owner[idx & self.mask] = oown[idx & (size - 1)]
 
     def route(self, events: np.ndarray):
         """Returns (batches, positions): positions[r] are the indices of rank r's events in the
@@ -71,7 +99,7 @@ class EventRouter:
         n = len(events)
         while n > (self.mask + 1) // 2:  # keep room for the batch plus as much history again
             self._grow()
-        owner = shard_of(events["res_id"], self.world)
+        owner = shard_of(events["res_id"], self.world, self.table)
         order = np.argsort(owner, kind="stable")
         cuts = np.searchsorted(owner[order], np.arange(self.world + 1))
         pos = [order[cuts[r]:cuts[r + 1]] for r in range(self.world)]
@@ -81,10 +109,14 @@ class EventRouter:
             loc[p] = self.gout[r] + np.arange(len(p), dtype=np.int64)
             self.gout[r] += len(p)
         self.local[gidx & self.mask] = loc
+        self.owner[gidx & self.mask] = owner
         aux = events["aux"].astype(np.uint64)
         isref = (events["kind"] != A.EV_ENTRY) & ((aux & _REF) != _REF)
         ref = (aux & _REF).astype(np.int64)
         ok = isref & (ref < gidx) & (ref >= self.gin + n - 1 - self.mask)  # ring slot not reused yet
+        # a reference to an event another rank holds (another resource's ENTRY) cannot be mapped: it would alias
+        # an unrelated event of this rank's numbering, so it becomes a self-reference the engine rejects
+        ok &= self.owner[ref & self.mask] == owner
         bad = isref & ~ok
         new = np.where(ok, self.local[ref & self.mask], loc)
         aux2 = np.where(isref, (aux & ~_REF) | (new.astype(np.uint64) & _REF), aux)
@@ -99,12 +131,12 @@ class EventRouter:
         return out, pos
 
 
-def shard_stream(events: np.ndarray, world: int, rank: int):
+def shard_stream(events: np.ndarray, world: int, rank: int, table=None):
     """Rank ``rank``'s share of a whole sg_event stream that starts at global index 0 (what one
     process of a multi-GPU run keeps of a trace every rank generates alike): its events in order,
     with EXIT/TRACE references rewritten to the rank's numbering, and their positions in the
     input.  O(n + m log m) for m events of the rank, no sort of the whole stream."""
-    pos = np.nonzero(shard_of(events["res_id"], world) == rank)[0]
+    pos = np.nonzero(shard_of(events["res_id"], world, table) == rank)[0]
     mine = events[pos].copy()
     aux = mine["aux"].astype(np.uint64)
     isref = (mine["kind"] != A.EV_ENTRY) & ((aux & _REF) != _REF)
@@ -118,14 +150,14 @@ def shard_stream(events: np.ndarray, world: int, rank: int):
     return mine, pos
 
 
-def route_events(events: np.ndarray, world: int):
+def route_events(events: np.ndarray, world: int, table=None):
     """Split a time-ordered sg_event stream that starts at global index 0 into the per-rank
     streams, with EXIT/TRACE references rewritten to each rank's numbering (see EventRouter).
     Returns (batches, positions)."""
     ring = 1
     while ring < max(2, len(events)):
         ring <<= 1
-    return EventRouter(world, ring_log2=ring.bit_length() - 1).route(events)
+    return EventRouter(world, ring_log2=ring.bit_length() - 1, table=table).route(events)
 
 
 def _device(group=None):

@@ -124,7 +124,7 @@ def _w_metrics(rank, world, port):
     dist.destroy_process_group()
 
 
-def _w_routed_decisions(rank, world, port):
+def _w_routed_decisions(rank, world, port, balanced=False):
     """Each rank decides its splitmix64 shard of one C4 stream (ENTRY/EXIT/TRACE, three batches) with its
     own engine; the merged decisions and the owned resources' node states equal one engine's run over the
     whole stream.  The oracle is the engine here (CPU), so this checks the routing: shards, order and the
@@ -138,7 +138,8 @@ def _w_routed_decisions(rank, world, port):
     ev = w.events
     mine = O.Oracle(max_slot_chain_size=0)
     w.install(mine)
-    router = D.EventRouter(world, ring_log2=18)
+    table = D.balanced_table(np.bincount(ev["res_id"], minlength=w.n_res), world) if balanced else None
+    router = D.EventRouter(world, ring_log2=18, table=table)
     cuts = np.linspace(0, len(ev), 4).astype(np.int64)
     dec = np.zeros(len(ev), dtype=np.uint32)
     for a, b in zip(cuts[:-1], cuts[1:]):
@@ -152,7 +153,7 @@ def _w_routed_decisions(rank, world, port):
     w.install(whole)
     ref = whole.submit(ev)
     assert np.array_equal(dec, ref), (rank, int(np.nonzero(dec != ref)[0][0]))
-    owned = np.nonzero(D.shard_of(np.arange(w.n_res), world) == rank)[0]
+    owned = np.nonzero(D.shard_of(np.arange(w.n_res), world, table) == rank)[0]
     for r in owned[:60]:
         g, o = mine.read_node(int(r)), whole.read_node(int(r))
         assert g["thread"] == o["thread"] and np.array_equal(g["minute"], o["minute"]), r
@@ -162,8 +163,33 @@ def _w_routed_decisions(rank, world, port):
     dist.destroy_process_group()
 
 
-def test_routed_decisions_equal_single_engine_gloo():
-    mp.spawn(_w_routed_decisions, args=(2, _port()), nprocs=2, join=True)
+@pytest.mark.parametrize("balanced", [False, True])
+def test_routed_decisions_equal_single_engine_gloo(balanced):
+    mp.spawn(_w_routed_decisions, args=(2, _port(), balanced), nprocs=2, join=True)
+
+
+def test_balanced_table_and_cross_rank_references():
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    from sentinel_amd import tracegen as T
+    # C4 popularity: the hottest resource holds ~12 % of the events; by hash its GPU also gets 1/8 of the rest
+    w = T.Workload(4, n_entries=300_000, n_res=100_000)
+    cnt = np.bincount(w.events["res_id"], minlength=w.n_res)
+    table = D.balanced_table(cnt, 8)
+    share = lambda own: np.bincount(own, weights=cnt, minlength=8) / cnt.sum()
+    hashed = share(D.shard_of(np.arange(w.n_res), 8))
+    bal = share(D.shard_of(np.arange(w.n_res), 8, table))
+    assert bal.max() < hashed.max() and bal.max() <= max(cnt.max() / cnt.sum(), 1 / 8) * 1.02, (bal, hashed)
+    assert (table[cnt == 0] == -1).all()  # unseen resources keep their hash rank
+    # an EXIT naming another resource's ENTRY held by another rank becomes a self-reference (rejected)
+    ev = np.zeros(3, dtype=A.EVENT_DTYPE)
+    ev["ts"] = T0 + np.arange(3)
+    tab = np.array([0, 1], dtype=np.int64)  # resource 0 on rank 0, resource 1 on rank 1
+    ev["res_id"] = [0, 1, 1]
+    ev["kind"] = [A.EV_ENTRY, A.EV_ENTRY, A.EV_EXIT]
+    ev["aux"] = [0, 0, A.aux_exit(0, 5)]  # rank 1's EXIT names rank 0's ENTRY
+    parts, pos = D.EventRouter(2, ring_log2=4, table=tab).route(ev)
+    assert list(pos[1]) == [1, 2] and int(parts[1]["aux"][1]) & A.REF_NONE == 1  # its own local index
 
 
 def test_router_rewrites_references():
