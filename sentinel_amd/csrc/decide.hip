@@ -1187,6 +1187,7 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
     } while (0)
 __device__ __forceinline__ uint32_t op_add(uint32_t a, uint32_t b) { return a + b; }
 __device__ __forceinline__ uint32_t op_min(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t op_max(uint32_t a, uint32_t b) { return a > b ? a : b; }
 // segmented count: bit31 = "reset here", low bits = count since the last reset; a is the earlier element
 __device__ __forceinline__ uint32_t op_seg(uint32_t a, uint32_t b) {
     return (b & 0x80000000u) ? b : ((a & 0x80000000u) | ((a + b) & 0x7fffffffu));
@@ -1268,6 +1269,8 @@ struct JacSh {
     uint32_t pad2;
     uint2 spn[NSPAN];          // [s, e) relative positions
     unsigned long long fl[NW]; // flagged-block ballots
+    uint32_t cg[NW][3];        // closed-form guesses: per-wave totals (entries, effective exits | last entry time, others)
+    uint32_t cgm[NW];          // ... per-wave minimum of the thread-grade admission bound
 };
 
 // leader: fold the round's committed deltas into the node (StatisticSlot bookkeeping of every
@@ -1466,6 +1469,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     }
     const bool has_rt = (pg.pflags & PF_RT) != 0;
     const bool frozen_prog = (pg.pflags & PF_FROZEN) != 0;
+    // single-stage programs with closed-form admission guesses (see the Jacobi iteration)
+    const bool tg_mode = nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_THREAD &&
+                         sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_DEFAULT && !(cfg.dbg_flags & 16);
+    const bool rl_mode = RL && nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_QPS &&
+                         (sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
+                          sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) && !(cfg.dbg_flags & 16);
 
     // diagnostics (SG_DEBUG=1): per-bin iteration counters; phase cycles of the bin's first segment
     // only in builds with -DSG_KPROF (the timers cost registers the 1024-lane kernel does not have)
@@ -1934,6 +1943,84 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 PROF_MARK(8)
                 continue;
             }
+        }
+
+        // ================= closed-form guesses of single-stage programs =================
+        // A guess only steers how many iterations a tile takes (every verdict is still verified below), but the
+        // default re-guess -- every later ENTRY takes the pivot's outcome -- costs two iterations per admission
+        // when admissions are sparse and state-driven: a saturated THREAD-grade DefaultController admits one
+        // ENTRY per freed thread, a saturated RateLimiter one per `cost` ms (C3's hottest resources).  Both
+        // admission sequences have closed forms given the statuses the guesses imply, so the uncommitted ENTRYs
+        // of the round are re-guessed with them at the start of every iteration (all in-round ENTRYs acquire 1).
+        //   THREAD (DefaultController.java:49-81): thread before ENTRY e = th_c + P(e) - X(e) (P passes, X effective
+        //   exits since c0); it passes iff P(e) < Z(e) = max(0, cap - th_c + X(e)) with Z non-decreasing, so
+        //   P(e + 1) = min(P(e) + 1, Z(e)), P(n) = E(n) + min(0, min_{j < n} W(j)), W(j) = Z(j) - E(j + 1)
+        //   (E: ENTRYs since c0): e passes iff W(e) >= min(0, min_{j < e} W(j)) -- a prefix-min scan.
+        //   RateLimiter (RateLimiterController.java:46-91): saturated, the k-th admission after the committed
+        //   latestPassedTime L is the first ENTRY with t >= L + k * cost - maxQueue: e passes iff
+        //   q(t_e) > q(t of the previous ENTRY), q(t) = max(0, floor((t - L + maxQueue) / cost)).
+        if (EP == 1 && (tg_mode || rl_mode)) {
+            const uint32_t kf = ev[0].kf, kind = kf & 0xFFu;
+            const bool inr = (kf & JK_VALID) && lp0 >= c0 && ev[0].dt >= dlo && ev[0].dt < dhi;
+            const bool eff = (kf & JK_WIN) ? (win[ev[0].wi] != 0) : ((kf & JK_VAL) != 0);
+            const uint32_t a = (inr && kind == SG_EV_ENTRY) ? 1u : 0u;
+            const uint32_t x = (inr && kind == SG_EV_EXIT && eff) ? 1u : 0u;
+            const uint32_t bad = (a && (ev[0].cz & 0xFFFFu) != 1u) ? 1u : 0u;
+            uint32_t ia = a, ix = tg_mode ? x : (a ? (uint32_t)(ev[0].dt - dlo) + 1u : 0u), ib = bad;
+            WAVE_SCAN(ia, 0u, op_add);
+            if (tg_mode) WAVE_SCAN(ix, 0u, op_add);
+            else WAVE_SCAN(ix, 0u, op_max);
+            WAVE_SCAN(ib, 0u, op_add);
+            if (lane == 63) { sh.cg[wv][0] = ia; sh.cg[wv][1] = ix; sh.cg[wv][2] = ib; }
+            lds_barrier();
+            uint32_t pa = 0, px = 0, tb = 0;
+            for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                if (w < wv) { pa += sh.cg[w][0]; px = tg_mode ? px + sh.cg[w][1] : op_max(px, sh.cg[w][1]); }
+                tb += sh.cg[w][2];
+            }
+            const bool use = uni(tb) == 0;
+            bool g = false;  // the closed-form outcome of this lane's ENTRY (pass)
+            if (use && tg_mode) {
+                const int64_t th_c = uni64(sh.bTH + sh.cTH);
+                const double cnt_thr = sh.rules[0].count;
+                const int64_t cap = cnt_thr <= 0 ? 0 : (cnt_thr >= 2147483647.0 ? 2147483647 : (int64_t)cnt_thr);
+                const int64_t Xb = (int64_t)(px + ix - x);        // effective exits strictly before e
+                const int64_t Ain = (int64_t)(pa + ia);           // ENTRYs up to and including e
+                int64_t Z = cap - th_c + Xb;
+                if (Z < 0) Z = 0;
+                int64_t W = inr ? Z - Ain : (int64_t)0x3FFFFFFF;
+                W = W > 0x3FFFFFFF ? 0x3FFFFFFF : W < -0x3FFFFFFF ? -0x3FFFFFFF : W;
+                const uint32_t wb = (uint32_t)(W + 0x40000000LL);  // biased for an unsigned min scan
+                uint32_t m = wb;
+                WAVE_SCAN(m, 0xFFFFFFFFu, op_min);
+                if (lane == 63) sh.cgm[wv] = m;
+                const uint32_t mex = shr1(m, 0xFFFFFFFFu);
+                lds_barrier();
+                uint32_t pm = 0xFFFFFFFFu;
+                for (uint32_t w = 0; w < wv; ++w) pm = op_min(pm, sh.cgm[w]);
+                const uint32_t me = op_min(pm, mex);
+                const int64_t M = me == 0xFFFFFFFFu ? 0 : ((int64_t)me - 0x40000000LL < 0 ? (int64_t)me - 0x40000000LL : 0);
+                g = W >= M;
+            } else if (use) {
+                const DRule& r = sh.rules[0];
+                const RState& st = ((sh.has_sync >> 0) & 1) ? sh.syn[0] : sh.rs[0];
+                const int64_t cost = rl_cost(r, st, 1);
+                const int64_t L = sh.rs[0].c, mq = r.max_queue;
+                auto q = [&](int64_t tt) -> int64_t {
+                    const int64_t d = tt - L + mq;
+                    return (d < 0 || cost <= 0) ? 0 : d / cost;
+                };
+                const uint32_t pv = shr1(ix, 0u);                  // previous in-round ENTRY's time (+1), 0: none
+                const uint32_t pprev = op_max(px, pv);
+                const int64_t qe = q(t0 + ev[0].dt);
+                const int64_t qp = pprev ? q(t0 + dlo + (int64_t)pprev - 1) : 0;
+                g = cost > 0 && r.count > 0 ? qe > qp : r.count > 0;
+            }
+            if (use && a) {
+                gg[0] = g ? (uint32_t)nr : 0u;
+                win[(tbase + lp0) & (WIN - 1)] = g ? 1 : 0;
+            }
+            lds_barrier();  // the statuses the guesses imply, before the iteration reads them
         }
 
         // ================= Jacobi iteration =================
