@@ -72,7 +72,9 @@ typedef struct sg_config {
     int32_t device;              /* HIP device ordinal this engine owns */
     uint32_t max_resources;      /* capacity of the resource table (dense ids 0..max-1) */
     uint32_t max_rules;          /* capacity of the compiled rule table (all kinds) */
-    uint32_t param_table_log2;   /* (rule,value) hash-table slots = 2^log2 */
+    uint32_t param_table_log2;   /* cap on the hot-parameter map pool: the bucket slots of every ParameterMetric
+                                    CacheMap together (~2x each map's LRU capacity, 32 B a slot) <= 2^log2;
+                                    rule loads past it fail SG_ECAPACITY.  Default 28 */
     uint32_t status_ring_log2;   /* entry-status ring for EXIT/TRACE references = 2^log2 events */
     uint32_t max_batch_events;   /* largest n accepted by sg_submit */
     /* token server (csrv/server/config/ServerFlowConfig.java:26-31) */

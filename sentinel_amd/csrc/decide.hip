@@ -603,7 +603,9 @@ __device__ void aux_stat(const DevState& S, const DevCfg& cfg, uint32_t res, uin
 
 enum { SEL_NONE = 0, SEL_CLUSTER = 1, SEL_ORIGIN = 2, SEL_DEFAULT = 3, SEL_RELATE = 4 };
 // FlowRuleChecker.selectNodeByRequesterAndStrategy / selectReferenceNode (FlowRuleChecker.java:67-124)
-__device__ __forceinline__ int flow_select(const DRule& r, const EvX& x, const DRule* flows, int nf) {
+// "other" also excludes the limitApps of the resource's cluster-only rules, which compile to no check (their
+// origin ids ride in the rule's hot list, engine.cpp upload_rules)
+__device__ __forceinline__ int flow_select(const DRule& r, const EvX& x, const DRule* flows, int nf, const DHot* hot) {
     bool applies;
     if (r.la_kind == LA_DEFAULT) applies = true;
     else if (r.la_kind == LA_ORIGIN) applies = x.origin != 0 && x.origin == r.la_origin;
@@ -611,6 +613,8 @@ __device__ __forceinline__ int flow_select(const DRule& r, const EvX& x, const D
         applies = x.origin != 0;
         for (int k = 0; k < nf; ++k)
             if (flows[k].la_origin == x.origin) applies = false;
+        for (uint32_t k = 0; k < r.hot_n; ++k)
+            if ((uint32_t)hot[r.hot_off + k].key == x.origin) applies = false;
     }
     if (!applies) return SEL_NONE;
     if (r.strategy == SG_STRATEGY_RELATE) return r.ref == NO_REF ? SEL_CLUSTER : SEL_RELATE;
@@ -712,7 +716,7 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                 else wait += w;
             } else if (s < nfl) {  // FlowSlot.checkFlow (FlowSlot.java:146-158)
                 if (s == np && (fl & SG_F_BLOCKED_UPSTREAM)) { status = ST_BLOCK_UPSTREAM; slot = 0; continue; }
-                const int sel = flow_select(r, x, rules + np, pg.n_flow);
+                const int sel = flow_select(r, x, rules + np, pg.n_flow, S.hot);
                 if (sel == SEL_NONE) continue;
                 int rc;
                 int64_t w = 0;

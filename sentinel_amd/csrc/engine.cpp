@@ -742,6 +742,14 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
         // flow rules: FlowRuleComparator order; limitApp and strategy pick the node each rule checks
         // (FlowRuleChecker.selectNodeByRequesterAndStrategy, FlowRuleChecker.java:90-124)
         const auto& fl = r < e->res_flow.size() ? e->res_flow[r] : std::vector<int>();
+        // FlowRuleManager.isOtherOrigin reads every rule of the resource, the cluster-only ones included
+        std::vector<uint32_t> skipped_origins;
+        for (size_t i = 0; i < fl.size(); ++i) {
+            const FlowR& f = e->flows[fl[i]];
+            if (!(f.r.cluster_mode && !f.r.cluster_fallback_to_local) || f.la == "default" || f.la == "other") continue;
+            auto oi = e->origin_ids.find(f.la);
+            if (oi != e->origin_ids.end()) skipped_origins.push_back(oi->second);
+        }
         for (size_t i = 0; i < fl.size(); ++i) {
             const FlowR& f = e->flows[fl[i]];
             if (f.r.cluster_mode && !f.r.cluster_fallback_to_local) continue; // no TokenService -> pass
@@ -758,6 +766,11 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             d.la_kind = f.la == "default" ? LA_DEFAULT : f.la == "other" ? LA_OTHER : LA_ORIGIN;
             auto oi = e->origin_ids.find(f.la);
             d.la_origin = oi == e->origin_ids.end() ? NO_ID : oi->second;
+            if (d.la_kind == LA_OTHER && !skipped_origins.empty()) {
+                d.hot_off = (uint32_t)hot.size();
+                d.hot_n = (uint32_t)skipped_origins.size();
+                for (uint32_t o : skipped_origins) hot.push_back(DHot{o, 0, 0});
+            }
             d.strategy = (uint32_t)f.r.strategy;
             d.chain_ctx = NO_ID;
             if (f.r.strategy == SG_STRATEGY_RELATE) {  // another resource's ClusterNode (same node if itself)

@@ -42,6 +42,9 @@ def _rules(n_res):
         elif k == 2:
             flow += [A.flow_rule(nm, 3, limit_app="other"), A.flow_rule(nm, 2, limit_app="appB",
                                                                         grade=A.FLOW_GRADE_THREAD)]
+            if i % 12 == 2:  # a cluster-only rule checks nothing but still names appC: not "other"
+                flow.append(A.flow_rule(nm, 1, limit_app="appC", cluster_mode=True, cluster_flow_id=2000 + i,
+                                        cluster_fallback_to_local=False))
         elif k == 3:
             flow += [A.flow_rule(nm, 5, strategy=A.STRATEGY_CHAIN, ref_resource="ctxA"),
                      A.flow_rule(nm, 8, limit_app="appA", strategy=A.STRATEGY_CHAIN, ref_resource="ctxB",
