@@ -136,8 +136,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const uint32_t m = *mp;  // segment count (the grid covers an upper bound: no host round trip)
-    // k_pq runs in batches without sg_submit_ex context/args and without EXITs that release thread counts
-    const bool pq = pq_ok && !force_lane && !(*bflags & BF_EXIT_ARGS);
+    // k_pq runs in batches without sg_submit_ex context/args
+    const bool pq = pq_ok && !force_lane;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < m) {
         Seg sg = segs[s];

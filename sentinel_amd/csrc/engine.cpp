@@ -842,14 +842,20 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || d.grade != SG_FLOW_GRADE_QPS) all_default_qps = false;
             }
             if (all_default_qps) p.pflags |= PF_FROZEN;
-            // k_pq (param.hip): QPS-grade param rules with a fixed paramIdx and LDS-sized rings, nothing else
+            // k_pq (param.hip): param rules with a fixed paramIdx and LDS-sized rings, nothing else; QPS-grade
+            // rules, and at most one THREAD-grade rule on paramIdx 0 checked last (its check and the entry's
+            // thread-count increment are one access of the thread-count map)
             bool pq = p.n_param >= 1 && p.n_param <= 4 && p.n_flow == 0 && p.n_degrade == 0 && !p.multi;
+            int last_checked = -1, n_thread = 0, thread_at = -1;
             for (int i = 0; i < p.n_param && pq; ++i) {
                 const DRule& d = rules[p.rule_off + i];
                 if (d.param_idx < 0) pq = false;
                 else if (d.behavior == PB_INIT_ONLY) continue;
+                else if (d.grade == SG_FLOW_GRADE_THREAD && d.param_idx == 0) { ++n_thread; thread_at = i; last_checked = i; }
                 else if (d.grade != SG_FLOW_GRADE_QPS || rule_map_cap(d.duration_sec) > 4080) pq = false;
+                else last_checked = i;
             }
+            if (n_thread > 1 || (n_thread == 1 && thread_at != last_checked)) pq = false;
             if (pq) p.pflags |= PF_PQ;
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
         }

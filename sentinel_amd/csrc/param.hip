@@ -67,6 +67,7 @@ struct PqSh {
     uint32_t red[NW][8];
     int64_t red64[NW][2];
     uint32_t flags_or, npend;
+    uint32_t freach;                // segment position + 1 of the tile's first ENTRY reaching rule k0
     uint64_t pend_key[PQ_NPEND];
     int64_t pend_stamp[PQ_NPEND];
     PData pend_dat[PQ_NPEND];
@@ -189,22 +190,132 @@ __device__ void pq_sort(PqSh<NW>& sh, uint32_t P) {
 }
 
 enum { PW_TOKEN = 0, PW_THROTTLE = 1, PW_COUNT = 2 };
+// thread-count map operations of a tile event (PW_COUNT; tkx bits 24-26), ParameterMetric.java:117-241:
+//   OP_ADD   addThreadCount of a passed ENTRY: putIfAbsent(v, 0) then increment, or put(v, 1) when absent;
+//   OP_CHK   a THREAD-grade rule's check (ParamFlowChecker.java:101-119): get(v) (a touch if present), pass iff
+//            count + 1 <= threshold, then OP_ADD for the entry that passed (the rule is the resource's last);
+//   OP_SUB   decreaseThreadCount of an EXIT: putIfAbsent(v, 0) -- an absent value stays at 0 -- else decrement,
+//            removed at <= 0;
+//   OP_SUBC  OP_SUB iff the referenced ENTRY (same tile, same key) passed its OP_CHK.
+enum { OP_NONE = 0, OP_ADD = 1, OP_CHK = 2, OP_SUB = 3, OP_SUBC = 4 };
+#define TV_BLOCK 1u      // walk verdict: blocked
+#define TV_HIT 4u        // leader event: its key was resident at its first access
+#define TV_INS 0x100u    // the access inserted its key
+#define TV_REM 0x200u    // the access removed its key
+#define GS_PRES 0x80000000u
+#define GS_TOUCH 0x40000000u
+#define GS_CNT 0x3FFFFFFFu
+
+__device__ __forceinline__ uint32_t pq_op(uint32_t kx) { return (kx >> 24) & 7u; }
+
+// the threshold of a THREAD-grade rule for value v: its hot item, else (long) count
+__device__ __forceinline__ int64_t pq_thread_thr(const DevState& S, const DRule* r, uint64_t v) {
+    for (uint32_t i = 0; i < r->hot_n; ++i) {
+        const DHot h = S.hot[r->hot_off + i];
+        if (h.key == v) return (int64_t)h.count;
+    }
+    return j_d2l(r->count);
+}
+
+// one access of a thread-count map by the state machine of its op; returns TV_* bits
+__device__ __forceinline__ uint32_t pq_count_op(uint32_t op, bool& pres, int64_t& c, int64_t thr) {
+    if (op == OP_ADD || op == OP_CHK) {
+        if (op == OP_CHK && (pres ? c : 0) + 1 > thr) return TV_BLOCK;  // the get only
+        if (pres) { ++c; return 0; }
+        pres = true; c = 1;
+        return TV_INS;
+    }
+    if (op == OP_SUB) {
+        if (!pres) { pres = true; c = 0; return TV_INS; }
+        if (--c <= 0) { pres = false; c = 0; return TV_REM; }
+    }
+    return 0;
+}
+
+// Exact sequential residency of one thread-count map's tile (one lane, in LDS): ops in tile order, each
+// insertion beyond cap evicting the oldest untouched key (the lowest live ring bit).  An access touches its key
+// (moves it to the MRU end) unless it does nothing: an EXIT whose ENTRY was blocked, a blocked check of an absent
+// value.  Taken only when the no-eviction hypothesis fails.  Leaves on every group leader whether the key was
+// resident at the group's first touching access (TV_HIT), the touched / evicted keys' ring bits cleared, and
+// returns the map's size at the tile end.
+template <int NW>
+__device__ __noinline__ uint32_t pq_count_seq(PqSh<NW>& sh, int mk, const DRule* r, const DevState& S, uint32_t tbase) {
+    PMap& m = sh.hdr[mk];
+    const int64_t RB = (int64_t)1 << m.rb_log2;
+    const uint32_t W = (uint32_t)(RB >> 6);
+    const uint32_t w0 = ring_word(m, m.thr);
+    uint64_t* bm = sh.bm[mk];
+    int64_t size = m.live;
+    uint32_t kw = 0;
+    for (uint32_t e = 0; e < PqSh<NW>::TE; ++e) {
+        uint32_t op = pq_op(sh.tkx[e]);
+        if (op == OP_NONE) continue;
+        const uint32_t g = (uint32_t)sh.lrank[e];
+        const uint32_t gs = sh.tdec[g];
+        const bool touched = (gs & GS_TOUCH) != 0;
+        bool pres, live_bit = false;
+        int64_t c;
+        const int64_t st = (int64_t)sh.tkey[g];
+        if (!touched) {  // resident iff its ring bit survived the evictions so far
+            live_bit = st >= 0 && ring_live(m, bm, st);
+            pres = live_bit;
+            c = pres ? (int64_t)(gs & GS_CNT) : 0;
+        } else {
+            pres = (gs & GS_PRES) != 0;
+            c = (int64_t)(gs & GS_CNT);
+        }
+        if (op == OP_SUBC) op = (sh.tver[sh.tx[e] - tbase] & TV_BLOCK) ? OP_NONE : OP_SUB;
+        const bool pb = pres;
+        const uint32_t v = pq_count_op(op, pres, c, op == OP_CHK ? pq_thread_thr(S, r, sh.skey[g]) : 0);
+        sh.tver[e] = (sh.tver[e] & TV_HIT) | v;
+        const bool t_now = op != OP_NONE && (pb || (v & TV_INS));
+        if (t_now && !touched) {
+            if (live_bit) {
+                const uint64_t p = (uint64_t)st & (uint64_t)(RB - 1);
+                bm[p >> 6] &= ~(1ull << (p & 63));
+            }
+            if (pb) sh.tver[sh.sidx[g]] |= TV_HIT;  // read by the leader's walk
+        }
+        if (v & TV_INS) ++size;
+        if (v & TV_REM) --size;
+        if (size > (int64_t)m.cap) {  // evict the oldest untouched key
+            while (kw < W) {
+                const uint32_t w = (w0 + kw) & (W - 1);
+                const uint64_t x = bm[w];
+                if (x) { bm[w] = x & (x - 1); break; }
+                ++kw;
+            }
+            --size;
+        }
+        if (touched || t_now) sh.tdec[g] = (pres ? GS_PRES : 0u) | GS_TOUCH | ((uint32_t)c & GS_CNT);
+    }
+    return (uint32_t)size;
+}
 
 // One map's accesses of the tile (acc[e] for the lane's events e = tid * PQ_EPL + q): residency, the walk of
-// every key group (WALK), commit.  Verdicts of rule walks land in sh.tver[e]: 0 pass | wait << 16, 1 block.
+// every key group (WALK), commit.  Verdicts of the walks land in sh.tver[e]: TV_BLOCK | wait << 16.
+// tbase: segment position of the tile's first event (OP_SUBC references).
 template <int NW>
 __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const DRule* r, const DevState& S, int64_t t0,
-                             const bool (&acc)[PQ_EPL], uint32_t* bflags) {
+                                          uint32_t tbase, const bool (&acc)[PQ_EPL], uint32_t* bflags,
+                                          bool force_seq = false) {
     constexpr uint32_t HW = PqSh<NW>::HW;
     constexpr uint32_t SP = PqSh<NW>::TE / HW;  // sorted positions per lane
     const uint32_t tid = threadIdx.x;
     // (a) accesses before each event, in tile order
     uint32_t la = 0;
+    bool rm_l = false;
 #pragma unroll
-    for (int q = 0; q < PQ_EPL; ++q) la += acc[q] ? 1u : 0u;
+    for (int q = 0; q < PQ_EPL; ++q) {
+        la += acc[q] ? 1u : 0u;
+        if (acc[q] && walk == PW_COUNT && pq_op(sh.tkx[tid * PQ_EPL + q]) != OP_ADD) rm_l = true;
+    }
     uint32_t na;
     uint32_t a0 = pq_scan<NW>(sh, la, &na);
     if (na == 0) return;  // uniform
+    // a thread-count tile with gets or decrements: residency by the no-eviction hypothesis, verified after the
+    // walks (the rank rule below counts every first access as an insertion and knows no removals)
+    const bool rmode = __syncthreads_or(rm_l) != 0;
 #pragma unroll
     for (int q = 0; q < PQ_EPL; ++q) {
         const uint32_t e = tid * PQ_EPL + q;
@@ -271,7 +382,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     __syncthreads();
     // (c) residency of every first access: the upper bound r + (first accesses before it) settles it unless the key
     // is near the LRU end; then the exact count of the earlier first accesses of keys older than it
-    {
+    if (!rmode) {
         uint32_t lf = 0;
 #pragma unroll
         for (int q = 0; q < PQ_EPL; ++q) lf += sh.lrank[tid * PQ_EPL + q] != RANK_REP ? 1u : 0u;
@@ -284,114 +395,180 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
             if (rk == RANK_REP) continue;
             uint32_t hit = 0;
             if (rk != RANK_NEW) {
-                if ((uint32_t)rk + F < cap) hit = 1;
+                if ((uint32_t)rk + F < cap) hit = TV_HIT;
                 else {
                     uint32_t d = (uint32_t)rk;
                     for (uint32_t j = 0; j < e && d < cap; ++j) {
                         const int32_t x = sh.lrank[j];
                         if (x != RANK_REP && x > rk) ++d;
                     }
-                    hit = d < cap ? 1u : 0u;
+                    hit = d < cap ? TV_HIT : 0u;
                 }
             }
             sh.tver[e] = hit;  // leader residency, read by the group's walker
             ++F;
         }
-    }
-    __syncthreads();
-    // (d) walks: one lane per key group, its accesses in tile order
-    uint32_t gend[SP];
-    PData gfin[SP];
-    bool ghit[SP];
+    } else {
 #pragma unroll
-    for (uint32_t q = 0; q < SP; ++q) {
-        const uint32_t s = tid + q * HW;
-        gend[q] = s;
-        gfin[q] = gd[q];
-        ghit[q] = false;
-        if (!glead[q]) continue;
-        const uint32_t e0 = sh.sidx[s];
-        ghit[q] = sh.tver[e0] != 0;
-        const uint64_t key = sh.skey[s];
-        uint32_t send = s + 1;
-        while (send < na && sh.skey[send] == key) ++send;
-        gend[q] = send;
-        PData st = gd[q];
-        int64_t tcl = 0;
-        int32_t maxc = 0;
-        if (walk != PW_COUNT) {  // the value's token count: its hot item, else (int) / (long) count
-            bool hf = false;
-            int32_t hc = 0;
-            for (uint32_t i = 0; i < r->hot_n; ++i) {
-                const DHot h = S.hot[r->hot_off + i];
-                if (h.key == key) { hf = true; hc = h.count; break; }
-            }
-            tcl = hf ? (int64_t)hc : (walk == PW_THROTTLE ? r->token_count_l : (int64_t)r->token_count);
-            maxc = j_iadd((int32_t)tcl, r->burst);
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q;
+            const int32_t rk = sh.lrank[e];
+            if (rk != RANK_REP) sh.tver[e] = rk != RANK_NEW ? TV_HIT : 0u;
         }
-        const int64_t dur_ms = r ? r->duration_sec * 1000 : 0;
-        bool first_miss = !ghit[q];
-        for (uint32_t p = s; p < send; ++p) {
-            const uint32_t e = sh.sidx[p];
-            const int64_t t = t0 + sh.tdt[e];
-            const int acq = (int)(sh.tcz[e] & 0xFFFFu);
-            uint32_t v = 0;
-            if (walk == PW_COUNT) {
-                st.v0 = first_miss ? 1 : st.v0 + 1;
-            } else if (walk == PW_THROTTLE) {  // passThrottleLocalCheck (ParamFlowChecker.java:198-248)
-                if (first_miss) {
-                    st.v0 = t;
-                } else {
-                    const int64_t cost = j_round(1.0 * 1000 * acq * (double)r->duration_sec / (double)tcl);
-                    const int64_t expected = st.v0 + cost;
-                    if (expected <= t || expected - t < r->max_queue) {
-                        const int64_t w = expected - t;
-                        st.v0 = w > 0 ? expected : t;
-                        if (w > 0) v = (uint32_t)(w > 0xFFFF ? 0xFFFF : w) << 16;
-                    } else {
-                        v = 1;
-                    }
-                }
-            } else {  // passDefaultLocalCheck (ParamFlowChecker.java:121-196)
-                if (first_miss) {
-                    st.v0 = t;
-                    st.v1 = j_iadd(maxc, -acq);
-                } else {
-                    const int64_t pass_time = t - st.v0;
-                    if (pass_time > dur_ms) {
-                        const int32_t to_add = (int32_t)((pass_time * tcl) / dur_ms);
-                        const int32_t sum = j_iadd(st.v1, to_add);
-                        const int32_t nq = sum > maxc ? j_iadd(maxc, -acq) : j_iadd(sum, -acq);
-                        if (nq < 0) v = 1;
-                        else { st.v1 = nq; st.v0 = t; }
-                    } else if (j_iadd(st.v1, -acq) >= 0) {
-                        st.v1 = j_iadd(st.v1, -acq);
-                    } else {
-                        v = 1;
-                    }
-                }
-            }
-            first_miss = false;
-            sh.tver[e] = v;
-        }
-        gfin[q] = st;
     }
     __syncthreads();
+    // (d) walks: one lane per key group, its accesses in tile order; a thread-count tile that fails the
+    // no-eviction check is replayed by pq_count_seq and walked again with its residencies
+    uint32_t gend[SP], glast[SP];
+    PData gfin[SP];
+    bool gpres[SP], gtouch[SP];
+    int mode = rmode ? 1 : 0;  // 0: rank rule, 1: no-eviction hypothesis (verified), 2: sequential replay
+    uint32_t seq_size = 0;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (uint32_t q = 0; q < SP; ++q) {
+            const uint32_t s = tid + q * HW;
+            gend[q] = s;
+            gfin[q] = gd[q];
+            gpres[q] = false;
+            gtouch[q] = false;
+            glast[q] = 0;
+            if (!glead[q]) continue;
+            const uint32_t e0 = sh.sidx[s];
+            const bool ghit = (sh.tver[e0] & TV_HIT) != 0;
+            const uint64_t key = sh.skey[s];
+            uint32_t send = s + 1;
+            while (send < na && sh.skey[send] == key) ++send;
+            gend[q] = send;
+            PData st = gd[q];
+            if (walk == PW_COUNT) {
+                bool pres = ghit;
+                int64_t c = ghit ? gd[q].v0 : 0;
+                const int64_t thr = r ? pq_thread_thr(S, r, key) : 0;
+                for (uint32_t p = s; p < send; ++p) {
+                    const uint32_t e = sh.sidx[p];
+                    uint32_t op = pq_op(sh.tkx[e]);
+                    if (op == OP_SUBC) op = (sh.tver[sh.tx[e] - tbase] & TV_BLOCK) ? OP_NONE : OP_SUB;
+                    const bool pb = pres;
+                    const uint32_t v = pq_count_op(op, pres, c, thr);
+                    sh.tver[e] = v;
+                    if (op != OP_NONE && (pb || (v & TV_INS))) { gtouch[q] = true; glast[q] = e; }
+                    if (rmode) sh.lrank[e] = (int32_t)s;  // the event's group (pq_count_seq)
+                }
+                st.v0 = c;
+                gpres[q] = pres;
+                gfin[q] = st;
+                continue;
+            }
+            gpres[q] = true;
+            gtouch[q] = true;
+            glast[q] = sh.sidx[send - 1];
+            int64_t tcl = 0;
+            int32_t maxc = 0;
+            {   // the value's token count: its hot item, else (int) / (long) count
+                bool hf = false;
+                int32_t hc = 0;
+                for (uint32_t i = 0; i < r->hot_n; ++i) {
+                    const DHot h = S.hot[r->hot_off + i];
+                    if (h.key == key) { hf = true; hc = h.count; break; }
+                }
+                tcl = hf ? (int64_t)hc : (walk == PW_THROTTLE ? r->token_count_l : (int64_t)r->token_count);
+                maxc = j_iadd((int32_t)tcl, r->burst);
+            }
+            const int64_t dur_ms = r->duration_sec * 1000;
+            bool first_miss = !ghit;
+            for (uint32_t p = s; p < send; ++p) {
+                const uint32_t e = sh.sidx[p];
+                const int64_t t = t0 + sh.tdt[e];
+                const int acq = (int)(sh.tcz[e] & 0xFFFFu);
+                uint32_t v = 0;
+                if (walk == PW_THROTTLE) {  // passThrottleLocalCheck (ParamFlowChecker.java:198-248)
+                    if (first_miss) {
+                        st.v0 = t;
+                    } else {
+                        const int64_t cost = j_round(1.0 * 1000 * acq * (double)r->duration_sec / (double)tcl);
+                        const int64_t expected = st.v0 + cost;
+                        if (expected <= t || expected - t < r->max_queue) {
+                            const int64_t w = expected - t;
+                            st.v0 = w > 0 ? expected : t;
+                            if (w > 0) v = (uint32_t)(w > 0xFFFF ? 0xFFFF : w) << 16;
+                        } else {
+                            v = TV_BLOCK;
+                        }
+                    }
+                } else {  // passDefaultLocalCheck (ParamFlowChecker.java:121-196)
+                    if (first_miss) {
+                        st.v0 = t;
+                        st.v1 = j_iadd(maxc, -acq);
+                    } else {
+                        const int64_t pass_time = t - st.v0;
+                        if (pass_time > dur_ms) {
+                            const int32_t to_add = (int32_t)((pass_time * tcl) / dur_ms);
+                            const int32_t sum = j_iadd(st.v1, to_add);
+                            const int32_t nq = sum > maxc ? j_iadd(maxc, -acq) : j_iadd(sum, -acq);
+                            if (nq < 0) v = TV_BLOCK;
+                            else { st.v1 = nq; st.v0 = t; }
+                        } else if (j_iadd(st.v1, -acq) >= 0) {
+                            st.v1 = j_iadd(st.v1, -acq);
+                        } else {
+                            v = TV_BLOCK;
+                        }
+                    }
+                }
+                first_miss = false;
+                sh.tver[e] = v;
+            }
+            gfin[q] = st;
+        }
+        __syncthreads();
+        if (mode != 1) break;
+        // the hypothesis holds iff the map's size, live0 + insertions - removals so far, never exceeds cap
+        int32_t run = 0, lmax = 0;
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t v = sh.tver[tid * PQ_EPL + q];
+            if (acc[q]) run += ((v & TV_INS) ? 1 : 0) - ((v & TV_REM) ? 1 : 0);
+            lmax = run > lmax ? run : lmax;
+        }
+        uint32_t tot;
+        const int32_t pre = (int32_t)pq_scan<NW>(sh, (uint32_t)run, &tot);
+        const int32_t peak = (int32_t)live0 + pre + lmax;
+        if (!force_seq && __syncthreads_or(peak > (int32_t)cap) == 0) break;  // (force_seq: SG_DEBUG_FLAGS 32)
+        // replay: per group its stamp (or -1) and count in LDS, then one lane in tile order
+#pragma unroll
+        for (uint32_t q = 0; q < SP; ++q) {
+            if (!glead[q]) continue;
+            const uint32_t s = tid + q * HW;
+            sh.tkey[s] = glive[q] ? (uint64_t)gst[q] : ~0ull;
+            sh.tdec[s] = glive[q] ? (uint32_t)(gd[q].v0 < 0 ? 0 : gd[q].v0 > (int64_t)GS_CNT ? GS_CNT : gd[q].v0) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) sh.tver[tid * PQ_EPL + q] = 0;
+        __syncthreads();
+        if (tid == 0) sh.red64[0][0] = (int64_t)pq_count_seq<NW>(sh, mk, r, S, tbase);
+        __syncthreads();
+        seq_size = (uint32_t)sh.red64[0][0];
+        __syncthreads();
+        mode = 2;
+    }
     // (e) commit: touched keys leave their old stamp; the oldest untouched keys beyond cap are evicted
     uint32_t nnew = 0;
 #pragma unroll
     for (uint32_t q = 0; q < SP; ++q) {
         if (!glead[q]) continue;
-        if (glive[q]) {
+        if (glive[q] && gtouch[q]) {  // an untouched key keeps its place
             const uint64_t p = (uint64_t)gst[q] & (uint64_t)(RB - 1);
             atomicAnd(reinterpret_cast<unsigned long long*>(&sh.bm[mk][p >> 6]), ~(1ull << (p & 63)));
-        } else {
-            ++nnew;
         }
+        if (mode == 0) nnew += glive[q] ? 0u : 1u;
+        else nnew += (glive[q] && gtouch[q] ? 1u : 0u) | (gtouch[q] && gpres[q] ? 0x10000u : 0u);
     }
     uint32_t ntot;
     (void)pq_scan<NW>(sh, nnew, &ntot);  // (barrier: the cleared bits are in place)
-    const uint32_t E = live0 + ntot > cap ? live0 + ntot - cap : 0u;
+    const uint32_t E = mode == 0 && live0 + ntot > cap ? live0 + ntot - cap : 0u;
+    const uint32_t live1 = mode == 0 ? live0 + ntot - E
+                         : mode == 1 ? live0 - (ntot & 0xFFFFu) + (ntot >> 16) : seq_size;
     if (E) {
         const uint32_t w0 = ring_word(m, m.thr);
         const uint32_t w = (w0 + tid) & (W - 1);
@@ -407,15 +584,16 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     }
     for (uint32_t i = tid; i < PQ_CLW; i += HW) sh.claim[i] = 0;
     __syncthreads();
-    // new stamps: the group's last access; keys with a slot (live or dead) keep it
+    // new stamps: the group's last access; keys with a slot (live or dead) keep it; a key removed by the tile
+    // keeps its slot with a dead stamp
     bool need[SP];
     int64_t gns[SP];
 #pragma unroll
     for (uint32_t q = 0; q < SP; ++q) {
         need[q] = false;
         gns[q] = 0;
-        if (!glead[q]) continue;
-        gns[q] = clock0 + (int64_t)sh.tA[sh.sidx[gend[q] - 1]];
+        if (!glead[q] || !gpres[q] || !gtouch[q]) continue;
+        gns[q] = clock0 + (int64_t)sh.tA[glast[q]];  // the group's last touching access
         const uint64_t p = (uint64_t)gns[q] & (uint64_t)(RB - 1);
         atomicOr(reinterpret_cast<unsigned long long*>(&sh.bm[mk][p >> 6]), 1ull << (p & 63));
         if (gslot[q] >= 0) {
@@ -429,7 +607,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     }
     if (tid == 0) {
         m.clock = clock0 + (int64_t)na;
-        m.live = live0 + ntot - E;
+        m.live = live1;
         sh.npend = 0;
     }
     __syncthreads();
@@ -629,7 +807,8 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     const uint32_t tm = (pg.tm_base == NO_ID) ? NO_ID : S.tmid[pg.tm_base];
     if (tid <= PQ_MAXP) {
         uint32_t id = NO_ID;
-        if ((int)tid < np && sh.rules[tid].behavior != PB_INIT_ONLY) id = sh.rules[tid].pmap;
+        if ((int)tid < np && sh.rules[tid].behavior != PB_INIT_ONLY && sh.rules[tid].grade == SG_FLOW_GRADE_QPS)
+            id = sh.rules[tid].pmap;
         if (tid == PQ_MAXP) id = tm;
         sh.mid[tid] = id;
         if (id != NO_ID) sh.hdr[tid] = S.pmap[id];
@@ -657,7 +836,18 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         else if (r.param_idx < SG_MAX_ARGS) all_bits |= ni_tm((uint32_t)r.param_idx);
     }
     const bool tm_on = tm != NO_ID && ((sh.node.flags | all_bits) & ni_tm(0)) != 0;
-    __syncthreads();
+    // the THREAD-grade rule (at most one, the last checked, paramIdx 0: engine.cpp PF_PQ) and the first rule whose
+    // visit sets the paramIdx-0 thread-map bit; an EXIT decrements only once NI_PM and that bit are set
+    int tk = -1, k0 = -1;
+    for (int k = 0; k < np; ++k) {
+        const DRule& r = sh.rules[k];
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_THREAD) tk = k;
+        const uint32_t b = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
+                           : (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
+        if (k0 < 0 && (b & ni_tm(0))) k0 = k;
+    }
+    // EXITs at segment positions >= tm_from release thread counts (uniform)
+    uint32_t tm_from = ((sh.node.flags & (NI_PM | ni_tm(0))) == (NI_PM | ni_tm(0))) ? 0u : 0xFFFFFFFFu;
 
     for (uint32_t tb = 0; tb < sg.len; tb += TE) {
         // ---- 1. the tile's events
@@ -678,17 +868,24 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         }
         __syncthreads();
         // ---- 2. ParamFlowSlot: the rules in order
+        if (tid == 0) sh.freach = 0xFFFFFFFFu;
+        __syncthreads();
         for (int k = 0; k < np; ++k) {
             const DRule& r = sh.rules[k];
             bool reach = false;
 #pragma unroll
-            for (int q = 0; q < PQ_EPL; ++q) reach |= (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY && st[q] == 0;
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const bool rq = (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY && st[q] == 0;
+                reach |= rq;
+                if (rq && k == k0 && tb + tid * PQ_EPL + q < sg.len) atomicMin(&sh.freach, tb + tid * PQ_EPL + q + 1);
+            }
             if (reach) {
                 const uint32_t bits = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
                                       : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
                 atomicOr(&sh.flags_or, bits | NI_PM);
             }
             if (r.behavior == PB_INIT_ONLY || r.param_idx != 0) continue;  // no check (idx >= args.length)
+            if (r.grade != SG_FLOW_GRADE_QPS) continue;                     // the THREAD rule: phase 3
             const int walk = r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ? PW_THROTTLE : PW_TOKEN;
             bool acc[PQ_EPL];
 #pragma unroll
@@ -713,7 +910,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                 }
                 acc[q] = true;
             }
-            pq_map_phase<NW>(sh, k, walk, &r, S, t0, acc, bflags);
+            pq_map_phase<NW>(sh, k, walk, &r, S, t0, sg.start + tb, acc, bflags);
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
                 if (!acc[q]) continue;
@@ -723,15 +920,63 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
             }
             __syncthreads();  // tver is rewritten by the next phase
         }
-        // ---- 3. ParamFlowStatisticEntryCallback.onPass: the thread-count map of paramIdx 0
+        // ---- 3. the thread-count map of paramIdx 0: the THREAD rule's checks (OP_CHK), else
+        // ParamFlowStatisticEntryCallback.onPass of the passed ENTRYs (OP_ADD), and the EXITs' releases
+        // (ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount of the ENTRY's argument, OP_SUB)
+        __syncthreads();  // every lane's atomicMin on freach is in
+        if (tm_from == 0xFFFFFFFFu) tm_from = sh.freach;  // uniform (LDS)
         if (tm_on) {
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) sh.tdec[tid * PQ_EPL + q] = st[q];
+            __syncthreads();
             bool acc[PQ_EPL];
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
-                const uint32_t kx = sh.tkx[tid * PQ_EPL + q];
-                acc[q] = (kx & 0xFFu) == SG_EV_ENTRY && ((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0;
+                const uint32_t e = tid * PQ_EPL + q, p = tb + e, kx = sh.tkx[e], kind = kx & 0xFFu;
+                uint32_t op = OP_NONE;
+                if (p < sg.len && kind == SG_EV_ENTRY) {
+                    if (((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0) op = tk >= 0 ? OP_CHK : OP_ADD;
+                } else if (p < sg.len && kind == SG_EV_EXIT && ((kx >> 8) & SG_F_EXIT_ARGS) && p >= tm_from
+                           && S.key_ring) {
+                    const uint32_t code = (kx >> 16) & 0xFFu;
+                    uint64_t ref = SG_REF_NONE;
+                    if (code == RC_PASSED) {
+                        ref = ev[vals[sg.start + p] & 0x7FFFFFFFu].aux & SG_REF_NONE;
+                        op = OP_SUB;
+                    } else if (code == RC_BATCH) {
+                        const uint32_t rel = sh.tx[e] - sg.start;
+                        if (rel < p) {
+                            ref = S.gbase + (vals[sh.tx[e]] & 0x7FFFFFFFu);
+                            if (rel >= tb) op = sh.tdec[rel - tb] != 0 ? OP_NONE : (tk >= 0 ? OP_SUBC : OP_SUB);
+                            else op = st_passed(ld32(&dec[sh.tx[e]]) & 0xFF) ? OP_SUB : OP_NONE;
+                        }
+                    }
+                    if (op != OP_NONE) {
+                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
+                        if (key == NO_KEY) op = OP_NONE;
+                        else sh.tkey[e] = key;
+                    }
+                }
+                sh.tkx[e] = (kx & 0x00FFFFFFu) | (op << 24);
+                acc[q] = op != OP_NONE;
             }
-            pq_map_phase<NW>(sh, PQ_MAXP, PW_COUNT, nullptr, S, t0, acc, bflags);
+            __syncthreads();
+            pq_map_phase<NW>(sh, PQ_MAXP, PW_COUNT, tk >= 0 ? &sh.rules[tk] : nullptr, S, t0, sg.start + tb, acc, bflags,
+                             (cfg.dbg_flags & 32) != 0);
+            if (tk >= 0) {
+#pragma unroll
+                for (int q = 0; q < PQ_EPL; ++q)
+                    if (pq_op(sh.tkx[tid * PQ_EPL + q]) == OP_CHK && (sh.tver[tid * PQ_EPL + q] & TV_BLOCK)) st[q] = (uint32_t)tk + 1;
+            }
+            __syncthreads();
+        } else if (tk >= 0) {  // no thread-count map: every count reads 0
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t e = tid * PQ_EPL + q, kx = sh.tkx[e];
+                if ((kx & 0xFFu) == SG_EV_ENTRY && ((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0 &&
+                    1 > pq_thread_thr(S, &sh.rules[tk], sh.tkey[e]))
+                    st[q] = (uint32_t)tk + 1;
+            }
         }
         // ---- 4. decisions
 #pragma unroll

@@ -130,9 +130,25 @@ def test_c4_minute_window_long_trace(batches, bin_mode):
     _run(4, batches=batches, n_entries=300_000, n_res=3_000, rate=2000.0)
 
 
-def test_c4_wide_keys_two_10bit_passes():
-    # 200k resources: 18-bit keys sort in two 10-bit radix passes (the 1M-resource bench layout)
+def test_c4_wide_keys_three_radix_passes():
+    # 200k resources: 18-bit keys take all three 8-bit radix passes of the group stage (as the 1M-resource
+    # bench layout does)
     _run(4, batches=2, n_entries=600_000, n_res=200_000)
+
+
+def test_switch_off_checks_nothing():
+    # Constants.ON = false (core/Constants.java:67): CtSph.entryWithPriority hands out an Entry with no
+    # chain (CtSph.java:130-133), so nothing is checked or counted; every entry is NO_CHECK on both sides
+    w = T.Workload(3, n_entries=200_000, n_res=5_000, variant=T.V_WARM_RL)
+    eng = _engine(max_resources=w.n_res, max_slot_chain_size=0, switch_on=0)
+    orc = O.Oracle(max_slot_chain_size=0, switch_on=0)
+    w.install(eng)
+    w.install(orc)
+    dg, do = _replay(w, eng, orc, 2)
+    _assert_same_decisions(dg, do, w.events)
+    ent = w.events["kind"] == A.EV_ENTRY
+    assert ((dg[ent] & 0xFF) == A.NO_CHECK).all()
+    _compare_nodes(w, eng, orc, _sample(w, k=50))
 
 
 def test_c5_param(bin_mode):

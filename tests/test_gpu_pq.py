@@ -1,11 +1,12 @@
 """The cooperative hot-parameter owner (sentinel_amd/csrc/param.hip k_pq) against the oracle.
 
-k_pq decides the segments of resources whose rules are QPS-grade ParamFlowRules (PF_PQ) a tile at a time: LRU
-residency of the CacheMaps from recency ranks, one lane per value group through the token bucket / throttle,
-statistics per 500 ms bucket.  These tests replay traces in which every such segment goes through it (batches
-without sg_submit_ex context and without exit(count, args)) and compare every decision and the ClusterNode
-windows with the event-sequential oracle (ParamFlowChecker.java:121-248, ParameterMetric.java:37-241,
-StatisticSlot.java:54-173).
+k_pq decides the segments of resources whose rules are ParamFlowRules (PF_PQ: QPS-grade rules, at most one
+THREAD-grade rule on paramIdx 0 checked last) a tile at a time: LRU residency of the CacheMaps from recency ranks,
+one lane per value group through the token bucket / throttle / thread count, the thread-count map's increments
+and exit(count, args) releases (with removals: a no-eviction hypothesis checked per tile, else a sequential
+replay), statistics per 500 ms bucket.  These tests replay traces in which every such segment goes through it
+(batches without sg_submit_ex context) and compare every decision and the ClusterNode windows with the
+event-sequential oracle (ParamFlowChecker.java:101-248, ParameterMetric.java:37-241, StatisticSlot.java:54-173).
 """
 import numpy as np
 import pytest
@@ -37,9 +38,12 @@ def _check(w, eng, orc, cuts, k_nodes=200):
 
 
 def test_pq_c5_survey_shape():
-    # 10k resources, one param rule each (count 5-50, burst 0-5, 1 s, 20 % throttle with
-    # maxQueue 100), values Zipf(1.1) over 10M keys; two batches of 2^23 events.  Every hot map fills and evicts.
-    w = T.Workload(5, n_res=10_000, n_entries=1 << 23, n_param_values=10_000_000)
+    # SURVEY.md §8(d) C5 as tools/config_bench.py runs it: 10k resources, one param rule each (count 5-50, burst
+    # 0-5, 1 s, 20 % throttle with maxQueue 100, a fifth THREAD grade), hot items, values Zipf(1.1) over 10M keys
+    # plus 50 % uniform, every EXIT releasing its argument; two batches of 2^23 events.  Every hot map fills and
+    # evicts.
+    w = T.Workload(5, n_res=10_000, n_entries=1 << 23, n_param_values=10_000_000,
+                   variant=T.V_HOT | T.V_UNIFORM | T.V_THREAD)
     ev = w.events
     eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=28, status_ring_log2=26,
                    max_batch_events=1 << 23)
@@ -50,12 +54,13 @@ def test_pq_c5_survey_shape():
 
 
 @pytest.mark.parametrize("wide", ["0", "1073741824"])
-@pytest.mark.parametrize("variant", ["hot", "uniform"])
+@pytest.mark.parametrize("variant", ["hot", "uniform", "thread"])
 def test_pq_variants(variant, wide, monkeypatch):
-    # hot items (per-value token counts, some 0: blocked without a map access) and uniform churn (a million
-    # distinct values); every segment on the 1024-lane owner (wide=0) or on the 256-lane one
+    # hot items (per-value token counts, some 0: blocked without a map access), uniform churn (a million
+    # distinct values), THREAD-grade rules with exits releasing their argument; every segment on the 1024-lane
+    # owner (wide=0) or on the 256-lane one
     monkeypatch.setenv("SG_PQ_WIDE", wide)
-    v = T.V_HOT if variant == "hot" else T.V_HOT | T.V_UNIFORM
+    v = {"hot": T.V_HOT, "uniform": T.V_HOT | T.V_UNIFORM, "thread": T.V_HOT | T.V_UNIFORM | T.V_THREAD}[variant]
     w = T.Workload(5, n_res=2_000, n_entries=600_000, n_param_values=2_000_000, variant=v)
     eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=26, status_ring_log2=24)
     orc = O.Oracle(max_slot_chain_size=0)
@@ -64,8 +69,8 @@ def test_pq_variants(variant, wide, monkeypatch):
     _check(w, eng, orc, np.linspace(0, len(w.events), 4).astype(np.int64))
 
 
-def _rules():
-    return [
+def _rules(thread_on_m3=False):
+    r = [
         # two checked rules on index 0 (token bucket with burst, then a throttle), hot items incl. a zero count
         A.param_rule("m0", 0, 3, burst_count=2, items=[("7", "long", 0), ("8", "long", 50)]),
         A.param_rule("m0", 0, 20, control_behavior=A.CONTROL_BEHAVIOR_RATE_LIMITER, max_queueing_time_ms=40),
@@ -75,58 +80,89 @@ def _rules():
         A.param_rule("m1", 0, 1, cluster_mode=True, cluster_flow_id=77),
         A.param_rule("m1", 0, 2),
         A.param_rule("m2", 0, 1, burst_count=1),
+        # THREAD grade alone (hot items: a zero and a large threshold)
+        A.param_rule("m4", 0, 2, grade=A.FLOW_GRADE_THREAD, items=[("3", "long", 0), ("4", "long", 40)]),
+        # QPS only: its thread-count map is kept by the releases and read once a THREAD rule arrives
+        A.param_rule("m3", 0, 30, burst_count=3),
     ]
+    if thread_on_m3:
+        r.append(A.param_rule("m3", 0, 3, grade=A.FLOW_GRADE_THREAD))
+    return r
 
 
-def _synthetic(seed, n, gbase, nres=3, nval=9000, t=T0):
-    # EXIT references name the ENTRY's global event index (batches are numbered consecutively)
+NAMES = ("m0", "m1", "m2", "m3", "m4")
+
+
+def _synthetic(seed, n, gbase, nres=5, nval=9000, t=T0, rt_max=30, exit_args=0.0):
+    # EXIT references name the ENTRY's global event index (batches are numbered consecutively); a fraction
+    # exit_args of the EXITs release their ENTRY's argument (Entry.exit(count, args))
     rng = np.random.default_rng(seed)
     ev = np.zeros(2 * n, dtype=A.EVENT_DTYPE)
     ts = t + np.sort(rng.integers(0, 6000, n))
     k = 0
     pend = []
+
+    def put_exit(tx, ref, rid):
+        nonlocal k
+        fl = A.F_EXIT_ARGS if rng.random() < exit_args else 0
+        ev[k] = (tx, rid, 1, A.EV_EXIT, fl, A.aux_exit(ref, 3))
+        k += 1
+
     for i in range(n):
         while pend and pend[0][0] <= ts[i]:
-            tx, ref, rid = pend.pop(0)
-            ev[k] = (tx, rid, 1, A.EV_EXIT, 0, A.aux_exit(ref, 3))
-            k += 1
+            put_exit(*pend.pop(0))
         rid = int(rng.integers(0, nres))
         v = int(rng.zipf(1.3)) if rng.random() < 0.6 else int(rng.integers(0, nval))
         flags = A.F_HAS_ARG if rng.random() < 0.97 else 0
         cnt = int(rng.choice([1, 1, 1, 2, 0, 6]))
         ev[k] = (ts[i], rid, cnt, A.EV_ENTRY, flags, E.param_key(str(v), "long"))
         if rng.random() < 0.5:
-            pend.append((int(ts[i]) + int(rng.integers(0, 30)), gbase + k, rid))
+            pend.append((int(ts[i]) + int(rng.integers(0, rt_max)), gbase + k, rid))
             pend.sort()
         k += 1
-    for tx, ref, rid in pend:
-        ev[k] = (tx, rid, 1, A.EV_EXIT, 0, A.aux_exit(ref, 3))
-        k += 1
+    for x in pend:
+        put_exit(*x)
     return ev[:k]
 
 
-def test_pq_rule_mix_and_alternating_paths():
+def _compare(eng, orc, ev, via_ext, what):
+    if via_ext:  # sg_submit_ex (an all-zero context/args table): the batch is the per-lane kernel's
+        ext = np.zeros(len(ev), dtype=A.EXT_DTYPE)
+        dg, do = eng.submit_ex(ev, ext), orc.submit_ex(ev, ext)
+    else:
+        dg, do = eng.submit(ev), orc.submit(ev)
+    bad = np.nonzero(dg != do)[0]
+    assert not len(bad), (what, "event", int(bad[0]), ev[bad[0]], hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+    return dg
+
+
+@pytest.mark.parametrize("rt_max", [30, 3000])
+def test_pq_rule_mix_thread_maps_and_alternating_paths(rt_max):
     # several param rules per resource, hot items, entries without an argument, zero and oversized acquires,
-    # > 4000 distinct values per resource (evictions inside and across tiles); batches alternate between k_pq and
-    # the per-lane kernel (an exit(count, args) sends a whole batch to k_lane): both work on the same maps
+    # > 4000 distinct values per resource (evictions inside and across tiles), exits releasing their argument;
+    # with rt_max = 3000 ms about 5000 values per resource are held at once, so the thread-count maps overflow
+    # while exits remove keys (the sequential replay).  Batches alternate between k_pq and the per-lane kernel
+    # (sg_submit_ex); both work on the same maps.  Then a THREAD rule is added on m3 and reads the thread-count
+    # map that m3's releases kept.
     eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=20, status_ring_log2=24)
     orc = O.Oracle(max_slot_chain_size=0)
-    for nm in ("m0", "m1", "m2"):
+    for nm in NAMES:
         assert eng.register(nm) == orc.register(nm)
     rules = _rules()
     assert eng.load_param_rules(rules) == orc.load_param_rules(rules)
     t, gbase = T0, 0
-    for b in range(6):
-        ev = _synthetic(100 + b, 30_000, gbase, t=t)
+    for b in range(7):
+        if b == 5:
+            rules = _rules(thread_on_m3=True)
+            assert eng.load_param_rules(rules) == orc.load_param_rules(rules)
+        ev = _synthetic(100 + b, 40_000, gbase, t=t, rt_max=rt_max, exit_args=0.9)
         gbase += len(ev)
-        if b % 2 == 1:  # one EXIT carries exit(count, args): this batch is the lane kernel's
-            ex = np.nonzero(ev["kind"] == A.EV_EXIT)[0][0]
-            ev["flags"][ex] |= A.F_EXIT_ARGS
-        dg, do = eng.submit(ev), orc.submit(ev)
-        bad = np.nonzero(dg != do)[0]
-        assert not len(bad), ("batch", b, "event", int(bad[0]), ev[bad[0]], hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+        d = _compare(eng, orc, ev, b % 3 == 1, "batch %d" % b)
+        if b >= 5:  # the THREAD rule on m3 blocks some of its entries
+            m3 = (ev["kind"] == A.EV_ENTRY) & (ev["res_id"] == NAMES.index("m3"))
+            assert int(((d[m3] & 0xFF) == A.BLOCK_PARAM).sum()) > 0
         t = int(ev["ts"].max()) + 1
-    for r in range(3):
+    for r in range(len(NAMES)):
         g, o = eng.read_node(r), orc.read_node(r)
         assert g["thread"] == o["thread"]
         np.testing.assert_array_equal(g["second"][:2], o["second"][:2])
