@@ -270,7 +270,7 @@ def main():
         barrier()
         elapsed += time.perf_counter() - t_start
         chunks += 1
-        stage_rows += eng.timing_log()  # per timed batch: [group, decide, post, total] device ms
+        stage_rows.extend(eng.timing_log().tolist())  # per timed batch: [group, decide, post, total] device ms
         entries += float(sum(p[2] for p in plan))
         touched += float(sum(p[3] for p in plan))
         events += float(sum(p[1] for p in plan))

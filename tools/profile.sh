@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-ARGS="--steps 2 --warmup 1 --sub-batches 2 --no-cpu-baseline"
+ARGS="--steps 2 --warmup 1 --sub-batches 2 --no-cpu-baseline --no-configs"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
