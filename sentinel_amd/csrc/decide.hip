@@ -1244,6 +1244,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR /* trip counts, 2 per word */ };
 
 #define NSPAN 64        // skipped spans per segment (LDS list for references into them)
+#define OPEN_EPL 4      // open stretches: events per lane per chunk of the 256-lane owner (2 for the others: 128-VGPR cap)
 
 template <int NW, int MF, int MD>
 struct JacSh {
@@ -1275,6 +1276,9 @@ struct JacSh {
     unsigned long long fl[NW]; // flagged-block ballots
     uint32_t cg[NW][3];        // closed-form guesses: per-wave totals (entries, effective exits | last entry time, others)
     uint32_t cgm[NW];          // ... per-wave minimum of the thread-grade admission bound
+    // open stretches: the stop's evaluated outcome and the RT breakers' segmented passCount state before it
+    uint32_t os_o;
+    uint32_t os_seg[MD];
 };
 
 // leader: fold the round's committed deltas into the node (StatisticSlot bookkeeping of every
@@ -1473,6 +1477,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     }
     const bool has_rt = (pg.pflags & PF_RT) != 0;
     const bool frozen_prog = (pg.pflags & PF_FROZEN) != 0;
+    // open stretches (all-pass prefix decisions, below): on unless debug flag 64; worth a chunk from one tile left
+    const bool open_on = !(cfg.dbg_flags & 64);
+    const uint32_t open_min = TILE;
     // single-stage programs with closed-form admission guesses (see the Jacobi iteration)
     const bool tg_mode = nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_THREAD &&
                          sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_DEFAULT && !(cfg.dbg_flags & 16);
@@ -1483,7 +1490,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     // diagnostics (SG_DEBUG=1): per-bin iteration counters; phase cycles of the bin's first segment
     // only in builds with -DSG_KPROF (the timers cost registers the 1024-lane kernel does not have)
     const bool prof = S.dbg != nullptr;
-    uint32_t n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0;
+    uint32_t n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0, n_opn = 0;
 #ifdef SG_KPROF
     const bool prof0 = prof && tid == 0;  // every block times itself; the longest segment reports
     unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1945,6 +1952,332 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 }
                 lds_barrier();
                 PROF_MARK(8)
+                continue;
+            }
+
+            // ================= open stretch =================
+            // Same program shape, nothing saturated, no breaker cut, and the last committed ENTRY passed:
+            // guess that every ENTRY from here on passes.  Under that guess the pass count, the window's
+            // success / RT / exception sums and the RT breakers' passCount before an ENTRY are prefix sums
+            // of the events before it, so the stretch is decided chunk by chunk at OPEN_EPL events per lane
+            // (one chain of scans and barriers per chunk instead of one per tile of Jacobi iterations): every
+            // ENTRY is checked against its prefix view in FlowRuleChecker / DegradeRule order, and the first
+            // one that does not pass, the first event past the round, or the segment end stops the stretch.
+            // Everything before the stop is exact (every earlier ENTRY did pass); the stop re-enters the
+            // Jacobi iteration with its evaluated outcome as the guess.  A long unsaturated segment (C4's J4
+            // body: 47k events under a 5250 QPS limit, no mismatch in 201 iterations) is a map + scan.
+            bool anycut = false;
+#pragma unroll
+            for (int k = 0; k < MD; ++k)
+                if (k < nd) anycut |= sh.rs[nf + k].a != 0;
+            anycut = uni(anycut ? 1u : 0u) != 0;
+            if (open_on && !anycut && uni(sh.last_out) == (uint32_t)nr && sg.len - (tbase + c0) >= open_min) {
+                constexpr uint32_t OE = NW == 4 ? OPEN_EPL : 2, OST = OE * HW;
+                static_assert(WIN - OST >= (FULL_FENCE_TILES + 1) * (OST + HW), "old references must precede a full fence");
+                flush(tbase);
+                __syncthreads();  // full fence at every stretch start (see lds_barrier)
+                const uint32_t fpos0 = tbase + c0;
+                // the view before the stretch: round base + committed (uniform)
+                const int64_t P0 = uni64(sh.bP + sh.cP), S0 = uni64(sh.bS + sh.cS), RT0 = uni64(sh.bRT + sh.cRT);
+                const int64_t E0 = uni64(sh.bE + sh.cE), EM0 = uni64(sh.bEM + sh.cE), B0 = uni64(sh.bB + sh.cB);
+                int64_t kP = 0, kS = 0, kRT = 0, kE = 0;  // carried over the stretch's earlier chunks (uniform)
+                uint32_t ksg[MD];                         // RT stages: segmented passCount carry
+                int32_t pcb0[MD];                         // ... and the breaker's passCount at the stretch start
+#pragma unroll
+                for (int k = 0; k < MD; ++k) {
+                    ksg[k] = 0;
+                    pcb0[k] = k < nd ? (int32_t)sh.rs[nf + k].b : 0;
+                }
+                uint32_t aP = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aTH = 0, aMin = NO_LANE;  // committed (lane)
+                const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
+                const uint32_t qmax = sg.len - 1;
+                uint4 rr[OE], rn[OE];
+                uint32_t sb = fpos0, nst = 0, fend = 0;
+#pragma unroll
+                for (int k = 0; k < (int)OE; ++k) {
+                    const uint32_t q = sb + tid * OE + k;
+                    rr[k] = r4[q < qmax ? q : qmax];
+                }
+                for (;;) {
+#pragma unroll
+                    for (int k = 0; k < (int)OE; ++k) {  // prefetch the next chunk
+                        const uint32_t q = sb + OST + tid * OE + k;
+                        rn[k] = r4[q < qmax ? q : qmax];
+                    }
+                    // classes under the all-pass guess; 0x80: a stop before evaluation (past the round / segment)
+                    uint32_t cl[OE];
+                    uint32_t lp = 0, ls = 0, lrt = 0, le = 0;
+#pragma unroll
+                    for (int k = 0; k < (int)OE; ++k) {
+                        const uint32_t q = sb + tid * OE + k;
+                        const int32_t edt = (int32_t)rr[k].x;
+                        const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
+                        const uint32_t code = (rr[k].w >> 16) & 0xFFu;
+                        uint32_t c = 0;
+                        if (q >= sg.len || edt >= dhi || edt < dlo) c = 0x80u;
+                        else if (ek == SG_EV_ENTRY) c = JC_ENT;
+                        else {
+                            bool eff = code == RC_NONE || code == RC_PASSED;
+                            if (code == RC_BATCH) {
+                                const uint32_t rel = rr[k].y - sg.start;
+                                if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+                                else if (rel >= fpos0) eff = true;  // an ENTRY of this stretch: passed
+                                else if (rel + WIN >= sb + OST) eff = win[rel & (WIN - 1)] != 0;
+                                else eff = !in_span(rel) &&
+                                           st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                            }
+                            if (eff && ek == SG_EV_EXIT) c = JC_XE;
+                            else if (eff && ek == SG_EV_TRACE && ec > 0) c = JC_TE;
+                        }
+                        cl[k] = c;
+                        lp += (c & JC_ENT) ? ec : 0u;
+                        ls += (c & JC_XE) ? ec : 0u;
+                        lrt += (c & JC_XE) ? ert : 0u;
+                        le += (c & JC_TE) ? ec : 0u;
+                    }
+                    // block-exclusive prefixes of the lane totals, and the chunk totals
+                    uint32_t xp = lp, xs = ls, xrt = lrt, xe = le;
+                    WAVE_SCAN(xp, 0u, op_add);
+                    WAVE_SCAN(xs, 0u, op_add);
+                    WAVE_SCAN(xrt, 0u, op_add);
+                    WAVE_SCAN(xe, 0u, op_add);
+                    uint32_t tP, tS, tRT, tE;
+                    if (NW == 1) {
+                        tP = (uint32_t)__builtin_amdgcn_readlane((int)xp, 63);
+                        tS = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
+                        tRT = (uint32_t)__builtin_amdgcn_readlane((int)xrt, 63);
+                        tE = (uint32_t)__builtin_amdgcn_readlane((int)xe, 63);
+                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le;
+                    } else {
+                        if (lane == 63) { sh.part[wv][0] = xp; sh.part[wv][1] = xs; sh.part[wv][2] = xrt; sh.part[wv][3] = xe; }
+                        lds_barrier();
+                        // lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv and the chunk total
+                        uint32_t* const xs4[4] = {&xp, &xs, &xrt, &xe};
+                        uint32_t* const ts4[4] = {&tP, &tS, &tRT, &tE};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            uint32_t v = lane < (uint32_t)NW ? sh.part[lane][i] : 0u;
+                            WAVE_SCAN(v, 0u, op_add);
+                            *xs4[i] += wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                            *ts4[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+                        }
+                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le;
+                    }
+                    // RT breakers: which ENTRYs see an average at the threshold, then the segmented passCount scan
+                    uint32_t badb = 0, segl[MD], segt[MD];
+#pragma unroll
+                    for (int k = 0; k < MD; ++k) segl[k] = segt[k] = 0;
+                    if (has_rt) {
+                        uint32_t agg[MD];
+#pragma unroll
+                        for (int k = 0; k < MD; ++k) agg[k] = 0;
+                        uint32_t rS = 0, rRT = 0;
+#pragma unroll
+                        for (int e = 0; e < (int)OE; ++e) {
+                            const int64_t vS = S0 + kS + (int64_t)(xs + rS), vRT = RT0 + kRT + (int64_t)(xrt + rRT);
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) {
+                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                    const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
+                                    const bool bad = !(avg < sh.rules[nf + k].count);
+                                    if (bad) badb |= 1u << (e * MD + k);
+                                    agg[k] = op_seg(agg[k], (cl[e] & JC_ENT) ? (bad ? 1u : 0x80000000u) : 0u);
+                                }
+                            }
+                            if (cl[e] & JC_XE) { rS += rr[e].z & 0xFFFFu; rRT += rr[e].z >> 16; }
+                        }
+#pragma unroll
+                        for (int k = 0; k < MD; ++k) {
+                            if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                uint32_t v = agg[k];
+                                WAVE_SCAN(v, 0u, op_seg);
+                                segl[k] = shr1(v, 0u);
+                                if (NW == 1) segt[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+                                else if (lane == 63) sh.pseg[wv][k] = v;
+                            }
+                        }
+                        if (NW > 1) {
+                            lds_barrier();
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) {
+                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                    uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
+                                    WAVE_SCAN(v, 0u, op_seg);
+                                    const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                                    segl[k] = op_seg(pre, segl[k]);
+                                    segt[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+                                }
+                            }
+                        }
+                    }
+                    // every ENTRY against its prefix view; the lane's first stop
+                    uint32_t mystop = NO_LANE, myo = (uint32_t)nr, sst[MD];
+                    uint32_t rp = 0, rs2 = 0, re = 0, rseg[MD];
+#pragma unroll
+                    for (int k = 0; k < MD; ++k) rseg[k] = sst[k] = 0;
+#pragma unroll
+                    for (int e = 0; e < (int)OE; ++e) {
+                        const uint32_t c = cl[e];
+                        const uint32_t ec = rr[e].z & 0xFFFFu;
+                        uint32_t o = (uint32_t)nr;
+                        if (c & 0x80u) o = NO_LANE;
+                        else if (c & JC_ENT) {
+                            const int64_t vP = P0 + kP + (int64_t)(xp + rp);
+                            const int64_t vS = S0 + kS + (int64_t)(xs + rs2);
+#pragma unroll
+                            for (int s = 0; s < MF; ++s)
+                                if (s < nf && o == (uint32_t)nr && (double)j_iadd(j_d2i((double)vP), (int)ec) > sh.rules[s].count)
+                                    o = (uint32_t)s;
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) {
+                                if (k < nd && o == (uint32_t)nr) {
+                                    const DRule& r = sh.rules[nf + k];
+                                    bool ok = true;
+                                    if (r.grade == SG_DEGRADE_GRADE_RT) {
+                                        const uint32_t x = op_seg(ksg[k], op_seg(segl[k], rseg[k]));
+                                        const int32_t cc = (int32_t)(x & 0x7fffffffu);
+                                        const int32_t pcb = (x & 0x80000000u) ? cc : pcb0[k] + cc;
+                                        ok = !((badb >> (e * MD + k)) & 1) || (pcb + 1 < 5);
+                                    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+                                        const double exc = (double)(E0 + kE + (int64_t)(xe + re)) / 1.0;
+                                        const double succ = (double)vS / 1.0;
+                                        const double total = (double)vP / 1.0 + (double)B0 / 1.0;
+                                        if (total < 5) ok = true;
+                                        else if (succ - exc <= 0 && exc < 5) ok = true;
+                                        else ok = exc / succ < r.count;
+                                    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) {
+                                        ok = (double)(EM0 + kE + (int64_t)(xe + re)) < r.count;
+                                    }
+                                    if (!ok) o = (uint32_t)(nf + k);
+                                }
+                            }
+                        }
+                        if (o != (uint32_t)nr && mystop == NO_LANE) {
+                            mystop = sb + tid * OE + (uint32_t)e;
+                            myo = o == NO_LANE ? (uint32_t)nr : o;
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) sst[k] = rseg[k];
+                        }
+                        rp += (c & JC_ENT) ? ec : 0u;
+                        rs2 += (c & JC_XE) ? ec : 0u;
+                        re += (c & JC_TE) ? ec : 0u;
+                        if (has_rt) {
+#pragma unroll
+                            for (int k = 0; k < MD; ++k)
+                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT)
+                                    rseg[k] = op_seg(rseg[k], (c & JC_ENT) ? (((badb >> (e * MD + k)) & 1) ? 1u : 0x80000000u) : 0u);
+                        }
+                    }
+                    uint32_t wmin = mystop;
+                    WAVE_SCAN(wmin, NO_LANE, op_min);
+                    if (lane == 63) sh.mism[mb][wv] = wmin;
+                    lds_barrier();
+                    uint32_t f = NO_LANE;
+                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    f = uni(f);
+                    mb ^= 1;
+                    ++n_opn;
+                    // commit every position before the stop (unconditional stores: masked lanes hit the sink)
+                    uint32_t appm = 0;
+#pragma unroll
+                    for (int k = 0; k < (int)OE; ++k) {
+                        const uint32_t q = sb + tid * OE + k;
+                        const bool cm = q < f && q < sg.len;
+                        const uint32_t c = cl[k];
+                        uint32_t d = 0;
+                        if (cm) {
+                            const uint32_t ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
+                            if (c & JC_ENT) {
+                                d = mk_dec(ST_PASS, 0, 0);
+                                win[q & (WIN - 1)] = 1;
+                                aP += ec; aTI += 1; aTH += 1;
+                                appm |= 1u << k;
+                            } else {
+                                d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                                win[q & (WIN - 1)] = 0;
+                                if (c & JC_XE) { aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1; }
+                                else if (c & JC_TE) { aE += ec; aTI += 1; }
+                            }
+                        }
+                        *(cm ? &dec[sg.start + q] : &S.sink[tid]) = d;
+                    }
+                    if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
+                        const uint32_t na = (uint32_t)__popc(appm);
+                        uint32_t incl = na;
+                        WAVE_SCAN(incl, 0u, op_add);
+                        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                        if (tot) {
+                            uint32_t base = 0;
+                            if (lane == 0) base = atomicAdd(&sh.npend, tot);
+                            base = (uint32_t)__shfl((int)base, 0, 64) + incl - na;
+#pragma unroll
+                            for (int k = 0; k < (int)OE; ++k)
+                                if ((appm >> k) & 1) S.pend[sg.start + base++] = sb + tid * OE + k;
+                        }
+                    }
+                    if (f != NO_LANE) {
+                        if (f >= sb + tid * OE && f < sb + tid * OE + OE) {  // the lane holding the stop
+                            sh.os_o = myo;
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) sh.os_seg[k] = op_seg(ksg[k], op_seg(segl[k], sst[k]));
+                        }
+                        fend = f < sg.len ? f : sg.len;
+                        break;
+                    }
+                    kP += tP; kS += tS; kRT += tRT; kE += tE;
+#pragma unroll
+                    for (int k = 0; k < MD; ++k) ksg[k] = op_seg(ksg[k], segt[k]);
+                    sb += OST;
+#pragma unroll
+                    for (int k = 0; k < (int)OE; ++k) rr[k] = rn[k];
+                    if (++nst % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
+                }
+                // stretch end: lane accumulators into the round's committed totals
+                WAVE_SCAN(aP, 0u, op_add);
+                WAVE_SCAN(aS, 0u, op_add);
+                WAVE_SCAN(aRT, 0u, op_add);
+                WAVE_SCAN(aE, 0u, op_add);
+                WAVE_SCAN(aTI, 0u, op_add);
+                WAVE_SCAN(aTH, 0u, op_add);
+                WAVE_SCAN(aMin, NO_LANE, op_min);
+                lds_barrier();  // sh.part's chunk exchange is read; sh.os_* is written
+                if (lane == 63) {
+                    sh.part[wv][0] = aP; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
+                    sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin;
+                }
+                const uint32_t g = uni(sh.os_o);
+                // re-enter the tile machinery at the stop; guesses = the stop's evaluated outcome
+                tbase = fend / TILE * TILE;
+                c0 = fend - tbase;
+                {
+                    SEv cur[EP];
+                    load(cur, tbase);
+                    load(nxt, tbase + TILE);
+#pragma unroll
+                    for (int e = 0; e < EP; ++e) ev[e] = decode(cur[e], tbase + lp0 + e);
+                }
+                guess_all(g, c0);
+#pragma unroll
+                for (int e = 0; e < EP; ++e)
+                    if ((ev[e].kf & JK_VALID) && lp0 + (uint32_t)e == c0) sh.tnext = t0 + ev[e].dt;
+                __syncthreads();
+                if (tid == 0) {
+                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                        sh.cP += sh.part[w][0]; sh.cS += sh.part[w][1]; sh.cRT += sh.part[w][2]; sh.cE += sh.part[w][3];
+                        sh.ctouch += sh.part[w][4]; sh.cTH += (int32_t)sh.part[w][5];
+                        sh.cminrt = op_min(sh.cminrt, sh.part[w][6]);
+                    }
+                    for (int k = 0; k < nd; ++k)
+                        if (sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                            const uint32_t x = sh.os_seg[k];
+                            const int32_t cc = (int32_t)(x & 0x7fffffffu);
+                            sh.rs[nf + k].b = (x & 0x80000000u) ? cc : sh.rs[nf + k].b + cc;
+                        }
+                    sh.last_out = g;
+                    sh.c0 = c0;
+                }
+                lds_barrier();
                 continue;
             }
         }
@@ -2495,6 +2828,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         atomicAdd(&S.dbg[3], (unsigned long long)n_mm);
         atomicAdd(&S.dbg[4], 1ull);
         atomicAdd(&S.dbg[6], (unsigned long long)n_frz);
+        atomicAdd(&S.dbg[7], (unsigned long long)n_opn);
 #ifdef SG_KPROF
         const unsigned long long tm_end = __builtin_amdgcn_s_memtime(), tot = tm_end - tm_start;
         if (atomicMax(&S.dbg[18], tot) < tot) {  // slowest segment so far: its phases, length, rounds

@@ -111,6 +111,15 @@ def test_c4_degrade(bin_mode):
     _run(4, batches=3, n_entries=400_000, n_res=50_000)
 
 
+@pytest.mark.parametrize("config", [2, 4])
+def test_cooperative_without_open_stretches(config, monkeypatch):
+    # the Jacobi iteration alone (debug flag 64 turns the all-pass open stretches off), every width exercised
+    for k, v in BIN_MODES["coop"].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("SG_DEBUG_FLAGS", "64")
+    _run(config, batches=3, n_entries=400_000, n_res=50_000 if config == 4 else 0)
+
+
 def test_c2_full_resource_count():
     # C2 at its configured 10k resources, 4M entries (4 s of trace) in 4 batches, default bins
     _run(2, batches=4, n_entries=4_000_000, n_res=10_000)
