@@ -1929,7 +1929,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         if (!bin_n[b]) continue;
         hipStream_t bs = serial_bins ? st : e->bin_stream[c];
         if (!serial_bins && !bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
-        HIPCHK(launch_pq(c == 0, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], S, dc, t0, e->d_dec,
+        DevState Sp = S;
+        Sp.dbg = (c == 0 && e->prof_bin == 3) ? e->d_dbg : nullptr;  // SG_PROF_BIN=3: k_pq<16> phase cycles (kprof builds)
+        HIPCHK(launch_pq(c == 0, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sp, dc, t0, e->d_dec,
                          e->d_bsmall + 0, bs));
         HIPCHK(hipEventRecord(e->join[c], bs));
     }

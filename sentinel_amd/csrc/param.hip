@@ -71,9 +71,24 @@ struct PqSh {
     uint64_t pend_key[PQ_NPEND];
     int64_t pend_stamp[PQ_NPEND];
     PData pend_dat[PQ_NPEND];
+#ifdef SG_KPROF
+    unsigned long long pt[16];      // phase cycles (thread 0's view; tools/pqprobe.py)
+    unsigned long long pt_t;
+#endif
 };
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// SG_KPROF builds: thread 0 charges the cycles since the last mark to phase k (call after a barrier)
+#ifdef SG_KPROF
+#define PQ_MARK(k)                                                  \
+    if (threadIdx.x == 0) {                                         \
+        const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+        sh.pt[k] += _n - sh.pt_t;                                   \
+        sh.pt_t = _n;                                               \
+    }
+#else
+#define PQ_MARK(k)
+#endif
 __device__ __forceinline__ uint64_t ld64(const void* p) {
     return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -328,7 +343,9 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     for (uint32_t i = na + tid; i < P; i += HW) { sh.skey[i] = PK_EMPTY; sh.sidx[i] = 0xFFFFFFFFu; }
     pq_reserve<NW>(sh, mk, S, na);
     __syncthreads();
+    PQ_MARK(1)
     pq_sort<NW>(sh, P);
+    PQ_MARK(2)
     PMap& m = sh.hdr[mk];
     const int64_t RB = (int64_t)1 << m.rb_log2;
     const uint32_t W = (uint32_t)(RB >> 6);
@@ -380,6 +397,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         sh.lrank[sh.sidx[s]] = rank;
     }
     __syncthreads();
+    PQ_MARK(3)
     // (c) residency of every first access: the upper bound r + (first accesses before it) settles it unless the key
     // is near the LRU end; then the exact count of the earlier first accesses of keys older than it
     if (!rmode) {
@@ -417,6 +435,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         }
     }
     __syncthreads();
+    PQ_MARK(4)
     // (d) walks: one lane per key group, its accesses in tile order; a thread-count tile that fails the
     // no-eviction check is replayed by pq_count_seq and walked again with its residencies
     uint32_t gend[SP], glast[SP];
@@ -552,6 +571,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         __syncthreads();
         mode = 2;
     }
+    PQ_MARK(5)
     // (e) commit: touched keys leave their old stamp; the oldest untouched keys beyond cap are evicted
     uint32_t nnew = 0;
 #pragma unroll
@@ -611,6 +631,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         sh.npend = 0;
     }
     __syncthreads();
+    PQ_MARK(6)
     // keys without a slot: a free slot (never used, or dead by the ring) of the less loaded bucket, claimed in LDS
 #pragma unroll
     for (uint32_t q = 0; q < SP; ++q) {
@@ -647,6 +668,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         }
     }
     __syncthreads();
+    PQ_MARK(7)
     if (tid == 0 && sh.npend) {  // displacement walks (pmap.h pm_insert_new), one lane
         const uint32_t np = sh.npend < PQ_NPEND ? sh.npend : PQ_NPEND;
         for (uint32_t k = 0; k < np; ++k) {
@@ -680,6 +702,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         __threadfence_block();
     }
     __syncthreads();
+    PQ_MARK(8)
 }
 
 // StatisticSlot on the ClusterNode for one tile (StatisticSlot.java:54-173, ClusterNode.trace): the events of
@@ -800,6 +823,10 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     if (tid == 0) {
         node_load(sh.node, S, res);
         sh.flags_or = 0;
+#ifdef SG_KPROF
+        for (int k = 0; k < 16; ++k) sh.pt[k] = 0;
+        sh.pt_t = __builtin_amdgcn_s_memtime();
+#endif
     }
     if ((int)tid < np) sh.rules[tid] = S.rules[pg.rule_off + tid];
     __syncthreads();
@@ -870,6 +897,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         // ---- 2. ParamFlowSlot: the rules in order
         if (tid == 0) sh.freach = 0xFFFFFFFFu;
         __syncthreads();
+        PQ_MARK(0)
         for (int k = 0; k < np; ++k) {
             const DRule& r = sh.rules[k];
             bool reach = false;
@@ -961,8 +989,10 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                 acc[q] = op != OP_NONE;
             }
             __syncthreads();
+            PQ_MARK(9)
             pq_map_phase<NW>(sh, PQ_MAXP, PW_COUNT, tk >= 0 ? &sh.rules[tk] : nullptr, S, t0, sg.start + tb, acc, bflags,
                              (cfg.dbg_flags & 32) != 0);
+            PQ_MARK(10)
             if (tk >= 0) {
 #pragma unroll
                 for (int q = 0; q < PQ_EPL; ++q)
@@ -991,9 +1021,19 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         }
         __syncthreads();
         // ---- 5. StatisticSlot: one bucket update per 500 ms bucket of the tile
+        PQ_MARK(11)
         pq_fold<NW>(sh, C, t0, tb, sg.start, sg.len, dec, bflags);
         __syncthreads();  // full fence: this tile's dec[] words are visible to the next tiles' EXIT lookups
+        PQ_MARK(12)
     }
+#ifdef SG_KPROF
+    if (S.dbg && tid == 0) {  // every block's phase cycles summed; [24] segments, [25] events, [26] longest segment
+        for (int k = 0; k < 13; ++k) atomicAdd(&S.dbg[8 + k], sh.pt[k]);
+        atomicAdd(&S.dbg[24], 1ull);
+        atomicAdd(&S.dbg[25], (unsigned long long)sg.len);
+        atomicMax(&S.dbg[26], (unsigned long long)sg.len);
+    }
+#endif
     // ---- segment end: node, map headers and rings back to HBM
     if (tid == 0) {
         Node& N = sh.node;

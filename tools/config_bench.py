@@ -25,6 +25,9 @@ CONFIGS = {
         "C3: 100k resources, 40% QPS / 20% thread / 20% WarmUp / 10% WarmUpRateLimiter / 10% RateLimiter"),
     5: (16_000_000, 1 << 23, {"param_table_log2": 27, "status_ring_log2": 27}, "c5",
         "C5: 10k resources, ParamFlow QPS (20% throttle) + thread-grade rules, hot items, 10M Zipf values + 50% uniform"),
+    # bench.py's C5 sub-line: QPS-grade param rules only, Zipf values
+    50: (12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
+         "C5 (bench.py sub-line): 10k resources, ParamFlow QPS rules (20% throttle) over 10M Zipf values"),
 }
 
 
@@ -35,7 +38,8 @@ def run(cfg: int):
     n_entries, gb, kw, var, desc = CONFIGS[cfg]
     variant = {0: 0, "warm_rl": T.V_WARM_RL, "c5": T.V_UNIFORM | T.V_HOT | T.V_THREAD}[var]
     t = time.time()
-    w = T.Workload(cfg, seed=T.SEED_BASE + cfg, n_entries=n_entries, variant=variant)
+    c = 5 if cfg == 50 else cfg
+    w = T.Workload(c, seed=T.SEED_BASE + c, n_entries=n_entries, variant=variant)
     ev = w.events
     gen_s = time.time() - t
     nb = (len(ev) + gb - 1) // gb
