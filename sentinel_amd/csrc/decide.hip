@@ -1222,6 +1222,33 @@ __device__ __forceinline__ int64_t wscan_i64_max(int64_t x) {
 
 #define NO_LANE 0xFFFFFFFFu
 
+// Block-wide exchanges of per-wave values in LDS (a[w], w < NW <= 16): lanes l < NW load a[l] at once and an
+// inclusive DPP scan runs within the first 16-lane row; lane NW-1 holds the total, lane wv-1 the waves before wv.
+// (A loop over the NW values in every lane issues NW dependent-latency LDS reads per exchange.)
+#define ROW_SCAN(v, ident, OP, NWV)                                    \
+    do {                                                               \
+        if ((NWV) > 1) DPP_STEP(v, ident, 0x111, 0xf, OP);              \
+        if ((NWV) > 2) DPP_STEP(v, ident, 0x112, 0xf, OP);              \
+        if ((NWV) > 4) DPP_STEP(v, ident, 0x114, 0xf, OP);              \
+        if ((NWV) > 8) DPP_STEP(v, ident, 0x118, 0xf, OP);              \
+    } while (0)
+template <int NW>
+__device__ __forceinline__ uint32_t blk_min(const uint32_t* a) {
+    static_assert(NW <= 16, "one DPP row");
+    uint32_t v = lane_id() < (uint32_t)NW ? a[lane_id()] : NO_LANE;
+    ROW_SCAN(v, NO_LANE, op_min, NW);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+}
+// sum over the waves before wv (exclusive) and the total, of a[w * stride]
+template <int NW>
+__device__ __forceinline__ uint32_t blk_sum_before(const uint32_t* a, uint32_t stride, uint32_t wv, uint32_t* tot) {
+    static_assert(NW <= 16, "one DPP row");
+    uint32_t v = lane_id() < (uint32_t)NW ? a[lane_id() * stride] : 0u;
+    ROW_SCAN(v, 0u, op_add, NW);
+    *tot = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+    return wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+}
+
 // Workgroup barrier that only drains LDS traffic.  __syncthreads() is a release/acquire fence over
 // global memory as well, i.e. it waits for every outstanding vector load -- including the next tile
 // prefetched into registers -- so each tile would pay a full HBM round trip.  All cross-wave data
@@ -1245,6 +1272,7 @@ enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR
 
 #define NSPAN 64        // skipped spans per segment (LDS list for references into them)
 #define OPEN_EPL 4      // open stretches: events per lane per chunk of the 256-lane owner (2 for the others: 128-VGPR cap)
+#define TG_PASSES 2     // closed-form passes per Jacobi iteration of a THREAD-grade program
 
 template <int NW, int MF, int MD>
 struct JacSh {
@@ -1476,7 +1504,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         }
     }
     const bool has_rt = (pg.pflags & PF_RT) != 0;
-    const bool frozen_prog = (pg.pflags & PF_FROZEN) != 0;
+    // frozen / open stretches need every flow stage's verdict to be a function of the round's pass count: QPS
+    // DefaultControllers (PF_FROZEN) and QPS WarmUpControllers, whose limit is fixed within a round once its second's
+    // token sync is known (WarmUpController.java:83-175: syncToken moves storedTokens once per second)
+    uint32_t warmm = 0;  // WarmUp flow stages (uniform)
+    bool fz = true;
+    for (int s = 0; s < nf; ++s) {
+        const DRule& r = sh.rules[s];
+        if (r.grade != SG_FLOW_GRADE_QPS) fz = false;
+        else if (r.behavior == SG_CONTROL_BEHAVIOR_WARM_UP) warmm |= 1u << s;
+        else if (r.behavior != SG_CONTROL_BEHAVIOR_DEFAULT) fz = false;
+    }
+    const bool frozen_prog = fz;
     // open stretches (all-pass prefix decisions, below): on unless debug flag 64; worth a chunk from one tile left
     const bool open_on = !(cfg.dbg_flags & 64);
     const uint32_t open_min = TILE;
@@ -1635,10 +1674,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             const int64_t Pfix = uni64(sh.bP + sh.cP);
             const int32_t pint = j_d2i((double)Pfix);
             const bool cutk0 = nd > 0 && uni(sh.rs[nf].a != 0);
+            // each flow stage's limit in this round: DefaultController count; WarmUp: warningQps above the
+            // warning token, else count (the synced state of the round's second)
+            double flim[MF];
+#pragma unroll
+            for (int s = 0; s < MF; ++s) {
+                flim[s] = 0.0;
+                if (s < nf) {
+                    const DRule& r = sh.rules[s];
+                    flim[s] = r.count;
+                    if ((warmm >> s) & 1) {
+                        const RState& st = ((sh.has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                        if (st.a >= r.warning_token) flim[s] = warm_qps(r, st.a);
+                    }
+                }
+            }
+            // stage s blocks an acquire of c at the round's pass count P
+            auto fblock = [&](int s, int64_t P, int c) -> bool {
+                return ((warmm >> s) & 1) ? !((double)(P + c) <= flim[s])
+                                          : (double)j_iadd(j_d2i((double)P), c) > flim[s];
+            };
             bool sat = false;
 #pragma unroll
             for (int s = 0; s < MF; ++s)
-                if (s < nf) sat |= (double)j_iadd(pint, 1) > sh.rules[s].count;
+                if (s < nf) sat |= fblock(s, Pfix, 1);
             sat = uni(sat) != 0;
             if (sat || cutk0) {
                 constexpr uint32_t EPL = 4, ST = EPL * HW;  // events per lane, positions per super-tile
@@ -1650,9 +1709,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 uint32_t fdec[MF];
 #pragma unroll
                 for (int s = 0; s < MF; ++s) {
-                    fcount[s] = s < nf ? sh.rules[s].count : 0.0;
+                    fcount[s] = flim[s];
                     fdec[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, sh.rules[s].slot, 0) : 0u;
                 }
+                uint32_t freach = 0;  // WarmUp stages a committed ENTRY of the stretch reached (token sync persists)
                 const uint32_t cdec = nd > 0 ? mk_dec(ST_BLOCK_DEGRADE, sh.rules[nf].slot, 0) : 0u;
                 uint32_t aB = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aMin = NO_LANE, aTH = 0;
                 uint32_t fend = 0;
@@ -1676,7 +1736,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         if (lane == 0) sh.mism[mb][wv] = bm ? wv * 64 + (uint32_t)(__ffsll((long long)bm) - 1) : NO_LANE;
                         lds_barrier();
                         uint32_t f = NO_LANE;
-                        for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                        f = blk_min<NW>(sh.mism[mb]);
                         f = uni(f);
                         mb ^= 1;
                         if (f == NO_LANE) {
@@ -1789,12 +1849,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 const uint64_t km = __ballot(keep);
                                 if (lane == 0) sh.mism[mb][wv] = (uint32_t)__popcll(km);
                                 lds_barrier();
-                                uint32_t before = 0, tot = 0;
-                                for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
-                                    const uint32_t c = sh.mism[mb][w];
-                                    if (w < wv) before += c;
-                                    tot += c;
-                                }
+                                uint32_t tot;
+                                const uint32_t before = blk_sum_before<NW>(sh.mism[mb], 1, wv, &tot);
                                 mb ^= 1;
                                 if (keep) S.pend[sg.start + kept + before + (uint32_t)__popcll(km & lanemask_lt())] = item;
                                 kept += uni(tot);
@@ -1849,10 +1905,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu;
                         const bool in = q < sg.len && edt >= dlo && edt < dhi;
                         const double curv = (double)j_iadd(pint, (int)ec);
+                        const double curw = (double)(Pfix + (int64_t)ec);
                         uint32_t fd = 0;
 #pragma unroll
                         for (int s = MF - 1; s >= 0; --s)
-                            if (s < nf && curv > fcount[s]) fd = fdec[s];
+                            if (s < nf && (((warmm >> s) & 1) ? !(curw <= fcount[s]) : curv > fcount[s])) fd = fdec[s];
                         if (fd == 0 && cutk0) fd = cdec;
                         fdv[k] = fd;
                         const bool stop = q < sg.len && (!in || (ek == SG_EV_ENTRY && fd == 0));
@@ -1863,7 +1920,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     if (lane == 63) sh.mism[mb][wv] = wmin;
                     lds_barrier();
                     uint32_t f = NO_LANE;
-                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    f = blk_min<NW>(sh.mism[mb]);
                     f = uni(f);
                     mb ^= 1;
                     ++n_frz;
@@ -1883,6 +1940,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 win[q & (WIN - 1)] = 0;
                                 aB += ec;
                                 aTI += 1;
+                                if (warmm) {  // stages up to the blocking one (all flow stages when a breaker blocks)
+                                    uint32_t bs = (uint32_t)nf;
+#pragma unroll
+                                    for (int s = MF - 1; s >= 0; --s)
+                                        if (s < nf && d == fdec[s]) bs = (uint32_t)s;
+                                    freach |= (2u << bs) - 1u;
+                                }
                             } else {
                                 bool eff = code == RC_NONE || code == RC_PASSED;
                                 if (code == RC_BATCH) {
@@ -1913,6 +1977,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 }
                 }  // !skipped
                 PROF_MARK(7)
+                if (warmm) {
+#pragma unroll
+                    for (int s = 0; s < MF; ++s)
+                        if (((warmm >> s) & 1) && __ballot((freach >> s) & 1) && lane == 0) atomicOr(&sh.warm_reach, 1u << s);
+                }
                 // stretch end: reduce the lane accumulators into the round's committed totals
                 WAVE_SCAN(aB, 0u, op_add);
                 WAVE_SCAN(aS, 0u, op_add);
@@ -1989,6 +2058,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     pcb0[k] = k < nd ? (int32_t)sh.rs[nf + k].b : 0;
                 }
                 uint32_t aP = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aTH = 0, aMin = NO_LANE;  // committed (lane)
+                bool oent = false;  // the lane committed an ENTRY
                 const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
                 const uint32_t qmax = sg.len - 1;
                 uint4 rr[OE], rn[OE];
@@ -2127,8 +2197,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                             const int64_t vS = S0 + kS + (int64_t)(xs + rs2);
 #pragma unroll
                             for (int s = 0; s < MF; ++s)
-                                if (s < nf && o == (uint32_t)nr && (double)j_iadd(j_d2i((double)vP), (int)ec) > sh.rules[s].count)
-                                    o = (uint32_t)s;
+                                if (s < nf && o == (uint32_t)nr && fblock(s, vP, (int)ec)) o = (uint32_t)s;
 #pragma unroll
                             for (int k = 0; k < MD; ++k) {
                                 if (k < nd && o == (uint32_t)nr) {
@@ -2174,7 +2243,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     if (lane == 63) sh.mism[mb][wv] = wmin;
                     lds_barrier();
                     uint32_t f = NO_LANE;
-                    for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+                    f = blk_min<NW>(sh.mism[mb]);
                     f = uni(f);
                     mb ^= 1;
                     ++n_opn;
@@ -2192,6 +2261,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 d = mk_dec(ST_PASS, 0, 0);
                                 win[q & (WIN - 1)] = 1;
                                 aP += ec; aTI += 1; aTH += 1;
+                                oent = true;
                                 appm |= 1u << k;
                             } else {
                                 d = mk_dec(ST_NOT_ENTRY, 0, 0);
@@ -2233,6 +2303,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     for (int k = 0; k < (int)OE; ++k) rr[k] = rn[k];
                     if (++nst % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
                 }
+                // every committed ENTRY passed every flow stage: a pending WarmUp token sync persists
+                if (warmm && __ballot(oent) && lane == 0) atomicOr(&sh.warm_reach, warmm);
                 // stretch end: lane accumulators into the round's committed totals
                 WAVE_SCAN(aP, 0u, op_add);
                 WAVE_SCAN(aS, 0u, op_add);
@@ -2296,7 +2368,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         //   RateLimiter (RateLimiterController.java:46-91): saturated, the k-th admission after the committed
         //   latestPassedTime L is the first ENTRY with t >= L + k * cost - maxQueue: e passes iff
         //   q(t_e) > q(t of the previous ENTRY), q(t) = max(0, floor((t - L + maxQueue) / cost)).
-        if (EP == 1 && (tg_mode || rl_mode)) {
+        // THREAD grade: an EXIT frees a thread only if its ENTRY passed, and in a hot segment half the EXITs name an
+        // ENTRY of the same tile (RT ~ Exp(20 ms) against a tile spanning ~16 ms), so the admissions of one pass feed
+        // the next: the closed form is re-run on its own guesses (TG_PASSES times) before the Jacobi iteration checks it.
+        const int cf_passes = tg_mode ? TG_PASSES : 1;
+        for (int cfp = 0; EP == 1 && (tg_mode || rl_mode) && cfp < cf_passes; ++cfp) {
             const uint32_t kf = ev[0].kf, kind = kf & 0xFFu;
             const bool inr = (kf & JK_VALID) && lp0 >= c0 && ev[0].dt >= dlo && ev[0].dt < dhi;
             const bool eff = (kf & JK_WIN) ? (win[ev[0].wi] != 0) : ((kf & JK_VAL) != 0);
@@ -2311,9 +2387,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             if (lane == 63) { sh.cg[wv][0] = ia; sh.cg[wv][1] = ix; sh.cg[wv][2] = ib; }
             lds_barrier();
             uint32_t pa = 0, px = 0, tb = 0;
-            for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
-                if (w < wv) { pa += sh.cg[w][0]; px = tg_mode ? px + sh.cg[w][1] : op_max(px, sh.cg[w][1]); }
-                tb += sh.cg[w][2];
+            if (NW > 1) {
+                uint32_t t0u;
+                pa = blk_sum_before<NW>(&sh.cg[0][0], 3, wv, &t0u);
+                (void)blk_sum_before<NW>(&sh.cg[0][2], 3, wv, &tb);
+                uint32_t v = lane < (uint32_t)NW ? sh.cg[lane][1] : 0u;
+                if (tg_mode) ROW_SCAN(v, 0u, op_add, NW);
+                else ROW_SCAN(v, 0u, op_max, NW);
+                px = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+            } else {
+                tb = sh.cg[0][2];
             }
             const bool use = uni(tb) == 0;
             bool g = false;  // the closed-form outcome of this lane's ENTRY (pass)
@@ -2334,7 +2417,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 const uint32_t mex = shr1(m, 0xFFFFFFFFu);
                 lds_barrier();
                 uint32_t pm = 0xFFFFFFFFu;
-                for (uint32_t w = 0; w < wv; ++w) pm = op_min(pm, sh.cgm[w]);
+                if (NW > 1) {
+                    uint32_t v = lane < (uint32_t)NW ? sh.cgm[lane] : 0xFFFFFFFFu;
+                    ROW_SCAN(v, 0xFFFFFFFFu, op_min, NW);
+                    pm = wv == 0 ? 0xFFFFFFFFu : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                }
                 const uint32_t me = op_min(pm, mex);
                 const int64_t M = me == 0xFFFFFFFFu ? 0 : ((int64_t)me - 0x40000000LL < 0 ? (int64_t)me - 0x40000000LL : 0);
                 g = W >= M;
@@ -2511,8 +2598,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
 #pragma unroll
             for (int k = 0; k < MD; ++k) {
                 if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                    uint32_t pre = 0;
-                    for (uint32_t w = 0; w < wv; ++w) pre = op_seg(pre, sh.pseg[w][k]);
+                    uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
+                    ROW_SCAN(v, 0u, op_seg, NW);
+                    const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
                     segl[k] = op_seg(pre, segl[k]);
                 }
             }
@@ -2671,7 +2759,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         PROF_MARK(3)
         lds_barrier();  // B4
         uint32_t f = NO_LANE;
-        for (uint32_t w = 0; w < (uint32_t)NW; ++w) f = op_min(f, sh.mism[mb][w]);
+        f = blk_min<NW>(sh.mism[mb]);
         f = uni(f);
         // the pivot's true outcome: the re-guess of every later ENTRY of the round.  Their own evaluated
         // outcomes saw the pivot's wrong guess (e.g. a guessed breaker trip blocks everything after it),
@@ -2840,6 +2928,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             S.dbg[25] = pg.pflags | (nf << 8) | (nd << 12) | ((nd ? sh.rules[nf].grade : 0xF) << 16);
             S.dbg[26] = (unsigned long long)sh.rules[0].count;
             S.dbg[27] = n_frz;
+            S.dbg[28] = nf ? ((uint64_t)sh.rules[0].behavior | ((uint64_t)sh.rules[0].grade << 8)) : 0xFFFFull;
+            S.dbg[29] = n_opn;
         }
         atomicMin(&S.dbg[20], tm_start);  // block start spread (waiting for a CU) and last end
         atomicMax(&S.dbg[21], tm_start);

@@ -64,6 +64,7 @@ struct PqSh {
     uint32_t tdec[TE];              // tile event -> decision word (EXIT references inside the tile)
     uint64_t skey[TE];
     uint32_t sidx[TE];
+    uint32_t olist[TE];             // residency: live first accesses at the LRU end (tile position << 12 | rank)
     uint32_t red[NW][8];
     int64_t red64[NW][2];
     uint32_t flags_or, npend;
@@ -99,6 +100,40 @@ __device__ __forceinline__ int64_t uni64_pq(int64_t v) {  // LDS-broadcast value
 }
 __device__ __forceinline__ uint32_t ld32(const void* p) {
     return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A key's slot in its two buckets (-1: absent).  All eight keys of a bucket are loaded before any is compared:
+// a compare-and-exit loop would make each load wait for the previous one (eight HBM / L2 round trips).
+__device__ __forceinline__ int32_t pq_find(const PBucket* B, uint32_t b1, uint32_t b2, uint64_t key) {
+    uint64_t k[PM_BKT];
+#pragma unroll
+    for (int j = 0; j < PM_BKT; ++j) k[j] = ld64(&B[b1].key[j]);
+#pragma unroll
+    for (int j = PM_BKT - 1; j >= 0; --j)
+        if (k[j] == key) return (int32_t)(b1 * PM_BKT + j);
+#pragma unroll
+    for (int j = 0; j < PM_BKT; ++j) k[j] = ld64(&B[b2].key[j]);
+    int32_t r = -1;
+#pragma unroll
+    for (int j = PM_BKT - 1; j >= 0; --j)
+        if (k[j] == key) r = (int32_t)(b2 * PM_BKT + j);
+    return r;
+}
+__device__ __forceinline__ bool ring_live(const PMap& m, const uint64_t* bm, int64_t s);
+// bit j: slot j of bucket b is free (never used, or its key's stamp is dead by the ring), keys and stamps loaded at once
+__device__ __forceinline__ uint32_t pq_free_mask(const PBucket* B, uint32_t b, const PMap& m, const uint64_t* bm) {
+    uint64_t k[PM_BKT];
+    int64_t st[PM_BKT];
+#pragma unroll
+    for (int j = 0; j < PM_BKT; ++j) {
+        k[j] = ld64(&B[b].key[j]);
+        st[j] = (int64_t)ld64(&B[b].stamp[j]);
+    }
+    uint32_t f = 0;
+#pragma unroll
+    for (int j = 0; j < PM_BKT; ++j)
+        if (k[j] == PK_EMPTY || !ring_live(m, bm, st[j])) f |= 1u << j;
+    return f;
 }
 
 // exclusive block scan of one u32 per lane; *tot = block total (uniform)
@@ -377,10 +412,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         glead[q] = true;
         uint32_t b1, b2;
         pm_buckets(m.nb, key, b1, b2);
-        for (int j = 0; j < PM_BKT && gslot[q] < 0; ++j)
-            if (ld64(&B[b1].key[j]) == key) gslot[q] = (int32_t)(b1 * PM_BKT + j);
-        for (int j = 0; j < PM_BKT && gslot[q] < 0; ++j)
-            if (ld64(&B[b2].key[j]) == key) gslot[q] = (int32_t)(b2 * PM_BKT + j);
+        gslot[q] = pq_find(B, b1, b2, key);
         int32_t rank = RANK_NEW;
         if (gslot[q] >= 0) {
             gst[q] = (int64_t)ld64(&B[gslot[q] / PM_BKT].stamp[gslot[q] % PM_BKT]);
@@ -401,11 +433,36 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     // (c) residency of every first access: the upper bound r + (first accesses before it) settles it unless the key
     // is near the LRU end; then the exact count of the earlier first accesses of keys older than it
     if (!rmode) {
-        uint32_t lf = 0;
+        // D = rk + N + G: N the tile's earlier first accesses of keys that were not live, G those of live keys older
+        // than this one (rank > rk).  G only matters when rk + F >= cap, i.e. rk >= cap - nf, so only live first
+        // accesses ranked >= cap - nf (the LRU end: few, old keys are rarely accessed again) are listed, in tile
+        // order, and G is counted over that list instead of over the whole tile.
+        uint32_t lf = 0, ln = 0;
 #pragma unroll
-        for (int q = 0; q < PQ_EPL; ++q) lf += sh.lrank[tid * PQ_EPL + q] != RANK_REP ? 1u : 0u;
-        uint32_t nf;
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const int32_t rk = sh.lrank[tid * PQ_EPL + q];
+            lf += rk != RANK_REP ? 1u : 0u;
+            ln += rk == RANK_NEW ? 1u : 0u;
+        }
+        uint32_t nf, nn;
         uint32_t F = pq_scan<NW>(sh, lf, &nf);
+        uint32_t N = pq_scan<NW>(sh, ln, &nn);
+        const uint32_t rlo = nf < cap ? cap - nf : 0u;
+        uint32_t lo = 0;
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const int32_t rk = sh.lrank[tid * PQ_EPL + q];
+            lo += (rk != RANK_REP && rk != RANK_NEW && (uint32_t)rk >= rlo) ? 1u : 0u;
+        }
+        uint32_t no;
+        uint32_t O = pq_scan<NW>(sh, lo, &no);
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t e = tid * PQ_EPL + q;
+            const int32_t rk = sh.lrank[e];
+            if (rk != RANK_REP && rk != RANK_NEW && (uint32_t)rk >= rlo) sh.olist[O++] = (e << 12) | (uint32_t)rk;
+        }
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < PQ_EPL; ++q) {
             const uint32_t e = tid * PQ_EPL + q;
@@ -414,17 +471,19 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
             uint32_t hit = 0;
             if (rk != RANK_NEW) {
                 if ((uint32_t)rk + F < cap) hit = TV_HIT;
-                else {
-                    uint32_t d = (uint32_t)rk;
-                    for (uint32_t j = 0; j < e && d < cap; ++j) {
-                        const int32_t x = sh.lrank[j];
-                        if (x != RANK_REP && x > rk) ++d;
+                else if ((uint32_t)rk + N < cap) {
+                    uint32_t d = (uint32_t)rk + N;
+                    for (uint32_t k = 0; k < no && d < cap; ++k) {
+                        const uint32_t x = sh.olist[k];
+                        if ((x >> 12) >= e) break;
+                        if ((x & 0xFFFu) > (uint32_t)rk) ++d;
                     }
                     hit = d < cap ? TV_HIT : 0u;
                 }
             }
             sh.tver[e] = hit;  // leader residency, read by the group's walker
             ++F;
+            if (rk == RANK_NEW) ++N;
         }
     } else {
 #pragma unroll
@@ -640,13 +699,15 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         uint32_t b1, b2;
         pm_buckets(m.nb, key, b1, b2);
         bool placed = false;
+        // the slots of both buckets that are free in HBM (never used, or dead by the ring): one round of loads
+        const uint32_t hf1 = pq_free_mask(B, b1, m, sh.bm[mk]), hf2 = pq_free_mask(B, b2, m, sh.bm[mk]);
         for (int attempt = 0; attempt < 4 && !placed; ++attempt) {
             int f1 = -1, f2 = -1, n1 = 0, n2 = 0;
             for (int j = 0; j < PM_BKT; ++j) {
                 const uint32_t i1 = b1 * PM_BKT + j, i2 = b2 * PM_BKT + j;
                 const bool c1 = (sh.claim[i1 >> 6] >> (i1 & 63)) & 1ull, c2 = (sh.claim[i2 >> 6] >> (i2 & 63)) & 1ull;
-                const bool fr1 = !c1 && (ld64(&B[b1].key[j]) == PK_EMPTY || !ring_live(m, sh.bm[mk], (int64_t)ld64(&B[b1].stamp[j])));
-                const bool fr2 = !c2 && (ld64(&B[b2].key[j]) == PK_EMPTY || !ring_live(m, sh.bm[mk], (int64_t)ld64(&B[b2].stamp[j])));
+                const bool fr1 = !c1 && ((hf1 >> j) & 1u);
+                const bool fr2 = !c2 && ((hf2 >> j) & 1u);
                 if (fr1) { if (f1 < 0) f1 = j; } else ++n1;
                 if (fr2) { if (f2 < 0) f2 = j; } else ++n2;
             }
@@ -1054,7 +1115,11 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
                      uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
-    if (wide) hipLaunchKernelGGL(k_pq<16>, dim3(m), dim3(1024), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    // the wide owner: 1024 lanes (128 VGPRs a lane: ~120 spilled) measured 15 % faster on C5 than 512 lanes with
+    // 256 VGPRs and no spill (SG_DEBUG_FLAGS 128 selects that form, for A/B runs)
+    if (wide && (cfg.dbg_flags & 128))
+        hipLaunchKernelGGL(k_pq<8>, dim3(m), dim3(512), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    else if (wide) hipLaunchKernelGGL(k_pq<16>, dim3(m), dim3(1024), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
     else hipLaunchKernelGGL(k_pq<4>, dim3(m), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
     return hipGetLastError();
 }

@@ -1,4 +1,5 @@
-"""Diagnostics: counters of one cooperative bin (SG_DEBUG=1; SG_PROF_BIN = 0 J16, 1 J4, 2 J1) on a C4 batch.
+"""Diagnostics: counters of one cooperative bin (SG_DEBUG=1; SG_PROF_BIN = 0 J16, 1 J4, 2 J1) on a C4 batch
+(or another config; SG_VARIANT: tracegen variant bits).
 
 usage: python tools/hotprobe.py [config] [n_entries] [batches] [R/N shard]
 """
@@ -19,7 +20,8 @@ n_entries = int(sys.argv[2]) if len(sys.argv) > 2 else 16_400_000
 nb = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 shard = tuple(int(x) for x in sys.argv[4].split("/")) if len(sys.argv) > 4 else None  # R/N: one rank's shard
 t = time.time()
-w = T.Workload(cfg, n_entries=n_entries, n_res=1_000_000 if cfg == 4 else 0)
+variant = int(os.environ.get("SG_VARIANT", "0"))  # tracegen variant bits (C3: 1 = WarmUpRateLimiter in the mix)
+w = T.Workload(cfg, n_entries=n_entries, n_res=1_000_000 if cfg == 4 else 0, variant=variant)
 print("generated %d events in %.1f s" % (w.n_events, time.time() - t), flush=True)
 eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=22, status_ring_log2=28,
                max_batch_events=1 << 25)
@@ -51,7 +53,9 @@ for i in range(nb):
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
     print("  slowest segment (len %d, %d rounds, %d cycles) phase cycles:" % (v[5], v[19], v[18]),
           {k: "%.0f" % ph[j] for j, k in enumerate(names)})
-    print("  slowest: iterations %d mismatched %d frozen-tiles %d prog %#x flow count %d" % (v[23], v[24], v[27], v[25], v[26]))
+    print("  slowest: iterations %d mismatched %d frozen-tiles %d open-chunks %d prog %#x flow count %d "
+          "first flow behaviour|grade<<8 %#x" % (v[23], v[24], v[27], v[29], v[25], v[26], v[28]))
+    print("  open-stretch chunks (all segments of the bin): %d" % d[7])
     mm = d[40:49].reshape(3, 3)
     print("  mismatch (guess row: pass/flow/degrade -> evaluated col):", mm.tolist(), "not-first", d[49], "sum(f-c0)", d[50])
     print("  J16 block starts spread %d cycles, first start -> last end %d cycles" % (v[21] - v[20], v[22] - v[20]))
