@@ -354,11 +354,12 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     const uint32_t tid = threadIdx.x;
     // (a) accesses before each event, in tile order
     uint32_t la = 0;
-    bool rm_l = false;
+    bool rm_l = false, nacq1 = false;
 #pragma unroll
     for (int q = 0; q < PQ_EPL; ++q) {
         la += acc[q] ? 1u : 0u;
         if (acc[q] && walk == PW_COUNT && pq_op(sh.tkx[tid * PQ_EPL + q]) != OP_ADD) rm_l = true;
+        if (acc[q] && (sh.tcz[tid * PQ_EPL + q] & 0xFFFFu) != 1u) nacq1 = true;
     }
     uint32_t na;
     uint32_t a0 = pq_scan<NW>(sh, la, &na);
@@ -366,6 +367,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     // a thread-count tile with gets or decrements: residency by the no-eviction hypothesis, verified after the
     // walks (the rank rule below counts every first access as an insertion and knows no removals)
     const bool rmode = __syncthreads_or(rm_l) != 0;
+    const bool all_acq1 = __syncthreads_or(nacq1) == 0;  // every access acquires 1 (the walks' closed forms)
 #pragma unroll
     for (int q = 0; q < PQ_EPL; ++q) {
         const uint32_t e = tid * PQ_EPL + q;
@@ -502,6 +504,16 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     bool gpres[SP], gtouch[SP];
     int mode = rmode ? 1 : 0;  // 0: rank rule, 1: no-eviction hypothesis (verified), 2: sequential replay
     uint32_t seq_size = 0;
+    // group ends without a sequential scan of the sorted keys: the leaders' sorted positions by group index
+    uint32_t gidx[SP], ngrp = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SP; ++q) {
+        uint32_t tq;
+        gidx[q] = ngrp + pq_scan<NW>(sh, glead[q] ? 1u : 0u, &tq);
+        if (glead[q]) sh.olist[gidx[q]] = tid + q * HW;
+        ngrp += tq;
+    }
+    __syncthreads();
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -516,13 +528,21 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
             const uint32_t e0 = sh.sidx[s];
             const bool ghit = (sh.tver[e0] & TV_HIT) != 0;
             const uint64_t key = sh.skey[s];
-            uint32_t send = s + 1;
-            while (send < na && sh.skey[send] == key) ++send;
+            const uint32_t send = gidx[q] + 1 < ngrp ? sh.olist[gidx[q] + 1] : na;
             gend[q] = send;
             PData st = gd[q];
             if (walk == PW_COUNT) {
                 bool pres = ghit;
                 int64_t c = ghit ? gd[q].v0 : 0;
+                if (!rmode) {  // increments only (OP_ADD): the first access inserts an absent key, each adds one
+                    for (uint32_t p = s; p < send; ++p) sh.tver[sh.sidx[p]] = (p == s && !ghit) ? TV_INS : 0u;
+                    st.v0 = c + (int64_t)(send - s);
+                    gpres[q] = true;
+                    gtouch[q] = true;
+                    glast[q] = sh.sidx[send - 1];
+                    gfin[q] = st;
+                    continue;
+                }
                 const int64_t thr = r ? pq_thread_thr(S, r, key) : 0;
                 for (uint32_t p = s; p < send; ++p) {
                     const uint32_t e = sh.sidx[p];
@@ -556,6 +576,25 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
             }
             const int64_t dur_ms = r->duration_sec * 1000;
             bool first_miss = !ghit;
+            if (ghit && all_acq1) {
+                // A resident value whose group's LAST access is blocked with the state it had at the group start is
+                // blocked throughout, and a blocked check changes nothing (times only grow along the group): no token
+                // refill before it (passTime <= duration) with no token left; a throttle's expected pass time still
+                // at least maxQueue ahead.  The group is then one check instead of a walk.
+                const int64_t tl = t0 + sh.tdt[glast[q]];
+                bool blocked;
+                if (walk == PW_THROTTLE) {
+                    const int64_t expected = st.v0 + j_round(1.0 * 1000 * 1 * (double)r->duration_sec / (double)tcl);
+                    blocked = !(expected <= tl || expected - tl < r->max_queue);
+                } else {
+                    blocked = tl - st.v0 <= dur_ms && j_iadd(st.v1, -1) < 0;
+                }
+                if (blocked) {
+                    for (uint32_t p = s; p < send; ++p) sh.tver[sh.sidx[p]] = TV_BLOCK;
+                    gfin[q] = st;
+                    continue;
+                }
+            }
             for (uint32_t p = s; p < send; ++p) {
                 const uint32_t e = sh.sidx[p];
                 const int64_t t = t0 + sh.tdt[e];

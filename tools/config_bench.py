@@ -23,7 +23,7 @@ CONFIGS = {
     2: (50_000_000, 1 << 25, {}, 0, "C2: 10k resources, QPS DefaultController flow rules, Zipf(1.1), 100M events"),
     3: (24_000_000, 1 << 24, {}, "warm_rl",
         "C3: 100k resources, 40% QPS / 20% thread / 20% WarmUp / 10% WarmUpRateLimiter / 10% RateLimiter"),
-    5: (16_000_000, 1 << 23, {"param_table_log2": 27, "status_ring_log2": 27}, "c5",
+    5: (16_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 27}, "c5",
         "C5: 10k resources, ParamFlow QPS (20% throttle) + thread-grade rules, hot items, 10M Zipf values + 50% uniform"),
     # bench.py's C5 sub-line: QPS-grade param rules only, Zipf values
     50: (12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
