@@ -65,6 +65,7 @@ struct PqSh {
     uint64_t skey[TE];
     uint32_t sidx[TE];
     uint32_t olist[TE];             // residency: live first accesses at the LRU end (tile position << 12 | rank)
+    uint32_t sorted_n;              // skey / sidx hold the last map phase's accesses sorted by (key, position): how many
     uint32_t red[NW][8];
     int64_t red64[NW][2];
     uint32_t flags_or, npend;
@@ -105,18 +106,19 @@ __device__ __forceinline__ uint32_t ld32(const void* p) {
 // A key's slot in its two buckets (-1: absent).  All eight keys of a bucket are loaded before any is compared:
 // a compare-and-exit loop would make each load wait for the previous one (eight HBM / L2 round trips).
 __device__ __forceinline__ int32_t pq_find(const PBucket* B, uint32_t b1, uint32_t b2, uint64_t key) {
-    uint64_t k[PM_BKT];
+    uint64_t k1[PM_BKT], k2[PM_BKT];  // both buckets in one round of loads (most probes of a churning map miss)
 #pragma unroll
-    for (int j = 0; j < PM_BKT; ++j) k[j] = ld64(&B[b1].key[j]);
-#pragma unroll
-    for (int j = PM_BKT - 1; j >= 0; --j)
-        if (k[j] == key) return (int32_t)(b1 * PM_BKT + j);
-#pragma unroll
-    for (int j = 0; j < PM_BKT; ++j) k[j] = ld64(&B[b2].key[j]);
+    for (int j = 0; j < PM_BKT; ++j) {
+        k1[j] = ld64(&B[b1].key[j]);
+        k2[j] = ld64(&B[b2].key[j]);
+    }
     int32_t r = -1;
 #pragma unroll
     for (int j = PM_BKT - 1; j >= 0; --j)
-        if (k[j] == key) r = (int32_t)(b2 * PM_BKT + j);
+        if (k2[j] == key) r = (int32_t)(b2 * PM_BKT + j);
+#pragma unroll
+    for (int j = PM_BKT - 1; j >= 0; --j)
+        if (k1[j] == key) r = (int32_t)(b1 * PM_BKT + j);
     return r;
 }
 __device__ __forceinline__ bool ring_live(const PMap& m, const uint64_t* bm, int64_t s);
@@ -218,25 +220,80 @@ __device__ void pq_reserve(PqSh<NW>& sh, int mk, const DevState& S, uint32_t k) 
     __syncthreads();
 }
 
-// bitonic sort of (skey, sidx) pairs [0, P) in LDS, P a power of two
+// one bitonic compare-exchange stage (k, j) over LDS pairs [0, P)
 template <int NW>
-__device__ void pq_sort(PqSh<NW>& sh, uint32_t P) {
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P / 2; i += PqSh<NW>::HW) {
-                const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
-                const bool up = (lo & k) == 0;
-                const uint64_t ka = sh.skey[lo], kb = sh.skey[hi];
-                const uint32_t ia = sh.sidx[lo], ib = sh.sidx[hi];
-                const bool gt = ka > kb || (ka == kb && ia > ib);
-                if (gt == up) {
-                    sh.skey[lo] = kb; sh.skey[hi] = ka;
-                    sh.sidx[lo] = ib; sh.sidx[hi] = ia;
-                }
-            }
-            lds_sync();
+__device__ __forceinline__ void pq_sort_stage(PqSh<NW>& sh, uint32_t P, uint32_t k, uint32_t j) {
+    for (uint32_t i = threadIdx.x; i < P / 2; i += PqSh<NW>::HW) {
+        const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+        const bool up = (lo & k) == 0;
+        const uint64_t ka = sh.skey[lo], kb = sh.skey[hi];
+        const uint32_t ia = sh.sidx[lo], ib = sh.sidx[hi];
+        const bool gt = ka > kb || (ka == kb && ia > ib);
+        if (gt == up) {
+            sh.skey[lo] = kb; sh.skey[hi] = ka;
+            sh.sidx[lo] = ib; sh.sidx[hi] = ia;
         }
     }
+    lds_sync();
+}
+// (key, idx) of the lane l ^ m of this wave
+__device__ __forceinline__ void pq_xchg(uint64_t k, uint32_t i, uint32_t m, uint64_t& tk, uint32_t& ti) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)k, (int)m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(k >> 32), (int)m, 64);
+    ti = (uint32_t)__shfl_xor((int)i, (int)m, 64);
+    tk = ((uint64_t)hi << 32) | lo;
+}
+// element e keeps the smaller of (mine, theirs) iff it is the lower position of its pair in an ascending block
+__device__ __forceinline__ void pq_keep(uint64_t& mk, uint32_t& mi, uint64_t tk, uint32_t ti, bool keep_min) {
+    const bool mine_lt = mk < tk || (mk == tk && mi < ti);
+    if (mine_lt != keep_min) { mk = tk; mi = ti; }
+}
+// Bitonic sort of (skey, sidx) pairs [0, P) in LDS, P a power of two.  From P >= 128 a wave holds 128 consecutive
+// elements in registers (two a lane): the stages whose partners are less than 128 apart run as register / lane
+// exchanges without a block barrier; only the stages across waves (j >= 128: 10 of the 66 for P = 2048) go
+// through LDS.
+template <int NW>
+__device__ void pq_sort(PqSh<NW>& sh, uint32_t P) {
+    if (P < 128) {
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) pq_sort_stage<NW>(sh, P, k, j);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t e0 = w * 128 + 2 * lane;
+    const bool act = e0 < P;
+    uint64_t ka = 0, kb = 0;
+    uint32_t ia = 0, ib = 0;
+    if (act) { ka = sh.skey[e0]; ia = sh.sidx[e0]; kb = sh.skey[e0 + 1]; ib = sh.sidx[e0 + 1]; }
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        uint32_t j = k >> 1;
+        if (j >= 128) {
+            lds_sync();  // every wave is done reading the lists it loaded
+            if (act) { sh.skey[e0] = ka; sh.sidx[e0] = ia; sh.skey[e0 + 1] = kb; sh.sidx[e0 + 1] = ib; }
+            lds_sync();
+            for (; j >= 128; j >>= 1) pq_sort_stage<NW>(sh, P, k, j);
+            if (act) { ka = sh.skey[e0]; ia = sh.sidx[e0]; kb = sh.skey[e0 + 1]; ib = sh.sidx[e0 + 1]; }
+        }
+        for (; j >= 2; j >>= 1) {  // partner lane l ^ (j / 2), same parity
+            uint64_t tk;
+            uint32_t ti;
+            pq_xchg(ka, ia, j >> 1, tk, ti);
+            pq_keep(ka, ia, tk, ti, ((e0 & k) == 0) == ((e0 & j) == 0));
+            pq_xchg(kb, ib, j >> 1, tk, ti);
+            pq_keep(kb, ib, tk, ti, (((e0 + 1) & k) == 0) == (((e0 + 1) & j) == 0));
+        }
+        {   // j = 1: the lane's own pair
+            const bool up = (e0 & k) == 0;
+            const bool gt = ka > kb || (ka == kb && ia > ib);
+            if (gt == up) {
+                const uint64_t x = ka; ka = kb; kb = x;
+                const uint32_t y = ia; ia = ib; ib = y;
+            }
+        }
+    }
+    lds_sync();
+    if (act) { sh.skey[e0] = ka; sh.sidx[e0] = ia; sh.skey[e0 + 1] = kb; sh.sidx[e0 + 1] = ib; }
+    lds_sync();
 }
 
 enum { PW_TOKEN = 0, PW_THROTTLE = 1, PW_COUNT = 2 };
@@ -345,10 +402,12 @@ __device__ __noinline__ uint32_t pq_count_seq(PqSh<NW>& sh, int mk, const DRule*
 // One map's accesses of the tile (acc[e] for the lane's events e = tid * PQ_EPL + q): residency, the walk of
 // every key group (WALK), commit.  Verdicts of the walks land in sh.tver[e]: TV_BLOCK | wait << 16.
 // tbase: segment position of the tile's first event (OP_SUBC references).
+// presorted (a thread-count map of increments only): the accesses are the passed subset of the last rule map
+// phase's accesses, with the same keys, so its sorted list is kept as it is instead of sorting again.
 template <int NW>
 __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const DRule* r, const DevState& S, int64_t t0,
                                           uint32_t tbase, const bool (&acc)[PQ_EPL], uint32_t* bflags,
-                                          bool force_seq = false) {
+                                          bool force_seq = false, bool presorted = false) {
     constexpr uint32_t HW = PqSh<NW>::HW;
     constexpr uint32_t SP = PqSh<NW>::TE / HW;  // sorted positions per lane
     const uint32_t tid = threadIdx.x;
@@ -363,25 +422,51 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     }
     uint32_t na;
     uint32_t a0 = pq_scan<NW>(sh, la, &na);
+    const uint32_t prev_n = sh.sorted_n;  // read before any lane rewrites it (pq_scan ends with a barrier)
+    __syncthreads();
+    if (tid == 0) sh.sorted_n = na;
     if (na == 0) return;  // uniform
     // a thread-count tile with gets or decrements: residency by the no-eviction hypothesis, verified after the
     // walks (the rank rule below counts every first access as an insertion and knows no removals)
     const bool rmode = __syncthreads_or(rm_l) != 0;
     const bool all_acq1 = __syncthreads_or(nacq1) == 0;  // every access acquires 1 (the walks' closed forms)
+    const bool keep_sorted = presorted && !rmode;
 #pragma unroll
     for (int q = 0; q < PQ_EPL; ++q) {
         const uint32_t e = tid * PQ_EPL + q;
         sh.tA[e] = a0;
         sh.lrank[e] = RANK_REP;
-        if (acc[q]) { sh.skey[a0] = sh.tkey[e]; sh.sidx[a0] = e; ++a0; }
+        if (keep_sorted) sh.olist[e] = acc[q] ? 1u : 0u;
+        else if (acc[q]) { sh.skey[a0] = sh.tkey[e]; sh.sidx[a0] = e; }
+        if (acc[q]) ++a0;
     }
     uint32_t P = 64;
     while (P < na) P <<= 1;
+    if (keep_sorted) {
+        // stable compaction of the previous sorted list to this phase's accesses (lanes own consecutive positions)
+        __syncthreads();
+        uint64_t kk[PQ_EPL];
+        uint32_t ki[PQ_EPL], nk = 0;
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q) {
+            const uint32_t s0 = tid * PQ_EPL + q;
+            ki[q] = s0 < prev_n ? sh.sidx[s0] : 0xFFFFFFFFu;
+            kk[q] = s0 < prev_n ? sh.skey[s0] : PK_EMPTY;
+            if (ki[q] != 0xFFFFFFFFu && sh.olist[ki[q]]) ++nk;
+            else ki[q] = 0xFFFFFFFFu;
+        }
+        uint32_t tot;
+        uint32_t o = pq_scan<NW>(sh, nk, &tot);  // (its barriers: every lane has read the old list)
+#pragma unroll
+        for (int q = 0; q < PQ_EPL; ++q)
+            if (ki[q] != 0xFFFFFFFFu) { sh.skey[o] = kk[q]; sh.sidx[o] = ki[q]; ++o; }
+        if (tot != na) atomicOr(bflags, BF_PTAB_FULL);  // not the subset it must be: fails the batch loudly
+    }
     for (uint32_t i = na + tid; i < P; i += HW) { sh.skey[i] = PK_EMPTY; sh.sidx[i] = 0xFFFFFFFFu; }
     pq_reserve<NW>(sh, mk, S, na);
     __syncthreads();
     PQ_MARK(1)
-    pq_sort<NW>(sh, P);
+    if (!keep_sorted) pq_sort<NW>(sh, P);
     PQ_MARK(2)
     PMap& m = sh.hdr[mk];
     const int64_t RB = (int64_t)1 << m.rb_log2;
@@ -417,15 +502,18 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
         gslot[q] = pq_find(B, b1, b2, key);
         int32_t rank = RANK_NEW;
         if (gslot[q] >= 0) {
+            // the stamp and the slot's values in one round of loads (the values are used only if the stamp is live)
+            const uint64_t* dp = reinterpret_cast<const uint64_t*>(&D[gslot[q]]);
             gst[q] = (int64_t)ld64(&B[gslot[q] / PM_BKT].stamp[gslot[q] % PM_BKT]);
+            const int64_t dv0 = (int64_t)ld64(dp);
+            const uint64_t dv1 = ld64(dp + 1);
             glive[q] = ring_live(m, sh.bm[mk], gst[q]);
             if (glive[q]) {
                 const uint64_t p = (uint64_t)gst[q] & (uint64_t)(RB - 1);
                 const uint32_t below = sh.wpre[p >> 6] + (uint32_t)__popcll(sh.bm[mk][p >> 6] & ((1ull << (p & 63)) - 1ull));
                 rank = (int32_t)(live0 - below - 1);
-                const uint64_t* dp = reinterpret_cast<const uint64_t*>(&D[gslot[q]]);
-                gd[q].v0 = (int64_t)ld64(dp);
-                gd[q].v1 = (int32_t)(uint32_t)ld64(dp + 1);
+                gd[q].v0 = dv0;
+                gd[q].v1 = (int32_t)(uint32_t)dv1;
             }
         }
         sh.lrank[sh.sidx[s]] = rank;
@@ -923,6 +1011,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     if (tid == 0) {
         node_load(sh.node, S, res);
         sh.flags_or = 0;
+        sh.sorted_n = 0;
 #ifdef SG_KPROF
         for (int k = 0; k < 16; ++k) sh.pt[k] = 0;
         sh.pt_t = __builtin_amdgcn_s_memtime();
@@ -995,6 +1084,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         }
         __syncthreads();
         // ---- 2. ParamFlowSlot: the rules in order
+        bool ran_qps = false;  // a rule map phase of this tile left its sorted accesses in skey / sidx
         if (tid == 0) sh.freach = 0xFFFFFFFFu;
         __syncthreads();
         PQ_MARK(0)
@@ -1039,6 +1129,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                 acc[q] = true;
             }
             pq_map_phase<NW>(sh, k, walk, &r, S, t0, sg.start + tb, acc, bflags);
+            ran_qps = true;
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
                 if (!acc[q]) continue;
@@ -1091,7 +1182,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
             __syncthreads();
             PQ_MARK(9)
             pq_map_phase<NW>(sh, PQ_MAXP, PW_COUNT, tk >= 0 ? &sh.rules[tk] : nullptr, S, t0, sg.start + tb, acc, bflags,
-                             (cfg.dbg_flags & 32) != 0);
+                             (cfg.dbg_flags & 32) != 0, ran_qps && !(cfg.dbg_flags & 256));
             PQ_MARK(10)
             if (tk >= 0) {
 #pragma unroll

@@ -18,8 +18,8 @@ for spec in "$@"; do
     fi
     v=$(echo "$spec" | tr '@, ' '___')
     if [ "$name" = base ]; then LIB=""; else LIB="$PWD/var/lib_$name.so"; fi
-    env $XE SG_LIB_PATH=$LIB timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --max-sub-batches 24 $XA > $OUT/$v.json 2> $OUT/$v.err
-    env $XE SG_LIB_PATH=$LIB timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_$v -o run -- python3 bench.py --steps 2 --warmup 1 --sub-batches 2 --no-cpu-baseline $XA > $OUT/tr_$v.log 2>&1
+    env $XE SG_LIB_PATH=$LIB timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs $XA > $OUT/$v.json 2> $OUT/$v.err
+    env $XE SG_LIB_PATH=$LIB timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_$v -o run -- python3 bench.py --steps 2 --warmup 1 --sub-batches 2 --no-cpu-baseline --no-configs $XA > $OUT/tr_$v.log 2>&1
     cp $(find $OUT/tr_$v -name '*kernel_stats.csv' | head -1) $OUT/ks_$v.csv
     rm -rf $OUT/tr_$v
     python3 - "$OUT/$v.json" "$OUT/ks_$v.csv" "$v" <<'EOF'
