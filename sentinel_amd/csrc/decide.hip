@@ -149,7 +149,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                           !prio[sg.res] && !p.multi;
         uint32_t bin;
         if (pq && (p.pflags & PF_PQ) && !prio[sg.res]) bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
-        else if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? BIN_J16 : sg.len > j1_max ? BIN_J4 : BIN_J1;
+        else if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? ((p.pflags & PF_FROZEN) ? BIN_J8 : BIN_J16)
+                              : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
@@ -1271,7 +1272,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR /* trip counts, 2 per word */ };
 
 #define NSPAN 64        // skipped spans per segment (LDS list for references into them)
-#define OPEN_EPL 4      // open stretches: events per lane per chunk of the 256-lane owner (2 for the others: 128-VGPR cap)
+#define OPEN_EPL 4      // open stretches: events per lane per chunk
 #define TG_PASSES 2     // closed-form passes per Jacobi iteration of a THREAD-grade program
 
 template <int NW, int MF, int MD>
@@ -1517,7 +1518,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     }
     const bool frozen_prog = fz;
     // open stretches (all-pass prefix decisions, below): on unless debug flag 64; worth a chunk from one tile left
-    const bool open_on = !(cfg.dbg_flags & 64);
+    // (the 256- and 512-lane owners only: inline in the 1024-lane and one-wave owners, whose 128-register budget the
+    // Jacobi iteration already fills, it spilled the iteration's registers and cost more than it saved)
+    constexpr bool OPEN = NW == 4 || NW == 8;
+    const bool open_on = OPEN && !(cfg.dbg_flags & 64);
     const uint32_t open_min = TILE;
     // single-stage programs with closed-form admission guesses (see the Jacobi iteration)
     const bool tg_mode = nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_THREAD &&
@@ -1697,7 +1701,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             bool sat = false;
 #pragma unroll
             for (int s = 0; s < MF; ++s)
-                if (s < nf) sat |= fblock(s, Pfix, 1);
+                if (s < nf) sat |= warmm ? fblock(s, Pfix, 1) : (double)j_iadd(pint, 1) > flim[s];
             sat = uni(sat) != 0;
             if (sat || cutk0) {
                 constexpr uint32_t EPL = 4, ST = EPL * HW;  // events per lane, positions per super-tile
@@ -1905,11 +1909,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu;
                         const bool in = q < sg.len && edt >= dlo && edt < dhi;
                         const double curv = (double)j_iadd(pint, (int)ec);
-                        const double curw = (double)(Pfix + (int64_t)ec);
                         uint32_t fd = 0;
+                        if (!warmm) {
 #pragma unroll
-                        for (int s = MF - 1; s >= 0; --s)
-                            if (s < nf && (((warmm >> s) & 1) ? !(curw <= fcount[s]) : curv > fcount[s])) fd = fdec[s];
+                            for (int s = MF - 1; s >= 0; --s)
+                                if (s < nf && curv > fcount[s]) fd = fdec[s];
+                        } else {
+                            const double curw = (double)(Pfix + (int64_t)ec);
+#pragma unroll
+                            for (int s = MF - 1; s >= 0; --s)
+                                if (s < nf && (((warmm >> s) & 1) ? !(curw <= fcount[s]) : curv > fcount[s])) fd = fdec[s];
+                        }
                         if (fd == 0 && cutk0) fd = cdec;
                         fdv[k] = fd;
                         const bool stop = q < sg.len && (!in || (ek == SG_EV_ENTRY && fd == 0));
@@ -2036,12 +2046,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             // Jacobi iteration with its evaluated outcome as the guess.  A long unsaturated segment (C4's J4
             // body: 47k events under a 5250 QPS limit, no mismatch in 201 iterations) is a map + scan.
             bool anycut = false;
+            if (OPEN) {  // (nothing of this in the owners without open stretches: it sits on every iteration's chain)
 #pragma unroll
-            for (int k = 0; k < MD; ++k)
-                if (k < nd) anycut |= sh.rs[nf + k].a != 0;
-            anycut = uni(anycut ? 1u : 0u) != 0;
-            if (open_on && !anycut && uni(sh.last_out) == (uint32_t)nr && sg.len - (tbase + c0) >= open_min) {
-                constexpr uint32_t OE = NW == 4 ? OPEN_EPL : 2, OST = OE * HW;
+                for (int k = 0; k < MD; ++k)
+                    if (k < nd) anycut |= sh.rs[nf + k].a != 0;
+                anycut = uni(anycut ? 1u : 0u) != 0;
+            }
+            if (OPEN && open_on && !anycut && uni(sh.last_out) == (uint32_t)nr && sg.len - (tbase + c0) >= open_min) {
+                constexpr uint32_t OE = OPEN_EPL, OST = OE * HW;
                 static_assert(WIN - OST >= (FULL_FENCE_TILES + 1) * (OST + HW), "old references must precede a full fence");
                 flush(tbase);
                 __syncthreads();  // full fence at every stretch start (see lds_barrier)
@@ -2598,10 +2610,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
 #pragma unroll
             for (int k = 0; k < MD; ++k) {
                 if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                    uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
-                    ROW_SCAN(v, 0u, op_seg, NW);
-                    const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
-                    segl[k] = op_seg(pre, segl[k]);
+                    if (NW > 1) {  // one wave: its prefixes are the block's
+                        uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
+                        ROW_SCAN(v, 0u, op_seg, NW);
+                        const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                        segl[k] = op_seg(pre, segl[k]);
+                    }
                 }
             }
         }
@@ -3019,7 +3033,7 @@ hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, 
                        cand, ev, prog, ext, max_ctx);
     return hipGetLastError();
 }
-// bin = BIN_J16 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16
+// bin = BIN_J16 / BIN_J8 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st) {
@@ -3028,6 +3042,13 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
                    // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS
         hipLaunchKernelGGL((k_jac<16, 1, 17, 2, 2, false, true>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
+                           dec, bflags);
+        break;
+    case BIN_J8:  // the J16 lengths of QPS-DefaultController programs (C2 / C4 heads): 512 lanes with 256 registers a
+                  // lane, room for the open stretches (the 1024-lane owner's 128 registers do not hold them);
+                  // measured: C4 J16-bin time 1.89 -> 1.53 ms, C2 4.03 -> 4.24 G entries/s.  THREAD-grade / WarmUp
+                  // heads keep 1024 lanes (C3: 0.39 vs 0.27 G entries/s)
+        hipLaunchKernelGGL((k_jac<8, 1, 17, 2, 2, false, true>), dim3(m), dim3(512), 0, st, recs, segs, order, m, S, cfg, t0,
                            dec, bflags);
         break;
     case BIN_J4:  // 256 lanes, one event each: two events per lane (k_jac<4, 2, ...>) measured 22 % faster alone

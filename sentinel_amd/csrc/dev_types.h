@@ -374,7 +374,8 @@ enum : uint32_t {
     BIN_J1 = 2,            // one wavefront per segment
     BIN_PQ16 = 3,          // PF_PQ segments: one 1024-lane k_pq workgroup (long segments)
     BIN_PQ4 = 4,           //                 one 256-lane k_pq workgroup
-    BIN_LANE = 5,          // one lane per segment, nr <= 4: bins 5..5+LANE_BINS-1 by descending log2(len)
+    BIN_J8 = 5,            // one 512-lane workgroup per segment: the J16 lengths of QPS-DefaultController programs
+    BIN_LANE = 6,          // one lane per segment, nr <= 4: bins 6..6+LANE_BINS-1 by descending log2(len)
     LANE_BINS = 19,
     BIN_LANE16 = BIN_LANE + LANE_BINS,  // one lane per segment, nr > 4 (rule state in scratch)
     BIN_LITE = BIN_LANE16 + LANE_BINS,  // one lane per segment, DefaultController flows + breakers only (k_lite)

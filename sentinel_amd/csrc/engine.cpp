@@ -1912,8 +1912,20 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const int coop[2] = {BIN_J16, BIN_J4};
     // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
     const bool serial_bins = (e->dbg_flags & 8) != 0;
+    // J8 (the QPS-DefaultController heads) takes J16's stream when every head is of that kind (C2, C4); beside
+    // THREAD-grade / WarmUp heads (C3: J16 is the decide stage's longest chain) it runs first on the main stream
+    const bool j8_own = bin_n[BIN_J8] && !bin_n[BIN_J16];
     for (int c = 0; c < 2; ++c) {
         const int b = coop[c];
+        if (c == 0 && bin_n[BIN_J8]) {
+            DevState Sb = S;
+            Sb.dbg = (e->prof_bin == 0 && e->d_dbg) ? e->d_dbg : nullptr;
+            hipStream_t bs = (serial_bins || !j8_own) ? st : e->bin_stream[0];
+            if (bs != st) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
+            HIPCHK(launch_decide_bin(BIN_J8, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J8], bin_n[BIN_J8], Sb, dc,
+                                     t0, e->d_dec, e->d_bsmall + 0, bs));
+            if (bs != st) HIPCHK(hipEventRecord(e->join[0], bs));
+        }
         if (!bin_n[b]) continue;
         DevState Sb = S;
         Sb.dbg = (c == e->prof_bin && e->d_dbg) ? e->d_dbg : nullptr;
@@ -1928,7 +1940,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         const int b = c == 0 ? BIN_PQ16 : BIN_PQ4;
         if (!bin_n[b]) continue;
         hipStream_t bs = serial_bins ? st : e->bin_stream[c];
-        if (!serial_bins && !bin_n[coop[c]]) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
+        if (!serial_bins && !bin_n[coop[c]] && !(c == 0 && j8_own)) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
         DevState Sp = S;
         Sp.dbg = (c == 0 && e->prof_bin == 3) ? e->d_dbg : nullptr;  // SG_PROF_BIN=3: k_pq<16> phase cycles (kprof builds)
         HIPCHK(launch_pq(c == 0, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[b], bin_n[b], Sp, dc, t0, e->d_dec,
@@ -1956,9 +1968,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                                  t0, e->d_dec, e->d_bsmall + 0, st));
     }
     for (int c = 0; c < 2; ++c)
-        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4]) HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
+        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4] || (c == 0 && j8_own))
+            HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped
-    if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J4]))
+    if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
