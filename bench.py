@@ -298,7 +298,7 @@ def main():
     achieved = alg / (batch_ms / 1e3) / 1e9
     decide_ms = float(stage_ms[:, 1].mean())
     dec_alg = alg * nb / (steps * per_step) / world  # one rank-local batch's share, over its decide-stage time
-    traffic, tnote = None, None
+    traffic, tnote, traffic_rw = None, None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     sha = src_sha()
     if os.path.exists(pmc):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh) on these sources
@@ -306,7 +306,10 @@ def main():
             pj = json.load(f)
         if pj.get("src_sha") == sha and pj.get("batch_events") == gb and world == 1 and not shard:
             traffic = pj.get("traffic_bytes_per_batch")
-            tnote = "profiles/pmc_latest.json (src_sha %s, git %s)" % (sha, pj.get("git_head"))
+            traffic_rw = {"read": pj.get("read_bytes_per_batch"), "write": pj.get("write_bytes_per_batch"),
+                          "all_fetches_doubled": pj.get("traffic_upper_bytes_per_batch")}
+            tnote = ("profiles/pmc_latest.json (src_sha %s, git %s): FETCH_SIZE doubled for the streaming kernels, "
+                     "as counted for the random-access ones" % (sha, pj.get("git_head")))
         else:
             why = ("src_sha %s != %s" % (pj.get("src_sha"), sha) if pj.get("src_sha") != sha else
                    "batch_events %s != %s" % (pj.get("batch_events"), gb) if pj.get("batch_events") != gb else
@@ -350,6 +353,7 @@ def main():
                        "rank_event_shares": [x / sum(shares) for x in shares]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
+                         "traffic_split": traffic_rw,
                          "traffic_GBps": traffic / (batch_ms / 1e3) / 1e9 if traffic else None,
                          "stream_copy_GBps": stream,
                          "frac_of_stream_copy": achieved / stream if stream else None,
