@@ -51,6 +51,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // k_seg_count writes the tile's segment-start count, a scan over tiles gives the offsets, and
 // k_seg_emit recounts and writes each Seg at its offset.  Reads the keys twice instead of
 // writing and re-reading an n-wide flag and position array.
+#define J8_MAX (1u << 23)  // longest segment of a QPS-DefaultController program on the 512-lane owner
 #define SEG_ITEMS 16
 #define SEG_TILE (256 * SEG_ITEMS)
 __device__ __forceinline__ uint32_t seg_flags16(const uint32_t* __restrict__ keys, uint64_t n, uint64_t i0,
@@ -149,8 +150,12 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                           !prio[sg.res] && !p.multi;
         uint32_t bin;
         if (pq && (p.pflags & PF_PQ) && !prio[sg.res]) bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
-        else if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16)) ? ((p.pflags & PF_FROZEN) ? BIN_J8 : BIN_J16)
-                              : sg.len > j1_max ? BIN_J4 : BIN_J1;
+        // QPS-DefaultController heads on the 512-lane owner (open stretches), up to J8_MAX events: a longer one (one
+        // rank's batch of a strong-scaling run can hold a single resource's 33M events, nearly all in frozen
+        // stretches) goes faster through the 1024-lane owner (8-way rehearsal: slowest rank 3.58 vs 2.64 ms)
+        else if (coop) bin = (sg.len > j4_max && (p.pflags & PF_J16))
+                                 ? (((p.pflags & PF_FROZEN) && sg.len <= J8_MAX) ? BIN_J8 : BIN_J16)
+                                 : sg.len > j1_max ? BIN_J4 : BIN_J1;
         else {
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
@@ -1449,7 +1454,9 @@ __device__ __forceinline__ bool rl_upd(const DRule& r, uint32_t c, uint32_t g, i
 // positions), so one chain of scans and barriers -- the latency that bounds an iteration -- decides
 // up to TILE events: a lane folds its events' quantities sequentially, the wave and block scans run on
 // the lane totals, and each event's view is the lane's exclusive prefix plus its running sum.
-template <int NW, int EP, int WINLOG, int MF, int MD, bool RL, bool SKIP>
+// CLS: 0 every segment of the dispatch list; 1 only QPS-DefaultController programs (PF_FROZEN), 2 only the others
+// (one bin's list decided by two instantiations, each with the registers its own kind of segment needs)
+template <int NW, int EP, int WINLOG, int MF, int MD, bool RL, bool SKIP, int CLS = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? (EP == 1 ? 4 : 2) : (EP == 1 ? 1 : 2)))) void k_jac(
     const SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t m,
     DevState S, DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
@@ -1468,6 +1475,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const Seg sg = segs[order[blockIdx.x]];
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
+    if (CLS != 0 && (((pg.pflags & PF_FROZEN) != 0) != (CLS == 1))) return;  // the other instantiation's segment
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
     if (tid == 0) {
@@ -3041,8 +3049,12 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     switch (bin) {
     case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
                    // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS
-        hipLaunchKernelGGL((k_jac<16, 1, 17, 2, 2, false, true>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0,
-                           dec, bflags);
+        // THREAD-grade / WarmUp heads (no frozen-stretch skipping: without it the iteration fits 128 registers,
+        // 1 VGPR spilled against 19), then the QPS-DefaultController heads longer than J8_MAX (skipping)
+        hipLaunchKernelGGL((k_jac<16, 1, 17, 2, 2, false, false, 2>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg,
+                           t0, dec, bflags);
+        hipLaunchKernelGGL((k_jac<16, 1, 17, 2, 2, false, true, 1>), dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg,
+                           t0, dec, bflags);
         break;
     case BIN_J8:  // the J16 lengths of QPS-DefaultController programs (C2 / C4 heads): 512 lanes with 256 registers a
                   // lane, room for the open stretches (the 1024-lane owner's 128 registers do not hold them);
