@@ -57,8 +57,9 @@ EPE = 2.05  # C4 events per entry (entry + exit + 5 % traces)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    # defaults: ~4 s of timed GPU work (20 steps x 48 global batches) so an outside utilisation sampler sees it
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--batch-events", type=int, default=1 << 25, help="events per global batch")
     p.add_argument("--base-batches", type=int, default=8, help="global batches generated on the host")
     p.add_argument("--sub-batches", type=int, default=48, help="global batches per step (a multiple of N)")
