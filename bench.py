@@ -362,7 +362,7 @@ def main():
                          "batch_ms": batch_ms, "alg_bytes_per_batch": alg,
                          "decide_stage": {"ms": decide_ms, "achieved": dec_alg / (decide_ms / 1e3) / 1e9,
                                           "frac": dec_alg / (decide_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-                                          "kernels": "k_jac<16>|k_jac<4>,k_jac<1>|k_lite,k_lane (streams), k_fill"}},
+                                          "kernels": "k_jac<8> (or k_jac<16>) | k_jac<4>, k_pq | k_lite, k_lane, k_jac<1> (streams), k_fill"}},
             "pipeline": {"group_ms": float(stage_ms[:, 0].mean()), "decide_ms": decide_ms,
                          "post_ms": float(stage_ms[:, 2].mean()), "device_ms": float(stage_ms[:, 3].mean()),
                          "wall_ms_per_batch": batch_ms},
