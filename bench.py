@@ -18,10 +18,12 @@ chunk its fresh batches are built (untimed), the chunk is bracketed by barrier +
 timed, and the step time is the chunks' total over K.  Inputs are resident in HBM whenever a timed
 chunk starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): ONE C4 trace,
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or bench.py --gpus N
+alone, which starts the N rank processes itself): ONE C4 trace,
 resources partitioned over the ranks (strong scaling).  Every rank generates the same trace and
 keeps its shard (EXIT/TRACE references rewritten to its own numbering).  The partition is a resource ->
-rank table balanced by the base trace's event counts (sentinel_amd/dist.py balanced_table; --sharding
+rank table balanced by the event counts of a history window, the first global batch
+(sentinel_amd/dist.py balanced_table; --sharding
 hash: splitmix64(res_id) % N), and each rank submits its shard in rank-local batches of ~--batch-events
 events (a step is S / N of them per rank), so the ranks advance independently: the decision path has
 no collective, and only the per-second MetricNode all-gather (RCCL) inside the timed chunks and the
@@ -122,9 +124,17 @@ def shifted_batch(base64, a: int, e: int, copy: int, tspan: int, n_base: int, ou
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.shard:
+        # `bench.py --gpus N` alone: start the N ranks here (sentinel_amd/launch.py), before anything imports
+        # torch -- this parent never touches a GPU; rank 0 prints the JSON line
+        from sentinel_amd.launch import launch_ranks
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not args.shard and world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d: launch one process per GPU (torchrun "
+                 "--nproc-per-node %d, or bench.py --gpus %d alone)" % (args.gpus, world, args.gpus, args.gpus))
     import torch
     # SG_BENCH_GLOO=1 rehearses the multi-rank path on a one-GPU box: gloo instead of RCCL, every rank on
     # device local % device_count (never used for a reported number)
@@ -159,8 +169,11 @@ def main():
     me = shard[0] if shard else rank
     table = None
     if nparts > 1:
-        if args.sharding == "balanced":  # every rank computes the same table from the same trace
-            table = D.balanced_table(np.bincount(ev["res_id"], minlength=args.resources), nparts)
+        # every rank computes the same table from the same history window: the event counts of the first
+        # global batch only (a router knows past load, not the future), so 7/8 of the timed events are
+        # batches the partition never saw (not the timed trace)
+        if args.sharding == "balanced":
+            table = D.balanced_table(np.bincount(ev["res_id"][:gb], minlength=args.resources), nparts)
         mine, pos = D.shard_stream(ev, nparts, me, table)
     else:
         mine = ev
@@ -275,8 +288,10 @@ def main():
         entries += float(sum(p[2] for p in plan))
         touched += float(sum(p[3] for p in plan))
         events += float(sum(p[1] for p in plan))
+    n_untimed = 0
     if dist is not None and n_gather == 0:  # at least one all-gather per run, untimed
         rows_gathered += gather_metrics(plan[-1][4])
+        n_untimed = 1
     stage_ms = np.array(stage_rows)
     if dist is not None:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
@@ -347,7 +362,8 @@ def main():
                        "events_per_step": events / steps, "entries_per_step": entries / steps,
                        "resources_touched_per_batch": touched / nb, "base_batches": B,
                        "timed_chunks": chunks, "rank_local_batches_per_step": per_step,
-                       "parallelism": ("resource-sharded x%d (%s)" % (world, "balanced by event counts"
+                       "parallelism": ("resource-sharded x%d (%s)" % (world, "balanced by the event counts of a "
+                                                                      "history window: base batch 0 of %d" % B
                                                                       if args.sharding == "balanced" else
                                                                       "splitmix64(res_id) %% %d" % world))
                                       if world > 1 else "one GPU",
@@ -369,7 +385,8 @@ def main():
             "h2d": {"GBps": n_base * 24 / (h2d_ms / 1e3) / 1e9, "pcie_inclusive_entries_per_s":
                     entries / (elapsed + h2d_ms / 1e3 * events / max(1, n_base) / world),
                     "note": "pinned host -> HBM copy of the events, measured on the base trace; not in value"},
-            "metric_gathers": {"count": n_gather, "rows": rows_gathered} if world > 1 else None,
+            "metric_gathers": {"count": n_gather + n_untimed, "timed": n_gather, "rows": rows_gathered}
+                              if world > 1 else None,
             "rehearsal": ("gloo, all ranks on one GPU: NOT a measurement" if rehearse else
                           "rank %d of %d alone on one GPU (per-rank step of an N-GPU run): NOT a measurement" % shard
                           if shard else None),

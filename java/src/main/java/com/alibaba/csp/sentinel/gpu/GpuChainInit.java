@@ -17,14 +17,34 @@ import com.alibaba.csp.sentinel.slotchain.SlotChainProvider;
  * (InitExecutor runs every InitFunc from Env's static initialiser, before CtSph builds any chain:
  * core/Env.java:33-38, core/init/InitExecutor.java:40-63) and installs {@link GpuSlotChainBuilder} as the
  * provider's resolved builder, then checks that a freshly built chain decides through {@link GpuDecisionSlot}.
- * If either step fails it says so in the Sentinel record log and on stderr and throws, so a process that would
- * silently run the reference slots on the JVM is visible at start-up.
+ *
+ * <p>It never throws.  InitExecutor.doInit catches an InitFunc's exception and stops running every later one
+ * (core/init/InitExecutor.java:51-62) -- the parameter extension's callback registration, the transport, the
+ * heartbeat -- which would leave a half-initialised process that looks alive.  A failure is instead recorded
+ * here ({@link #failure()}), said in the record log and on stderr, and every chain that does reach
+ * {@link GpuDecisionSlot} refuses its entries with {@link GpuUnavailableException} (a BlockException, so CtSph
+ * exits the entry and rethrows it to the caller: core/CtSph.java:157-166) instead of deciding anything.
  */
 @InitOrder(Integer.MIN_VALUE)
 public class GpuChainInit implements InitFunc {
 
+    private static volatile String failure;
+
+    /** Why the drop-in is not deciding on the GPU, or null when it is. */
+    public static String failure() {
+        return failure;
+    }
+
     @Override
-    public void init() throws Exception {
+    public void init() {
+        try {
+            install();
+        } catch (Throwable t) {   // never through InitExecutor: the other InitFuncs must still run
+            fail("GpuChainInit failed", t);
+        }
+    }
+
+    private static void install() {
         try {
             Field f = SlotChainProvider.class.getDeclaredField("builder");
             f.setAccessible(true);
@@ -36,6 +56,7 @@ public class GpuChainInit implements InitFunc {
             f.set(null, (SlotChainBuilder)new GpuSlotChainBuilder());
         } catch (ReflectiveOperationException | RuntimeException ex) {
             fail("cannot install GpuSlotChainBuilder into SlotChainProvider", ex);
+            return;
         }
         ProcessorSlotChain chain = SlotChainProvider.newSlotChain();
         for (AbstractLinkedProcessorSlot<?> s = chain.getNext(); s != null; s = s.getNext()) {
@@ -47,10 +68,16 @@ public class GpuChainInit implements InitFunc {
         fail("the slot chain SlotChainProvider builds has no GpuDecisionSlot", null);
     }
 
+    /** Records the failure (the first one wins) and says so; entries that reach GpuDecisionSlot are refused. */
     static void fail(String msg, Throwable cause) {
-        String m = "[sentinel-gpu] " + msg + ": decisions would run on the JVM slots instead of the GPU engine";
+        String m = "[sentinel-gpu] " + msg + ": the GPU engine does not decide; GpuDecisionSlot refuses entries";
+        if (failure == null) {
+            failure = m + (cause == null ? "" : " (" + cause + ")");
+        }
         RecordLog.warn(m, cause);
         System.err.println(m);
-        throw new IllegalStateException(m, cause);
+        if (cause != null) {
+            cause.printStackTrace();
+        }
     }
 }

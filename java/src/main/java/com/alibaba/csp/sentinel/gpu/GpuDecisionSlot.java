@@ -48,7 +48,19 @@ public class GpuDecisionSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
     @Override
     public void entry(Context context, ResourceWrapper resourceWrapper, DefaultNode node, int count,
                       boolean prioritized, Object... args) throws Throwable {
-        GpuEngine eng = GpuEngine.get();
+        // fail closed and visibly: a drop-in that could not take over the path refuses the entry (a
+        // BlockException the caller sees) rather than pass it with no rule checked
+        String down = GpuChainInit.failure();
+        if (down != null) {
+            throw new GpuUnavailableException(down);
+        }
+        GpuEngine eng;
+        try {
+            eng = GpuEngine.get();
+        } catch (RuntimeException ex) {
+            GpuChainInit.fail("engine creation failed", ex);
+            throw new GpuUnavailableException(GpuChainInit.failure());
+        }
         String name = resourceWrapper.getName();
         if (count < 0 || count > 0xFFFF) {
             throw new IllegalArgumentException("sentinel_gpu: acquire count " + count + " outside [0, 65535]");

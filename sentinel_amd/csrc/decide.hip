@@ -131,8 +131,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  const Prog* __restrict__ prog, const uint32_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
-                                                 uint32_t nblk, uint32_t pq_ok, const uint32_t* __restrict__ bflags,
-                                                 uint32_t pq_wide) {
+                                                 uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
@@ -2990,11 +2989,11 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 // mp: the segment count on the device; mb: an upper bound of it (the grid)
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, const uint32_t* bflags, uint32_t pq_wide, hipStream_t st) {
+                          uint32_t pq_ok, uint32_t pq_wide, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, bflags, pq_wide);
+                       blkcnt, nblk, pq_ok, pq_wide);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

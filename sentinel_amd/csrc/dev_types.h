@@ -336,8 +336,9 @@ struct DevState {
 };
 
 enum : uint32_t { BF_PRIORITIZED = 1,
-                  BF_EXIT_ARGS = 2,     // an EXIT releases thread counts (SG_F_EXIT_ARGS): no k_pq this batch
-                  BF_PTAB_FULL = 4, BF_BAD_RES = 8, BF_BAD_REF = 16,
+                  BF_PQ_INVARIANT = 2,  // k_pq: a tile's presorted key subset is not what it must be (internal error)
+                  BF_PTAB_FULL = 4,     // a param map could not place a key (the map then holds a ghost entry)
+                  BF_BAD_RES = 8, BF_BAD_REF = 16,
                   BF_BACKWARD = 32, BF_TSPAN = 64,
                   BF_BAD_ARGS = 512,    // an sg_event_ext names args outside the table, or more than SG_MAX_ARGS
                   BF_AUX_FULL = 1024,   // the origin / context node pool is full

@@ -47,7 +47,7 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
                       uint32_t* part, uint32_t* nseg);
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, const uint32_t* bflags, uint32_t pq_wide, hipStream_t st);
+                          uint32_t pq_ok, uint32_t pq_wide, hipStream_t st);
 // param.hip
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
@@ -478,6 +478,7 @@ struct sg_engine {
     int last = -1;               // slot of the last batch submitted
     hipStream_t gstream = nullptr;
     std::vector<std::array<double, 4>> tlog;  // per batch [group, decide, post, total] ms, by collect()
+    std::string fatal;           // non-empty: a batch left device state inconsistent; every later submit fails
     uint32_t* d_prio = nullptr;  // [res] sticky PM_* marks (DevState.prio)
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
     AuxSlot* d_auxtab = nullptr;
@@ -655,7 +656,13 @@ static int collect(sg_engine* e, int k) {
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
-    if (bflags & BF_PTAB_FULL) return fail(SG_ECAPACITY, "a hot-parameter map table could not place a key");
+    // A map that could not place a key has already committed its ring bit and live count (a ghost entry), and a
+    // failed k_pq invariant leaves its maps in an unknown state: the engine refuses every later batch.
+    if (bflags & BF_PQ_INVARIANT)
+        e->fatal = "internal error: a k_pq tile's presorted key subset did not match its accesses";
+    else if (bflags & BF_PTAB_FULL)
+        e->fatal = "a hot-parameter map table could not place a key (its map holds a ghost entry)";
+    if (bflags & (BF_PQ_INVARIANT | BF_PTAB_FULL)) return fail(SG_ECAPACITY, e->fatal + " -- engine unusable");
     return SG_OK;
 }
 // every batch in flight done (called by the API functions that read or write engine state)
@@ -1709,6 +1716,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                        uint64_t n_args, uint32_t* out) {
     if (!e || (n && (!ev || !out))) return fail(SG_EINVAL, "null argument");
     if (n_args && !args) return fail(SG_EINVAL, "null args table");
+    if (!e->fatal.empty()) return fail(SG_ESTATE, e->fatal + " -- engine unusable, recreate it");
     if (n == 0) return SG_OK;
     if (n > e->cfg.max_batch_events || n >= (1ull << 31)) return fail(SG_EINVAL, "batch larger than max_batch_events");
     HIPCHK(hipSetDevice(e->device));
@@ -1802,7 +1810,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         j4_max = std::min<uint32_t>(j4_max, 4096);
     }
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
-                          force_lane ? 1 : 0, e->d_blkcnt, (ext || !e->pq_on) ? 0u : 1u, e->d_bsmall + 0, e->pq_wide, gs));
+                          force_lane ? 1 : 0, e->d_blkcnt, (ext || !e->pq_on) ? 0u : 1u, e->pq_wide, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets

@@ -121,7 +121,6 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             if (e.flags & SG_F_BLOCKED_UPSTREAM) mark |= PM_LANE;
         } else {
             if (e.kind == SG_EV_EXIT) {
-                if (e.flags & SG_F_EXIT_ARGS) fl |= BF_EXIT_ARGS;
                 const int64_t raw = (int64_t)(e.aux >> 48);
                 r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
             }

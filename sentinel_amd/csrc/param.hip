@@ -460,7 +460,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
 #pragma unroll
         for (int q = 0; q < PQ_EPL; ++q)
             if (ki[q] != 0xFFFFFFFFu) { sh.skey[o] = kk[q]; sh.sidx[o] = ki[q]; ++o; }
-        if (tot != na) atomicOr(bflags, BF_PTAB_FULL);  // not the subset it must be: fails the batch loudly
+        if (tot != na) atomicOr(bflags, BF_PQ_INVARIANT);  // not the subset it must be: fails the engine loudly
     }
     for (uint32_t i = na + tid; i < P; i += HW) { sh.skey[i] = PK_EMPTY; sh.sidx[i] = 0xFFFFFFFFu; }
     pq_reserve<NW>(sh, mk, S, na);

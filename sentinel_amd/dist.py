@@ -38,7 +38,7 @@ def shard_of(res_ids, world: int, table=None) -> np.ndarray:
     """Owning rank of each resource: table[res_id] where a ShardMap table gives one (>= 0), else
     splitmix64(res_id) % world."""
     h = (splitmix64(res_ids) % np.uint64(world)).astype(np.int64)
-    if table is None:
+    if table is None or len(table) == 0:  # an empty table places nothing: every resource by the hash
         return h
     r = np.asarray(res_ids, dtype=np.int64)
     t = np.where(r < len(table), table[np.minimum(r, len(table) - 1)], -1)

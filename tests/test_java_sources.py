@@ -139,7 +139,34 @@ def test_init_func_makes_the_builder_deterministic():
     if os.path.exists(ref):  # the field the InitFunc sets is the one newSlotChain() returns from
         txt = open(ref).read()
         assert "private static volatile SlotChainBuilder builder" in txt and "return builder.build();" in txt
-    assert "instanceof GpuDecisionSlot" in src and "throw new IllegalStateException" in src
+    assert "instanceof GpuDecisionSlot" in src
+
+
+def _code(text):
+    text = re.sub(r'"(\\.|[^"\\])*"', '""', text)
+    return re.sub(r"/\*.*?\*/|//[^\n]*", "", text, flags=re.S)
+
+
+def test_init_failure_refuses_entries_instead_of_throwing():
+    # InitExecutor.doInit catches an InitFunc's exception and stops running the later ones
+    # (core/init/InitExecutor.java:51-62), so GpuChainInit must never throw; a failure poisons the decision slot,
+    # which refuses entries with a BlockException (CtSph exits and rethrows those, core/CtSph.java:157-166)
+    ref = "/root/reference/sentinel-core/src/main/java/com/alibaba/csp/sentinel/init/InitExecutor.java"
+    if os.path.exists(ref):
+        txt = open(ref).read()
+        assert "w.func.init();" in txt and "catch (Exception ex)" in txt  # the loop is inside the catch
+    init = _code(open(os.path.join(JAVA, "GpuChainInit.java")).read())
+    assert "throw " not in init                                        # no exception reaches InitExecutor
+    assert re.search(r"public void init\(\)\s*\{\s*try\s*\{\s*install\(\);\s*\}\s*catch \(Throwable", init)
+    assert "failure = " in init and "public static String failure()" in init
+    exc = _code(open(os.path.join(JAVA, "GpuUnavailableException.java")).read())
+    assert "class GpuUnavailableException extends BlockException" in exc
+    slot = _code(open(os.path.join(JAVA, "GpuDecisionSlot.java")).read())
+    body = slot[slot.index("public void entry("):]
+    body = body[:body.index("String name = resourceWrapper.getName();")]
+    # the poison check is the first thing an entry does, and an engine that cannot be created poisons too
+    assert re.search(r"GpuChainInit\.failure\(\);\s*if \(down != null\)\s*\{\s*throw new GpuUnavailableException", body)
+    assert "GpuChainInit.fail(" in body and body.count("throw new GpuUnavailableException") == 2
 
 
 def test_java_sources_are_balanced():
