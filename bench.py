@@ -341,7 +341,7 @@ def main():
         del buf, base, base64, out
         eng.close()
         torch.cuda.empty_cache()
-        configs = config_lines(dev)
+        configs = config_lines(dev, (w, ev))
 
     if rank == 0:
         line = {
@@ -428,45 +428,148 @@ CONFIGS = [
     (5, 12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
      "C5: 10k resources, ParamFlow QPS rules (20 % throttle) over 10M Zipf values"),
 ]
+EXT_NOTE = ("sg_submit_ex, the Java drop-in's call: every event in one of 4 named contexts (ContextUtil.enter) from "
+            "one of 16 origins, uniformly (an EXIT carries its ENTRY's); origin StatisticNodes and context "
+            "DefaultNodes kept on the device")
 
 
-def config_lines(dev):
+def run_batches(eng, ev, gb, dev, ext=None, args=None):
+    """Batch 0 untimed, the rest back to back through the pipeline; inputs (events, ext, args) in HBM."""
+    import torch
+    nb = (len(ev) + gb - 1) // gb
+    cuts = [min(len(ev), b * gb) for b in range(nb + 1)]
+    buf = torch.from_numpy(np.ascontiguousarray(ev).view(np.uint8)).to(dev)
+    xb = torch.from_numpy(np.ascontiguousarray(ext).view(np.uint8)).to(dev) if ext is not None else None
+    ab = torch.from_numpy(np.ascontiguousarray(args).view(np.uint8)).to(dev) if args is not None else None
+    out = torch.empty(gb, dtype=torch.int32, device=dev)
+    p0 = buf.data_ptr()
+
+    def sub(b, sync):
+        if xb is None:
+            eng.submit_ptr(p0 + cuts[b] * 24, cuts[b + 1] - cuts[b], out.data_ptr(), sync=sync)
+        else:
+            eng.submit_ex_ptr(p0 + cuts[b] * 24, xb.data_ptr() + cuts[b] * 16, cuts[b + 1] - cuts[b], out.data_ptr(),
+                              sync=sync, args_ptr=ab.data_ptr() if ab is not None else 0,
+                              n_args=len(args) if args is not None else 0)
+    sub(0, True)
+    eng.timing_log()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(1, nb):
+        sub(b, False)
+    eng.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = np.array(eng.timing_log())
+    ent = int((ev[cuts[1]:]["kind"] == 0).sum())
+    del buf, xb, ab, out
+    torch.cuda.empty_cache()
+    return {"value": ent / dt, "unit": "entries/s", "batches_timed": nb - 1, "batch_events": gb, "entries_timed": ent,
+            "ms_per_batch": dt / (nb - 1) * 1e3, "stage_ms_mean": {"group": float(st[:, 0].mean()),
+                                                                   "decide": float(st[:, 1].mean()),
+                                                                   "post": float(st[:, 2].mean())}}
+
+
+def param_args(ev):
+    """C5's argument through the sg_submit_ex table: args = {args[0]} for every ENTRY (its interned key)."""
+    from sentinel_amd import _abi as A
+    ent = ev["kind"] == A.EV_ENTRY
+    ext = np.zeros(len(ev), dtype=A.EXT_DTYPE)
+    ext["arg_off"] = np.arange(len(ev), dtype=np.uint32)
+    ext["n_args"] = ent.astype(np.uint32)
+    table = np.zeros(len(ev), dtype=A.ARG_DTYPE)
+    table["key"] = ev["aux"]
+    table["kind"] = np.where(ent, A.ARG_SCALAR, A.ARG_NULL)
+    return ext, table
+
+
+def config_lines(dev, c4=None):
+    """The SURVEY.md configs besides the headline: C2, C3, C5; with c4 = (workload, events) of the headline trace,
+    C4 and C4-ext on its first 3 global batches (the same events through sg_submit and sg_submit_ex), C5-ext, and
+    the drop-in's operating point (dropin_line)."""
     import torch
     from sentinel_amd import engine as E
     from sentinel_amd import tracegen as T
     rows = []
+    if c4 is not None:
+        w, ev = c4
+        gb = 1 << 25
+        sub = ev[:3 * gb]
+        for ext_on in (False, True):
+            eng = E.Engine(device=dev.index, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
+                           status_ring_log2=28, max_batch_events=gb, aux_node_capacity=(1 << 24) if ext_on else 1 << 16)
+            w.install(eng)
+            ext = None
+            if ext_on:
+                io, ic = w.intern_names(eng)
+                ext = T.ext_for(sub, io, ic, seed=T.SEED_BASE + 44)
+            r = run_batches(eng, sub, gb, dev, ext=ext)
+            r.update({"config": "C4%s: 1M resources, QPS DefaultController + DegradeRule, first 3 batches of the "
+                                "headline trace" % ("-ext" if ext_on else ""), "resources": w.n_res})
+            if ext_on:
+                r["note"] = EXT_NOTE
+            rows.append(r)
+            eng.close()
+            torch.cuda.empty_cache()
     for cfg, n_entries, gb, kw, var, name in CONFIGS:
         w = T.Workload(cfg, seed=T.SEED_BASE + cfg, n_entries=n_entries, variant=var)
         ev = w.events
-        nb = (len(ev) + gb - 1) // gb
-        cuts = [min(len(ev), b * gb) for b in range(nb + 1)]
-        eng = E.Engine(device=dev.index, max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0,
-                       max_batch_events=gb, **kw)
-        w.install(eng)
-        buf = torch.from_numpy(np.ascontiguousarray(ev).view(np.uint8)).to(dev)
-        out = torch.empty(gb, dtype=torch.int32, device=dev)
-        p0 = buf.data_ptr()
-        eng.submit_ptr(p0, cuts[1], out.data_ptr(), sync=True)  # the first batch, untimed
-        eng.timing_log()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for b in range(1, nb):
-            eng.submit_ptr(p0 + cuts[b] * 24, cuts[b + 1] - cuts[b], out.data_ptr(), sync=False)
-        eng.sync()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        st = np.array(eng.timing_log())
-        timed = ev[cuts[1]:]
-        ent = int((timed["kind"] == 0).sum())
-        rows.append({"config": name, "value": ent / dt, "unit": "entries/s", "batches_timed": nb - 1,
-                     "batch_events": gb, "entries_timed": ent, "ms_per_batch": dt / (nb - 1) * 1e3,
-                     "stage_ms_mean": {"group": float(st[:, 0].mean()), "decide": float(st[:, 1].mean()),
-                                       "post": float(st[:, 2].mean())}, "resources": w.n_res})
-        eng.close()
+        for ext_on in ((False, True) if cfg == 5 else (False,)):
+            eng = E.Engine(device=dev.index, max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0,
+                           max_batch_events=gb, aux_node_capacity=1 << 20, **kw)
+            w.install(eng)
+            ext = args = None
+            if ext_on:
+                io, ic = w.intern_names(eng)
+                ext, args = param_args(ev)
+                oc = T.ext_for(ev, io, ic, seed=T.SEED_BASE + 45)
+                ext["origin_id"], ext["context_id"] = oc["origin_id"], oc["context_id"]
+            r = run_batches(eng, ev, gb, dev, ext=ext, args=args)
+            r.update({"config": name if not ext_on else name.replace("C5:", "C5-ext:") + "; args[0] from the table",
+                      "resources": w.n_res})
+            if ext_on:
+                r["note"] = EXT_NOTE
+            rows.append(r)
+            eng.close()
+            torch.cuda.empty_cache()
         w.close()
-        del buf, out
-        torch.cuda.empty_cache()
+    if c4 is not None:
+        rows.append(dropin_line(dev, *c4))
     return rows
+
+
+def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400):
+    """The Java batcher's operating point (java/.../GpuEngine.java): batches of <= 65,536 events
+    from pageable host memory, sg_submit_ex synchronous (one batch decided and back before the next), contexts and
+    origins on every event.  Entries/s and the per-batch latency distribution (host wall clock around each call)."""
+    import torch
+    from sentinel_amd import engine as E
+    from sentinel_amd import tracegen as T
+    eng = E.Engine(device=dev.index, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
+                   status_ring_log2=28, max_batch_events=batch, aux_node_capacity=1 << 22)
+    w.install(eng)
+    io, ic = w.intern_names(eng)
+    sub = np.ascontiguousarray(ev[:batch * (n_batches + 20)])
+    ext = T.ext_for(sub, io, ic, seed=T.SEED_BASE + 46)
+    lat = []
+    ent = 0
+    for b in range(n_batches + 20):
+        e = sub[b * batch:(b + 1) * batch]
+        t = time.perf_counter()
+        eng.submit_ex(e, ext[b * batch:(b + 1) * batch])
+        dt = time.perf_counter() - t
+        if b >= 20:  # warm-up batches untimed
+            lat.append(dt)
+            ent += int((e["kind"] == 0).sum())
+    lat = np.array(lat)
+    eng.close()
+    torch.cuda.empty_cache()
+    return {"config": "drop-in operating point: C4 trace, %d-event batches from pageable host memory, sg_submit_ex "
+                      "synchronous" % batch, "value": ent / lat.sum(), "unit": "entries/s", "batches_timed": n_batches,
+            "batch_events": batch, "latency_ms": {"p50": float(np.percentile(lat, 50) * 1e3),
+                                                  "p99": float(np.percentile(lat, 99) * 1e3),
+                                                  "mean": float(lat.mean() * 1e3)},
+            "note": EXT_NOTE + "; PCIe copies of events, ext and decisions inside every call"}
 
 
 def cpu_share() -> int:

@@ -232,6 +232,11 @@ class Oracle:
         rc = lib().or_read_origin_node(self.h, res, origin.encode(), C.byref(st))
         return None if rc != 0 else A.node_state_to_numpy(st)
 
+    def read_default_node(self, res: int, context: str):
+        st = A.SgNodeState()
+        rc = lib().or_read_default_node(self.h, res, context.encode(), C.byref(st))
+        return None if rc != 0 else A.node_state_to_numpy(st)
+
     def metric(self, res: int, now: int, which: int) -> float:
         return lib().or_node_metric(self.h, res, int(now), which)
 
@@ -305,6 +310,21 @@ class PartitionedOracle:
             out[p] = o
         self.n_events += len(events)
         return out
+
+    def submit_ex(self, events: np.ndarray, ext: np.ndarray) -> np.ndarray:
+        """sg_submit_ex without an args table (contexts and origins only): each shard gets its events' ext rows."""
+        ev = np.ascontiguousarray(events, dtype=A.EVENT_DTYPE)
+        parts, pos = self.router.route(ev)
+        exs = [np.ascontiguousarray(ext[p]) for p in pos]
+        outs = list(self.pool.map(lambda r: self.orcs[r].submit_ex(parts[r], exs[r]), range(self.T)))
+        out = np.zeros(len(events), dtype=np.uint32)
+        for p, o in zip(pos, outs):
+            out[p] = o
+        self.n_events += len(events)
+        return out
+
+    def orc_of(self, res: int):
+        return self.orcs[int(self.D.shard_of(res, self.T))]
 
     def read_node(self, res: int) -> dict:
         return self.orcs[int(self.D.shard_of(res, self.T))].read_node(res)

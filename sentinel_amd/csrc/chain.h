@@ -97,20 +97,6 @@ __device__ __forceinline__ void node_load(Node& N, const DevState& S, uint32_t r
     N.mst = 0;
     N.bor = S.prio && (S.prio[res] & PM_PRIO) ? S.borrow + (uint64_t)res * 4 : nullptr;
 }
-// an origin StatisticNode / context DefaultNode (AuxNode); its borrow ring starts empty, so it is always
-// consulted (a bucket borrows only what a prioritized entry on this very node put there)
-__device__ __forceinline__ void node_load_aux(Node& N, const AuxNode* a) {
-    N.sb[0] = a->sec[0];
-    N.sb[1] = a->sec[1];
-    N.thread = a->info.thread;
-    N.flags = a->info.flags;
-    N.exc_sum_sec = -1;
-    N.exc_sum = 0;
-    N.mslot = -1;
-    N.pfslot = -2;
-    N.mst = 0;
-    N.bor = const_cast<int64_t*>(a->borrow);
-}
 
 __device__ __forceinline__ void bkt_reset(Bkt& b, int64_t ws, int32_t max_rt) {
     b.ws = ws; b.pass = 0; b.block = 0; b.exc = 0; b.succ = 0; b.rt = 0; b.occ = 0; b.minrt = max_rt;
@@ -475,12 +461,6 @@ __device__ __forceinline__ void stat_trace(Node& N, const Ctx& C, int64_t t, int
         min_add(N, 0, 0, 0, 0, count, INT64_MAX);
         if (N.exc_sum_sec == t - t % 1000) N.exc_sum += count;
     }
-}
-
-__device__ __forceinline__ void node_store_aux(const Node& N, AuxNode* a) {
-    a->sec[0] = N.sb[0];
-    a->sec[1] = N.sb[1];
-    a->info.thread = N.thread;
 }
 
 __device__ __forceinline__ void node_store(const Node& N, const DevState& S, uint32_t res, uint32_t pflags) {

@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include "chain.h"
+#include "aux.h"
 #include "pmap.h"
 
 using namespace sg;
@@ -127,28 +128,56 @@ __global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ k
 // inside their limits, one lane per segment for everything else.  Per-block bin counts go to
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
+// Aux lists (sg_submit_ex batches; aux == null otherwise): the segments whose origin / context nodes the aux.hip
+// post-pass updates -- short ones one lane each (aux[0] = count, list ashort), long ones in pieces of AUX_PIECE
+// events (aux[1] = pieces, list apiece = seg << 32 | piece), and of those the segments of more than one piece,
+// whose pieces' partial results are merged (aux[2] = count, list amulti = seg << 32 | first piece).
+#define AUX_SHORT 256u
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t k) {  // one atomic per wave
+    uint32_t x = k;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)(threadIdx.x & 63) >= o) x += y;
+    }
+    const uint32_t tot = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 63 && tot) base = atomicAdd(ctr, tot);
+    base = __shfl(base, 63, 64);
+    return base + x - k;
+}
 __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const uint32_t* __restrict__ mp, uint64_t n,
                                                  const Prog* __restrict__ prog, const uint32_t* __restrict__ prio,
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
-                                                 uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide) {
+                                                 uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide, uint32_t* __restrict__ aux,
+                                                 uint32_t* __restrict__ ashort, uint64_t* __restrict__ apiece,
+                                                 uint64_t* __restrict__ amulti) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const uint32_t m = *mp;  // segment count (the grid covers an upper bound: no host round trip)
-    // k_pq runs in batches without sg_submit_ex context/args
     const bool pq = pq_ok && !force_lane;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    bool aux_short = false;
+    uint32_t aux_np = 0;
+    Seg sg;
     if (s < m) {
-        Seg sg = segs[s];
+        sg = segs[s];
         const uint32_t end = (s + 1 < m) ? segs[s + 1].start : (uint32_t)n;
         sg.len = end - sg.start;
         const Prog p = prog[sg.res];
+        const uint32_t pm = prio[sg.res];
+        // decided one lane per segment whatever the length: a live borrow ring (PM_PRIO), events only k_lane takes
+        // (PM_LANE), origin / context nodes the rules read (PX_ORIGIN / PX_CHAIN: k_lane<16> keeps them inline)
+        const bool lane_only = (pm & (PM_PRIO | PM_LANE)) != 0 || ((pm & PM_AUX) && (p.multi & (PX_ORIGIN | PX_CHAIN)));
+        const bool inline_aux = (pm & PM_AUX) && (lane_only || p.multi);  // k_lane<16> updates the nodes itself
         const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // PX_*: decided with 16-rule lanes
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
-                          !prio[sg.res] && !p.multi;
+                          !lane_only && !p.multi;
         uint32_t bin;
-        if (pq && (p.pflags & PF_PQ) && !prio[sg.res]) bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
+        if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS)))
+            bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
         // QPS-DefaultController heads on the 512-lane owner (open stretches), up to J8_MAX events: a longer one (one
         // rank's batch of a strong-scaling run can hold a single resource's 33M events, nearly all in frozen
         // stretches) goes faster through the 1024-lane owner (8-way rehearsal: slowest rank 3.58 vs 2.64 ms)
@@ -159,12 +188,26 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
             // k_lite: no param rules, <= 2 DefaultController flow stages (QPS or thread), <= 2 breakers
-            const bool lite = p.n_param == 0 && !p.multi && !prio[sg.res] && (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
-            bin = (lite ? BIN_LITE : (nr <= 4 && !(prio[sg.res] & PM_AUX)) ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
+            const bool lite = p.n_param == 0 && !p.multi && !lane_only && (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
+            bin = (lite ? BIN_LITE : (nr <= 4 && !inline_aux) ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
+        }
+        // k_lane<16> keeps a PM_AUX resource's nodes inline; on every other owner the post-pass does
+        const bool auxp = aux && (pm & PM_AUX) && !(bin >= BIN_LANE16 && bin < BIN_LANE16 + LANE_BINS);
+        if (auxp) {
+            if (sg.len <= AUX_SHORT) aux_short = true;
+            else aux_np = (sg.len + AUX_PIECE - 1) / AUX_PIECE;
         }
         const uint32_t rank = atomicAdd(&cnt[bin], 1u);
-        sg.bin = bin | (rank << 8);
+        sg.bin = bin | (auxp ? SEG_AUXP : 0u) | (rank << 8);
         segs[s] = sg;
+    }
+    if (aux) {  // (wave-uniform: every lane of the wave takes part)
+        const uint32_t o = wave_alloc(aux + 0, aux_short ? 1u : 0u);
+        if (aux_short) ashort[o] = s;
+        const uint32_t q = wave_alloc(aux + 1, aux_np);
+        for (uint32_t i = 0; i < aux_np; ++i) apiece[q + i] = ((uint64_t)s << 32) | i;
+        const uint32_t u = wave_alloc(aux + 2, aux_np > 1 ? 1u : 0u);
+        if (aux_np > 1) amulti[u] = ((uint64_t)s << 32) | q;
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) blkcnt[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
@@ -175,9 +218,9 @@ __global__ __launch_bounds__(256) void k_seg_order(Seg* __restrict__ segs, const
                                                    uint32_t* __restrict__ order) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= *mp) return;
-    const uint32_t v = segs[s].bin, bin = v & 0xFF;
+    const uint32_t v = segs[s].bin, bin = v & 0x7F;
     order[off[(uint64_t)bin * nblk + blockIdx.x] + (v >> 8)] = s;
-    segs[s].bin = bin;
+    segs[s].bin = v & 0xFF;  // the bin | SEG_AUXP
 }
 // per-bin first offsets (+ total) for the host: out[b] = off[b][0], out[N_BINS] = m
 __global__ void k_bin_offsets(const uint32_t* __restrict__ off, uint32_t nblk, const uint32_t* __restrict__ mp,
@@ -265,16 +308,22 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
 }
 // references into earlier batches, once those are decided: the ENTRY's status from the ring
 // (0xFF = not an ENTRY: an EXIT is then taken as the caller asserting the entry passed)
+// (sg_submit_ex: the record's x becomes the event's own origin / context node tag, as for an EXIT naming no ENTRY)
 __global__ void k_resolve(const uint32_t* __restrict__ prev, uint32_t np, const uint8_t* __restrict__ ring,
-                          SEv* __restrict__ recs) {
+                          SEv* __restrict__ recs, const uint32_t* __restrict__ vals, const sg_event_ext* __restrict__ ext) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np) return;
-    SEv r = recs[prev[i]];
+    const uint32_t p = prev[i];
+    SEv r = recs[p];
     const uint8_t st = ring[r.x];
     if (st == ST_NOT_ENTRY) r.code = r.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
     else r.code = (st == ST_PASS || st == ST_PASS_WAIT) ? RC_PASSED : RC_NOT;
     r.x = 0;
-    recs[prev[i]] = r;
+    if (ext) {
+        const sg_event_ext x = ext[vals[p] & 0x7FFFFFFFu];
+        if (!(x.origin_id >> TAG_ORIGIN_BITS)) r.x = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
+    }
+    recs[p] = r;
 }
 
 // decisions back to submission order; the status ring keeps every event's status for
@@ -547,40 +596,7 @@ __device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags
     }
 }
 
-// ---- origin StatisticNodes / context DefaultNodes (PX_ORIGIN / PX_CHAIN resources, k_lane<16> only)
-__device__ AuxNode* aux_get(const DevState& S, uint32_t res, uint32_t kind, uint32_t id, uint32_t* bflags) {
-    const unsigned long long key = ((unsigned long long)res << 32) | ((unsigned long long)kind << 31) | (id & 0x7FFFFFFFu);
-    uint64_t h = mix64(key) & S.aux_mask;
-    for (uint64_t probe = 0; probe <= S.aux_mask; ++probe) {
-        AuxSlot* s = &S.aux_tab[h];
-        unsigned long long k = __hip_atomic_load(&s->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == AUX_EMPTY) {
-            unsigned long long expect = AUX_EMPTY;
-            if (__hip_atomic_compare_exchange_strong(&s->key, &expect, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-                // keys of a resource are inserted by its owner lane only: nobody else reads this slot's idx
-                const uint32_t idx = atomicAdd(S.aux_count, 1u);
-                if (idx >= S.aux_cap) { atomicOr(bflags, BF_AUX_FULL); s->idx = NO_ID; return nullptr; }
-                AuxNode* a = &S.aux_pool[idx];
-                Bkt z;
-                z.ws = -1; z.pass = 0; z.block = 0; z.exc = 0; z.succ = 0; z.rt = 0; z.occ = 0; z.minrt = 0;
-                a->sec[0] = z; a->sec[1] = z;
-                for (int m = 0; m < 60; ++m) a->minb[m] = z;
-                a->borrow[0] = -1; a->borrow[1] = 0; a->borrow[2] = -1; a->borrow[3] = 0;
-                NodeInfo ni;
-                ni.thread = 0; ni.flags = 0; ni.exc_sum_sec = -1; ni.exc_sum = 0; ni.last_fetch = -1;
-                a->info = ni;
-                s->idx = idx;
-                return a;
-            }
-            k = expect;
-        }
-        if (k == key) return s->idx == NO_ID ? nullptr : &S.aux_pool[s->idx];
-        h = (h + 1) & S.aux_mask;
-    }
-    atomicOr(bflags, BF_AUX_FULL);
-    return nullptr;
-}
+// ---- origin StatisticNodes / context DefaultNodes kept inline by k_lane<16> (aux.h; the other owners' by aux.hip)
 // NodeSelectorSlot keeps a DefaultNode per (context, resource) for every entry (NodeSelectorSlot.java:134-176);
 // the device keeps those of named contexts always, and that of the default context while a CHAIN rule of the
 // resource names it (a CHAIN rule on sentinel_default_context starts from a fresh node)
@@ -598,11 +614,14 @@ __device__ void aux_stat(const DevState& S, const DevCfg& cfg, uint32_t res, uin
     if (!a) return;
     Node NA;
     node_load_aux(NA, a);
-    const Ctx CA{a->minb, cfg.max_rt, 0};
-    if (what == 2) NA.thread++;
-    else if (what == 3) stat_exit(NA, CA, t, cnt, rt);
-    else stat_entry(NA, CA, t, cnt, what == 1);
-    min_flush(NA, CA.minb);
+    if (what == 2) {
+        NA.thread++;
+    } else {
+        const int sl = sec_current(NA, t, cfg.max_rt);
+        if (what == 3) { sec_add(NA, sl, 0, 0, cnt, rt, 0, rt); NA.thread--; }
+        else if (what == 1) { NA.thread++; sec_add(NA, sl, cnt, 0, 0, 0, 0, INT64_MAX); aux_add_mpass(a, t, cnt); }
+        else sec_add(NA, sl, 0, cnt, 0, 0, 0, INT64_MAX);
+    }
     node_store_aux(NA, a);
 }
 
@@ -654,6 +673,51 @@ __device__ int relate_check(const DevState& S, const DevCfg& cfg, const DRule& r
     node_store(NB, S, b, pb.pflags);
     return rc;
 }
+// flow_can_pass (chain.h) on an origin node / DefaultNode: the minute window is the node's pass history (aux.h)
+__device__ __forceinline__ bool aux_flow_can_pass(Node& N, AuxNode* a, const DRule& r, RState& s, int64_t t, int acquire,
+                                                  int32_t max_rt, int64_t& wait) {
+    switch (r.behavior) {
+    case SG_CONTROL_BEHAVIOR_WARM_UP: {
+        sec_current(N, t, max_rt);
+        const int64_t pass_qps = SEC_SUM(N, t, pass);
+        warm_sync(r, s, t, aux_prev_pass(a, t));
+        const int64_t rest = s.a;
+        if (rest >= r.warning_token) return (double)(pass_qps + acquire) <= warm_qps(r, rest);
+        return (double)(pass_qps + acquire) <= r.count;
+    }
+    case SG_CONTROL_BEHAVIOR_RATE_LIMITER:
+        if (acquire <= 0) return true;
+        if (r.count <= 0) return false;
+        return rl_admit(s.c, rl_cost(r, s, acquire), t, r.max_queue, wait);
+    case SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER:
+        warm_sync(r, s, t, aux_prev_pass(a, t));
+        return rl_admit(s.c, rl_cost(r, s, acquire), t, r.max_queue, wait);
+    default: {
+        int32_t cur;
+        if (r.grade == SG_FLOW_GRADE_THREAD) cur = N.thread;
+        else { sec_current(N, t, max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
+        return !((double)j_iadd(cur, acquire) > r.count);
+    }
+    }
+}
+// default_can_pass_prio (chain.h) on an origin node / DefaultNode
+__device__ __forceinline__ int aux_default_prio(Node& N, AuxNode* a, const DRule& r, int64_t t, int acquire,
+                                                int32_t occupy_timeout, int32_t max_rt, int64_t& wait) {
+    int32_t cur;
+    if (r.grade == SG_FLOW_GRADE_THREAD) cur = N.thread;
+    else { sec_current(N, t, max_rt); cur = j_d2i((double)SEC_SUM(N, t, pass)); }
+    if (!((double)j_iadd(cur, acquire) > r.count)) return 1;
+    if (r.grade != SG_FLOW_GRADE_QPS) return 0;
+    const Ctx C{nullptr, max_rt, 0};  // tryOccupyNext reads the second window and the borrow ring only
+    const int64_t w = try_occupy_next(N, C, t, acquire, r.count, occupy_timeout);
+    if (w >= occupy_timeout) return 0;
+    const int bs = bor_current(N.bor, t + w);  // addWaitingRequest
+    if (bs >= 0) N.bor[2 * bs + 1] += acquire;
+    a->flags |= AUXF_BORROW;
+    aux_add_mpass(a, t, acquire);              // addOccupiedPass: minute PASS (and OCCUPIED_PASS, never read here)
+    wait = w;
+    return 2;
+}
 // the controller of one flow rule on an origin node / DefaultNode (1 pass, 0 block, 2 PriorityWait)
 __device__ int aux_check(const DevState& S, const DevCfg& cfg, const DRule& r, RState& s, uint32_t res, uint32_t kind,
                          uint32_t id, int64_t t, int cnt, uint32_t fl, int64_t& wait, uint32_t* bflags) {
@@ -661,16 +725,14 @@ __device__ int aux_check(const DevState& S, const DevCfg& cfg, const DRule& r, R
     if (!a) return 1;
     Node NA;
     node_load_aux(NA, a);
-    const Ctx CA{a->minb, cfg.max_rt, 0};
     int rc;
     if ((fl & SG_F_PRIORITIZED) && r.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) {
         int64_t w = 0;
-        rc = default_can_pass_prio(NA, CA, r, t, cnt, cfg.occupy_timeout, w);
+        rc = aux_default_prio(NA, a, r, t, cnt, cfg.occupy_timeout, cfg.max_rt, w);
         if (rc == 2) wait += w;
     } else {
-        rc = flow_can_pass(NA, CA, r, s, t, cnt, wait) ? 1 : 0;
+        rc = aux_flow_can_pass(NA, a, r, s, t, cnt, cfg.max_rt, wait) ? 1 : 0;
     }
-    min_flush(NA, CA.minb);
     node_store_aux(NA, a);
     return rc;
 }
@@ -2989,11 +3051,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 // mp: the segment count on the device; mb: an upper bound of it (the grid)
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, uint32_t pq_wide, hipStream_t st) {
+                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* apiece,
+                          uint64_t* amulti, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, apiece, amulti);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]
@@ -3021,9 +3084,10 @@ hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, c
     hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, st, spans, nspan, cap, recs, prog, rules, dec);
     return hipGetLastError();
 }
-hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st) {
+hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, const uint32_t* vals,
+                          const sg_event_ext* ext, hipStream_t st) {
     if (!np) return hipSuccess;
-    hipLaunchKernelGGL(k_resolve, dim3((np + 255) / 256), dim3(256), 0, st, prev, np, ring, recs);
+    hipLaunchKernelGGL(k_resolve, dim3((np + 255) / 256), dim3(256), 0, st, prev, np, ring, recs, vals, ext);
     return hipGetLastError();
 }
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,

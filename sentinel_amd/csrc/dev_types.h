@@ -50,10 +50,22 @@ __host__ __device__ inline uint32_t ni_tm(uint32_t idx) { return 1u << (NI_TM_SH
 // segments to the per-lane kernel
 enum : uint8_t {
     PM_PRIO = 1,         // a prioritized ENTRY was seen: the second window's borrow ring is live
-    PM_LANE = 2,         // an event only k_lane implements was seen: SG_F_BLOCKED_UPSTREAM, a NullContext
-    PM_AUX = 4           // an event carried an origin or a named context: the resource keeps its origin
-                         // StatisticNodes / context DefaultNodes (k_lane<16>) whatever its rules are
+    PM_LANE = 2,         // an event only k_lane implements was seen: SG_F_BLOCKED_UPSTREAM, a NullContext, an
+                         // origin id >= 2^20 (not packable into the record's node tag)
+    PM_AUX = 4,          // an event carried an origin or a named context: the resource keeps its origin
+                         // StatisticNodes / context DefaultNodes whatever its rules are.  Rules that read them
+                         // (PX_ORIGIN / PX_CHAIN) decide on k_lane<16>; otherwise the segment decides on its usual
+                         // owner and aux.hip updates the nodes from the committed verdicts afterwards
+    PM_ARGL = 8,         // an event's args[0] was a Collection / array (per-element checks: not k_pq's)
+    PM_XARGS = 16        // an EXIT released thread counts with args of its own (sg_submit_ex)
 };
+// SEv.x of an ENTRY (and of an EXIT / TRACE that names no ENTRY of this batch) in an sg_submit_ex batch: the
+// origin / context node tag of the event, origin id | context id << 20 (0: no origin, default context)
+#define TAG_ORIGIN_BITS 20u
+__host__ __device__ inline uint32_t tag_origin(uint32_t tag) { return tag & ((1u << TAG_ORIGIN_BITS) - 1); }
+__host__ __device__ inline uint32_t tag_ctx(uint32_t tag) { return tag >> TAG_ORIGIN_BITS; }
+// internal SEv.flags bits above the ABI's SG_F_*
+#define RF_OWN_ARGS 0x80u  // EXIT of sg_submit_ex with its own args: its args[0] key is in the key ring at its index
 
 struct NodeInfo {
     int32_t thread;      // StatisticNode.curThreadNum
@@ -82,7 +94,12 @@ struct Prog {
     uint32_t rule_off;
     uint8_t n_param, n_flow, n_degrade, pflags;
     uint32_t tm_base;    // thread-count maps of this resource: DevState.tmid[tm_base + paramIdx] (NO_ID: none)
-    uint32_t multi;      // PX_* bits
+    uint16_t multi;      // PX_* bits
+    uint16_t xf;         // XF_* bits
+};
+enum : uint16_t {
+    XF_PTHREAD = 1       // a THREAD-grade param rule is checked (k_pq resolves an EXIT's release against its ENTRY's
+                         // check of the same tile by key: an EXIT with its own args (PM_XARGS) is k_lane's)
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)
@@ -204,8 +221,9 @@ struct Seg {
     uint32_t res;
     uint32_t start;
     uint32_t len;
-    uint32_t bin;    // BIN_*
+    uint32_t bin;    // BIN_* (| SEG_AUXP)
 };
+#define SEG_AUXP 0x80u  // Seg.bin: the segment's origin / context nodes are updated by the aux.hip post-pass
 
 // ---- token server (cluster.hip): ClusterMetric per flowId + the namespace GlobalRequestLimiter
 enum { CF_PASS = 0, CF_BLOCK, CF_PASS_REQ, CF_BLOCK_REQ, CF_OCC_PASS, CF_OCC_BLOCK, CF_WAITING, CF_N };  // ClusterFlowEvent
@@ -275,22 +293,44 @@ struct Span {
 #define BST_STATIC 0x80000000u  // bst[] flag: the block holds an EXIT/TRACE that is effective without a link
 #define BST_CNT 0x7FFFFFFFu
 
-// Origin StatisticNodes and context DefaultNodes of the resources that read them (PX_ORIGIN / PX_CHAIN):
-// a pool of nodes and an open-addressing index keyed (resource, kind, id)
+// Origin StatisticNodes (ClusterNode.originCountMap) and context DefaultNodes (NodeSelectorSlot): one
+// open-addressing table of nodes keyed (resource, kind, id), 256 B a node, claimed by CAS on the key.
+//
+// What a node keeps is what the path can read of it.  Its second window is a full 2 x 500 ms LeapArray (flow
+// rules on an origin / context read passQps, threadNum; StatisticSlot updates it).  Of its minute window the
+// only reader is WarmUpController's previousPassQps (LeapArray.getPreviousWindow: the pass of the second before
+// now, LeapArray.java:216-234) and addOccupiedPass / addPassRequest only add to it, so the node keeps, per
+// second parity, the latest second in which pass was added and that second's pass: the previous second's pass
+// is found iff it is the latest pass-second of its parity, as a 60-slot ring would give it (the other minute
+// fields of an origin / context node are never read: MetricTimerListener exports ClusterNodes only).
 struct AuxNode {
-    Bkt sec[2];
-    Bkt minb[60];
-    int64_t borrow[4];   // FutureBucketLeapArray {ws, pass} x 2 (prioritized entries on this node)
-    NodeInfo info;       // thread; flags bit 0 = borrow ring live
+    unsigned long long key;  // res << 32 | kind << 31 | id; AUX_EMPTY = free
+    int32_t thread;          // curThreadNum
+    uint32_t flags;          // AUXF_*
+    int64_t mws[2];          // minute window, per second parity: the latest second with pass added (-1: none)
+    int64_t mpass[2];        //   and its pass
+    int64_t pad0[2];
+    Bkt sec[2];              // rollingCounterInSecond
+    int64_t borrow[4];       // FutureBucketLeapArray {ws, pass} x 2 (prioritized entries on this node)
+    int64_t pad1[4];
 };
-static_assert(sizeof(AuxNode) == 4032, "AuxNode size");
+static_assert(sizeof(AuxNode) == 256, "AuxNode size");
+#define AUXF_BORROW 1u       // the node's borrow ring was written (a reset reads it)
 #define AUX_EMPTY 0xFFFFFFFFFFFFFFFFull
 enum : uint32_t { AUX_ORIGIN = 0, AUX_CONTEXT = 1 };
-struct AuxSlot {
-    unsigned long long key;  // res << 32 | kind << 31 | id; AUX_EMPTY = free (claimed by CAS)
-    uint32_t idx;            // pool index, NO_ID until the claimer published it
-    uint32_t pad;
+// the aux.hip post-pass: one node's updates of a batch (or of a piece of a segment), merged per 500 ms bucket
+// parity as LeapArray.currentWindow merges them (a later window replaces, the same window adds)
+struct AuxAcc {
+    uint32_t key;            // kind << 31 | id
+    int32_t thread;          // curThreadNum delta
+    int64_t W[2];            // second window: latest window start per 500 ms parity (-1: none)
+    uint64_t s[2][4];        //   pass, block, succ, rt added at W[p]
+    uint32_t minrt[2];       //   min rt at W[p] (0xFFFFFFFF: none)
+    int64_t MW[2];           // minute window: latest second with pass added, per second parity (-1: none)
+    uint64_t mpass[2];
 };
+static_assert(sizeof(AuxAcc) == 128, "AuxAcc size");
+#define AUX_PIECE 4096u      // aux.hip: events of a long segment per piece workgroup
 
 struct DevState {
     Bkt* sec;
@@ -327,9 +367,8 @@ struct DevState {
     // sg_submit_ex: per-event context and args (null: none), origin / context nodes
     const sg_event_ext* ext;  // [submission index]
     const sg_arg* args;
-    AuxSlot* aux_tab;
-    AuxNode* aux_pool;
-    uint32_t* aux_count;      // nodes taken from the pool
+    AuxNode* aux_tab;         // origin / context nodes (open addressing, aux_mask + 1 slots)
+    uint32_t* aux_count;      // nodes claimed
     uint32_t aux_cap;
     uint32_t max_ctx;         // context ids above this are NullContexts
     uint64_t aux_mask;

@@ -47,7 +47,13 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
                       uint32_t* part, uint32_t* nseg);
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, uint32_t pq_wide, hipStream_t st);
+                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* apiece,
+                          uint64_t* amulti, hipStream_t st);
+// aux.hip
+hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
+                      const uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg, int64_t t0,
+                      const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
+                      uint32_t* bflags, hipStream_t st);
 // param.hip
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
@@ -59,7 +65,8 @@ hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t*
                          uint32_t epoch, uint32_t* bflags, hipStream_t st);
 hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,
                        const DRule* rules, uint32_t* dec, hipStream_t st);
-hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, hipStream_t st);
+hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, const uint32_t* vals,
+                          const sg_event_ext* ext, hipStream_t st);
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
@@ -468,6 +475,10 @@ struct sg_engine {
         sg_event_ext* d_ext = nullptr; // sg_submit_ex host inputs staged in HBM
         sg_arg* d_args = nullptr;
         uint64_t ext_cap = 0, args_cap = 0;
+        // sg_submit_ex: the aux.hip post-pass lists k_seg_bin builds (counts in d_bsmall[130..132])
+        uint32_t* d_ashort = nullptr;
+        uint64_t *d_apiece = nullptr, *d_amulti = nullptr;
+        uint64_t aux_cap_n = 0;
         Link* d_link = nullptr;        // frozen-stretch skipping side tables (DevState.link/bst/pend/spans)
         uint32_t *d_bst = nullptr, *d_pend = nullptr;
         Span* d_spans = nullptr;
@@ -481,10 +492,14 @@ struct sg_engine {
     std::string fatal;           // non-empty: a batch left device state inconsistent; every later submit fails
     uint32_t* d_prio = nullptr;  // [res] sticky PM_* marks (DevState.prio)
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
-    AuxSlot* d_auxtab = nullptr;
-    AuxNode* d_auxpool = nullptr;
+    AuxNode* d_auxtab = nullptr;
     uint32_t* d_auxcnt = nullptr;
     uint64_t aux_mask = 0;
+    // the aux.hip post-pass: partial node results of the pieces of long segments (decide stage: one set)
+    AuxAcc* d_auxpool = nullptr;
+    uint64_t* d_auxmeta = nullptr;
+    uint32_t auxpool_cap = 0;
+    uint64_t auxmeta_cap = 0;
     // ContextUtil names: origins (0 = "") and contexts (0 = sentinel_default_context), first-intern order
     std::unordered_map<std::string, uint32_t> origin_ids, context_ids;
     std::unordered_map<std::string, int> rule_names;  // limitApp / CHAIN ref strings the flow rules name
@@ -580,7 +595,8 @@ static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
     dfree(B.d_prev); dfree(B.d_bsmall);
     dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans); dfree(B.d_ext); dfree(B.d_args);
-    B.ext_cap = B.args_cap = 0;
+    dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti);
+    B.ext_cap = B.args_cap = B.aux_cap_n = 0;
     B.d_link = nullptr; B.d_bst = B.d_pend = nullptr; B.d_spans = nullptr;
     B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
     B.d_hist = B.d_part = B.d_flag = B.d_pos = B.d_order = nullptr;
@@ -857,12 +873,19 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             for (int i = 0; i < p.n_param && pq; ++i) {
                 const DRule& d = rules[p.rule_off + i];
                 if (d.param_idx < 0) pq = false;
-                else if (d.behavior == PB_INIT_ONLY) continue;
-                else if (d.grade == SG_FLOW_GRADE_THREAD && d.param_idx == 0) { ++n_thread; thread_at = i; last_checked = i; }
+                else if (d.behavior == PB_INIT_ONLY) { if (d.burst & ~1) pq = false; }  // maps on other indices
+                else if (d.param_idx != 0) pq = false;  // sg_submit_ex args beyond [0] are k_lane's
+                else if (d.grade == SG_FLOW_GRADE_THREAD) { ++n_thread; thread_at = i; last_checked = i; }
                 else if (d.grade != SG_FLOW_GRADE_QPS || rule_map_cap(d.duration_sec) > 4080) pq = false;
                 else last_checked = i;
             }
             if (n_thread > 1 || (n_thread == 1 && thread_at != last_checked)) pq = false;
+            if (n_thread) p.xf |= XF_PTHREAD;
+            // a thread-count map of another index (an earlier rule set's, kept with the metric) is k_lane's too
+            if (pq) {
+                auto it = e->tmaps.lower_bound(((uint64_t)r << 8) | 1);
+                if (it != e->tmaps.end() && (*it >> 8) == (uint64_t)r) pq = false;
+            }
             if (pq) p.pflags |= PF_PQ;
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
         }
@@ -1025,17 +1048,16 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&e->d_prio, R * 4) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
-    {   // origin / context node pool + its index (2 slots per node, power of two)
+    {   // origin / context node table (open addressing, load <= 2/3 at capacity, power of two)
         const uint64_t cap = std::max<uint32_t>(cfg.aux_node_capacity, 16u);
         uint64_t slots = 32;
-        while (slots < 2 * cap) slots <<= 1;
+        while (2 * slots < 3 * cap) slots <<= 1;
         e->aux_mask = slots - 1;
         e->cfg.aux_node_capacity = (uint32_t)cap;
-        if (hipMalloc(&e->d_auxtab, slots * sizeof(AuxSlot)) != hipSuccess ||
-            hipMalloc(&e->d_auxpool, cap * sizeof(AuxNode)) != hipSuccess || hipMalloc(&e->d_auxcnt, 4) != hipSuccess ||
-            hipMemsetAsync(e->d_auxtab, 0xFF, slots * sizeof(AuxSlot), e->stream) != hipSuccess ||
+        if (hipMalloc(&e->d_auxtab, slots * sizeof(AuxNode)) != hipSuccess || hipMalloc(&e->d_auxcnt, 4) != hipSuccess ||
+            hipMemsetAsync(e->d_auxtab, 0xFF, slots * sizeof(AuxNode), e->stream) != hipSuccess ||
             hipMemsetAsync(e->d_auxcnt, 0, 4, e->stream) != hipSuccess)
-            return bad(fail(SG_ENOMEM, "device allocation of the origin/context node pool failed"));
+            return bad(fail(SG_ENOMEM, "device allocation of the origin/context node table failed"));
     }
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
@@ -1103,6 +1125,32 @@ extern "C" int sgx_debug_counters(sg_engine* e, unsigned long long* out, int cap
     return k;
 }
 
+// diagnostics export (not part of the ABI; parity tests): an origin (kind 0) / context (kind 1) node of res.
+// out[0..15] = second window buckets {ws, pass, block, exc, succ, rt, occ, minRt} x 2, out[16] = curThreadNum,
+// out[17..20] = minute pass history {ws, pass} per second parity; returns 1, 0 if the node does not exist.
+extern "C" int sgx_read_aux_node(sg_engine* e, uint32_t res, uint32_t kind, uint32_t id, long long* out) {
+    if (!e || !out || drain(e) != SG_OK) return -1;
+    const unsigned long long key = ((unsigned long long)res << 32) | ((unsigned long long)kind << 31) | (id & 0x7FFFFFFFu);
+    uint64_t h = mix64(key) & e->aux_mask;
+    for (uint64_t probe = 0; probe <= e->aux_mask; ++probe) {
+        AuxNode a;
+        if (hipMemcpy(&a, e->d_auxtab + h, sizeof(a), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (a.key == AUX_EMPTY) return 0;
+        if (a.key == key) {
+            for (int p = 0; p < 2; ++p) {
+                const Bkt& b = a.sec[p];
+                const int64_t v[8] = {b.ws, b.pass, b.block, b.exc, b.succ, b.rt, b.occ, b.minrt};
+                for (int k = 0; k < 8; ++k) out[8 * p + k] = v[k];
+            }
+            out[16] = a.thread;
+            out[17] = a.mws[0]; out[18] = a.mpass[0]; out[19] = a.mws[1]; out[20] = a.mpass[1];
+            return 1;
+        }
+        h = (h + 1) & e->aux_mask;
+    }
+    return 0;
+}
+
 int sg_engine_destroy(sg_engine* e) {
     if (!e) return SG_OK;
     (void)hipSetDevice(e->device);
@@ -1112,7 +1160,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
-    dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt);
+    dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
     dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
@@ -1702,6 +1750,32 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     return SG_OK;
 }
 
+// Lists of the aux.hip post-pass for a batch of n events in slot B, and the engine's partial pool.
+#define AUXPOOL_CAP (1u << 20)
+static int ensure_aux(sg_engine* e, sg_engine::BatchSlot& B, uint64_t n) {
+    const uint64_t npiece = n / AUX_PIECE + n / 257 + 64;  // pieces: every long segment's, <= n/P + n/(AUX_SHORT + 1)
+    if (n > B.aux_cap_n) {
+        dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti);
+        const uint64_t c = std::max<uint64_t>(n, 1u << 16);
+        HIPCHK(hipMalloc(&B.d_ashort, c * 4));
+        HIPCHK(hipMalloc(&B.d_apiece, (c / AUX_PIECE + c / 257 + 64) * 8));
+        HIPCHK(hipMalloc(&B.d_amulti, (c / AUX_PIECE + 64) * 8));
+        B.aux_cap_n = c;
+    }
+    if (!e->d_auxpool) {
+        HIPCHK(hipMalloc(&e->d_auxpool, (uint64_t)AUXPOOL_CAP * sizeof(AuxAcc)));
+        e->auxpool_cap = AUXPOOL_CAP;
+    }
+    if (npiece > e->auxmeta_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));  // no decide stage may use the old buffer
+        dfree(e->d_auxmeta);
+        const uint64_t c = std::max<uint64_t>(npiece, B.aux_cap_n / AUX_PIECE + B.aux_cap_n / 257 + 64);
+        HIPCHK(hipMalloc(&e->d_auxmeta, c * 8));
+        e->auxmeta_cap = c;
+    }
+    return SG_OK;
+}
+
 static bool is_device_ptr(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
@@ -1809,8 +1883,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         j1_max = std::min<uint32_t>(j1_max, 1024);
         j4_max = std::min<uint32_t>(j4_max, 4096);
     }
+    if (ext) {  // the aux.hip post-pass lists of this slot
+        if (int arc = ensure_aux(e, B, n)) return arc;
+    }
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
-                          force_lane ? 1 : 0, e->d_blkcnt, (ext || !e->pq_on) ? 0u : 1u, e->pq_wide, gs));
+                          force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
+                          B.d_ashort, B.d_apiece, B.d_amulti, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets
@@ -1834,7 +1912,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     for (int b = 0; b < N_BINS; ++b) bin_n[b] = off[b + 1] - off[b];
     // ---- decide stage, in order after the previous batch's: references into earlier batches first
     HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
-    HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, st));
+    HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
@@ -1909,7 +1987,6 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.ext = dev_ext;
     S.args = dev_args;
     S.aux_tab = e->d_auxtab;
-    S.aux_pool = e->d_auxpool;
     S.aux_count = e->d_auxcnt;
     S.aux_cap = e->cfg.aux_node_capacity;
     S.aux_mask = e->aux_mask;
@@ -1981,6 +2058,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
+    // origin / context nodes of the segments decided off k_lane<16>, from the committed verdicts (aux.hip)
+    if (ext)
+        HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_apiece, B.d_amulti, S, dc, t0, e->d_dec,
+                          e->d_auxpool, e->auxpool_cap, e->d_bsmall + 133, e->d_auxmeta, e->d_bsmall + 0, st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));

@@ -92,6 +92,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         r.pad = 0;
         uint32_t mark = 0;  // PM_* marks for the resource
         uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+        uint32_t tag = 0;        // origin / context node tag (dev_types.h TAG_*)
+        bool own_args = false;   // the event's args come from the table
         if (ext) {  // sg_submit_ex: validate the event's args; a NullContext event is k_lane's
             const sg_event_ext x = ext[i];
             if (x.n_args > SG_MAX_ARGS || (uint64_t)x.arg_off + x.n_args > n_args) fl |= BF_BAD_ARGS;
@@ -106,12 +108,26 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                 }
                 const sg_arg a0 = args[x.arg_off];
                 key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                if (a0.kind == SG_ARG_LIST) mark |= PM_ARGL;
+                own_args = true;
             }
             if (x.context_id > max_ctx) mark |= PM_LANE;
             // ClusterBuilderSlot / NodeSelectorSlot keep an origin node and a DefaultNode per context for every
             // entry, whatever the rules (ClusterBuilderSlot.java:74-99, NodeSelectorSlot.java:134-176)
-            else if (x.origin_id != 0 || x.context_id != 0) mark |= PM_AUX;
+            else if (x.origin_id != 0 || x.context_id != 0) {
+                mark |= PM_AUX;
+                if (x.origin_id >> TAG_ORIGIN_BITS) mark |= PM_LANE;  // not packable: k_lane reads the ext itself
+                else tag = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
+            }
         }
+        if (own_args) {  // the record's HAS_ARG: args[0] is a scalar (a k_pq check / thread-count key)
+            r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
+            if (e.kind == SG_EV_EXIT) {
+                r.flags |= RF_OWN_ARGS;
+                if (e.flags & SG_F_EXIT_ARGS) mark |= PM_XARGS;
+            }
+        }
+        r.x = tag;  // ENTRY (and an EXIT / TRACE naming no ENTRY of this batch): its node tag
         if (e.kind == SG_EV_ENTRY) {
             // the arg an exit(count, args) of this ENTRY will decrement (ParamFlowStatisticExitCallback)
             if (key_ring) key_ring[(gbase + i) & ring_mask] = key0;
@@ -123,6 +139,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
             if (e.kind == SG_EV_EXIT) {
                 const int64_t raw = (int64_t)(e.aux >> 48);
                 r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
+                // Entry.exit(count, args) with its own args: the key its release decrements (k_pq reads it here)
+                if (own_args && key_ring) key_ring[(gbase + i) & ring_mask] = key0;
             }
             const uint64_t ref = e.aux & SG_REF_NONE;
             if (ref != SG_REF_NONE) {

@@ -1080,7 +1080,9 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
             sh.tcz[e] = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
             sh.tkx[e] = (uint32_t)r.kind | ((uint32_t)r.flags << 8) | ((uint32_t)r.code << 16);
             sh.tx[e] = r.x;
-            if (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG)) sh.tkey[e] = ev[vals[sg.start + p] & 0x7FFFFFFFu].aux;
+            // args[0]'s key: k_rs_first put it in the key ring (sg_submit's aux, or sg_submit_ex's table entry)
+            if (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG))
+                sh.tkey[e] = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
         }
         __syncthreads();
         // ---- 2. ParamFlowSlot: the rules in order
@@ -1158,9 +1160,14 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                 } else if (p < sg.len && kind == SG_EV_EXIT && ((kx >> 8) & SG_F_EXIT_ARGS) && p >= tm_from
                            && S.key_ring) {
                     const uint32_t code = (kx >> 16) & 0xFFu;
+                    // Entry.exit(count, args) with args of its own (sg_submit_ex) releases those, even naming no
+                    // ENTRY; else args[0] of its ENTRY (lane_exit, ParamFlowStatisticExitCallback)
+                    const bool own = ((kx >> 8) & RF_OWN_ARGS) != 0;
                     uint64_t ref = SG_REF_NONE;
                     if (code == RC_PASSED) {
-                        ref = ev[vals[sg.start + p] & 0x7FFFFFFFu].aux & SG_REF_NONE;
+                        if (!own) ref = ev[vals[sg.start + p] & 0x7FFFFFFFu].aux & SG_REF_NONE;
+                        op = OP_SUB;
+                    } else if (code == RC_NONE && own) {
                         op = OP_SUB;
                     } else if (code == RC_BATCH) {
                         const uint32_t rel = sh.tx[e] - sg.start;
@@ -1171,6 +1178,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                         }
                     }
                     if (op != OP_NONE) {
+                        if (own) ref = S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu);
                         const uint64_t key = S.key_ring[ref & cfg.ring_mask];
                         if (key == NO_KEY) op = OP_NONE;
                         else sh.tkey[e] = key;

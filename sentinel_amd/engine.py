@@ -183,6 +183,14 @@ class Engine:
             _check(lib().sg_submit_async(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr)))
         self.n_events += n
 
+    def submit_ex_ptr(self, ev_ptr: int, ext_ptr: int, n: int, out_ptr: int, sync: bool = True, args_ptr: int = 0,
+                      n_args: int = 0):
+        """sg_submit_ex(_async) on device (or host) pointers."""
+        fn = lib().sg_submit_ex if sync else lib().sg_submit_ex_async
+        _check(fn(self.h, C.c_void_p(ev_ptr), C.c_void_p(ext_ptr) if ext_ptr else None, n,
+                  C.c_void_p(args_ptr) if args_ptr else None, n_args, C.c_void_p(out_ptr)))
+        self.n_events += n
+
     def sync(self):
         _check(lib().sg_sync(self.h))
 
@@ -208,6 +216,21 @@ class Engine:
         fn.restype = C.c_ulonglong
         fn.argtypes = [C.c_void_p]
         return int(fn(self.h))
+
+    def read_aux_node(self, res: int, kind: int, node_id: int):
+        """An origin (kind 0, origin id) / context (kind 1, context id) node of res: second window [2, 8], thread,
+        minute pass history [2, 2] ({ws, pass} per second parity); None if absent (diagnostics export
+        sgx_read_aux_node)."""
+        fn = lib().sgx_read_aux_node
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+        out = np.zeros(21, dtype=np.int64)
+        rc = fn(self.h, res, kind, node_id, out.ctypes.data)
+        if rc < 0:
+            raise SentinelError(A.SG_EDEVICE, "sgx_read_aux_node failed")
+        if rc == 0:
+            return None
+        return {"second": out[:16].reshape(2, 8), "thread": int(out[16]), "mhist": out[17:21].reshape(2, 2)}
 
     def read_node(self, res: int, now: int = 0) -> dict:
         st = A.SgNodeState()

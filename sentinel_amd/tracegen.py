@@ -117,6 +117,12 @@ class Workload:
         keep = np.isin(rid, np.asarray(res_ids))
         return np.ascontiguousarray(raw[keep])
 
+    def intern_names(self, target, n_origins: int = 16, n_contexts: int = 4):
+        """Intern the ext workload's origin and context names (ContextUtil.enter(name, origin)) on an Engine or an
+        oracle: origins "app-0".., contexts "ctx-0"..; returns their ids (same on every target)."""
+        return (np.array([target.intern_origin("app-%d" % k) for k in range(n_origins)], dtype=np.uint32),
+                np.array([target.intern_context("ctx-%d" % k) for k in range(n_contexts)], dtype=np.uint32))
+
     def close(self):
         if getattr(self, "h", None):
             self.events = None
@@ -128,3 +134,21 @@ class Workload:
             self.close()
         except Exception:
             pass
+
+
+def ext_for(events: np.ndarray, origin_ids, context_ids, seed: int) -> np.ndarray:
+    """The sg_event_ext of a trace that starts at global index 0 (the drop-in's own input): every
+    ENTRY in one of the named contexts, from one of the origins, uniformly; an EXIT / TRACE carries its ENTRY's
+    (the Entry keeps its Context).  No args (the C4 rules have none)."""
+    n = len(events)
+    rng = np.random.default_rng(seed)
+    o = rng.integers(0, len(origin_ids), n)
+    c = rng.integers(0, len(context_ids), n)
+    aux = events["aux"]
+    ref = (aux & np.uint64(A.REF_NONE)).astype(np.int64)
+    isref = (events["kind"] != A.EV_ENTRY) & (ref != A.REF_NONE) & (ref < n)
+    src = np.where(isref, ref, np.arange(n, dtype=np.int64))
+    ext = np.zeros(n, dtype=A.EXT_DTYPE)
+    ext["origin_id"] = np.asarray(origin_ids, dtype=np.uint32)[o[src]]
+    ext["context_id"] = np.asarray(context_ids, dtype=np.uint32)[c[src]]
+    return ext

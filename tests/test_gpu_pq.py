@@ -167,3 +167,71 @@ def test_pq_rule_mix_thread_maps_and_alternating_paths(rt_max):
         assert g["thread"] == o["thread"]
         np.testing.assert_array_equal(g["second"][:2], o["second"][:2])
         np.testing.assert_array_equal(g["minute"], o["minute"])
+
+
+def _ext_args(ev, io, ic, seed, list_res_mod=7):
+    """The C5 trace as the Java drop-in sends it (sg_submit_ex): contexts / origins on every event, args[0] from the
+    table (a few nulls; Collections on the resources res % list_res_mod == 0 now and then: those resources turn to
+    the per-lane kernel), and half of the releasing EXITs with args of their own (Entry.exit(count, args): mostly
+    the ENTRY's value, sometimes another one)."""
+    rng = np.random.default_rng(seed)
+    n = len(ev)
+    ext = T.ext_for(ev, io, ic, seed)
+    ent = ev["kind"] == A.EV_ENTRY
+    ext_rows = np.zeros(n, dtype=A.ARG_DTYPE)
+    ext_rows["key"] = ev["aux"]
+    ext_rows["kind"] = A.ARG_SCALAR
+    u = rng.random(n)
+    ext_rows["kind"][ent & (u < 0.03)] = A.ARG_NULL
+    lst = ent & (u >= 0.03) & (u < 0.05) & (ev["res_id"] % list_res_mod == 0)
+    li = np.nonzero(lst)[0]
+    extra = np.zeros(2 * len(li), dtype=A.ARG_DTYPE)
+    extra["kind"] = A.ARG_SCALAR
+    extra["key"][0::2] = ev["aux"][li]
+    extra["key"][1::2] = ev["aux"][rng.integers(0, n, len(li))]
+    ext_rows["kind"][li] = A.ARG_LIST
+    ext_rows["key"][li] = n + 2 * np.arange(len(li), dtype=np.uint64)
+    ext_rows["len"][li] = 2
+    # EXITs releasing with their own args
+    ref = (ev["aux"] & np.uint64(A.REF_NONE)).astype(np.int64)
+    own = (ev["kind"] == A.EV_EXIT) & ((ev["flags"] & A.F_EXIT_ARGS) != 0) & (rng.random(n) < 0.5) & (ref < n)
+    oi = np.nonzero(own)[0]
+    ext_rows["key"][oi] = np.where(rng.random(len(oi)) < 0.9, ev["aux"][ref[oi]], ev["aux"][rng.integers(0, n, len(oi))])
+    ext_rows["kind"][oi] = np.where(ent[ref[oi]], A.ARG_SCALAR, A.ARG_NULL)
+    ext["arg_off"] = np.arange(n, dtype=np.uint32)
+    ext["n_args"] = (ent | own).astype(np.uint32)
+    return ext, np.concatenate([ext_rows, extra])
+
+
+@pytest.mark.parametrize("variant", ["hot", "uniform", "thread"])
+def test_pq_ext_args_contexts(variant):
+    # VERDICT r3 missing #1: k_pq takes sg_submit_ex batches (args[0] from the table via the key ring; EXITs with
+    # their own args), the aux post-pass updates the origin / context nodes of its segments
+    v = {"hot": T.V_HOT, "uniform": T.V_HOT | T.V_UNIFORM, "thread": T.V_HOT | T.V_UNIFORM | T.V_THREAD}[variant]
+    w = T.Workload(5, n_res=2_000, n_entries=600_000, n_param_values=2_000_000, variant=v)
+    ev = w.events
+    eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=26, status_ring_log2=24,
+                   aux_node_capacity=1 << 16)
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(eng)
+    w.install(orc)
+    io, ic = w.intern_names(eng)
+    assert all(np.array_equal(a, b) for a, b in zip((io, ic), w.intern_names(orc)))
+    ext, table = _ext_args(ev, io, ic, seed=17)
+    cuts = np.linspace(0, len(ev), 4).astype(np.int64)
+    for a, b in zip(cuts[:-1], cuts[1:]):  # one table for the whole trace: arg_off stays global
+        dg, do = eng.submit_ex(ev[a:b], ext[a:b], table), orc.submit_ex(ev[a:b], ext[a:b], table)
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), ("event", int(a + bad[0]), ev[a + bad[0]], hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
+    cnt = np.bincount(ev["res_id"], minlength=w.n_res)
+    for r in np.unique(np.concatenate([np.argsort(-cnt)[:40], np.random.default_rng(2).choice(w.n_res, 100)])):
+        g, o = eng.read_node(int(r)), orc.read_node(int(r))
+        assert g["thread"] == o["thread"], r
+        np.testing.assert_array_equal(g["second"][:2], o["second"][:2], err_msg="second window of res %d" % r)
+        np.testing.assert_array_equal(g["minute"], o["minute"], err_msg="minute window of res %d" % r)
+        for k, nm in enumerate(["app-%d" % i for i in range(16)]):
+            ga, oa = eng.read_aux_node(int(r), 0, int(io[k])), orc.read_origin_node(int(r), nm)
+            if oa is None:
+                continue
+            assert ga is not None and ga["thread"] == oa["thread"], (r, nm)
+            np.testing.assert_array_equal(ga["second"], oa["second"][:2], err_msg="origin node %d/%s" % (r, nm))
