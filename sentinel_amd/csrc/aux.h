@@ -27,8 +27,12 @@ __device__ __forceinline__ void aux_init(AuxNode* a) {
     a->borrow[0] = -1; a->borrow[1] = 0; a->borrow[2] = -1; a->borrow[3] = 0;
 }
 
-// the node of (res, kind, id), created on first use (BF_AUX_FULL once more than aux_cap nodes are claimed)
-__device__ __forceinline__ AuxNode* aux_get(const DevState& S, uint32_t res, uint32_t kind, uint32_t id, uint32_t* bflags) {
+// the node of (res, kind, id), created on first use (BF_AUX_FULL once more than aux_cap nodes are claimed).  claims:
+// where a new node is counted -- a workgroup's LDS counter the kernel adds to aux_count once (aux_flush_claims), or
+// null for aux_count itself; *fresh (optional): the node was created here (its state is aux_init's)
+__device__ __forceinline__ AuxNode* aux_get(const DevState& S, uint32_t res, uint32_t kind, uint32_t id, uint32_t* bflags,
+                                            uint32_t* claims = nullptr, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     const unsigned long long key = ((unsigned long long)res << 32) | ((unsigned long long)kind << 31) | (id & 0x7FFFFFFFu);
     uint64_t h = mix64(key) & S.aux_mask;
     for (uint64_t probe = 0; probe <= S.aux_mask; ++probe) {
@@ -39,8 +43,10 @@ __device__ __forceinline__ AuxNode* aux_get(const DevState& S, uint32_t res, uin
             unsigned long long expect = AUX_EMPTY;
             if (__hip_atomic_compare_exchange_strong(&a->key, &expect, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)) {
-                if (atomicAdd(S.aux_count, 1u) >= S.aux_cap) atomicOr(bflags, BF_AUX_FULL);
-                aux_init(a);
+                if (claims) atomicAdd(claims, 1u);
+                else if (atomicAdd(S.aux_count, 1u) >= S.aux_cap) atomicOr(bflags, BF_AUX_FULL);
+                if (fresh) *fresh = true;
+                else aux_init(a);
                 return a;
             }
             if (expect == key) return a;
@@ -88,9 +94,32 @@ __device__ __forceinline__ void node_store_aux(const Node& N, AuxNode* a) {
 // the node's bucket (reset, with the pass its borrow bucket holds: OccupiableBucketLeapArray.resetWindowTo) and the
 // same window adds (LeapArray.currentWindow, LeapArray.java:117-208); likewise the minute pass history
 __device__ __forceinline__ void aux_commit(const DevState& S, int32_t max_rt, uint32_t res, const AuxAcc& A,
-                                           uint32_t* bflags) {
-    AuxNode* a = aux_get(S, res, A.key >> 31, A.key & 0x7FFFFFFFu, bflags);
+                                           uint32_t* bflags, uint32_t* claims = nullptr) {
+    bool fresh;
+    AuxNode* a = aux_get(S, res, A.key >> 31, A.key & 0x7FFFFFFFu, bflags, claims, &fresh);
     if (!a) return;
+    if (fresh) {  // a new node: its whole state written at once, nothing read back
+        a->thread = A.thread;
+        a->flags = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) { a->mws[q] = A.MW[q]; a->mpass[q] = A.MW[q] < 0 ? 0 : (int64_t)A.mpass[q]; }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            Bkt b;
+            const int64_t mrt = A.minrt[p] == 0xFFFFFFFFu ? INT64_MAX : (int64_t)A.minrt[p];
+            b.ws = A.W[p];
+            b.pass = A.W[p] < 0 ? 0 : (int64_t)A.s[p][0];
+            b.block = A.W[p] < 0 ? 0 : (int64_t)A.s[p][1];
+            b.exc = 0;
+            b.succ = A.W[p] < 0 ? 0 : (int64_t)A.s[p][2];
+            b.rt = A.W[p] < 0 ? 0 : (int64_t)A.s[p][3];
+            b.occ = 0;
+            b.minrt = A.W[p] < 0 ? 0 : (mrt < max_rt ? mrt : max_rt);
+            a->sec[p] = b;
+        }
+        a->borrow[0] = -1; a->borrow[1] = 0; a->borrow[2] = -1; a->borrow[3] = 0;
+        return;
+    }
     a->thread += A.thread;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -129,6 +158,11 @@ __device__ __forceinline__ void aux_commit(const DevState& S, int32_t max_rt, ui
         }
         a->sec[p] = b;
     }
+}
+
+// a workgroup's claimed nodes into aux_count (one atomic a workgroup), the capacity check
+__device__ __forceinline__ void aux_flush_claims(const DevState& S, uint32_t n, uint32_t* bflags) {
+    if (n && atomicAdd(S.aux_count, n) + n > S.aux_cap) atomicOr(bflags, BF_AUX_FULL);
 }
 
 } // namespace sg

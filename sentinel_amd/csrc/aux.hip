@@ -13,10 +13,11 @@
 // a bucket to a later window in place, so earlier events of the same parity are overwritten.  Per second parity q
 // likewise the minute pass history (aux.h), and curThreadNum moves by passes minus exits.  So "later window
 // replaces, same window adds" is an associative merge (AuxAcc) and a segment's events can be cut anywhere:
-//   * k_aux_short : one lane per segment of <= AUX_SHORT events, walking it with a 4-node register cache;
-//   * k_aux_piece : one workgroup per AUX_PIECE events of a longer segment: an LDS table of the piece's nodes,
-//                   merged in two phases (the latest window of every node-parity, then the sums of that window);
-//                   a one-piece segment commits its nodes, the pieces of a longer one leave partial AuxAccs;
+//   * k_aux_cold  : one workgroup per AUX_G segments of <= AUX_SHORT events, their events 256 at a time: an LDS
+//                   table of the chunk's nodes, merged in two phases (the latest window of every node-parity, then
+//                   the sums of that window), committed one node a thread;
+//   * k_aux_piece : one workgroup per AUX_PIECE events of a longer segment, the same table: a one-piece segment
+//                   commits its nodes, the pieces of a longer one leave partial AuxAccs;
 //   * k_aux_merge : one workgroup per multi-piece segment: the pieces' partials merged the same way, committed.
 // An event updates the origin node (origin != 0) and the context node (named context: without a CHAIN rule the
 // default context's DefaultNode is not kept, decide.hip chain_ctx_kept) of its tag (SEv.x: the ENTRY's own, an
@@ -30,8 +31,7 @@
 
 using namespace sg;
 
-#define AUX_K 4           // k_aux_short: nodes cached per lane
-#define AUX_S 512         // k_aux_piece / k_aux_merge: LDS node slots (power of two)
+#define AUX_K 4           // aux_walk (the sequential fallback): nodes cached per lane
 #define AUX_NONE 0x7FFFFFFF
 #define AUX_EMPTY32 0xFFFFFFFFu
 
@@ -172,31 +172,24 @@ __device__ __forceinline__ bool seg_chain(const DevState& S, const DevCfg& cfg, 
     return (S.info[res].flags & NI_CHAIN) != 0 && cfg.switch_on;
 }
 
-__global__ __launch_bounds__(256) void k_aux_short(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
-                                                   const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
-                                                   DevState S, DevCfg cfg, int64_t t0, const uint32_t* __restrict__ dec,
-                                                   uint32_t* __restrict__ bflags) {
-    const uint32_t m = *cnt;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        const Seg sg = segs[list[i]];
-        aux_walk(recs, dec, S, cfg.max_rt, sg.res, seg_chain(S, cfg, sg.res), sg.start, sg.start + sg.len, t0, bflags);
-    }
-}
-
-// ---------------------------------------------------------------- the LDS node table (pieces, merges)
-struct AuxTab {
-    uint32_t key[AUX_S];
-    int64_t W[AUX_S][2], MW[AUX_S][2];   // latest windows (absolute ms; -1 none)
-    unsigned long long s[AUX_S][2][4];
-    uint32_t minrt[AUX_S][2];
-    unsigned long long mpass[AUX_S][2];
-    int32_t thread[AUX_S];
-    uint32_t used[AUX_S];                // slots in use, in insertion order
+// ---------------------------------------------------------------- the LDS node table
+// Slots keyed by a 32-bit node key; windows as indices relative to the batch (500 ms / 1 s units), sums in 32 bits
+// (a chunk or piece holds <= AUX_PIECE events of <= 65535 each).  Updates merge in two phases separated by a
+// barrier: the latest window of every node-parity first (a read, an atomicMax only when later), then the sums of
+// the updates in that window and the thread deltas of all of them.
+#define TAB_S 512
+struct Tab {
+    uint32_t key[TAB_S];
+    int32_t W[TAB_S][2], MW[TAB_S][2];
+    uint32_t s[TAB_S][2][4];
+    uint32_t minrt[TAB_S][2];
+    uint32_t mpass[TAB_S][2];
+    int32_t thread[TAB_S];
+    uint32_t used[TAB_S];
     uint32_t nused, overflow;
 };
-
-__device__ __forceinline__ void tab_init(AuxTab& T) {
-    for (uint32_t i = threadIdx.x; i < AUX_S; i += blockDim.x) {
+__device__ __forceinline__ void tab_clear(Tab& T) {  // every slot (the first time)
+    for (uint32_t i = threadIdx.x; i < TAB_S; i += blockDim.x) {
         T.key[i] = AUX_EMPTY32;
         T.W[i][0] = T.W[i][1] = T.MW[i][0] = T.MW[i][1] = -1;
         for (int p = 0; p < 2; ++p) {
@@ -208,32 +201,176 @@ __device__ __forceinline__ void tab_init(AuxTab& T) {
     }
     if (threadIdx.x == 0) { T.nused = 0; T.overflow = 0; }
 }
-// the slot of key (inserted on first sight); -1 when the table is full
-__device__ __forceinline__ int tab_slot(AuxTab& T, uint32_t key) {
-    uint32_t h = (uint32_t)(mix64(key) & (AUX_S - 1));
-    for (int probe = 0; probe < AUX_S; ++probe) {
-        const uint32_t old = atomicCAS(&T.key[h], AUX_EMPTY32, key);
-        if (old == AUX_EMPTY32) { T.used[atomicAdd(&T.nused, 1u)] = h; return (int)h; }
-        if (old == key) return (int)h;
-        h = (h + 1) & (AUX_S - 1);
+__device__ __forceinline__ void tab_reset_used(Tab& T) {  // the used slots only (after a flush)
+    const uint32_t nu = T.nused;
+    for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
+        const uint32_t i = T.used[u];
+        T.key[i] = AUX_EMPTY32;
+        T.W[i][0] = T.W[i][1] = T.MW[i][0] = T.MW[i][1] = -1;
+        for (int p = 0; p < 2; ++p) {
+            for (int k = 0; k < 4; ++k) T.s[i][p][k] = 0;
+            T.minrt[i][p] = 0xFFFFFFFFu;
+            T.mpass[i][p] = 0;
+        }
+        T.thread[i] = 0;
+    }
+}
+// the slot of key, inserted on first sight (a plain read finds a present key: no atomic); -1 when full
+__device__ __forceinline__ int tab_find(Tab& T, uint32_t key) {
+    uint32_t h = (uint32_t)(mix64(key) & (TAB_S - 1));
+    for (int probe = 0; probe < TAB_S; ++probe) {
+        uint32_t k = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == AUX_EMPTY32) {
+            k = atomicCAS(&T.key[h], AUX_EMPTY32, key);
+            if (k == AUX_EMPTY32) { T.used[atomicAdd(&T.nused, 1u)] = h; return (int)h; }
+        }
+        if (k == key) return (int)h;
+        h = (h + 1) & (TAB_S - 1);
     }
     atomicOr(&T.overflow, 1u);
     return -1;
 }
-__device__ __forceinline__ void tab_acc(const AuxTab& T, uint32_t i, AuxAcc& A) {
-    A.key = T.key[i];
+__device__ __forceinline__ void tab_p1(Tab& T, int i, uint32_t what, int32_t wi, int32_t si) {
+    const int p = wi & 1, q = si & 1;
+    if (wi > T.W[i][p]) atomicMax(&T.W[i][p], wi);
+    if (what == AW_PASS && si > T.MW[i][q]) atomicMax(&T.MW[i][q], si);
+}
+__device__ __forceinline__ void tab_p2(Tab& T, int i, uint32_t what, int32_t wi, int32_t si, uint32_t c, uint32_t rt) {
+    const int p = wi & 1, q = si & 1;
+    const bool in_w = T.W[i][p] == wi;
+    if (what == AW_PASS) {
+        atomicAdd(&T.thread[i], 1);
+        if (in_w) atomicAdd(&T.s[i][p][0], c);
+        if (T.MW[i][q] == si) atomicAdd(&T.mpass[i][q], c);
+    } else if (what == AW_BLOCK) {
+        if (in_w) atomicAdd(&T.s[i][p][1], c);
+    } else {
+        atomicAdd(&T.thread[i], -1);
+        if (in_w) {
+            atomicAdd(&T.s[i][p][2], c);
+            atomicAdd(&T.s[i][p][3], rt);
+            atomicMin(&T.minrt[i][p], rt);
+        }
+    }
+}
+// slot i as an AuxAcc (absolute windows; key = kind << 31 | id)
+__device__ __forceinline__ void tab_acc(const Tab& T, uint32_t i, uint32_t key, int64_t b500, int64_t b1000, AuxAcc& A) {
+    A.key = key;
     A.thread = T.thread[i];
     for (int p = 0; p < 2; ++p) {
-        A.W[p] = T.W[i][p];
-        A.MW[p] = T.MW[i][p];
+        A.W[p] = T.W[i][p] < 0 ? -1 : (b500 + T.W[i][p]) * 500;
+        A.MW[p] = T.MW[i][p] < 0 ? -1 : (b1000 + T.MW[i][p]) * 1000;
         A.minrt[p] = T.minrt[i][p];
         A.mpass[p] = T.mpass[i][p];
         for (int k = 0; k < 4; ++k) A.s[p][k] = T.s[i][p][k];
     }
 }
 
-// One piece of a long segment: apiece[k] = seg << 32 | piece.  meta[k] = pool offset << 32 | count of its partial
-// (count AUX_NONE: the piece overflowed; a one-piece segment commits instead and leaves no meta).
+// The short segments (<= AUX_SHORT events): a workgroup per AUX_G of them, their events in chunks of 256 (one a
+// thread), every chunk's nodes merged in the table and committed (several commits of one node are fine: the merge
+// is associative, and one workgroup owns its segments' nodes).  Node key: segment-in-group << 25 | kind << 24 | id.
+#define AUX_G 64
+__global__ __launch_bounds__(256) void k_aux_cold(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                                                  DevState S, DevCfg cfg, int64_t t0, const uint32_t* __restrict__ dec,
+                                                  uint32_t* __restrict__ bflags) {
+    __shared__ Tab T;
+    __shared__ uint32_t gstart[AUX_G], gres[AUX_G], gpre[AUX_G + 1], gchain[AUX_G];
+    __shared__ uint32_t claims;
+    const uint32_t m = *cnt;
+    const int64_t b500 = t0 / 500, b1000 = t0 / 1000;
+    tab_clear(T);
+    if (threadIdx.x == 0) claims = 0;
+    for (uint32_t g0 = blockIdx.x * AUX_G; g0 < m; g0 += gridDim.x * AUX_G) {
+        const uint32_t ng = min((uint32_t)AUX_G, m - g0);
+        __syncthreads();
+        if (threadIdx.x < 64) {  // the group's segments and the exclusive prefix of their lengths (one wave)
+            const uint32_t l = threadIdx.x;
+            uint32_t len = 0;
+            if (l < ng) {
+                const Seg sg = segs[list[g0 + l]];
+                gstart[l] = sg.start;
+                gres[l] = sg.res;
+                gchain[l] = seg_chain(S, cfg, sg.res) ? 1u : 0u;
+                len = sg.len;
+            }
+            uint32_t x = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if ((int)l >= o) x += y;
+            }
+            gpre[l] = x - len;
+            if (l == 63) gpre[AUX_G] = x;
+        }
+        __syncthreads();
+        const uint32_t tot = gpre[AUX_G];
+        for (uint32_t c0 = 0; c0 < tot; c0 += 256) {
+            const uint32_t e = c0 + threadIdx.x;
+            uint32_t what = AW_NONE, tag = 0, g = 0, cz = 0;
+            int32_t wi = 0, si = 0;
+            if (e < tot) {
+                uint32_t lo = 0, hi = ng;  // the segment holding event e: gpre[g] <= e < gpre[g + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (gpre[mid] <= e) lo = mid; else hi = mid;
+                }
+                g = lo;
+                const uint32_t p = gstart[g] + (e - gpre[g]);
+                const SEv r = recs[p];
+                what = aux_what(r, p, recs, dec, gchain[g] != 0, &tag);
+                const int64_t t = t0 + r.dt;
+                wi = (int32_t)(t / 500 - b500);
+                si = (int32_t)(t / 1000 - b1000);
+                cz = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
+            }
+            int sl[2] = {-1, -1};
+            if (what != AW_NONE && tag && !(cfg.dbg_flags & 1024)) {
+                const uint32_t o = tag_origin(tag), cx = tag_ctx(tag);
+                if (o) sl[0] = tab_find(T, (g << 25) | o);
+                if (cx) sl[1] = tab_find(T, (g << 25) | (1u << 24) | cx);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (sl[u] >= 0) tab_p1(T, sl[u], what, wi, si);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (sl[u] >= 0) tab_p2(T, sl[u], what, wi, si, cz & 0xFFFFu, cz >> 16);
+            __syncthreads();
+            const uint32_t nu = T.nused;  // (<= 512 updates a chunk: the table cannot overflow)
+            for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
+                const uint32_t i = T.used[u], k = T.key[i];
+                AuxAcc A;
+                tab_acc(T, i, ((k >> 24) & 1u) << 31 | (k & 0xFFFFFFu), b500, b1000, A);
+                if (!(cfg.dbg_flags & 2048)) aux_commit(S, cfg.max_rt, gres[k >> 25], A, bflags, &claims);
+            }
+            __syncthreads();
+            tab_reset_used(T);
+            __syncthreads();
+            if (threadIdx.x == 0) T.nused = 0;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) aux_flush_claims(S, claims, bflags);
+}
+
+// Long segments: the pieces of every one (apiece[k] = seg << 32 | piece), expanded from the long list
+// (along[j] = seg << 32 | first piece) one workgroup a segment
+__global__ __launch_bounds__(256) void k_aux_expand(const Seg* __restrict__ segs, const uint64_t* __restrict__ along,
+                                                    const uint32_t* __restrict__ cnt, uint64_t* __restrict__ apiece) {
+    const uint32_t m = *cnt;
+    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+        const uint64_t e = along[j];
+        const uint32_t s = (uint32_t)(e >> 32), q = (uint32_t)e;
+        const uint32_t np = (segs[s].len + AUX_PIECE - 1) / AUX_PIECE;
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) apiece[q + i] = ((uint64_t)s << 32) | i;
+    }
+}
+
+// One piece of a long segment.  meta[k] = pool offset << 32 | count of its partial AuxAccs (count AUX_NONE: the
+// piece overflowed the table or the pool); a one-piece segment commits instead and leaves no meta.
 #define PIECE_EPL (AUX_PIECE / 256)
 __global__ __launch_bounds__(256) void k_aux_piece(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                                    const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
@@ -241,8 +378,12 @@ __global__ __launch_bounds__(256) void k_aux_piece(const SEv* __restrict__ recs,
                                                    AuxAcc* __restrict__ pool, uint32_t pool_cap,
                                                    uint32_t* __restrict__ pool_n, uint64_t* __restrict__ meta,
                                                    uint32_t* __restrict__ bflags) {
-    __shared__ AuxTab T;
+    __shared__ Tab T;
+    __shared__ uint32_t off, claims;
     const uint32_t m = *cnt;
+    const int64_t b500 = t0 / 500, b1000 = t0 / 1000;
+    tab_clear(T);
+    if (threadIdx.x == 0) claims = 0;
     for (uint32_t k = blockIdx.x; k < m; k += gridDim.x) {
         const uint64_t e = list[k];
         const Seg sg = segs[(uint32_t)(e >> 32)];
@@ -251,131 +392,144 @@ __global__ __launch_bounds__(256) void k_aux_piece(const SEv* __restrict__ recs,
         const uint32_t b = min(a + AUX_PIECE, sg.start + sg.len);
         const bool one = sg.len <= AUX_PIECE;
         const bool chain = seg_chain(S, cfg, sg.res);
-        __syncthreads();  // the previous piece's table is read out
-        tab_init(T);
         __syncthreads();
-        // the piece's updates: (slot, what, window, second, count, rt) per event, two nodes each
+        // the piece's updates: (slots, what, windows, count | rt) per event
         int sl[PIECE_EPL][2];
         uint32_t wh[PIECE_EPL], cz[PIECE_EPL];
-        int64_t tt[PIECE_EPL];
+        int32_t wi[PIECE_EPL], si[PIECE_EPL];
 #pragma unroll
         for (int j = 0; j < PIECE_EPL; ++j) {
             const uint32_t p = a + j * 256 + threadIdx.x;
             sl[j][0] = sl[j][1] = -1;
             wh[j] = AW_NONE;
             cz[j] = 0;
-            tt[j] = 0;
+            wi[j] = si[j] = 0;
             if (p >= b) continue;
             const SEv r = recs[p];
             uint32_t tag;
             const uint32_t w = aux_what(r, p, recs, dec, chain, &tag);
-            if (w == AW_NONE || tag == 0) continue;
+            if (w == AW_NONE || tag == 0 || (cfg.dbg_flags & 1024)) continue;
             wh[j] = w;
             cz[j] = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
-            tt[j] = t0 + r.dt;
+            const int64_t t = t0 + r.dt;
+            wi[j] = (int32_t)(t / 500 - b500);
+            si[j] = (int32_t)(t / 1000 - b1000);
             const uint32_t o = tag_origin(tag), cx = tag_ctx(tag);
-            if (o) sl[j][0] = tab_slot(T, o);
-            if (cx) sl[j][1] = tab_slot(T, (1u << 31) | cx);
+            if (o) sl[j][0] = tab_find(T, o);
+            if (cx) sl[j][1] = tab_find(T, (1u << 31) | cx);
         }
         __syncthreads();
         if (T.overflow) {  // more nodes than slots: the segment is walked by one lane (exact)
             if (one) {
                 if (threadIdx.x == 0) aux_walk(recs, dec, S, cfg.max_rt, sg.res, chain, a, b, t0, bflags);
             } else if (threadIdx.x == 0) meta[k] = AUX_NONE;
+            __syncthreads();
+            tab_clear(T);
             continue;
         }
-        // phase 1: the latest window of every node-parity (and pass-second of every node-second-parity)
 #pragma unroll
-        for (int j = 0; j < PIECE_EPL; ++j) {
-            if (wh[j] == AW_NONE) continue;
-            const int64_t W = tt[j] - tt[j] % 500, M = tt[j] - tt[j] % 1000;
-            const int p = (int)((W / 500) & 1), q = (int)((M / 1000) & 1);
-            for (int u = 0; u < 2; ++u) {
-                const int i = sl[j][u];
-                if (i < 0) continue;
-                atomicMax((long long*)&T.W[i][p], (long long)W);
-                if (wh[j] == AW_PASS) atomicMax((long long*)&T.MW[i][q], (long long)M);
-            }
-        }
+        for (int j = 0; j < PIECE_EPL; ++j)
+            for (int u = 0; u < 2; ++u)
+                if (sl[j][u] >= 0) tab_p1(T, sl[j][u], wh[j], wi[j], si[j]);
         __syncthreads();
-        // phase 2: the sums of those windows, the thread deltas
 #pragma unroll
-        for (int j = 0; j < PIECE_EPL; ++j) {
-            if (wh[j] == AW_NONE) continue;
-            const int64_t W = tt[j] - tt[j] % 500, M = tt[j] - tt[j] % 1000;
-            const int p = (int)((W / 500) & 1), q = (int)((M / 1000) & 1);
-            const uint32_t c = cz[j] & 0xFFFFu, rt = cz[j] >> 16;
-            for (int u = 0; u < 2; ++u) {
-                const int i = sl[j][u];
-                if (i < 0) continue;
-                if (wh[j] == AW_PASS) {
-                    atomicAdd(&T.thread[i], 1);
-                    if (T.W[i][p] == W) atomicAdd(&T.s[i][p][0], (unsigned long long)c);
-                    if (T.MW[i][q] == M) atomicAdd(&T.mpass[i][q], (unsigned long long)c);
-                } else if (wh[j] == AW_BLOCK) {
-                    if (T.W[i][p] == W) atomicAdd(&T.s[i][p][1], (unsigned long long)c);
-                } else {
-                    atomicAdd(&T.thread[i], -1);
-                    if (T.W[i][p] == W) {
-                        atomicAdd(&T.s[i][p][2], (unsigned long long)c);
-                        atomicAdd(&T.s[i][p][3], (unsigned long long)rt);
-                        atomicMin(&T.minrt[i][p], rt);
-                    }
-                }
-            }
-        }
+        for (int j = 0; j < PIECE_EPL; ++j)
+            for (int u = 0; u < 2; ++u)
+                if (sl[j][u] >= 0) tab_p2(T, sl[j][u], wh[j], wi[j], si[j], cz[j] & 0xFFFFu, cz[j] >> 16);
         __syncthreads();
         const uint32_t nu = T.nused;
         if (one) {  // the whole segment: commit
             for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
+                const uint32_t i = T.used[u];
                 AuxAcc A;
-                tab_acc(T, T.used[u], A);
-                aux_commit(S, cfg.max_rt, sg.res, A, bflags);
+                tab_acc(T, i, T.key[i], b500, b1000, A);
+                if (!(cfg.dbg_flags & 2048)) aux_commit(S, cfg.max_rt, sg.res, A, bflags, &claims);
             }
-            continue;
-        }
-        __shared__ uint32_t off;
-        if (threadIdx.x == 0) {
-            off = atomicAdd(pool_n, nu);
-            meta[k] = off + nu <= pool_cap ? (((uint64_t)off << 32) | nu) : (uint64_t)AUX_NONE;
+        } else {
+            if (threadIdx.x == 0) {
+                off = atomicAdd(pool_n, nu);
+                meta[k] = off + nu <= pool_cap ? (((uint64_t)off << 32) | nu) : (uint64_t)AUX_NONE;
+            }
+            __syncthreads();
+            if (off + nu <= pool_cap)
+                for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
+                    const uint32_t i = T.used[u];
+                    tab_acc(T, i, T.key[i], b500, b1000, pool[off + u]);
+                }
         }
         __syncthreads();
-        if (off + nu <= pool_cap)
-            for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) tab_acc(T, T.used[u], pool[off + u]);
+        tab_reset_used(T);
+        __syncthreads();
+        if (threadIdx.x == 0) T.nused = 0;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) aux_flush_claims(S, claims, bflags);
 }
 
-// one multi-piece segment: amulti[k] = seg << 32 | its first piece's index in the piece list
+// one multi-piece segment (amulti[k] = seg << 32 | its first piece): the pieces' partials merged in a table with
+// 64-bit sums (every thread folds whole pieces), then committed
+struct MTab {
+    uint32_t key[TAB_S];
+    long long W[TAB_S][2], MW[TAB_S][2];
+    unsigned long long s[TAB_S][2][4];
+    uint32_t minrt[TAB_S][2];
+    unsigned long long mpass[TAB_S][2];
+    int32_t thread[TAB_S];
+    uint32_t used[TAB_S];
+    uint32_t nused, overflow;
+};
+__device__ __forceinline__ int mtab_find(MTab& T, uint32_t key) {
+    uint32_t h = (uint32_t)(mix64(key) & (TAB_S - 1));
+    for (int probe = 0; probe < TAB_S; ++probe) {
+        uint32_t k = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == AUX_EMPTY32) {
+            k = atomicCAS(&T.key[h], AUX_EMPTY32, key);
+            if (k == AUX_EMPTY32) { T.used[atomicAdd(&T.nused, 1u)] = h; return (int)h; }
+        }
+        if (k == key) return (int)h;
+        h = (h + 1) & (TAB_S - 1);
+    }
+    atomicOr(&T.overflow, 1u);
+    return -1;
+}
 __global__ __launch_bounds__(256) void k_aux_merge(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                                    const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                                                    DevState S, DevCfg cfg, int64_t t0, const uint32_t* __restrict__ dec,
                                                    const AuxAcc* __restrict__ pool, const uint64_t* __restrict__ meta,
                                                    uint32_t* __restrict__ bflags) {
-    __shared__ AuxTab T;
-    __shared__ uint32_t bad;
+    __shared__ MTab T;
+    __shared__ uint32_t bad, claims;
     const uint32_t m = *cnt;
+    if (threadIdx.x == 0) claims = 0;
     for (uint32_t k = blockIdx.x; k < m; k += gridDim.x) {
         const uint64_t e = list[k];
         const Seg sg = segs[(uint32_t)(e >> 32)];
         const uint32_t q0 = (uint32_t)e, np = (sg.len + AUX_PIECE - 1) / AUX_PIECE;
         __syncthreads();
-        tab_init(T);
-        if (threadIdx.x == 0) bad = 0;
+        for (uint32_t i = threadIdx.x; i < TAB_S; i += blockDim.x) {
+            T.key[i] = AUX_EMPTY32;
+            T.W[i][0] = T.W[i][1] = T.MW[i][0] = T.MW[i][1] = -1;
+            for (int p = 0; p < 2; ++p) {
+                for (int c = 0; c < 4; ++c) T.s[i][p][c] = 0;
+                T.minrt[i][p] = 0xFFFFFFFFu;
+                T.mpass[i][p] = 0;
+            }
+            T.thread[i] = 0;
+        }
+        if (threadIdx.x == 0) { bad = 0; T.nused = 0; T.overflow = 0; }
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < np; q += blockDim.x)
-            if ((uint32_t)meta[q0 + q] == AUX_NONE) bad = 1;
-        __syncthreads();
-        // phase 1 over every partial of every piece: keys, latest windows
-        for (uint32_t q = 0; q < np && !bad; ++q) {
+        // phase 1: every thread folds whole pieces (keys, latest windows)
+        for (uint32_t q = threadIdx.x; q < np; q += blockDim.x) {
             const uint64_t mt = meta[q0 + q];
             const uint32_t off = (uint32_t)(mt >> 32), n = (uint32_t)mt;
-            for (uint32_t u = threadIdx.x; u < n; u += blockDim.x) {
+            if (n == AUX_NONE) { bad = 1; continue; }
+            for (uint32_t u = 0; u < n; ++u) {
                 const AuxAcc& A = pool[off + u];
-                const int i = tab_slot(T, A.key);
+                const int i = mtab_find(T, A.key);
                 if (i < 0) continue;
                 for (int p = 0; p < 2; ++p) {
-                    if (A.W[p] >= 0) atomicMax((long long*)&T.W[i][p], (long long)A.W[p]);
-                    if (A.MW[p] >= 0) atomicMax((long long*)&T.MW[i][p], (long long)A.MW[p]);
+                    if (A.W[p] > T.W[i][p]) atomicMax(&T.W[i][p], (long long)A.W[p]);
+                    if (A.MW[p] > T.MW[i][p]) atomicMax(&T.MW[i][p], (long long)A.MW[p]);
                 }
             }
         }
@@ -386,38 +540,52 @@ __global__ __launch_bounds__(256) void k_aux_merge(const SEv* __restrict__ recs,
                          bflags);
             continue;
         }
-        for (uint32_t q = 0; q < np; ++q) {
+        for (uint32_t q = threadIdx.x; q < np; q += blockDim.x) {
             const uint64_t mt = meta[q0 + q];
             const uint32_t off = (uint32_t)(mt >> 32), n = (uint32_t)mt;
-            for (uint32_t u = threadIdx.x; u < n; u += blockDim.x) {
+            for (uint32_t u = 0; u < n; ++u) {
                 const AuxAcc& A = pool[off + u];
-                const int i = tab_slot(T, A.key);
-                atomicAdd(&T.thread[i], A.thread);
+                const int i = mtab_find(T, A.key);
+                if (A.thread) atomicAdd(&T.thread[i], A.thread);
                 for (int p = 0; p < 2; ++p) {
                     if (A.W[p] >= 0 && A.W[p] == T.W[i][p]) {
-                        for (int c = 0; c < 4; ++c) atomicAdd(&T.s[i][p][c], (unsigned long long)A.s[p][c]);
-                        atomicMin(&T.minrt[i][p], A.minrt[p]);
+                        for (int c = 0; c < 4; ++c)
+                            if (A.s[p][c]) atomicAdd(&T.s[i][p][c], (unsigned long long)A.s[p][c]);
+                        if (A.minrt[p] != 0xFFFFFFFFu) atomicMin(&T.minrt[i][p], A.minrt[p]);
                     }
-                    if (A.MW[p] >= 0 && A.MW[p] == T.MW[i][p]) atomicAdd(&T.mpass[i][p], (unsigned long long)A.mpass[p]);
+                    if (A.MW[p] >= 0 && A.MW[p] == T.MW[i][p] && A.mpass[p])
+                        atomicAdd(&T.mpass[i][p], (unsigned long long)A.mpass[p]);
                 }
             }
         }
         __syncthreads();
         for (uint32_t u = threadIdx.x; u < T.nused; u += blockDim.x) {
+            const uint32_t i = T.used[u];
             AuxAcc A;
-            tab_acc(T, T.used[u], A);
-            aux_commit(S, cfg.max_rt, sg.res, A, bflags);
+            A.key = T.key[i];
+            A.thread = T.thread[i];
+            for (int p = 0; p < 2; ++p) {
+                A.W[p] = T.W[i][p];
+                A.MW[p] = T.MW[i][p];
+                A.minrt[p] = T.minrt[i][p];
+                A.mpass[p] = T.mpass[i][p];
+                for (int c = 0; c < 4; ++c) A.s[p][c] = T.s[i][p][c];
+            }
+            if (!(cfg.dbg_flags & 2048)) aux_commit(S, cfg.max_rt, sg.res, A, bflags, &claims);
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) aux_flush_claims(S, claims, bflags);
 }
 
 namespace sg {
-// aux[0..2] = short / piece / multi counts (device); lists from k_seg_bin
+// aux[0..3] = short / piece / multi / long counts (device); lists from k_seg_bin
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
-                      const uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg, int64_t t0,
-                      const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
+                      const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
+                      int64_t t0, const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
                       uint32_t* bflags, hipStream_t st) {
-    hipLaunchKernelGGL(k_aux_short, dim3(1024), dim3(256), 0, st, recs, segs, ashort, aux + 0, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_aux_cold, dim3(2048), dim3(256), 0, st, recs, segs, ashort, aux + 0, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_aux_expand, dim3(512), dim3(256), 0, st, segs, along, aux + 3, apiece);
     hipLaunchKernelGGL(k_aux_piece, dim3(2048), dim3(256), 0, st, recs, segs, apiece, aux + 1, S, cfg, t0, dec, pool,
                        pool_cap, pool_n, meta, bflags);
     hipLaunchKernelGGL(k_aux_merge, dim3(256), dim3(256), 0, st, recs, segs, amulti, aux + 2, S, cfg, t0, dec, pool, meta,

@@ -129,9 +129,10 @@ __global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ k
 // blkcnt[bin][block] (a scan turns them into dispatch offsets); the rank inside the block rides
 // in Seg.bin's upper bits until k_seg_order places the segment.
 // Aux lists (sg_submit_ex batches; aux == null otherwise): the segments whose origin / context nodes the aux.hip
-// post-pass updates -- short ones one lane each (aux[0] = count, list ashort), long ones in pieces of AUX_PIECE
-// events (aux[1] = pieces, list apiece = seg << 32 | piece), and of those the segments of more than one piece,
-// whose pieces' partial results are merged (aux[2] = count, list amulti = seg << 32 | first piece).
+// post-pass updates -- short ones (aux[0] = count, list ashort), long ones (aux[3] = count, list along = seg << 32 |
+// first piece; aux[1] = their pieces of AUX_PIECE events, expanded by k_aux_expand), and of those the segments of
+// more than one piece, whose pieces' partial results are merged (aux[2] = count, list amulti = seg << 32 | first
+// piece).
 #define AUX_SHORT 256u
 __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t k) {  // one atomic per wave
     uint32_t x = k;
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  uint32_t lane_max, uint32_t j1_max,
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
                                                  uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide, uint32_t* __restrict__ aux,
-                                                 uint32_t* __restrict__ ashort, uint64_t* __restrict__ apiece,
+                                                 uint32_t* __restrict__ ashort, uint64_t* __restrict__ along,
                                                  uint64_t* __restrict__ amulti) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
@@ -205,7 +206,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const uint32_t o = wave_alloc(aux + 0, aux_short ? 1u : 0u);
         if (aux_short) ashort[o] = s;
         const uint32_t q = wave_alloc(aux + 1, aux_np);
-        for (uint32_t i = 0; i < aux_np; ++i) apiece[q + i] = ((uint64_t)s << 32) | i;
+        const uint32_t j = wave_alloc(aux + 3, aux_np ? 1u : 0u);
+        if (aux_np) along[j] = ((uint64_t)s << 32) | q;
         const uint32_t u = wave_alloc(aux + 2, aux_np > 1 ? 1u : 0u);
         if (aux_np > 1) amulti[u] = ((uint64_t)s << 32) | q;
     }
@@ -3051,12 +3053,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 // mp: the segment count on the device; mb: an upper bound of it (the grid)
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* apiece,
+                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, apiece, amulti);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

@@ -47,12 +47,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
                       uint32_t* part, uint32_t* nseg);
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
-                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* apiece,
+                          uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, hipStream_t st);
 // aux.hip
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
-                      const uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg, int64_t t0,
-                      const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
+                      const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
+                      int64_t t0, const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
                       uint32_t* bflags, hipStream_t st);
 // param.hip
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
@@ -475,9 +475,9 @@ struct sg_engine {
         sg_event_ext* d_ext = nullptr; // sg_submit_ex host inputs staged in HBM
         sg_arg* d_args = nullptr;
         uint64_t ext_cap = 0, args_cap = 0;
-        // sg_submit_ex: the aux.hip post-pass lists k_seg_bin builds (counts in d_bsmall[130..132])
+        // sg_submit_ex: the aux.hip post-pass lists k_seg_bin builds (counts in d_bsmall[130..133])
         uint32_t* d_ashort = nullptr;
-        uint64_t *d_apiece = nullptr, *d_amulti = nullptr;
+        uint64_t *d_apiece = nullptr, *d_amulti = nullptr, *d_along = nullptr;
         uint64_t aux_cap_n = 0;
         Link* d_link = nullptr;        // frozen-stretch skipping side tables (DevState.link/bst/pend/spans)
         uint32_t *d_bst = nullptr, *d_pend = nullptr;
@@ -595,7 +595,7 @@ static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
     dfree(B.d_prev); dfree(B.d_bsmall);
     dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans); dfree(B.d_ext); dfree(B.d_args);
-    dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti);
+    dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti); dfree(B.d_along);
     B.ext_cap = B.args_cap = B.aux_cap_n = 0;
     B.d_link = nullptr; B.d_bst = B.d_pend = nullptr; B.d_spans = nullptr;
     B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
@@ -1755,9 +1755,10 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
 static int ensure_aux(sg_engine* e, sg_engine::BatchSlot& B, uint64_t n) {
     const uint64_t npiece = n / AUX_PIECE + n / 257 + 64;  // pieces: every long segment's, <= n/P + n/(AUX_SHORT + 1)
     if (n > B.aux_cap_n) {
-        dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti);
+        dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti); dfree(B.d_along);
         const uint64_t c = std::max<uint64_t>(n, 1u << 16);
         HIPCHK(hipMalloc(&B.d_ashort, c * 4));
+        HIPCHK(hipMalloc(&B.d_along, (c / 257 + 64) * 8));
         HIPCHK(hipMalloc(&B.d_apiece, (c / AUX_PIECE + c / 257 + 64) * 8));
         HIPCHK(hipMalloc(&B.d_amulti, (c / AUX_PIECE + 64) * 8));
         B.aux_cap_n = c;
@@ -1888,7 +1889,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     }
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
-                          B.d_ashort, B.d_apiece, B.d_amulti, gs));
+                          B.d_ashort, B.d_along, B.d_amulti, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets
@@ -2060,8 +2061,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
     // origin / context nodes of the segments decided off k_lane<16>, from the committed verdicts (aux.hip)
     if (ext)
-        HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_apiece, B.d_amulti, S, dc, t0, e->d_dec,
-                          e->d_auxpool, e->auxpool_cap, e->d_bsmall + 133, e->d_auxmeta, e->d_bsmall + 0, st));
+        HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_along, B.d_apiece, B.d_amulti, S, dc,
+                          t0, e->d_dec, e->d_auxpool, e->auxpool_cap, e->d_bsmall + 134, e->d_auxmeta, e->d_bsmall + 0,
+                          st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
     HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
