@@ -31,7 +31,7 @@ chunk barriers synchronise them.  The step time is the max over ranks and value 
 entries / that time.
 
 After the C4 line's measurement (N = 1), the same pipeline measures the other SURVEY.md §8(d) configs
-C2, C3 and C5 (bounded traces, inputs in HBM) and reports them under "configs" (--no-configs: skip).
+C2, C3, C5 and C6 (bounded traces, inputs in HBM) and reports them under "configs" (--no-configs: skip).
 """
 from __future__ import annotations
 
@@ -70,7 +70,7 @@ def parse():
                    help="fraction of free HBM for one timed chunk's inputs")
     p.add_argument("--sharding", choices=("balanced", "hash"), default="balanced",
                    help="resource -> GPU partition: balanced by event counts, or splitmix64(res_id) %% N")
-    p.add_argument("--no-configs", action="store_true", help="skip the C2 / C3 / C5 sub-lines")
+    p.add_argument("--no-configs", action="store_true", help="skip the C2 / C3 / C5 / C6 sub-lines")
     p.add_argument("--resources", type=int, default=1_000_000)
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="partitioned oracle threads (0: this job's CPU share -- cgroup cpu.max, else min(16, cores))")
@@ -427,6 +427,9 @@ CONFIGS = [
     (3, 24_000_000, 1 << 24, {}, 1, "C3: 100k resources, QPS / thread / WarmUp / RateLimiter / WarmUpRateLimiter"),
     (5, 12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
      "C5: 10k resources, ParamFlow QPS rules (20 % throttle) over 10M Zipf values"),
+    (6, 49_500_000, 1 << 25, {"param_table_log2": 28, "status_ring_log2": 28}, 0,
+     "C6 (north_star's mixed rules): 1M resources, each a QPS flow rule + a DegradeRule + a QPS ParamFlowRule on "
+     "args[0] (values Zipf(1.1) over 10M), Zipf(1.1) traffic"),
 ]
 EXT_NOTE = ("sg_submit_ex, the Java drop-in's call: every event in one of 4 named contexts (ContextUtil.enter) from "
             "one of 16 origins, uniformly (an EXIT carries its ENTRY's); origin StatisticNodes and context "
@@ -484,7 +487,7 @@ def param_args(ev):
 
 
 def config_lines(dev, c4=None):
-    """The SURVEY.md configs besides the headline: C2, C3, C5; with c4 = (workload, events) of the headline trace,
+    """The SURVEY.md configs besides the headline: C2, C3, C5, C6 (mixed rules); with c4 = (workload, events) of the headline trace,
     C4 and C4-ext on its first 3 global batches (the same events through sg_submit and sg_submit_ex), C5-ext, and
     the drop-in's operating point (dropin_line)."""
     import torch

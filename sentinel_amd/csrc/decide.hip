@@ -153,7 +153,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  uint32_t j4_max, uint32_t force_lane, uint32_t* __restrict__ blkcnt,
                                                  uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide, uint32_t* __restrict__ aux,
                                                  uint32_t* __restrict__ ashort, uint64_t* __restrict__ along,
-                                                 uint64_t* __restrict__ amulti) {
+                                                 uint64_t* __restrict__ amulti, uint32_t* __restrict__ mixc,
+                                                 uint32_t* __restrict__ mix, uint32_t mix_cap) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     bool aux_short = false;
     uint32_t aux_np = 0;
+    uint32_t mixk = 0;  // 1: an XF_MIX segment of a cooperative bin (narrow pre / post pass), 2: wide
     Seg sg;
     if (s < m) {
         sg = segs[s];
@@ -174,8 +176,11 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const bool lane_only = (pm & (PM_PRIO | PM_LANE)) != 0 || ((pm & PM_AUX) && (p.multi & (PX_ORIGIN | PX_CHAIN)));
         const bool inline_aux = (pm & PM_AUX) && (lane_only || p.multi);  // k_lane<16> updates the nodes itself
         const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // PX_*: decided with 16-rule lanes
-        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && p.n_param == 0 && sg.len > lane_max &&
+        // XF_MIX: the param checks run in k_pq's pre pass (args[0] from the key ring: no argument lists)
+        const bool mixp = (p.xf & XF_MIX) && pq && mix && !(pm & PM_ARGL);
+        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && (p.n_param == 0 || mixp) && sg.len > lane_max &&
                           !lane_only && !p.multi;
+        if (coop && p.n_param) mixk = sg.len > pq_wide ? 2u : 1u;
         uint32_t bin;
         if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS)))
             bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
@@ -210,6 +215,12 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         if (aux_np) along[j] = ((uint64_t)s << 32) | q;
         const uint32_t u = wave_alloc(aux + 2, aux_np > 1 ? 1u : 0u);
         if (aux_np > 1) amulti[u] = ((uint64_t)s << 32) | q;
+    }
+    if (mix) {  // (wave-uniform)
+        const uint32_t a = wave_alloc(mixc + 0, mixk == 1 ? 1u : 0u);
+        if (mixk == 1) mix[a] = s;
+        const uint32_t b = wave_alloc(mixc + 1, mixk == 2 ? 1u : 0u);
+        if (mixk == 2) mix[mix_cap + b] = s;
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) blkcnt[(uint64_t)b * nblk + blockIdx.x] = cnt[b];
@@ -370,18 +381,20 @@ __global__ __launch_bounds__(256) void k_fill(const Span* __restrict__ spans, co
         const bool cut = (sp.res >> 31) != 0;
         const Prog pg = prog[res];
         const int nf = pg.n_flow < 4 ? pg.n_flow : 4;
+        const uint32_t fo = pg.rule_off + pg.n_param;  // the flow stages (XF_MIX: after the param rules)
         double fc[4];
         uint32_t fd[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            fc[s] = s < nf ? rules[pg.rule_off + s].count : 0.0;
-            fd[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, rules[pg.rule_off + s].slot, 0) : 0u;
+            fc[s] = s < nf ? rules[fo + s].count : 0.0;
+            fd[s] = s < nf ? mk_dec(ST_BLOCK_FLOW, rules[fo + s].slot, 0) : 0u;
         }
-        const uint32_t cdec = (cut && pg.n_degrade) ? mk_dec(ST_BLOCK_DEGRADE, rules[pg.rule_off + pg.n_flow].slot, 0) : 0u;
+        const uint32_t cdec = (cut && pg.n_degrade) ? mk_dec(ST_BLOCK_DEGRADE, rules[fo + pg.n_flow].slot, 0) : 0u;
         for (uint32_t p = sp.s + threadIdx.x; p < sp.e; p += blockDim.x) {
             const uint4 r = reinterpret_cast<const uint4*>(recs)[p];
             uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
             if ((r.w & 0xFFu) == SG_EV_ENTRY) {
+                if ((r.w >> 8) & RF_PBLK) continue;  // the param pre pass's verdict stands
                 const double curv = (double)j_iadd(sp.pint, (int)(r.z & 0xFFFFu));
                 uint32_t v = 0;
 #pragma unroll
@@ -1473,24 +1486,25 @@ struct JEv {
     uint32_t kf;  // kind (0xFF: no event) | JK_VALID | JK_WIN | JK_VAL
     uint32_t wi;  // JK_WIN: status-window index of the referenced ENTRY
 };
-enum : uint32_t { JK_VALID = 0x100u, JK_WIN = 0x200u, JK_VAL = 0x400u };
-// an event's class in one Jacobi iteration: in the round, ENTRY, effective EXIT, effective TRACE
-enum : uint32_t { JC_INR = 1u, JC_ENT = 2u, JC_XE = 4u, JC_TE = 8u };
+enum : uint32_t { JK_VALID = 0x100u, JK_WIN = 0x200u, JK_VAL = 0x400u, JK_PB = 0x800u /* RF_PBLK ENTRY */ };
+// an event's class in one Jacobi iteration: in the round, ENTRY, effective EXIT, effective TRACE, ENTRY a param rule
+// blocked (XF_MIX: a block in the statistics, no flow / degrade check)
+enum : uint32_t { JC_INR = 1u, JC_ENT = 2u, JC_XE = 4u, JC_TE = 8u, JC_PB = 16u };
 
 // the scanned quantities (Q_*) of one event under its outcome guess g
 template <int NQ>
 __device__ __forceinline__ void jac_q(uint32_t (&q)[NQ], uint32_t c, uint32_t g, uint32_t cz, uint32_t nr, uint32_t nf) {
     const uint32_t cnt = cz & 0xFFFFu, rtv = cz >> 16;
-    const bool ent = (c & JC_ENT) != 0, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0;
+    const bool ent = (c & JC_ENT) != 0, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0, pb = (c & JC_PB) != 0;
     const bool gp = ent && g == nr;
     q[Q_P] = gp ? cnt : 0u;
-    q[Q_B] = (ent && !gp) ? cnt : 0u;
+    q[Q_B] = ((ent && !gp) || pb) ? cnt : 0u;
     q[Q_S] = xe ? cnt : 0u;
     q[Q_RT] = xe ? rtv : 0u;
     q[Q_E] = te ? cnt : 0u;
     q[Q_TH] = gp ? 1u : (xe ? 0xFFFFFFFFu : 0u);
     q[Q_MIN] = xe ? rtv : NO_LANE;
-    q[Q_TI] = ((ent || xe || te) ? 1u : 0u) | ((c & JC_INR) ? 0x10000u : 0u);
+    q[Q_TI] = ((ent || xe || te || pb) ? 1u : 0u) | ((c & JC_INR) ? 0x10000u : 0u);
 #pragma unroll
     for (int k = Q_TR; k < NQ; ++k) {  // guessed breaker trips, two degrade stages per word
         const uint32_t s0 = nf + 2u * (uint32_t)(k - Q_TR);
@@ -1541,6 +1555,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     if (CLS != 0 && (((pg.pflags & PF_FROZEN) != 0) != (CLS == 1))) return;  // the other instantiation's segment
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    // XF_MIX: the param rules come first in the program and k_pq's pre pass has decided them: an ENTRY one of them
+    // blocked carries RF_PBLK (its dec[] word is final) and is a block here, nothing more
+    const uint32_t roff = pg.rule_off + pg.n_param;
+    const bool mixp = pg.n_param != 0;
     if (tid == 0) {
         node_load(sh.node, S, res);
         sh.round_open = 0;
@@ -1550,8 +1568,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         sh.nsp = 0;
     }
     if ((int)tid < nr) {
-        sh.rules[tid] = S.rules[pg.rule_off + tid];
-        sh.rs[tid] = S.rstate[pg.rule_off + tid];
+        sh.rules[tid] = S.rules[roff + tid];
+        sh.rs[tid] = S.rstate[roff + tid];
     }
     __syncthreads();
     const bool chain = (sh.node.flags & NI_CHAIN) != 0;  // host routes switch_on == 0 to k_lane
@@ -1595,9 +1613,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const bool open_on = OPEN && !(cfg.dbg_flags & 64);
     const uint32_t open_min = TILE;
     // single-stage programs with closed-form admission guesses (see the Jacobi iteration)
+    // (not with param-blocked ENTRYs in the mix: the closed forms count every ENTRY as an acquire)
     const bool tg_mode = nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_THREAD &&
-                         sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_DEFAULT && !(cfg.dbg_flags & 16);
-    const bool rl_mode = RL && nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_QPS &&
+                         sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_DEFAULT && !(cfg.dbg_flags & 16) && !mixp;
+    const bool rl_mode = RL && !mixp && nf == 1 && nd == 0 && sh.rules[0].grade == SG_FLOW_GRADE_QPS &&
                          (sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
                           sh.rules[0].behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) && !(cfg.dbg_flags & 16);
 
@@ -1640,6 +1659,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         x.dt = valid ? r.dt : 0;
         x.cz = (uint32_t)r.cnt | ((uint32_t)r.rt << 16);
         x.kf = valid ? ((uint32_t)r.kind | JK_VALID) : 0xFFu;
+        if (valid && r.kind == SG_EV_ENTRY && (r.flags & RF_PBLK)) x.kf |= JK_PB;
         x.wi = 0;
         if (valid && r.kind != SG_EV_ENTRY) {
             if (r.code == RC_NONE || r.code == RC_PASSED) x.kf |= JK_VAL;  // the chain exists here
@@ -1668,7 +1688,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         for (int e = 0; e < EP; ++e) {
             gg[e] = g0;
             if ((ev[e].kf & JK_VALID) && lp0 + (uint32_t)e >= from)
-                win[(tbase + lp0 + e) & (WIN - 1)] = ((ev[e].kf & 0xFFu) == SG_EV_ENTRY && g0 == (uint32_t)nr) ? 1 : 0;
+                win[(tbase + lp0 + e) & (WIN - 1)] =
+                    ((ev[e].kf & (0xFFu | JK_PB)) == SG_EV_ENTRY && g0 == (uint32_t)nr) ? 1 : 0;
         }
     };
     static_assert(WIN - TILE >= (FULL_FENCE_TILES + 1) * TILE, "old references must be older than one full fence");
@@ -1992,6 +2013,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 if (s < nf && (((warmm >> s) & 1) ? !(curw <= fcount[s]) : curv > fcount[s])) fd = fdec[s];
                         }
                         if (fd == 0 && cutk0) fd = cdec;
+                        if ((rr[k].w >> 8) & RF_PBLK) fd = 1u;  // blocked by a param rule: its word is written
                         fdv[k] = fd;
                         const bool stop = q < sg.len && (!in || (ek == SG_EV_ENTRY && fd == 0));
                         if (stop && q < mystop) mystop = q;
@@ -2021,7 +2043,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 win[q & (WIN - 1)] = 0;
                                 aB += ec;
                                 aTI += 1;
-                                if (warmm) {  // stages up to the blocking one (all flow stages when a breaker blocks)
+                                if (warmm && d != 1u) {  // stages up to the blocking one (all flow stages when a breaker blocks)
                                     uint32_t bs = (uint32_t)nf;
 #pragma unroll
                                     for (int s = MF - 1; s >= 0; --s)
@@ -2047,7 +2069,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 }
                             }
                         }
-                        *(cm ? &dec[sg.start + q] : &S.sink[tid]) = d;
+                        *((cm && d != 1u) ? &dec[sg.start + q] : &S.sink[tid]) = d;
                     }
                     if (f != NO_LANE) { fend = f; break; }
                     sb += ST;
@@ -2140,7 +2162,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     ksg[k] = 0;
                     pcb0[k] = k < nd ? (int32_t)sh.rs[nf + k].b : 0;
                 }
+                int64_t kB = 0;                           // XF_MIX: param-blocked units of the earlier chunks
                 uint32_t aP = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aTH = 0, aMin = NO_LANE;  // committed (lane)
+                uint32_t aB = 0;    // XF_MIX: committed param-blocked units (lane)
                 bool oent = false;  // the lane committed an ENTRY
                 const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
                 const uint32_t qmax = sg.len - 1;
@@ -2159,7 +2183,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     }
                     // classes under the all-pass guess; 0x80: a stop before evaluation (past the round / segment)
                     uint32_t cl[OE];
-                    uint32_t lp = 0, ls = 0, lrt = 0, le = 0;
+                    uint32_t lp = 0, ls = 0, lrt = 0, le = 0, lb = 0;
 #pragma unroll
                     for (int k = 0; k < (int)OE; ++k) {
                         const uint32_t q = sb + tid * OE + k;
@@ -2168,13 +2192,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         const uint32_t code = (rr[k].w >> 16) & 0xFFu;
                         uint32_t c = 0;
                         if (q >= sg.len || edt >= dhi || edt < dlo) c = 0x80u;
-                        else if (ek == SG_EV_ENTRY) c = JC_ENT;
+                        else if (ek == SG_EV_ENTRY) c = ((rr[k].w >> 8) & RF_PBLK) ? JC_PB : JC_ENT;
                         else {
                             bool eff = code == RC_NONE || code == RC_PASSED;
                             if (code == RC_BATCH) {
                                 const uint32_t rel = rr[k].y - sg.start;
                                 if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
-                                else if (rel >= fpos0) eff = true;  // an ENTRY of this stretch: passed
+                                else if (rel >= fpos0)  // an ENTRY of this stretch: passed, unless a param rule blocked it
+                                    eff = !mixp || !((reinterpret_cast<const uint4*>(recs)[rr[k].y].w >> 8) & RF_PBLK);
                                 else if (rel + WIN >= sb + OST) eff = win[rel & (WIN - 1)] != 0;
                                 else eff = !in_span(rel) &&
                                            st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
@@ -2188,34 +2213,41 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         ls += (c & JC_XE) ? ec : 0u;
                         lrt += (c & JC_XE) ? ert : 0u;
                         le += (c & JC_TE) ? ec : 0u;
+                        lb += (c & JC_PB) ? ec : 0u;
                     }
                     // block-exclusive prefixes of the lane totals, and the chunk totals
-                    uint32_t xp = lp, xs = ls, xrt = lrt, xe = le;
+                    uint32_t xp = lp, xs = ls, xrt = lrt, xe = le, xb = lb;
                     WAVE_SCAN(xp, 0u, op_add);
                     WAVE_SCAN(xs, 0u, op_add);
                     WAVE_SCAN(xrt, 0u, op_add);
                     WAVE_SCAN(xe, 0u, op_add);
-                    uint32_t tP, tS, tRT, tE;
+                    if (mixp) WAVE_SCAN(xb, 0u, op_add);
+                    uint32_t tP, tS, tRT, tE, tB = 0;
                     if (NW == 1) {
                         tP = (uint32_t)__builtin_amdgcn_readlane((int)xp, 63);
                         tS = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
                         tRT = (uint32_t)__builtin_amdgcn_readlane((int)xrt, 63);
                         tE = (uint32_t)__builtin_amdgcn_readlane((int)xe, 63);
-                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le;
+                        if (mixp) tB = (uint32_t)__builtin_amdgcn_readlane((int)xb, 63);
+                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le; xb -= lb;
                     } else {
-                        if (lane == 63) { sh.part[wv][0] = xp; sh.part[wv][1] = xs; sh.part[wv][2] = xrt; sh.part[wv][3] = xe; }
+                        if (lane == 63) {
+                            sh.part[wv][0] = xp; sh.part[wv][1] = xs; sh.part[wv][2] = xrt; sh.part[wv][3] = xe;
+                            sh.part[wv][4] = xb;
+                        }
                         lds_barrier();
                         // lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv and the chunk total
-                        uint32_t* const xs4[4] = {&xp, &xs, &xrt, &xe};
-                        uint32_t* const ts4[4] = {&tP, &tS, &tRT, &tE};
+                        uint32_t* const xs4[5] = {&xp, &xs, &xrt, &xe, &xb};
+                        uint32_t* const ts4[5] = {&tP, &tS, &tRT, &tE, &tB};
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
+                        for (int i = 0; i < 5; ++i) {
+                            if (i == 4 && !mixp) break;
                             uint32_t v = lane < (uint32_t)NW ? sh.part[lane][i] : 0u;
                             WAVE_SCAN(v, 0u, op_add);
                             *xs4[i] += wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
                             *ts4[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
                         }
-                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le;
+                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le; xb -= lb;
                     }
                     // RT breakers: which ENTRYs see an average at the threshold, then the segmented passCount scan
                     uint32_t badb = 0, segl[MD], segt[MD];
@@ -2266,7 +2298,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     }
                     // every ENTRY against its prefix view; the lane's first stop
                     uint32_t mystop = NO_LANE, myo = (uint32_t)nr, sst[MD];
-                    uint32_t rp = 0, rs2 = 0, re = 0, rseg[MD];
+                    uint32_t rp = 0, rs2 = 0, re = 0, rb = 0, rseg[MD];
 #pragma unroll
                     for (int k = 0; k < MD; ++k) rseg[k] = sst[k] = 0;
 #pragma unroll
@@ -2294,7 +2326,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                     } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
                                         const double exc = (double)(E0 + kE + (int64_t)(xe + re)) / 1.0;
                                         const double succ = (double)vS / 1.0;
-                                        const double total = (double)vP / 1.0 + (double)B0 / 1.0;
+                                        const double total = (double)vP / 1.0 + (double)(B0 + kB + (int64_t)(xb + rb)) / 1.0;
                                         if (total < 5) ok = true;
                                         else if (succ - exc <= 0 && exc < 5) ok = true;
                                         else ok = exc / succ < r.count;
@@ -2314,6 +2346,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         rp += (c & JC_ENT) ? ec : 0u;
                         rs2 += (c & JC_XE) ? ec : 0u;
                         re += (c & JC_TE) ? ec : 0u;
+                        rb += (c & JC_PB) ? ec : 0u;
                         if (has_rt) {
 #pragma unroll
                             for (int k = 0; k < MD; ++k)
@@ -2351,9 +2384,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 win[q & (WIN - 1)] = 0;
                                 if (c & JC_XE) { aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1; }
                                 else if (c & JC_TE) { aE += ec; aTI += 1; }
+                                else if (c & JC_PB) { aB += ec; aTI += 1; }
                             }
                         }
-                        *(cm ? &dec[sg.start + q] : &S.sink[tid]) = d;
+                        *((cm && !(c & JC_PB)) ? &dec[sg.start + q] : &S.sink[tid]) = d;
                     }
                     if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
                         const uint32_t na = (uint32_t)__popc(appm);
@@ -2378,7 +2412,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         fend = f < sg.len ? f : sg.len;
                         break;
                     }
-                    kP += tP; kS += tS; kRT += tRT; kE += tE;
+                    kP += tP; kS += tS; kRT += tRT; kE += tE; kB += tB;
 #pragma unroll
                     for (int k = 0; k < MD; ++k) ksg[k] = op_seg(ksg[k], segt[k]);
                     sb += OST;
@@ -2396,10 +2430,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 WAVE_SCAN(aTI, 0u, op_add);
                 WAVE_SCAN(aTH, 0u, op_add);
                 WAVE_SCAN(aMin, NO_LANE, op_min);
+                if (mixp) WAVE_SCAN(aB, 0u, op_add);
                 lds_barrier();  // sh.part's chunk exchange is read; sh.os_* is written
                 if (lane == 63) {
                     sh.part[wv][0] = aP; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
-                    sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin;
+                    sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin; sh.part[wv][7] = aB;
                 }
                 const uint32_t g = uni(sh.os_o);
                 // re-enter the tile machinery at the stop; guesses = the stop's evaluated outcome
@@ -2422,6 +2457,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         sh.cP += sh.part[w][0]; sh.cS += sh.part[w][1]; sh.cRT += sh.part[w][2]; sh.cE += sh.part[w][3];
                         sh.ctouch += sh.part[w][4]; sh.cTH += (int32_t)sh.part[w][5];
                         sh.cminrt = op_min(sh.cminrt, sh.part[w][6]);
+                        sh.cB += sh.part[w][7];
                     }
                     for (int k = 0; k < nd; ++k)
                         if (sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
@@ -2541,7 +2577,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             uint32_t c = 0;
             if (inr) {
                 c = JC_INR;
-                if (kind == SG_EV_ENTRY) c |= JC_ENT;
+                if (kind == SG_EV_ENTRY) c |= (kf & JK_PB) ? JC_PB : JC_ENT;
                 else if (kind == SG_EV_EXIT && eff) c |= JC_XE;
                 else if (kind == SG_EV_TRACE && eff && (ev[e].cz & 0xFFFFu) > 0) c |= JC_TE;
             }
@@ -2897,11 +2933,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             }
 #endif
             if (com) {
+                const bool pbe = (c & JC_PB) != 0;  // its word is the param pre pass's
                 pdec[e] = kind == SG_EV_ENTRY ? out_to_dec(sh.rules, nr, nf, fo, wq[e]) : mk_dec(ST_NOT_ENTRY, 0, 0);
-                pmask |= 1u << e;
-                win[pos & (WIN - 1)] = (kind == SG_EV_ENTRY && fo == (uint32_t)nr) ? 1 : 0;
+                if (!pbe) pmask |= 1u << e;
+                win[pos & (WIN - 1)] = ((c & JC_ENT) && fo == (uint32_t)nr) ? 1 : 0;
                 gg[e] = fo;
-                if (kind == SG_EV_ENTRY) {
+                if (c & JC_ENT) {
                     if (fo == (uint32_t)nr) appm |= 1u << e;
                     if (fo + 1 > fmax) fmax = fo + 1;
                     // the first blocking degrade verdict of a committed ENTRY trips the breaker (DegradeRule.passCheck cut)
@@ -2918,15 +2955,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     }
                 }
                 if (pt == cend - 1) {  // pivot: the last committed event carries the committed totals
-                    const bool ce = kind == SG_EV_ENTRY, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0;
+                    const bool ce = (c & JC_ENT) != 0, xe = (c & JC_XE) != 0, te = (c & JC_TE) != 0;
                     const bool cp = ce && fo == (uint32_t)nr;
                     sh.cP += (int64_t)(ex[Q_P] + run[Q_P]) + (cp ? cnt : 0);
-                    sh.cB += (int64_t)(ex[Q_B] + run[Q_B]) + ((ce && !cp) ? cnt : 0);
+                    sh.cB += (int64_t)(ex[Q_B] + run[Q_B]) + (((ce && !cp) || pbe) ? cnt : 0);
                     sh.cS += (int64_t)(ex[Q_S] + run[Q_S]) + (xe ? cnt : 0);
                     sh.cRT += (int64_t)(ex[Q_RT] + run[Q_RT]) + (xe ? rtv : 0);
                     sh.cE += (int64_t)(ex[Q_E] + run[Q_E]) + (te ? cnt : 0);
                     sh.cTH += (int64_t)(int32_t)(ex[Q_TH] + run[Q_TH]) + (cp ? 1 : (xe ? -1 : 0));
-                    sh.ctouch += ((ex[Q_TI] + run[Q_TI]) & 0xFFFFu) + ((ce || xe || te) ? 1 : 0);
+                    sh.ctouch += ((ex[Q_TI] + run[Q_TI]) & 0xFFFFu) + ((ce || xe || te || pbe) ? 1 : 0);
                     sh.cminrt = op_min(sh.cminrt, op_min(op_min(ex[Q_MIN], run[Q_MIN]), xe ? rtv : NO_LANE));
                     if (RL) {
 #pragma unroll
@@ -3031,7 +3068,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         node_store(sh.node, S, res, pg.pflags);
     }
     __syncthreads();
-    if ((int)tid < nr) S.rstate[pg.rule_off + tid] = sh.rs[tid];
+    if ((int)tid < nr) S.rstate[roff + tid] = sh.rs[tid];
 }
 
 // =================================================================================
@@ -3054,11 +3091,11 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
-                          uint64_t* amulti, hipStream_t st) {
+                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

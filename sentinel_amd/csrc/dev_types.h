@@ -66,6 +66,8 @@ __host__ __device__ inline uint32_t tag_origin(uint32_t tag) { return tag & ((1u
 __host__ __device__ inline uint32_t tag_ctx(uint32_t tag) { return tag >> TAG_ORIGIN_BITS; }
 // internal SEv.flags bits above the ABI's SG_F_*
 #define RF_OWN_ARGS 0x80u  // EXIT of sg_submit_ex with its own args: its args[0] key is in the key ring at its index
+#define RF_PBLK 0x40u      // ENTRY of an XF_MIX segment that a param rule blocked (param.hip k_pq pre pass): its dec[]
+                           // word is final; the flow / degrade owner counts it as a block and evaluates nothing
 
 struct NodeInfo {
     int32_t thread;      // StatisticNode.curThreadNum
@@ -98,8 +100,12 @@ struct Prog {
     uint16_t xf;         // XF_* bits
 };
 enum : uint16_t {
-    XF_PTHREAD = 1       // a THREAD-grade param rule is checked (k_pq resolves an EXIT's release against its ENTRY's
+    XF_PTHREAD = 1,      // a THREAD-grade param rule is checked (k_pq resolves an EXIT's release against its ENTRY's
                          // check of the same tile by key: an EXIT with its own args (PM_XARGS) is k_lane's)
+    XF_MIX = 2           // param rules beside flow / degrade rules, cooperatively decided: k_pq's
+                         // pre pass decides the QPS param checks per value first (nothing before ParamFlowSlot
+                         // blocks), the Jacobi owner the flow / degrade chain with those verdicts as inputs, and
+                         // k_pq's post pass the thread-count map from the final verdicts
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)
@@ -187,12 +193,18 @@ struct PData {
     uint32_t pad;
 };
 static_assert(sizeof(PData) == 16, "PData must be 16 B");
+// A map's buckets are a region of one pool: CacheMaps grow with their keys (ConcurrentLinkedHashMap allocates per
+// entry), so a region starts at PM_MIN_NB buckets and is moved to a larger one (param.hip k_pm_grow) before a batch
+// could put more keys in it than half its slots -- up to map_buckets(cap) (<= 50 % load at capacity).  1M resources
+// with a rule each would otherwise reserve 2 x 256 KiB of HBM per resource.
+#define PM_MIN_NB 2u
+__host__ __device__ inline uint32_t map_buckets(uint32_t cap) { return (2u * cap + PM_BKT - 1) / PM_BKT > 2u ? (2u * cap + PM_BKT - 1) / PM_BKT : 2u; }
 struct PMap {
     uint64_t base;   // first bucket in DevState.pbkt (its slots' data at pdat[base * PM_BKT ...])
     uint64_t bm;     // first word of the live-stamp ring in DevState.pbm (and of the rank scratch in pre)
     int64_t clock;   // next stamp
     int64_t thr;     // <= the lowest live stamp (eviction scans start here)
-    uint32_t nb;     // buckets (>= 2)
+    uint32_t nb;     // buckets (PM_MIN_NB .. map_buckets(cap))
     uint32_t cap;    // min(4000 * durationInSec, 200000) for rule maps, 4000 for thread-count maps
     uint32_t live;   // keys in the map
     uint32_t rb_log2;// ring bits = 2^rb_log2 >= 4 * cap
@@ -381,6 +393,7 @@ enum : uint32_t { BF_PRIORITIZED = 1,
                   BF_BACKWARD = 32, BF_TSPAN = 64,
                   BF_BAD_ARGS = 512,    // an sg_event_ext names args outside the table, or more than SG_MAX_ARGS
                   BF_AUX_FULL = 1024,   // the origin / context node pool is full
+                  BF_POOL_FULL = 2048,  // a param map could not grow: the bucket pool (param_table_log2) is used up
                   BF_MULTI_LINK = 128,  // an ENTRY is referenced by two EXITs (or two TRACEs) of the batch
                   BF_ZERO_CNT = 256 };  // an ENTRY acquires 0 (it may pass inside a saturated stretch)
 

@@ -48,7 +48,7 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
-                          uint64_t* amulti, hipStream_t st);
+                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, hipStream_t st);
 // aux.hip
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
                       const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
@@ -58,6 +58,13 @@ hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, con
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
                      uint32_t* bflags, hipStream_t st);
+hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
+                          uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
+hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
+                              uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
+hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                         const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
+                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st);
 hipError_t launch_seg_order(Seg* segs, const uint32_t* mp, uint32_t mb, const uint32_t* off, uint32_t* order,
                             uint32_t* bin_off, hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
@@ -411,6 +418,7 @@ template <class T> void dfree(T*& p) {
 } // namespace
 
 // =====================================================================================
+#define TMAP_KEY (1ull << 63)  // pmap_key of a thread-count map: TMAP_KEY | res << 8 | paramIdx
 struct sg_engine {
     sg_config cfg;
     int device = 0;
@@ -439,6 +447,11 @@ struct sg_engine {
     std::unordered_map<uint32_t, uint32_t> pmap_index;         // psid -> map index
     std::vector<uint32_t> tm_base;                              // per resource: Prog.tm_base
     uint64_t n_pslot = 0;                                       // bucket slots in the pool (param_table_log2 bound)
+    uint64_t pool_nb = 0;                                       // pool buckets (regions grow into it: k_pm_grow)
+    unsigned long long* d_pool_next = nullptr;                  // next free pool bucket
+    unsigned long long* h_pool_next = nullptr;                  // pinned copy, refreshed by every batch (compaction)
+    uint64_t n_compact = 0;                                     // pool compactions (diagnostics)
+    uint64_t pool_floor = 0;                                    // pool buckets the regions took at the last layout
     uint32_t n_dev_rules = 0;
 
     // device state
@@ -479,6 +492,8 @@ struct sg_engine {
         uint32_t* d_ashort = nullptr;
         uint64_t *d_apiece = nullptr, *d_amulti = nullptr, *d_along = nullptr;
         uint64_t aux_cap_n = 0;
+        uint32_t* d_mix = nullptr;     // XF_MIX segments of the cooperative bins: [0, nmix0) narrow, [mix_cap, ..) wide
+        uint64_t mix_cap = 0;
         Link* d_link = nullptr;        // frozen-stretch skipping side tables (DevState.link/bst/pend/spans)
         uint32_t *d_bst = nullptr, *d_pend = nullptr;
         Span* d_spans = nullptr;
@@ -544,6 +559,8 @@ struct sg_engine {
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
     bool pq_on = true;          // PF_PQ segments to k_pq (SG_PQ=0: the per-lane kernel, as before round 3)
     uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
+    bool mix_on = true;         // XF_MIX programs (SG_MIX=0: every param + flow / degrade resource one lane)
+    bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -595,8 +612,9 @@ static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
     dfree(B.d_prev); dfree(B.d_bsmall);
     dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans); dfree(B.d_ext); dfree(B.d_args);
-    dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti); dfree(B.d_along);
-    B.ext_cap = B.args_cap = B.aux_cap_n = 0;
+    dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti); dfree(B.d_along); dfree(B.d_mix);
+    B.d_mix = nullptr;
+    B.ext_cap = B.args_cap = B.aux_cap_n = B.mix_cap = 0;
     B.d_link = nullptr; B.d_bst = B.d_pend = nullptr; B.d_spans = nullptr;
     B.d_ev = nullptr; B.d_out = nullptr; B.d_k0 = B.d_v0 = B.d_k1 = B.d_v1 = nullptr;
     B.d_hist = B.d_part = B.d_flag = B.d_pos = B.d_order = nullptr;
@@ -672,13 +690,15 @@ static int collect(sg_engine* e, int k) {
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
+    if (bflags & BF_POOL_FULL)  // a map that could not grow may have lost a key (a ghost entry, as below)
+        e->fatal = "the hot-parameter map pool is used up (raise param_table_log2)";
     // A map that could not place a key has already committed its ring bit and live count (a ghost entry), and a
     // failed k_pq invariant leaves its maps in an unknown state: the engine refuses every later batch.
     if (bflags & BF_PQ_INVARIANT)
         e->fatal = "internal error: a k_pq tile's presorted key subset did not match its accesses";
     else if (bflags & BF_PTAB_FULL)
         e->fatal = "a hot-parameter map table could not place a key (its map holds a ghost entry)";
-    if (bflags & (BF_PQ_INVARIANT | BF_PTAB_FULL)) return fail(SG_ECAPACITY, e->fatal + " -- engine unusable");
+    if (bflags & (BF_PQ_INVARIANT | BF_PTAB_FULL | BF_POOL_FULL)) return fail(SG_ECAPACITY, e->fatal + " -- engine unusable");
     return SG_OK;
 }
 // every batch in flight done (called by the API functions that read or write engine state)
@@ -716,6 +736,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
         HIPCHK(hipMemcpy(old_prog.data(), e->d_prog, R * sizeof(Prog), hipMemcpyDeviceToHost));
     }
     size_t nres = e->names.size();
+    bool any_mix = false;
     std::vector<std::pair<uint32_t, uint32_t>> relate;  // (resource, referenced resource) of RELATE rules
     for (size_t r = 0; r < nres && r < R; ++r) {
         Prog p;
@@ -858,7 +879,26 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (b == SG_CONTROL_BEHAVIOR_RATE_LIMITER || b == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER) ++n_rl;
             }
             if (n_rl) p.pflags |= PF_RL;
-            if (p.n_param || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2 || p.multi) p.pflags |= PF_SERIAL;
+            // param rules beside flow / degrade rules (XF_MIX): QPS DefaultController-style token buckets on
+            // paramIdx 0 with LDS-sized maps only -- their verdicts are then a function of earlier checks of the
+            // same (rule, value) alone (no THREAD grade: its count moves with full-chain passes; no throttle:
+            // its wait would add to the flow stages')
+            bool mix = p.n_param >= 1 && p.n_param <= 4 && (p.n_flow + p.n_degrade) > 0 && !p.multi;
+            for (int i = 0; i < p.n_param && mix; ++i) {
+                const DRule& d = rules[p.rule_off + i];
+                if (d.param_idx < 0) mix = false;
+                else if (d.behavior == PB_INIT_ONLY) { if (d.burst & ~1) mix = false; }
+                else if (d.param_idx != 0 || d.grade != SG_FLOW_GRADE_QPS ||
+                         d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || rule_map_cap(d.duration_sec) > 4080)
+                    mix = false;
+            }
+            if (mix) {  // a thread-count map of another index is k_lane's
+                auto it = e->tmaps.lower_bound(((uint64_t)r << 8) | 1);
+                if (it != e->tmaps.end() && (*it >> 8) == (uint64_t)r) mix = false;
+            }
+            if (mix && e->mix_on) { p.xf |= XF_MIX; any_mix = true; }
+            if ((p.n_param && !(p.xf & XF_MIX)) || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2 || p.multi)
+                p.pflags |= PF_SERIAL;
             bool all_default_qps = true;
             for (int i = 0; i < p.n_flow; ++i) {
                 const DRule& d = rules[p.rule_off + p.n_param + i];
@@ -931,6 +971,36 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             if (ni[k].flags & NI_CHAIN) ni[k].flags |= NI_TOUCHED;
             HIPCHK(hipMemcpy(e->d_info + members[k], &ni[k], sizeof(NodeInfo), hipMemcpyHostToDevice));
         }
+        // their param maps at full size: a member's events sort under the representative, so the per-segment
+        // growth (k_pm_grow) never sees them
+        if (e->d_pmap) {
+            const std::set<uint32_t> ms(members.begin(), members.end());
+            std::vector<uint32_t> ids;
+            for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i)
+                if ((e->pmap_key[i] & TMAP_KEY) && ms.count((uint32_t)(e->pmap_key[i] >> 8))) ids.push_back(i);
+            for (const auto& kv : e->psid_of) {
+                auto it = e->ids.find(kv.first.substr(0, kv.first.find('\0')));
+                auto pi = e->pmap_index.find(kv.second);
+                if (it != e->ids.end() && ms.count(it->second) && pi != e->pmap_index.end()) ids.push_back(pi->second);
+            }
+            if (!ids.empty()) {
+                uint32_t* d_ids = nullptr;
+                HIPCHK(hipMalloc(&d_ids, ids.size() * 4));
+                HIPCHK(hipMemcpy(d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+                DevState Sg{};
+                std::memset(&Sg, 0, sizeof(Sg));
+                Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
+                HIPCHK(hipMemset(e->d_small, 0, 4));
+                HIPCHK(launch_pm_grow_ids(d_ids, (uint32_t)ids.size(), Sg, e->d_pool_next, e->pool_nb, e->d_small, e->stream));
+                uint32_t fl = 0;
+                HIPCHK(hipMemcpyAsync(&fl, e->d_small, 4, hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                (void)hipFree(d_ids);
+                if (fl & (BF_POOL_FULL | BF_PTAB_FULL))
+                    return fail(SG_ECAPACITY, "hot-parameter map pool too small for the maps of STRATEGY_RELATE members "
+                                              "(raise param_table_log2)");
+            }
+        }
     }
     if (rules.size() > e->cfg.max_rules) return fail(SG_ECAPACITY, "compiled rule table exceeds max_rules");
     if (rules.size() > e->rules_cap) {
@@ -952,6 +1022,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
     if (!hot.empty()) HIPCHK(hipMemcpy(e->d_hot, hot.data(), hot.size() * sizeof(DHot), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->d_prog, prog.data(), R * sizeof(Prog), hipMemcpyHostToDevice));
     e->n_dev_rules = (uint32_t)rules.size();
+    e->has_mix = any_mix;
     if (comp.empty()) {
         dfree(e->d_comp);
         e->d_comp = nullptr;
@@ -1081,6 +1152,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
+    if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
     if (const char* v = std::getenv("SG_PQ_WIDE")) e->pq_wide = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_SKIP_MIN")) {
         e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
@@ -1150,6 +1222,14 @@ extern "C" int sgx_read_aux_node(sg_engine* e, uint32_t res, uint32_t kind, uint
     }
     return 0;
 }
+// diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last layout, compactions}
+extern "C" int sgx_param_pool(sg_engine* e, unsigned long long* out) {
+    if (!e || !out || drain(e) != SG_OK) return -1;
+    unsigned long long next = 0;
+    if (e->d_pool_next && hipMemcpy(&next, e->d_pool_next, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    out[0] = e->pool_nb; out[1] = next; out[2] = e->pool_floor; out[3] = e->n_compact;
+    return 0;
+}
 
 int sg_engine_destroy(sg_engine* e) {
     if (!e) return SG_OK;
@@ -1158,6 +1238,8 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
     dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
+    dfree(e->d_pool_next);
+    if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
@@ -1519,34 +1601,40 @@ static int rebuild_cluster_param(sg_engine* e, const sg_param_rule* rules, const
 }
 
 // ---- ParameterMetric maps (dev_types.h PMap)
-#define TMAP_KEY (1ull << 63)
 // A map's cuckoo table: two-choice buckets of PM_BKT slots at <= 50 % load; its live-stamp ring: >= 4 x cap bits
-static uint32_t map_buckets(uint32_t cap) { return std::max<uint32_t>(2u, (2u * cap + PM_BKT - 1) / PM_BKT); }
-static uint32_t region_slots(uint32_t cap) { return map_buckets(cap) * PM_BKT; }
 static uint32_t ring_log2(uint32_t cap) {
     uint32_t k = 10;
     while ((1ull << k) < 4ull * cap + 64) ++k;
     return k;
 }
 
-// Lay out one region per map in fresh pools, carrying the entries, stamps, rings and counters of the maps that
-// stay.  Everything that can fail (the capacity check, the allocations) happens before the engine changes: an
-// SG_ECAPACITY leaves the old maps in place.
+// Lay out one region per map in a fresh pool, carrying the entries, stamps, rings and counters of the maps that
+// stay (each at its current size; a new map starts at PM_MIN_NB buckets and grows per batch, k_pm_grow).  The pool
+// holds 2^param_table_log2 slots, or less when that is more than the maps could ever take (twice their full
+// regions: they grow by doubling).  Everything that can fail (the capacity check, the allocations) happens before
+// the engine changes: an SG_ECAPACITY leaves the old maps in place.  Called with the current maps it compacts the
+// pool (the regions the maps grew out of are dropped).
 static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap, const std::set<uint64_t>& tmaps) {
+    std::vector<PMap> old(e->pmap_key.size());
+    if (!old.empty()) HIPCHK(hipMemcpy(old.data(), e->d_pmap, old.size() * sizeof(PMap), hipMemcpyDeviceToHost));
+    std::unordered_map<uint64_t, uint32_t> was;
+    for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i) was[e->pmap_key[i]] = i;
     std::vector<uint64_t> keys;
     std::vector<PMap> hdr;
-    uint64_t nbkt = 0, nword = 0;
+    uint64_t nbkt = 0, nword = 0, nfull = 0;
     auto add = [&](uint64_t key, uint32_t cap) {
         PMap m;
         std::memset(&m, 0, sizeof(m));
         m.base = nbkt;
-        m.nb = map_buckets(cap);
+        auto it = was.find(key);
+        m.nb = it == was.end() ? PM_MIN_NB : old[it->second].nb;
         m.cap = cap;
         m.rb_log2 = ring_log2(cap);
         m.bm = nword;
         keys.push_back(key);
         hdr.push_back(m);
         nbkt += m.nb;
+        nfull += 2ull * map_buckets(cap);
         nword += (1ull << m.rb_log2) / 64;
     };
     for (const auto& kv : rcap) add(kv.first, kv.second);
@@ -1556,16 +1644,13 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
         return fail(SG_ECAPACITY, "hot-parameter maps need " + std::to_string(total) + " slots, param_table_log2 = " +
                                       std::to_string(e->cfg.param_table_log2) + " allows " +
                                       std::to_string(1ull << e->cfg.param_table_log2));
-    std::vector<PMap> old(e->pmap_key.size());
-    if (!old.empty()) HIPCHK(hipMemcpy(old.data(), e->d_pmap, old.size() * sizeof(PMap), hipMemcpyDeviceToHost));
-    std::unordered_map<uint64_t, uint32_t> was;
-    for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i) was[e->pmap_key[i]] = i;
+    const uint64_t pool_nb = keys.empty() ? 0 : std::max<uint64_t>(nbkt, std::min<uint64_t>((1ull << e->cfg.param_table_log2) / PM_BKT, nfull + nbkt));
     std::vector<uint64_t> tri_b, tri_d, tri_w;  // {source word, destination word, words} per pool
     for (size_t i = 0; i < keys.size(); ++i) {
         auto it = was.find(keys[i]);
         if (it == was.end()) continue;
         const PMap& o = old[it->second];
-        if (o.nb != hdr[i].nb || o.rb_log2 != hdr[i].rb_log2) continue;  // cannot happen: fixed by the map's identity
+        if (o.rb_log2 != hdr[i].rb_log2) continue;  // cannot happen: fixed by the map's identity
         hdr[i].clock = o.clock;
         hdr[i].thr = o.thr;
         hdr[i].live = o.live;
@@ -1591,18 +1676,22 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     uint64_t* dtri = nullptr;
     auto release = [&]() { dfree(nbk); dfree(ndt); dfree(nbm); dfree(npr); dfree(nh); dfree(nt); dfree(dtri); };
     const size_t ntri = std::max(tri_b.size(), std::max(tri_d.size(), tri_w.size()));
-    if ((nbkt && (hipMalloc(&nbk, nbkt * sizeof(PBucket)) != hipSuccess ||
-                  hipMalloc(&ndt, total * sizeof(PData)) != hipSuccess ||
+    if ((nbkt && (hipMalloc(&nbk, pool_nb * sizeof(PBucket)) != hipSuccess ||
+                  hipMalloc(&ndt, pool_nb * PM_BKT * sizeof(PData)) != hipSuccess ||
                   hipMalloc(&nbm, nword * 8) != hipSuccess || hipMalloc(&npr, nword * 4) != hipSuccess)) ||
         (!hdr.empty() && hipMalloc(&nh, hdr.size() * sizeof(PMap)) != hipSuccess) ||
         (!tmid.empty() && hipMalloc(&nt, tmid.size() * 4) != hipSuccess) ||
         (ntri && hipMalloc(&dtri, 3 * ntri * 8) != hipSuccess)) {
         release();
         (void)hipGetLastError();
-        return fail(SG_ECAPACITY, "device memory for " + std::to_string(total) + " hot-parameter map slots");
+        return fail(SG_ECAPACITY, "device memory for " + std::to_string(pool_nb * PM_BKT) + " hot-parameter map slots");
+    }
+    if (!e->d_pool_next) {
+        HIPCHK(hipMalloc(&e->d_pool_next, 8));
+        HIPCHK(hipHostMalloc(&e->h_pool_next, 8));
     }
     if (nbkt) {
-        HIPCHK(hipMemsetAsync(nbk, 0xFF, nbkt * sizeof(PBucket), e->stream));  // PK_EMPTY keys
+        HIPCHK(hipMemsetAsync(nbk, 0xFF, pool_nb * sizeof(PBucket), e->stream));  // PK_EMPTY keys (regions grow into it)
         HIPCHK(hipMemsetAsync(ndt, 0, total * sizeof(PData), e->stream));
         HIPCHK(hipMemsetAsync(nbm, 0, nword * 8, e->stream));
     }
@@ -1629,6 +1718,13 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     e->d_pmap = nh;
     e->d_tmid = nt;
     e->n_pslot = total;
+    e->pool_nb = pool_nb;
+    e->pool_floor = nbkt;
+    {
+        const unsigned long long next = nbkt;
+        HIPCHK(hipMemcpy(e->d_pool_next, &next, 8, hipMemcpyHostToDevice));
+        *e->h_pool_next = next;
+    }
     e->pmap_key = keys;
     e->pmap_index.clear();
     for (uint32_t i = 0; i < (uint32_t)keys.size(); ++i)
@@ -1713,9 +1809,7 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
                 if (idx < 0 || idx == k) tmaps.insert(((uint64_t)r << 8) | (uint64_t)k);
         }
     // the capacity check first: with SG_ECAPACITY neither the cluster rules nor the maps change
-    uint64_t need = 0;
-    for (const auto& kv : rcap) need += region_slots(kv.second);
-    need += tmaps.size() * (uint64_t)region_slots(PM_BASE_CAP);
+    uint64_t need = (rcap.size() + tmaps.size()) * (uint64_t)PM_MIN_NB * PM_BKT;  // (new maps' first regions)
     if (need > (1ull << e->cfg.param_table_log2))
         return fail(SG_ECAPACITY, "hot-parameter maps need " + std::to_string(need) + " slots, param_table_log2 = " +
                                       std::to_string(e->cfg.param_table_log2) + " allows " +
@@ -1747,6 +1841,16 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
         HIPCHK(hipMemset(e->d_keyring, 0xFF, nk * sizeof(uint64_t)));  // NO_KEY
     }
     if (n_loaded) *n_loaded = (uint32_t)e->params.size();
+    return SG_OK;
+}
+
+// The XF_MIX segment lists of slot B for up to mb segments (narrow, then wide at mix_cap)
+static int ensure_mix(sg_engine::BatchSlot& B, uint64_t mb) {
+    if (mb > B.mix_cap) {
+        dfree(B.d_mix);
+        B.mix_cap = std::max<uint64_t>(mb, 1u << 12);
+        HIPCHK(hipMalloc(&B.d_mix, B.mix_cap * 2 * 4));
+    }
     return SG_OK;
 }
 
@@ -1800,6 +1904,13 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const int k = e->cur;
     rc = collect(e, k);  // the batch that last used this slot (two batches ago) is decided
     if (rc) return rc;
+    // the param map pool: the regions maps grew out of are dropped by a relayout once the growth since the last
+    // layout took half of what was free (the count is a batch or two old)
+    if (e->pool_nb && *e->h_pool_next > e->pool_floor + (e->pool_nb - e->pool_floor) / 2) {
+        if (int drc = drain(e)) return drc;
+        if (int crc = rebuild_pmaps(e, e->rmap_cap, e->tmaps)) return crc;
+        ++e->n_compact;
+    }
     activate(e, k);
     auto& B = e->slot[k];
     hipStream_t gs = e->gstream, st = e->stream;
@@ -1887,12 +1998,16 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (ext) {  // the aux.hip post-pass lists of this slot
         if (int arc = ensure_aux(e, B, n)) return arc;
     }
+    if (e->has_mix) {  // the XF_MIX lists of this slot
+        if (int mrc = ensure_mix(B, mb)) return mrc;
+    }
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
-                          B.d_ashort, B.d_along, B.d_amulti, gs));
+                          B.d_ashort, B.d_along, B.d_amulti, e->d_bsmall + 6, e->has_mix ? B.d_mix : nullptr,
+                          (uint32_t)B.mix_cap, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
-    uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [8..] bin offsets
+    uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..] bin offsets
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
     HIPCHK(hipEventRecord(B.ev[1], gs));
     HIPCHK(hipStreamSynchronize(gs));
@@ -1914,6 +2029,16 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // ---- decide stage, in order after the previous batch's: references into earlier batches first
     HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
     HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
+    // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
+    // compaction check of a later submit
+    if (e->pool_nb) {
+        DevState Sg{};
+        std::memset(&Sg, 0, sizeof(Sg));
+        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid;
+        Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
+        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, st));
+        HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
+    }
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
@@ -1992,6 +2117,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.aux_cap = e->cfg.aux_node_capacity;
     S.aux_mask = e->aux_mask;
     S.max_ctx = SG_MAX_CONTEXTS;
+    // XF_MIX segments of the cooperative bins: their param checks first (k_pq pre pass), the owners then decide
+    // the flow / degrade chain on them
+    const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
+    if (n_mix || n_mixw)
+        HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
+                             e->d_dec, e->d_bsmall + 0, st));
     HIPCHK(hipEventRecord(e->fork, st));
     // J16 and J4 on their own streams; J1 after the lane bins on the main stream (J4 + J1 in series was the
     // longest chain of the decide stage)
@@ -2059,6 +2190,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
+    // XF_MIX: the thread-count maps and ParameterMetric bits from the final verdicts (k_pq post pass)
+    if (n_mix || n_mixw)
+        HIPCHK(launch_pq_mix(1, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
+                             e->d_dec, e->d_bsmall + 0, st));
     // origin / context nodes of the segments decided off k_lane<16>, from the committed verdicts (aux.hip)
     if (ext)
         HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_along, B.d_apiece, B.d_amulti, S, dc,

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
         r.cnt = e.count;
         r.rt = 0;
         r.kind = e.kind;
-        r.flags = e.flags;
+        r.flags = (uint8_t)(e.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
         r.code = RC_NONE;
         r.pad = 0;
         uint32_t mark = 0;  // PM_* marks for the resource

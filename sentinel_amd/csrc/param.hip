@@ -994,8 +994,16 @@ __device__ __noinline__ void pq_fold(PqSh<NW>& sh, const Ctx& C, int64_t t0, uin
     }
 }
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+// MODE (XF_MIX segments, whose flow / degrade chain a k_jac owner decides between the two passes):
+//   PQ_FULL  the resource's whole decision (PF_PQ);
+//   PQ_PRE   ParamFlowSlot's QPS checks only.  Nothing before ParamFlowSlot blocks, so they see every ENTRY whatever
+//            the later slots decide; a blocked ENTRY gets its final dec[] word and RF_PBLK, the
+//            passed ones are left to the owner.  No statistics, no thread-count map;
+//   PQ_POST  ParamFlowStatisticEntryCallback / ExitCallback from the final verdicts: the thread-count map of
+//            paramIdx 0 (passed ENTRYs add, EXITs of passed ENTRYs release) and the node's ParameterMetric bits.
+enum { PQ_FULL = 0, PQ_PRE = 1, PQ_POST = 2 };
+template <int NW, int MODE>
+__global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg_event* __restrict__ ev,
                                                 const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                                                 const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                                 int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
@@ -1023,25 +1031,27 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     const uint32_t tm = (pg.tm_base == NO_ID) ? NO_ID : S.tmid[pg.tm_base];
     if (tid <= PQ_MAXP) {
         uint32_t id = NO_ID;
-        if ((int)tid < np && sh.rules[tid].behavior != PB_INIT_ONLY && sh.rules[tid].grade == SG_FLOW_GRADE_QPS)
+        if (MODE != PQ_POST && (int)tid < np && sh.rules[tid].behavior != PB_INIT_ONLY &&
+            sh.rules[tid].grade == SG_FLOW_GRADE_QPS)
             id = sh.rules[tid].pmap;
-        if (tid == PQ_MAXP) id = tm;
+        if (tid == PQ_MAXP) id = MODE == PQ_PRE ? NO_ID : tm;
         sh.mid[tid] = id;
         if (id != NO_ID) sh.hdr[tid] = S.pmap[id];
     }
     __syncthreads();
+    const bool chain = (sh.node.flags & NI_CHAIN) != 0;  // the host routes switch_on == 0 to k_lane
+    if (!chain) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted, no map is touched
+        if (MODE == PQ_FULL)
+            for (uint32_t p = tid; p < sg.len; p += HW)
+                if (recs[sg.start + p].kind == SG_EV_ENTRY) dec[sg.start + p] = mk_dec(ST_NO_CHECK, 0, 0);
+        return;  // (XF_MIX: the owner writes them)
+    }
     for (int k = 0; k <= PQ_MAXP; ++k) {
         if (sh.mid[k] == NO_ID) continue;
         const uint32_t W = 1u << (sh.hdr[k].rb_log2 - 6);
         for (uint32_t w = tid; w < W; w += HW) sh.bm[k][w] = S.pbm[sh.hdr[k].bm + w];
     }
-    const bool chain = (sh.node.flags & NI_CHAIN) != 0;  // the host routes switch_on == 0 to k_lane
-    if (!chain) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted, no map is touched
-        for (uint32_t p = tid; p < sg.len; p += HW)
-            if (recs[sg.start + p].kind == SG_EV_ENTRY) dec[sg.start + p] = mk_dec(ST_NO_CHECK, 0, 0);
-        return;
-    }
-    if (tid == 0 && sg.len && (t0 + recs[sg.start].dt) < (sh.node.sb[0].ws > sh.node.sb[1].ws ? sh.node.sb[0].ws : sh.node.sb[1].ws))
+    if (MODE != PQ_POST && tid == 0 && sg.len && (t0 + recs[sg.start].dt) < (sh.node.sb[0].ws > sh.node.sb[1].ws ? sh.node.sb[0].ws : sh.node.sb[1].ws))
         atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
     // tm bit of paramIdx 0 for a passed ENTRY: it has visited every rule (ParamFlowSlot sets the bits of the
     // rules it checks: ni_tm(paramIdx), or an initialise-only run's map set)
@@ -1083,6 +1093,16 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
             // args[0]'s key: k_rs_first put it in the key ring (sg_submit's aux, or sg_submit_ex's table entry)
             if (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG))
                 sh.tkey[e] = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
+            if (MODE == PQ_POST && p < sg.len && r.kind == SG_EV_ENTRY) {  // the final verdict as the rule it stopped at
+                const uint32_t d = dec[sg.start + p];
+                if (!st_passed(d & 0xFFu)) {
+                    st[q] = (uint32_t)np + 1;  // a flow / degrade stage blocked it: every param rule was visited
+                    if ((d & 0xFFu) == ST_BLOCK_PARAM)
+                        for (int k = 0; k < np; ++k)
+                            if (sh.rules[k].behavior != PB_INIT_ONLY && sh.rules[k].slot == ((d >> 8) & 0xFFu))
+                                st[q] = (uint32_t)k + 1;
+                }
+            }
         }
         __syncthreads();
         // ---- 2. ParamFlowSlot: the rules in order
@@ -1092,6 +1112,21 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         PQ_MARK(0)
         for (int k = 0; k < np; ++k) {
             const DRule& r = sh.rules[k];
+            if (MODE == PQ_POST) {  // the visits only (the node's ParameterMetric bits, the first visit of rule k0)
+                bool reach = false;
+#pragma unroll
+                for (int q = 0; q < PQ_EPL; ++q) {
+                    const bool rq = (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY && (st[q] == 0 || st[q] > (uint32_t)k);
+                    reach |= rq;
+                    if (rq && k == k0 && tb + tid * PQ_EPL + q < sg.len) atomicMin(&sh.freach, tb + tid * PQ_EPL + q + 1);
+                }
+                if (reach) {
+                    const uint32_t bits = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
+                                          : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
+                    atomicOr(&sh.flags_or, bits | NI_PM);
+                }
+                continue;
+            }
             bool reach = false;
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
@@ -1146,7 +1181,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
         // (ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount of the ENTRY's argument, OP_SUB)
         __syncthreads();  // every lane's atomicMin on freach is in
         if (tm_from == 0xFFFFFFFFu) tm_from = sh.freach;  // uniform (LDS)
-        if (tm_on) {
+        if (MODE != PQ_PRE && tm_on) {
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) sh.tdec[tid * PQ_EPL + q] = st[q];
             __syncthreads();
@@ -1198,7 +1233,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
                     if (pq_op(sh.tkx[tid * PQ_EPL + q]) == OP_CHK && (sh.tver[tid * PQ_EPL + q] & TV_BLOCK)) st[q] = (uint32_t)tk + 1;
             }
             __syncthreads();
-        } else if (tk >= 0) {  // no thread-count map: every count reads 0
+        } else if (MODE == PQ_FULL && tk >= 0) {  // no thread-count map: every count reads 0
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
                 const uint32_t e = tid * PQ_EPL + q, kx = sh.tkx[e];
@@ -1208,20 +1243,31 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
             }
         }
         // ---- 4. decisions
+        if (MODE == PQ_PRE) {  // the param-blocked ENTRYs: final words, marked for the owner
 #pragma unroll
-        for (int q = 0; q < PQ_EPL; ++q) {
-            const uint32_t e = tid * PQ_EPL + q, p = tb + e;
-            uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
-            if ((sh.tkx[e] & 0xFFu) == SG_EV_ENTRY) {
-                d = st[q] == 0 ? mk_dec(ST_PASS, 0, wt[q]) : mk_dec(ST_BLOCK_PARAM, sh.rules[st[q] - 1].slot, 0);
-                if (p < sg.len) dec[sg.start + p] = d;
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t p = tb + tid * PQ_EPL + q;
+                if (p < sg.len && st[q] != 0 && (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY) {
+                    dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, sh.rules[st[q] - 1].slot, 0);
+                    recs[sg.start + p].flags = (uint8_t)(((sh.tkx[tid * PQ_EPL + q] >> 8) & 0xFFu) | RF_PBLK);
+                }
             }
-            sh.tdec[e] = d;
+        } else if (MODE == PQ_FULL) {
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t e = tid * PQ_EPL + q, p = tb + e;
+                uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                if ((sh.tkx[e] & 0xFFu) == SG_EV_ENTRY) {
+                    d = st[q] == 0 ? mk_dec(ST_PASS, 0, wt[q]) : mk_dec(ST_BLOCK_PARAM, sh.rules[st[q] - 1].slot, 0);
+                    if (p < sg.len) dec[sg.start + p] = d;
+                }
+                sh.tdec[e] = d;
+            }
+            __syncthreads();
+            // ---- 5. StatisticSlot: one bucket update per 500 ms bucket of the tile
+            PQ_MARK(11)
+            pq_fold<NW>(sh, C, t0, tb, sg.start, sg.len, dec, bflags);
         }
-        __syncthreads();
-        // ---- 5. StatisticSlot: one bucket update per 500 ms bucket of the tile
-        PQ_MARK(11)
-        pq_fold<NW>(sh, C, t0, tb, sg.start, sg.len, dec, bflags);
         __syncthreads();  // full fence: this tile's dec[] words are visible to the next tiles' EXIT lookups
         PQ_MARK(12)
     }
@@ -1234,12 +1280,13 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     }
 #endif
     // ---- segment end: node, map headers and rings back to HBM
-    if (tid == 0) {
+    if (MODE == PQ_FULL && tid == 0) {
         Node& N = sh.node;
         N.flags |= sh.flags_or;
         min_flush(N, C.minb);
         node_store(N, S, res, pg.pflags);
     }
+    if (MODE == PQ_POST && tid == 0 && sh.flags_or) atomicOr(&S.info[res].flags, sh.flags_or);  // (the owner wrote the node)
     for (int k = 0; k <= PQ_MAXP; ++k) {
         if (sh.mid[k] == NO_ID) continue;
         const uint32_t W = 1u << (sh.hdr[k].rb_log2 - 6);
@@ -1248,17 +1295,137 @@ __global__ __launch_bounds__(NW * 64) void k_pq(const SEv* __restrict__ recs, co
     }
 }
 
+// ---- elastic map regions (dev_types.h PM_MIN_NB)
+// Move map id to a region of nn buckets at nbase (fresh pool buckets: every key PK_EMPTY): its live keys, with their
+// stamps and values, by two-choice cuckoo placement (every key of the new table is live: a slot is free iff empty).
+__device__ void pm_move(const DevState& S, uint32_t id, PMap m, uint64_t nbase, uint32_t nn, uint32_t* bflags) {
+    const PBucket* OB = S.pbkt + m.base;
+    const PData* OD = S.pdat + m.base * PM_BKT;
+    PBucket* NB = S.pbkt + nbase;
+    PData* ND = S.pdat + nbase * PM_BKT;
+    const uint64_t* bm = S.pbm + m.bm;
+    for (uint32_t b = 0; b < m.nb; ++b) {
+        for (int j = 0; j < PM_BKT; ++j) {
+            uint64_t ck = OB[b].key[j];
+            int64_t cs = OB[b].stamp[j];
+            if (ck == PK_EMPTY || !pm_live(m, bm, cs)) continue;
+            PData cd = OD[b * PM_BKT + j];
+            uint32_t b1, b2;
+            pm_buckets(nn, ck, b1, b2);
+            uint32_t c = b1;
+            bool placed = false;
+            for (int step = 0; step < 512 && !placed; ++step) {
+                for (int q = 0; q < PM_BKT; ++q) {  // a free slot in either candidate (the first step) or in c
+                    if (NB[c].key[q] == PK_EMPTY) { NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd; placed = true; break; }
+                }
+                if (placed) break;
+                if (step == 0) {
+                    for (int q = 0; q < PM_BKT; ++q) {
+                        if (NB[b2].key[q] == PK_EMPTY) { NB[b2].key[q] = ck; NB[b2].stamp[q] = cs; ND[b2 * PM_BKT + q] = cd; placed = true; break; }
+                    }
+                    if (placed) break;
+                }
+                const int q = (int)((cs + step * 5) & 7);  // displace one key of c to its other bucket
+                const uint64_t nk = NB[c].key[q];
+                const int64_t ns = NB[c].stamp[q];
+                const PData nd = ND[c * PM_BKT + q];
+                NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd;
+                ck = nk; cs = ns; cd = nd;
+                c = pm_alt(nn, ck, c);
+            }
+            if (!placed) atomicOr(bflags, BF_PTAB_FULL);  // (cannot happen at <= 50 % load)
+        }
+    }
+    PMap* h = &S.pmap[id];
+    h->base = nbase;
+    h->nb = nn;
+}
+// the map before up to `adds` more keys arrive: at most half its slots used, else a region twice as large (or
+// large enough), up to map_buckets(cap)
+__device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned long long* pool_next, uint64_t pool_nb,
+                        uint32_t* bflags) {
+    const PMap m = S.pmap[id];
+    uint64_t need = (uint64_t)m.live + adds;
+    if (need > m.cap) need = m.cap;
+    const uint32_t want = map_buckets((uint32_t)need), full = map_buckets(m.cap);
+    if (want <= m.nb) return;
+    uint32_t nn = want > 2 * m.nb ? want : 2 * m.nb;
+    if (nn > full) nn = full;
+    const uint64_t nbase = atomicAdd(pool_next, (unsigned long long)nn);
+    if (nbase + nn > pool_nb) { atomicOr(bflags, BF_POOL_FULL); return; }
+    pm_move(S, id, m, nbase, nn, bflags);
+}
+// Decide stage, before every kernel that touches the maps: the maps a segment may add keys to -- its QPS rules'
+// maps and its thread-count maps -- grown for the segment's events (an upper bound of its accesses); one lane each.
+// (Maps of STRATEGY_RELATE members, whose events sort under another resource, are grown to capacity at rule load.)
+__global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, const uint32_t* __restrict__ mp, DevState S,
+                                                 unsigned long long* pool_next, uint64_t pool_nb, uint32_t* bflags) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *mp) return;
+    const Seg sg = segs[s];
+    const Prog pg = S.prog[sg.res];
+    if (pg.tm_base == NO_ID && pg.n_param == 0) return;
+    for (int k = 0; k < pg.n_param; ++k) {
+        const DRule& r = S.rules[pg.rule_off + k];
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, sg.len, pool_next, pool_nb, bflags);
+    }
+    if (pg.tm_base != NO_ID)
+        for (int i = 0; i < SG_MAX_ARGS; ++i) {
+            const uint32_t id = S.tmid[pg.tm_base + i];
+            if (id != NO_ID) pm_grow(S, id, sg.len, pool_next, pool_nb, bflags);
+        }
+}
+// listed maps to full size (rule load: STRATEGY_RELATE members)
+__global__ void k_pm_grow_ids(const uint32_t* __restrict__ ids, uint32_t n, DevState S, unsigned long long* pool_next,
+                              uint64_t pool_nb, uint32_t* bflags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) pm_grow(S, ids[i], 0xFFFFFFFFull, pool_next, pool_nb, bflags);
+}
+
 namespace sg {
+hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
+                          uint64_t pool_nb, uint32_t* bflags, hipStream_t st) {
+    if (!mb) return hipSuccess;
+    hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags);
+    return hipGetLastError();
+}
+hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
+                              uint64_t pool_nb, uint32_t* bflags, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pm_grow_ids, dim3((n + 255) / 256), dim3(256), 0, st, ids, n, S, pool_next, pool_nb, bflags);
+    return hipGetLastError();
+}
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
                      uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
     // the wide owner: 1024 lanes (128 VGPRs a lane: ~120 spilled) measured 15 % faster on C5 than 512 lanes with
     // 256 VGPRs and no spill (SG_DEBUG_FLAGS 128 selects that form, for A/B runs)
+    SEv* r = const_cast<SEv*>(recs);  // (PQ_FULL reads the records only)
     if (wide && (cfg.dbg_flags & 128))
-        hipLaunchKernelGGL(k_pq<8>, dim3(m), dim3(512), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
-    else if (wide) hipLaunchKernelGGL(k_pq<16>, dim3(m), dim3(1024), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
-    else hipLaunchKernelGGL(k_pq<4>, dim3(m), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+        hipLaunchKernelGGL((k_pq<8, PQ_FULL>), dim3(m), dim3(512), 0, st, r, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    else if (wide)
+        hipLaunchKernelGGL((k_pq<16, PQ_FULL>), dim3(m), dim3(1024), 0, st, r, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    else hipLaunchKernelGGL((k_pq<4, PQ_FULL>), dim3(m), dim3(256), 0, st, r, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
+    return hipGetLastError();
+}
+// XF_MIX segments: the pre pass (post = 0) before the cooperative owners, the post pass (post = 1) after them and
+// k_fill; list = the narrow segments (k_pq<4>), list + wide_off the wide ones (k_pq<16>)
+hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
+                         const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
+                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
+    if (n_wide) {
+        if (post) hipLaunchKernelGGL((k_pq<16, PQ_POST>), dim3(n_wide), dim3(1024), 0, st, recs, ev, vals, segs,
+                                     list + wide_off, n_wide, S, cfg, t0, dec, bflags);
+        else hipLaunchKernelGGL((k_pq<16, PQ_PRE>), dim3(n_wide), dim3(1024), 0, st, recs, ev, vals, segs, list + wide_off,
+                                n_wide, S, cfg, t0, dec, bflags);
+    }
+    if (n_narrow) {
+        if (post) hipLaunchKernelGGL((k_pq<4, PQ_POST>), dim3(n_narrow), dim3(256), 0, st, recs, ev, vals, segs, list,
+                                     n_narrow, S, cfg, t0, dec, bflags);
+        else hipLaunchKernelGGL((k_pq<4, PQ_PRE>), dim3(n_narrow), dim3(256), 0, st, recs, ev, vals, segs, list, n_narrow,
+                                S, cfg, t0, dec, bflags);
+    }
     return hipGetLastError();
 }
 } // namespace sg

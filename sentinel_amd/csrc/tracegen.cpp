@@ -1,4 +1,5 @@
-// tracegen.cpp -- seeded synthetic Sentinel workloads.
+// tracegen.cpp -- seeded synthetic Sentinel workloads (north_star's
+// >= 1M resources with mixed flow / degrade / param rules).
 //
 // Host-only C++ (no GPU).  Produces the resource names, the rules of each
 // config and a time-ordered sg_event trace; bench.py and the tests hand the
@@ -204,7 +205,7 @@ void gen_c1(Workload& w, uint64_t seed, int seconds) {
     finalize(w, raw);
 }
 
-// C2-C5: Zipf(1.1) resources, Poisson arrivals at `rate` entries/s.
+// C2-C6: Zipf(1.1) resources, Poisson arrivals at `rate` entries/s.
 void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n_entries, double rate,
               uint64_t n_param_values, uint32_t variant) {
     Rng rng(seed);
@@ -254,6 +255,32 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
             default: d.grade = SG_DEGRADE_GRADE_EXCEPTION_COUNT; d.count = 20; break;
             }
             w.degrade.push_back(d);
+        } else if (config == 6) {  // C4's flow + degrade rules and a C5-style QPS param rule on args[0]
+            w.flow.push_back(flow_default(nm, log_uniform(rng, 10, 1e4)));
+            sg_degrade_rule d;
+            std::memset(&d, 0, sizeof(d));
+            d.resource = nm;
+            d.limit_app = "default";
+            d.time_window = 10;
+            switch (i % 3) {
+            case 0: d.grade = SG_DEGRADE_GRADE_RT; d.count = 50; break;
+            case 1: d.grade = SG_DEGRADE_GRADE_EXCEPTION_RATIO; d.count = 0.2; break;
+            default: d.grade = SG_DEGRADE_GRADE_EXCEPTION_COUNT; d.count = 20; break;
+            }
+            w.degrade.push_back(d);
+            sg_param_rule p;
+            std::memset(&p, 0, sizeof(p));
+            p.resource = nm;
+            p.limit_app = "default";
+            p.count = (double)(5 + rng.below(46));
+            p.duration_in_sec = 1;
+            p.grade = SG_FLOW_GRADE_QPS;
+            p.param_idx = 0;
+            p.has_param_idx = 1;
+            p.burst_count = (int32_t)rng.below(6);
+            p.cluster_sample_count = 10;
+            p.cluster_window_interval_ms = 1000;
+            w.param.push_back(p);
         } else if (config == 5) {
             sg_param_rule p;
             std::memset(&p, 0, sizeof(p));
@@ -288,7 +315,7 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
     for (uint32_t i = n_res; i > 1; --i) std::swap(perm[i - 1], perm[rng.below(i)]);
     Alias pa;
     std::vector<uint64_t> pkey;
-    if (config == 5) {
+    if (config == 5 || config == 6) {
         pa.build(n_param_values, 1.1);
         pkey.resize(n_param_values);
         Rng kr(seed ^ 0x5eed5eedULL);
@@ -321,7 +348,7 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
     const uint8_t exit_flags = (config == 5 && (variant & TG_V_THREAD)) ? SG_F_EXIT_ARGS : 0;
 
     std::vector<Raw> raw;
-    raw.reserve(n_entries * (config == 4 ? 21 : 20) / 10);
+    raw.reserve(n_entries * (config == 4 || config == 6 ? 21 : 20) / 10);
     double t_us = 0;
     const double mean_gap_us = 1e6 / rate;
     for (uint64_t i = 0; i < n_entries; ++i) {
@@ -329,14 +356,14 @@ void gen_zipf(Workload& w, int config, uint64_t seed, uint32_t n_res, uint64_t n
         uint64_t ms = (uint64_t)(t_us / 1000.0);
         uint32_t res = perm[za.sample(rng)];
         Raw e{ms * 4 + 0, i, res, 1, SG_EV_ENTRY, 0, 0};
-        if (config == 5) {
+        if (config == 5 || config == 6) {
             e.flags = SG_F_HAS_ARG;
             e.aux = pkey[(variant & TG_V_UNIFORM) && rng.uniform() < 0.5 ? rng.below(n_param_values) : pa.sample(rng)];
         }
         raw.push_back(e);
         int64_t rt = exp_rt(rng);
         uint64_t xms = ms + (uint64_t)rt;
-        if (config == 4 && rng.uniform() < 0.05) raw.push_back(Raw{xms * 4 + 1, i, res, 1, SG_EV_TRACE, 0, 0});
+        if ((config == 4 || config == 6) && rng.uniform() < 0.05) raw.push_back(Raw{xms * 4 + 1, i, res, 1, SG_EV_TRACE, 0, 0});
         raw.push_back(Raw{xms * 4 + 2, i, res, 1, SG_EV_EXIT, exit_flags, (uint64_t)rt});
     }
     w.n_entries = n_entries;
@@ -350,7 +377,7 @@ extern "C" {
 
 typedef struct tg_workload tg_workload;
 
-// config 1..5; n_res/n_entries/rate = 0 pick the SURVEY.md defaults.
+// config 1..6; n_res/n_entries/rate = 0 pick the SURVEY.md defaults.
 tg_workload* tg_create(int config, uint64_t seed, uint32_t n_res, uint64_t n_entries, double rate, int64_t t0,
                        uint64_t n_param_values, uint32_t variant) {
     Workload* w = new Workload();
@@ -359,7 +386,7 @@ tg_workload* tg_create(int config, uint64_t seed, uint32_t n_res, uint64_t n_ent
     if (config == 1) {
         gen_c1(*w, seed, n_entries ? (int)n_entries : 100);
     } else {
-        uint32_t dres = config == 2 ? 10000 : config == 3 ? 100000 : config == 4 ? 1000000 : 10000;
+        uint32_t dres = config == 2 ? 10000 : config == 3 ? 100000 : (config == 4 || config == 6) ? 1000000 : 10000;
         gen_zipf(*w, config, seed, n_res ? n_res : dres, n_entries ? n_entries : 100000000ULL,
                  rate > 0 ? rate : 1e6, n_param_values ? n_param_values : 10000000ULL, variant);
     }

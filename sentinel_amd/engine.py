@@ -232,6 +232,17 @@ class Engine:
             return None
         return {"second": out[:16].reshape(2, 8), "thread": int(out[16]), "mhist": out[17:21].reshape(2, 2)}
 
+    def param_pool(self) -> dict:
+        """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last layout,
+        compactions."""
+        fn = lib().sgx_param_pool
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_void_p]
+        out = np.zeros(4, dtype=np.uint64)
+        if fn(self.h, out.ctypes.data) != 0:
+            raise SentinelError(A.SG_EDEVICE, "sgx_param_pool failed")
+        return {"buckets": int(out[0]), "taken": int(out[1]), "floor": int(out[2]), "compactions": int(out[3])}
+
     def read_node(self, res: int, now: int = 0) -> dict:
         st = A.SgNodeState()
         _check(lib().sg_read_node(self.h, res, now, C.byref(st)))

@@ -1,4 +1,5 @@
-"""Seeded synthetic workloads, generated in C++.
+"""Seeded synthetic workloads (C6 = C4 plus a QPS param rule on every resource,
+north_star's mixed flow / degrade / param target), generated in C++.
 
 See sentinel_amd/csrc/tracegen.cpp for the trace model.
 """

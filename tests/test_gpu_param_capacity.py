@@ -1,6 +1,7 @@
 """The device's bounded ParameterMetric maps (dev_types.h PMap) against the oracle's (tests/test_param_capacity.py):
 LRU eviction at min(4000 * durationInSec, 200000) / 4000 values, the capacity check at rule load that leaves the
-engine unchanged (SG_ECAPACITY), and a C5 trace with more than five million distinct values through a pool sized
+engine unchanged (SG_ECAPACITY), regions that grow with their keys in a pool that is compacted between batches and
+whose exhaustion fails the engine, and a C5 trace with more than five million distinct values through a pool sized
 by param_table_log2 = 24."""
 import numpy as np
 import pytest
@@ -65,23 +66,62 @@ def test_capacity_follows_the_duration_on_the_device():
 
 
 def test_ecapacity_at_rule_load_leaves_the_engine_unchanged():
-    # 2^14 slots hold one resource's maps (a rule map + a thread-count map of 6016 slots each) but not two
-    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=14)
+    # 2^5 slots hold the first regions of one resource's maps (a rule map + a thread-count map, PM_MIN_NB = 2
+    # buckets of 8 each) but not two; batches of <= 8 events never grow a region
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=5)
     orc = O.Oracle(max_slot_chain_size=0)
     for n in ("a", "b"):
         assert eng.register(n) == orc.register(n)
     first = [A.param_rule("a", 0, 2)]
     assert eng.load_param_rules(first) == 1 and orc.load_param_rules(first) == 1
-    ev = _entries(0, [_long(v % 7) for v in range(50)])
+    ev = _entries(0, [_long(v % 3) for v in range(8)])
     np.testing.assert_array_equal(eng.submit(ev), orc.submit(ev))
     with pytest.raises(E.SentinelError) as ei:
         eng.load_param_rules(first + [A.param_rule("b", 0, 1)])
     assert ei.value.code == A.SG_ECAPACITY and "param_table_log2" in str(ei.value)
     # the rules and the maps of "a" are what they were: the next batch still matches the oracle that never saw
     # the failed load, including the tokens consumed before it
-    ev2 = _entries(0, [_long(v % 9) for v in range(60)], t=T0 + 500)
-    ev2 = np.concatenate([ev2, _entries(1, [_long(1)] * 3, t=T0 + 500)])
+    ev2 = _entries(0, [_long(v % 3) for v in range(7)], t=T0 + 500)
+    ev2 = np.concatenate([ev2, _entries(1, [_long(1)], t=T0 + 500)])
     np.testing.assert_array_equal(eng.submit(ev2), orc.submit(ev2))
+
+
+def test_pool_used_up_fails_the_batch_and_the_engine():
+    # the maps' regions grow with their keys (k_pm_grow); 2^8 slots cannot hold a map of 100 keys: the batch
+    # fails with SG_ECAPACITY and every later submit is refused (a key may have been lost)
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=8)
+    rid = eng.register("a")
+    eng.load_param_rules([A.param_rule("a", 0, 2)])
+    np.asarray(eng.submit(_entries(rid, [_long(v) for v in range(6)])))  # fits the first regions
+    with pytest.raises(E.SentinelError) as ei:
+        eng.submit(_entries(rid, [_long(v) for v in range(100)], t=T0 + 10))
+    assert ei.value.code == A.SG_ECAPACITY and "param_table_log2" in str(ei.value)
+    with pytest.raises(E.SentinelError):
+        eng.submit(_entries(rid, [_long(1)], t=T0 + 20))
+
+
+def test_regions_grow_and_the_pool_compacts():
+    # 300 resources, each map growing over 12 batches from 2 buckets towards full size, in a pool a little larger
+    # than the final regions: the regions grown out of fill it and are dropped by relayouts between batches
+    # (rebuild_pmaps); every decision against the oracle
+    n_res = 300
+    eng = E.Engine(max_resources=512, max_slot_chain_size=0, param_table_log2=21)
+    orc = O.Oracle(max_slot_chain_size=0)
+    names = ["g%d" % i for i in range(n_res)]
+    for nm in names:
+        assert eng.register(nm) == orc.register(nm)
+    rules = [A.param_rule(nm, 0, 3, burst_count=1) for nm in names]
+    assert eng.load_param_rules(rules) == orc.load_param_rules(rules)
+    rng = np.random.default_rng(5)
+    for b in range(12):
+        rid = rng.integers(0, n_res, 40_000)
+        keys = [_long(int(v)) for v in rng.integers(0, 150 * (b + 1), len(rid))]
+        ev = np.concatenate([_entries(int(r), [k], t=T0 + 300 * b) for r, k in zip(rid, keys)])
+        dg, do = eng.submit(ev), orc.submit(ev)
+        bad = np.nonzero(dg != do)[0]
+        assert not len(bad), (b, int(bad[0]), hex(dg[bad[0]]), hex(do[bad[0]]))
+    pool = eng.param_pool()
+    assert pool["compactions"] >= 1 and pool["taken"] <= pool["buckets"], pool
 
 
 def test_c5_five_million_distinct_values():

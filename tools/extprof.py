@@ -1,5 +1,5 @@
 """Profiling driver: C4 (or C5) batches through sg_submit_ex with contexts / origins (bench.py's C4-ext / C5-ext
-sub-lines, without the rest of bench.py), for rocprofv3 --kernel-trace --stats."""
+sub-lines, without the rest of bench.py), or C6 (mixed rules, sg_submit), for rocprofv3 --kernel-trace --stats."""
 import os
 import sys
 import time
@@ -28,6 +28,14 @@ if which.startswith("c4"):
         ext = T.ext_for(ev, io, ic, seed=T.SEED_BASE + 44)
     t = time.time()
     r = bench.run_batches(eng, ev, GB, dev, ext=ext)
+elif which == "c6":
+    w = T.Workload(6, seed=T.SEED_BASE + 6, n_entries=int(nb * GB / 2.05) + 1000)
+    ev = w.events[:nb * GB]
+    eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=28, status_ring_log2=28,
+                   max_batch_events=GB)
+    w.install(eng)
+    r = bench.run_batches(eng, ev, GB, dev)
+    r["pool"] = eng.param_pool()
 else:
     w = T.Workload(5, seed=T.SEED_BASE + 5, n_entries=12_000_000)
     eng = E.Engine(max_resources=1 << 14, max_slot_chain_size=0, max_batch_events=1 << 23, param_table_log2=28,
