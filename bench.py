@@ -538,7 +538,53 @@ def config_lines(dev, c4=None):
         w.close()
     if c4 is not None:
         rows.append(dropin_line(dev, *c4))
+    rows.append(token_line(dev))
     return rows
+
+
+def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60):
+    """C5's cluster half: the token server over 10k GLOBAL flowIds (thresholds 10^3..10^5 per
+    window, 1-10 samples of 0.5-2 s), Zipf(1.1) requests in time order, requests and results in HBM
+    (sg_cluster_request_tokens with device buffers, as dist.request_tokens_tensor calls it); first batch untimed."""
+    import torch
+    from sentinel_amd import _abi as A
+    from sentinel_amd import engine as E
+    rng = np.random.default_rng(20240601 + 15)
+    fids = np.arange(1_000_001, 1_000_001 + n_flows)
+    eng = E.Engine(device=dev.index, max_resources=max(1 << 14, n_flows + 16), cluster_max_allowed_qps=10 ** 9)
+    eng.register_many(["r%d" % f for f in fids])
+    rules = [A.flow_rule("r%d" % f, float(int(np.exp(rng.uniform(np.log(1e3), np.log(1e5))))), cluster_mode=True,
+                         cluster_flow_id=int(f), cluster_threshold_type=A.CLUSTER_THRESHOLD_GLOBAL,
+                         cluster_sample_count=int(rng.choice([1, 2, 5, 10])),
+                         cluster_window_interval_ms=int(rng.choice([500, 1000, 2000]))) for f in fids]
+    eng.load_flow_rules(rules)
+    p = 1.0 / np.arange(1, n_flows + 1) ** 1.1
+    p /= p.sum()
+    reqs = np.zeros(n_req, dtype=A.TOKEN_REQ_DTYPE)
+    reqs["ts"] = 1_700_000_000_000 + np.sort(rng.integers(0, seconds * 1000, n_req))
+    reqs["flow_id"] = fids[rng.choice(n_flows, n_req, p=p)]
+    reqs["acquire_count"] = rng.integers(1, 4, n_req)
+    reqs["prioritized"] = rng.random(n_req) < 0.2
+    rq, rs = A.TOKEN_REQ_DTYPE.itemsize, A.TOKEN_RES_DTYPE.itemsize
+    dq = torch.from_numpy(reqs.view(np.uint8)).to(dev)
+    dr = torch.empty(n_req * rs, dtype=torch.uint8, device=dev)
+    cuts = list(range(0, n_req, batch)) + [n_req]
+    eng.cluster_request_ptr(dq.data_ptr(), cuts[1], dr.data_ptr())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in zip(cuts[1:-1], cuts[2:]):
+        eng.cluster_request_ptr(dq.data_ptr() + a * rq, b - a, dr.data_ptr() + a * rs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = dr.view(torch.int32).view(-1, 4)[:, 0].cpu().numpy()
+    n_t = n_req - cuts[1]
+    eng.close()
+    del dq, dr
+    torch.cuda.empty_cache()
+    return {"config": "C5 cluster half: token server, %d GLOBAL flowIds (counts 1e3-1e5), Zipf(1.1) requests over %d s, "
+                      "buffers in HBM, %d-request calls" % (n_flows, seconds, batch),
+            "value": n_t / dt, "unit": "token requests/s", "requests_timed": n_t, "ms_per_call": dt / (len(cuts) - 2) * 1e3,
+            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
 
 
 def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400):

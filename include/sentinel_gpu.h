@@ -370,7 +370,8 @@ int sg_snapshot_metrics(sg_engine* e, int64_t now_ms, sg_metric_node* out, uint6
 
 /* Batched TokenService.requestToken (core/cluster/TokenService.java:26-35,
  * csrv/flow/DefaultTokenService.java:37-48).  Rules come from the flow rules
- * loaded with cluster_mode=1 (the ClusterFlowRuleManager role). */
+ * loaded with cluster_mode=1 (the ClusterFlowRuleManager role).  reqs / out may be host or device
+ * memory; the call returns when the results are written. */
 int sg_cluster_set_connected_count(sg_engine* e, int64_t flow_id, int32_t connected);
 int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n, sg_token_result* out);
 

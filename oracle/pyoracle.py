@@ -61,7 +61,7 @@ def lib():
         L.or_param_thread_count.argtypes = [P, C.c_uint32, C.c_int32, C.c_uint64, C.POINTER(C.c_int64)]
         L.or_param_set_thread_count.argtypes = [P, C.c_uint32, C.c_int32, C.c_uint64, C.c_int64]
         L.or_cluster_set_connected_count.argtypes = [P, C.c_int64, C.c_int32]
-        L.or_cluster_request_tokens.argtypes = [P, C.POINTER(A.SgTokenReq), C.c_uint64, C.POINTER(A.SgTokenResult)]
+        L.or_cluster_request_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p]
         L.or_cluster_request_param_tokens.argtypes = [P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
         L.or_ctrl_new.restype = P
         L.or_ctrl_new.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_int]
@@ -263,8 +263,20 @@ class Oracle:
         for i, (ts, fid, acq, pr) in enumerate(reqs):
             arr[i].ts, arr[i].flow_id, arr[i].acquire_count, arr[i].prioritized = ts, fid, acq, int(pr)
         out = (A.SgTokenResult * max(1, len(reqs)))()
-        assert lib().or_cluster_request_tokens(self.h, arr, len(reqs), out) == 0
+        assert lib().or_cluster_request_tokens(self.h, C.cast(arr, C.c_void_p), len(reqs), C.cast(out, C.c_void_p)) == 0
         return [(out[i].status, out[i].remaining, out[i].wait_in_ms) for i in range(len(reqs))]
+
+    def cluster_request_ptr(self, req_ptr, n, out_ptr):
+        """Host buffers: n A.TOKEN_REQ_DTYPE rows at req_ptr -> A.TOKEN_RES_DTYPE rows at out_ptr."""
+        assert lib().or_cluster_request_tokens(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr)) == 0
+
+    def cluster_request_array(self, reqs):
+        """reqs: A.TOKEN_REQ_DTYPE array -> A.TOKEN_RES_DTYPE array."""
+        reqs = np.ascontiguousarray(reqs, dtype=A.TOKEN_REQ_DTYPE)
+        out = np.zeros(max(1, len(reqs)), dtype=A.TOKEN_RES_DTYPE)
+        if len(reqs):
+            self.cluster_request_ptr(reqs.ctypes.data, len(reqs), out.ctypes.data)
+        return out[: len(reqs)]
 
     def cluster_request_param(self, reqs):
         """reqs: list of (ts, flow_id, acquire, [value keys]) -> list of (status, remaining, wait)."""

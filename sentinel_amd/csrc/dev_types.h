@@ -56,7 +56,8 @@ enum : uint8_t {
                          // StatisticNodes / context DefaultNodes whatever its rules are.  Rules that read them
                          // (PX_ORIGIN / PX_CHAIN) decide on k_lane<16>; otherwise the segment decides on its usual
                          // owner and aux.hip updates the nodes from the committed verdicts afterwards
-    PM_ARGL = 8,         // an event's args[0] was a Collection / array (per-element checks: not k_pq's)
+    PM_ARGL = 8,         // an event's argument was a Collection / array (per-element checks: not k_pq's; its maps
+                         // are grown to full size)
     PM_XARGS = 16        // an EXIT released thread counts with args of its own (sg_submit_ex)
 };
 // SEv.x of an ENTRY (and of an EXIT / TRACE that names no ENTRY of this batch) in an sg_submit_ex batch: the

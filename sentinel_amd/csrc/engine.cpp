@@ -2034,7 +2034,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (e->pool_nb) {
         DevState Sg{};
         std::memset(&Sg, 0, sizeof(Sg));
-        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid;
+        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
         Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
         HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, st));
         HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
@@ -2407,7 +2407,8 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
         e->ctab_mask = 15;
     }
     const uint32_t nflows = (uint32_t)e->cflows.size();
-    HIPCHK(hipMemcpyAsync(e->d_treq, reqs, n * sizeof(sg_token_req), hipMemcpyHostToDevice, st));
+    // requests and results may be host or device memory (dist.request_tokens keeps them in HBM under RCCL)
+    HIPCHK(hipMemcpyAsync(e->d_treq, reqs, n * sizeof(sg_token_req), hipMemcpyDefault, st));
     HIPCHK(hipMemsetAsync(e->d_small, 0, 4, st));
     HIPCHK(launch_tok_classify(e->d_treq, n, e->d_ctab, e->ctab_mask, e->d_tfidx, e->d_tres, e->d_small, st));
     uint32_t flags = 0;
@@ -2433,7 +2434,7 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
         HIPCHK(launch_tok_flow(kin, vin, n, e->d_treq, e->d_cflow, nflows, e->d_cbkt, e->cfg.cluster_exceed_count,
                                e->cfg.cluster_max_occupy_ratio, e->d_tres, st));
     }
-    HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDefault, st));
     HIPCHK(hipStreamSynchronize(st));
     return SG_OK;
 }

@@ -102,13 +102,14 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
                     const sg_arg a = args[x.arg_off + k];
                     if (a.kind > SG_ARG_LIST || (a.kind == SG_ARG_LIST && (a.key > n_args || a.len > n_args - a.key)))
                         fl |= BF_BAD_ARGS;
-                    else if (a.kind == SG_ARG_LIST)
+                    else if (a.kind == SG_ARG_LIST) {
+                        mark |= PM_ARGL;  // (at any index: one map access per element, param.hip k_pm_grow)
                         for (uint32_t q = 0; q < a.len; ++q)
                             if (args[a.key + q].kind > SG_ARG_SCALAR) fl |= BF_BAD_ARGS;
+                    }
                 }
                 const sg_arg a0 = args[x.arg_off];
                 key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
-                if (a0.kind == SG_ARG_LIST) mark |= PM_ARGL;
                 own_args = true;
             }
             if (x.context_id > max_ctx) mark |= PM_LANE;

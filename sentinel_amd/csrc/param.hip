@@ -1075,15 +1075,77 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
     // EXITs at segment positions >= tm_from release thread counts (uniform)
     uint32_t tm_from = ((sh.node.flags & (NI_PM | ni_tm(0))) == (NI_PM | ni_tm(0))) ? 0u : 0xFFFFFFFFu;
 
-    for (uint32_t tb = 0; tb < sg.len; tb += TE) {
+    // The passes around an owner (XF_MIX) walk only the events that touch a map, listed in order into the segment's
+    // pend[] scratch (free outside the owner's run): the pre pass the ENTRYs with args[0], the post pass the passed
+    // ones and the EXITs releasing args.  A C6 head segment of 4M events is then 2M / ~0.2M accesses.  The post pass
+    // takes every ENTRY's visits of the rules (the node's ParameterMetric bits, the first visit of rule k0) from the
+    // final verdicts on the way.
+    uint32_t nev = sg.len;
+    if (MODE != PQ_FULL) {
+        uint32_t kbits[PQ_MAXP];
+        for (int k = 0; k < PQ_MAXP; ++k) {
+            kbits[k] = 0;
+            if (k < np) {
+                const DRule& r = sh.rules[k];
+                kbits[k] = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
+                           : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
+            }
+        }
+        if (tid == 0) sh.freach = 0xFFFFFFFFu;
+        __syncthreads();
+        uint32_t fbits = 0, base = 0;
+        for (uint32_t c = 0; c < sg.len; c += HW) {  // (uniform trip count)
+            const uint32_t p = c + tid;
+            bool take = false;
+            if (p < sg.len) {
+                const uint32_t w = reinterpret_cast<const uint4*>(recs)[sg.start + p].w;
+                const uint32_t kind = w & 0xFFu, fl = (w >> 8) & 0xFFu;
+                if (MODE == PQ_PRE) {
+                    take = kind == SG_EV_ENTRY && (fl & SG_F_HAS_ARG);
+                } else if (kind == SG_EV_ENTRY) {  // the final verdict as the rule it stopped at
+                    const uint32_t d = dec[sg.start + p];
+                    uint32_t stq = 0;
+                    if (!st_passed(d & 0xFFu)) {
+                        stq = (uint32_t)np + 1;  // a flow / degrade stage blocked it: every param rule was visited
+                        if ((d & 0xFFu) == ST_BLOCK_PARAM)
+                            for (int k = 0; k < np; ++k)
+                                if (sh.rules[k].behavior != PB_INIT_ONLY && sh.rules[k].slot == ((d >> 8) & 0xFFu))
+                                    stq = (uint32_t)k + 1;
+                    }
+                    for (int k = 0; k < np; ++k)
+                        if (stq == 0 || stq > (uint32_t)k) {
+                            fbits |= kbits[k] | NI_PM;
+                            if (k == k0) atomicMin(&sh.freach, p + 1);
+                        }
+                    take = stq == 0 && (fl & SG_F_HAS_ARG);
+                } else if (kind == SG_EV_EXIT) {
+                    take = (fl & SG_F_EXIT_ARGS) != 0;
+                }
+            }
+            uint32_t tot;
+            const uint32_t o = pq_scan<NW>(sh, take ? 1u : 0u, &tot);
+            if (take) S.pend[sg.start + base + o] = p;
+            base += tot;
+        }
+        if (fbits) atomicOr(&sh.flags_or, fbits);
+        nev = base;
+        __syncthreads();
+        if (MODE == PQ_POST && tm_from == 0xFFFFFFFFu) tm_from = sh.freach;
+    }
+
+    for (uint32_t tb = 0; tb < nev; tb += TE) {
         // ---- 1. the tile's events
         uint32_t st[PQ_EPL], wt[PQ_EPL];  // st: 0 pending / passed, else the blocking rule + 1
+        uint32_t pp[PQ_EPL];              // segment positions (the listed ones around an owner)
 #pragma unroll
         for (int q = 0; q < PQ_EPL; ++q) {
-            const uint32_t e = tid * PQ_EPL + q, p = tb + e;
+            const uint32_t e = tid * PQ_EPL + q, ci = tb + e;
+            const bool ok = ci < nev;
+            const uint32_t p = MODE == PQ_FULL ? ci : (ok ? S.pend[sg.start + ci] : 0xFFFFFFFFu);
+            pp[q] = ok ? p : 0xFFFFFFFFu;
             SEv r;
             r.kind = 0xFF; r.flags = 0; r.code = 0; r.dt = 0; r.cnt = 0; r.rt = 0; r.x = 0;
-            if (p < sg.len) r = recs[sg.start + p];
+            if (ok) r = recs[sg.start + p];
             st[q] = 0;
             wt[q] = 0;
             sh.tdt[e] = r.dt;
@@ -1093,40 +1155,16 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
             // args[0]'s key: k_rs_first put it in the key ring (sg_submit's aux, or sg_submit_ex's table entry)
             if (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG))
                 sh.tkey[e] = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
-            if (MODE == PQ_POST && p < sg.len && r.kind == SG_EV_ENTRY) {  // the final verdict as the rule it stopped at
-                const uint32_t d = dec[sg.start + p];
-                if (!st_passed(d & 0xFFu)) {
-                    st[q] = (uint32_t)np + 1;  // a flow / degrade stage blocked it: every param rule was visited
-                    if ((d & 0xFFu) == ST_BLOCK_PARAM)
-                        for (int k = 0; k < np; ++k)
-                            if (sh.rules[k].behavior != PB_INIT_ONLY && sh.rules[k].slot == ((d >> 8) & 0xFFu))
-                                st[q] = (uint32_t)k + 1;
-                }
-            }
         }
         __syncthreads();
         // ---- 2. ParamFlowSlot: the rules in order
         bool ran_qps = false;  // a rule map phase of this tile left its sorted accesses in skey / sidx
-        if (tid == 0) sh.freach = 0xFFFFFFFFu;
+        if (tid == 0 && MODE == PQ_FULL) sh.freach = 0xFFFFFFFFu;
         __syncthreads();
         PQ_MARK(0)
         for (int k = 0; k < np; ++k) {
             const DRule& r = sh.rules[k];
-            if (MODE == PQ_POST) {  // the visits only (the node's ParameterMetric bits, the first visit of rule k0)
-                bool reach = false;
-#pragma unroll
-                for (int q = 0; q < PQ_EPL; ++q) {
-                    const bool rq = (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY && (st[q] == 0 || st[q] > (uint32_t)k);
-                    reach |= rq;
-                    if (rq && k == k0 && tb + tid * PQ_EPL + q < sg.len) atomicMin(&sh.freach, tb + tid * PQ_EPL + q + 1);
-                }
-                if (reach) {
-                    const uint32_t bits = r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
-                                          : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
-                    atomicOr(&sh.flags_or, bits | NI_PM);
-                }
-                continue;
-            }
+            if (MODE == PQ_POST) break;  // (its visits were taken with the list)
             bool reach = false;
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
@@ -1180,7 +1218,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
         // ParamFlowStatisticEntryCallback.onPass of the passed ENTRYs (OP_ADD), and the EXITs' releases
         // (ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount of the ENTRY's argument, OP_SUB)
         __syncthreads();  // every lane's atomicMin on freach is in
-        if (tm_from == 0xFFFFFFFFu) tm_from = sh.freach;  // uniform (LDS)
+        if (MODE == PQ_FULL && tm_from == 0xFFFFFFFFu) tm_from = sh.freach;  // uniform (LDS)
         if (MODE != PQ_PRE && tm_on) {
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) sh.tdec[tid * PQ_EPL + q] = st[q];
@@ -1188,11 +1226,12 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
             bool acc[PQ_EPL];
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
-                const uint32_t e = tid * PQ_EPL + q, p = tb + e, kx = sh.tkx[e], kind = kx & 0xFFu;
+                const uint32_t e = tid * PQ_EPL + q, p = pp[q], kx = sh.tkx[e], kind = kx & 0xFFu;
+                const bool ok = p != 0xFFFFFFFFu;
                 uint32_t op = OP_NONE;
-                if (p < sg.len && kind == SG_EV_ENTRY) {
+                if (ok && kind == SG_EV_ENTRY) {
                     if (((kx >> 8) & SG_F_HAS_ARG) && st[q] == 0) op = tk >= 0 ? OP_CHK : OP_ADD;
-                } else if (p < sg.len && kind == SG_EV_EXIT && ((kx >> 8) & SG_F_EXIT_ARGS) && p >= tm_from
+                } else if (ok && kind == SG_EV_EXIT && ((kx >> 8) & SG_F_EXIT_ARGS) && p >= tm_from
                            && S.key_ring) {
                     const uint32_t code = (kx >> 16) & 0xFFu;
                     // Entry.exit(count, args) with args of its own (sg_submit_ex) releases those, even naming no
@@ -1208,8 +1247,8 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
                         const uint32_t rel = sh.tx[e] - sg.start;
                         if (rel < p) {
                             ref = S.gbase + (vals[sh.tx[e]] & 0x7FFFFFFFu);
-                            if (rel >= tb) op = sh.tdec[rel - tb] != 0 ? OP_NONE : (tk >= 0 ? OP_SUBC : OP_SUB);
-                            else op = st_passed(ld32(&dec[sh.tx[e]]) & 0xFF) ? OP_SUB : OP_NONE;
+                            if (MODE == PQ_FULL && rel >= tb) op = sh.tdec[rel - tb] != 0 ? OP_NONE : (tk >= 0 ? OP_SUBC : OP_SUB);
+                            else op = st_passed(ld32(&dec[sh.tx[e]]) & 0xFF) ? OP_SUB : OP_NONE;  // (post: final)
                         }
                     }
                     if (op != OP_NONE) {
@@ -1246,8 +1285,8 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
         if (MODE == PQ_PRE) {  // the param-blocked ENTRYs: final words, marked for the owner
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {
-                const uint32_t p = tb + tid * PQ_EPL + q;
-                if (p < sg.len && st[q] != 0 && (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY) {
+                const uint32_t p = pp[q];
+                if (p != 0xFFFFFFFFu && st[q] != 0 && (sh.tkx[tid * PQ_EPL + q] & 0xFFu) == SG_EV_ENTRY) {
                     dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, sh.rules[st[q] - 1].slot, 0);
                     recs[sg.start + p].flags = (uint8_t)(((sh.tkx[tid * PQ_EPL + q] >> 8) & 0xFFu) | RF_PBLK);
                 }
@@ -1365,14 +1404,16 @@ __global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, c
     const Seg sg = segs[s];
     const Prog pg = S.prog[sg.res];
     if (pg.tm_base == NO_ID && pg.n_param == 0) return;
+    // an argument that is a Collection / array is one access per element (PM_ARGL): no bound, full size
+    const uint64_t adds = (S.prio && (S.prio[sg.res] & PM_ARGL)) ? 0xFFFFFFFFull : (uint64_t)sg.len;
     for (int k = 0; k < pg.n_param; ++k) {
         const DRule& r = S.rules[pg.rule_off + k];
-        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, sg.len, pool_next, pool_nb, bflags);
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags);
     }
     if (pg.tm_base != NO_ID)
         for (int i = 0; i < SG_MAX_ARGS; ++i) {
             const uint32_t id = S.tmid[pg.tm_base + i];
-            if (id != NO_ID) pm_grow(S, id, sg.len, pool_next, pool_nb, bflags);
+            if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags);
         }
 }
 // listed maps to full size (rule load: STRATEGY_RELATE members)

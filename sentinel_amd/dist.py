@@ -194,6 +194,47 @@ def gather_metrics(snapshot: np.ndarray, group=None) -> np.ndarray:
     return allr[np.lexsort((allr["res_id"], allr["reserved"], allr["timestamp"]))]
 
 
+def request_tokens_tensor(reqs: "torch.Tensor", decide_ptr=None, server: int = 0, group=None) -> "torch.Tensor":
+    """Device-resident token requests: ``reqs`` = this rank's A.TOKEN_REQ_DTYPE rows (time-ordered) as a uint8
+    tensor on the group's device (HBM under RCCL), returns its A.TOKEN_RES_DTYPE rows as a uint8 tensor there.
+    Nothing goes through host memory: the rows are all-gathered, the server rank orders the whole namespace by time
+    (a stable sort on ts of the rank-ordered concatenation = (ts, rank, index) order), decides them in one call of
+    ``decide_ptr(req_ptr, n, out_ptr)`` (``Engine.cluster_request_ptr``: sg_cluster_request_tokens takes device
+    buffers) and broadcasts the results.  Collective, like request_tokens."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rq, rs = A.TOKEN_REQ_DTYPE.itemsize, A.TOKEN_RES_DTYPE.itemsize
+    dev = reqs.device
+    n = reqs.numel() // rq
+    cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    ns = [int(c.item()) for c in cnts]
+    total = sum(ns)
+    if total == 0:
+        return torch.zeros(0, dtype=torch.uint8, device=dev)
+    width = max(ns) * rq
+    mine = torch.zeros(width, dtype=torch.uint8, device=dev)
+    mine[: n * rq] = reqs.reshape(-1)
+    outs = [torch.empty(width, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(outs, mine, group=group)
+    res = torch.zeros(total * rs, dtype=torch.uint8, device=dev)
+    if rank == server:
+        if decide_ptr is None:
+            raise ValueError("the token-server rank needs a decide function")
+        allq = torch.cat([outs[r][: ns[r] * rq] for r in range(world)]).view(total, rq)
+        ts = allq[:, :8].contiguous().view(torch.int64).view(-1)
+        order = torch.sort(ts, stable=True).indices
+        q = allq.index_select(0, order).contiguous()
+        out = torch.empty((total, rs), dtype=torch.uint8, device=dev)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)  # (the engine's own stream reads q)
+        decide_ptr(q.data_ptr(), total, out.data_ptr())
+        res.view(total, rs).index_copy_(0, order, out)
+    dist.broadcast(res, src=server, group=group)
+    off = sum(ns[:rank])
+    return res[off * rs: (off + n) * rs]
+
+
 def request_tokens(reqs: np.ndarray, decide=None, server: int = 0, group=None) -> np.ndarray:
     """Token requests of this rank (A.TOKEN_REQ_DTYPE, time-ordered) -> results (A.TOKEN_RES_DTYPE).
 

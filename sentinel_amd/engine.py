@@ -272,6 +272,10 @@ class Engine:
         _check(lib().sg_cluster_request_tokens(self.h, reqs.ctypes.data, len(reqs), out.ctypes.data))
         return out
 
+    def cluster_request_ptr(self, req_ptr: int, n: int, out_ptr: int):
+        """Device (or host) buffers: n A.TOKEN_REQ_DTYPE rows at req_ptr -> A.TOKEN_RES_DTYPE rows at out_ptr."""
+        _check(lib().sg_cluster_request_tokens(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr)))
+
     def cluster_request(self, reqs):
         """reqs: list of (ts, flow_id, acquire, prioritized) -> list of (status, remaining, wait)."""
         arr = np.zeros(len(reqs), dtype=A.TOKEN_REQ_DTYPE)

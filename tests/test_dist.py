@@ -101,6 +101,53 @@ def _w_tokens(rank, world, port, use_gpu):
     dist.destroy_process_group()
 
 
+def _w_tokens_tensor(rank, world, port, backend):
+    # request_tokens_tensor: the requests and results stay tensors on the group's device (HBM under RCCL), the
+    # server decides through a pointer call (the engine's device buffers, or the oracle's host ones under gloo)
+    import torch
+    import torch.distributed as dist
+    for p in (ROOT, os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    import pyoracle as O
+    from sentinel_amd import _abi as A
+    from sentinel_amd import dist as D
+    fids = list(range(11, 19))
+    dev = torch.device("cuda", 0) if backend == "nccl" else torch.device("cpu")
+    decide = None
+    if rank == 0:
+        if backend == "nccl":
+            from sentinel_amd import engine as E
+            eng = E.Engine(max_resources=64, cluster_max_allowed_qps=250)
+            eng.load_flow_rules(_cluster_rules(A, fids))
+            decide = eng.cluster_request_ptr
+        else:
+            o = O.Oracle(cluster_max_allowed_qps=250)
+            o.load_flow_rules(_cluster_rules(A, fids))
+            decide = o.cluster_request_ptr
+    ref = _oracle_decider(O, A, fids, cluster_max_allowed_qps=250)
+    for rnd in range(len(PLAN)):
+        mine = _batch(A, rank, rnd)
+        t = torch.from_numpy(mine.view(np.uint8).copy()).to(dev)
+        got = D.request_tokens_tensor(t, decide)
+        assert got.device.type == dev.type
+        got = got.cpu().numpy().view(A.TOKEN_RES_DTYPE)
+        allq = [_batch(A, r, rnd) for r in range(world)]
+        cat = np.concatenate(allq)
+        src = np.concatenate([np.full(len(q), r) for r, q in enumerate(allq)])
+        loc = np.concatenate([np.arange(len(q)) for q in allq])
+        order = np.lexsort((loc, src, cat["ts"]))
+        res = np.zeros(len(cat), dtype=A.TOKEN_RES_DTYPE)
+        res[order] = ref(cat[order])
+        off = sum(len(q) for q in allq[:rank])
+        assert np.array_equal(got, res[off: off + len(mine)]), (rank, rnd)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _w_metrics(rank, world, port):
     dist = _init(rank, world, port)
     from sentinel_amd import _abi as A
@@ -248,6 +295,17 @@ def test_request_tokens_gloo():
 @pytest.mark.gpu
 def test_request_tokens_gpu_server():
     mp.spawn(_w_tokens, args=(2, _port(), True), nprocs=2, join=True)
+
+
+def test_request_tokens_tensor_gloo():
+    mp.spawn(_w_tokens_tensor, args=(2, _port(), "gloo"), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
+def test_request_tokens_tensor_rccl():
+    # one GPU on the box: a one-rank RCCL group, every buffer in HBM (the ordering, the pointer call into the
+    # engine and the broadcast on device tensors)
+    mp.spawn(_w_tokens_tensor, args=(1, _port(), "nccl"), nprocs=1, join=True)
 
 
 def test_partitioned_oracle_equals_one_oracle():

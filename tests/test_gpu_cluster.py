@@ -138,3 +138,57 @@ def test_unordered_requests_rejected():
     eng.load_flow_rules([_rule(7, 5)])
     with pytest.raises(E.SentinelError):
         eng.cluster_request([(T0 + 5, 7, 1, False), (T0, 7, 1, False)])
+
+
+def _flows_10k(rng, n_flows=10_000):
+    fids = np.arange(1_000_001, 1_000_001 + n_flows)
+    rules = []
+    for f in fids:
+        rules.append(A.flow_rule("r%d" % f, float(int(np.exp(rng.uniform(np.log(1e3), np.log(1e5))))),
+                                 cluster_mode=True, cluster_flow_id=int(f),
+                                 cluster_threshold_type=A.CLUSTER_THRESHOLD_GLOBAL,
+                                 cluster_sample_count=int(rng.choice([1, 2, 5, 10])),
+                                 cluster_window_interval_ms=int(rng.choice([500, 1000, 2000]))))
+    return fids, rules
+
+
+def _requests_10k(rng, fids, n, seconds):
+    ts = T0 + np.sort(rng.integers(0, seconds * 1000, n))
+    p = 1.0 / np.arange(1, len(fids) + 1) ** 1.1
+    p /= p.sum()
+    out = np.zeros(n, dtype=A.TOKEN_REQ_DTYPE)
+    out["ts"], out["flow_id"] = ts, fids[rng.choice(len(fids), n, p=p)]
+    out["acquire_count"] = rng.integers(1, 4, n)
+    out["prioritized"] = rng.random(n) < 0.2
+    return out
+
+
+def test_ten_thousand_global_flows():
+    # SURVEY.md §8(d) C5's cluster half at config size: 10k flowIds with GLOBAL thresholds of
+    # 10^3..10^5 per window (1-10 samples of 0.5-2 s), Zipf(1.1) over the flows, 3M requests over 12 s through the
+    # token server with device-resident buffers, against the oracle request by request
+    rng = np.random.default_rng(20240601 + 15)
+    fids, rules = _flows_10k(rng)
+    eng = E.Engine(max_resources=16_384, cluster_max_allowed_qps=400_000)  # the namespace limiter above the traffic
+    orc = O.Oracle(cluster_max_allowed_qps=400_000)
+    for x in (eng, orc):
+        for f in fids:
+            x.register("r%d" % f)
+        x.load_flow_rules(rules)
+    reqs = _requests_10k(rng, fids, 3_000_000, 12)
+    import torch
+    dev = torch.device("cuda", 0)
+    dq = torch.from_numpy(reqs.view(np.uint8).copy()).to(dev)
+    dr = torch.empty(len(reqs) * A.TOKEN_RES_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    rq, rs = A.TOKEN_REQ_DTYPE.itemsize, A.TOKEN_RES_DTYPE.itemsize
+    cuts = [0, 1, 250_000, 1_000_000, 2_000_000, len(reqs)]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        eng.cluster_request_ptr(dq.data_ptr() + a * rq, b - a, dr.data_ptr() + a * rs)
+    got = dr.cpu().numpy().view(A.TOKEN_RES_DTYPE)
+    want = np.concatenate([orc.cluster_request_array(reqs[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    for k in ("status", "remaining", "wait_in_ms"):
+        bad = np.nonzero(got[k] != want[k])[0]
+        assert len(bad) == 0, "%s of request %d: gpu %s oracle %s (%d mismatches)" % (
+            k, bad[0], got[bad[0]], want[bad[0]], len(bad))
+    st = np.bincount(got["status"] + 1)
+    assert (got["status"] == A.TOKEN_OK).sum() > 0 and (got["status"] == A.TOKEN_BLOCKED).sum() > 1000, st
