@@ -83,7 +83,7 @@ static_assert(sizeof(NodeInfo) == 32, "NodeInfo must be 32 B");
 enum : uint8_t {
     PF_EXC_COUNT = 1,   // has an EXCEPTION_COUNT breaker (minute exception running sum)
     PF_WARM = 2,        // has a WarmUp / WarmUpRateLimiter controller
-    PF_PQ = 4,          // only QPS-grade param rules with a fixed paramIdx and maps of capacity <= 4080: the
+    PF_PQ = 4,          // only QPS-grade param rules with a fixed paramIdx and maps of capacity <= PQ_MAX_CAP: the
                         // cooperative param owner (param.hip k_pq) decides it in batches it is enabled for
     PF_SERIAL = 8,      // outside the cooperative (Jacobi) kernels' limits: per-lane serial kernel only
     PF_RL = 16,         // has a RateLimiter / WarmUpRateLimiter controller
@@ -214,6 +214,7 @@ struct PMap {
 static_assert(sizeof(PMap) == 64, "PMap must be 64 B");
 #define PM_BASE_CAP 4000u      // ParameterMetric.BASE_PARAM_MAX_CAPACITY / THREAD_COUNT_MAX_CAPACITY
 #define PM_TOTAL_CAP 200000u   // ParameterMetric.TOTAL_MAX_CAPACITY
+#define PQ_MAX_CAP 8176u       // largest map k_pq holds (its live-stamp ring of 2^15 bits in LDS: durationInSec <= 2)
 
 enum : uint8_t { ST_PASS = 0, ST_PASS_WAIT = 1, ST_BLOCK_FLOW = 2, ST_BLOCK_DEGRADE = 3, ST_BLOCK_PARAM = 4,
                  ST_NO_CHECK = 5, ST_BLOCK_UPSTREAM = 6, ST_NOT_ENTRY = 0xFF };

@@ -690,12 +690,12 @@ static int collect(sg_engine* e, int k) {
     if (bflags & BF_BACKWARD)
         return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
     if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
-    if (bflags & BF_POOL_FULL)  // a map that could not grow may have lost a key (a ghost entry, as below)
-        e->fatal = "the hot-parameter map pool is used up (raise param_table_log2)";
     // A map that could not place a key has already committed its ring bit and live count (a ghost entry), and a
     // failed k_pq invariant leaves its maps in an unknown state: the engine refuses every later batch.
     if (bflags & BF_PQ_INVARIANT)
         e->fatal = "internal error: a k_pq tile's presorted key subset did not match its accesses";
+    else if (bflags & BF_POOL_FULL)  // a map that could not grow may have lost a key (a ghost entry, as below)
+        e->fatal = "the hot-parameter map pool is used up (raise param_table_log2)";
     else if (bflags & BF_PTAB_FULL)
         e->fatal = "a hot-parameter map table could not place a key (its map holds a ghost entry)";
     if (bflags & (BF_PQ_INVARIANT | BF_PTAB_FULL | BF_POOL_FULL)) return fail(SG_ECAPACITY, e->fatal + " -- engine unusable");
@@ -889,7 +889,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (d.param_idx < 0) mix = false;
                 else if (d.behavior == PB_INIT_ONLY) { if (d.burst & ~1) mix = false; }
                 else if (d.param_idx != 0 || d.grade != SG_FLOW_GRADE_QPS ||
-                         d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || rule_map_cap(d.duration_sec) > 4080)
+                         d.behavior != SG_CONTROL_BEHAVIOR_DEFAULT || rule_map_cap(d.duration_sec) > PQ_MAX_CAP)
                     mix = false;
             }
             if (mix) {  // a thread-count map of another index is k_lane's
@@ -916,7 +916,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 else if (d.behavior == PB_INIT_ONLY) { if (d.burst & ~1) pq = false; }  // maps on other indices
                 else if (d.param_idx != 0) pq = false;  // sg_submit_ex args beyond [0] are k_lane's
                 else if (d.grade == SG_FLOW_GRADE_THREAD) { ++n_thread; thread_at = i; last_checked = i; }
-                else if (d.grade != SG_FLOW_GRADE_QPS || rule_map_cap(d.duration_sec) > 4080) pq = false;
+                else if (d.grade != SG_FLOW_GRADE_QPS || rule_map_cap(d.duration_sec) > PQ_MAX_CAP) pq = false;
                 else last_checked = i;
             }
             if (n_thread > 1 || (n_thread == 1 && thread_at != last_checked)) pq = false;

@@ -35,10 +35,10 @@
 using namespace sg;
 
 #define PQ_MAXP 4          // param rules of a k_pq resource (engine.cpp PF_PQ)
-#define PQ_RBW 256         // ring words a map may have (2^14 bits: capacity <= 4080)
+#define PQ_RBW 512         // ring words a map may have (2^15 bits: capacity <= 8176, durationInSec <= 2)
 #define PQ_EPL 2           // events per lane per tile
 #define PQ_NPEND 64        // keys waiting for a displacement walk per tile (more: BF_PTAB_FULL)
-#define PQ_CLW 128         // claim bitmap words (>= buckets * 8 / 64 for capacity <= 4080)
+#define PQ_CLW 256         // claim bitmap words (>= buckets * 8 / 64 for capacity <= 8176)
 #define RANK_REP (-1)      // not a first access of its key in the tile
 #define RANK_NEW 0x7FFFFFFF
 
@@ -174,6 +174,24 @@ __device__ __forceinline__ bool ring_live(const PMap& m, const uint64_t* bm, int
 
 // Tighten thr to the lowest live stamp; renumber the live stamps densely (pm_compact, in parallel) when the ring
 // would otherwise wrap onto a live stamp within the next `k` stamps.
+// wpre[w] = live stamps in the W ring words before word w, in stamp order from word w0 (a thread takes
+// ceil(W / lanes) consecutive words: W can exceed the 256-lane owner's lanes)
+template <int NW>
+__device__ __forceinline__ void pq_word_ranks(PqSh<NW>& sh, int mk, uint32_t w0, uint32_t W) {
+    constexpr uint32_t HW = PqSh<NW>::HW;
+    const uint32_t per = (W + HW - 1) / HW, l0 = threadIdx.x * per;
+    uint32_t c = 0;
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) c += (uint32_t)__popcll(sh.bm[mk][(w0 + l0 + u) & (W - 1)]);
+    uint32_t tot;
+    uint32_t run = pq_scan<NW>(sh, c, &tot);
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) {
+            const uint32_t w = (w0 + l0 + u) & (W - 1);
+            sh.wpre[w] = run;
+            run += (uint32_t)__popcll(sh.bm[mk][w]);
+        }
+}
 template <int NW>
 __device__ void pq_reserve(PqSh<NW>& sh, int mk, const DevState& S, uint32_t k) {
     PMap& m = sh.hdr[mk];
@@ -185,12 +203,7 @@ __device__ void pq_reserve(PqSh<NW>& sh, int mk, const DevState& S, uint32_t k) 
     __syncthreads();
     if (m.clock + (int64_t)k - m.thr <= RB - 64) return;
     // ranks of the live stamps in stamp order
-    const uint32_t w0 = ring_word(m, m.thr);
-    const uint32_t lw = threadIdx.x;
-    const uint32_t c = lw < W ? (uint32_t)__popcll(sh.bm[mk][(w0 + lw) & (W - 1)]) : 0u;
-    uint32_t tot;
-    const uint32_t pre = pq_scan<NW>(sh, c, &tot);
-    if (lw < W) sh.wpre[(w0 + lw) & (W - 1)] = pre;
+    pq_word_ranks<NW>(sh, mk, ring_word(m, m.thr), W);
     __syncthreads();
     const int64_t base = m.clock - (int64_t)m.live;
     PBucket* B = S.pbkt + m.base;
@@ -473,13 +486,7 @@ __device__ __noinline__ void pq_map_phase(PqSh<NW>& sh, int mk, int walk, const 
     const uint32_t W = (uint32_t)(RB >> 6);
     const int64_t clock0 = m.clock;
     const uint32_t live0 = m.live, cap = m.cap;
-    {   // ranks: live stamps before each ring word, in stamp order from thr
-        const uint32_t w0 = ring_word(m, m.thr);
-        const uint32_t c = tid < W ? (uint32_t)__popcll(sh.bm[mk][(w0 + tid) & (W - 1)]) : 0u;
-        uint32_t tot;
-        const uint32_t pre = pq_scan<NW>(sh, c, &tot);
-        if (tid < W) sh.wpre[(w0 + tid) & (W - 1)] = pre;
-    }
+    pq_word_ranks<NW>(sh, mk, ring_word(m, m.thr), W);  // ranks: live stamps before each ring word, from thr
     __syncthreads();
     // (b) group leaders probe the map; their ranks by tile event
     PBucket* B = S.pbkt + m.base;

@@ -67,7 +67,7 @@ def test_capacity_follows_the_duration_on_the_device():
 
 def test_ecapacity_at_rule_load_leaves_the_engine_unchanged():
     # 2^5 slots hold the first regions of one resource's maps (a rule map + a thread-count map, PM_MIN_NB = 2
-    # buckets of 8 each) but not two; batches of <= 8 events never grow a region
+    # buckets of 8 each) but not two; a region grows only once live keys + a batch's events exceed 8
     eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=5)
     orc = O.Oracle(max_slot_chain_size=0)
     for n in ("a", "b"):
@@ -81,7 +81,7 @@ def test_ecapacity_at_rule_load_leaves_the_engine_unchanged():
     assert ei.value.code == A.SG_ECAPACITY and "param_table_log2" in str(ei.value)
     # the rules and the maps of "a" are what they were: the next batch still matches the oracle that never saw
     # the failed load, including the tokens consumed before it
-    ev2 = _entries(0, [_long(v % 3) for v in range(7)], t=T0 + 500)
+    ev2 = _entries(0, [_long(v % 3) for v in range(4)], t=T0 + 500)  # 3 live keys + 5 events (with b's)
     ev2 = np.concatenate([ev2, _entries(1, [_long(1)], t=T0 + 500)])
     np.testing.assert_array_equal(eng.submit(ev2), orc.submit(ev2))
 

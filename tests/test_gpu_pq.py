@@ -235,3 +235,33 @@ def test_pq_ext_args_contexts(variant):
                 continue
             assert ga is not None and ga["thread"] == oa["thread"], (r, nm)
             np.testing.assert_array_equal(ga["second"], oa["second"][:2], err_msg="origin node %d/%s" % (r, nm))
+
+
+@pytest.mark.parametrize("wide", ["0", "1073741824"])
+def test_pq_duration_two_maps(wide, monkeypatch):
+    # durationInSec = 2: CacheMaps of min(4000 * 2, 200000) = 8000 values (ParameterMetric.java:37-39), a 2^15-bit
+    # live-stamp ring in k_pq's LDS; > 8000 distinct values per resource so the maps fill and evict, exits releasing
+    # their argument; on the 1024-lane (wide=0) and the 256-lane owner
+    monkeypatch.setenv("SG_PQ_WIDE", wide)
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=22, status_ring_log2=24)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for nm in NAMES:
+        assert eng.register(nm) == orc.register(nm)
+    rules = [A.param_rule("m0", 0, 3, duration_in_sec=2, burst_count=2),
+             A.param_rule("m1", 0, 2, duration_in_sec=2),
+             A.param_rule("m1", 0, 9, duration_in_sec=1),
+             A.param_rule("m2", 0, 5, duration_in_sec=2, control_behavior=A.CONTROL_BEHAVIOR_RATE_LIMITER,
+                          max_queueing_time_ms=30),
+             A.param_rule("m3", 0, 4, duration_in_sec=3)]  # 12000 values: beyond k_pq's rings, the per-lane kernel
+    assert eng.load_param_rules(rules) == orc.load_param_rules(rules)
+    t, gbase = T0, 0
+    for b in range(4):
+        ev = _synthetic(300 + b, 60_000, gbase, nres=4, nval=30_000, t=t, exit_args=0.5)
+        gbase += len(ev)
+        d = _compare(eng, orc, ev, False, "batch %d" % b)
+        t = int(ev["ts"].max()) + 1
+    assert int(((d & 0xFF) == A.BLOCK_PARAM).sum()) > 0
+    for r in range(4):
+        g, o = eng.read_node(r), orc.read_node(r)
+        assert g["thread"] == o["thread"]
+        np.testing.assert_array_equal(g["second"][:2], o["second"][:2])
