@@ -341,7 +341,7 @@ def main():
         del buf, base, base64, out
         eng.close()
         torch.cuda.empty_cache()
-        configs = config_lines(dev, (w, ev))
+        configs = config_lines(dev, (w, ev), 0 if args.no_cpu_baseline else 4_000_000)
 
     if rank == 0:
         line = {
@@ -486,7 +486,24 @@ def param_args(ev):
     return ext, table
 
 
-def config_lines(dev, c4=None):
+def config_cpu_baseline(w, ev, n_events):
+    """The oracle on the config's first n_events events (rounded down to whole EXIT references: a prefix of the
+    trace is self-contained), this job's CPU share partitioned by resource, as the C4 line's cpu_baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    T = cpu_share()
+    sample = ev[:min(len(ev), n_events)]
+    po = O.PartitionedOracle(w, T, max_slot_chain_size=0)
+    spent = []
+    po.submit(sample, timed=spent)
+    po.close()
+    n_ent = int((sample["kind"] == 0).sum())
+    return {"value": n_ent / spent[0], "unit": "entries/s", "cores": T, "kind": "port",
+            "sample": "first %d events (%d entries) of the config's trace, oracle/liboracle.so, %d threads partitioned "
+                      "by splitmix64(res_id) %% %d (routing excluded)" % (len(sample), n_ent, T, T)}
+
+
+def config_lines(dev, c4=None, cpu_events=4_000_000):
     """The SURVEY.md configs besides the headline: C2, C3, C5, C6 (mixed rules); with c4 = (workload, events) of the headline trace,
     C4 and C4-ext on its first 3 global batches (the same events through sg_submit and sg_submit_ex), C5-ext, and
     the drop-in's operating point (dropin_line)."""
@@ -532,9 +549,11 @@ def config_lines(dev, c4=None):
                       "resources": w.n_res})
             if ext_on:
                 r["note"] = EXT_NOTE
-            rows.append(r)
             eng.close()
             torch.cuda.empty_cache()
+            if not ext_on and cpu_events:
+                r["cpu_baseline"] = config_cpu_baseline(w, ev, cpu_events)
+            rows.append(r)
         w.close()
     if c4 is not None:
         rows.append(dropin_line(dev, *c4))
