@@ -154,7 +154,8 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  uint32_t nblk, uint32_t pq_ok, uint32_t pq_wide, uint32_t* __restrict__ aux,
                                                  uint32_t* __restrict__ ashort, uint64_t* __restrict__ along,
                                                  uint64_t* __restrict__ amulti, uint32_t* __restrict__ mixc,
-                                                 uint32_t* __restrict__ mix, uint32_t mix_cap) {
+                                                 uint32_t* __restrict__ mix, uint32_t mix_cap,
+                                                 uint32_t* __restrict__ mixlen) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && (p.n_param == 0 || mixp) && sg.len > lane_max &&
                           !lane_only && !p.multi;
         if (coop && p.n_param) mixk = sg.len > pq_wide ? 2u : 1u;
+        if (mixk == 2 && mixlen) atomicAdd(mixlen, sg.len);  // (pvalue.hip's scratch bound)
         uint32_t bin;
         if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS)))
             bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
@@ -3091,11 +3093,12 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
-                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, hipStream_t st) {
+                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
+                          hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap, mixlen);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

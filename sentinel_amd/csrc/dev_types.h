@@ -238,6 +238,43 @@ struct Seg {
     uint32_t bin;    // BIN_* (| SEG_AUXP)
 };
 #define SEG_AUXP 0x80u  // Seg.bin: the segment's origin / context nodes are updated by the aux.hip post-pass
+#define SEG_PV 0x40u    // Seg.bin: pvalue.hip decided the segment's param checks (k_pq's pre pass leaves it)
+
+// pvalue.hip: the value-parallel pre pass of long XF_MIX segments
+// per listed segment (the wide XF_MIX list): what the pre pass found
+struct PvSeg {
+    uint32_t ok;        // decided here (else k_pq's pre pass)
+    uint32_t n;         // accesses
+    uint32_t off;       // first access in the dense arrays
+    uint32_t mid;       // rule map
+    uint32_t rk;        // the checked rule's index in the program
+    uint32_t pad[3];
+};
+
+struct PvBuf {          // dense per-access arrays (capacity >= the listed segments' events)
+    uint64_t* key;
+    uint32_t* pos;      // segment-relative position
+    int32_t* dt;
+    uint32_t* acq;      // acquire | (token count of the value) << 16 is not enough: tc in its own array
+    int32_t* tc;
+    uint32_t* seg;      // listed segment index
+    uint32_t* gid;      // sort keys (group = hash slot) -> after the sort: sorted keys
+    uint32_t* idx;      // sort values -> after the sort: accesses in (group, order) order
+    uint32_t* gid2;
+    uint32_t* idx2;
+    int32_t* prev;      // previous access of the value (dense index), PV_NONE
+    int32_t* w;         // first access of a value: its recency rank at the start (PV_INF: absent); others -1
+    int32_t* sprev;     // prev sorted per block
+    int32_t* sw;        // w sorted per block
+    int32_t* fslot;     // first access: the value's slot in the map (any liveness), -1
+    uint8_t* hit;
+    uint8_t* keep;      // last access of a value: the value stays in the map
+    int64_t* flast;     // last access of a value: its final (lastAddTime, tokens)
+    int32_t* ftok;
+    unsigned long long* htab;  // 2 slots per access: the per-segment hash tables of values
+};
+
+
 
 // ---- token server (cluster.hip): ClusterMetric per flowId + the namespace GlobalRequestLimiter
 enum { CF_PASS = 0, CF_BLOCK, CF_PASS_REQ, CF_BLOCK_REQ, CF_OCC_PASS, CF_OCC_BLOCK, CF_WAITING, CF_N };  // ClusterFlowEvent

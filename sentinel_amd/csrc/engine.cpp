@@ -48,7 +48,8 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
 hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n, const Prog* prog, const uint32_t* prio,
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
-                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, hipStream_t st);
+                          uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
+                          hipStream_t st);
 // aux.hip
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
                       const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
@@ -62,6 +63,14 @@ hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, cons
                           uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
                               uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
+hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                     const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
+                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
+                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                                 uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                     hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                     uint32_t tile);
 hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                          const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
                          const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st);
@@ -561,6 +570,12 @@ struct sg_engine {
     uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
     bool mix_on = true;         // XF_MIX programs (SG_MIX=0: every param + flow / degrade resource one lane)
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
+    bool pv_on = false;         // SG_PV=1: the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
+    PvBuf pvb{};                // its scratch (decide stage only: one set)
+    uint64_t pv_cap = 0;
+    PvSeg* d_pvseg = nullptr;
+    uint64_t pvseg_cap = 0;
+    uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr;
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -1153,6 +1168,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
+    if (const char* v = std::getenv("SG_PV")) e->pv_on = v[0] != '0';
     if (const char* v = std::getenv("SG_PQ_WIDE")) e->pq_wide = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_SKIP_MIN")) {
         e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
@@ -1231,6 +1247,8 @@ extern "C" int sgx_param_pool(sg_engine* e, unsigned long long* out) {
     return 0;
 }
 
+static void free_pv(sg_engine* e);
+
 int sg_engine_destroy(sg_engine* e) {
     if (!e) return SG_OK;
     (void)hipSetDevice(e->device);
@@ -1240,6 +1258,8 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
     dfree(e->d_pool_next);
     if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
+    free_pv(e);
+    dfree(e->d_pvseg); dfree(e->d_pvtot);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
@@ -1844,6 +1864,44 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
     return SG_OK;
 }
 
+// pvalue.hip's scratch for up to cap accesses of up to m listed segments (the decide stage's: a batch in flight may
+// still use the old arrays, so the stream drains first)
+static void free_pv(sg_engine* e) {
+    PvBuf& B = e->pvb;
+    dfree(B.key); dfree(B.pos); dfree(B.dt); dfree(B.acq); dfree(B.tc); dfree(B.seg); dfree(B.gid); dfree(B.idx);
+    dfree(B.gid2); dfree(B.idx2); dfree(B.prev); dfree(B.w); dfree(B.sprev); dfree(B.sw); dfree(B.fslot); dfree(B.hit);
+    dfree(B.keep); dfree(B.flast); dfree(B.ftok); dfree(B.htab); dfree(e->d_pvhist); dfree(e->d_pvpart);
+    B = PvBuf{};
+    e->d_pvhist = e->d_pvpart = nullptr;
+    e->pv_cap = 0;
+}
+static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
+    if (m > e->pvseg_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        dfree(e->d_pvseg);
+        e->pvseg_cap = std::max<uint64_t>(m, 1024);
+        HIPCHK(hipMalloc(&e->d_pvseg, e->pvseg_cap * sizeof(PvSeg)));
+    }
+    if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
+    if (cap <= e->pv_cap) return SG_OK;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    free_pv(e);
+    const uint64_t c = std::max<uint64_t>(cap + cap / 8, 1u << 16);
+    PvBuf& B = e->pvb;
+    HIPCHK(hipMalloc(&B.key, c * 8)); HIPCHK(hipMalloc(&B.pos, c * 4)); HIPCHK(hipMalloc(&B.dt, c * 4));
+    HIPCHK(hipMalloc(&B.acq, c * 4)); HIPCHK(hipMalloc(&B.tc, c * 4)); HIPCHK(hipMalloc(&B.seg, c * 4));
+    HIPCHK(hipMalloc(&B.gid, c * 4)); HIPCHK(hipMalloc(&B.idx, c * 4)); HIPCHK(hipMalloc(&B.gid2, c * 4));
+    HIPCHK(hipMalloc(&B.idx2, c * 4)); HIPCHK(hipMalloc(&B.prev, c * 4)); HIPCHK(hipMalloc(&B.w, c * 4));
+    HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
+    HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
+    HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
+    const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
+    HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
+    HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
+    e->pv_cap = c;
+    return SG_OK;
+}
+
 // The XF_MIX segment lists of slot B for up to mb segments (narrow, then wide at mix_cap)
 static int ensure_mix(sg_engine::BatchSlot& B, uint64_t mb) {
     if (mb > B.mix_cap) {
@@ -2004,10 +2062,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
                           B.d_ashort, B.d_along, B.d_amulti, e->d_bsmall + 6, e->has_mix ? B.d_mix : nullptr,
-                          (uint32_t)B.mix_cap, gs));
+                          (uint32_t)B.mix_cap, e->d_bsmall + 72, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
-    uint32_t head[8 + N_BINS + 1];  // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..] bin offsets
+    // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..8+N_BINS] bin offsets [72] wide XF_MIX events
+    uint32_t head[73];
+    static_assert(8 + N_BINS + 1 <= 72, "head layout");
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
     HIPCHK(hipEventRecord(B.ev[1], gs));
     HIPCHK(hipStreamSynchronize(gs));
@@ -2120,6 +2180,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // XF_MIX segments of the cooperative bins: their param checks first (k_pq pre pass), the owners then decide
     // the flow / degrade chain on them
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
+    if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
+        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
+        HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
+                         e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, st, launch_radix_hist,
+                         launch_radix_scatter, launch_scan, radix_tile()));
+    }
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
                              e->d_dec, e->d_bsmall + 0, st));

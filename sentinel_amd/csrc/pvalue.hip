@@ -1,0 +1,633 @@
+// pvalue.hip -- ParamFlowSlot's pre pass for the long segments of mixed resources (XF_MIX), value-parallel.
+//
+// k_pq decides a segment a tile at a time in one workgroup, so one hot resource's argument accesses run in series
+// (C6: 2M accesses of one resource per batch).  For a resource with one QPS token-bucket rule
+// (ParamFlowChecker.passDefaultLocalCheck, ParamFlowChecker.java:121-196) the verdict of an access depends only on
+// the earlier accesses of the same value -- and on LRU residency in the rule's CacheMap (ParameterMetric.java:37-39,
+// SURVEY Q13), whose closed form is the LRU stack distance: with prev(j) the previous access of access j's value,
+//     j hits  <=>  D(j) = #{k in (prev(j), j) : prev(k) < prev(j)} < cap
+// (the distinct values accessed since; DESIGN.md §9.1 has the derivation and the check against an exact LRU), and a
+// first access of a value that was live at the segment start with recency rank r hits iff
+//     r + #{first accesses k < j of values ranked below r or absent} < cap.
+// So the pass runs over all long mixed segments of the batch at once:
+//   prep     one workgroup per segment: eligibility, the accesses counted (the checks before any map access --
+//            token count 0, acquire above maxCount -- decided here), the map's ring prefix counts;
+//   fill     accesses in order into dense arrays, each value's group id from a per-segment hash table;
+//   sort     the (group id, access) pairs, stable radix (kernels.hip): each value's accesses contiguous, in order;
+//   prev     previous access of the same value; the first access probes the map (slot, recency rank, state);
+//   blocks   prev / rank values sorted per 256-access block, for counts with an early exit at cap;
+//   resid    hit / miss of every access;
+//   walk     one lane per value through passDefaultLocalCheck (a miss re-inserts the value with a full bucket);
+//            blocked ENTRYs get their word and RF_PBLK, exactly as k_pq's pre pass;
+//   commit   one workgroup per segment: the map after the segment -- the cap most recent values (accessed ones by
+//            last access, then untouched live ones in their old order) with fresh stamps, reused or new slots.
+// Segments that are not eligible (more than one checked rule, a throttle, lists) keep the k_pq pre pass.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "chain.h"
+#include "pmap.h"
+
+using namespace sg;
+
+#define PV_B 256u          // block of accesses with sorted prev / rank copies
+#define PV_INF 0x7FFFFFFF  // rank of a value absent at the segment start
+#define PV_NONE (-1)
+
+__device__ __forceinline__ uint32_t pv_word(const PMap& m, int64_t s) {
+    return (uint32_t)(((uint64_t)s & (uint64_t)((1ull << m.rb_log2) - 1)) >> 6);
+}
+// recency rank at the start (live keys more recent) of a live stamp, from the ring and its per-word prefix counts
+__device__ __forceinline__ int32_t pv_rank(const PMap& m, const uint64_t* bm, const uint32_t* pre, int64_t s) {
+    const uint64_t p = (uint64_t)s & (uint64_t)((1ull << m.rb_log2) - 1);
+    const uint32_t below = pre[p >> 6] + (uint32_t)__popcll(bm[p >> 6] & ((1ull << (p & 63)) - 1ull));
+    return (int32_t)m.live - 1 - (int32_t)below;
+}
+
+// the program's one checked param rule (QPS DefaultController behaviour) and no other checked rule; -1: not eligible
+__device__ __forceinline__ int pv_rule(const DevState& S, const Prog& pg) {
+    int k1 = -1;
+    for (int k = 0; k < pg.n_param; ++k) {
+        const DRule& r = S.rules[pg.rule_off + k];
+        if (r.behavior == PB_INIT_ONLY) continue;
+        if (k1 >= 0 || r.param_idx != 0 || r.grade != SG_FLOW_GRADE_QPS || r.behavior != SG_CONTROL_BEHAVIOR_DEFAULT)
+            return -1;
+        k1 = k;
+    }
+    return k1;
+}
+
+// the value's token count (a hot item's, else the rule's)
+__device__ __forceinline__ int32_t pv_tc(const DevState& S, const DRule& r, uint64_t key) {
+    for (uint32_t i = 0; i < r.hot_n; ++i) {
+        const DHot h = S.hot[r.hot_off + i];
+        if (h.key == key) return h.count;
+    }
+    return r.token_count;
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t pv_scan(uint32_t v, uint32_t* red, uint32_t* tot) {  // block exclusive scan
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    if (l == 63) red[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint32_t c = red[k];
+        if ((uint32_t)k < w) pre += c;
+        t += c;
+    }
+    __syncthreads();
+    *tot = t;
+    return pre + x - v;
+}
+
+// ---- prep: one workgroup per listed segment
+__global__ __launch_bounds__(256) void k_pv_prep(SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
+                                                 Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                 uint32_t m, DevState S, DevCfg cfg, PvSeg* __restrict__ pv,
+                                                 uint32_t* __restrict__ dec) {
+    __shared__ uint32_t red[4];
+    __shared__ uint32_t okf;
+    const uint32_t i = blockIdx.x, tid = threadIdx.x;
+    if (i >= m) return;
+    const Seg sg = segs[list[i]];
+    const Prog pg = S.prog[sg.res];
+    const int k1 = pv_rule(S, pg);
+    if (tid == 0) {
+        // eligible: one checked rule, its map within the commit's LDS (<= PQ_MAX_CAP), no argument lists, a chain
+        uint32_t ok = k1 >= 0 && !(S.prio && (S.prio[sg.res] & PM_ARGL)) && (S.info[sg.res].flags & NI_CHAIN);
+        if (ok && S.pmap[S.rules[pg.rule_off + k1].pmap].cap > PQ_MAX_CAP) ok = 0;
+        okf = ok;
+    }
+    __syncthreads();
+    if (!okf) {
+        if (tid == 0) { PvSeg z{}; z.ok = 0; pv[i] = z; }
+        return;
+    }
+    const DRule r = S.rules[pg.rule_off + k1];
+    uint32_t cnt = 0;
+    for (uint32_t p = tid; p < sg.len; p += 256) {
+        const SEv e = recs[sg.start + p];
+        if (e.kind != SG_EV_ENTRY || !(e.flags & SG_F_HAS_ARG)) continue;
+        const uint64_t key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
+        const int32_t tc = pv_tc(S, r, key);
+        if (tc == 0 || (int32_t)e.cnt > j_iadd(tc, r.burst)) {  // blocked before any map access
+            dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
+            recs[sg.start + p].flags = (uint8_t)(e.flags | RF_PBLK);
+            continue;
+        }
+        ++cnt;
+    }
+    uint32_t tot;
+    (void)pv_scan<4>(cnt, red, &tot);
+    // the map's per-word live-stamp prefix counts in stamp order from thr (ppre: free scratch of this map here)
+    const PMap mp = S.pmap[r.pmap];
+    const uint32_t W = 1u << (mp.rb_log2 - 6), w0 = pv_word(mp, mp.thr);
+    const uint32_t per = (W + 255) / 256, l0 = tid * per;
+    uint32_t c = 0;
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) c += (uint32_t)__popcll(S.pbm[mp.bm + ((w0 + l0 + u) & (W - 1))]);
+    uint32_t t2;
+    uint32_t run = pv_scan<4>(c, red, &t2);
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) {
+            const uint32_t w = (w0 + l0 + u) & (W - 1);
+            S.ppre[mp.bm + w] = run;
+            run += (uint32_t)__popcll(S.pbm[mp.bm + w]);
+        }
+    if (tid == 0) {
+        PvSeg o{};
+        o.ok = 1; o.n = tot; o.off = 0; o.mid = r.pmap; o.rk = (uint32_t)k1;
+        pv[i] = o;
+        segs[list[i]].bin = sg.bin | SEG_PV;  // (k_pq's pre pass leaves it)
+    }
+}
+
+// dense offsets of the listed segments' accesses (one block; m <= a few thousand); tot[0] = all accesses
+__global__ __launch_bounds__(256) void k_pv_offsets(PvSeg* __restrict__ pv, uint32_t m, uint32_t* __restrict__ tot) {
+    __shared__ uint32_t red[4];
+    uint32_t base = 0;
+    for (uint32_t c = 0; c < m; c += 256) {
+        const uint32_t i = c + threadIdx.x;
+        const uint32_t v = (i < m && pv[i].ok) ? pv[i].n : 0u;
+        uint32_t t;
+        const uint32_t o = pv_scan<4>(v, red, &t);
+        if (i < m) pv[i].off = base + o;
+        base += t;
+    }
+    if (threadIdx.x == 0) *tot = base;
+}
+
+// ---- fill: one workgroup per listed segment: accesses in order, group ids from the segment's hash table
+__global__ __launch_bounds__(256) void k_pv_fill(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
+                                                 const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                 uint32_t m, DevState S, DevCfg cfg, const PvSeg* __restrict__ pv,
+                                                 PvBuf B) {
+    __shared__ uint32_t red[4];
+    const uint32_t i = blockIdx.x, tid = threadIdx.x;
+    if (i >= m) return;
+    const PvSeg ps = pv[i];
+    if (!ps.ok) return;
+    const Seg sg = segs[list[i]];
+    const Prog pg = S.prog[sg.res];
+    const DRule r = S.rules[pg.rule_off + ps.rk];
+    const uint64_t H = 2ull * ps.n;  // table slots of this segment
+    unsigned long long* tab = B.htab + 2ull * ps.off;
+    for (uint64_t s = tid; s < H; s += 256) tab[s] = PK_EMPTY;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t c = 0; c < sg.len; c += 256) {  // (uniform trip count)
+        const uint32_t p = c + tid;
+        bool take = false;
+        uint64_t key = 0;
+        int32_t tc = 0;
+        SEv e;
+        if (p < sg.len) {
+            e = recs[sg.start + p];
+            if (e.kind == SG_EV_ENTRY && (e.flags & SG_F_HAS_ARG) && !(e.flags & RF_PBLK)) {
+                key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
+                tc = pv_tc(S, r, key);
+                take = true;
+            }
+        }
+        uint32_t t;
+        const uint32_t o = pv_scan<4>(take ? 1u : 0u, red, &t);
+        if (take) {
+            const uint32_t g = ps.off + base + o;
+            B.key[g] = key;
+            B.pos[g] = p;
+            B.dt[g] = e.dt;
+            B.acq[g] = e.cnt;
+            B.tc[g] = tc;
+            B.seg[g] = i;
+            B.prev[g] = PV_NONE;
+            B.w[g] = -1;
+            B.fslot[g] = -1;
+            B.keep[g] = 0;
+            // the value's slot in the segment's table: its group id
+            uint64_t h = mix64(key ^ 0x5BD1E9955BD1E995ull) % H;
+            for (;;) {
+                unsigned long long cur = tab[h];
+                if (cur == key) break;
+                if (cur == PK_EMPTY) {
+                    const unsigned long long prv = atomicCAS(&tab[h], (unsigned long long)PK_EMPTY, (unsigned long long)key);
+                    if (prv == PK_EMPTY || prv == key) break;
+                }
+                h = h + 1 == H ? 0 : h + 1;
+            }
+            B.gid[g] = (uint32_t)(2ull * ps.off + h);
+            B.idx[g] = g;
+        }
+        base += t;
+    }
+}
+
+// padding of the sort arrays beyond the accesses: [tot, cap) sorts last
+__global__ void k_pv_pad(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < cap && g >= *tot) { B.gid[g] = 0xFFFFFFFFu; B.idx[g] = g; }
+}
+
+// ---- prev / first accesses (sorted order: after the sort B.gid / B.idx hold the sorted keys / accesses)
+__global__ void k_pv_prev(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *tot) return;
+    const uint32_t g = B.idx[q], gd = B.gid[q];
+    const bool first = q == 0 || B.gid[q - 1] != gd;
+    if (!first) { B.prev[g] = (int32_t)B.idx[q - 1]; return; }
+    // the value's first access of the segment: its slot in the map, its rank (if live), its state
+    const PvSeg ps = pv[B.seg[g]];
+    const PMap mp = S.pmap[ps.mid];
+    const uint64_t key = B.key[g];
+    uint32_t b1, b2;
+    pm_buckets(mp.nb, key, b1, b2);
+    const PBucket* BK = S.pbkt + mp.base;
+    int32_t slot = -1;
+    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b2].key[j] == key) slot = (int32_t)(b2 * PM_BKT + j);
+    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b1].key[j] == key) slot = (int32_t)(b1 * PM_BKT + j);
+    B.fslot[g] = slot;
+    int32_t w = PV_INF;
+    if (slot >= 0) {
+        const int64_t s = BK[slot / PM_BKT].stamp[slot % PM_BKT];
+        if (pm_live(mp, S.pbm + mp.bm, s)) {
+            w = pv_rank(mp, S.pbm + mp.bm, S.ppre + mp.bm, s);
+            const PData d = S.pdat[mp.base * PM_BKT + slot];
+            B.flast[g] = d.v0;
+            B.ftok[g] = d.v1;
+        }
+    }
+    B.w[g] = w;
+}
+
+// ---- blocks: prev and rank values sorted within each 256-access block (bitonic in LDS)
+__global__ __launch_bounds__(256) void k_pv_blocks(PvBuf B, const uint32_t* __restrict__ tot) {
+    __shared__ int32_t a[PV_B], b[PV_B];
+    const uint32_t n = *tot, base = blockIdx.x * PV_B, t = threadIdx.x;
+    if (base >= n) return;
+    a[t] = base + t < n ? B.prev[base + t] : 0x7FFFFFFF;
+    b[t] = base + t < n ? B.w[base + t] : 0x7FFFFFFF;
+    __syncthreads();
+    for (uint32_t k = 2; k <= PV_B; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t x = t ^ j;
+            if (x > t) {
+                const bool up = (t & k) == 0;
+                if ((a[t] > a[x]) == up) { const int32_t v = a[t]; a[t] = a[x]; a[x] = v; }
+                if ((b[t] > b[x]) == up) { const int32_t v = b[t]; b[t] = b[x]; b[x] = v; }
+            }
+            __syncthreads();
+        }
+    if (base + t < n) { B.sprev[base + t] = a[t]; B.sw[base + t] = b[t]; }
+}
+
+// #{k in (lo, hi) : prev[k] < v}, stopping once it reaches lim
+__device__ int32_t pv_count_lt(const PvBuf& B, int64_t lo, int64_t hi, int32_t v, int32_t lim) {
+    int32_t c = 0;
+    int64_t k = lo + 1;
+    while (k < hi && (k % PV_B) != 0) { c += B.prev[k] < v; ++k; }
+    if (c >= lim) return c;
+    while (k + PV_B <= hi) {
+        const int32_t* s = B.sprev + k;
+        uint32_t l = 0, h = PV_B;  // first element >= v
+        while (l < h) { const uint32_t md = (l + h) >> 1; if (s[md] < v) l = md + 1; else h = md; }
+        c += (int32_t)l;
+        k += PV_B;
+        if (c >= lim) return c;
+    }
+    while (k < hi) { c += B.prev[k] < v; ++k; }
+    return c;
+}
+// #{k in [lo, hi) : w[k] > r}, stopping once it reaches lim
+__device__ int32_t pv_count_gt(const PvBuf& B, int64_t lo, int64_t hi, int32_t r, int32_t lim) {
+    int32_t c = 0;
+    int64_t k = lo;
+    while (k < hi && (k % PV_B) != 0) { c += B.w[k] > r; ++k; }
+    if (c >= lim) return c;
+    while (k + PV_B <= hi) {
+        const int32_t* s = B.sw + k;
+        uint32_t l = 0, h = PV_B;  // first element > r
+        while (l < h) { const uint32_t md = (l + h) >> 1; if (s[md] <= r) l = md + 1; else h = md; }
+        c += (int32_t)(PV_B - l);
+        k += PV_B;
+        if (c >= lim) return c;
+    }
+    while (k < hi) { c += B.w[k] > r; ++k; }
+    return c;
+}
+
+// ---- residency of every access; for a value's last access, whether the value stays in the map
+__global__ void k_pv_resid(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= *tot) return;
+    const PvSeg ps = pv[B.seg[g]];
+    const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
+    const int32_t p = B.prev[g];
+    bool hit;
+    if (p >= 0) hit = (int64_t)g - p - 1 < cap || pv_count_lt(B, p, g, p, cap) < cap;
+    else {
+        const int32_t r = B.w[g];
+        hit = r != PV_INF && pv_count_gt(B, ps.off, g, r, cap - r) < cap - r;
+    }
+    B.hit[g] = hit ? 1 : 0;
+}
+
+// ---- walk: one lane per value (its accesses contiguous in sorted order)
+__global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                          PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S,
+                          int64_t t0, uint32_t* __restrict__ dec) {
+    const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = *tot;
+    if (q0 >= n) return;
+    const uint32_t gd = B.gid[q0];
+    if (q0 > 0 && B.gid[q0 - 1] == gd) return;  // not a group start
+    const uint32_t g0 = B.idx[q0];
+    const uint32_t si = B.seg[g0];
+    const PvSeg ps = pv[si];
+    const Seg sg = segs[list[si]];
+    const Prog pg = S.prog[sg.res];
+    const DRule r = S.rules[pg.rule_off + ps.rk];
+    const int64_t D = r.duration_sec * 1000;
+    const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
+    const uint32_t blk = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
+    int64_t last = B.flast[g0];  // (valid when the first access hits: the value was live)
+    int32_t tok = B.ftok[g0];
+    uint32_t g = g0;
+    for (uint32_t q = q0; q < n && B.gid[q] == gd; ++q) {
+        g = B.idx[q];
+        const int64_t t = t0 + B.dt[g];
+        const int32_t a = (int32_t)B.acq[g], tc = B.tc[g], maxc = j_iadd(tc, r.burst);
+        bool pass;
+        if (!B.hit[g]) {  // inserted: timeCounters / tokenCounters.putIfAbsent
+            last = t;
+            tok = j_iadd(maxc, -a);
+            pass = true;
+        } else {
+            const int64_t pt = t - last;
+            if (pt > D) {
+                const int32_t add = (int32_t)((pt * (int64_t)tc) / D);
+                const int32_t sum = j_iadd(tok, add);
+                const int32_t nq = sum > maxc ? j_iadd(maxc, -a) : j_iadd(sum, -a);
+                pass = nq >= 0;
+                if (pass) { tok = nq; last = t; }
+            } else {
+                pass = j_iadd(tok, -a) >= 0;
+                if (pass) tok = j_iadd(tok, -a);
+            }
+        }
+        if (!pass) {
+            const uint32_t p = B.pos[g];
+            dec[sg.start + p] = blk;
+            recs[sg.start + p].flags = (uint8_t)(recs[sg.start + p].flags | RF_PBLK);
+        }
+    }
+    // the value's last access g: it stays iff fewer than cap distinct values are accessed after it
+    const int64_t end = (int64_t)ps.off + ps.n;
+    B.keep[g] = pv_count_lt(B, g, end, (int32_t)g, cap) < cap ? 1 : 0;
+    B.flast[g] = last;
+    B.ftok[g] = tok;
+    B.fslot[g] = B.fslot[g0];  // (the value's slot, carried to its last access for the commit)
+}
+
+// ---- commit: one workgroup per segment: the map after the segment
+#define PV_RW 512u   // ring words (cap <= PQ_MAX_CAP)
+#define PV_CW 256u   // claim words (slots <= map_buckets(PQ_MAX_CAP) * 8)
+__global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __restrict__ pv, uint32_t m, DevState S,
+                                                    uint32_t* __restrict__ bflags) {
+    __shared__ uint64_t ring[PV_RW], touch[PV_RW];
+    __shared__ uint32_t pre[PV_RW];
+    __shared__ unsigned long long claim[PV_CW];
+    __shared__ uint32_t red[16];
+    __shared__ uint32_t nfail;
+    __shared__ uint32_t fail[64];
+    const uint32_t i = blockIdx.x, tid = threadIdx.x;
+    if (i >= m) return;
+    const PvSeg ps = pv[i];
+    if (!ps.ok) return;
+    PMap mp = S.pmap[ps.mid];
+    const uint32_t W = 1u << (mp.rb_log2 - 6);
+    const int32_t cap = (int32_t)mp.cap;
+    PBucket* BK = S.pbkt + mp.base;
+    PData* DT = S.pdat + mp.base * PM_BKT;
+    const uint32_t nslot = mp.nb * PM_BKT;
+    for (uint32_t w = tid; w < W; w += 1024) { ring[w] = S.pbm[mp.bm + w]; touch[w] = 0; }
+    for (uint32_t w = tid; w < PV_CW; w += 1024) claim[w] = 0;
+    if (tid == 0) nfail = 0;
+    __syncthreads();
+    // (1) live stamps of values accessed in the segment; the number of distinct values accessed (G) and kept
+    uint32_t ng = 0;
+    for (uint32_t k = tid; k < ps.n; k += 1024) {
+        const uint32_t g = ps.off + k;
+        if (B.w[g] >= 0) {  // a value's first access
+            ++ng;
+            const int32_t sl = B.fslot[g];
+            if (sl >= 0 && B.w[g] != PV_INF) {
+                const int64_t s = BK[sl / PM_BKT].stamp[sl % PM_BKT];
+                const uint64_t p = (uint64_t)s & (uint64_t)((1ull << mp.rb_log2) - 1);
+                atomicOr(reinterpret_cast<unsigned long long*>(&touch[p >> 6]), 1ull << (p & 63));
+            }
+        }
+    }
+    uint32_t G;
+    (void)pv_scan<16>(ng, red, &G);
+    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay
+    // (2) untouched live values: the (cap - KA) most recent stay; prefix counts of untouched stamps from thr
+    const uint32_t w0 = pv_word(mp, mp.thr);
+    {
+        const uint32_t per = (W + 1023) / 1024, l0 = tid * per;
+        uint32_t c = 0;
+        for (uint32_t u = 0; u < per; ++u)
+            if (l0 + u < W) c += (uint32_t)__popcll(ring[(w0 + l0 + u) & (W - 1)] & ~touch[(w0 + l0 + u) & (W - 1)]);
+        uint32_t tU;
+        uint32_t run = pv_scan<16>(c, red, &tU);
+        for (uint32_t u = 0; u < per; ++u)
+            if (l0 + u < W) {
+                const uint32_t w = (w0 + l0 + u) & (W - 1);
+                pre[w] = run;
+                run += (uint32_t)__popcll(ring[w] & ~touch[w]);
+            }
+        if (tid == 0) red[15] = tU;
+    }
+    __syncthreads();
+    const uint32_t U = red[15];
+    const uint32_t KU = U < (uint32_t)cap - KA ? U : (uint32_t)cap - KA;  // untouched values that stay
+    const int64_t base = mp.clock;                                          // new stamps [base, base + KU + KA)
+    // (3) untouched values: new stamps in their old order, claimed slots; the others die with the old stamps
+    for (uint32_t sl = tid; sl < nslot; sl += 1024) {
+        const uint64_t key = BK[sl / PM_BKT].key[sl % PM_BKT];
+        if (key == PK_EMPTY) continue;
+        const int64_t s = BK[sl / PM_BKT].stamp[sl % PM_BKT];
+        if (!(s >= mp.thr && s < mp.clock)) continue;
+        const uint64_t p = (uint64_t)s & (uint64_t)((1ull << mp.rb_log2) - 1);
+        const uint64_t bit = 1ull << (p & 63);
+        if (!(ring[p >> 6] & bit) || (touch[p >> 6] & bit)) continue;
+        const uint32_t below = pre[p >> 6] + (uint32_t)__popcll(ring[p >> 6] & ~touch[p >> 6] & (bit - 1ull));
+        if (below + KU < U) continue;  // not among the KU most recent untouched
+        BK[sl / PM_BKT].stamp[sl % PM_BKT] = base + (int64_t)(below - (U - KU));
+        atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
+    }
+    __syncthreads();
+    // (4) accessed values that stay, in last-access order: new stamps above; their slot reused or claimed
+    uint32_t kbase = 0;
+    for (uint32_t c = 0; c < ps.n; c += 1024) {  // (uniform)
+        const uint32_t k = c + tid;
+        const uint32_t g = ps.off + k;
+        const bool kp = k < ps.n && B.keep[g];
+        uint32_t t;
+        const uint32_t o = pv_scan<16>(kp ? 1u : 0u, red, &t);
+        if (kp) {
+            const uint32_t rank = kbase + o;  // among the kept, by last access
+            const int64_t s = base + (int64_t)KU + (int64_t)rank;
+            PData d;
+            d.v0 = B.flast[g]; d.v1 = B.ftok[g]; d.pad = 0;
+            const int32_t sl = B.fslot[g];
+            if (sl >= 0) {
+                BK[sl / PM_BKT].stamp[sl % PM_BKT] = s;
+                DT[sl] = d;
+                atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
+            } else {
+                B.fslot[g] = -2 - (int32_t)rank;  // placed below
+            }
+        }
+        kbase += t;
+    }
+    __syncthreads();
+    // (5) new values: a free slot (empty, or an old value's that did not stay) in either bucket
+    for (uint32_t c = 0; c < ps.n; c += 1024) {
+        const uint32_t k = c + tid;
+        const uint32_t g = ps.off + k;
+        if (k >= ps.n || !B.keep[g] || B.fslot[g] >= 0) continue;
+        const uint32_t rank = (uint32_t)(-2 - B.fslot[g]);
+        const uint64_t key = B.key[g];
+        const int64_t s = base + (int64_t)KU + (int64_t)rank;
+        uint32_t b1, b2;
+        pm_buckets(mp.nb, key, b1, b2);
+        int32_t got = -1;
+        for (int h = 0; h < 2 && got < 0; ++h) {
+            const uint32_t bb = h ? b2 : b1;
+            for (int j = 0; j < PM_BKT && got < 0; ++j) {
+                const uint32_t sl = bb * PM_BKT + j;
+                const unsigned long long o = atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
+                if (!(o & (1ull << (sl & 63)))) got = (int32_t)sl;
+            }
+        }
+        PData d;
+        d.v0 = B.flast[g]; d.v1 = B.ftok[g]; d.pad = 0;
+        if (got >= 0) {
+            BK[got / PM_BKT].key[got % PM_BKT] = key;
+            BK[got / PM_BKT].stamp[got % PM_BKT] = s;
+            DT[got] = d;
+        } else {
+            const uint32_t f = atomicAdd(&nfail, 1u);
+            if (f < 64) fail[f] = g;
+            else atomicOr(bflags, BF_PTAB_FULL);
+        }
+    }
+    __syncthreads();
+    // (6) the rare value whose two buckets are taken: a displacement walk (one lane), moving claimed values to their
+    // other bucket; slots claimed by nobody are free
+    if (tid == 0) {
+        const uint32_t nf = nfail < 64 ? nfail : 64;
+        for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t g = fail[f];
+            uint64_t ck = B.key[g];
+            int64_t cs = base + (int64_t)KU + (int64_t)(uint32_t)(-2 - B.fslot[g]);
+            PData cd;
+            cd.v0 = B.flast[g]; cd.v1 = B.ftok[g]; cd.pad = 0;
+            uint32_t b1, b2;
+            pm_buckets(mp.nb, ck, b1, b2);
+            uint32_t bb = b1;
+            bool done = false;
+            for (int step = 0; step < 512 && !done; ++step) {
+                for (int j = 0; j < PM_BKT; ++j) {
+                    const uint32_t sl = bb * PM_BKT + j;
+                    if (!((claim[sl >> 6] >> (sl & 63)) & 1ull)) {
+                        claim[sl >> 6] |= 1ull << (sl & 63);
+                        BK[bb].key[j] = ck; BK[bb].stamp[j] = cs; DT[sl] = cd;
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                const int j = (int)((cs + step * 5) & 7);  // swap with a claimed value, carry it to its other bucket
+                const uint32_t sl = bb * PM_BKT + j;
+                const uint64_t nk = BK[bb].key[j];
+                const int64_t ns = BK[bb].stamp[j];
+                const PData nd = DT[sl];
+                BK[bb].key[j] = ck; BK[bb].stamp[j] = cs; DT[sl] = cd;
+                ck = nk; cs = ns; cd = nd;
+                bb = pm_alt(mp.nb, ck, bb);
+            }
+            if (!done) atomicOr(bflags, BF_PTAB_FULL);
+        }
+    }
+    __syncthreads();
+    // (7) the ring holds exactly the new stamps; header
+    const uint32_t K = KU + KA;
+    for (uint32_t w = tid; w < W; w += 1024) ring[w] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < K; k += 1024) {
+        const uint64_t p = (uint64_t)(base + (int64_t)k) & (uint64_t)((1ull << mp.rb_log2) - 1);
+        atomicOr(reinterpret_cast<unsigned long long*>(&ring[p >> 6]), 1ull << (p & 63));
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < W; w += 1024) S.pbm[mp.bm + w] = ring[w];
+    if (tid == 0) {
+        PMap* h = &S.pmap[ps.mid];
+        h->clock = base + (int64_t)K;
+        h->thr = base;
+        h->live = K;
+    }
+}
+
+namespace sg {
+// the value-parallel pre pass over the wide XF_MIX list (cap accesses at most); pv[] tells k_pq which segments
+// are done.  Scratch: PvBuf arrays of cap entries, htab 2 x cap, radix scratch (hist, part), tot (device word).
+hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                     const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
+                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
+                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                                 uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                     hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                     uint32_t tile) {
+    if (!m || !cap) return hipSuccess;
+    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, recs, vals, segs, list, m, S, cfg, pv, dec);
+    hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, tot);
+    hipLaunchKernelGGL(k_pv_fill, dim3(m), dim3(256), 0, st, recs, vals, segs, list, m, S, cfg, pv, B);
+    const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pv_pad, dim3(nb), dim3(256), 0, st, B, tot, cap);
+    // group ids < 2 x cap: stable LSD radix on 8-bit digits (each value's accesses stay in access order)
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < 2ull * cap) ++bits;
+    const int passes = (bits + 7) / 8;
+    const uint32_t nblocks = (cap + tile - 1) / tile;
+    uint32_t *kin = B.gid, *vin = B.idx, *kout = B.gid2, *vout = B.idx2;
+    for (int p = 0; p < passes; ++p) {
+        hipError_t e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
+        if (e == hipSuccess) e = scan(hist, hist, (uint64_t)nblocks << 8, part, nullptr, st);
+        if (e == hipSuccess) e = radix_scatter(kin, vin, cap, p * 8, hist, nblocks, kout, vout, nullptr, st);
+        if (e != hipSuccess) return e;
+        uint32_t* tk = kin; kin = kout; kout = tk;
+        uint32_t* tv = vin; vin = vout; vout = tv;
+    }
+    if (kin != B.gid) {  // sorted arrays back into gid / idx (an odd number of passes)
+        hipError_t e = hipMemcpyAsync(B.gid, kin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(B.idx, vin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
+    hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec);
+    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags);
+    return hipGetLastError();
+}
+} // namespace sg

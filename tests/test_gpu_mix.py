@@ -43,11 +43,14 @@ def _nodes(eng, orc, res):
         np.testing.assert_array_equal(g["minute"], o["minute"], err_msg="minute window of res %d" % r)
 
 
+@pytest.mark.parametrize("pv", ["0", "1"])
 @pytest.mark.parametrize("nval", [3_000, 300_000])
-def test_mix_c6_shapes(nval):
+def test_mix_c6_shapes(nval, pv, monkeypatch):
     # C6 (every resource: a QPS flow rule, a breaker, a QPS param rule on args[0]) at 3000 resources: the Zipf head
     # is a J8 / J16 segment (wide pre / post pass), the body J4 / J1 (narrow), the tail one lane each; few values
     # (maps never evict, hot values get blocked) and many (the maps churn)
+    # pv = 1: the long segments' param checks value-parallel (pvalue.hip), the maps rewritten after each segment
+    monkeypatch.setenv("SG_PV", pv)
     n_res = 3000
     w = T.Workload(6, seed=T.SEED_BASE + 60, n_res=n_res, n_entries=500_000, n_param_values=nval)
     ev = w.events
@@ -133,12 +136,14 @@ def _mix_rules(flow_count, thread_rule=False):
     return f, d, p
 
 
+@pytest.mark.parametrize("pv", ["0", "1"])
 @pytest.mark.parametrize("flow_count", [30, 1e5])
-def test_mix_stretches_and_thread_maps(flow_count):
+def test_mix_stretches_and_thread_maps(flow_count, pv, monkeypatch):
     # one long segment per batch (x0: frozen stretches, skipped spans, the Jacobi iteration with param blocks at a
     # low flow limit; open stretches at a high one), an exception-ratio breaker beside param blocks (x1: the
     # ratio's total counts them), a WarmUp stage, a THREAD-grade flow stage, a rate limiter (x5: the J4 owner);
     # EXIT references across batches; then THREAD-grade param rules read the thread-count maps
+    monkeypatch.setenv("SG_PV", pv)
     eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=22, status_ring_log2=24)
     orc = O.Oracle(max_slot_chain_size=0)
     for nm in NAMES:
