@@ -248,7 +248,9 @@ struct PvSeg {
     uint32_t off;       // first access in the dense arrays
     uint32_t mid;       // rule map
     uint32_t rk;        // the checked rule's index in the program
-    uint32_t pad[3];
+    uint32_t ch0;       // first extraction chunk
+    uint32_t nch;       // extraction chunks
+    uint32_t pad;
 };
 
 struct PvBuf {          // dense per-access arrays (capacity >= the listed segments' events)
@@ -272,6 +274,16 @@ struct PvBuf {          // dense per-access arrays (capacity >= the listed segme
     int64_t* flast;     // last access of a value: its final (lastAddTime, tokens)
     int32_t* ftok;
     unsigned long long* htab;  // 2 slots per access: the per-segment hash tables of values
+    // extraction chunks (PV_CH positions of one segment each): (listed segment, first position), accesses, offsets
+    uint2* chunk;
+    uint32_t* ccnt;
+    uint32_t* cof;
+    // the walk's inputs in sorted order: time, acquire | hit << 16, record index; misses per 256 sorted positions
+    int32_t* gdt;
+    uint32_t* gaw;
+    uint32_t* gpos;
+    uint32_t* mflag;
+    uint4* range;       // blocked stretches the walk jumped over: {first, end, decision word}; count in tot[2]
 };
 
 

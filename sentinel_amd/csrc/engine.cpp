@@ -65,7 +65,8 @@ hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S
                               uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
 hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                      const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
-                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
+                     hipStream_t st,
                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
@@ -576,6 +577,7 @@ struct sg_engine {
     PvSeg* d_pvseg = nullptr;
     uint64_t pvseg_cap = 0;
     uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr;
+    uint32_t pv_last_m = 0;     // listed segments of the last batch that ran it (diagnostics)
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
     // configuration (ClusterFlowRuleManager.FLOW_RULES / ClusterMetricStatistics roles)
@@ -1238,6 +1240,21 @@ extern "C" int sgx_read_aux_node(sg_engine* e, uint32_t res, uint32_t kind, uint
     }
     return 0;
 }
+// diagnostics export: the last batch's value-parallel pre pass (pvalue.hip), out = {listed segments it decided, accesses,
+// blocked stretches the walk jumped}
+extern "C" int sgx_pv_last(sg_engine* e, unsigned long long* out) {
+    if (!e || !out || drain(e) != SG_OK) return -1;
+    out[0] = out[1] = out[2] = 0;
+    if (!e->d_pvseg || !e->d_pvtot || !e->pv_last_m) return 0;
+    std::vector<PvSeg> v(e->pv_last_m);
+    uint32_t tot[4] = {0, 0, 0, 0};
+    if (hipMemcpy(v.data(), e->d_pvseg, v.size() * sizeof(PvSeg), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(tot, e->d_pvtot, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (const auto& s : v) out[0] += s.ok ? 1 : 0;
+    out[1] = tot[0];
+    out[2] = tot[2];
+    return 0;
+}
 // diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last layout, compactions}
 extern "C" int sgx_param_pool(sg_engine* e, unsigned long long* out) {
     if (!e || !out || drain(e) != SG_OK) return -1;
@@ -1870,7 +1887,8 @@ static void free_pv(sg_engine* e) {
     PvBuf& B = e->pvb;
     dfree(B.key); dfree(B.pos); dfree(B.dt); dfree(B.acq); dfree(B.tc); dfree(B.seg); dfree(B.gid); dfree(B.idx);
     dfree(B.gid2); dfree(B.idx2); dfree(B.prev); dfree(B.w); dfree(B.sprev); dfree(B.sw); dfree(B.fslot); dfree(B.hit);
-    dfree(B.keep); dfree(B.flast); dfree(B.ftok); dfree(B.htab); dfree(e->d_pvhist); dfree(e->d_pvpart);
+    dfree(B.keep); dfree(B.flast); dfree(B.ftok); dfree(B.htab); dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
+    dfree(B.gdt); dfree(B.gaw); dfree(B.gpos); dfree(B.mflag); dfree(B.range); dfree(e->d_pvhist); dfree(e->d_pvpart);
     B = PvBuf{};
     e->d_pvhist = e->d_pvpart = nullptr;
     e->pv_cap = 0;
@@ -1881,6 +1899,7 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
         dfree(e->d_pvseg);
         e->pvseg_cap = std::max<uint64_t>(m, 1024);
         HIPCHK(hipMalloc(&e->d_pvseg, e->pvseg_cap * sizeof(PvSeg)));
+        free_pv(e);  // (the chunk arrays are sized by pvseg_cap)
     }
     if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
     if (cap <= e->pv_cap) return SG_OK;
@@ -1895,6 +1914,11 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
     HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
     HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
     HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
+    // chunks: cap / PV_CH (4096) + one per segment; m <= pvseg_cap
+    const uint64_t nch = c / 4096 + e->pvseg_cap + 16;
+    HIPCHK(hipMalloc(&B.chunk, nch * 8)); HIPCHK(hipMalloc(&B.ccnt, nch * 4)); HIPCHK(hipMalloc(&B.cof, nch * 4 + 4));
+    HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
+    HIPCHK(hipMalloc(&B.mflag, (c / 256 + 1) * 4)); HIPCHK(hipMalloc(&B.range, c * 16));
     const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
     HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
     HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
@@ -2182,8 +2206,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
     if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
         if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
+        e->pv_last_m = n_mixw;
         HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
-                         e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, st, launch_radix_hist,
+                         e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
+                         (bflags & BF_ZERO_CNT) ? 0u : 1u, st, launch_radix_hist,
                          launch_radix_scatter, launch_scan, radix_tile()));
     }
     if (n_mix || n_mixw)

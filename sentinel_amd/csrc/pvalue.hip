@@ -89,11 +89,10 @@ __device__ __forceinline__ uint32_t pv_scan(uint32_t v, uint32_t* red, uint32_t*
     return pre + x - v;
 }
 
-// ---- prep: one workgroup per listed segment
-__global__ __launch_bounds__(256) void k_pv_prep(SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
-                                                 Seg* __restrict__ segs, const uint32_t* __restrict__ list,
-                                                 uint32_t m, DevState S, DevCfg cfg, PvSeg* __restrict__ pv,
-                                                 uint32_t* __restrict__ dec) {
+// ---- prep: one workgroup per listed segment: eligibility, the map's ring prefix counts, extraction chunks
+#define PV_CH 4096u  // positions per extraction chunk
+__global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
+                                                 DevState S, PvSeg* __restrict__ pv) {
     __shared__ uint32_t red[4];
     __shared__ uint32_t okf;
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
@@ -112,22 +111,7 @@ __global__ __launch_bounds__(256) void k_pv_prep(SEv* __restrict__ recs, const u
         if (tid == 0) { PvSeg z{}; z.ok = 0; pv[i] = z; }
         return;
     }
-    const DRule r = S.rules[pg.rule_off + k1];
-    uint32_t cnt = 0;
-    for (uint32_t p = tid; p < sg.len; p += 256) {
-        const SEv e = recs[sg.start + p];
-        if (e.kind != SG_EV_ENTRY || !(e.flags & SG_F_HAS_ARG)) continue;
-        const uint64_t key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
-        const int32_t tc = pv_tc(S, r, key);
-        if (tc == 0 || (int32_t)e.cnt > j_iadd(tc, r.burst)) {  // blocked before any map access
-            dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
-            recs[sg.start + p].flags = (uint8_t)(e.flags | RF_PBLK);
-            continue;
-        }
-        ++cnt;
-    }
-    uint32_t tot;
-    (void)pv_scan<4>(cnt, red, &tot);
+    const DRule& r = S.rules[pg.rule_off + k1];
     // the map's per-word live-stamp prefix counts in stamp order from thr (ppre: free scratch of this map here)
     const PMap mp = S.pmap[r.pmap];
     const uint32_t W = 1u << (mp.rb_log2 - 6), w0 = pv_word(mp, mp.thr);
@@ -145,52 +129,107 @@ __global__ __launch_bounds__(256) void k_pv_prep(SEv* __restrict__ recs, const u
         }
     if (tid == 0) {
         PvSeg o{};
-        o.ok = 1; o.n = tot; o.off = 0; o.mid = r.pmap; o.rk = (uint32_t)k1;
+        o.ok = 1; o.mid = r.pmap; o.rk = (uint32_t)k1; o.nch = (sg.len + PV_CH - 1) / PV_CH;
         pv[i] = o;
         segs[list[i]].bin = sg.bin | SEG_PV;  // (k_pq's pre pass leaves it)
     }
 }
 
-// dense offsets of the listed segments' accesses (one block; m <= a few thousand); tot[0] = all accesses
-__global__ __launch_bounds__(256) void k_pv_offsets(PvSeg* __restrict__ pv, uint32_t m, uint32_t* __restrict__ tot) {
+// the chunk table: (listed segment, first position) of every chunk, segment by segment; tot[1] = chunks
+__global__ __launch_bounds__(256) void k_pv_chunks(PvSeg* __restrict__ pv, uint32_t m, PvBuf B, uint32_t* __restrict__ tot) {
     __shared__ uint32_t red[4];
     uint32_t base = 0;
     for (uint32_t c = 0; c < m; c += 256) {
         const uint32_t i = c + threadIdx.x;
-        const uint32_t v = (i < m && pv[i].ok) ? pv[i].n : 0u;
+        const uint32_t v = i < m ? pv[i].nch : 0u;
         uint32_t t;
-        const uint32_t o = pv_scan<4>(v, red, &t);
-        if (i < m) pv[i].off = base + o;
+        const uint32_t o = base + pv_scan<4>(v, red, &t);
+        if (i < m) {
+            pv[i].ch0 = o;
+            for (uint32_t k = 0; k < v; ++k) B.chunk[o + k] = make_uint2(i, k * PV_CH);
+        }
         base += t;
     }
-    if (threadIdx.x == 0) *tot = base;
+    if (threadIdx.x == 0) tot[1] = base;
 }
 
-// ---- fill: one workgroup per listed segment: accesses in order, group ids from the segment's hash table
+// ---- count: one workgroup per chunk: its accesses; the checks before any map access decided here
+__global__ __launch_bounds__(256) void k_pv_count(SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
+                                                  const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                  DevState S, DevCfg cfg, const PvSeg* __restrict__ pv, PvBuf B,
+                                                  const uint32_t* __restrict__ tot, uint32_t* __restrict__ dec) {
+    __shared__ uint32_t red[4];
+    const uint32_t c = blockIdx.x, tid = threadIdx.x;
+    if (c >= tot[1]) return;
+    const uint2 ch = B.chunk[c];
+    const PvSeg ps = pv[ch.x];
+    const Seg sg = segs[list[ch.x]];
+    const DRule& r = S.rules[S.prog[sg.res].rule_off + ps.rk];
+    const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
+    uint32_t cnt = 0;
+    for (uint32_t p = ch.y + tid; p < end; p += 256) {
+        const SEv e = recs[sg.start + p];
+        if (e.kind != SG_EV_ENTRY || !(e.flags & SG_F_HAS_ARG)) continue;
+        const uint64_t key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
+        const int32_t tc = pv_tc(S, r, key);
+        if (tc == 0 || (int32_t)e.cnt > j_iadd(tc, r.burst)) {  // blocked before any map access
+            dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
+            recs[sg.start + p].flags = (uint8_t)(e.flags | RF_PBLK);
+            continue;
+        }
+        ++cnt;
+    }
+    uint32_t t;
+    (void)pv_scan<4>(cnt, red, &t);
+    if (tid == 0) B.ccnt[c] = t;
+}
+
+// dense offsets: chunks' (exclusive scan), segments' first access and count; tot[0] = all accesses (one block)
+__global__ __launch_bounds__(256) void k_pv_offsets(PvSeg* __restrict__ pv, uint32_t m, PvBuf B, uint32_t* __restrict__ tot) {
+    __shared__ uint32_t red[4];
+    const uint32_t nc = tot[1];
+    uint32_t base = 0;
+    for (uint32_t c = 0; c < nc; c += 256) {
+        const uint32_t k = c + threadIdx.x;
+        const uint32_t v = k < nc ? B.ccnt[k] : 0u;
+        uint32_t t;
+        const uint32_t o = pv_scan<4>(v, red, &t);
+        if (k < nc) B.cof[k] = base + o;
+        base += t;
+    }
+    if (threadIdx.x == 0) { B.cof[nc] = base; tot[0] = base; }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        if (!pv[i].ok) continue;
+        const uint32_t a = B.cof[pv[i].ch0], e = B.cof[pv[i].ch0 + pv[i].nch];
+        pv[i].off = a;
+        pv[i].n = e - a;
+    }
+}
+
+// ---- fill: one workgroup per chunk: accesses in order into the dense arrays, group ids from the segment's table
 __global__ __launch_bounds__(256) void k_pv_fill(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
                                                  const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
-                                                 uint32_t m, DevState S, DevCfg cfg, const PvSeg* __restrict__ pv,
-                                                 PvBuf B) {
+                                                 DevState S, DevCfg cfg, const PvSeg* __restrict__ pv, PvBuf B,
+                                                 const uint32_t* __restrict__ tot) {
     __shared__ uint32_t red[4];
-    const uint32_t i = blockIdx.x, tid = threadIdx.x;
-    if (i >= m) return;
-    const PvSeg ps = pv[i];
-    if (!ps.ok) return;
-    const Seg sg = segs[list[i]];
-    const Prog pg = S.prog[sg.res];
-    const DRule r = S.rules[pg.rule_off + ps.rk];
-    const uint64_t H = 2ull * ps.n;  // table slots of this segment
+    const uint32_t c = blockIdx.x, tid = threadIdx.x;
+    if (c >= tot[1]) return;
+    const uint2 ch = B.chunk[c];
+    const PvSeg ps = pv[ch.x];
+    const Seg sg = segs[list[ch.x]];
+    const DRule& r = S.rules[S.prog[sg.res].rule_off + ps.rk];
+    const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
+    const uint64_t H = 2ull * ps.n;  // the segment's table slots
     unsigned long long* tab = B.htab + 2ull * ps.off;
-    for (uint64_t s = tid; s < H; s += 256) tab[s] = PK_EMPTY;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t c = 0; c < sg.len; c += 256) {  // (uniform trip count)
-        const uint32_t p = c + tid;
+    uint32_t base = B.cof[c];
+    for (uint32_t c0 = ch.y; c0 < end; c0 += 256) {  // (uniform trip count)
+        const uint32_t p = c0 + tid;
         bool take = false;
         uint64_t key = 0;
         int32_t tc = 0;
         SEv e;
-        if (p < sg.len) {
+        if (p < end) {
             e = recs[sg.start + p];
             if (e.kind == SG_EV_ENTRY && (e.flags & SG_F_HAS_ARG) && !(e.flags & RF_PBLK)) {
                 key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
@@ -201,21 +240,20 @@ __global__ __launch_bounds__(256) void k_pv_fill(const SEv* __restrict__ recs, c
         uint32_t t;
         const uint32_t o = pv_scan<4>(take ? 1u : 0u, red, &t);
         if (take) {
-            const uint32_t g = ps.off + base + o;
+            const uint32_t g = base + o;
             B.key[g] = key;
             B.pos[g] = p;
             B.dt[g] = e.dt;
             B.acq[g] = e.cnt;
             B.tc[g] = tc;
-            B.seg[g] = i;
+            B.seg[g] = ch.x;
             B.prev[g] = PV_NONE;
             B.w[g] = -1;
             B.fslot[g] = -1;
             B.keep[g] = 0;
-            // the value's slot in the segment's table: its group id
-            uint64_t h = mix64(key ^ 0x5BD1E9955BD1E995ull) % H;
+            uint64_t h = mix64(key ^ 0x5BD1E9955BD1E995ull) % H;  // the value's slot: its group id
             for (;;) {
-                unsigned long long cur = tab[h];
+                const unsigned long long cur = tab[h];
                 if (cur == key) break;
                 if (cur == PK_EMPTY) {
                     const unsigned long long prv = atomicCAS(&tab[h], (unsigned long long)PK_EMPTY, (unsigned long long)key);
@@ -339,33 +377,70 @@ __global__ void k_pv_resid(PvBuf B, const uint32_t* __restrict__ tot, const PvSe
     B.hit[g] = hit ? 1 : 0;
 }
 
-// ---- walk: one lane per value (its accesses contiguous in sorted order)
+// ---- gather: the walk's inputs in sorted order (each value's accesses contiguous), misses per 256 positions
+__global__ void k_pv_gather(const Seg* __restrict__ segs, const uint32_t* __restrict__ list, PvBuf B,
+                            const uint32_t* __restrict__ tot) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *tot) return;
+    const uint32_t g = B.idx[q];
+    B.gdt[q] = B.dt[g];
+    const bool hit = B.hit[g] != 0;
+    B.gaw[q] = (B.acq[g] & 0xFFFFu) | (hit ? 0x10000u : 0u);
+    B.gpos[q] = segs[list[B.seg[g]]].start + B.pos[g];
+    if (!hit) atomicOr(&B.mflag[q / PV_B], 1u);
+}
+
+// first miss in sorted positions [lo, hi) (hi if none)
+__device__ uint32_t pv_first_miss(const PvBuf& B, uint32_t lo, uint32_t hi) {
+    uint32_t q = lo;
+    while (q < hi) {
+        if ((q % PV_B) == 0 && q + PV_B <= hi && !B.mflag[q / PV_B]) { q += PV_B; continue; }
+        if (!(B.gaw[q] & 0x10000u)) return q;
+        ++q;
+    }
+    return hi;
+}
+
+// ---- walk: one lane per value through passDefaultLocalCheck.  Once the bucket is empty, every access up to the
+// next refill (pass time > durationInSec) blocks without a state change -- unless an acquire is 0 (jumps off for a
+// batch with such ENTRYs: BF_ZERO_CNT) or a miss re-inserts the value -- so the lane jumps there by binary search
+// over the value's times and leaves the stretch's verdicts to k_pv_ranges: a hot value is ~ (batch seconds /
+// durationInSec) x maxCount steps, not one step an access.
 __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
-                          PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S,
-                          int64_t t0, uint32_t* __restrict__ dec) {
+                          PvBuf B, uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S, int64_t t0,
+                          uint32_t* __restrict__ dec, uint32_t jumps, uint32_t range_cap, uint32_t* __restrict__ bflags) {
     const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = *tot;
+    const uint32_t n = tot[0];
     if (q0 >= n) return;
     const uint32_t gd = B.gid[q0];
     if (q0 > 0 && B.gid[q0 - 1] == gd) return;  // not a group start
+    uint32_t qb = q0 + 1;                       // group end: doubling then binary search over the sorted keys
+    {
+        uint32_t step = 1;
+        while (qb < n && B.gid[qb] == gd) { qb = (q0 + 2 * step < n) ? q0 + 2 * step : n; step *= 2; }
+        uint32_t lo = q0 + step / 2, hi = qb;  // gid[lo] == gd (or lo == q0), the end lies in (lo, hi]
+        if (lo < q0 + 1) lo = q0 + 1;
+        while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (B.gid[md] == gd) lo = md + 1; else hi = md; }
+        qb = lo;
+    }
     const uint32_t g0 = B.idx[q0];
     const uint32_t si = B.seg[g0];
     const PvSeg ps = pv[si];
     const Seg sg = segs[list[si]];
-    const Prog pg = S.prog[sg.res];
-    const DRule r = S.rules[pg.rule_off + ps.rk];
+    const DRule& r = S.rules[S.prog[sg.res].rule_off + ps.rk];
     const int64_t D = r.duration_sec * 1000;
     const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
+    const int32_t tc = B.tc[g0], maxc = j_iadd(tc, r.burst);
     const uint32_t blk = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
     int64_t last = B.flast[g0];  // (valid when the first access hits: the value was live)
     int32_t tok = B.ftok[g0];
-    uint32_t g = g0;
-    for (uint32_t q = q0; q < n && B.gid[q] == gd; ++q) {
-        g = B.idx[q];
-        const int64_t t = t0 + B.dt[g];
-        const int32_t a = (int32_t)B.acq[g], tc = B.tc[g], maxc = j_iadd(tc, r.burst);
+    uint32_t q = q0;
+    while (q < qb) {
+        const int64_t t = t0 + B.gdt[q];
+        const uint32_t aw = B.gaw[q];
+        const int32_t a = (int32_t)(aw & 0xFFFFu);
         bool pass;
-        if (!B.hit[g]) {  // inserted: timeCounters / tokenCounters.putIfAbsent
+        if (!(aw & 0x10000u)) {  // a miss: inserted (timeCounters / tokenCounters.putIfAbsent)
             last = t;
             tok = j_iadd(maxc, -a);
             pass = true;
@@ -383,17 +458,46 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
             }
         }
         if (!pass) {
-            const uint32_t p = B.pos[g];
-            dec[sg.start + p] = blk;
-            recs[sg.start + p].flags = (uint8_t)(recs[sg.start + p].flags | RF_PBLK);
+            const uint32_t rp = B.gpos[q];
+            dec[rp] = blk;
+            recs[rp].flags = (uint8_t)(recs[rp].flags | RF_PBLK);
+        }
+        ++q;
+        if (jumps && tok == 0 && q < qb) {
+            // the first access that may refill: time > last + D (times are non-decreasing within the value)
+            const int64_t lim64 = last + D - t0;
+            const int32_t lim = lim64 > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)lim64;
+            uint32_t lo = q, hi = qb;
+            while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (B.gdt[md] <= lim) lo = md + 1; else hi = md; }
+            const uint32_t tgt = pv_first_miss(B, q, lo);
+            if (tgt > q + 8) {  // a stretch of blocks: to k_pv_ranges
+                const uint32_t k = atomicAdd(&tot[2], 1u);
+                if (k < range_cap) { B.range[k] = make_uint4(q, tgt, blk, 0u); q = tgt; }
+                else atomicSub(&tot[2], 1u);  // (full: walk it)
+            }
         }
     }
     // the value's last access g: it stays iff fewer than cap distinct values are accessed after it
+    const uint32_t g = B.idx[qb - 1];
     const int64_t end = (int64_t)ps.off + ps.n;
     B.keep[g] = pv_count_lt(B, g, end, (int32_t)g, cap) < cap ? 1 : 0;
     B.flast[g] = last;
     B.ftok[g] = tok;
     B.fslot[g] = B.fslot[g0];  // (the value's slot, carried to its last access for the commit)
+}
+
+// blocked stretches of the walk: a workgroup per stretch
+__global__ __launch_bounds__(256) void k_pv_ranges(SEv* __restrict__ recs, PvBuf B, const uint32_t* __restrict__ tot,
+                                                   uint32_t range_cap, uint32_t* __restrict__ dec) {
+    const uint32_t nr = tot[2] < range_cap ? tot[2] : range_cap;
+    for (uint32_t k = blockIdx.x; k < nr; k += gridDim.x) {
+        const uint4 rg = B.range[k];
+        for (uint32_t q = rg.x + threadIdx.x; q < rg.y; q += 256) {
+            const uint32_t rp = B.gpos[q];
+            dec[rp] = rg.z;
+            recs[rp].flags = (uint8_t)(recs[rp].flags | RF_PBLK);
+        }
+    }
 }
 
 // ---- commit: one workgroup per segment: the map after the segment
@@ -589,19 +693,28 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
 
 namespace sg {
 // the value-parallel pre pass over the wide XF_MIX list (cap accesses at most); pv[] tells k_pq which segments
-// are done.  Scratch: PvBuf arrays of cap entries, htab 2 x cap, radix scratch (hist, part), tot (device word).
+// are done.  Scratch: PvBuf arrays of cap entries (chunks: cap / PV_CH + m), htab 2 x cap, radix scratch (hist,
+// part), tot (device words: [0] accesses, [1] chunks, [2] ranges).  jumps: the batch has no zero-acquire ENTRY.
 hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                      const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
-                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
+                     hipStream_t st,
                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                      uint32_t tile) {
     if (!m || !cap) return hipSuccess;
-    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, recs, vals, segs, list, m, S, cfg, pv, dec);
-    hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, tot);
-    hipLaunchKernelGGL(k_pv_fill, dim3(m), dim3(256), 0, st, recs, vals, segs, list, m, S, cfg, pv, B);
+    const uint32_t nchunk = cap / PV_CH + m + 1;
+    hipError_t e = hipMemsetAsync(tot, 0, 16, st);
+    if (e == hipSuccess) e = hipMemsetAsync(B.htab, 0xFF, 2ull * cap * 8, st);  // the segments' tables: PK_EMPTY
+    if (e == hipSuccess) e = hipMemsetAsync(B.mflag, 0, ((cap + PV_B - 1) / PV_B) * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv);
+    hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
+    hipLaunchKernelGGL(k_pv_count, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot, dec);
+    hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
+    hipLaunchKernelGGL(k_pv_fill, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot);
     const uint32_t nb = (cap + 255) / 256;
     hipLaunchKernelGGL(k_pv_pad, dim3(nb), dim3(256), 0, st, B, tot, cap);
     // group ids < 2 x cap: stable LSD radix on 8-bit digits (each value's accesses stay in access order)
@@ -611,7 +724,7 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
     const uint32_t nblocks = (cap + tile - 1) / tile;
     uint32_t *kin = B.gid, *vin = B.idx, *kout = B.gid2, *vout = B.idx2;
     for (int p = 0; p < passes; ++p) {
-        hipError_t e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
+        e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
         if (e == hipSuccess) e = scan(hist, hist, (uint64_t)nblocks << 8, part, nullptr, st);
         if (e == hipSuccess) e = radix_scatter(kin, vin, cap, p * 8, hist, nblocks, kout, vout, nullptr, st);
         if (e != hipSuccess) return e;
@@ -619,14 +732,16 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
         uint32_t* tv = vin; vin = vout; vout = tv;
     }
     if (kin != B.gid) {  // sorted arrays back into gid / idx (an odd number of passes)
-        hipError_t e = hipMemcpyAsync(B.gid, kin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
+        e = hipMemcpyAsync(B.gid, kin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(B.idx, vin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
     hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
-    hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec);
+    hipLaunchKernelGGL(k_pv_gather, dim3(nb), dim3(256), 0, st, segs, list, B, tot);
+    hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags);
+    hipLaunchKernelGGL(k_pv_ranges, dim3(2048), dim3(256), 0, st, recs, B, tot, cap, dec);
     hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags);
     return hipGetLastError();
 }

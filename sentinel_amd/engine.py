@@ -232,6 +232,17 @@ class Engine:
             return None
         return {"second": out[:16].reshape(2, 8), "thread": int(out[16]), "mhist": out[17:21].reshape(2, 2)}
 
+    def pv_last(self) -> dict:
+        """The last batch's value-parallel pre pass (diagnostics export sgx_pv_last): segments, accesses,
+        blocked stretches its walk jumped."""
+        fn = lib().sgx_pv_last
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_void_p]
+        out = np.zeros(3, dtype=np.uint64)
+        if fn(self.h, out.ctypes.data) != 0:
+            raise SentinelError(A.SG_EDEVICE, "sgx_pv_last failed")
+        return {"segments": int(out[0]), "accesses": int(out[1]), "ranges": int(out[2])}
+
     def param_pool(self) -> dict:
         """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last layout,
         compactions."""

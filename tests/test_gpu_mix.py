@@ -60,6 +60,9 @@ def test_mix_c6_shapes(nval, pv, monkeypatch):
     w.install(orc)
     cuts = np.linspace(0, len(ev), 4).astype(np.int64)
     dg = np.concatenate([_cmp(eng, orc, ev[a:b], "batch %d" % i) for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:]))])
+    if pv == "1":  # the value-parallel pass took the long segments
+        st = eng.pv_last()
+        assert st["segments"] >= 3 and st["accesses"] > 20_000, st
     cnt = np.bincount(ev["res_id"], minlength=n_res)
     assert cnt.max() > 3 * 2 * 8192 and ((cnt > 3 * 1100) & (cnt < 3 * 8000)).sum() > 10  # wide and narrow passes
     _nodes(eng, orc, range(n_res))

@@ -32,9 +32,10 @@ elif which == "c6":
     w = T.Workload(6, seed=T.SEED_BASE + 6, n_entries=int(nb * GB / 2.05) + 1000)
     ev = w.events[:nb * GB]
     eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=28, status_ring_log2=28,
-                   max_batch_events=GB)
+                   max_batch_events=GB, max_rules=1 << 22)
     w.install(eng)
     r = bench.run_batches(eng, ev, GB, dev)
+    r["pv"] = eng.pv_last()
     r["pool"] = eng.param_pool()
 else:
     w = T.Workload(5, seed=T.SEED_BASE + 5, n_entries=12_000_000)
