@@ -387,6 +387,12 @@ int sg_cluster_request_param_tokens(sg_engine* e, const sg_param_token_req* reqs
 /* Node read-back for parity tests: the ClusterNode of res_id. */
 int sg_read_node(sg_engine* e, uint32_t res_id, int64_t now_ms, sg_node_state* out);
 
+/* ParameterMetric.getThreadCount(paramIdx, value) of res_id (param/ParameterMetric.java:233-241): the value's
+ * thread count in the resource's thread-count map of paramIdx, 0 when the map or the value is absent; *present
+ * (optional) tells the two apart.  A read-back: unlike CacheMap.get it does not move the value in the LRU order. */
+int sg_param_thread_count(sg_engine* e, uint32_t res_id, int32_t param_idx, uint64_t key, int64_t* count,
+                          int32_t* present);
+
 /* Last error message of the calling thread ("" if none). */
 const char* sg_last_error(void);
 

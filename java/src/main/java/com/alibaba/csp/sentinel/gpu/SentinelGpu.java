@@ -215,6 +215,9 @@ final class SentinelGpu {
     static final MethodHandle CLUSTER_REQUEST_PARAM_TOKENS = fn("sg_cluster_request_param_tokens",
         rc(ADDRESS, ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS));
     static final MethodHandle READ_NODE = fn("sg_read_node", rc(ADDRESS, JAVA_INT, JAVA_LONG, ADDRESS));
+    /** ParameterMetric.getThreadCount(paramIdx, value): (engine, res, paramIdx, key, long* count, int* present). */
+    static final MethodHandle PARAM_THREAD_COUNT =
+        fn("sg_param_thread_count", rc(ADDRESS, JAVA_INT, JAVA_INT, JAVA_LONG, ADDRESS, ADDRESS));
     static final MethodHandle LAST_ERROR = fn("sg_last_error", FunctionDescriptor.of(ADDRESS));
     static final MethodHandle LAST_TIMINGS = fn("sg_last_timings", rc(ADDRESS, ADDRESS, JAVA_INT));
 

@@ -239,17 +239,22 @@ struct Seg {
 };
 #define SEG_AUXP 0x80u  // Seg.bin: the segment's origin / context nodes are updated by the aux.hip post-pass
 #define SEG_PV 0x40u    // Seg.bin: pvalue.hip decided the segment's param checks (k_pq's pre pass leaves it)
+#define SEG_PVT 0x100u  // Seg.bin: pvalue.hip's post pass updated the thread-count map (k_pq's post pass leaves it)
 
 // pvalue.hip: the value-parallel pre pass of long XF_MIX segments
 // per listed segment (the wide XF_MIX list): what the pre pass found
 struct PvSeg {
-    uint32_t ok;        // decided here (else k_pq's pre pass)
+    uint32_t ok;        // decided here (else k_pq's pre / post pass)
     uint32_t n;         // accesses
     uint32_t off;       // first access in the dense arrays
-    uint32_t mid;       // rule map
+    uint32_t mid;       // rule map (the post pass: the thread-count map of paramIdx 0)
     uint32_t rk;        // the checked rule's index in the program
     uint32_t ch0;       // first extraction chunk
     uint32_t nch;       // extraction chunks
+    uint32_t fbits;     // post pass: ParameterMetric bits of the rules the segment's ENTRYs visited
+    uint32_t freach;    // post pass: segment position + 1 of the first ENTRY visiting rule k0 (EXITs release from it)
+    int32_t peak;       // post pass: the thread-count map's largest growth over its start size
+    uint32_t tm0;       // post pass: EXITs release from position 0 (the node had the bits already)
     uint32_t pad;
 };
 

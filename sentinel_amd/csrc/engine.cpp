@@ -21,6 +21,7 @@
 
 #include "../../include/sentinel_gpu.h"
 #include "dev_types.h"
+#include "pmap.h"  // (pm_buckets: sg_param_thread_count)
 
 namespace sg {
 // kernels.hip
@@ -72,6 +73,14 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                      uint32_t tile);
+hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                      const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
+                      uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
+                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                      uint32_t tile);
 hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                          const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
                          const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st);
@@ -575,6 +584,8 @@ struct sg_engine {
     PvBuf pvb{};                // its scratch (decide stage only: one set)
     uint64_t pv_cap = 0;
     PvSeg* d_pvseg = nullptr;
+    PvSeg* d_pvtseg = nullptr;  // the post pass's (pvalue.hip launch_pvt)
+    bool pvt_on = false;        // SG_PVT (default: SG_PV): the value-parallel post pass (thread-count maps)
     uint64_t pvseg_cap = 0;
     uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr;
     uint32_t pv_last_m = 0;     // listed segments of the last batch that ran it (diagnostics)
@@ -1171,6 +1182,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
     if (const char* v = std::getenv("SG_PV")) e->pv_on = v[0] != '0';
+    e->pvt_on = e->pv_on;
+    if (const char* v = std::getenv("SG_PVT")) e->pvt_on = v[0] != '0';
     if (const char* v = std::getenv("SG_PQ_WIDE")) e->pq_wide = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_SKIP_MIN")) {
         e->skip_min = std::max<uint32_t>(1u, (uint32_t)std::strtoul(v, nullptr, 0));
@@ -1240,19 +1253,26 @@ extern "C" int sgx_read_aux_node(sg_engine* e, uint32_t res, uint32_t kind, uint
     }
     return 0;
 }
-// diagnostics export: the last batch's value-parallel pre pass (pvalue.hip), out = {listed segments it decided, accesses,
-// blocked stretches the walk jumped}
+// diagnostics export: the last batch's value-parallel passes (pvalue.hip), out = {pre pass: listed segments it decided,
+// accesses, blocked stretches the walk jumped; post pass: segments eligible, ops, segments committed}
 extern "C" int sgx_pv_last(sg_engine* e, unsigned long long* out) {
     if (!e || !out || drain(e) != SG_OK) return -1;
-    out[0] = out[1] = out[2] = 0;
+    out[0] = out[1] = out[2] = out[3] = out[4] = out[5] = 0;
     if (!e->d_pvseg || !e->d_pvtot || !e->pv_last_m) return 0;
     std::vector<PvSeg> v(e->pv_last_m);
-    uint32_t tot[4] = {0, 0, 0, 0};
+    uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpy(v.data(), e->d_pvseg, v.size() * sizeof(PvSeg), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    if (hipMemcpy(tot, e->d_pvtot, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(tot, e->d_pvtot, 32, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     for (const auto& s : v) out[0] += s.ok ? 1 : 0;
     out[1] = tot[0];
     out[2] = tot[2];
+    if (e->pvt_on && e->d_pvtseg) {
+        if (hipMemcpy(v.data(), e->d_pvtseg, v.size() * sizeof(PvSeg), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        for (const auto& s : v) out[3] += s.ok ? 1 : 0;
+        out[4] = tot[4];
+        out[5] = tot[7];
+    }
+    if (!e->pv_on) out[0] = out[1] = out[2] = 0;
     return 0;
 }
 // diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last layout, compactions}
@@ -1276,7 +1296,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_pool_next);
     if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
     free_pv(e);
-    dfree(e->d_pvseg); dfree(e->d_pvtot);
+    dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
@@ -1897,8 +1917,10 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
     if (m > e->pvseg_cap) {
         HIPCHK(hipStreamSynchronize(e->stream));
         dfree(e->d_pvseg);
+        dfree(e->d_pvtseg);
         e->pvseg_cap = std::max<uint64_t>(m, 1024);
         HIPCHK(hipMalloc(&e->d_pvseg, e->pvseg_cap * sizeof(PvSeg)));
+        HIPCHK(hipMalloc(&e->d_pvtseg, e->pvseg_cap * sizeof(PvSeg)));
         free_pv(e);  // (the chunk arrays are sized by pvseg_cap)
     }
     if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
@@ -2204,9 +2226,11 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // XF_MIX segments of the cooperative bins: their param checks first (k_pq pre pass), the owners then decide
     // the flow / degrade chain on them
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
-    if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
-        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
+    if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
+        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;  // (before this batch's decide work is queued)
         e->pv_last_m = n_mixw;
+    }
+    if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
         HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
                          e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
                          (bflags & BF_ZERO_CNT) ? 0u : 1u, st, launch_radix_hist,
@@ -2282,7 +2306,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))
         HIPCHK(launch_fill(e->d_spans, S.nspan, e->span_cap, e->d_recs, e->d_prog, e->d_rules, e->d_dec, st));
-    // XF_MIX: the thread-count maps and ParameterMetric bits from the final verdicts (k_pq post pass)
+    // XF_MIX: the thread-count maps and ParameterMetric bits from the final verdicts (the long ones value-parallel
+    // where the maps do not overflow, pvalue.hip; the rest by k_pq's post pass)
+    if (n_mixw && e->pvt_on && head[72])
+        HIPCHK(launch_pvt(e->d_recs, dev_ev, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec,
+                          e->d_bsmall + 0, e->d_pvtseg, e->pvb, head[72], e->d_pvtot + 4, e->d_pvhist, e->d_pvpart, st,
+                          launch_radix_hist, launch_radix_scatter, launch_scan, radix_tile()));
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(1, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
                              e->d_dec, e->d_bsmall + 0, st));
@@ -2376,6 +2405,45 @@ int sg_last_timings(sg_engine* e, double* ms, int cap) {
     int k = 0;
     for (; k < cap && k < 4; ++k) ms[k] = e->last_ms[k];
     return k;
+}
+
+int sg_param_thread_count(sg_engine* e, uint32_t res, int32_t idx, uint64_t key, int64_t* count, int32_t* present) {
+    if (!e || !count) return fail(SG_EINVAL, "null argument");
+    if (res >= e->cfg.max_resources) return fail(SG_EINVAL, "res_id out of range");
+    if (int rc = drain(e)) return rc;
+    *count = 0;
+    if (present) *present = 0;
+    if (idx < 0 || idx >= SG_MAX_ARGS) return SG_OK;
+    const uint64_t want = TMAP_KEY | ((uint64_t)res << 8) | (uint64_t)idx;
+    uint32_t id = NO_ID;
+    for (uint32_t i = 0; i < (uint32_t)e->pmap_key.size(); ++i)
+        if (e->pmap_key[i] == want) { id = i; break; }
+    if (id == NO_ID) return SG_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    PMap m;
+    HIPCHK(hipMemcpy(&m, e->d_pmap + id, sizeof(m), hipMemcpyDeviceToHost));
+    uint32_t b[2];
+    pm_buckets(m.nb, key, b[0], b[1]);
+    for (int h = 0; h < 2; ++h) {
+        PBucket bk;
+        HIPCHK(hipMemcpy(&bk, e->d_pbkt + m.base + b[h], sizeof(bk), hipMemcpyDeviceToHost));
+        for (int j = 0; j < PM_BKT; ++j) {
+            if (bk.key[j] != key) continue;
+            const int64_t st = bk.stamp[j];
+            if (st < m.thr || st >= m.clock) continue;  // a dead slot
+            const uint64_t p = (uint64_t)st & ((1ull << m.rb_log2) - 1);
+            uint64_t w = 0;
+            HIPCHK(hipMemcpy(&w, e->d_pbm + m.bm + (p >> 6), 8, hipMemcpyDeviceToHost));
+            if (!((w >> (p & 63)) & 1ull)) continue;
+            PData d;
+            HIPCHK(hipMemcpy(&d, e->d_pdat + (m.base + b[h]) * PM_BKT + j, sizeof(d), hipMemcpyDeviceToHost));
+            *count = d.v0;
+            if (present) *present = 1;
+            return SG_OK;
+        }
+    }
+    return SG_OK;
 }
 
 int sg_read_node(sg_engine* e, uint32_t res, int64_t now_ms, sg_node_state* out) {

@@ -1019,7 +1019,8 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
     if (blockIdx.x >= m) return;
     const uint32_t tid = threadIdx.x;
     const Seg sg = segs[order[blockIdx.x]];
-    if (MODE == PQ_PRE && (sg.bin & SEG_PV)) return;  // pvalue.hip decided its param checks
+    if (MODE == PQ_PRE && (sg.bin & SEG_PV)) return;    // pvalue.hip decided its param checks
+    if (MODE == PQ_POST && (sg.bin & SEG_PVT)) return;  // pvalue.hip's post pass took its thread-count map
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
     const int np = pg.n_param;

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_pv_fill(const SEv* __restrict__ recs, c
 // padding of the sort arrays beyond the accesses: [tot, cap) sorts last
 __global__ void k_pv_pad(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < cap && g >= *tot) { B.gid[g] = 0xFFFFFFFFu; B.idx[g] = g; }
+    if (g < cap && g >= *tot) { B.gid[g] = 0xFFFFFFFFu; B.idx[g] = g; B.prev[g] = 0; }
 }
 
 // ---- prev / first accesses (sorted order: after the sort B.gid / B.idx hold the sorted keys / accesses)
@@ -500,11 +500,280 @@ __global__ __launch_bounds__(256) void k_pv_ranges(SEv* __restrict__ recs, PvBuf
     }
 }
 
+// ==== the post pass (ParamFlowStatisticEntryCallback / ExitCallback from the final verdicts, k_pq PQ_POST):
+// thread-count map of paramIdx 0, ParameterMetric.java:117-241 -- a passed ENTRY adds (putIfAbsent then increment),
+// an EXIT of a passed ENTRY releases (an absent value is put at 0; at <= 0 removed).  Under the hypothesis that
+// the map never grows beyond cap within the segment (no eviction), each value's ops are independent: one lane per
+// value walks them, the map's size over the segment is a scan of the walks' +1 / -1, and the commit keeps every
+// value present at its last op.  A segment whose peak passes cap is left to k_pq's sequential replay.
+#define PVT_ADD 1u
+#define PVT_SUB 3u
+
+// rule k visited by an ENTRY of final word d (PQ_POST's prologue): passed -> every rule; blocked by param rule k ->
+// rules 0..k; blocked by a later slot -> every rule
+__device__ __forceinline__ uint32_t pvt_stq(const DevState& S, const Prog& pg, uint32_t d) {
+    if (st_passed(d & 0xFFu)) return 0;
+    uint32_t stq = (uint32_t)pg.n_param + 1;
+    if ((d & 0xFFu) == ST_BLOCK_PARAM)
+        for (int k = 0; k < pg.n_param; ++k) {
+            const DRule& r = S.rules[pg.rule_off + k];
+            if (r.behavior != PB_INIT_ONLY && r.slot == ((d >> 8) & 0xFFu)) stq = (uint32_t)k + 1;
+        }
+    return stq;
+}
+__device__ __forceinline__ uint32_t pvt_kbits(const DRule& r) {
+    return r.behavior == PB_INIT_ONLY ? (uint32_t)r.burst << NI_TM_SHIFT
+                                      : NI_PM | (r.param_idx < SG_MAX_ARGS ? ni_tm((uint32_t)r.param_idx) : 0u);
+}
+
+// the op of segment position p (k_pq phase 3 of the post pass) and its value's key
+__device__ __forceinline__ uint32_t pvt_op(const SEv& e, uint32_t p, const Seg& sg, uint32_t tm_from,
+                                           const sg_event* __restrict__ ev, const uint32_t* __restrict__ vals,
+                                           const DevState& S, const DevCfg& cfg, const uint32_t* __restrict__ dec,
+                                           uint64_t& key) {
+    const uint32_t gp = sg.start + p;
+    if (e.kind == SG_EV_ENTRY) {
+        if (!(e.flags & SG_F_HAS_ARG) || !st_passed(dec[gp] & 0xFFu)) return 0;
+        key = S.key_ring[(S.gbase + (vals[gp] & 0x7FFFFFFFu)) & cfg.ring_mask];
+        return PVT_ADD;
+    }
+    if (e.kind != SG_EV_EXIT || !(e.flags & SG_F_EXIT_ARGS) || p < tm_from) return 0;
+    const bool own = (e.flags & RF_OWN_ARGS) != 0;
+    uint64_t ref = SG_REF_NONE;
+    uint32_t op = 0;
+    if (e.code == RC_PASSED) {
+        if (!own) ref = ev[vals[gp] & 0x7FFFFFFFu].aux & SG_REF_NONE;
+        op = PVT_SUB;
+    } else if (e.code == RC_NONE && own) {
+        op = PVT_SUB;
+    } else if (e.code == RC_BATCH) {
+        const uint32_t rel = e.x - sg.start;
+        if (rel < p) {
+            ref = S.gbase + (vals[e.x] & 0x7FFFFFFFu);
+            op = st_passed(dec[e.x] & 0xFFu) ? PVT_SUB : 0u;
+        }
+    }
+    if (op) {
+        if (own) ref = S.gbase + (vals[gp] & 0x7FFFFFFFu);
+        key = S.key_ring[ref & cfg.ring_mask];
+        if (key == NO_KEY) op = 0;
+    }
+    return op;
+}
+
+// per listed segment (a lane each): eligibility -- a chain, a thread-count map of paramIdx 0 that is on, within the
+// commit's LDS, no THREAD-grade rule (XF_MIX) -- and the first rule whose visit sets the map's bit (k0)
+__global__ void k_pvt_prep(const Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m, DevState S,
+                           PvSeg* __restrict__ pv) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const Seg sg = segs[list[i]];
+    const Prog pg = S.prog[sg.res];
+    const uint32_t flags = S.info[sg.res].flags;
+    const uint32_t tm = pg.tm_base == NO_ID ? NO_ID : S.tmid[pg.tm_base];
+    PvSeg o{};
+    uint32_t all_bits = NI_PM, k0 = 0xFFFFFFFFu;
+    bool thr = false;
+    for (int k = 0; k < pg.n_param; ++k) {
+        const DRule& r = S.rules[pg.rule_off + k];
+        const uint32_t b = pvt_kbits(r);
+        all_bits |= b;
+        if (k0 == 0xFFFFFFFFu && (b & ni_tm(0))) k0 = (uint32_t)k;
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_THREAD) thr = true;
+    }
+    bool ok = (flags & NI_CHAIN) && tm != NO_ID && S.key_ring && !thr && ((flags | all_bits) & ni_tm(0));
+    if (ok) {
+        const PMap mp = S.pmap[tm];
+        ok = mp.cap <= PQ_MAX_CAP && (mp.rb_log2 - 6) <= 9;
+    }
+    if (ok) {
+        o.ok = 1; o.mid = tm; o.rk = k0; o.nch = (sg.len + PV_CH - 1) / PV_CH;
+        o.freach = 0xFFFFFFFFu;
+        o.tm0 = (flags & (NI_PM | ni_tm(0))) == (NI_PM | ni_tm(0)) ? 1u : 0u;
+    }
+    pv[i] = o;
+}
+
+// per chunk: the rules its ENTRYs visited (the node's bits) and the first ENTRY visiting rule k0
+__global__ __launch_bounds__(256) void k_pvt_reach(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                                   const uint32_t* __restrict__ list, DevState S, PvSeg* __restrict__ pv,
+                                                   PvBuf B, const uint32_t* __restrict__ tot,
+                                                   const uint32_t* __restrict__ dec) {
+    __shared__ uint32_t sb, sr;
+    const uint32_t c = blockIdx.x, tid = threadIdx.x;
+    if (c >= tot[1]) return;
+    if (tid == 0) { sb = 0; sr = 0xFFFFFFFFu; }
+    __syncthreads();
+    const uint2 ch = B.chunk[c];
+    const PvSeg ps = pv[ch.x];
+    const Seg sg = segs[list[ch.x]];
+    const Prog pg = S.prog[sg.res];
+    const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
+    uint32_t fb = 0, fr = 0xFFFFFFFFu;
+    for (uint32_t p = ch.y + tid; p < end; p += 256) {
+        if (recs[sg.start + p].kind != SG_EV_ENTRY) continue;
+        const uint32_t stq = pvt_stq(S, pg, dec[sg.start + p]);
+        for (int k = 0; k < pg.n_param; ++k)
+            if (stq == 0 || stq > (uint32_t)k) {
+                fb |= pvt_kbits(S.rules[pg.rule_off + k]) | NI_PM;
+                if ((uint32_t)k == ps.rk && p + 1 < fr) fr = p + 1;
+            }
+    }
+    if (fb) atomicOr(&sb, fb);
+    if (fr != 0xFFFFFFFFu) atomicMin(&sr, fr);
+    __syncthreads();
+    if (tid == 0) {
+        if (sb) atomicOr(&pv[ch.x].fbits, sb);
+        if (sr != 0xFFFFFFFFu) atomicMin(&pv[ch.x].freach, sr);
+    }
+}
+
+// per chunk: its ops
+__global__ __launch_bounds__(256) void k_pvt_count(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                                   const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                                   const uint32_t* __restrict__ list, DevState S, DevCfg cfg,
+                                                   const PvSeg* __restrict__ pv, PvBuf B, const uint32_t* __restrict__ tot,
+                                                   const uint32_t* __restrict__ dec) {
+    __shared__ uint32_t red[4];
+    const uint32_t c = blockIdx.x, tid = threadIdx.x;
+    if (c >= tot[1]) return;
+    const uint2 ch = B.chunk[c];
+    const PvSeg ps = pv[ch.x];
+    const Seg sg = segs[list[ch.x]];
+    const uint32_t tm_from = ps.tm0 ? 0u : ps.freach;
+    const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
+    uint32_t cnt = 0;
+    for (uint32_t p = ch.y + tid; p < end; p += 256) {
+        uint64_t key;
+        cnt += pvt_op(recs[sg.start + p], p, sg, tm_from, ev, vals, S, cfg, dec, key) ? 1u : 0u;
+    }
+    uint32_t t;
+    (void)pv_scan<4>(cnt, red, &t);
+    if (tid == 0) B.ccnt[c] = t;
+}
+
+// per chunk: the ops in order into the dense arrays (acq: the op), group ids from the segment's table
+__global__ __launch_bounds__(256) void k_pvt_fill(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                                  const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                                  const uint32_t* __restrict__ list, DevState S, DevCfg cfg,
+                                                  const PvSeg* __restrict__ pv, PvBuf B, const uint32_t* __restrict__ tot,
+                                                  const uint32_t* __restrict__ dec) {
+    __shared__ uint32_t red[4];
+    const uint32_t c = blockIdx.x, tid = threadIdx.x;
+    if (c >= tot[1]) return;
+    const uint2 ch = B.chunk[c];
+    const PvSeg ps = pv[ch.x];
+    const Seg sg = segs[list[ch.x]];
+    const uint32_t tm_from = ps.tm0 ? 0u : ps.freach;
+    const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
+    const uint64_t H = 2ull * ps.n;
+    unsigned long long* tab = B.htab + 2ull * ps.off;
+    uint32_t base = B.cof[c];
+    for (uint32_t c0 = ch.y; c0 < end; c0 += 256) {  // (uniform trip count)
+        const uint32_t p = c0 + tid;
+        uint64_t key = 0;
+        const uint32_t op = p < end ? pvt_op(recs[sg.start + p], p, sg, tm_from, ev, vals, S, cfg, dec, key) : 0u;
+        uint32_t t;
+        const uint32_t o = pv_scan<4>(op ? 1u : 0u, red, &t);
+        if (op) {
+            const uint32_t g = base + o;
+            B.key[g] = key;
+            B.pos[g] = p;
+            B.acq[g] = op;
+            B.seg[g] = ch.x;
+            B.prev[g] = 0;
+            B.w[g] = -1;
+            B.fslot[g] = -1;
+            B.keep[g] = 0;
+            uint64_t h = mix64(key ^ 0x5BD1E9955BD1E995ull) % H;
+            for (;;) {
+                const unsigned long long cur = tab[h];
+                if (cur == key) break;
+                if (cur == PK_EMPTY) {
+                    const unsigned long long prv = atomicCAS(&tab[h], (unsigned long long)PK_EMPTY, (unsigned long long)key);
+                    if (prv == PK_EMPTY || prv == key) break;
+                }
+                h = h + 1 == H ? 0 : h + 1;
+            }
+            B.gid[g] = (uint32_t)(2ull * ps.off + h);
+            B.idx[g] = g;
+        }
+        base += t;
+    }
+}
+
+// one lane per value (sorted order): probe the map, walk the ops; prev[g] = the op's change of the map's size
+__global__ void k_pvt_walk(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S) {
+    const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = tot[0];
+    if (q0 >= n) return;
+    const uint32_t gd = B.gid[q0];
+    if (q0 > 0 && B.gid[q0 - 1] == gd) return;
+    uint32_t qb = q0 + 1;
+    while (qb < n && B.gid[qb] == gd) ++qb;  // (a value's ops: passed ENTRYs and their EXITs, few)
+    const uint32_t g0 = B.idx[q0];
+    const PvSeg ps = pv[B.seg[g0]];
+    const PMap mp = S.pmap[ps.mid];
+    const uint64_t key = B.key[g0];
+    uint32_t b1, b2;
+    pm_buckets(mp.nb, key, b1, b2);
+    const PBucket* BK = S.pbkt + mp.base;
+    int32_t slot = -1;
+    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b2].key[j] == key) slot = (int32_t)(b2 * PM_BKT + j);
+    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b1].key[j] == key) slot = (int32_t)(b1 * PM_BKT + j);
+    bool pres = false;
+    int64_t c = 0;
+    if (slot >= 0 && pm_live(mp, S.pbm + mp.bm, BK[slot / PM_BKT].stamp[slot % PM_BKT])) {
+        pres = true;
+        c = S.pdat[mp.base * PM_BKT + slot].v0;
+    }
+    B.fslot[g0] = slot;
+    B.w[g0] = pres ? 0 : PV_INF;
+    for (uint32_t q = q0; q < qb; ++q) {
+        const uint32_t g = B.idx[q];
+        int32_t d = 0;
+        if (B.acq[g] == PVT_ADD) {
+            if (pres) ++c;
+            else { pres = true; c = 1; d = 1; }
+        } else {
+            if (!pres) { pres = true; c = 0; d = 1; }
+            else if (--c <= 0) { pres = false; c = 0; d = -1; }
+        }
+        B.prev[g] = d;
+    }
+    const uint32_t g = B.idx[qb - 1];
+    B.keep[g] = pres ? 1 : 0;
+    B.flast[g] = c;
+    B.ftok[g] = 0;
+    B.fslot[g] = slot;
+}
+
+// the map's size over the segment: peak growth over its start size (X: exclusive scan of prev as uint32)
+__global__ void k_pvt_peak(PvBuf B, const uint32_t* __restrict__ X, const uint32_t* __restrict__ tot,
+                           PvSeg* __restrict__ pv) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = g < tot[0];
+    const uint32_t s = in ? B.seg[g] : 0xFFFFFFFFu;
+    int32_t v = 0;
+    if (in) v = (int32_t)(X[g] + (uint32_t)B.prev[g] - X[pv[s].off]);
+    const uint32_t s0 = (uint32_t)__shfl((int)s, 0, 64);
+    if (__all(s == s0)) {  // one segment in the wave: one atomic
+        for (int o = 32; o > 0; o >>= 1) { const int32_t y = __shfl_xor(v, o, 64); v = y > v ? y : v; }
+        if ((threadIdx.x & 63) == 0 && in && v > 0) atomicMax(&pv[s].peak, v);
+    } else if (in && v > 0) {
+        atomicMax(&pv[s].peak, v);
+    }
+}
+
 // ---- commit: one workgroup per segment: the map after the segment
 #define PV_RW 512u   // ring words (cap <= PQ_MAX_CAP)
 #define PV_CW 256u   // claim words (slots <= map_buckets(PQ_MAX_CAP) * 8)
+// tmode (the post pass): the thread-count map; every value present at its last access stays (no eviction: the
+// map never outgrew cap, else k_pq's post pass takes the segment), and the segment gets SEG_PVT and its bits.
 __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __restrict__ pv, uint32_t m, DevState S,
-                                                    uint32_t* __restrict__ bflags) {
+                                                    uint32_t* __restrict__ bflags, uint32_t tmode,
+                                                    Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                    uint32_t* __restrict__ ndone) {
     __shared__ uint64_t ring[PV_RW], touch[PV_RW];
     __shared__ uint32_t pre[PV_RW];
     __shared__ unsigned long long claim[PV_CW];
@@ -518,6 +787,7 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     PMap mp = S.pmap[ps.mid];
     const uint32_t W = 1u << (mp.rb_log2 - 6);
     const int32_t cap = (int32_t)mp.cap;
+    if (tmode && (int64_t)mp.live + ps.peak > (int64_t)cap) return;  // an eviction: the sequential replay's
     PBucket* BK = S.pbkt + mp.base;
     PData* DT = S.pdat + mp.base * PM_BKT;
     const uint32_t nslot = mp.nb * PM_BKT;
@@ -529,8 +799,9 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     uint32_t ng = 0;
     for (uint32_t k = tid; k < ps.n; k += 1024) {
         const uint32_t g = ps.off + k;
+        if (tmode) ng += B.keep[g];
         if (B.w[g] >= 0) {  // a value's first access
-            ++ng;
+            if (!tmode) ++ng;
             const int32_t sl = B.fslot[g];
             if (sl >= 0 && B.w[g] != PV_INF) {
                 const int64_t s = BK[sl / PM_BKT].stamp[sl % PM_BKT];
@@ -541,7 +812,7 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     }
     uint32_t G;
     (void)pv_scan<16>(ng, red, &G);
-    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay
+    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay (tmode: G kept)
     // (2) untouched live values: the (cap - KA) most recent stay; prefix counts of untouched stamps from thr
     const uint32_t w0 = pv_word(mp, mp.thr);
     {
@@ -688,10 +959,48 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
         h->clock = base + (int64_t)K;
         h->thr = base;
         h->live = K;
+        if (tmode) {
+            const Seg sg = segs[list[i]];
+            segs[list[i]].bin = sg.bin | SEG_PVT;
+            if (ps.fbits) atomicOr(&S.info[sg.res].flags, ps.fbits);
+            atomicAdd(ndone, 1u);
+        }
     }
 }
 
 namespace sg {
+// the accesses [0, tot) by group id, stable (pads [tot, cap) to sort last)
+static hipError_t pv_sort(PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                          hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
+                          hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                                      uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                          hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                          uint32_t tile) {
+    hipError_t e = hipSuccess;
+    const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pv_pad, dim3(nb), dim3(256), 0, st, B, tot, cap);
+    // group ids < 2 x cap: stable LSD radix on 8-bit digits (each value's accesses stay in access order)
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < 2ull * cap) ++bits;
+    const int passes = (bits + 7) / 8;
+    const uint32_t nblocks = (cap + tile - 1) / tile;
+    uint32_t *kin = B.gid, *vin = B.idx, *kout = B.gid2, *vout = B.idx2;
+    for (int p = 0; p < passes; ++p) {
+        e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
+        if (e == hipSuccess) e = scan(hist, hist, (uint64_t)nblocks << 8, part, nullptr, st);
+        if (e == hipSuccess) e = radix_scatter(kin, vin, cap, p * 8, hist, nblocks, kout, vout, nullptr, st);
+        if (e != hipSuccess) return e;
+        uint32_t* tk = kin; kin = kout; kout = tk;
+        uint32_t* tv = vin; vin = vout; vout = tv;
+    }
+    if (kin != B.gid) {  // sorted arrays back into gid / idx (an odd number of passes)
+        e = hipMemcpyAsync(B.gid, kin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(B.idx, vin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 // the value-parallel pre pass over the wide XF_MIX list (cap accesses at most); pv[] tells k_pq which segments
 // are done.  Scratch: PvBuf arrays of cap entries (chunks: cap / PV_CH + m), htab 2 x cap, radix scratch (hist,
 // part), tot (device words: [0] accesses, [1] chunks, [2] ranges).  jumps: the batch has no zero-acquire ENTRY.
@@ -716,33 +1025,48 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
     hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
     hipLaunchKernelGGL(k_pv_fill, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot);
     const uint32_t nb = (cap + 255) / 256;
-    hipLaunchKernelGGL(k_pv_pad, dim3(nb), dim3(256), 0, st, B, tot, cap);
-    // group ids < 2 x cap: stable LSD radix on 8-bit digits (each value's accesses stay in access order)
-    int bits = 1;
-    while (bits < 32 && (1ull << bits) < 2ull * cap) ++bits;
-    const int passes = (bits + 7) / 8;
-    const uint32_t nblocks = (cap + tile - 1) / tile;
-    uint32_t *kin = B.gid, *vin = B.idx, *kout = B.gid2, *vout = B.idx2;
-    for (int p = 0; p < passes; ++p) {
-        e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
-        if (e == hipSuccess) e = scan(hist, hist, (uint64_t)nblocks << 8, part, nullptr, st);
-        if (e == hipSuccess) e = radix_scatter(kin, vin, cap, p * 8, hist, nblocks, kout, vout, nullptr, st);
-        if (e != hipSuccess) return e;
-        uint32_t* tk = kin; kin = kout; kout = tk;
-        uint32_t* tv = vin; vin = vout; vout = tv;
-    }
-    if (kin != B.gid) {  // sorted arrays back into gid / idx (an odd number of passes)
-        e = hipMemcpyAsync(B.gid, kin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(B.idx, vin, (uint64_t)cap * 4, hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
-    }
+    e = pv_sort(B, cap, tot, hist, part, st, radix_hist, radix_scatter, scan, tile);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
     hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_gather, dim3(nb), dim3(256), 0, st, segs, list, B, tot);
     hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags);
     hipLaunchKernelGGL(k_pv_ranges, dim3(2048), dim3(256), 0, st, recs, B, tot, cap, dec);
-    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags);
+    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 0u, segs, list, nullptr);
     return hipGetLastError();
 }
+
+// the post pass over the wide XF_MIX list (after the final verdicts; before k_pq's post pass, which leaves the
+// segments with SEG_PVT); tot: 4 device words of its own
+hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                      const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
+                      uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
+                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
+                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                      uint32_t tile) {
+    if (!m || !cap) return hipSuccess;
+    const uint32_t nchunk = cap / PV_CH + m + 1;
+    hipError_t e = hipMemsetAsync(tot, 0, 16, st);
+    if (e == hipSuccess) e = hipMemsetAsync(B.htab, 0xFF, 2ull * cap * 8, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pvt_prep, dim3((m + 255) / 256), dim3(256), 0, st, segs, list, m, S, pv);
+    hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
+    hipLaunchKernelGGL(k_pvt_reach, dim3(nchunk), dim3(256), 0, st, recs, segs, list, S, pv, B, tot, dec);
+    hipLaunchKernelGGL(k_pvt_count, dim3(nchunk), dim3(256), 0, st, recs, ev, vals, segs, list, S, cfg, pv, B, tot, dec);
+    hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
+    hipLaunchKernelGGL(k_pvt_fill, dim3(nchunk), dim3(256), 0, st, recs, ev, vals, segs, list, S, cfg, pv, B, tot, dec);
+    e = pv_sort(B, cap, tot, hist, part, st, radix_hist, radix_scatter, scan, tile);
+    if (e != hipSuccess) return e;
+    const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pvt_walk, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    e = scan(reinterpret_cast<const uint32_t*>(B.prev), reinterpret_cast<uint32_t*>(B.sprev), cap, part, nullptr, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pvt_peak, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.sprev), tot, pv);
+    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 1u, segs, list, tot + 3);
+    return hipGetLastError();
+}
+
 } // namespace sg

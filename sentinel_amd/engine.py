@@ -24,7 +24,7 @@ EXPORTS = (
     "sg_load_flow_rules", "sg_load_degrade_rules", "sg_load_param_rules", "sg_param_key", "sg_submit",
     "sg_submit_async", "sg_sync", "sg_snapshot_metrics", "sg_cluster_set_connected_count",
     "sg_cluster_request_tokens", "sg_cluster_request_param_tokens", "sg_read_node", "sg_last_error", "sg_last_timings",
-    "sg_submit_ex", "sg_submit_ex_async", "sg_intern_origin", "sg_intern_context",
+    "sg_submit_ex", "sg_submit_ex_async", "sg_intern_origin", "sg_intern_context", "sg_param_thread_count",
 )
 
 
@@ -233,15 +233,16 @@ class Engine:
         return {"second": out[:16].reshape(2, 8), "thread": int(out[16]), "mhist": out[17:21].reshape(2, 2)}
 
     def pv_last(self) -> dict:
-        """The last batch's value-parallel pre pass (diagnostics export sgx_pv_last): segments, accesses,
-        blocked stretches its walk jumped."""
+        """The last batch's value-parallel pre pass (diagnostics export sgx_pv_last): pre pass segments,
+        accesses, blocked stretches its walk jumped; post pass segments eligible, ops, segments committed."""
         fn = lib().sgx_pv_last
         fn.restype = C.c_int
         fn.argtypes = [C.c_void_p, C.c_void_p]
-        out = np.zeros(3, dtype=np.uint64)
+        out = np.zeros(6, dtype=np.uint64)
         if fn(self.h, out.ctypes.data) != 0:
             raise SentinelError(A.SG_EDEVICE, "sgx_pv_last failed")
-        return {"segments": int(out[0]), "accesses": int(out[1]), "ranges": int(out[2])}
+        return {"segments": int(out[0]), "accesses": int(out[1]), "ranges": int(out[2]),
+                "post_segments": int(out[3]), "post_ops": int(out[4]), "post_done": int(out[5])}
 
     def param_pool(self) -> dict:
         """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last layout,
@@ -253,6 +254,16 @@ class Engine:
         if fn(self.h, out.ctypes.data) != 0:
             raise SentinelError(A.SG_EDEVICE, "sgx_param_pool failed")
         return {"buckets": int(out[0]), "taken": int(out[1]), "floor": int(out[2]), "compactions": int(out[3])}
+
+    def param_thread_count(self, res: int, idx: int, key: int, with_presence: bool = False):
+        """ParameterMetric.getThreadCount (sg_param_thread_count): the value's count in the thread-count map of
+        paramIdx idx, 0 if absent; with_presence: (count, present).  Does not reorder the map's LRU."""
+        fn = lib().sg_param_thread_count
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+        c, p = C.c_int64(), C.c_int32()
+        _check(fn(self.h, res, idx, key, C.byref(c), C.byref(p)))
+        return (c.value, bool(p.value)) if with_presence else c.value
 
     def read_node(self, res: int, now: int = 0) -> dict:
         st = A.SgNodeState()

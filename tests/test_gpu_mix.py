@@ -35,6 +35,18 @@ def _cmp(eng, orc, ev, what, ext=None):
     return dg
 
 
+def _thread_maps(eng, orc, ev, res, per=1500):
+    # ParameterMetric.getThreadCount of paramIdx 0 for the values the resources saw (the last read: the oracle's
+    # get moves the value in its LRU order)
+    for r in res:
+        m = (ev["res_id"] == r) & (ev["kind"] == A.EV_ENTRY) & ((ev["flags"] & A.F_HAS_ARG) != 0)
+        keys = np.unique(ev["aux"][m])[:per]
+        g = [eng.param_thread_count(int(r), 0, int(k)) for k in keys]
+        o = [orc.param_thread_count(int(r), 0, int(k)) for k in keys]
+        bad = [i for i in range(len(keys)) if g[i] != o[i]]
+        assert not bad, ("thread count", int(r), hex(int(keys[bad[0]])), g[bad[0]], o[bad[0]], len(bad))
+
+
 def _nodes(eng, orc, res):
     for r in res:
         g, o = eng.read_node(int(r)), orc.read_node(int(r))
@@ -60,10 +72,12 @@ def test_mix_c6_shapes(nval, pv, monkeypatch):
     w.install(orc)
     cuts = np.linspace(0, len(ev), 4).astype(np.int64)
     dg = np.concatenate([_cmp(eng, orc, ev[a:b], "batch %d" % i) for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:]))])
-    if pv == "1":  # the value-parallel pass took the long segments
+    if pv == "1":  # the value-parallel passes took the long segments
         st = eng.pv_last()
         assert st["segments"] >= 3 and st["accesses"] > 20_000, st
+        assert st["post_segments"] >= 3 and st["post_done"] >= 3 and st["post_ops"] > 1000, st
     cnt = np.bincount(ev["res_id"], minlength=n_res)
+    _thread_maps(eng, orc, ev, np.argsort(-cnt)[:4])
     assert cnt.max() > 3 * 2 * 8192 and ((cnt > 3 * 1100) & (cnt < 3 * 8000)).sum() > 10  # wide and narrow passes
     _nodes(eng, orc, range(n_res))
     st = dg[ev["kind"] == A.EV_ENTRY] & 0xFF
