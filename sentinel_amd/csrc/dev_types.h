@@ -255,7 +255,7 @@ struct PvSeg {
     uint32_t freach;    // post pass: segment position + 1 of the first ENTRY visiting rule k0 (EXITs release from it)
     int32_t peak;       // post pass: the thread-count map's largest growth over its start size
     uint32_t tm0;       // post pass: EXITs release from position 0 (the node had the bits already)
-    uint32_t pad;
+    uint32_t sub;       // post pass: the segment releases thread counts (else increments only: LRU residency)
 };
 
 struct PvBuf {          // dense per-access arrays (capacity >= the listed segments' events)

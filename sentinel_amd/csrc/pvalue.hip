@@ -89,6 +89,24 @@ __device__ __forceinline__ uint32_t pv_scan(uint32_t v, uint32_t* red, uint32_t*
     return pre + x - v;
 }
 
+// the map's per-word live-stamp prefix counts in stamp order from thr (ppre: free scratch of this map here), by
+// a 256-lane workgroup
+__device__ void pv_ring_prefix(const DevState& S, const PMap& mp, uint32_t* red) {
+    const uint32_t W = 1u << (mp.rb_log2 - 6), w0 = pv_word(mp, mp.thr);
+    const uint32_t per = (W + 255) / 256, l0 = threadIdx.x * per;
+    uint32_t c = 0;
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) c += (uint32_t)__popcll(S.pbm[mp.bm + ((w0 + l0 + u) & (W - 1))]);
+    uint32_t t2;
+    uint32_t run = pv_scan<4>(c, red, &t2);
+    for (uint32_t u = 0; u < per; ++u)
+        if (l0 + u < W) {
+            const uint32_t w = (w0 + l0 + u) & (W - 1);
+            S.ppre[mp.bm + w] = run;
+            run += (uint32_t)__popcll(S.pbm[mp.bm + w]);
+        }
+}
+
 // ---- prep: one workgroup per listed segment: eligibility, the map's ring prefix counts, extraction chunks
 #define PV_CH 4096u  // positions per extraction chunk
 __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
@@ -112,21 +130,7 @@ __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const u
         return;
     }
     const DRule& r = S.rules[pg.rule_off + k1];
-    // the map's per-word live-stamp prefix counts in stamp order from thr (ppre: free scratch of this map here)
-    const PMap mp = S.pmap[r.pmap];
-    const uint32_t W = 1u << (mp.rb_log2 - 6), w0 = pv_word(mp, mp.thr);
-    const uint32_t per = (W + 255) / 256, l0 = tid * per;
-    uint32_t c = 0;
-    for (uint32_t u = 0; u < per; ++u)
-        if (l0 + u < W) c += (uint32_t)__popcll(S.pbm[mp.bm + ((w0 + l0 + u) & (W - 1))]);
-    uint32_t t2;
-    uint32_t run = pv_scan<4>(c, red, &t2);
-    for (uint32_t u = 0; u < per; ++u)
-        if (l0 + u < W) {
-            const uint32_t w = (w0 + l0 + u) & (W - 1);
-            S.ppre[mp.bm + w] = run;
-            run += (uint32_t)__popcll(S.pbm[mp.bm + w]);
-        }
+    pv_ring_prefix(S, S.pmap[r.pmap], red);
     if (tid == 0) {
         PvSeg o{};
         o.ok = 1; o.mid = r.pmap; o.rk = (uint32_t)k1; o.nch = (sg.len + PV_CH - 1) / PV_CH;
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(256) void k_pv_fill(const SEv* __restrict__ recs, c
 // padding of the sort arrays beyond the accesses: [tot, cap) sorts last
 __global__ void k_pv_pad(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < cap && g >= *tot) { B.gid[g] = 0xFFFFFFFFu; B.idx[g] = g; B.prev[g] = 0; }
+    if (g < cap && g >= *tot) { B.gid[g] = 0xFFFFFFFFu; B.idx[g] = g; B.tc[g] = 0; }
 }
 
 // ---- prev / first accesses (sorted order: after the sort B.gid / B.idx hold the sorted keys / accesses)
@@ -502,10 +506,14 @@ __global__ __launch_bounds__(256) void k_pv_ranges(SEv* __restrict__ recs, PvBuf
 
 // ==== the post pass (ParamFlowStatisticEntryCallback / ExitCallback from the final verdicts, k_pq PQ_POST):
 // thread-count map of paramIdx 0, ParameterMetric.java:117-241 -- a passed ENTRY adds (putIfAbsent then increment),
-// an EXIT of a passed ENTRY releases (an absent value is put at 0; at <= 0 removed).  Under the hypothesis that
-// the map never grows beyond cap within the segment (no eviction), each value's ops are independent: one lane per
-// value walks them, the map's size over the segment is a scan of the walks' +1 / -1, and the commit keeps every
-// value present at its last op.  A segment whose peak passes cap is left to k_pq's sequential replay.
+// an EXIT of a passed ENTRY releases (an absent value is put at 0; at <= 0 removed).  Two cases per segment:
+//   increments only (no release: C6's EXITs carry no args) -- every op touches and inserts, so residency is the
+//     pre pass's LRU stack distance (k_pv_prev / blocks / resid over the thread-count map) and a value's count
+//     restarts at 1 after each miss; the commit keeps the cap most recent, as the pre pass's;
+//   with releases -- removals break the stack distance; under the hypothesis that the map never grows beyond cap
+//     within the segment (no eviction) each value's ops are independent: one lane per value walks them, the map's
+//     size over the segment is a scan of the walks' +1 / -1, and the commit keeps every value present at its last
+//     op.  A segment whose peak passes cap is left to k_pq's sequential replay.
 #define PVT_ADD 1u
 #define PVT_SUB 3u
 
@@ -561,37 +569,45 @@ __device__ __forceinline__ uint32_t pvt_op(const SEv& e, uint32_t p, const Seg& 
     return op;
 }
 
-// per listed segment (a lane each): eligibility -- a chain, a thread-count map of paramIdx 0 that is on, within the
-// commit's LDS, no THREAD-grade rule (XF_MIX) -- and the first rule whose visit sets the map's bit (k0)
-__global__ void k_pvt_prep(const Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m, DevState S,
-                           PvSeg* __restrict__ pv) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// per listed segment (a workgroup each): eligibility -- a chain, a thread-count map of paramIdx 0 that is on, within
+// the commit's LDS, no THREAD-grade rule (XF_MIX) -- the first rule whose visit sets the map's bit (k0), the map's
+// ring prefix counts (ranks of the increments-only case)
+__global__ __launch_bounds__(256) void k_pvt_prep(const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                  uint32_t m, DevState S, PvSeg* __restrict__ pv) {
+    __shared__ uint32_t red[4];
+    __shared__ uint32_t okf;
+    const uint32_t i = blockIdx.x;
     if (i >= m) return;
     const Seg sg = segs[list[i]];
     const Prog pg = S.prog[sg.res];
     const uint32_t flags = S.info[sg.res].flags;
     const uint32_t tm = pg.tm_base == NO_ID ? NO_ID : S.tmid[pg.tm_base];
-    PvSeg o{};
-    uint32_t all_bits = NI_PM, k0 = 0xFFFFFFFFu;
-    bool thr = false;
-    for (int k = 0; k < pg.n_param; ++k) {
-        const DRule& r = S.rules[pg.rule_off + k];
-        const uint32_t b = pvt_kbits(r);
-        all_bits |= b;
-        if (k0 == 0xFFFFFFFFu && (b & ni_tm(0))) k0 = (uint32_t)k;
-        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_THREAD) thr = true;
+    if (threadIdx.x == 0) {
+        PvSeg o{};
+        uint32_t all_bits = NI_PM, k0 = 0xFFFFFFFFu;
+        bool thr = false;
+        for (int k = 0; k < pg.n_param; ++k) {
+            const DRule& r = S.rules[pg.rule_off + k];
+            const uint32_t b = pvt_kbits(r);
+            all_bits |= b;
+            if (k0 == 0xFFFFFFFFu && (b & ni_tm(0))) k0 = (uint32_t)k;
+            if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_THREAD) thr = true;
+        }
+        bool ok = (flags & NI_CHAIN) && tm != NO_ID && S.key_ring && !thr && ((flags | all_bits) & ni_tm(0));
+        if (ok) {
+            const PMap mp = S.pmap[tm];
+            ok = mp.cap <= PQ_MAX_CAP && (mp.rb_log2 - 6) <= 9;
+        }
+        if (ok) {
+            o.ok = 1; o.mid = tm; o.rk = k0; o.nch = (sg.len + PV_CH - 1) / PV_CH;
+            o.freach = 0xFFFFFFFFu;
+            o.tm0 = (flags & (NI_PM | ni_tm(0))) == (NI_PM | ni_tm(0)) ? 1u : 0u;
+        }
+        pv[i] = o;
+        okf = o.ok;
     }
-    bool ok = (flags & NI_CHAIN) && tm != NO_ID && S.key_ring && !thr && ((flags | all_bits) & ni_tm(0));
-    if (ok) {
-        const PMap mp = S.pmap[tm];
-        ok = mp.cap <= PQ_MAX_CAP && (mp.rb_log2 - 6) <= 9;
-    }
-    if (ok) {
-        o.ok = 1; o.mid = tm; o.rk = k0; o.nch = (sg.len + PV_CH - 1) / PV_CH;
-        o.freach = 0xFFFFFFFFu;
-        o.tm0 = (flags & (NI_PM | ni_tm(0))) == (NI_PM | ni_tm(0)) ? 1u : 0u;
-    }
-    pv[i] = o;
+    __syncthreads();
+    if (okf) pv_ring_prefix(S, S.pmap[tm], red);
 }
 
 // per chunk: the rules its ENTRYs visited (the node's bits) and the first ENTRY visiting rule k0
@@ -632,7 +648,7 @@ __global__ __launch_bounds__(256) void k_pvt_reach(const SEv* __restrict__ recs,
 __global__ __launch_bounds__(256) void k_pvt_count(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
                                                    const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                                                    const uint32_t* __restrict__ list, DevState S, DevCfg cfg,
-                                                   const PvSeg* __restrict__ pv, PvBuf B, const uint32_t* __restrict__ tot,
+                                                   PvSeg* __restrict__ pv, PvBuf B, const uint32_t* __restrict__ tot,
                                                    const uint32_t* __restrict__ dec) {
     __shared__ uint32_t red[4];
     const uint32_t c = blockIdx.x, tid = threadIdx.x;
@@ -642,14 +658,17 @@ __global__ __launch_bounds__(256) void k_pvt_count(const SEv* __restrict__ recs,
     const Seg sg = segs[list[ch.x]];
     const uint32_t tm_from = ps.tm0 ? 0u : ps.freach;
     const uint32_t end = sg.len - ch.y < PV_CH ? sg.len : ch.y + PV_CH;
-    uint32_t cnt = 0;
+    uint32_t cnt = 0, sub = 0;
     for (uint32_t p = ch.y + tid; p < end; p += 256) {
         uint64_t key;
-        cnt += pvt_op(recs[sg.start + p], p, sg, tm_from, ev, vals, S, cfg, dec, key) ? 1u : 0u;
+        const uint32_t op = pvt_op(recs[sg.start + p], p, sg, tm_from, ev, vals, S, cfg, dec, key);
+        cnt += op ? 1u : 0u;
+        sub |= op == PVT_SUB ? 1u : 0u;
     }
     uint32_t t;
     (void)pv_scan<4>(cnt, red, &t);
     if (tid == 0) B.ccnt[c] = t;
+    if (sub) pv[ch.x].sub = 1;  // (any lane: one value)
 }
 
 // per chunk: the ops in order into the dense arrays (acq: the op), group ids from the segment's table
@@ -681,7 +700,8 @@ __global__ __launch_bounds__(256) void k_pvt_fill(const SEv* __restrict__ recs, 
             B.pos[g] = p;
             B.acq[g] = op;
             B.seg[g] = ch.x;
-            B.prev[g] = 0;
+            B.tc[g] = 0;
+            B.prev[g] = PV_NONE;
             B.w[g] = -1;
             B.fslot[g] = -1;
             B.keep[g] = 0;
@@ -702,7 +722,10 @@ __global__ __launch_bounds__(256) void k_pvt_fill(const SEv* __restrict__ recs, 
     }
 }
 
-// one lane per value (sorted order): probe the map, walk the ops; prev[g] = the op's change of the map's size
+// one lane per value (sorted order; k_pv_prev probed the map at its first op: w = rank or PV_INF, flast = count).
+// Increments only: c + 1 on a hit, 1 on a miss (put(v, 1) after an eviction); the value stays iff fewer than cap
+// distinct values follow its last op.  With releases: the ops' state machine, tc[g] = the op's change of the
+// map's size.
 __global__ void k_pvt_walk(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S) {
     const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = tot[0];
@@ -710,52 +733,44 @@ __global__ void k_pvt_walk(PvBuf B, const uint32_t* __restrict__ tot, const PvSe
     const uint32_t gd = B.gid[q0];
     if (q0 > 0 && B.gid[q0 - 1] == gd) return;
     uint32_t qb = q0 + 1;
-    while (qb < n && B.gid[qb] == gd) ++qb;  // (a value's ops: passed ENTRYs and their EXITs, few)
+    while (qb < n && B.gid[qb] == gd) ++qb;  // (a value's ops: its passed ENTRYs and their EXITs)
     const uint32_t g0 = B.idx[q0];
     const PvSeg ps = pv[B.seg[g0]];
-    const PMap mp = S.pmap[ps.mid];
-    const uint64_t key = B.key[g0];
-    uint32_t b1, b2;
-    pm_buckets(mp.nb, key, b1, b2);
-    const PBucket* BK = S.pbkt + mp.base;
-    int32_t slot = -1;
-    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b2].key[j] == key) slot = (int32_t)(b2 * PM_BKT + j);
-    for (int j = PM_BKT - 1; j >= 0; --j) if (BK[b1].key[j] == key) slot = (int32_t)(b1 * PM_BKT + j);
-    bool pres = false;
-    int64_t c = 0;
-    if (slot >= 0 && pm_live(mp, S.pbm + mp.bm, BK[slot / PM_BKT].stamp[slot % PM_BKT])) {
-        pres = true;
-        c = S.pdat[mp.base * PM_BKT + slot].v0;
-    }
-    B.fslot[g0] = slot;
-    B.w[g0] = pres ? 0 : PV_INF;
-    for (uint32_t q = q0; q < qb; ++q) {
-        const uint32_t g = B.idx[q];
-        int32_t d = 0;
-        if (B.acq[g] == PVT_ADD) {
-            if (pres) ++c;
-            else { pres = true; c = 1; d = 1; }
-        } else {
-            if (!pres) { pres = true; c = 0; d = 1; }
-            else if (--c <= 0) { pres = false; c = 0; d = -1; }
-        }
-        B.prev[g] = d;
-    }
+    bool pres = B.w[g0] != PV_INF;
+    int64_t c = pres ? B.flast[g0] : 0;
     const uint32_t g = B.idx[qb - 1];
-    B.keep[g] = pres ? 1 : 0;
+    if (!ps.sub) {
+        for (uint32_t q = q0; q < qb; ++q) c = B.hit[B.idx[q]] ? c + 1 : 1;
+        const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
+        B.keep[g] = pv_count_lt(B, g, (int64_t)ps.off + ps.n, (int32_t)g, cap) < cap ? 1 : 0;
+    } else {
+        for (uint32_t q = q0; q < qb; ++q) {
+            const uint32_t gq = B.idx[q];
+            int32_t d = 0;
+            if (B.acq[gq] == PVT_ADD) {
+                if (pres) ++c;
+                else { pres = true; c = 1; d = 1; }
+            } else {
+                if (!pres) { pres = true; c = 0; d = 1; }
+                else if (--c <= 0) { pres = false; c = 0; d = -1; }
+            }
+            B.tc[gq] = d;
+        }
+        B.keep[g] = pres ? 1 : 0;
+    }
     B.flast[g] = c;
     B.ftok[g] = 0;
-    B.fslot[g] = slot;
+    B.fslot[g] = B.fslot[g0];
 }
 
-// the map's size over the segment: peak growth over its start size (X: exclusive scan of prev as uint32)
+// the map's size over the segment: peak growth over its start size (X: exclusive scan of tc as uint32)
 __global__ void k_pvt_peak(PvBuf B, const uint32_t* __restrict__ X, const uint32_t* __restrict__ tot,
                            PvSeg* __restrict__ pv) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = g < tot[0];
     const uint32_t s = in ? B.seg[g] : 0xFFFFFFFFu;
     int32_t v = 0;
-    if (in) v = (int32_t)(X[g] + (uint32_t)B.prev[g] - X[pv[s].off]);
+    if (in) v = (int32_t)(X[g] + (uint32_t)B.tc[g] - X[pv[s].off]);
     const uint32_t s0 = (uint32_t)__shfl((int)s, 0, 64);
     if (__all(s == s0)) {  // one segment in the wave: one atomic
         for (int o = 32; o > 0; o >>= 1) { const int32_t y = __shfl_xor(v, o, 64); v = y > v ? y : v; }
@@ -787,7 +802,8 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     PMap mp = S.pmap[ps.mid];
     const uint32_t W = 1u << (mp.rb_log2 - 6);
     const int32_t cap = (int32_t)mp.cap;
-    if (tmode && (int64_t)mp.live + ps.peak > (int64_t)cap) return;  // an eviction: the sequential replay's
+    const bool kcount = tmode && ps.sub;  // the kept values are the ones present at their last op
+    if (kcount && (int64_t)mp.live + ps.peak > (int64_t)cap) return;  // an eviction: the sequential replay's
     PBucket* BK = S.pbkt + mp.base;
     PData* DT = S.pdat + mp.base * PM_BKT;
     const uint32_t nslot = mp.nb * PM_BKT;
@@ -799,9 +815,9 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     uint32_t ng = 0;
     for (uint32_t k = tid; k < ps.n; k += 1024) {
         const uint32_t g = ps.off + k;
-        if (tmode) ng += B.keep[g];
+        if (kcount) ng += B.keep[g];
         if (B.w[g] >= 0) {  // a value's first access
-            if (!tmode) ++ng;
+            if (!kcount) ++ng;
             const int32_t sl = B.fslot[g];
             if (sl >= 0 && B.w[g] != PV_INF) {
                 const int64_t s = BK[sl / PM_BKT].stamp[sl % PM_BKT];
@@ -812,7 +828,7 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     }
     uint32_t G;
     (void)pv_scan<16>(ng, red, &G);
-    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay (tmode: G kept)
+    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay (kcount: G kept)
     // (2) untouched live values: the (cap - KA) most recent stay; prefix counts of untouched stamps from thr
     const uint32_t w0 = pv_word(mp, mp.thr);
     {
@@ -1052,7 +1068,7 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
     hipError_t e = hipMemsetAsync(tot, 0, 16, st);
     if (e == hipSuccess) e = hipMemsetAsync(B.htab, 0xFF, 2ull * cap * 8, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pvt_prep, dim3((m + 255) / 256), dim3(256), 0, st, segs, list, m, S, pv);
+    hipLaunchKernelGGL(k_pvt_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv);
     hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
     hipLaunchKernelGGL(k_pvt_reach, dim3(nchunk), dim3(256), 0, st, recs, segs, list, S, pv, B, tot, dec);
     hipLaunchKernelGGL(k_pvt_count, dim3(nchunk), dim3(256), 0, st, recs, ev, vals, segs, list, S, cfg, pv, B, tot, dec);
@@ -1061,10 +1077,14 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
     e = pv_sort(B, cap, tot, hist, part, st, radix_hist, radix_scatter, scan, tile);
     if (e != hipSuccess) return e;
     const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
+    hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pvt_walk, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
-    e = scan(reinterpret_cast<const uint32_t*>(B.prev), reinterpret_cast<uint32_t*>(B.sprev), cap, part, nullptr, st);
+    // (the peak of the segments with releases; the scan's output in gdt: free in the post pass)
+    e = scan(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, part, nullptr, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pvt_peak, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.sprev), tot, pv);
+    hipLaunchKernelGGL(k_pvt_peak, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.gdt), tot, pv);
     hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 1u, segs, list, tot + 3);
     return hipGetLastError();
 }
