@@ -572,6 +572,7 @@ struct sg_engine {
     // gets (GPU_MAX_HW_QUEUES): a fifth stream would share a queue and serialise behind another's kernels
     hipStream_t bin_stream[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    hipEvent_t fork0 = nullptr;  // XF_MIX batches: the pre passes on bin_stream[1] start here, beside the lane bins
     bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
@@ -580,7 +581,7 @@ struct sg_engine {
     uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
     bool mix_on = true;         // XF_MIX programs (SG_MIX=0: every param + flow / degrade resource one lane)
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
-    bool pv_on = false;         // SG_PV=1: the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
+    bool pv_on = true;          // SG_PV (default 1): the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
     PvBuf pvb{};                // its scratch (decide stage only: one set)
     uint64_t pv_cap = 0;
     PvSeg* d_pvseg = nullptr;
@@ -1166,7 +1167,9 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
     for (auto& s : e->bin_stream)
         if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
-    if (hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
+    if (hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->fork0, hipEventDisableTiming) != hipSuccess)
+        return bad(fail(SG_EDEVICE, "event"));
     for (auto& v : e->join)
         if (hipEventCreateWithFlags(&v, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
     if (const char* d = std::getenv("SG_DEBUG")) {
@@ -1309,6 +1312,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->gstream) (void)hipStreamDestroy(e->gstream);
     for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
     if (e->fork) (void)hipEventDestroy(e->fork);
+    if (e->fork0) (void)hipEventDestroy(e->fork0);
     for (auto& s : e->bin_stream) if (s) (void)hipStreamDestroy(s);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2226,6 +2230,16 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // XF_MIX segments of the cooperative bins: their param checks first (k_pq pre pass), the owners then decide
     // the flow / degrade chain on them
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
+    // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
+    const bool serial_bins = (e->dbg_flags & 8) != 0;
+    // the pre passes concern the cooperative XF_MIX segments only: they run on bin_stream[1] (whose J4 / J1 wait
+    // for them anyway) while the lane bins, which check their params inline, start on the main stream
+    const bool pre_split = (n_mix || n_mixw) && !serial_bins;
+    hipStream_t ps = pre_split ? e->bin_stream[1] : st;
+    if (pre_split) {
+        HIPCHK(hipEventRecord(e->fork0, st));
+        HIPCHK(hipStreamWaitEvent(ps, e->fork0, 0));
+    }
     if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
         if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;  // (before this batch's decide work is queued)
         e->pv_last_m = n_mixw;
@@ -2233,18 +2247,37 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
         HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
                          e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
-                         (bflags & BF_ZERO_CNT) ? 0u : 1u, st, launch_radix_hist,
+                         (bflags & BF_ZERO_CNT) ? 0u : 1u, ps, launch_radix_hist,
                          launch_radix_scatter, launch_scan, radix_tile()));
     }
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
-                             e->d_dec, e->d_bsmall + 0, st));
-    HIPCHK(hipEventRecord(e->fork, st));
+                             e->d_dec, e->d_bsmall + 0, ps));
+    HIPCHK(hipEventRecord(e->fork, ps));
+    auto lane_bins = [&]() -> int {
+        {
+            DevState Sl = S;
+            Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..36]
+            HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
+                                     off[BIN_LANE + LANE_BINS] - off[BIN_LANE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+        }
+        HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
+                                 off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+        {
+            DevState Sl = S;
+            Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..37]
+            HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
+                                     off[BIN_LITE + LANE_BINS] - off[BIN_LITE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+        }
+        return SG_OK;
+    };
+    if (pre_split) {
+        if (int lrc = lane_bins()) return lrc;
+        HIPCHK(hipStreamWaitEvent(st, e->fork, 0));  // (J8 / J1 on the main stream read the pre passes' verdicts)
+    }
     // J16 and J4 on their own streams; J1 after the lane bins on the main stream (J4 + J1 in series was the
     // longest chain of the decide stage)
     const int coop[2] = {BIN_J16, BIN_J4};
-    // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
-    const bool serial_bins = (e->dbg_flags & 8) != 0;
     // J8 (the QPS-DefaultController heads) takes J16's stream when every head is of that kind (C2, C4); beside
     // THREAD-grade / WarmUp heads (C3: J16 is the decide stage's longest chain) it runs first on the main stream
     const bool j8_own = bin_n[BIN_J8] && !bin_n[BIN_J16];
@@ -2280,20 +2313,8 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                          e->d_bsmall + 0, bs));
         HIPCHK(hipEventRecord(e->join[c], bs));
     }
-    {
-        DevState Sl = S;
-        Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..36]
-        HIPCHK(launch_decide_bin(BIN_LANE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE],
-                                 off[BIN_LANE + LANE_BINS] - off[BIN_LANE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
-    }
-    HIPCHK(launch_decide_bin(BIN_LANE16, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LANE16],
-                             off[BIN_LANE16 + LANE_BINS] - off[BIN_LANE16], S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
-    {
-        DevState Sl = S;
-        Sl.dbg = e->d_dbg;  // SG_KPROF builds: lane-kernel phase cycles in dbg[32..37]
-        HIPCHK(launch_decide_bin(BIN_LITE, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_LITE],
-                                 off[BIN_LITE + LANE_BINS] - off[BIN_LITE], Sl, dc, t0, e->d_dec, e->d_bsmall + 0, st));
-    }
+    if (!pre_split)
+        if (int lrc = lane_bins()) return lrc;
     if (bin_n[BIN_J1]) {
         DevState Sj = S;
         Sj.dbg = (e->prof_bin == 2 && e->d_dbg) ? e->d_dbg : nullptr;
