@@ -33,6 +33,10 @@ hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uin
 // db = digit bits (8 or 10)
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st);
+hipError_t launch_radix_hist_n(const uint32_t* keys, uint64_t n, const uint32_t* ndev, int shift, uint32_t* ghist,
+                               uint32_t nblocks, hipStream_t st);
+hipError_t launch_radix_scatter_n(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev, int shift,
+                                  const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
 uint32_t radix_tile();
@@ -61,24 +65,24 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
                      uint32_t* bflags, hipStream_t st);
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
-                          uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
+                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, hipStream_t st);
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
                               uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
 hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                      const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
                      PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
                      hipStream_t st,
-                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
-                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                                 uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                      uint32_t tile);
 hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                       const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
                       uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
-                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
-                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t tile);
 hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
@@ -467,7 +471,9 @@ struct sg_engine {
     std::vector<uint32_t> tm_base;                              // per resource: Prog.tm_base
     uint64_t n_pslot = 0;                                       // bucket slots in the pool (param_table_log2 bound)
     uint64_t pool_nb = 0;                                       // pool buckets (regions grow into it: k_pm_grow)
-    unsigned long long* d_pool_next = nullptr;                  // next free pool bucket
+    unsigned long long* d_pool_next = nullptr;
+    uint4* d_pmoves = nullptr;  // k_pm_grow's move list (one entry a map) + its count word at [pmoves_cap]
+    uint64_t pmoves_cap = 0;                  // next free pool bucket
     unsigned long long* h_pool_next = nullptr;                  // pinned copy, refreshed by every batch (compaction)
     uint64_t n_compact = 0;                                     // pool compactions (diagnostics)
     uint64_t pool_floor = 0;                                    // pool buckets the regions took at the last layout
@@ -1257,10 +1263,11 @@ extern "C" int sgx_read_aux_node(sg_engine* e, uint32_t res, uint32_t kind, uint
     return 0;
 }
 // diagnostics export: the last batch's value-parallel passes (pvalue.hip), out = {pre pass: listed segments it decided,
-// accesses, blocked stretches the walk jumped; post pass: segments eligible, ops, segments committed}
+// accesses, blocked stretches the walk jumped; post pass: segments eligible, ops, segments committed; the pre
+// pass's longest walk (steps, when over 256)}
 extern "C" int sgx_pv_last(sg_engine* e, unsigned long long* out) {
     if (!e || !out || drain(e) != SG_OK) return -1;
-    out[0] = out[1] = out[2] = out[3] = out[4] = out[5] = 0;
+    out[0] = out[1] = out[2] = out[3] = out[4] = out[5] = out[6] = 0;
     if (!e->d_pvseg || !e->d_pvtot || !e->pv_last_m) return 0;
     std::vector<PvSeg> v(e->pv_last_m);
     uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1269,13 +1276,14 @@ extern "C" int sgx_pv_last(sg_engine* e, unsigned long long* out) {
     for (const auto& s : v) out[0] += s.ok ? 1 : 0;
     out[1] = tot[0];
     out[2] = tot[2];
+    out[6] = tot[3];
     if (e->pvt_on && e->d_pvtseg) {
         if (hipMemcpy(v.data(), e->d_pvtseg, v.size() * sizeof(PvSeg), hipMemcpyDeviceToHost) != hipSuccess) return -1;
         for (const auto& s : v) out[3] += s.ok ? 1 : 0;
         out[4] = tot[4];
         out[5] = tot[7];
     }
-    if (!e->pv_on) out[0] = out[1] = out[2] = 0;
+    if (!e->pv_on) out[0] = out[1] = out[2] = out[6] = 0;
     return 0;
 }
 // diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last layout, compactions}
@@ -1296,7 +1304,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
     dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
-    dfree(e->d_pool_next);
+    dfree(e->d_pool_next); dfree(e->d_pmoves);
     if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
     free_pv(e);
     dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot);
@@ -1793,6 +1801,11 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     e->tm_base = tb;
     e->rmap_cap = rcap;
     e->tmaps = tmaps;
+    if (keys.size() > e->pmoves_cap) {  // (the stream is drained: rebuild_pmaps synchronised it above)
+        dfree(e->d_pmoves);
+        e->pmoves_cap = keys.size();
+        HIPCHK(hipMalloc(&e->d_pmoves, (e->pmoves_cap + 1) * sizeof(uint4)));
+    }
     return SG_OK;
 }
 
@@ -2146,7 +2159,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         std::memset(&Sg, 0, sizeof(Sg));
         Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
         Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
-        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, st));
+        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, e->d_pmoves,
+                              e->d_pmoves ? reinterpret_cast<uint32_t*>(e->d_pmoves + e->pmoves_cap) : nullptr,
+                              (uint32_t)e->pmoves_cap, st));
         HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
     }
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
@@ -2247,8 +2262,8 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
         HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
                          e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
-                         (bflags & BF_ZERO_CNT) ? 0u : 1u, ps, launch_radix_hist,
-                         launch_radix_scatter, launch_scan, radix_tile()));
+                         (bflags & BF_ZERO_CNT) ? 0u : 1u, ps, launch_radix_hist_n,
+                         launch_radix_scatter_n, launch_scan, radix_tile()));
     }
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
@@ -2332,7 +2347,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (n_mixw && e->pvt_on && head[72])
         HIPCHK(launch_pvt(e->d_recs, dev_ev, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec,
                           e->d_bsmall + 0, e->d_pvtseg, e->pvb, head[72], e->d_pvtot + 4, e->d_pvhist, e->d_pvpart, st,
-                          launch_radix_hist, launch_radix_scatter, launch_scan, radix_tile()));
+                          launch_radix_hist_n, launch_radix_scatter_n, launch_scan, radix_tile()));
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(1, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
                              e->d_dec, e->d_bsmall + 0, st));

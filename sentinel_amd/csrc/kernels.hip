@@ -176,9 +176,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
 }
 
 template <int DB>
+// ndev (optional): the key count on the device, at most n (the grid is sized for n)
 __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, uint64_t n, int shift,
-                                                        uint32_t* __restrict__ ghist, uint32_t nblocks) {
+                                                        uint32_t* __restrict__ ghist, uint32_t nblocks,
+                                                        const uint32_t* __restrict__ ndev) {
     constexpr int NB = 1 << DB;
+    if (ndev && *ndev < n) n = *ndev;
     __shared__ uint32_t h[NB];
     for (int i = threadIdx.x; i < NB; i += RS_THREADS) h[i] = 0;
     __syncthreads();
@@ -207,8 +210,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                           uint32_t* __restrict__ pos_of) {
+                                                           uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ ndev) {
     constexpr int NB = 1 << DB;
+    if (ndev && *ndev < n) n = *ndev;
+    if ((uint64_t)blockIdx.x * RS_TILE >= n) return;  // (a tile past the device count: nothing to move)
     constexpr int DPT = NB / RS_THREADS;  // digits per thread in the offset scan
     static_assert(NB % RS_THREADS == 0, "whole digits per thread");
     __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
@@ -482,13 +487,26 @@ hipError_t launch_rs_first(const sg_event* ev, uint64_t n, uint32_t max_res, uin
 }
 hipError_t launch_radix_hist(const uint32_t* keys, uint64_t n, int shift, uint32_t* ghist, uint32_t nblocks,
                              hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks);
+    hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks,
+                       (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+// the same over min(n, *ndev) keys (a count known on the device only; the grid is sized for n)
+hipError_t launch_radix_hist_n(const uint32_t* keys, uint64_t n, const uint32_t* ndev, int shift, uint32_t* ghist,
+                               uint32_t nblocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_hist<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, keys, n, shift, ghist, nblocks, ndev);
+    return hipGetLastError();
+}
+hipError_t launch_radix_scatter_n(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev, int shift,
+                                  const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
+                       kout, vout, (uint32_t*)nullptr, ndev);
     return hipGetLastError();
 }
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, pos_of);
+                       kout, vout, pos_of, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 

@@ -1390,8 +1390,9 @@ __device__ void pm_move(const DevState& S, uint32_t id, PMap m, uint64_t nbase, 
 }
 // the map before up to `adds` more keys arrive: at most half its slots used, else a region twice as large (or
 // large enough), up to map_buckets(cap)
+// mv (k_pm_grow): the move is listed for k_pm_move_list (a workgroup per map) instead of done by this lane
 __device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned long long* pool_next, uint64_t pool_nb,
-                        uint32_t* bflags) {
+                        uint32_t* bflags, uint4* mv = nullptr, uint32_t* nmv = nullptr, uint32_t mcap = 0) {
     const PMap m = S.pmap[id];
     uint64_t need = (uint64_t)m.live + adds;
     if (need > m.cap) need = m.cap;
@@ -1401,13 +1402,98 @@ __device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned 
     if (nn > full) nn = full;
     const uint64_t nbase = atomicAdd(pool_next, (unsigned long long)nn);
     if (nbase + nn > pool_nb) { atomicOr(bflags, BF_POOL_FULL); return; }
+    if (mv) {
+        const uint32_t k = atomicAdd(nmv, 1u);
+        if (k < mcap) { mv[k] = make_uint4(id, (uint32_t)nbase, (uint32_t)(nbase >> 32), nn); return; }
+    }
     pm_move(S, id, m, nbase, nn, bflags);
+}
+// the listed moves, a workgroup per map: every live key of the old region into the new one (PK_EMPTY-filled pool),
+// claimed by compare-and-swap in either of its buckets; the rare key finding both full is placed afterwards by one
+// lane with pm_move's displacement walk.  The map's order lives in its stamps and ring, not in the slots, so the
+// placement is free.
+__global__ __launch_bounds__(256) void k_pm_move_list(const uint4* __restrict__ mv, const uint32_t* __restrict__ nmv,
+                                                      uint32_t mcap, DevState S, uint32_t* __restrict__ bflags) {
+    __shared__ uint32_t npend;
+    __shared__ uint32_t pend[64];
+    const uint32_t n = *nmv < mcap ? *nmv : mcap;
+    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const uint4 v = mv[k];
+        const uint32_t id = v.x, nn = v.w;
+        const uint64_t nbase = (uint64_t)v.y | ((uint64_t)v.z << 32);
+        const PMap m = S.pmap[id];
+        if (threadIdx.x == 0) npend = 0;
+        __syncthreads();
+        const PBucket* OB = S.pbkt + m.base;
+        const PData* OD = S.pdat + m.base * PM_BKT;
+        PBucket* NB = S.pbkt + nbase;
+        PData* ND = S.pdat + nbase * PM_BKT;
+        const uint64_t* bm = S.pbm + m.bm;
+        for (uint32_t sl = threadIdx.x; sl < m.nb * PM_BKT; sl += 256) {
+            const uint64_t ck = OB[sl / PM_BKT].key[sl % PM_BKT];
+            const int64_t cs = OB[sl / PM_BKT].stamp[sl % PM_BKT];
+            if (ck == PK_EMPTY || !pm_live(m, bm, cs)) continue;
+            uint32_t b1, b2;
+            pm_buckets(nn, ck, b1, b2);
+            bool placed = false;
+            for (int h = 0; h < 2 && !placed; ++h) {
+                const uint32_t bb = h ? b2 : b1;
+                for (int q = 0; q < PM_BKT; ++q) {
+                    if (NB[bb].key[q] != PK_EMPTY) continue;
+                    const unsigned long long o = atomicCAS(reinterpret_cast<unsigned long long*>(&NB[bb].key[q]),
+                                                           (unsigned long long)PK_EMPTY, (unsigned long long)ck);
+                    if (o == PK_EMPTY) {
+                        NB[bb].stamp[q] = cs;
+                        ND[bb * PM_BKT + q] = OD[sl];
+                        placed = true;
+                        break;
+                    }
+                }
+            }
+            if (!placed) {
+                const uint32_t p = atomicAdd(&npend, 1u);
+                if (p < 64) pend[p] = sl;
+                else atomicOr(bflags, BF_PTAB_FULL);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t f = 0; f < (npend < 64 ? npend : 64u); ++f) {
+                const uint32_t sl = pend[f];
+                uint64_t ck = OB[sl / PM_BKT].key[sl % PM_BKT];
+                int64_t cs = OB[sl / PM_BKT].stamp[sl % PM_BKT];
+                PData cd = OD[sl];
+                uint32_t b1, b2;
+                pm_buckets(nn, ck, b1, b2);
+                uint32_t c = b1;
+                bool placed = false;
+                for (int step = 0; step < 512 && !placed; ++step) {
+                    for (int q = 0; q < PM_BKT; ++q)
+                        if (NB[c].key[q] == PK_EMPTY) { NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd; placed = true; break; }
+                    if (placed) break;
+                    const int q = (int)((cs + step * 5) & 7);
+                    const uint64_t nk = NB[c].key[q];
+                    const int64_t ns = NB[c].stamp[q];
+                    const PData nd = ND[c * PM_BKT + q];
+                    NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd;
+                    ck = nk; cs = ns; cd = nd;
+                    c = pm_alt(nn, ck, c);
+                }
+                if (!placed) atomicOr(bflags, BF_PTAB_FULL);
+            }
+            PMap* hd = &S.pmap[id];
+            hd->base = nbase;
+            hd->nb = nn;
+        }
+        __syncthreads();
+    }
 }
 // Decide stage, before every kernel that touches the maps: the maps a segment may add keys to -- its QPS rules'
 // maps and its thread-count maps -- grown for the segment's events (an upper bound of its accesses); one lane each.
 // (Maps of STRATEGY_RELATE members, whose events sort under another resource, are grown to capacity at rule load.)
 __global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, const uint32_t* __restrict__ mp, DevState S,
-                                                 unsigned long long* pool_next, uint64_t pool_nb, uint32_t* bflags) {
+                                                 unsigned long long* pool_next, uint64_t pool_nb, uint32_t* bflags,
+                                                 uint4* mv, uint32_t* nmv, uint32_t mcap) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= *mp) return;
     const Seg sg = segs[s];
@@ -1417,12 +1503,12 @@ __global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, c
     const uint64_t adds = (S.prio && (S.prio[sg.res] & PM_ARGL)) ? 0xFFFFFFFFull : (uint64_t)sg.len;
     for (int k = 0; k < pg.n_param; ++k) {
         const DRule& r = S.rules[pg.rule_off + k];
-        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags);
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags, mv, nmv, mcap);
     }
     if (pg.tm_base != NO_ID)
         for (int i = 0; i < SG_MAX_ARGS; ++i) {
             const uint32_t id = S.tmid[pg.tm_base + i];
-            if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags);
+            if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags, mv, nmv, mcap);
         }
 }
 // listed maps to full size (rule load: STRATEGY_RELATE members)
@@ -1433,10 +1519,18 @@ __global__ void k_pm_grow_ids(const uint32_t* __restrict__ ids, uint32_t n, DevS
 }
 
 namespace sg {
+// mv / nmv / mcap: the move list (null: each lane moves its maps itself)
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
-                          uint64_t pool_nb, uint32_t* bflags, hipStream_t st) {
+                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, hipStream_t st) {
     if (!mb) return hipSuccess;
-    hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags);
+    if (!mcap) mv = nullptr;
+    if (mv) {
+        const hipError_t e = hipMemsetAsync(nmv, 0, 4, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags,
+                       mv, nmv, mcap);
+    if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 4096 ? mcap : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
     return hipGetLastError();
 }
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,

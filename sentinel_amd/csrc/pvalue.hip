@@ -365,18 +365,98 @@ __device__ int32_t pv_count_gt(const PvBuf& B, int64_t lo, int64_t hi, int32_t r
     return c;
 }
 
-// ---- residency of every access; for a value's last access, whether the value stays in the map
-__global__ void k_pv_resid(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S) {
+// ---- residency of every access.  Exact counts (pv_count_lt / gt) only in a narrow band; around it bounds settle
+// an access in O(1):
+//   a repeat (prev p, at g): its window (p, g) holds fewer than cap values when g - p - 1 < cap; else by the
+//     horizons Z[b] of the block starts P_b = 256 b (the end y of the shortest window (P_b, y) holding cap distinct
+//     values, cap of P_b's segment): windows (P_b1, g) and (P_b2, g), b1 = p / 256 < b2, enclose / lie inside
+//     (p, g), so g < Z[b1] is a hit (P_b1 in the segment) and g >= Z[b2] a miss;
+//   a first access of a value of rank r: hit iff r + #(earlier first accesses of values absent or ranked below r)
+//     < cap; that count lies between the segment's earlier new values (NN) and earlier first accesses (NF).
+__global__ void k_pv_fflags(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= cap) return;
+    const int32_t w = g < *tot ? B.w[g] : -1;
+    reinterpret_cast<uint32_t*>(B.gdt)[g] = w >= 0 ? 1u : 0u;  // -> NF (scan)
+    B.gaw[g] = w == PV_INF ? 1u : 0u;                          // -> NN (scan)
+}
+// one wavefront per block start: Z[b] (0xFFFFFFFF: the accesses end first), 64 blocks a round
+__global__ __launch_bounds__(256) void k_pv_horizon(PvBuf B, const uint32_t* __restrict__ tot,
+                                                    const PvSeg* __restrict__ pv, DevState S,
+                                                    uint32_t* __restrict__ Z) {
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+    const uint32_t n = *tot;
+    if ((uint64_t)b * PV_B >= n) return;
+    const int32_t P = (int32_t)(b * PV_B);
+    const int32_t cap = (int32_t)S.pmap[pv[B.seg[P]].mid].cap;
+    const uint32_t nblk = (n + PV_B - 1) / PV_B;
+    int32_t need = cap;
+    uint32_t z = 0xFFFFFFFFu;
+    for (uint32_t c0 = b; c0 < nblk; c0 += 64) {
+        const uint32_t c = c0 + l;
+        int32_t cnt = 0;
+        if (c < nblk) {  // #{k in block c, k > P : prev(k) <= P}
+            const int32_t* sp = B.sprev + (uint64_t)c * PV_B;
+            uint32_t lo = 0, hi = PV_B;
+            while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (sp[md] <= P) lo = md + 1; else hi = md; }
+            cnt = (int32_t)lo - (c == b ? 1 : 0);  // (k = P itself: prev(P) < P)
+        }
+        int32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(inc, o, 64);
+            if (l >= (uint32_t)o) inc += y;
+        }
+        const uint64_t reach = __ballot(inc >= need);
+        if (reach) {
+            const uint32_t lf = (uint32_t)__ffsll((unsigned long long)reach) - 1;
+            int32_t left = need - __shfl(inc - cnt, lf, 64);  // values still to find inside block c0 + lf
+            const uint32_t k0 = (c0 + lf) * PV_B;
+            for (uint32_t r = 0; r < PV_B; r += 64) {  // positions in order, a wavefront at a time
+                const uint32_t k = k0 + r + l;
+                const bool f = k < n && (int32_t)k > P && B.prev[k] <= P;
+                const uint64_t bm = __ballot(f);
+                const int32_t nf = __popcll(bm);
+                if (nf >= left) {  // the left-th flagged position
+                    uint64_t x = bm;
+                    for (int q = 1; q < left; ++q) x &= x - 1;
+                    z = k0 + r + (uint32_t)(__ffsll((unsigned long long)x) - 1) + 1;
+                    break;
+                }
+                left -= nf;
+            }
+            break;
+        }
+        need -= __shfl(inc, 63, 64);
+    }
+    if (l == 0) Z[b] = z;
+}
+__global__ void k_pv_resid(PvBuf B, const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S,
+                           const uint32_t* __restrict__ NF, const uint32_t* __restrict__ NN,
+                           const uint32_t* __restrict__ Z) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= *tot) return;
     const PvSeg ps = pv[B.seg[g]];
     const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
     const int32_t p = B.prev[g];
     bool hit;
-    if (p >= 0) hit = (int64_t)g - p - 1 < cap || pv_count_lt(B, p, g, p, cap) < cap;
-    else {
+    if (p >= 0) {
+        if ((int64_t)g - p - 1 < cap) hit = true;
+        else {
+            const uint32_t b1 = (uint32_t)p / PV_B;  // (Z[b1] only from inside the segment: its cap)
+            if (b1 * PV_B >= ps.off && g < Z[b1]) hit = true;
+            else if (g >= Z[b1 + 1]) hit = false;
+            else hit = pv_count_lt(B, p, g, p, cap) < cap;
+        }
+    } else {
         const int32_t r = B.w[g];
-        hit = r != PV_INF && pv_count_gt(B, ps.off, g, r, cap - r) < cap - r;
+        if (r == PV_INF) hit = false;
+        else {
+            const int32_t nf = (int32_t)(NF[g] - NF[ps.off]), nn = (int32_t)(NN[g] - NN[ps.off]);
+            if (r + nf < cap) hit = true;
+            else if (r + nn >= cap) hit = false;
+            else hit = pv_count_gt(B, ps.off, g, r, cap - r) < cap - r;
+        }
     }
     B.hit[g] = hit ? 1 : 0;
 }
@@ -433,13 +513,13 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
     const Seg sg = segs[list[si]];
     const DRule& r = S.rules[S.prog[sg.res].rule_off + ps.rk];
     const int64_t D = r.duration_sec * 1000;
-    const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
     const int32_t tc = B.tc[g0], maxc = j_iadd(tc, r.burst);
     const uint32_t blk = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
     int64_t last = B.flast[g0];  // (valid when the first access hits: the value was live)
     int32_t tok = B.ftok[g0];
-    uint32_t q = q0;
+    uint32_t q = q0, steps = 0;
     while (q < qb) {
+        ++steps;
         const int64_t t = t0 + B.gdt[q];
         const uint32_t aw = B.gaw[q];
         const int32_t a = (int32_t)(aw & 0xFFFFu);
@@ -481,10 +561,11 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
             }
         }
     }
-    // the value's last access g: it stays iff fewer than cap distinct values are accessed after it
+    if (steps > 256) atomicMax(&tot[3], steps);  // (diagnostics: the longest walk)
+    // the value's last access g: it stays iff fewer than cap distinct values are accessed after it, i.e. it is among
+    // the segment's cap latest last accesses (the commit counts them with a scan)
     const uint32_t g = B.idx[qb - 1];
-    const int64_t end = (int64_t)ps.off + ps.n;
-    B.keep[g] = pv_count_lt(B, g, end, (int32_t)g, cap) < cap ? 1 : 0;
+    B.keep[g] = 1;  // (the commit keeps the cap latest of these)
     B.flast[g] = last;
     B.ftok[g] = tok;
     B.fslot[g] = B.fslot[g0];  // (the value's slot, carried to its last access for the commit)
@@ -741,8 +822,7 @@ __global__ void k_pvt_walk(PvBuf B, const uint32_t* __restrict__ tot, const PvSe
     const uint32_t g = B.idx[qb - 1];
     if (!ps.sub) {
         for (uint32_t q = q0; q < qb; ++q) c = B.hit[B.idx[q]] ? c + 1 : 1;
-        const int32_t cap = (int32_t)S.pmap[ps.mid].cap;
-        B.keep[g] = pv_count_lt(B, g, (int64_t)ps.off + ps.n, (int32_t)g, cap) < cap ? 1 : 0;
+        B.keep[g] = 1;  // (its last op: the commit keeps the cap latest)
     } else {
         for (uint32_t q = q0; q < qb; ++q) {
             const uint32_t gq = B.idx[q];
@@ -780,16 +860,44 @@ __global__ void k_pvt_peak(PvBuf B, const uint32_t* __restrict__ X, const uint32
     }
 }
 
-// ---- commit: one workgroup per segment: the map after the segment
+// ---- commit: the map after the segment.  Per access first (grids over the accesses): the kept values listed in
+// last-access order (keep flags -> exclusive scan -> list), the touched values' old stamps cleared from the map's
+// ring; then one workgroup per segment over at most cap kept values and the map's slots.
+// A segment commits unless its post pass (tmode, releases) found the map outgrowing cap: k_pq's replay then.
+__device__ __forceinline__ bool pv_commits(const PvSeg& ps, const PMap& mp, uint32_t tmode) {
+    return ps.ok && !(tmode && ps.sub && (int64_t)mp.live + ps.peak > (int64_t)mp.cap);
+}
+__global__ void k_pv_keepw(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < cap) B.tc[g] = g < *tot ? (uint32_t)B.keep[g] : 0u;
+}
+// X = exclusive scan of keep (the flagged last accesses): the list L[X[g]] = g (segment-major, last-access order
+// within a segment); and the old stamps of the values live at the start and accessed (first accesses: w a rank)
+// leave the ring
+__global__ void k_pv_klist(PvBuf B, const uint32_t* __restrict__ X, uint32_t* __restrict__ L,
+                           const uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S, uint32_t tmode) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= *tot) return;
+    if (B.keep[g]) L[X[g]] = g;
+    const int32_t w = B.w[g], sl = B.fslot[g];
+    if (w < 0 || w == PV_INF || sl < 0) return;
+    const PvSeg ps = pv[B.seg[g]];
+    const PMap mp = S.pmap[ps.mid];
+    if (!pv_commits(ps, mp, tmode)) return;
+    const int64_t st = S.pbkt[mp.base + sl / PM_BKT].stamp[sl % PM_BKT];
+    const uint64_t p = (uint64_t)st & (uint64_t)((1ull << mp.rb_log2) - 1);
+    atomicAnd(reinterpret_cast<unsigned long long*>(&S.pbm[mp.bm + (p >> 6)]), ~(1ull << (p & 63)));
+}
+
 #define PV_RW 512u   // ring words (cap <= PQ_MAX_CAP)
 #define PV_CW 256u   // claim words (slots <= map_buckets(PQ_MAX_CAP) * 8)
-// tmode (the post pass): the thread-count map; every value present at its last access stays (no eviction: the
-// map never outgrew cap, else k_pq's post pass takes the segment), and the segment gets SEG_PVT and its bits.
+// tmode (the post pass): the thread-count map; the segment gets SEG_PVT and its ParameterMetric bits
 __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __restrict__ pv, uint32_t m, DevState S,
                                                     uint32_t* __restrict__ bflags, uint32_t tmode,
                                                     Seg* __restrict__ segs, const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ X, const uint32_t* __restrict__ L,
                                                     uint32_t* __restrict__ ndone) {
-    __shared__ uint64_t ring[PV_RW], touch[PV_RW];
+    __shared__ uint64_t ring[PV_RW];
     __shared__ uint32_t pre[PV_RW];
     __shared__ unsigned long long claim[PV_CW];
     __shared__ uint32_t red[16];
@@ -798,51 +906,36 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
     if (i >= m) return;
     const PvSeg ps = pv[i];
-    if (!ps.ok) return;
     PMap mp = S.pmap[ps.mid];
+    if (!pv_commits(ps, mp, tmode)) return;
     const uint32_t W = 1u << (mp.rb_log2 - 6);
     const int32_t cap = (int32_t)mp.cap;
-    const bool kcount = tmode && ps.sub;  // the kept values are the ones present at their last op
-    if (kcount && (int64_t)mp.live + ps.peak > (int64_t)cap) return;  // an eviction: the sequential replay's
     PBucket* BK = S.pbkt + mp.base;
     PData* DT = S.pdat + mp.base * PM_BKT;
     const uint32_t nslot = mp.nb * PM_BKT;
-    for (uint32_t w = tid; w < W; w += 1024) { ring[w] = S.pbm[mp.bm + w]; touch[w] = 0; }
+    for (uint32_t w = tid; w < W; w += 1024) ring[w] = S.pbm[mp.bm + w];  // (untouched live stamps: k_pv_klist)
     for (uint32_t w = tid; w < PV_CW; w += 1024) claim[w] = 0;
     if (tid == 0) nfail = 0;
+    // (1) the accessed values that stay: the flagged last accesses L[X[off], X[off] + G) in order; the latest
+    // KA = min(G, cap) of them (an LRU map holds the cap most recently used), or (releases) every value present
+    const uint32_t G = ps.n ? X[ps.off + ps.n - 1] + (uint32_t)B.keep[ps.off + ps.n - 1] - X[ps.off] : 0u;
+    const uint32_t KA = (tmode && ps.sub) || G < (uint32_t)cap ? G : (uint32_t)cap;
+    const uint32_t ks = ps.n ? X[ps.off] + (G - KA) : 0u;
     __syncthreads();
-    // (1) live stamps of values accessed in the segment; the number of distinct values accessed (G) and kept
-    uint32_t ng = 0;
-    for (uint32_t k = tid; k < ps.n; k += 1024) {
-        const uint32_t g = ps.off + k;
-        if (kcount) ng += B.keep[g];
-        if (B.w[g] >= 0) {  // a value's first access
-            if (!kcount) ++ng;
-            const int32_t sl = B.fslot[g];
-            if (sl >= 0 && B.w[g] != PV_INF) {
-                const int64_t s = BK[sl / PM_BKT].stamp[sl % PM_BKT];
-                const uint64_t p = (uint64_t)s & (uint64_t)((1ull << mp.rb_log2) - 1);
-                atomicOr(reinterpret_cast<unsigned long long*>(&touch[p >> 6]), 1ull << (p & 63));
-            }
-        }
-    }
-    uint32_t G;
-    (void)pv_scan<16>(ng, red, &G);
-    const uint32_t KA = G < (uint32_t)cap ? G : (uint32_t)cap;  // accessed values that stay (kcount: G kept)
-    // (2) untouched live values: the (cap - KA) most recent stay; prefix counts of untouched stamps from thr
+    // (2) untouched live values: the (cap - KA) most recent stay; prefix counts of their stamps from thr
     const uint32_t w0 = pv_word(mp, mp.thr);
     {
         const uint32_t per = (W + 1023) / 1024, l0 = tid * per;
         uint32_t c = 0;
         for (uint32_t u = 0; u < per; ++u)
-            if (l0 + u < W) c += (uint32_t)__popcll(ring[(w0 + l0 + u) & (W - 1)] & ~touch[(w0 + l0 + u) & (W - 1)]);
+            if (l0 + u < W) c += (uint32_t)__popcll(ring[(w0 + l0 + u) & (W - 1)]);
         uint32_t tU;
         uint32_t run = pv_scan<16>(c, red, &tU);
         for (uint32_t u = 0; u < per; ++u)
             if (l0 + u < W) {
                 const uint32_t w = (w0 + l0 + u) & (W - 1);
                 pre[w] = run;
-                run += (uint32_t)__popcll(ring[w] & ~touch[w]);
+                run += (uint32_t)__popcll(ring[w]);
             }
         if (tid == 0) red[15] = tU;
     }
@@ -858,43 +951,33 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
         if (!(s >= mp.thr && s < mp.clock)) continue;
         const uint64_t p = (uint64_t)s & (uint64_t)((1ull << mp.rb_log2) - 1);
         const uint64_t bit = 1ull << (p & 63);
-        if (!(ring[p >> 6] & bit) || (touch[p >> 6] & bit)) continue;
-        const uint32_t below = pre[p >> 6] + (uint32_t)__popcll(ring[p >> 6] & ~touch[p >> 6] & (bit - 1ull));
+        if (!(ring[p >> 6] & bit)) continue;
+        const uint32_t below = pre[p >> 6] + (uint32_t)__popcll(ring[p >> 6] & (bit - 1ull));
         if (below + KU < U) continue;  // not among the KU most recent untouched
         BK[sl / PM_BKT].stamp[sl % PM_BKT] = base + (int64_t)(below - (U - KU));
         atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
     }
     __syncthreads();
     // (4) accessed values that stay, in last-access order: new stamps above; their slot reused or claimed
-    uint32_t kbase = 0;
-    for (uint32_t c = 0; c < ps.n; c += 1024) {  // (uniform)
-        const uint32_t k = c + tid;
-        const uint32_t g = ps.off + k;
-        const bool kp = k < ps.n && B.keep[g];
-        uint32_t t;
-        const uint32_t o = pv_scan<16>(kp ? 1u : 0u, red, &t);
-        if (kp) {
-            const uint32_t rank = kbase + o;  // among the kept, by last access
-            const int64_t s = base + (int64_t)KU + (int64_t)rank;
-            PData d;
-            d.v0 = B.flast[g]; d.v1 = B.ftok[g]; d.pad = 0;
-            const int32_t sl = B.fslot[g];
-            if (sl >= 0) {
-                BK[sl / PM_BKT].stamp[sl % PM_BKT] = s;
-                DT[sl] = d;
-                atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
-            } else {
-                B.fslot[g] = -2 - (int32_t)rank;  // placed below
-            }
+    for (uint32_t rank = tid; rank < KA; rank += 1024) {
+        const uint32_t g = L[ks + rank];
+        const int64_t s = base + (int64_t)KU + (int64_t)rank;
+        PData d;
+        d.v0 = B.flast[g]; d.v1 = B.ftok[g]; d.pad = 0;
+        const int32_t sl = B.fslot[g];
+        if (sl >= 0) {
+            BK[sl / PM_BKT].stamp[sl % PM_BKT] = s;
+            DT[sl] = d;
+            atomicOr(&claim[sl >> 6], 1ull << (sl & 63));
+        } else {
+            B.fslot[g] = -2 - (int32_t)rank;  // placed below
         }
-        kbase += t;
     }
     __syncthreads();
     // (5) new values: a free slot (empty, or an old value's that did not stay) in either bucket
-    for (uint32_t c = 0; c < ps.n; c += 1024) {
-        const uint32_t k = c + tid;
-        const uint32_t g = ps.off + k;
-        if (k >= ps.n || !B.keep[g] || B.fslot[g] >= 0) continue;
+    for (uint32_t kr = tid; kr < KA; kr += 1024) {
+        const uint32_t g = L[ks + kr];
+        if (B.fslot[g] >= 0) continue;
         const uint32_t rank = (uint32_t)(-2 - B.fslot[g]);
         const uint64_t key = B.key[g];
         const int64_t s = base + (int64_t)KU + (int64_t)rank;
@@ -985,11 +1068,11 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
 }
 
 namespace sg {
-// the accesses [0, tot) by group id, stable (pads [tot, cap) to sort last)
+// the accesses [0, tot) by group id, stable (tot on the device: the tiles past it idle; pads [tot, cap))
 static hipError_t pv_sort(PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
-                          hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
-                          hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                                      uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                          hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                          hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                           hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                           uint32_t tile) {
     hipError_t e = hipSuccess;
@@ -1002,9 +1085,9 @@ static hipError_t pv_sort(PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, 
     const uint32_t nblocks = (cap + tile - 1) / tile;
     uint32_t *kin = B.gid, *vin = B.idx, *kout = B.gid2, *vout = B.idx2;
     for (int p = 0; p < passes; ++p) {
-        e = radix_hist(kin, cap, p * 8, hist, nblocks, st);
+        e = radix_hist(kin, cap, tot, p * 8, hist, nblocks, st);
         if (e == hipSuccess) e = scan(hist, hist, (uint64_t)nblocks << 8, part, nullptr, st);
-        if (e == hipSuccess) e = radix_scatter(kin, vin, cap, p * 8, hist, nblocks, kout, vout, nullptr, st);
+        if (e == hipSuccess) e = radix_scatter(kin, vin, cap, tot, p * 8, hist, nblocks, kout, vout, st);
         if (e != hipSuccess) return e;
         uint32_t* tk = kin; kin = kout; kout = tk;
         uint32_t* tv = vin; vin = vout; vout = tv;
@@ -1017,6 +1100,35 @@ static hipError_t pv_sort(PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, 
     return hipSuccess;
 }
 
+// residency (after k_pv_prev / k_pv_blocks): NF / NN prefix counts in gdt / gaw, horizons in gpos
+static hipError_t pv_resid(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv, const DevState& S, uint32_t* part,
+                           hipStream_t st,
+                           hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t)) {
+    const uint32_t nb = (cap + 255) / 256, nblk = (cap + PV_B - 1) / PV_B;
+    uint32_t* nf = reinterpret_cast<uint32_t*>(B.gdt);
+    hipLaunchKernelGGL(k_pv_fflags, dim3(nb), dim3(256), 0, st, B, tot, cap);
+    hipError_t e = scan(nf, nf, cap, part, nullptr, st);
+    if (e == hipSuccess) e = scan(B.gaw, B.gaw, cap, part, nullptr, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_horizon, dim3((nblk + 3) / 4), dim3(256), 0, st, B, tot, pv, S, B.gpos);
+    hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S, nf, B.gaw, B.gpos);
+    return hipGetLastError();
+}
+
+// the commit's kept list (gdt: exclusive scan of the keep flags, idx2: the list) and the touched stamps' removal
+static hipError_t pv_klist(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv, const DevState& S, uint32_t tmode,
+                           uint32_t* part, hipStream_t st,
+                           hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t)) {
+    const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pv_keepw, dim3(nb), dim3(256), 0, st, B, tot, cap);
+    const hipError_t e = scan(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, part,
+                              nullptr, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_klist, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, tot,
+                       pv, S, tmode);
+    return hipGetLastError();
+}
+
 // the value-parallel pre pass over the wide XF_MIX list (cap accesses at most); pv[] tells k_pq which segments
 // are done.  Scratch: PvBuf arrays of cap entries (chunks: cap / PV_CH + m), htab 2 x cap, radix scratch (hist,
 // part), tot (device words: [0] accesses, [1] chunks, [2] ranges).  jumps: the batch has no zero-acquire ENTRY.
@@ -1024,9 +1136,9 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
                      const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
                      PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
                      hipStream_t st,
-                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
-                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                                 uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                      uint32_t tile) {
     if (!m || !cap) return hipSuccess;
@@ -1045,11 +1157,15 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
-    hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    e = pv_resid(B, cap, tot, pv, S, part, st, scan);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_gather, dim3(nb), dim3(256), 0, st, segs, list, B, tot);
     hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags);
     hipLaunchKernelGGL(k_pv_ranges, dim3(2048), dim3(256), 0, st, recs, B, tot, cap, dec);
-    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 0u, segs, list, nullptr);
+    e = pv_klist(B, cap, tot, pv, S, 0u, part, st, scan);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 0u, segs, list,
+                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, nullptr);
     return hipGetLastError();
 }
 
@@ -1058,9 +1174,9 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
 hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                       const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
                       uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
-                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, int, uint32_t*, uint32_t, hipStream_t),
-                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, int, const uint32_t*,
-                                                  uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t),
+                      hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                       uint32_t tile) {
     if (!m || !cap) return hipSuccess;
@@ -1079,13 +1195,17 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
     const uint32_t nb = (cap + 255) / 256;
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
-    hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
+    e = pv_resid(B, cap, tot, pv, S, part, st, scan);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pvt_walk, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     // (the peak of the segments with releases; the scan's output in gdt: free in the post pass)
     e = scan(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, part, nullptr, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pvt_peak, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.gdt), tot, pv);
-    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 1u, segs, list, tot + 3);
+    e = pv_klist(B, cap, tot, pv, S, 1u, part, st, scan);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 1u, segs, list,
+                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, tot + 3);
     return hipGetLastError();
 }
 

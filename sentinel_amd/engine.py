@@ -238,11 +238,12 @@ class Engine:
         fn = lib().sgx_pv_last
         fn.restype = C.c_int
         fn.argtypes = [C.c_void_p, C.c_void_p]
-        out = np.zeros(6, dtype=np.uint64)
+        out = np.zeros(7, dtype=np.uint64)
         if fn(self.h, out.ctypes.data) != 0:
             raise SentinelError(A.SG_EDEVICE, "sgx_pv_last failed")
         return {"segments": int(out[0]), "accesses": int(out[1]), "ranges": int(out[2]),
-                "post_segments": int(out[3]), "post_ops": int(out[4]), "post_done": int(out[5])}
+                "post_segments": int(out[3]), "post_ops": int(out[4]), "post_done": int(out[5]),
+                "walk_max": int(out[6])}
 
     def param_pool(self) -> dict:
         """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last layout,
