@@ -460,6 +460,70 @@ __device__ int32_t hot_count(const DevState& S, const DRule& r, uint64_t v, bool
     *found = false;
     return 0;
 }
+// pm_put (pmap.h) with its memory rounds overlapped, for the lane path: both candidate buckets' keys and stamps
+// in one round, the stamp's ring word and the slot's values in the next, ring bits of a hit changed by atomics
+// nobody waits for (the lane owns the map: only the order of its own accesses matters).  Same map state and
+// result as pm_put; *d = the slot's values before the access (zero for an inserted key).
+__device__ int32_t pm_put_lane(PMap& m, const PRef& R, uint64_t v, bool* present, PData* d, uint32_t* bflags) {
+    pm_reserve(m, R, 1);
+    uint32_t b1, b2;
+    pm_buckets(m.nb, v, b1, b2);
+    const PBucket B1 = R.B[b1], B2 = R.B[b2];
+    int32_t i = -1;
+    int64_t st = 0;
+#pragma unroll
+    for (int j = PM_BKT - 1; j >= 0; --j) if (B2.key[j] == v) { i = (int32_t)(b2 * PM_BKT + j); st = B2.stamp[j]; }
+#pragma unroll
+    for (int j = PM_BKT - 1; j >= 0; --j) if (B1.key[j] == v) { i = (int32_t)(b1 * PM_BKT + j); st = B1.stamp[j]; }
+    const uint64_t RM = (uint64_t)pm_rbits(m) - 1;
+    if (i >= 0) {
+        const uint64_t p = (uint64_t)st & RM;
+        const uint64_t wd = R.bm[p >> 6];
+        const PData dd = R.D[i];
+        if (st >= m.thr && st < m.clock && ((wd >> (p & 63)) & 1ull)) {
+            atomicAnd(reinterpret_cast<unsigned long long*>(&R.bm[p >> 6]), ~(1ull << (p & 63)));
+            const int64_t s = m.clock++;
+            const uint64_t q = (uint64_t)s & RM;
+            atomicOr(reinterpret_cast<unsigned long long*>(&R.bm[q >> 6]), 1ull << (q & 63));
+            R.B[i / PM_BKT].stamp[i % PM_BKT] = s;
+            *present = true;
+            *d = dd;
+            return i;
+        }
+    }
+    *present = false;
+    PData z;
+    z.v0 = 0; z.v1 = 0; z.pad = 0;
+    *d = z;
+    if (m.live >= m.cap) pm_evict_oldest(m, R);
+    m.live++;
+    if (i >= 0) {  // the key's own dead slot
+        pm_restamp(m, R, i, false);
+        R.D[i] = z;
+        return i;
+    }
+    // a free slot (empty, or dead by the ring) of the bucket with fewer live keys: pm_insert_new's choice, the
+    // ring words of both buckets' stamps loaded together
+    int f1 = -1, f2 = -1, n1 = 0, n2 = 0;
+#pragma unroll
+    for (int j = 0; j < PM_BKT; ++j) {
+        const bool fr1 = B1.key[j] == PK_EMPTY || !pm_live(m, R.bm, B1.stamp[j]);
+        const bool fr2 = B2.key[j] == PK_EMPTY || !pm_live(m, R.bm, B2.stamp[j]);
+        if (fr1) { if (f1 < 0) f1 = j; } else ++n1;
+        if (fr2) { if (f2 < 0) f2 = j; } else ++n2;
+    }
+    const bool u1 = f1 >= 0 && (f2 < 0 || n1 <= n2);
+    if (!u1 && f2 < 0) return pm_insert_new(m, R, v, bflags);  // both full: the displacement walk
+    const uint32_t b = u1 ? b1 : b2;
+    const int j = u1 ? f1 : f2;
+    const int64_t s = m.clock++;
+    const uint64_t q = (uint64_t)s & RM;
+    atomicOr(reinterpret_cast<unsigned long long*>(&R.bm[q >> 6]), 1ull << (q & 63));
+    R.B[b].key[j] = v;
+    R.B[b].stamp[j] = s;
+    R.D[b * PM_BKT + j] = z;
+    return (int32_t)(b * PM_BKT + j);
+}
 __device__ __forceinline__ uint32_t tmap_of(const DevState& S, uint32_t tm_base, uint32_t idx) {
     return tm_base == NO_ID || idx >= SG_MAX_ARGS ? NO_ID : S.tmid[tm_base + idx];
 }
@@ -483,11 +547,12 @@ __device__ void thread_count_add(const DevState& S, uint32_t tm_base, uint32_t i
     PMap m = S.pmap[id];
     const PRef R = pm_ref(S, m);
     bool present;
-    const int32_t i = pm_put(m, R, v, &present, bflags);
+    PData od;
+    const int32_t i = pm_put_lane(m, R, v, &present, &od, bflags);
     if (!present) {
         R.D[i].v0 = d > 0 ? 1 : 0;
     } else {
-        const int64_t c = R.D[i].v0 + (d > 0 ? 1 : -1);
+        const int64_t c = od.v0 + (d > 0 ? 1 : -1);
         if (c <= 0 && d < 0) pm_erase(m, R, i);
         else R.D[i].v0 = c;
     }
@@ -506,12 +571,13 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
             PMap m = S.pmap[r.pmap];
             const PRef R = pm_ref(S, m);
             bool present;
-            const int32_t i = pm_put(m, R, v, &present, bflags);  // timeRecorderMap.putIfAbsent(value, now)
+            PData od;
+            const int32_t i = pm_put_lane(m, R, v, &present, &od, bflags);  // timeRecorderMap.putIfAbsent(value, now)
             bool ok = true;
             if (!present) {
                 R.D[i].v0 = t;
             } else {
-                const int64_t last = R.D[i].v0;
+                const int64_t last = od.v0;
                 const int64_t expected = last + cost;
                 if (expected <= t || expected - t < r.max_queue) {
                     const int64_t w = expected - t;
@@ -532,7 +598,8 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
         PMap m = S.pmap[r.pmap];
         const PRef R = pm_ref(S, m);
         bool present;
-        const int32_t i = pm_put(m, R, v, &present, bflags);  // timeCounters.putIfAbsent, then tokenCounters
+        PData od;
+        const int32_t i = pm_put_lane(m, R, v, &present, &od, bflags);  // timeCounters.putIfAbsent, then tokenCounters
         bool ok = true;
         if (!present) {
             PData d;
@@ -541,7 +608,7 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
             d.pad = 0;
             R.D[i] = d;
         } else {
-            PData d = R.D[i];
+            PData d = od;
             const int64_t pass_time = t - d.v0;
             if (pass_time > r.duration_sec * 1000) {
                 int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
