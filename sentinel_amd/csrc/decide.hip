@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  uint32_t* __restrict__ ashort, uint64_t* __restrict__ along,
                                                  uint64_t* __restrict__ amulti, uint32_t* __restrict__ mixc,
                                                  uint32_t* __restrict__ mix, uint32_t mix_cap,
-                                                 uint32_t* __restrict__ mixlen) {
+                                                 uint32_t* __restrict__ mixlen, uint32_t mix_wide) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const bool mixp = (p.xf & XF_MIX) && pq && mix && !(pm & PM_ARGL);
         const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && (p.n_param == 0 || mixp) && sg.len > lane_max &&
                           !lane_only && !p.multi;
-        if (coop && p.n_param) mixk = sg.len > pq_wide ? 2u : 1u;
+        if (coop && p.n_param) mixk = sg.len > mix_wide ? 2u : 1u;  // (wide: pvalue.hip's passes, where on)
         if (mixk == 2 && mixlen) atomicAdd(mixlen, sg.len);  // (pvalue.hip's scratch bound)
         uint32_t bin;
         if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS)))
@@ -3161,11 +3161,11 @@ hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
-                          hipStream_t st) {
+                          uint32_t mix_wide, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap, mixlen);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap, mixlen, mix_wide);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

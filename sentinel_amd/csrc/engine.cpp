@@ -54,6 +54,7 @@ hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
+                          uint32_t mix_wide,
                           hipStream_t st);
 // aux.hip
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
@@ -594,6 +595,7 @@ struct sg_engine {
     PvSeg* d_pvtseg = nullptr;  // the post pass's (pvalue.hip launch_pvt)
     bool pvt_on = false;        // SG_PVT (default: SG_PV): the value-parallel post pass (thread-count maps)
     uint64_t pvseg_cap = 0;
+    uint64_t pvch_cap = 0;      // pvalue.hip's extraction chunk arrays
     uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr;
     uint32_t pv_last_m = 0;     // listed segments of the last batch that ran it (diagnostics)
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
@@ -1929,39 +1931,47 @@ static void free_pv(sg_engine* e) {
     B = PvBuf{};
     e->d_pvhist = e->d_pvpart = nullptr;
     e->pv_cap = 0;
+    e->pvch_cap = 0;
 }
+// (grown with headroom: a reallocation drains the stream, so it must stay rare)
 static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
     if (m > e->pvseg_cap) {
         HIPCHK(hipStreamSynchronize(e->stream));
         dfree(e->d_pvseg);
         dfree(e->d_pvtseg);
-        e->pvseg_cap = std::max<uint64_t>(m, 1024);
+        e->pvseg_cap = std::max<uint64_t>(m + m / 2, 1024);
         HIPCHK(hipMalloc(&e->d_pvseg, e->pvseg_cap * sizeof(PvSeg)));
         HIPCHK(hipMalloc(&e->d_pvtseg, e->pvseg_cap * sizeof(PvSeg)));
-        free_pv(e);  // (the chunk arrays are sized by pvseg_cap)
     }
     if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
-    if (cap <= e->pv_cap) return SG_OK;
-    HIPCHK(hipStreamSynchronize(e->stream));
-    free_pv(e);
-    const uint64_t c = std::max<uint64_t>(cap + cap / 8, 1u << 16);
     PvBuf& B = e->pvb;
-    HIPCHK(hipMalloc(&B.key, c * 8)); HIPCHK(hipMalloc(&B.pos, c * 4)); HIPCHK(hipMalloc(&B.dt, c * 4));
-    HIPCHK(hipMalloc(&B.acq, c * 4)); HIPCHK(hipMalloc(&B.tc, c * 4)); HIPCHK(hipMalloc(&B.seg, c * 4));
-    HIPCHK(hipMalloc(&B.gid, c * 4)); HIPCHK(hipMalloc(&B.idx, c * 4)); HIPCHK(hipMalloc(&B.gid2, c * 4));
-    HIPCHK(hipMalloc(&B.idx2, c * 4)); HIPCHK(hipMalloc(&B.prev, c * 4)); HIPCHK(hipMalloc(&B.w, c * 4));
-    HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
-    HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
-    HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
-    // chunks: cap / PV_CH (4096) + one per segment; m <= pvseg_cap
-    const uint64_t nch = c / 4096 + e->pvseg_cap + 16;
-    HIPCHK(hipMalloc(&B.chunk, nch * 8)); HIPCHK(hipMalloc(&B.ccnt, nch * 4)); HIPCHK(hipMalloc(&B.cof, nch * 4 + 4));
-    HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
-    HIPCHK(hipMalloc(&B.mflag, (c / 256 + 1) * 4)); HIPCHK(hipMalloc(&B.range, c * 16));
-    const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
-    HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
-    HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
-    e->pv_cap = c;
+    if (cap > e->pv_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        free_pv(e);
+        const uint64_t c = std::max<uint64_t>(cap + cap / 4, 1u << 16);
+        HIPCHK(hipMalloc(&B.key, c * 8)); HIPCHK(hipMalloc(&B.pos, c * 4)); HIPCHK(hipMalloc(&B.dt, c * 4));
+        HIPCHK(hipMalloc(&B.acq, c * 4)); HIPCHK(hipMalloc(&B.tc, c * 4)); HIPCHK(hipMalloc(&B.seg, c * 4));
+        HIPCHK(hipMalloc(&B.gid, c * 4)); HIPCHK(hipMalloc(&B.idx, c * 4)); HIPCHK(hipMalloc(&B.gid2, c * 4));
+        HIPCHK(hipMalloc(&B.idx2, c * 4)); HIPCHK(hipMalloc(&B.prev, c * 4)); HIPCHK(hipMalloc(&B.w, c * 4));
+        HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
+        HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
+        HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
+        HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
+        HIPCHK(hipMalloc(&B.mflag, (c / 256 + 1) * 4)); HIPCHK(hipMalloc(&B.range, c * 16));
+        const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
+        HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
+        HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
+        e->pv_cap = c;
+    }
+    // chunks: cap / PV_CH (4096) + one per segment (launch_pv's grid: pv_cap / 4096 + m + 1)
+    const uint64_t nch = e->pv_cap / 4096 + m + 16;
+    if (nch > e->pvch_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
+        e->pvch_cap = nch + nch / 2;
+        HIPCHK(hipMalloc(&B.chunk, e->pvch_cap * 8)); HIPCHK(hipMalloc(&B.ccnt, e->pvch_cap * 4));
+        HIPCHK(hipMalloc(&B.cof, e->pvch_cap * 4 + 4));
+    }
     return SG_OK;
 }
 
@@ -2125,7 +2135,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
                           B.d_ashort, B.d_along, B.d_amulti, e->d_bsmall + 6, e->has_mix ? B.d_mix : nullptr,
-                          (uint32_t)B.mix_cap, e->d_bsmall + 72, gs));
+                          (uint32_t)B.mix_cap, e->d_bsmall + 72, (e->pv_on || e->pvt_on) ? 0u : e->pq_wide, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..8+N_BINS] bin offsets [72] wide XF_MIX events
