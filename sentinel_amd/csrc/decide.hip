@@ -1027,17 +1027,26 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     SEv rn[2];        // software prefetch, two events ahead
     rn[0] = recs[sg.start];
     if (sg.len > 1) rn[1] = recs[sg.start + 1];
+    // the caller's record is read only for an ENTRY's argument key or an EXIT(args) of an earlier batch's ENTRY:
+    // its aux (a random load in submission order) is fetched one event ahead
+    auto need_ev = [](const SEv& r) {
+        return (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG)) ||
+               (r.kind == SG_EV_EXIT && r.code == RC_PASSED && (r.flags & SG_F_EXIT_ARGS));
+    };
+    uint32_t oin = vals[sg.start] & 0x7FFFFFFFu;
+    uint64_t auxn = need_ev(rn[0]) ? ev[oin].aux : 0;
     LPROF(kta)
     for (uint32_t j = 0; j < sg.len; ++j) {
         const SEv r = rn[0];
+        const uint32_t oi = oin;
+        const uint64_t aux = auxn;
         rn[0] = rn[1];
         if (j + 2 < sg.len) rn[1] = recs[sg.start + j + 2];
+        if (j + 1 < sg.len) {
+            oin = vals[sg.start + j + 1] & 0x7FFFFFFFu;
+            auxn = need_ev(rn[0]) ? ev[oin].aux : 0;
+        }
         const int64_t t = t0 + r.dt;
-        const uint32_t oi = vals[sg.start + j] & 0x7FFFFFFFu;
-        // the caller's record is read only for an ENTRY's argument key or an EXIT(args) of an earlier batch's ENTRY
-        const bool need_ev = (r.kind == SG_EV_ENTRY && (r.flags & SG_F_HAS_ARG)) ||
-                             (r.kind == SG_EV_EXIT && r.code == RC_PASSED && (r.flags & SG_F_EXIT_ARGS));
-        const uint64_t aux = need_ev ? ev[oi].aux : 0;
         const EvX x = evx_of(S, oi, r.flags, aux, r.kind == SG_EV_ENTRY);
         const bool has_chain = has_chain_r && x.ctx <= S.max_ctx;  // NullContext: no chain, no statistics
         const bool chain = has_chain && cfg.switch_on;

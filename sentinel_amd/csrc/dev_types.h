@@ -283,11 +283,10 @@ struct PvBuf {          // dense per-access arrays (capacity >= the listed segme
     uint2* chunk;
     uint32_t* ccnt;
     uint32_t* cof;
-    // the walk's inputs in sorted order: time, acquire | hit << 16, record index; misses per 256 sorted positions
+    // the walk's inputs in sorted order: time, acquire | hit << 16, record index
     int32_t* gdt;
     uint32_t* gaw;
     uint32_t* gpos;
-    uint32_t* mflag;
     uint4* range;       // blocked stretches the walk jumped over: {first, end, decision word}; count in tot[2]
 };
 

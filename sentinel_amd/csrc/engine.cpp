@@ -77,7 +77,7 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                       const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                     uint32_t tile);
+                     uint32_t tile, uint32_t* rest);
 hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                       const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
                       uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
@@ -85,10 +85,11 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
                       hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                       const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                      uint32_t tile);
+                      uint32_t tile, uint32_t* rest);
 hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                          const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
-                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st);
+                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st,
+                         const uint32_t* rest, const uint32_t* rest_n);
 hipError_t launch_seg_order(Seg* segs, const uint32_t* mp, uint32_t mb, const uint32_t* off, uint32_t* order,
                             uint32_t* bin_off, hipStream_t st);
 hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t* skeys, uint64_t n,
@@ -593,6 +594,7 @@ struct sg_engine {
     uint64_t pv_cap = 0;
     PvSeg* d_pvseg = nullptr;
     PvSeg* d_pvtseg = nullptr;  // the post pass's (pvalue.hip launch_pvt)
+    uint32_t* d_pvrest = nullptr;  // the wide segments the passes left to k_pq: pre [0, pvseg_cap], post after
     bool pvt_on = false;        // SG_PVT (default: SG_PV): the value-parallel post pass (thread-count maps)
     uint64_t pvseg_cap = 0;
     uint64_t pvch_cap = 0;      // pvalue.hip's extraction chunk arrays
@@ -1309,7 +1311,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_pool_next); dfree(e->d_pmoves);
     if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
     free_pv(e);
-    dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot);
+    dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot); dfree(e->d_pvrest);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
     dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
@@ -1927,7 +1929,7 @@ static void free_pv(sg_engine* e) {
     dfree(B.key); dfree(B.pos); dfree(B.dt); dfree(B.acq); dfree(B.tc); dfree(B.seg); dfree(B.gid); dfree(B.idx);
     dfree(B.gid2); dfree(B.idx2); dfree(B.prev); dfree(B.w); dfree(B.sprev); dfree(B.sw); dfree(B.fslot); dfree(B.hit);
     dfree(B.keep); dfree(B.flast); dfree(B.ftok); dfree(B.htab); dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
-    dfree(B.gdt); dfree(B.gaw); dfree(B.gpos); dfree(B.mflag); dfree(B.range); dfree(e->d_pvhist); dfree(e->d_pvpart);
+    dfree(B.gdt); dfree(B.gaw); dfree(B.gpos); dfree(B.range); dfree(e->d_pvhist); dfree(e->d_pvpart);
     B = PvBuf{};
     e->d_pvhist = e->d_pvpart = nullptr;
     e->pv_cap = 0;
@@ -1942,6 +1944,8 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
         e->pvseg_cap = std::max<uint64_t>(m + m / 2, 1024);
         HIPCHK(hipMalloc(&e->d_pvseg, e->pvseg_cap * sizeof(PvSeg)));
         HIPCHK(hipMalloc(&e->d_pvtseg, e->pvseg_cap * sizeof(PvSeg)));
+        dfree(e->d_pvrest);
+        HIPCHK(hipMalloc(&e->d_pvrest, 2 * (e->pvseg_cap + 1) * 4));
     }
     if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
     PvBuf& B = e->pvb;
@@ -1957,7 +1961,7 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
         HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
         HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
         HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
-        HIPCHK(hipMalloc(&B.mflag, (c / 256 + 1) * 4)); HIPCHK(hipMalloc(&B.range, c * 16));
+        HIPCHK(hipMalloc(&B.range, c * 16));
         const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
         HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
         HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
@@ -2273,11 +2277,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
                          e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
                          (bflags & BF_ZERO_CNT) ? 0u : 1u, ps, launch_radix_hist_n,
-                         launch_radix_scatter_n, launch_scan, radix_tile()));
+                         launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
     }
+    const bool pv_ran = n_mixw && e->pv_on && head[72];  // (k_pq's pre pass: the wide segments it left)
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
-                             e->d_dec, e->d_bsmall + 0, ps));
+                             e->d_dec, e->d_bsmall + 0, ps, pv_ran ? e->d_pvrest + 1 : nullptr, e->d_pvrest));
     HIPCHK(hipEventRecord(e->fork, ps));
     auto lane_bins = [&]() -> int {
         {
@@ -2357,10 +2362,13 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (n_mixw && e->pvt_on && head[72])
         HIPCHK(launch_pvt(e->d_recs, dev_ev, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec,
                           e->d_bsmall + 0, e->d_pvtseg, e->pvb, head[72], e->d_pvtot + 4, e->d_pvhist, e->d_pvpart, st,
-                          launch_radix_hist_n, launch_radix_scatter_n, launch_scan, radix_tile()));
+                          launch_radix_hist_n, launch_radix_scatter_n, launch_scan, radix_tile(),
+                          e->d_pvrest + e->pvseg_cap + 1));
+    const bool pvt_ran = n_mixw && e->pvt_on && head[72];
+    uint32_t* prest = e->d_pvrest + e->pvseg_cap + 1;
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(1, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
-                             e->d_dec, e->d_bsmall + 0, st));
+                             e->d_dec, e->d_bsmall + 0, st, pvt_ran ? prest + 1 : nullptr, prest));
     // origin / context nodes of the segments decided off k_lane<16>, from the committed verdicts (aux.hip)
     if (ext)
         HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_along, B.d_apiece, B.d_amulti, S, dc,

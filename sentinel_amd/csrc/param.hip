@@ -1009,16 +1009,14 @@ __device__ __noinline__ void pq_fold(PqSh<NW>& sh, const Ctx& C, int64_t t0, uin
 //   PQ_POST  ParamFlowStatisticEntryCallback / ExitCallback from the final verdicts: the thread-count map of
 //            paramIdx 0 (passed ENTRYs add, EXITs of passed ENTRYs release) and the node's ParameterMetric bits.
 enum { PQ_FULL = 0, PQ_PRE = 1, PQ_POST = 2 };
+// one segment by one workgroup (every return below is uniform over the workgroup)
 template <int NW, int MODE>
-__global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg_event* __restrict__ ev,
-                                                const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
-                                                const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
-                                                int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+__device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restrict__ recs,
+                                       const sg_event* __restrict__ ev, const uint32_t* __restrict__ vals,
+                                       const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* __restrict__ dec,
+                                       uint32_t* __restrict__ bflags) {
     constexpr uint32_t HW = PqSh<NW>::HW, TE = PqSh<NW>::TE;
-    __shared__ PqSh<NW> sh;
-    if (blockIdx.x >= m) return;
     const uint32_t tid = threadIdx.x;
-    const Seg sg = segs[order[blockIdx.x]];
     if (MODE == PQ_PRE && (sg.bin & SEG_PV)) return;    // pvalue.hip decided its param checks
     if (MODE == PQ_POST && (sg.bin & SEG_PVT)) return;  // pvalue.hip's post pass took its thread-count map
     const uint32_t res = sg.res;
@@ -1343,6 +1341,30 @@ __global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg
     }
 }
 
+template <int NW, int MODE>
+__global__ __launch_bounds__(NW * 64) void k_pq(SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                                const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                                const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                                int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    __shared__ PqSh<NW> sh;
+    if (blockIdx.x >= m) return;
+    pq_seg<NW, MODE>(sh, segs[order[blockIdx.x]], recs, ev, vals, S, cfg, t0, dec, bflags);
+}
+// the segments of a list whose length is on the device (the ones pvalue.hip left), workgroups looping over it
+template <int NW, int MODE>
+__global__ __launch_bounds__(NW * 64) void k_pq_list(SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                                     const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                                     const uint32_t* __restrict__ order, const uint32_t* __restrict__ cnt,
+                                                     DevState S, DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec,
+                                                     uint32_t* __restrict__ bflags) {
+    __shared__ PqSh<NW> sh;
+    const uint32_t n = *cnt;
+    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+        pq_seg<NW, MODE>(sh, segs[order[k]], recs, ev, vals, S, cfg, t0, dec, bflags);
+        __syncthreads();
+    }
+}
+
 // ---- elastic map regions (dev_types.h PM_MIN_NB)
 // Move map id to a region of nn buckets at nbase (fresh pool buckets: every key PK_EMPTY): its live keys, with their
 // stamps and values, by two-choice cuckoo placement (every key of the new table is live: a slot is free iff empty).
@@ -1408,28 +1430,29 @@ __device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned 
     }
     pm_move(S, id, m, nbase, nn, bflags);
 }
-// the listed moves, a workgroup per map: every live key of the old region into the new one (PK_EMPTY-filled pool),
+// the listed moves, a wavefront per map: every live key of the old region into the new one (PK_EMPTY-filled pool),
 // claimed by compare-and-swap in either of its buckets; the rare key finding both full is placed afterwards by one
 // lane with pm_move's displacement walk.  The map's order lives in its stamps and ring, not in the slots, so the
-// placement is free.
+// placement is free.  (Most moves are of small maps: 16 to 128 slots.)
 __global__ __launch_bounds__(256) void k_pm_move_list(const uint4* __restrict__ mv, const uint32_t* __restrict__ nmv,
                                                       uint32_t mcap, DevState S, uint32_t* __restrict__ bflags) {
-    __shared__ uint32_t npend;
-    __shared__ uint32_t pend[64];
+    __shared__ uint32_t npend[4];
+    __shared__ uint32_t pend[4][64];
+    const uint32_t wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t n = *nmv < mcap ? *nmv : mcap;
-    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    for (uint32_t k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
         const uint4 v = mv[k];
         const uint32_t id = v.x, nn = v.w;
         const uint64_t nbase = (uint64_t)v.y | ((uint64_t)v.z << 32);
         const PMap m = S.pmap[id];
-        if (threadIdx.x == 0) npend = 0;
-        __syncthreads();
+        if (l == 0) npend[wv] = 0;
+        __builtin_amdgcn_wave_barrier();
         const PBucket* OB = S.pbkt + m.base;
         const PData* OD = S.pdat + m.base * PM_BKT;
         PBucket* NB = S.pbkt + nbase;
         PData* ND = S.pdat + nbase * PM_BKT;
         const uint64_t* bm = S.pbm + m.bm;
-        for (uint32_t sl = threadIdx.x; sl < m.nb * PM_BKT; sl += 256) {
+        for (uint32_t sl = l; sl < m.nb * PM_BKT; sl += 64) {
             const uint64_t ck = OB[sl / PM_BKT].key[sl % PM_BKT];
             const int64_t cs = OB[sl / PM_BKT].stamp[sl % PM_BKT];
             if (ck == PK_EMPTY || !pm_live(m, bm, cs)) continue;
@@ -1451,15 +1474,17 @@ __global__ __launch_bounds__(256) void k_pm_move_list(const uint4* __restrict__ 
                 }
             }
             if (!placed) {
-                const uint32_t p = atomicAdd(&npend, 1u);
-                if (p < 64) pend[p] = sl;
+                const uint32_t p = atomicAdd(&npend[wv], 1u);
+                if (p < 64) pend[wv][p] = sl;
                 else atomicOr(bflags, BF_PTAB_FULL);
             }
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (uint32_t f = 0; f < (npend < 64 ? npend : 64u); ++f) {
-                const uint32_t sl = pend[f];
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (l == 0) {
+            const uint32_t np = npend[wv] < 64 ? npend[wv] : 64u;
+            for (uint32_t f = 0; f < np; ++f) {
+                const uint32_t sl = pend[wv][f];
                 uint64_t ck = OB[sl / PM_BKT].key[sl % PM_BKT];
                 int64_t cs = OB[sl / PM_BKT].stamp[sl % PM_BKT];
                 PData cd = OD[sl];
@@ -1485,7 +1510,7 @@ __global__ __launch_bounds__(256) void k_pm_move_list(const uint4* __restrict__ 
             hd->base = nbase;
             hd->nb = nn;
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
     }
 }
 // Decide stage, before every kernel that touches the maps: the maps a segment may add keys to -- its QPS rules'
@@ -1530,7 +1555,7 @@ hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, cons
     }
     hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags,
                        mv, nmv, mcap);
-    if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 4096 ? mcap : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
+    if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 16384 ? (mcap + 3) / 4 : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
     return hipGetLastError();
 }
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
@@ -1555,10 +1580,19 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
 }
 // XF_MIX segments: the pre pass (post = 0) before the cooperative owners, the post pass (post = 1) after them and
 // k_fill; list = the narrow segments (k_pq<4>), list + wide_off the wide ones (k_pq<16>)
+// rest / rest_n (optional): the wide segments pvalue.hip left, listed on the device: a few workgroups loop over
+// them instead of one launched (and mostly idle: a k_pq<16> workgroup holds a CU's LDS) per wide segment
 hipError_t launch_pq_mix(int post, SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                          const uint32_t* list, uint32_t n_narrow, uint64_t wide_off, uint32_t n_wide, const DevState& S,
-                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
-    if (n_wide) {
+                         const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st,
+                         const uint32_t* rest, const uint32_t* rest_n) {
+    if (n_wide && rest) {
+        const uint32_t g = n_wide < 256 ? n_wide : 256;
+        if (post) hipLaunchKernelGGL((k_pq_list<16, PQ_POST>), dim3(g), dim3(1024), 0, st, recs, ev, vals, segs, rest,
+                                     rest_n, S, cfg, t0, dec, bflags);
+        else hipLaunchKernelGGL((k_pq_list<16, PQ_PRE>), dim3(g), dim3(1024), 0, st, recs, ev, vals, segs, rest, rest_n,
+                                S, cfg, t0, dec, bflags);
+    } else if (n_wide) {
         if (post) hipLaunchKernelGGL((k_pq<16, PQ_POST>), dim3(n_wide), dim3(1024), 0, st, recs, ev, vals, segs,
                                      list + wide_off, n_wide, S, cfg, t0, dec, bflags);
         else hipLaunchKernelGGL((k_pq<16, PQ_PRE>), dim3(n_wide), dim3(1024), 0, st, recs, ev, vals, segs, list + wide_off,

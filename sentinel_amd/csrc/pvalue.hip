@@ -110,7 +110,7 @@ __device__ void pv_ring_prefix(const DevState& S, const PMap& mp, uint32_t* red)
 // ---- prep: one workgroup per listed segment: eligibility, the map's ring prefix counts, extraction chunks
 #define PV_CH 4096u  // positions per extraction chunk
 __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
-                                                 DevState S, PvSeg* __restrict__ pv) {
+                                                 DevState S, PvSeg* __restrict__ pv, uint32_t* __restrict__ rest) {
     __shared__ uint32_t red[4];
     __shared__ uint32_t okf;
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const u
         okf = ok;
     }
     __syncthreads();
-    if (!okf) {
-        if (tid == 0) { PvSeg z{}; z.ok = 0; pv[i] = z; }
+    if (!okf) {  // k_pq's pre pass: rest[1 + k], count rest[0]
+        if (tid == 0) { PvSeg z{}; z.ok = 0; pv[i] = z; rest[1 + atomicAdd(&rest[0], 1u)] = list[i]; }
         return;
     }
     const DRule& r = S.rules[pg.rule_off + k1];
@@ -471,18 +471,34 @@ __global__ void k_pv_gather(const Seg* __restrict__ segs, const uint32_t* __rest
     const bool hit = B.hit[g] != 0;
     B.gaw[q] = (B.acq[g] & 0xFFFFu) | (hit ? 0x10000u : 0u);
     B.gpos[q] = segs[list[B.seg[g]]].start + B.pos[g];
-    if (!hit) atomicOr(&B.mflag[q / PV_B], 1u);
+    reinterpret_cast<uint32_t*>(B.sw)[q] = hit ? 0u : 1u;  // -> MC: misses before each sorted position (scan)
 }
 
-// first miss in sorted positions [lo, hi) (hi if none)
-__device__ uint32_t pv_first_miss(const PvBuf& B, uint32_t lo, uint32_t hi) {
-    uint32_t q = lo;
-    while (q < hi) {
-        if ((q % PV_B) == 0 && q + PV_B <= hi && !B.mflag[q / PV_B]) { q += PV_B; continue; }
-        if (!(B.gaw[q] & 0x10000u)) return q;
-        ++q;
+// the value groups of the sorted accesses, densely: F[q] = q starts a group (scan -> its index), list G[index] = q
+__global__ void k_pv_gflags(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap, uint32_t* __restrict__ F) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= cap) return;
+    F[q] = q < *tot && (q == 0 || B.gid[q] != B.gid[q - 1]) ? 1u : 0u;
+}
+__global__ void k_pv_glist(PvBuf B, const uint32_t* __restrict__ tot, const uint32_t* __restrict__ X,
+                           uint32_t* __restrict__ G) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *tot) return;
+    if (q == 0 || B.gid[q] != B.gid[q - 1]) G[X[q]] = q;
+}
+
+// first miss in sorted positions [lo, hi) (hi if none); MC = exclusive scan of the miss flags (binary search)
+__device__ uint32_t pv_first_miss(const PvBuf& B, const uint32_t* __restrict__ MC, uint32_t lo, uint32_t hi) {
+    if (lo >= hi) return hi;
+    const uint32_t m0 = MC[lo];
+    const uint32_t mend = MC[hi - 1] + ((B.gaw[hi - 1] & 0x10000u) ? 0u : 1u);  // misses before hi
+    if (mend == m0) return hi;
+    uint32_t a = lo + 1, b = hi;  // the first y in (lo, hi] with misses-before(y) > m0 is the miss + 1
+    while (a < b) {
+        const uint32_t md = (a + b) >> 1;
+        if (MC[md] > m0) b = md; else a = md + 1;
     }
-    return hi;
+    return a - 1;
 }
 
 // ---- walk: one lane per value through passDefaultLocalCheck.  Once the bucket is empty, every access up to the
@@ -492,21 +508,12 @@ __device__ uint32_t pv_first_miss(const PvBuf& B, uint32_t lo, uint32_t hi) {
 // durationInSec) x maxCount steps, not one step an access.
 __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ list,
                           PvBuf B, uint32_t* __restrict__ tot, const PvSeg* __restrict__ pv, DevState S, int64_t t0,
-                          uint32_t* __restrict__ dec, uint32_t jumps, uint32_t range_cap, uint32_t* __restrict__ bflags) {
-    const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = tot[0];
-    if (q0 >= n) return;
-    const uint32_t gd = B.gid[q0];
-    if (q0 > 0 && B.gid[q0 - 1] == gd) return;  // not a group start
-    uint32_t qb = q0 + 1;                       // group end: doubling then binary search over the sorted keys
-    {
-        uint32_t step = 1;
-        while (qb < n && B.gid[qb] == gd) { qb = (q0 + 2 * step < n) ? q0 + 2 * step : n; step *= 2; }
-        uint32_t lo = q0 + step / 2, hi = qb;  // gid[lo] == gd (or lo == q0), the end lies in (lo, hi]
-        if (lo < q0 + 1) lo = q0 + 1;
-        while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (B.gid[md] == gd) lo = md + 1; else hi = md; }
-        qb = lo;
-    }
+                          uint32_t* __restrict__ dec, uint32_t jumps, uint32_t range_cap, uint32_t* __restrict__ bflags,
+                          const uint32_t* __restrict__ GL) {
+    const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;  // the value group (GL: their starts, tot[8] of them)
+    const uint32_t n = tot[0], ng = tot[8];
+    if (gi >= ng) return;
+    const uint32_t q0 = GL[gi], qb = gi + 1 < ng ? GL[gi + 1] : n;
     const uint32_t g0 = B.idx[q0];
     const uint32_t si = B.seg[g0];
     const PvSeg ps = pv[si];
@@ -553,7 +560,7 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
             const int32_t lim = lim64 > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)lim64;
             uint32_t lo = q, hi = qb;
             while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (B.gdt[md] <= lim) lo = md + 1; else hi = md; }
-            const uint32_t tgt = pv_first_miss(B, q, lo);
+            const uint32_t tgt = pv_first_miss(B, reinterpret_cast<const uint32_t*>(B.sw), q, lo);
             if (tgt > q + 8) {  // a stretch of blocks: to k_pv_ranges
                 const uint32_t k = atomicAdd(&tot[2], 1u);
                 if (k < range_cap) { B.range[k] = make_uint4(q, tgt, blk, 0u); q = tgt; }
@@ -896,7 +903,7 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
                                                     uint32_t* __restrict__ bflags, uint32_t tmode,
                                                     Seg* __restrict__ segs, const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ X, const uint32_t* __restrict__ L,
-                                                    uint32_t* __restrict__ ndone) {
+                                                    uint32_t* __restrict__ ndone, uint32_t* __restrict__ rest) {
     __shared__ uint64_t ring[PV_RW];
     __shared__ uint32_t pre[PV_RW];
     __shared__ unsigned long long claim[PV_CW];
@@ -906,8 +913,11 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
     if (i >= m) return;
     const PvSeg ps = pv[i];
-    PMap mp = S.pmap[ps.mid];
-    if (!pv_commits(ps, mp, tmode)) return;
+    PMap mp = S.pmap[ps.ok ? ps.mid : 0];
+    if (!pv_commits(ps, mp, tmode)) {  // (post pass) k_pq's post pass: rest[1 + k], count rest[0]
+        if (tmode && tid == 0) rest[1 + atomicAdd(&rest[0], 1u)] = list[i];
+        return;
+    }
     const uint32_t W = 1u << (mp.rb_log2 - 6);
     const int32_t cap = (int32_t)mp.cap;
     PBucket* BK = S.pbkt + mp.base;
@@ -1140,14 +1150,15 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
                      hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                       const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                      hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                     uint32_t tile) {
+                     uint32_t tile, uint32_t* rest) {
     if (!m || !cap) return hipSuccess;
     const uint32_t nchunk = cap / PV_CH + m + 1;
     hipError_t e = hipMemsetAsync(tot, 0, 16, st);
     if (e == hipSuccess) e = hipMemsetAsync(B.htab, 0xFF, 2ull * cap * 8, st);  // the segments' tables: PK_EMPTY
-    if (e == hipSuccess) e = hipMemsetAsync(B.mflag, 0, ((cap + PV_B - 1) / PV_B) * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv);
+    e = hipMemsetAsync(rest, 0, 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv, rest);
     hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
     hipLaunchKernelGGL(k_pv_count, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot, dec);
     hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
@@ -1160,12 +1171,23 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
     e = pv_resid(B, cap, tot, pv, S, part, st, scan);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_gather, dim3(nb), dim3(256), 0, st, segs, list, B, tot);
-    hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags);
+    {   // MC in place (its values up to tot read only the flags before them)
+        uint32_t* mc = reinterpret_cast<uint32_t*>(B.sw);
+        e = scan(mc, mc, cap, part, nullptr, st);
+        if (e != hipSuccess) return e;
+    }
+    // the groups' starts, densely (flags in gid2, scanned in place, count in tot[8]; list in idx2)
+    hipLaunchKernelGGL(k_pv_gflags, dim3(nb), dim3(256), 0, st, B, tot, cap, B.gid2);
+    e = scan(B.gid2, B.gid2, cap, part, tot + 8, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pv_glist, dim3(nb), dim3(256), 0, st, B, tot, B.gid2, B.idx2);
+    hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags,
+                       B.idx2);
     hipLaunchKernelGGL(k_pv_ranges, dim3(2048), dim3(256), 0, st, recs, B, tot, cap, dec);
     e = pv_klist(B, cap, tot, pv, S, 0u, part, st, scan);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 0u, segs, list,
-                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, nullptr);
+                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, nullptr, rest);
     return hipGetLastError();
 }
 
@@ -1178,11 +1200,13 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
                       hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                       const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                      uint32_t tile) {
+                      uint32_t tile, uint32_t* rest) {
     if (!m || !cap) return hipSuccess;
     const uint32_t nchunk = cap / PV_CH + m + 1;
     hipError_t e = hipMemsetAsync(tot, 0, 16, st);
     if (e == hipSuccess) e = hipMemsetAsync(B.htab, 0xFF, 2ull * cap * 8, st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(rest, 0, 4, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pvt_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv);
     hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
@@ -1205,7 +1229,7 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
     e = pv_klist(B, cap, tot, pv, S, 1u, part, st, scan);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_commit, dim3(m), dim3(1024), 0, st, B, pv, m, S, bflags, 1u, segs, list,
-                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, tot + 3);
+                       reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, tot + 3, rest);
     return hipGetLastError();
 }
 
