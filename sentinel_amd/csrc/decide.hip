@@ -635,6 +635,66 @@ __device__ bool param_check(const DevState& S, uint32_t tm_base, const DRule& r,
     return true;
 }
 
+// The lane path's common XF_MIX shape -- one QPS DefaultController param rule on args[0] beside the thread-count
+// map of paramIdx 0 -- keeps both map headers in registers over the segment (the lane owns its resource's maps:
+// no other lane reads them) instead of a header load and store per access.
+struct PmLane {
+    uint32_t mid, tid;  // the rule's map / the thread-count map of paramIdx 0 (NO_ID: not held)
+    PMap mp, tm;
+};
+// param_check's passDefaultLocalCheck on the held rule map
+__device__ __forceinline__ bool param_default_lane(const DevState& S, const DRule& r, PMap& m, int acquire, uint64_t v,
+                                                   int64_t t, uint32_t* bflags) {
+    bool hf;
+    const int32_t hc = hot_count(S, r, v, &hf);
+    const int32_t token_count = hf ? hc : r.token_count;
+    if (token_count == 0) return false;
+    const int32_t max_count = j_iadd(token_count, r.burst);
+    if (acquire > max_count) return false;
+    const PRef R = pm_ref(S, m);
+    bool present;
+    PData od;
+    const int32_t i = pm_put_lane(m, R, v, &present, &od, bflags);
+    if (!present) {
+        PData d;
+        d.v0 = t;
+        d.v1 = j_iadd(max_count, -acquire);
+        d.pad = 0;
+        R.D[i] = d;
+        return true;
+    }
+    PData d = od;
+    const int64_t pass_time = t - d.v0;
+    if (pass_time > r.duration_sec * 1000) {
+        const int32_t to_add = (int32_t)((pass_time * token_count) / (r.duration_sec * 1000));
+        const int32_t sum = j_iadd(d.v1, to_add);
+        const int32_t nq = sum > max_count ? j_iadd(max_count, -acquire) : j_iadd(sum, -acquire);
+        if (nq < 0) return false;
+        d.v1 = nq; d.v0 = t;
+        R.D[i] = d;
+        return true;
+    }
+    if (j_iadd(d.v1, -acquire) >= 0) {
+        R.D[i].v1 = j_iadd(d.v1, -acquire);
+        return true;
+    }
+    return false;
+}
+// thread_count_add on the held thread-count map
+__device__ __forceinline__ void thread_add_lane(const DevState& S, PMap& m, uint64_t v, int64_t d, uint32_t* bflags) {
+    const PRef R = pm_ref(S, m);
+    bool present;
+    PData od;
+    const int32_t i = pm_put_lane(m, R, v, &present, &od, bflags);
+    if (!present) {
+        R.D[i].v0 = d > 0 ? 1 : 0;
+    } else {
+        const int64_t c = od.v0 + (d > 0 ? 1 : -1);
+        if (c <= 0 && d < 0) pm_erase(m, R, i);
+        else R.D[i].v0 = c;
+    }
+}
+
 // ---- the Context and args of one event (sg_submit_ex, include/sentinel_gpu.h sg_event_ext)
 struct EvX {
     uint32_t origin, ctx;  // interned ids (0: no origin / sentinel_default_context)
@@ -676,6 +736,26 @@ __device__ void thread_args(const DevState& S, uint32_t tm_base, uint32_t nflags
             }
         } else if (v.kind == SG_ARG_SCALAR) {
             thread_count_add(S, tm_base, i, v.key, d, bflags);
+        }
+    }
+}
+// the same with the thread-count map of paramIdx 0 held by the lane (L->tid)
+__device__ __forceinline__ void thread_args_l(const DevState& S, uint32_t tm_base, uint32_t nflags, const EvX& x,
+                                              int64_t d, uint32_t* bflags, PmLane* L) {
+    if (!L || L->tid == NO_ID) { thread_args(S, tm_base, nflags, x, d, bflags); return; }
+    for (uint32_t i = 0; i < x.n && i < SG_MAX_ARGS; ++i) {
+        if (!(nflags & ni_tm(i))) continue;
+        const sg_arg v = evx_arg(x, i);
+        if (v.kind == SG_ARG_LIST) {
+            for (uint32_t k = 0; k < v.len; ++k) {
+                const sg_arg el = S.args[v.key + k];
+                if (el.kind != SG_ARG_SCALAR) return;
+                if (i == 0) thread_add_lane(S, L->tm, el.key, d, bflags);
+                else thread_count_add(S, tm_base, i, el.key, d, bflags);
+            }
+        } else if (v.kind == SG_ARG_SCALAR) {
+            if (i == 0) thread_add_lane(S, L->tm, v.key, d, bflags);
+            else thread_count_add(S, tm_base, i, v.key, d, bflags);
         }
     }
 }
@@ -828,7 +908,7 @@ __device__ int aux_check(const DevState& S, const DevCfg& cfg, const DRule& r, R
 template <int NRMAX, bool MULTI = false>
 __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg,
                                                const Prog& pg, RState (&rs)[NRMAX], uint32_t res, int64_t t, int cnt,
-                                               uint32_t fl, const EvX& x, uint32_t* bflags) {
+                                               uint32_t fl, const EvX& x, uint32_t* bflags, PmLane* L = nullptr) {
     const DRule* rules = S.rules + pg.rule_off;
     const int np = pg.n_param, nfl = np + pg.n_flow, nr = nfl + pg.n_degrade;
     const bool aux = NRMAX >= 16;  // origin nodes / DefaultNodes (PM_AUX resources and PX_* rules are k_lane<16>'s)
@@ -854,14 +934,17 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
                 const sg_arg v = evx_arg(x, (uint32_t)idx);
                 bool ok = true;
                 int64_t w = 0;
+                const bool held = L && L->mid == r.pmap;  // (a QPS DefaultController rule: no wait)
                 if (v.kind == SG_ARG_LIST) {  // Collection / array: element by element (ParamFlowChecker.java:75-90)
                     for (uint32_t k = 0; k < v.len && ok; ++k) {
                         const sg_arg el = S.args[v.key + k];
                         if (el.kind != SG_ARG_SCALAR) break;  // a null element throws: passLocalCheck passes
-                        ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, el.key, t, w, bflags);
+                        ok = held ? param_default_lane(S, r, L->mp, cnt, el.key, t, bflags)
+                                  : param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, el.key, t, w, bflags);
                     }
                 } else if (v.kind == SG_ARG_SCALAR) {
-                    ok = param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, v.key, t, w, bflags);
+                    ok = held ? param_default_lane(S, r, L->mp, cnt, v.key, t, bflags)
+                              : param_check(S, pg.tm_base, r, (uint32_t)idx, cnt, v.key, t, w, bflags);
                 }
                 if (!ok) { status = ST_BLOCK_PARAM; slot = r.slot; }
                 else wait += w;
@@ -895,13 +978,13 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
     }
     if (status == ST_PASS_WAIT) {  // StatisticSlot.entry catch PriorityWaitException (StatisticSlot.java:82-96)
         N.thread++;
-        if (N.flags & NI_PM) thread_args(S, pg.tm_base, N.flags, x, 1, bflags);
+        if (N.flags & NI_PM) thread_args_l(S, pg.tm_base, N.flags, x, 1, bflags, L);
         return mk_dec(ST_PASS_WAIT, slot, wait);
     }
     const bool passed = status == ST_PASS;
     stat_entry(N, C, t, cnt, passed);
     // ParamFlowStatisticEntryCallback.onPass -> ParameterMetric.addThreadCount(args)
-    if (passed && (N.flags & NI_PM)) thread_args(S, pg.tm_base, N.flags, x, 1, bflags);
+    if (passed && (N.flags & NI_PM)) thread_args_l(S, pg.tm_base, N.flags, x, 1, bflags, L);
     return passed ? mk_dec(ST_PASS, 0, wait) : mk_dec(status, slot, 0);
 }
 
@@ -911,7 +994,7 @@ __device__ __forceinline__ uint32_t lane_entry(Node& N, const Ctx& C, const DevS
 template <int NRMAX>
 __device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState& S, const DevCfg& cfg, const Prog& pg,
                                           uint32_t res, int64_t t, const SEv& r, const EvX& x, uint64_t ref,
-                                          uint32_t* bflags) {
+                                          uint32_t* bflags, PmLane* L = nullptr) {
     stat_exit(N, C, t, r.cnt, r.rt);
     if (NRMAX >= 16) {  // the exit runs on the nodes its entry counted on (the same origin and context)
         const DRule* flows = S.rules + pg.rule_off + pg.n_param;
@@ -919,13 +1002,13 @@ __device__ __forceinline__ void lane_exit(Node& N, const Ctx& C, const DevState&
         if (chain_ctx_kept(flows, pg.n_flow, x.ctx)) aux_stat(S, cfg, res, AUX_CONTEXT, x.ctx, 3, t, r.cnt, r.rt, bflags);
     }
     if (!(r.flags & SG_F_EXIT_ARGS) || !(N.flags & NI_PM)) return;
-    if (x.n) { thread_args(S, pg.tm_base, N.flags, x, -1, bflags); return; }
+    if (x.n) { thread_args_l(S, pg.tm_base, N.flags, x, -1, bflags, L); return; }
     if (!S.key_ring || ref == SG_REF_NONE) return;
     const uint64_t key = S.key_ring[ref & cfg.ring_mask];
     if (key == NO_KEY) return;
     EvX k;
     k.origin = 0; k.ctx = 0; k.n = 1; k.a = nullptr; k.k0 = key;
-    thread_args(S, pg.tm_base, N.flags, k, -1, bflags);
+    thread_args_l(S, pg.tm_base, N.flags, k, -1, bflags, L);
 }
 
 // A STRATEGY_RELATE component (one segment, members in event order): each event runs on its own
@@ -1021,6 +1104,23 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
 #pragma unroll
     for (int s = 0; s < NRMAX; ++s) if (s < nr) rs[s] = S.rstate[pg.rule_off + s];
     const bool has_chain_r = (N.flags & NI_CHAIN) != 0;
+    PmLane L;  // the common XF_MIX shape's map headers, held over the segment (k_lane<4>)
+    L.mid = L.tid = NO_ID;
+    if (NRMAX <= 4 && pg.n_param) {
+        if (pg.n_param == 1) {
+            const DRule r0 = S.rules[pg.rule_off];
+            if (r0.behavior == SG_CONTROL_BEHAVIOR_DEFAULT && r0.grade == SG_FLOW_GRADE_QPS && r0.param_idx == 0) {
+                L.mid = r0.pmap;
+                L.mp = S.pmap[L.mid];
+            }
+        }
+        const uint32_t tm0 = tmap_of(S, pg.tm_base, 0);
+        if (tm0 != NO_ID && L.mid != NO_ID) {  // (with a THREAD-grade rule n_param > 1: its reads stay in memory)
+            L.tid = tm0;
+            L.tm = S.pmap[tm0];
+        }
+    }
+    PmLane* LP = NRMAX <= 4 ? &L : nullptr;
     if (sg.len && (t0 + recs[sg.start].dt) < (N.sb[0].ws > N.sb[1].ws ? N.sb[0].ws : N.sb[1].ws))
         atomicOr(bflags, BF_BACKWARD);  // Q3: the clock went back across batches
     uint64_t pm = 0;  // passed bits of the segment's first 64 positions
@@ -1053,7 +1153,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
         uint32_t d = mk_dec(ST_NOT_ENTRY, 0, 0);
         if (r.kind == SG_EV_ENTRY) {
             if (!chain) d = mk_dec(ST_NO_CHECK, 0, 0);
-            else d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, x, bflags);
+            else d = lane_entry<NRMAX>(N, C, S, cfg, pg, rs, res, t, r.cnt, r.flags, x, bflags, LP);
             if (j < 64 && st_passed(d & 0xFF)) pm |= 1ull << j;
             LPROF(ktb)
         } else {
@@ -1070,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
                 if (r.kind == SG_EV_EXIT) {
                     const uint64_t ref = r.code == RC_NONE ? SG_REF_NONE
                                          : r.code == RC_BATCH ? S.gbase + (vals[r.x] & 0x7FFFFFFFu) : (aux & SG_REF_NONE);
-                    lane_exit<NRMAX>(N, C, S, cfg, pg, res, t, r, x, ref, bflags);
+                    lane_exit<NRMAX>(N, C, S, cfg, pg, res, t, r, x, ref, bflags, LP);
                 } else {
                     stat_trace(N, C, t, r.cnt);
                 }
@@ -1081,6 +1181,8 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     }
     min_flush(N, C.minb);
     node_store(N, S, res, pg.pflags);
+    if (L.mid != NO_ID) pm_store(S, L.mid, L.mp);
+    if (L.tid != NO_ID) pm_store(S, L.tid, L.tm);
 #pragma unroll
     for (int s = 0; s < NRMAX; ++s) if (s < nr) S.rstate[pg.rule_off + s] = rs[s];
 #ifdef SG_KPROF
