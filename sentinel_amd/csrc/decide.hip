@@ -196,7 +196,9 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
             // k_lite: no param rules, <= 2 DefaultController flow stages (QPS or thread), <= 2 breakers
-            const bool lite = p.n_param == 0 && !p.multi && !lane_only && (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
+            // (or one QPS DefaultController param rule on args[0] before them, scalar args: k_lite<true>)
+            const bool lite = (p.n_param == 0 || ((p.xf & XF_PLITE) && !(pm & PM_ARGL))) && !p.multi && !lane_only &&
+                              (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
             bin = (lite ? BIN_LITE : (nr <= 4 && !inline_aux) ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
         }
         // k_lane<16> keeps a PM_AUX resource's nodes inline; on every other owner the post-pass does
@@ -1256,7 +1258,13 @@ __device__ __forceinline__ void lm_roll(LiteMin& L, Node& N, Bkt* minb, int64_t 
     }
 }
 
-__global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+// PL (XF_PLITE programs, the launch's other lanes return): ParamFlowSlot's one QPS DefaultController rule on args[0]
+// first (ParamFlowSlot.java:77-101, ParamFlowChecker.passDefaultLocalCheck), its map and the thread-count map of
+// paramIdx 0 held by the lane (PmLane), ParamFlowStatisticEntryCallback / ExitCallback on them
+// (ParameterMetric.java:117-241); args[0]'s key from the key ring (k_rs_first).
+template <bool PL>
+__global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                              const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                                               const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                               int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1264,8 +1272,19 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
     const Seg sg = segs[order[i]];
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
+    if (((pg.xf & XF_PLITE) != 0) != PL) return;
     const int nf = pg.n_flow, nd = pg.n_degrade;  // <= 2 each (PF_J16)
-    const DRule* rules = S.rules + pg.rule_off;
+    const DRule* rules = S.rules + pg.rule_off + (PL ? 1 : 0);  // (flow stages, then breakers)
+    PmLane PLM;
+    PLM.mid = PLM.tid = NO_ID;
+    DRule pr;
+    if (PL) {
+        pr = S.rules[pg.rule_off];
+        PLM.mid = pr.pmap;
+        PLM.mp = S.pmap[pr.pmap];
+        PLM.tid = tmap_of(S, pg.tm_base, 0);
+        if (PLM.tid != NO_ID) PLM.tm = S.pmap[PLM.tid];
+    }
     // per-segment rule constants: flow thresholds, degrade grades/thresholds/windows
     double fcnt[2] = {0.0, 0.0};
     bool fthr[2] = {false, false};
@@ -1283,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
         if (k < nd) {
             dr[k] = deg_param(rules[nf + k]);
             dslot[k] = rules[nf + k].slot;
-            ds[k] = S.rstate[pg.rule_off + nf + k];
+            ds[k] = S.rstate[pg.rule_off + (PL ? 1 : 0) + nf + k];
         }
     }
 #ifdef SG_KPROF
@@ -1343,6 +1362,16 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
             else {
                 if (T != L.T) lm_roll(L, N, C.minb, T, C.max_rt, C.pflags);
                 uint32_t status = ST_PASS, slot = 0;
+                uint64_t key = NO_KEY;
+                if (PL) {  // ParamFlowSlot: initHotParamMetricsFor, the rule's index bit, then its check
+                    N.flags |= NI_PM | ni_tm(0);
+                    if ((rw.w >> 8) & SG_F_HAS_ARG)
+                        key = S.key_ring[(S.gbase + (vals[sg.start + j] & 0x7FFFFFFFu)) & cfg.ring_mask];
+                    if (key != NO_KEY && !param_default_lane(S, pr, PLM.mp, cntv, key, t, bflags)) {
+                        status = ST_BLOCK_PARAM;
+                        slot = pr.slot;
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {  // FlowSlot: DefaultController on the ClusterNode
                     if (k < nf && status == ST_PASS) {
@@ -1375,6 +1404,8 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                     L.pd.b += cntv;
                 }
                 LPROF(kth)
+                // ParamFlowStatisticEntryCallback.onPass -> addThreadCount(args[0])
+                if (PL && passed && key != NO_KEY && PLM.tid != NO_ID) thread_add_lane(S, PLM.tm, key, 1, bflags);
                 d = passed ? mk_dec(ST_PASS, 0, 0) : mk_dec(status, slot, 0);
                 if (passed && j < 256) {
                     const uint64_t b = 1ull << (j & 63);
@@ -1403,6 +1434,18 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
                 L.pd.rt += rtv;
                 if (rtv < L.pd.minrt) L.pd.minrt = rtv;
                 N.thread--;
+                const uint32_t rfl = (rw.w >> 8) & 0xFFu;
+                if (PL && (rfl & SG_F_EXIT_ARGS) && (N.flags & NI_PM) && (N.flags & ni_tm(0)) && PLM.tid != NO_ID) {
+                    // ParamFlowStatisticExitCallback: its own args[0], else its ENTRY's (lane_exit)
+                    uint64_t ref = SG_REF_NONE;
+                    if (rfl & RF_OWN_ARGS) ref = S.gbase + (vals[sg.start + j] & 0x7FFFFFFFu);
+                    else if (code == RC_BATCH) ref = S.gbase + (vals[rx] & 0x7FFFFFFFu);
+                    else if (code == RC_PASSED) ref = ev[vals[sg.start + j] & 0x7FFFFFFFu].aux & SG_REF_NONE;
+                    if (ref != SG_REF_NONE) {
+                        const uint64_t key = S.key_ring[ref & cfg.ring_mask];
+                        if (key != NO_KEY) thread_add_lane(S, PLM.tm, key, -1, bflags);
+                    }
+                }
             } else if (eff && cntv > 0) {  // ClusterNode.trace
                 if (T != L.T) lm_roll(L, N, C.minb, T, C.max_rt, C.pflags);
                 const int sl = sec_current(N, t, C.max_rt);
@@ -1426,7 +1469,11 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
     node_store(N, S, res, pg.pflags);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-        if (k < nd) S.rstate[pg.rule_off + nf + k] = ds[k];
+        if (k < nd) S.rstate[pg.rule_off + (PL ? 1 : 0) + nf + k] = ds[k];
+    if (PL) {
+        pm_store(S, PLM.mid, PLM.mp);
+        if (PLM.tid != NO_ID) pm_store(S, PLM.tid, PLM.tm);
+    }
     LPROF(ktd)
 #ifdef SG_KPROF
     if (kp) {
@@ -3356,7 +3403,11 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
                            cfg, t0, dec, bflags);
         break;
     case BIN_LITE:
-        hipLaunchKernelGGL(k_lite, dim3((m + 255) / 256), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+        hipLaunchKernelGGL(k_lite<false>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg,
+                           t0, dec, bflags);
+        if (S.key_ring)  // (param rules exist: XF_PLITE programs may)
+            hipLaunchKernelGGL(k_lite<true>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S,
+                               cfg, t0, dec, bflags);
         break;
     case BIN_LANE:
         hipLaunchKernelGGL(k_lane<4>, dim3((m + 255) / 256), dim3(256), 0, st, recs, ev, vals, segs, order, m, S, cfg,

@@ -103,10 +103,11 @@ struct Prog {
 enum : uint16_t {
     XF_PTHREAD = 1,      // a THREAD-grade param rule is checked (k_pq resolves an EXIT's release against its ENTRY's
                          // check of the same tile by key: an EXIT with its own args (PM_XARGS) is k_lane's)
-    XF_MIX = 2           // param rules beside flow / degrade rules, cooperatively decided: k_pq's
+    XF_MIX = 2,          // param rules beside flow / degrade rules, cooperatively decided: k_pq's
                          // pre pass decides the QPS param checks per value first (nothing before ParamFlowSlot
                          // blocks), the Jacobi owner the flow / degrade chain with those verdicts as inputs, and
                          // k_pq's post pass the thread-count map from the final verdicts
+    XF_PLITE = 4         // XF_MIX with exactly one (checked) param rule: its short segments take k_lite<true>
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)

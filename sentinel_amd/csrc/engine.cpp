@@ -936,6 +936,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (it != e->tmaps.end() && (*it >> 8) == (uint64_t)r) mix = false;
             }
             if (mix && e->mix_on) { p.xf |= XF_MIX; any_mix = true; }
+            if ((p.xf & XF_MIX) && p.n_param == 1 && rules[p.rule_off].behavior != PB_INIT_ONLY) p.xf |= XF_PLITE;
             if ((p.n_param && !(p.xf & XF_MIX)) || p.n_flow > 4 || p.n_degrade > 4 || n_rl > 2 || p.multi)
                 p.pflags |= PF_SERIAL;
             bool all_default_qps = true;
