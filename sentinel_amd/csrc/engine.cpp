@@ -67,6 +67,10 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
                      uint32_t* bflags, hipStream_t st);
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
                           uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, hipStream_t st);
+hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PData* od, PBucket* nbk, PData* nd,
+                             uint32_t* sz, uint32_t* off, uint32_t* part, unsigned long long* pool_next,
+                             hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                             hipStream_t st);
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
                               uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
 hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
@@ -475,6 +479,9 @@ struct sg_engine {
     uint64_t pool_nb = 0;                                       // pool buckets (regions grow into it: k_pm_grow)
     unsigned long long* d_pool_next = nullptr;
     uint4* d_pmoves = nullptr;  // k_pm_grow's move list (one entry a map) + its count word at [pmoves_cap]
+    PBucket* d_pbkt2 = nullptr;  // the other pool of the device compaction (compact_pmaps), and its values
+    PData* d_pdat2 = nullptr;
+    uint32_t* d_pcwork = nullptr;  // its scratch: sizes, offsets, scan partials (3 x pmoves_cap + 4096 words)
     uint64_t pmoves_cap = 0;                  // next free pool bucket
     unsigned long long* h_pool_next = nullptr;                  // pinned copy, refreshed by every batch (compaction)
     uint64_t n_compact = 0;                                     // pool compactions (diagnostics)
@@ -1309,7 +1316,7 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     dfree(e->d_sec); dfree(e->d_minb); dfree(e->d_info); dfree(e->d_prog); dfree(e->d_rules); dfree(e->d_rstate);
     dfree(e->d_hot); dfree(e->d_pmap); dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_tmid); dfree(e->d_ring); dfree(e->d_small); dfree(e->d_sink);
-    dfree(e->d_pool_next); dfree(e->d_pmoves);
+    dfree(e->d_pool_next); dfree(e->d_pmoves); dfree(e->d_pbkt2); dfree(e->d_pdat2); dfree(e->d_pcwork);
     if (e->h_pool_next) (void)hipHostFree(e->h_pool_next);
     free_pv(e);
     dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot); dfree(e->d_pvrest);
@@ -1808,9 +1815,42 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     e->tmaps = tmaps;
     if (keys.size() > e->pmoves_cap) {  // (the stream is drained: rebuild_pmaps synchronised it above)
         dfree(e->d_pmoves);
+        dfree(e->d_pcwork);
         e->pmoves_cap = keys.size();
         HIPCHK(hipMalloc(&e->d_pmoves, (e->pmoves_cap + 1) * sizeof(uint4)));
     }
+    dfree(e->d_pbkt2);  // (sized by the pool: compact_pmaps allocates it again)
+    dfree(e->d_pdat2);
+    return SG_OK;
+}
+
+// The pool's compaction between batches (drained): on the device, every map's region back to back into the
+// other pool (kept allocated: a host relayout of ~2M maps took a second), then the pools swap.  Without the memory
+// for a second pool, the host relayout (rebuild_pmaps).
+static int compact_pmaps(sg_engine* e) {
+    const uint32_t nm = (uint32_t)e->pmap_key.size();
+    if (!nm) return SG_OK;
+    if (!e->d_pbkt2) {
+        if (hipMalloc(&e->d_pbkt2, e->pool_nb * sizeof(PBucket)) != hipSuccess ||
+            hipMalloc(&e->d_pdat2, e->pool_nb * PM_BKT * sizeof(PData)) != hipSuccess) {
+            (void)hipGetLastError();
+            dfree(e->d_pbkt2);
+            dfree(e->d_pdat2);
+            return rebuild_pmaps(e, e->rmap_cap, e->tmaps);
+        }
+    }
+    if (!e->d_pcwork) HIPCHK(hipMalloc(&e->d_pcwork, (3ull * e->pmoves_cap + 4096) * 4));
+    hipStream_t st = e->stream;
+    HIPCHK(hipMemsetAsync(e->d_pbkt2, 0xFF, e->pool_nb * sizeof(PBucket), st));  // PK_EMPTY: regions grow into it
+    HIPCHK(launch_pm_compact(e->d_pmap, nm, e->d_pbkt, e->d_pdat, e->d_pbkt2, e->d_pdat2, e->d_pcwork,
+                             e->d_pcwork + e->pmoves_cap, e->d_pcwork + 2 * e->pmoves_cap, e->d_pool_next, launch_scan, st));
+    unsigned long long next = 0;
+    HIPCHK(hipMemcpyAsync(&next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::swap(e->d_pbkt, e->d_pbkt2);
+    std::swap(e->d_pdat, e->d_pdat2);
+    e->pool_floor = next;
+    *e->h_pool_next = next;
     return SG_OK;
 }
 
@@ -2044,7 +2084,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // layout took half of what was free (the count is a batch or two old)
     if (e->pool_nb && *e->h_pool_next > e->pool_floor + (e->pool_nb - e->pool_floor) / 2) {
         if (int drc = drain(e)) return drc;
-        if (int crc = rebuild_pmaps(e, e->rmap_cap, e->tmaps)) return crc;
+        if (int crc = compact_pmaps(e)) return crc;
         ++e->n_compact;
     }
     activate(e, k);

@@ -1543,6 +1543,33 @@ __global__ void k_pm_grow_ids(const uint32_t* __restrict__ ids, uint32_t n, DevS
     if (i < n) pm_grow(S, ids[i], 0xFFFFFFFFull, pool_next, pool_nb, bflags);
 }
 
+// ---- pool compaction on the device: every map's region, back to back in map order, into the other pool (the
+// regions maps grew out of are dropped); the rings stay where they are
+__global__ void k_pc_nb(const PMap* __restrict__ pm, uint32_t n, uint32_t* __restrict__ sz) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sz[i] = pm[i].nb;
+}
+// a wavefront per map: buckets (128 B) and values (8 x 16 B a bucket) as 16-byte words; the header's base last
+__global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t n, const uint32_t* __restrict__ off,
+                                                 const PBucket* __restrict__ ob, const PData* __restrict__ od,
+                                                 PBucket* __restrict__ nbk, PData* __restrict__ nd,
+                                                 unsigned long long* __restrict__ pool_next) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+    if (i >= n) return;
+    const PMap m = pm[i];
+    const uint64_t nb = off[i];
+    const uint4* sb = reinterpret_cast<const uint4*>(ob + m.base);
+    uint4* db = reinterpret_cast<uint4*>(nbk + nb);
+    for (uint32_t w = l; w < m.nb * 8u; w += 64) db[w] = sb[w];  // (PBucket: 8 x 16 B)
+    const uint4* sd = reinterpret_cast<const uint4*>(od + m.base * PM_BKT);
+    uint4* dd = reinterpret_cast<uint4*>(nd + nb * PM_BKT);
+    for (uint32_t w = l; w < m.nb * PM_BKT; w += 64) dd[w] = sd[w];  // (PData: 16 B)
+    if (l == 0) {
+        pm[i].base = nb;
+        if (i == n - 1) *pool_next = nb + m.nb;
+    }
+}
+
 namespace sg {
 // mv / nmv / mcap: the move list (null: each lane moves its maps itself)
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
@@ -1556,6 +1583,18 @@ hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, cons
     hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags,
                        mv, nmv, mcap);
     if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 16384 ? (mcap + 3) / 4 : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
+    return hipGetLastError();
+}
+// sz / off: n words each; part: scan partials
+hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PData* od, PBucket* nbk, PData* nd,
+                             uint32_t* sz, uint32_t* off, uint32_t* part, unsigned long long* pool_next,
+                             hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                             hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pc_nb, dim3((n + 255) / 256), dim3(256), 0, st, pm, n, sz);
+    const hipError_t e = scan(sz, off, n, part, nullptr, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pc_copy, dim3((n + 3) / 4), dim3(256), 0, st, pm, n, off, ob, od, nbk, nd, pool_next);
     return hipGetLastError();
 }
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
