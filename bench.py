@@ -427,7 +427,7 @@ CONFIGS = [
     (3, 24_000_000, 1 << 24, {}, 1, "C3: 100k resources, QPS / thread / WarmUp / RateLimiter / WarmUpRateLimiter"),
     (5, 12_000_000, 1 << 23, {"param_table_log2": 28, "status_ring_log2": 26}, 0,
      "C5: 10k resources, ParamFlow QPS rules (20 % throttle) over 10M Zipf values"),
-    (6, 49_500_000, 1 << 25, {"param_table_log2": 28, "status_ring_log2": 28, "max_rules": 1 << 22}, 0,
+    (6, 49_500_000, 1 << 25, {"param_table_log2": 29, "status_ring_log2": 28, "max_rules": 1 << 22}, 0,
      "C6 (north_star's mixed rules): 1M resources, each a QPS flow rule + a DegradeRule + a QPS ParamFlowRule on "
      "args[0] (values Zipf(1.1) over 10M), Zipf(1.1) traffic"),
 ]

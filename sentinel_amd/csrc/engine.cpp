@@ -595,6 +595,7 @@ struct sg_engine {
     bool pq_on = true;          // PF_PQ segments to k_pq (SG_PQ=0: the per-lane kernel, as before round 3)
     uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
     bool mix_on = true;         // XF_MIX programs (SG_MIX=0: every param + flow / degrade resource one lane)
+    bool mix_pq = false;        // SG_MIX_PQ=1: param-only programs of the XF_MIX shape decided as XF_MIX too
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
     bool pv_on = true;          // SG_PV (default 1): the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
     PvBuf pvb{};                // its scratch (decide stage only: one set)
@@ -929,7 +930,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
             // paramIdx 0 with LDS-sized maps only -- their verdicts are then a function of earlier checks of the
             // same (rule, value) alone (no THREAD grade: its count moves with full-chain passes; no throttle:
             // its wait would add to the flow stages')
-            bool mix = p.n_param >= 1 && p.n_param <= 4 && (p.n_flow + p.n_degrade) > 0 && !p.multi;
+            bool mix = p.n_param >= 1 && p.n_param <= 4 && ((p.n_flow + p.n_degrade) > 0 || e->mix_pq) && !p.multi;
             for (int i = 0; i < p.n_param && mix; ++i) {
                 const DRule& d = rules[p.rule_off + i];
                 if (d.param_idx < 0) mix = false;
@@ -973,7 +974,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 auto it = e->tmaps.lower_bound(((uint64_t)r << 8) | 1);
                 if (it != e->tmaps.end() && (*it >> 8) == (uint64_t)r) pq = false;
             }
-            if (pq) p.pflags |= PF_PQ;
+            if (pq && !(p.xf & XF_MIX)) p.pflags |= PF_PQ;
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
         }
         // carry controller / breaker state of kinds that were not reloaded
@@ -1202,6 +1203,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
+    if (const char* v = std::getenv("SG_MIX_PQ")) e->mix_pq = v[0] != '0';
     if (const char* v = std::getenv("SG_PV")) e->pv_on = v[0] != '0';
     e->pvt_on = e->pv_on;
     if (const char* v = std::getenv("SG_PVT")) e->pvt_on = v[0] != '0';

@@ -31,7 +31,7 @@ if which.startswith("c4"):
 elif which == "c6":
     w = T.Workload(6, seed=T.SEED_BASE + 6, n_entries=int(nb * GB / 2.05) + 1000)
     ev = w.events[:nb * GB]
-    eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=28, status_ring_log2=28,
+    eng = E.Engine(max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=29, status_ring_log2=28,
                    max_batch_events=GB, max_rules=1 << 22)
     w.install(eng)
     r = bench.run_batches(eng, ev, GB, dev)
@@ -49,4 +49,5 @@ else:
         oc = T.ext_for(w.events, io, ic, seed=T.SEED_BASE + 45)
         ext["origin_id"], ext["context_id"] = oc["origin_id"], oc["context_id"]
     r = bench.run_batches(eng, w.events, 1 << 23, dev, ext=ext, args=args)
+    r["pv"] = eng.pv_last()
 print(which, r, flush=True)
