@@ -184,8 +184,14 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         if (coop && p.n_param) mixk = sg.len > mix_wide ? 2u : 1u;  // (wide: pvalue.hip's passes, where on)
         if (mixk == 2 && mixlen) atomicAdd(mixlen, sg.len);  // (pvalue.hip's scratch bound)
         uint32_t bin;
-        if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS)))
+        if (pq && (p.pflags & PF_PQ) && !lane_only && !(pm & PM_ARGL) && !((p.xf & XF_PTHREAD) && (pm & PM_XARGS))) {
             bin = sg.len > pq_wide ? BIN_PQ16 : BIN_PQ4;
+            // its checks by the value-parallel passes (pvalue.hip), k_pq folding the statistics (long segments)
+            if ((p.xf & XF_PVPQ) && mix && mix_wide == 0 && sg.len > lane_max) {
+                mixk = 2;
+                if (mixlen) atomicAdd(mixlen, sg.len);
+            }
+        }
         // QPS-DefaultController heads on the 512-lane owner (open stretches), up to J8_MAX events: a longer one (one
         // rank's batch of a strong-scaling run can hold a single resource's 33M events, nearly all in frozen
         // stretches) goes faster through the 1024-lane owner (8-way rehearsal: slowest rank 3.58 vs 2.64 ms)

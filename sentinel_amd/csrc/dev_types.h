@@ -107,7 +107,9 @@ enum : uint16_t {
                          // pre pass decides the QPS param checks per value first (nothing before ParamFlowSlot
                          // blocks), the Jacobi owner the flow / degrade chain with those verdicts as inputs, and
                          // k_pq's post pass the thread-count map from the final verdicts
-    XF_PLITE = 4         // XF_MIX with exactly one (checked) param rule: its short segments take k_lite<true>
+    XF_PLITE = 4,        // XF_MIX with exactly one (checked) param rule: its short segments take k_lite<true>
+    XF_PVPQ = 8          // PF_PQ with one QPS rule (DefaultController or throttle) on paramIdx 0: its long segments'
+                         // checks by pvalue.hip's passes, k_pq then folding the statistics only (SG_PV_PQ)
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)

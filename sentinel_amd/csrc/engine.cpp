@@ -596,6 +596,7 @@ struct sg_engine {
     uint32_t pq_wide = 8192;    // PF_PQ segments longer than this get the 1024-lane k_pq
     bool mix_on = true;         // XF_MIX programs (SG_MIX=0: every param + flow / degrade resource one lane)
     bool mix_pq = false;        // SG_MIX_PQ=1: param-only programs of the XF_MIX shape decided as XF_MIX too
+    bool pv_pq = true;          // SG_PV_PQ (default 1): XF_PVPQ programs' long segments through the value-parallel passes
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
     bool pv_on = true;          // SG_PV (default 1): the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
     PvBuf pvb{};                // its scratch (decide stage only: one set)
@@ -975,6 +976,12 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 if (it != e->tmaps.end() && (*it >> 8) == (uint64_t)r) pq = false;
             }
             if (pq && !(p.xf & XF_MIX)) p.pflags |= PF_PQ;
+            // one checked QPS rule (DefaultController or throttle), no THREAD grade: the value-parallel passes
+            if ((p.pflags & PF_PQ) && e->pv_pq && e->pv_on && p.n_param == 1 && n_thread == 0 &&
+                rules[p.rule_off].behavior != PB_INIT_ONLY) {
+                p.xf |= XF_PVPQ;
+                any_mix = true;
+            }
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
         }
         // carry controller / breaker state of kinds that were not reloaded
@@ -1204,6 +1211,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX_PQ")) e->mix_pq = v[0] != '0';
+    if (const char* v = std::getenv("SG_PV_PQ")) e->pv_pq = v[0] != '0';
     if (const char* v = std::getenv("SG_PV")) e->pv_on = v[0] != '0';
     e->pvt_on = e->pv_on;
     if (const char* v = std::getenv("SG_PVT")) e->pvt_on = v[0] != '0';

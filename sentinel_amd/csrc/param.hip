@@ -1023,6 +1023,9 @@ __device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restri
     const Prog pg = S.prog[res];
     const int np = pg.n_param;
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    // an XF_PVPQ segment pvalue.hip's passes took: its param verdicts are in (RF_PBLK, the passed words with their
+    // throttle wait), its thread-count map and ParameterMetric bits are the post pass's -- only the statistics here
+    const bool pvd = MODE == PQ_FULL && (sg.bin & SEG_PV) != 0;
     if (tid == 0) {
         node_load(sh.node, S, res);
         sh.flags_or = 0;
@@ -1042,6 +1045,7 @@ __device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restri
             sh.rules[tid].grade == SG_FLOW_GRADE_QPS)
             id = sh.rules[tid].pmap;
         if (tid == PQ_MAXP) id = MODE == PQ_PRE ? NO_ID : tm;
+        if (pvd) id = NO_ID;  // (no map is this kernel's)
         sh.mid[tid] = id;
         if (id != NO_ID) sh.hdr[tid] = S.pmap[id];
     }
@@ -1068,7 +1072,7 @@ __device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restri
         if (r.behavior == PB_INIT_ONLY) all_bits |= (uint32_t)r.burst << NI_TM_SHIFT;
         else if (r.param_idx < SG_MAX_ARGS) all_bits |= ni_tm((uint32_t)r.param_idx);
     }
-    const bool tm_on = tm != NO_ID && ((sh.node.flags | all_bits) & ni_tm(0)) != 0;
+    const bool tm_on = tm != NO_ID && ((sh.node.flags | all_bits) & ni_tm(0)) != 0 && !pvd;
     // the THREAD-grade rule (at most one, the last checked, paramIdx 0: engine.cpp PF_PQ) and the first rule whose
     // visit sets the paramIdx-0 thread-map bit; an EXIT decrements only once NI_PM and that bit are set
     int tk = -1, k0 = -1;
@@ -1169,9 +1173,18 @@ __device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restri
         if (tid == 0 && MODE == PQ_FULL) sh.freach = 0xFFFFFFFFu;
         __syncthreads();
         PQ_MARK(0)
+        if (pvd) {  // the value-parallel pre pass's verdicts (one checked rule: rules[0])
+#pragma unroll
+            for (int q = 0; q < PQ_EPL; ++q) {
+                const uint32_t e = tid * PQ_EPL + q, kx = sh.tkx[e];
+                if ((kx & 0xFFu) != SG_EV_ENTRY || tb + e >= sg.len) continue;
+                if ((kx >> 8) & RF_PBLK) st[q] = 1;
+                else if ((kx >> 8) & SG_F_HAS_ARG) wt[q] = ld32(&dec[sg.start + tb + e]) >> 16;
+            }
+        }
         for (int k = 0; k < np; ++k) {
             const DRule& r = sh.rules[k];
-            if (MODE == PQ_POST) break;  // (its visits were taken with the list)
+            if (MODE == PQ_POST || pvd) break;  // (its visits were taken with the list / by pvalue.hip)
             bool reach = false;
 #pragma unroll
             for (int q = 0; q < PQ_EPL; ++q) {

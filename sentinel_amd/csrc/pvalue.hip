@@ -44,25 +44,29 @@ __device__ __forceinline__ int32_t pv_rank(const PMap& m, const uint64_t* bm, co
     return (int32_t)m.live - 1 - (int32_t)below;
 }
 
-// the program's one checked param rule (QPS DefaultController behaviour) and no other checked rule; -1: not eligible
+// the program's one checked param rule (QPS, DefaultController or throttle) and no other checked rule; -1: not eligible
 __device__ __forceinline__ int pv_rule(const DevState& S, const Prog& pg) {
     int k1 = -1;
     for (int k = 0; k < pg.n_param; ++k) {
         const DRule& r = S.rules[pg.rule_off + k];
         if (r.behavior == PB_INIT_ONLY) continue;
-        if (k1 >= 0 || r.param_idx != 0 || r.grade != SG_FLOW_GRADE_QPS || r.behavior != SG_CONTROL_BEHAVIOR_DEFAULT)
-            return -1;
+        if (k1 >= 0 || r.param_idx != 0 || r.grade != SG_FLOW_GRADE_QPS ||
+            (r.behavior != SG_CONTROL_BEHAVIOR_DEFAULT && r.behavior != SG_CONTROL_BEHAVIOR_RATE_LIMITER))
+            return -1;  // (a throttle only in XF_PVPQ programs: XF_MIX has none)
         k1 = k;
     }
     return k1;
 }
 
-// the value's token count (a hot item's, else the rule's)
+// the value's token count (a hot item's, else the rule's: int for passDefaultLocalCheck, long -- held clamped to int
+// here -- for passThrottleLocalCheck)
 __device__ __forceinline__ int32_t pv_tc(const DevState& S, const DRule& r, uint64_t key) {
     for (uint32_t i = 0; i < r.hot_n; ++i) {
         const DHot h = S.hot[r.hot_off + i];
         if (h.key == key) return h.count;
     }
+    if (r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER)
+        return r.token_count_l > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)r.token_count_l;
     return r.token_count;
 }
 
@@ -125,8 +129,13 @@ __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const u
         okf = ok;
     }
     __syncthreads();
-    if (!okf) {  // k_pq's pre pass: rest[1 + k], count rest[0]
-        if (tid == 0) { PvSeg z{}; z.ok = 0; pv[i] = z; rest[1 + atomicAdd(&rest[0], 1u)] = list[i]; }
+    if (!okf) {  // k_pq's pre pass: rest[1 + k], count rest[0] (an XF_PVPQ segment: k_pq's full pass decides it)
+        if (tid == 0) {
+            PvSeg z{};
+            z.ok = 0;
+            pv[i] = z;
+            if (!(pg.xf & XF_PVPQ)) rest[1 + atomicAdd(&rest[0], 1u)] = list[i];
+        }
         return;
     }
     const DRule& r = S.rules[pg.rule_off + k1];
@@ -176,7 +185,8 @@ __global__ __launch_bounds__(256) void k_pv_count(SEv* __restrict__ recs, const 
         if (e.kind != SG_EV_ENTRY || !(e.flags & SG_F_HAS_ARG)) continue;
         const uint64_t key = S.key_ring[(S.gbase + (vals[sg.start + p] & 0x7FFFFFFFu)) & cfg.ring_mask];
         const int32_t tc = pv_tc(S, r, key);
-        if (tc == 0 || (int32_t)e.cnt > j_iadd(tc, r.burst)) {  // blocked before any map access
+        const bool thr = r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER;
+        if (tc == 0 || (!thr && (int32_t)e.cnt > j_iadd(tc, r.burst))) {  // blocked before any map access
             dec[sg.start + p] = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
             recs[sg.start + p].flags = (uint8_t)(e.flags | RF_PBLK);
             continue;
@@ -522,14 +532,55 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
     const int64_t D = r.duration_sec * 1000;
     const int32_t tc = B.tc[g0], maxc = j_iadd(tc, r.burst);
     const uint32_t blk = mk_dec(ST_BLOCK_PARAM, r.slot, 0);
+    const bool thr = r.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER;  // passThrottleLocalCheck (XF_PVPQ only)
+    const bool pvpq = (S.prog[sg.res].xf & XF_PVPQ) != 0;             // passed words are final: written here
     int64_t last = B.flast[g0];  // (valid when the first access hits: the value was live)
-    int32_t tok = B.ftok[g0];
+    int32_t tok = thr ? 0 : B.ftok[g0];  // (a throttle map's second value stays 0)
     uint32_t q = q0, steps = 0;
     while (q < qb) {
         ++steps;
         const int64_t t = t0 + B.gdt[q];
         const uint32_t aw = B.gaw[q];
         const int32_t a = (int32_t)(aw & 0xFFFFu);
+        if (thr) {  // ParamFlowChecker.java:198-248: timeRecorderMap, the expected pass time within maxQueueingTime
+            bool pass = true;
+            int64_t wt = 0;
+            if (!(aw & 0x10000u)) {
+                last = t;
+            } else {
+                const int64_t cost = j_round(1.0 * 1000 * a * (double)r.duration_sec / (double)tc);
+                const int64_t expected = last + cost;
+                if (expected <= t || expected - t < r.max_queue) {
+                    wt = expected - t;
+                    last = wt > 0 ? expected : t;
+                } else {
+                    pass = false;
+                }
+            }
+            const uint32_t rp = B.gpos[q];
+            if (!pass) {
+                dec[rp] = blk;
+                recs[rp].flags = (uint8_t)(recs[rp].flags | RF_PBLK);
+            } else if (pvpq) {
+                dec[rp] = mk_dec(ST_PASS, 0, wt);
+            }
+            ++q;
+            if (!pass && jumps && q < qb) {
+                // every access before last + cost(1) - (maxQueue - 1) blocks (cost grows with the acquire)
+                const int64_t c1 = j_round(1.0 * 1000 * 1 * (double)r.duration_sec / (double)tc);
+                const int64_t lim64 = last + c1 - (r.max_queue > 0 ? r.max_queue - 1 : 0) - 1 - t0;  // blocked: dt <= lim
+                const int32_t lim = lim64 > 0x7FFFFFFF ? 0x7FFFFFFF : lim64 < -0x7FFFFFFF ? -0x7FFFFFFF : (int32_t)lim64;
+                uint32_t lo = q, hi = qb;
+                while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (B.gdt[md] <= lim) lo = md + 1; else hi = md; }
+                const uint32_t tgt = pv_first_miss(B, reinterpret_cast<const uint32_t*>(B.sw), q, lo);
+                if (tgt > q + 8) {
+                    const uint32_t k = atomicAdd(&tot[2], 1u);
+                    if (k < range_cap) { B.range[k] = make_uint4(q, tgt, blk, 0u); q = tgt; }
+                    else atomicSub(&tot[2], 1u);
+                }
+            }
+            continue;
+        }
         bool pass;
         if (!(aw & 0x10000u)) {  // a miss: inserted (timeCounters / tokenCounters.putIfAbsent)
             last = t;
@@ -552,6 +603,8 @@ __global__ void k_pv_walk(SEv* __restrict__ recs, const Seg* __restrict__ segs, 
             const uint32_t rp = B.gpos[q];
             dec[rp] = blk;
             recs[rp].flags = (uint8_t)(recs[rp].flags | RF_PBLK);
+        } else if (pvpq) {
+            dec[B.gpos[q]] = mk_dec(ST_PASS, 0, 0);
         }
         ++q;
         if (jumps && tok == 0 && q < qb) {
@@ -682,6 +735,7 @@ __global__ __launch_bounds__(256) void k_pvt_prep(const Seg* __restrict__ segs, 
             if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_THREAD) thr = true;
         }
         bool ok = (flags & NI_CHAIN) && tm != NO_ID && S.key_ring && !thr && ((flags | all_bits) & ni_tm(0));
+        if ((pg.xf & XF_PVPQ) && !(sg.bin & SEG_PV)) ok = false;  // (k_pq's full pass took its thread-count map)
         if (ok) {
             const PMap mp = S.pmap[tm];
             ok = mp.cap <= PQ_MAX_CAP && (mp.rb_log2 - 6) <= 9;
@@ -915,7 +969,10 @@ __global__ __launch_bounds__(1024) void k_pv_commit(PvBuf B, const PvSeg* __rest
     const PvSeg ps = pv[i];
     PMap mp = S.pmap[ps.ok ? ps.mid : 0];
     if (!pv_commits(ps, mp, tmode)) {  // (post pass) k_pq's post pass: rest[1 + k], count rest[0]
-        if (tmode && tid == 0) rest[1 + atomicAdd(&rest[0], 1u)] = list[i];
+        if (tmode && tid == 0) {  // (an XF_PVPQ segment the pre pass did not take: k_pq's full pass did it all)
+            const Seg sgc = segs[list[i]];
+            if (!(S.prog[sgc.res].xf & XF_PVPQ) || (sgc.bin & SEG_PV)) rest[1 + atomicAdd(&rest[0], 1u)] = list[i];
+        }
         return;
     }
     const uint32_t W = 1u << (mp.rb_log2 - 6);
