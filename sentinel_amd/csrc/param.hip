@@ -1001,6 +1001,139 @@ __device__ __noinline__ void pq_fold(PqSh<NW>& sh, const Ctx& C, int64_t t0, uin
     }
 }
 
+// XF_PVPQ segments pvalue.hip decided (SEG_PV): StatisticSlot over the final verdicts (StatisticSlot.java:54-173),
+// a workgroup per segment, 4 events a lane a round, one node update per 500 ms bucket (as pq_fold); the passed
+// ENTRYs without an argument get their word here (the ones with one got theirs, with a throttle's wait, from the
+// walk).  An EXIT naming an ENTRY of the batch reads that ENTRY's record flags, not its word (written concurrently).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_pvf(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                                 const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                                 int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    constexpr uint32_t HW = NW * 64, EPL = 4;
+    __shared__ Node node;
+    __shared__ uint32_t red[NW][8];
+    __shared__ int64_t rnx[NW];
+    __shared__ int64_t bnext;
+    if (blockIdx.x >= m) return;
+    const Seg sg = segs[order[blockIdx.x]];
+    if (!(sg.bin & SEG_PV)) return;  // (k_pq's full pass decides the others)
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const Prog pg = S.prog[sg.res];
+    const Ctx C{S.minb + (uint64_t)sg.res * 60, cfg.max_rt, pg.pflags};
+    if (tid == 0) {
+        node_load(node, S, sg.res);
+        if (sg.len && (t0 + recs[sg.start].dt) < (node.sb[0].ws > node.sb[1].ws ? node.sb[0].ws : node.sb[1].ws))
+            atomicOr(bflags, BF_BACKWARD);  // Q3
+    }
+    __syncthreads();
+    for (uint32_t base = 0; base < sg.len; base += HW * EPL) {
+        SEv ev[EPL];
+        bool in[EPL], eff[EPL], pass[EPL];
+        int64_t bk[EPL];
+#pragma unroll
+        for (uint32_t q = 0; q < EPL; ++q) {
+            const uint32_t p = base + q * HW + tid;
+            in[q] = p < sg.len;
+            eff[q] = pass[q] = false;
+            bk[q] = INT64_MAX;
+            if (!in[q]) continue;
+            ev[q] = recs[sg.start + p];
+            bk[q] = (t0 + ev[q].dt) / 500;
+            if (ev[q].kind == SG_EV_ENTRY) {
+                pass[q] = !(ev[q].flags & RF_PBLK);
+                if (!(ev[q].flags & SG_F_HAS_ARG)) dec[sg.start + p] = mk_dec(ST_PASS, 0, 0);
+            } else if (ev[q].code == RC_NONE || ev[q].code == RC_PASSED) {
+                eff[q] = true;
+            } else if (ev[q].code == RC_BATCH) {
+                const uint32_t rel = ev[q].x - sg.start;
+                if (rel >= p) atomicOr(bflags, BF_BAD_REF);
+                else eff[q] = !(recs[ev[q].x].flags & RF_PBLK);
+            }
+        }
+        int64_t bcur = bk[0];  // the round's first bucket: the minimum over the workgroup
+#pragma unroll
+        for (uint32_t q = 1; q < EPL; ++q) bcur = bk[q] < bcur ? bk[q] : bcur;
+        for (int o = 32; o > 0; o >>= 1) { const int64_t y = __shfl_xor(bcur, o, 64); bcur = y < bcur ? y : bcur; }
+        if (l == 0) rnx[w] = bcur;
+        __syncthreads();
+        if (tid == 0) {
+            int64_t b = INT64_MAX;
+            for (int k = 0; k < NW; ++k) b = rnx[k] < b ? rnx[k] : b;
+            bnext = b;
+        }
+        __syncthreads();
+        bcur = uni64_pq(bnext);
+        __syncthreads();
+        while (bcur != INT64_MAX) {
+            uint32_t a[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};  // pass block succ rt exc minrt thread touched
+            int64_t nxt = INT64_MAX;
+#pragma unroll
+            for (uint32_t q = 0; q < EPL; ++q) {
+                if (!in[q]) continue;
+                if (bk[q] != bcur) {
+                    if (bk[q] > bcur && bk[q] < nxt) nxt = bk[q];
+                    continue;
+                }
+                const uint32_t cnt = ev[q].cnt, rt = ev[q].rt;
+                if (ev[q].kind == SG_EV_ENTRY) {
+                    a[7] += 1;
+                    if (pass[q]) { a[0] += cnt; a[6] += 1; }
+                    else a[1] += cnt;
+                } else if (eff[q]) {
+                    if (ev[q].kind == SG_EV_EXIT) {
+                        a[7] += 1;
+                        a[2] += cnt; a[3] += rt; a[5] = rt < a[5] ? rt : a[5]; a[6] -= 1;
+                    } else if (cnt > 0) {
+                        a[7] += 1;
+                        a[4] += cnt;
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t y = (uint32_t)__shfl_xor((int)a[k], o, 64);
+                    a[k] = k == 5 ? (y < a[k] ? y : a[k]) : a[k] + y;
+                }
+                const int64_t yn = __shfl_xor(nxt, o, 64);
+                nxt = yn < nxt ? yn : nxt;
+            }
+            if (l == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) red[w][k] = a[k];
+                rnx[w] = nxt;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t t[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};
+                int64_t nx = INT64_MAX;
+                for (int ww = 0; ww < NW; ++ww) {
+                    for (int k = 0; k < 8; ++k) t[k] = k == 5 ? (red[ww][k] < t[k] ? red[ww][k] : t[k]) : t[k] + red[ww][k];
+                    nx = rnx[ww] < nx ? rnx[ww] : nx;
+                }
+                if (t[7]) {  // the bucket's first touching event resets a stale bucket (LeapArray.currentWindow)
+                    const int64_t tc = bcur * 500;
+                    const int64_t mrt = t[5] == 0xFFFFFFFFu ? INT64_MAX : (int64_t)t[5];
+                    const int sl = sec_current(node, tc, C.max_rt);
+                    sec_add(node, sl, t[0], t[1], t[2], t[3], t[4], mrt);
+                    min_current(node, C.minb, tc, C.max_rt, C.pflags);
+                    min_add(node, t[0], t[1], t[2], t[3], t[4], mrt);
+                    node.thread += (int32_t)t[6];
+                }
+                bnext = nx;
+            }
+            __syncthreads();
+            bcur = uni64_pq(bnext);
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        min_flush(node, C.minb);
+        node_store(node, S, sg.res, pg.pflags);
+    }
+}
+
 // MODE (XF_MIX segments, whose flow / degrade chain a k_jac owner decides between the two passes):
 //   PQ_FULL  the resource's whole decision (PF_PQ);
 //   PQ_PRE   ParamFlowSlot's QPS checks only.  Nothing before ParamFlowSlot blocks, so they see every ENTRY whatever
@@ -1018,6 +1151,7 @@ __device__ __forceinline__ void pq_seg(PqSh<NW>& sh, const Seg sg, SEv* __restri
     constexpr uint32_t HW = PqSh<NW>::HW, TE = PqSh<NW>::TE;
     const uint32_t tid = threadIdx.x;
     if (MODE == PQ_PRE && (sg.bin & SEG_PV)) return;    // pvalue.hip decided its param checks
+    if (MODE == PQ_FULL && (sg.bin & SEG_PV)) return;   // (XF_PVPQ: k_pvf folds its statistics)
     if (MODE == PQ_POST && (sg.bin & SEG_PVT)) return;  // pvalue.hip's post pass took its thread-count map
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
@@ -1623,6 +1757,10 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
     // the wide owner: 1024 lanes (128 VGPRs a lane: ~120 spilled) measured 15 % faster on C5 than 512 lanes with
     // 256 VGPRs and no spill (SG_DEBUG_FLAGS 128 selects that form, for A/B runs)
     SEv* r = const_cast<SEv*>(recs);  // (PQ_FULL reads the records only)
+    if (S.key_ring) {  // the XF_PVPQ segments pvalue.hip decided: their statistics (the others' WGs return at once)
+        if (wide) hipLaunchKernelGGL(k_pvf<16>, dim3(m), dim3(1024), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+        else hipLaunchKernelGGL(k_pvf<4>, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    }
     if (wide && (cfg.dbg_flags & 128))
         hipLaunchKernelGGL((k_pq<8, PQ_FULL>), dim3(m), dim3(512), 0, st, r, ev, vals, segs, order, m, S, cfg, t0, dec, bflags);
     else if (wide)
