@@ -1005,11 +1005,54 @@ __device__ __noinline__ void pq_fold(PqSh<NW>& sh, const Ctx& C, int64_t t0, uin
 // a workgroup per segment, 4 events a lane a round, one node update per 500 ms bucket (as pq_fold); the passed
 // ENTRYs without an argument get their word here (the ones with one got theirs, with a throttle's wait, from the
 // walk).  An EXIT naming an ENTRY of the batch reads that ENTRY's record flags, not its word (written concurrently).
+// the workgroup's sums of one 500 ms bucket onto the node (tid 0): LeapArray.currentWindow (the bucket's first
+// touching event resets a stale bucket), then the additions; uniform call (barriers)
+template <int NW>
+__device__ __forceinline__ void pvf_apply(uint32_t (&a)[8], int64_t b, Node& node, const Ctx& C, uint32_t (*red)[8]) {
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t y = (uint32_t)__shfl_xor((int)a[k], o, 64);
+            a[k] = k == 5 ? (y < a[k] ? y : a[k]) : a[k] + y;
+        }
+    }
+    if (l == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[w][k] = a[k];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};
+        for (int ww = 0; ww < NW; ++ww)
+            for (int k = 0; k < 8; ++k) t[k] = k == 5 ? (red[ww][k] < t[k] ? red[ww][k] : t[k]) : t[k] + red[ww][k];
+        if (t[7]) {
+            const int64_t tc = b * 500;
+            const int64_t mrt = t[5] == 0xFFFFFFFFu ? INT64_MAX : (int64_t)t[5];
+            const int sl = sec_current(node, tc, C.max_rt);
+            sec_add(node, sl, t[0], t[1], t[2], t[3], t[4], mrt);
+            min_current(node, C.minb, tc, C.max_rt, C.pflags);
+            min_add(node, t[0], t[1], t[2], t[3], t[4], mrt);
+            node.thread += (int32_t)t[6];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = k == 5 ? 0xFFFFFFFFu : 0u;
+}
+
+// XF_PVPQ segments pvalue.hip decided (SEG_PV): StatisticSlot over the final verdicts (StatisticSlot.java:54-173),
+// a workgroup per segment, 8 events a lane a round, one node update per 500 ms bucket (as pq_fold): a round within
+// the pending bucket (its first and last events' times tell, the events being in time order) only adds to the
+// lanes' sums.  The passed ENTRYs without an argument get their word here (the ones with one got theirs, with a
+// throttle's wait, from the walk).  An EXIT naming an ENTRY of the batch reads that ENTRY's record flags, not its
+// word (written concurrently).
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_pvf(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                                  const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                                  int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
-    constexpr uint32_t HW = NW * 64, EPL = 4;
+    constexpr uint32_t HW = NW * 64, EPL = 8;
     __shared__ Node node;
     __shared__ uint32_t red[NW][8];
     __shared__ int64_t rnx[NW];
@@ -1026,6 +1069,8 @@ __global__ __launch_bounds__(NW * 64) void k_pvf(const SEv* __restrict__ recs, c
             atomicOr(bflags, BF_BACKWARD);  // Q3
     }
     __syncthreads();
+    uint32_t a[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};  // pass block succ rt exc minrt thread touched (pending bucket)
+    int64_t pend = INT64_MIN;                            // the pending bucket (uniform)
     for (uint32_t base = 0; base < sg.len; base += HW * EPL) {
         SEv ev[EPL];
         bool in[EPL], eff[EPL], pass[EPL];
@@ -1050,22 +1095,28 @@ __global__ __launch_bounds__(NW * 64) void k_pvf(const SEv* __restrict__ recs, c
                 else eff[q] = !(recs[ev[q].x].flags & RF_PBLK);
             }
         }
-        int64_t bcur = bk[0];  // the round's first bucket: the minimum over the workgroup
+        const uint32_t rend = sg.len - base < HW * EPL ? sg.len : base + HW * EPL;
+        const int64_t bfirst = (t0 + recs[sg.start + base].dt) / 500, blast = (t0 + recs[sg.start + rend - 1].dt) / 500;
+        if (bfirst == blast && (pend == bfirst || pend == INT64_MIN)) {  // (uniform) one bucket, the pending one
+            pend = bfirst;
 #pragma unroll
-        for (uint32_t q = 1; q < EPL; ++q) bcur = bk[q] < bcur ? bk[q] : bcur;
-        for (int o = 32; o > 0; o >>= 1) { const int64_t y = __shfl_xor(bcur, o, 64); bcur = y < bcur ? y : bcur; }
-        if (l == 0) rnx[w] = bcur;
-        __syncthreads();
-        if (tid == 0) {
-            int64_t b = INT64_MAX;
-            for (int k = 0; k < NW; ++k) b = rnx[k] < b ? rnx[k] : b;
-            bnext = b;
+            for (uint32_t q = 0; q < EPL; ++q) {
+                if (!in[q]) continue;
+                const uint32_t cnt = ev[q].cnt, rt = ev[q].rt;
+                if (ev[q].kind == SG_EV_ENTRY) {
+                    a[7] += 1;
+                    if (pass[q]) { a[0] += cnt; a[6] += 1; }
+                    else a[1] += cnt;
+                } else if (eff[q]) {
+                    if (ev[q].kind == SG_EV_EXIT) { a[7] += 1; a[2] += cnt; a[3] += rt; a[5] = rt < a[5] ? rt : a[5]; a[6] -= 1; }
+                    else if (cnt > 0) { a[7] += 1; a[4] += cnt; }
+                }
+            }
+            continue;
         }
-        __syncthreads();
-        bcur = uni64_pq(bnext);
-        __syncthreads();
+        if (pend != INT64_MIN) { pvf_apply<NW>(a, pend, node, C, red); pend = INT64_MIN; }
+        int64_t bcur = bfirst;
         while (bcur != INT64_MAX) {
-            uint32_t a[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};  // pass block succ rt exc minrt thread touched
             int64_t nxt = INT64_MAX;
 #pragma unroll
             for (uint32_t q = 0; q < EPL; ++q) {
@@ -1080,54 +1131,27 @@ __global__ __launch_bounds__(NW * 64) void k_pvf(const SEv* __restrict__ recs, c
                     if (pass[q]) { a[0] += cnt; a[6] += 1; }
                     else a[1] += cnt;
                 } else if (eff[q]) {
-                    if (ev[q].kind == SG_EV_EXIT) {
-                        a[7] += 1;
-                        a[2] += cnt; a[3] += rt; a[5] = rt < a[5] ? rt : a[5]; a[6] -= 1;
-                    } else if (cnt > 0) {
-                        a[7] += 1;
-                        a[4] += cnt;
-                    }
+                    if (ev[q].kind == SG_EV_EXIT) { a[7] += 1; a[2] += cnt; a[3] += rt; a[5] = rt < a[5] ? rt : a[5]; a[6] -= 1; }
+                    else if (cnt > 0) { a[7] += 1; a[4] += cnt; }
                 }
             }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t y = (uint32_t)__shfl_xor((int)a[k], o, 64);
-                    a[k] = k == 5 ? (y < a[k] ? y : a[k]) : a[k] + y;
-                }
-                const int64_t yn = __shfl_xor(nxt, o, 64);
-                nxt = yn < nxt ? yn : nxt;
-            }
-            if (l == 0) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) red[w][k] = a[k];
-                rnx[w] = nxt;
-            }
+            for (int o = 32; o > 0; o >>= 1) { const int64_t y = __shfl_xor(nxt, o, 64); nxt = y < nxt ? y : nxt; }
+            if (l == 0) rnx[w] = nxt;
             __syncthreads();
             if (tid == 0) {
-                uint32_t t[8] = {0, 0, 0, 0, 0, 0xFFFFFFFFu, 0, 0};
                 int64_t nx = INT64_MAX;
-                for (int ww = 0; ww < NW; ++ww) {
-                    for (int k = 0; k < 8; ++k) t[k] = k == 5 ? (red[ww][k] < t[k] ? red[ww][k] : t[k]) : t[k] + red[ww][k];
-                    nx = rnx[ww] < nx ? rnx[ww] : nx;
-                }
-                if (t[7]) {  // the bucket's first touching event resets a stale bucket (LeapArray.currentWindow)
-                    const int64_t tc = bcur * 500;
-                    const int64_t mrt = t[5] == 0xFFFFFFFFu ? INT64_MAX : (int64_t)t[5];
-                    const int sl = sec_current(node, tc, C.max_rt);
-                    sec_add(node, sl, t[0], t[1], t[2], t[3], t[4], mrt);
-                    min_current(node, C.minb, tc, C.max_rt, C.pflags);
-                    min_add(node, t[0], t[1], t[2], t[3], t[4], mrt);
-                    node.thread += (int32_t)t[6];
-                }
+                for (int ww = 0; ww < NW; ++ww) nx = rnx[ww] < nx ? rnx[ww] : nx;
                 bnext = nx;
             }
+            // the round's last bucket stays pending (the next round may continue it)
             __syncthreads();
-            bcur = uni64_pq(bnext);
-            __syncthreads();
+            const int64_t nb = uni64_pq(bnext);
+            if (nb == INT64_MAX) { pend = bcur; break; }
+            pvf_apply<NW>(a, bcur, node, C, red);
+            bcur = nb;
         }
     }
+    if (pend != INT64_MIN) pvf_apply<NW>(a, pend, node, C, red);
     if (tid == 0) {
         min_flush(node, C.minb);
         node_store(node, S, sg.res, pg.pflags);
