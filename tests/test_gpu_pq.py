@@ -53,13 +53,16 @@ def test_pq_c5_survey_shape():
     _check(w, eng, orc, [0, 1 << 23, len(ev)])
 
 
+@pytest.mark.parametrize("pvpq", ["0", "1"])
 @pytest.mark.parametrize("wide", ["0", "1073741824"])
 @pytest.mark.parametrize("variant", ["hot", "uniform", "thread"])
-def test_pq_variants(variant, wide, monkeypatch):
+def test_pq_variants(variant, wide, pvpq, monkeypatch):
     # hot items (per-value token counts, some 0: blocked without a map access), uniform churn (a million
     # distinct values), THREAD-grade rules with exits releasing their argument; every segment on the 1024-lane
-    # owner (wide=0) or on the 256-lane one
+    # owner (wide=0) or on the 256-lane one.  pvpq = 1: the long segments of one-rule resources (token bucket or
+    # throttle) through the value-parallel passes, k_pvf folding their statistics (XF_PVPQ)
     monkeypatch.setenv("SG_PQ_WIDE", wide)
+    monkeypatch.setenv("SG_PV_PQ", pvpq)
     v = {"hot": T.V_HOT, "uniform": T.V_HOT | T.V_UNIFORM, "thread": T.V_HOT | T.V_UNIFORM | T.V_THREAD}[variant]
     w = T.Workload(5, n_res=2_000, n_entries=600_000, n_param_values=2_000_000, variant=v)
     eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, param_table_log2=26, status_ring_log2=24)
@@ -67,6 +70,9 @@ def test_pq_variants(variant, wide, monkeypatch):
     w.install(eng)
     w.install(orc)
     _check(w, eng, orc, np.linspace(0, len(w.events), 4).astype(np.int64))
+    if pvpq == "1":
+        st = eng.pv_last()
+        assert st["segments"] > 0 and st["accesses"] > 10_000 and st["post_done"] > 0, st
 
 
 def _rules(thread_on_m3=False):
