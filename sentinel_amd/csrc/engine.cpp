@@ -73,15 +73,19 @@ hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PDat
                              hipStream_t st);
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,
                               uint64_t pool_nb, uint32_t* bflags, hipStream_t st);
-hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
-                     const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
-                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
-                     hipStream_t st,
-                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
-                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
-                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
-                     hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                     uint32_t tile, uint32_t* rest);
+hipError_t launch_pv_a(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                       const DevState& S, const DevCfg& cfg, uint32_t* dec, PvSeg* pv, PvBuf B, uint32_t cap,
+                       uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                       hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                       hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                   const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
+                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                       uint32_t tile, uint32_t* rest);
+hipError_t launch_pv_b(SEv* recs, Seg* segs, const uint32_t* list, uint32_t m, const DevState& S, int64_t t0,
+                       uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* part,
+                       uint32_t jumps, hipStream_t st,
+                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                       uint32_t* rest);
 hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
                       const DevState& S, const DevCfg& cfg, uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B,
                       uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
@@ -588,6 +592,7 @@ struct sg_engine {
     hipStream_t bin_stream[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     hipEvent_t fork0 = nullptr;  // XF_MIX batches: the pre passes on bin_stream[1] start here, beside the lane bins
+    hipEvent_t grown = nullptr;  // ... and their map-touching part after the maps' growth
     bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
@@ -1194,7 +1199,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     for (auto& s : e->bin_stream)
         if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi) != hipSuccess) return bad(fail(SG_EDEVICE, "stream"));
     if (hipEventCreateWithFlags(&e->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->fork0, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&e->fork0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->grown, hipEventDisableTiming) != hipSuccess)
         return bad(fail(SG_EDEVICE, "event"));
     for (auto& v : e->join)
         if (hipEventCreateWithFlags(&v, hipEventDisableTiming) != hipSuccess) return bad(fail(SG_EDEVICE, "event"));
@@ -1343,6 +1349,7 @@ int sg_engine_destroy(sg_engine* e) {
     for (auto& v : e->join) if (v) (void)hipEventDestroy(v);
     if (e->fork) (void)hipEventDestroy(e->fork);
     if (e->fork0) (void)hipEventDestroy(e->fork0);
+    if (e->grown) (void)hipEventDestroy(e->grown);
     for (auto& s : e->bin_stream) if (s) (void)hipStreamDestroy(s);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2214,52 +2221,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const uint32_t* off = head + 8;
     uint32_t bin_n[N_BINS];
     for (int b = 0; b < N_BINS; ++b) bin_n[b] = off[b + 1] - off[b];
-    // ---- decide stage, in order after the previous batch's: references into earlier batches first
-    HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
-    HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
-    // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
-    // compaction check of a later submit
-    if (e->pool_nb) {
-        DevState Sg{};
-        std::memset(&Sg, 0, sizeof(Sg));
-        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
-        Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
-        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, e->d_pmoves,
-                              e->d_pmoves ? reinterpret_cast<uint32_t*>(e->d_pmoves + e->pmoves_cap) : nullptr,
-                              (uint32_t)e->pmoves_cap, st));
-        HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
-    }
-    // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
-    if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
-        const bool grant_all = e->cfg.max_slot_chain_size <= 0;
-        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand,
-                            dev_ev, e->d_prog, dev_ext, SG_MAX_CONTEXTS, st));
-        if (!grant_all) {
-            uint32_t ncand = 0;
-            HIPCHK(hipMemcpyAsync(&ncand, e->d_bsmall + 2, 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            if (ncand) {
-                std::vector<uint64_t> cand(ncand);
-                HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
-                std::sort(cand.begin(), cand.end());  // by batch index of the first ENTRY
-                std::vector<uint64_t> upd;
-                std::unordered_map<uint32_t, int> seen;  // RELATE components list every ENTRY
-                for (uint32_t i = 0; i < ncand; ++i) {
-                    uint32_t res = (uint32_t)cand[i];
-                    if (!seen.emplace(res, 1).second) continue;
-                    bool grant = e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
-                    if (grant) e->n_chains++;
-                    upd.push_back(((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63));
-                }
-                ncand = (uint32_t)upd.size();
-                HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
-                HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
-                HIPCHK(hipStreamSynchronize(st));
-            }
-        }
-    }
-    HIPCHK(hipEventRecord(B.ev[2], st));
-    // ---- 3. decide: cooperative bins on their own streams, lane bins on the main stream
+    // ---- 3. decide: cooperative bins on their own streams, lane bins on the main stream (state for every kernel)
     DevCfg dc;
     std::memset(&dc, 0, sizeof(dc));
     dc.max_rt = e->cfg.statistic_max_rt;
@@ -2307,13 +2269,15 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.aux_cap = e->cfg.aux_node_capacity;
     S.aux_mask = e->aux_mask;
     S.max_ctx = SG_MAX_CONTEXTS;
-    // XF_MIX segments of the cooperative bins: their param checks first (k_pq pre pass), the owners then decide
-    // the flow / degrade chain on them
+    // ---- decide stage, in order after the previous batch's: references into earlier batches first
+    HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
+    // XF_MIX segments of the cooperative bins (and XF_PVPQ ones): their param checks first (the value-parallel pre
+    // pass, else k_pq's), the owners then decide the flow / degrade chain on them.  The pre pass runs on
+    // bin_stream[1] (whose J4 / J1 wait for it anyway); its extraction and sort touch no map, so they start now,
+    // beside the references' resolution and the maps' growth on the main stream; the rest waits for the growth.
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
     // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
     const bool serial_bins = (e->dbg_flags & 8) != 0;
-    // the pre passes concern the cooperative XF_MIX segments only: they run on bin_stream[1] (whose J4 / J1 wait
-    // for them anyway) while the lane bins, which check their params inline, start on the main stream
     const bool pre_split = (n_mix || n_mixw) && !serial_bins;
     hipStream_t ps = pre_split ? e->bin_stream[1] : st;
     if (pre_split) {
@@ -2321,16 +2285,66 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(hipStreamWaitEvent(ps, e->fork0, 0));
     }
     if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
-        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;  // (before this batch's decide work is queued)
+        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
         e->pv_last_m = n_mixw;
     }
-    if (n_mixw && e->pv_on && head[72]) {  // the long ones' param checks value-parallel where eligible (pvalue.hip)
-        HIPCHK(launch_pv(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, t0, e->d_dec, e->d_bsmall + 0,
-                         e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart,
-                         (bflags & BF_ZERO_CNT) ? 0u : 1u, ps, launch_radix_hist_n,
-                         launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
+    const bool pv_ran = n_mixw && e->pv_on && head[72];
+    if (pv_ran)
+        HIPCHK(launch_pv_a(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec, e->d_pvseg, e->pvb,
+                           head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, ps, launch_radix_hist_n,
+                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
+    HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
+    // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
+    // compaction check of a later submit
+    if (e->pool_nb) {
+        DevState Sg{};
+        std::memset(&Sg, 0, sizeof(Sg));
+        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
+        Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
+        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, e->d_pmoves,
+                              e->d_pmoves ? reinterpret_cast<uint32_t*>(e->d_pmoves + e->pmoves_cap) : nullptr,
+                              (uint32_t)e->pmoves_cap, st));
+        HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
     }
-    const bool pv_ran = n_mixw && e->pv_on && head[72];  // (k_pq's pre pass: the wide segments it left)
+    // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
+    if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
+        const bool grant_all = e->cfg.max_slot_chain_size <= 0;
+        HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand,
+                            dev_ev, e->d_prog, dev_ext, SG_MAX_CONTEXTS, st));
+        if (!grant_all) {
+            uint32_t ncand = 0;
+            HIPCHK(hipMemcpyAsync(&ncand, e->d_bsmall + 2, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (ncand) {
+                std::vector<uint64_t> cand(ncand);
+                HIPCHK(hipMemcpy(cand.data(), e->d_cand, ncand * 8ull, hipMemcpyDeviceToHost));
+                std::sort(cand.begin(), cand.end());  // by batch index of the first ENTRY
+                std::vector<uint64_t> upd;
+                std::unordered_map<uint32_t, int> seen;  // RELATE components list every ENTRY
+                for (uint32_t i = 0; i < ncand; ++i) {
+                    uint32_t res = (uint32_t)cand[i];
+                    if (!seen.emplace(res, 1).second) continue;
+                    bool grant = e->n_chains < (uint32_t)e->cfg.max_slot_chain_size;
+                    if (grant) e->n_chains++;
+                    upd.push_back(((uint64_t)(grant ? NI_CHAIN : NI_REJECTED) << 32) | res | (1ull << 63));
+                }
+                ncand = (uint32_t)upd.size();
+                HIPCHK(hipMemcpyAsync(e->d_cand, upd.data(), ncand * 8ull, hipMemcpyHostToDevice, st));
+                HIPCHK(launch_set_flags(e->d_info, e->d_cand, ncand, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+        }
+    }
+    HIPCHK(hipEventRecord(B.ev[2], st));
+    if (pv_ran) {  // the rest of the pre pass, after the maps grew (they move)
+        if (pre_split) {
+            HIPCHK(hipEventRecord(e->grown, st));
+            HIPCHK(hipStreamWaitEvent(ps, e->grown, 0));
+        }
+        HIPCHK(launch_pv_b(e->d_recs, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, t0, e->d_dec, e->d_bsmall + 0,
+                           e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvpart, (bflags & BF_ZERO_CNT) ? 0u : 1u, ps,
+                           launch_scan, e->d_pvrest));
+    }
     if (n_mix || n_mixw)
         HIPCHK(launch_pq_mix(0, e->d_recs, dev_ev, vin, e->d_segs, B.d_mix, n_mix, B.mix_cap, n_mixw, S, dc, t0,
                              e->d_dec, e->d_bsmall + 0, ps, pv_ran ? e->d_pvrest + 1 : nullptr, e->d_pvrest));

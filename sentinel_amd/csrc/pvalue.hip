@@ -1198,16 +1198,17 @@ static hipError_t pv_klist(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv
 
 // the value-parallel pre pass over the wide XF_MIX list (cap accesses at most); pv[] tells k_pq which segments
 // are done.  Scratch: PvBuf arrays of cap entries (chunks: cap / PV_CH + m), htab 2 x cap, radix scratch (hist,
-// part), tot (device words: [0] accesses, [1] chunks, [2] ranges).  jumps: the batch has no zero-acquire ENTRY.
-hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
-                     const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, PvSeg* pv,
-                     PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, uint32_t* part, uint32_t jumps,
-                     hipStream_t st,
-                     hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
-                     hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
-                                                      const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
-                     hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                     uint32_t tile, uint32_t* rest) {
+// part), tot (device words: [0] accesses, [1] chunks, [2] ranges, [3] longest walk, [8] groups).  In two parts:
+// (a) extraction and sort touch no map (they overlap the maps' growth on the main stream), (b) the rest after it.
+// jumps: the batch has no zero-acquire ENTRY.
+hipError_t launch_pv_a(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t* list, uint32_t m,
+                       const DevState& S, const DevCfg& cfg, uint32_t* dec, PvSeg* pv, PvBuf B, uint32_t cap,
+                       uint32_t* tot, uint32_t* hist, uint32_t* part, hipStream_t st,
+                       hipError_t (*radix_hist)(const uint32_t*, uint64_t, const uint32_t*, int, uint32_t*, uint32_t, hipStream_t),
+                       hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
+                                                   const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
+                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                       uint32_t tile, uint32_t* rest) {
     if (!m || !cap) return hipSuccess;
     const uint32_t nchunk = cap / PV_CH + m + 1;
     hipError_t e = hipMemsetAsync(tot, 0, 16, st);
@@ -1220,9 +1221,16 @@ hipError_t launch_pv(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_t*
     hipLaunchKernelGGL(k_pv_count, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot, dec);
     hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
     hipLaunchKernelGGL(k_pv_fill, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot);
+    return pv_sort(B, cap, tot, hist, part, st, radix_hist, radix_scatter, scan, tile);
+}
+hipError_t launch_pv_b(SEv* recs, Seg* segs, const uint32_t* list, uint32_t m, const DevState& S, int64_t t0,
+                       uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* part,
+                       uint32_t jumps, hipStream_t st,
+                       hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                       uint32_t* rest) {
+    if (!m || !cap) return hipSuccess;
+    hipError_t e = hipSuccess;
     const uint32_t nb = (cap + 255) / 256;
-    e = pv_sort(B, cap, tot, hist, part, st, radix_hist, radix_scatter, scan, tile);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
     e = pv_resid(B, cap, tot, pv, S, part, st, scan);
