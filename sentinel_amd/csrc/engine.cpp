@@ -2336,11 +2336,11 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         }
     }
     HIPCHK(hipEventRecord(B.ev[2], st));
-    if (pv_ran) {  // the rest of the pre pass, after the maps grew (they move)
-        if (pre_split) {
-            HIPCHK(hipEventRecord(e->grown, st));
-            HIPCHK(hipStreamWaitEvent(ps, e->grown, 0));
-        }
+    if (pre_split) {  // every map-touching pre-pass kernel after the maps grew (they move) and the chains
+        HIPCHK(hipEventRecord(e->grown, st));
+        HIPCHK(hipStreamWaitEvent(ps, e->grown, 0));
+    }
+    if (pv_ran) {  // the rest of the value-parallel pre pass
         HIPCHK(launch_pv_b(e->d_recs, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, t0, e->d_dec, e->d_bsmall + 0,
                            e->d_pvseg, e->pvb, head[72], e->d_pvtot, e->d_pvpart, (bflags & BF_ZERO_CNT) ? 0u : 1u, ps,
                            launch_scan, e->d_pvrest));
