@@ -37,6 +37,13 @@ elif which == "c6":
     r = bench.run_batches(eng, ev, GB, dev)
     r["pv"] = eng.pv_last()
     r["pool"] = eng.param_pool()
+elif which == "c3":
+    # bench.py's C3 sub-line: 100k resources, all five controller kinds (tracegen variant 1)
+    w = T.Workload(3, seed=T.SEED_BASE + 3, n_entries=24_000_000, variant=1)
+    eng = E.Engine(max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0, max_batch_events=1 << 24,
+                   aux_node_capacity=1 << 20)
+    w.install(eng)
+    r = bench.run_batches(eng, w.events, 1 << 24, dev)
 else:
     w = T.Workload(5, seed=T.SEED_BASE + 5, n_entries=12_000_000)
     eng = E.Engine(max_resources=1 << 14, max_slot_chain_size=0, max_batch_events=1 << 23, param_table_log2=28,
