@@ -94,7 +94,16 @@ public class GpuDecisionSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
                                            SentinelGpu.EV_ENTRY, flags, 0L, eng.originId(context.getOrigin()),
                                            eng.contextId(context.getName()), hasParam ? args : null,
                                            Thread.currentThread());
-        int d = eng.decide(op);
+        int d;
+        try {
+            d = eng.decide(op);
+        } catch (RuntimeException ex) {
+            // the engine died at run time (a batch failed: a full map pool, a poisoned batcher, a device error).
+            // CtSph.entryWithPriority catches anything but a BlockException and lets the entry pass unchecked
+            // (core/CtSph.java:163-166), so record the failure and fail closed, for this entry and every later one
+            GpuChainInit.fail("the engine failed at run time", ex);
+            throw new GpuUnavailableException(GpuChainInit.failure());
+        }
         int status = SentinelGpu.status(d);
         boolean in = resourceWrapper.getType() == EntryType.IN;
         switch (status) {

@@ -202,6 +202,10 @@ static_assert(sizeof(PData) == 16, "PData must be 16 B");
 // could put more keys in it than half its slots -- up to map_buckets(cap) (<= 50 % load at capacity).  1M resources
 // with a rule each would otherwise reserve 2 x 256 KiB of HBM per resource.
 #define PM_MIN_NB 2u
+// The pool's control words (engine.cpp d_pool_next, 4 x u64): the next free bucket, the buckets taken at the last
+// compaction, the on-device compactions so far, and the epoch of the batch whose growth found the pool short (that
+// batch compacts on the device and grows again, param.hip launch_pm_grow)
+enum { PC_NEXT = 0, PC_FLOOR = 1, PC_RESCUES = 2, PC_RESCUE = 3, PC_WORDS = 4 };
 __host__ __device__ inline uint32_t map_buckets(uint32_t cap) { return (2u * cap + PM_BKT - 1) / PM_BKT > 2u ? (2u * cap + PM_BKT - 1) / PM_BKT : 2u; }
 struct PMap {
     uint64_t base;   // first bucket in DevState.pbkt (its slots' data at pdat[base * PM_BKT ...])

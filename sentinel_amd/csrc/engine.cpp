@@ -66,7 +66,10 @@ hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
                      uint32_t* bflags, hipStream_t st);
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
-                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, hipStream_t st);
+                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, uint32_t epoch,
+                          uint32_t nm, PBucket* b2, PData* d2, uint32_t* sz, uint32_t* off, uint32_t* part,
+                          hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                          hipStream_t st);
 hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PData* od, PBucket* nbk, PData* nd,
                              uint32_t* sz, uint32_t* off, uint32_t* part, unsigned long long* pool_next,
                              hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
@@ -489,7 +492,7 @@ struct sg_engine {
     uint64_t pmoves_cap = 0;                  // next free pool bucket
     unsigned long long* h_pool_next = nullptr;                  // pinned copy, refreshed by every batch (compaction)
     uint64_t n_compact = 0;                                     // pool compactions (diagnostics)
-    uint64_t pool_floor = 0;                                    // pool buckets the regions took at the last layout
+    uint64_t pool2_nb = 0;                                      // buckets of d_pbkt2 / d_pdat2 (= pool_nb once laid out)
     uint32_t n_dev_rules = 0;
 
     // device state
@@ -1314,12 +1317,13 @@ extern "C" int sgx_pv_last(sg_engine* e, unsigned long long* out) {
     if (!e->pv_on) out[0] = out[1] = out[2] = out[6] = 0;
     return 0;
 }
-// diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last layout, compactions}
+// diagnostics export: the param map pool, out = {pool buckets, buckets taken, taken at the last compaction,
+// compactions between batches, compactions inside a batch (on the device)}
 extern "C" int sgx_param_pool(sg_engine* e, unsigned long long* out) {
     if (!e || !out || drain(e) != SG_OK) return -1;
-    unsigned long long next = 0;
-    if (e->d_pool_next && hipMemcpy(&next, e->d_pool_next, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    out[0] = e->pool_nb; out[1] = next; out[2] = e->pool_floor; out[3] = e->n_compact;
+    unsigned long long ctl[PC_WORDS] = {0, 0, 0, 0};
+    if (e->d_pool_next && hipMemcpy(ctl, e->d_pool_next, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    out[0] = e->pool_nb; out[1] = ctl[PC_NEXT]; out[2] = ctl[PC_FLOOR]; out[3] = e->n_compact; out[4] = ctl[PC_RESCUES];
     return 0;
 }
 
@@ -1772,21 +1776,36 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     PMap* nh = nullptr;
     uint32_t* nt = nullptr;
     uint64_t* dtri = nullptr;
-    auto release = [&]() { dfree(nbk); dfree(ndt); dfree(nbm); dfree(npr); dfree(nh); dfree(nt); dfree(dtri); };
+    // the compactions' second pool and scratch, allocated with the pool (a compaction that is needed later cannot
+    // fail for memory: ADVICE r4)
+    PBucket* nbk2 = nullptr;
+    PData* ndt2 = nullptr;
+    uint32_t* nwork = nullptr;
+    const uint64_t mcap = std::max<uint64_t>(e->pmoves_cap, keys.size());
+    auto release = [&]() {
+        dfree(nbk); dfree(ndt); dfree(nbm); dfree(npr); dfree(nh); dfree(nt); dfree(dtri); dfree(nbk2); dfree(ndt2);
+        dfree(nwork);
+    };
     const size_t ntri = std::max(tri_b.size(), std::max(tri_d.size(), tri_w.size()));
     if ((nbkt && (hipMalloc(&nbk, pool_nb * sizeof(PBucket)) != hipSuccess ||
                   hipMalloc(&ndt, pool_nb * PM_BKT * sizeof(PData)) != hipSuccess ||
-                  hipMalloc(&nbm, nword * 8) != hipSuccess || hipMalloc(&npr, nword * 4) != hipSuccess)) ||
+                  hipMalloc(&nbm, nword * 8) != hipSuccess || hipMalloc(&npr, nword * 4) != hipSuccess ||
+                  hipMalloc(&nbk2, pool_nb * sizeof(PBucket)) != hipSuccess ||
+                  hipMalloc(&ndt2, pool_nb * PM_BKT * sizeof(PData)) != hipSuccess ||
+                  hipMalloc(&nwork, (3ull * mcap + 4096) * 4) != hipSuccess)) ||
         (!hdr.empty() && hipMalloc(&nh, hdr.size() * sizeof(PMap)) != hipSuccess) ||
         (!tmid.empty() && hipMalloc(&nt, tmid.size() * 4) != hipSuccess) ||
         (ntri && hipMalloc(&dtri, 3 * ntri * 8) != hipSuccess)) {
         release();
         (void)hipGetLastError();
-        return fail(SG_ECAPACITY, "device memory for " + std::to_string(pool_nb * PM_BKT) + " hot-parameter map slots");
+        return fail(SG_ECAPACITY, "device memory for " + std::to_string(pool_nb * PM_BKT) +
+                                      " hot-parameter map slots and their compaction copy (lower param_table_log2)");
     }
     if (!e->d_pool_next) {
-        HIPCHK(hipMalloc(&e->d_pool_next, 8));
-        HIPCHK(hipHostMalloc(&e->h_pool_next, 8));
+        HIPCHK(hipMalloc(&e->d_pool_next, PC_WORDS * 8));
+        HIPCHK(hipMemset(e->d_pool_next, 0, PC_WORDS * 8));
+        HIPCHK(hipHostMalloc(&e->h_pool_next, PC_WORDS * 8));
+        std::memset(e->h_pool_next, 0, PC_WORDS * 8);
     }
     if (nbkt) {
         HIPCHK(hipMemsetAsync(nbk, 0xFF, pool_nb * sizeof(PBucket), e->stream));  // PK_EMPTY keys (regions grow into it)
@@ -1809,6 +1828,11 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     HIPCHK(hipStreamSynchronize(e->stream));
     dfree(dtri);
     dfree(e->d_pbkt); dfree(e->d_pdat); dfree(e->d_pbm); dfree(e->d_ppre); dfree(e->d_pmap); dfree(e->d_tmid);
+    dfree(e->d_pbkt2); dfree(e->d_pdat2); dfree(e->d_pcwork);
+    e->d_pbkt2 = nbk2;
+    e->d_pdat2 = ndt2;
+    e->d_pcwork = nwork;
+    e->pool2_nb = nbkt ? pool_nb : 0;
     e->d_pbkt = nbk;
     e->d_pdat = ndt;
     e->d_pbm = nbm;
@@ -1817,11 +1841,10 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     e->d_tmid = nt;
     e->n_pslot = total;
     e->pool_nb = pool_nb;
-    e->pool_floor = nbkt;
     {
-        const unsigned long long next = nbkt;
-        HIPCHK(hipMemcpy(e->d_pool_next, &next, 8, hipMemcpyHostToDevice));
-        *e->h_pool_next = next;
+        const unsigned long long next[2] = {nbkt, nbkt};  // PC_NEXT, PC_FLOOR
+        HIPCHK(hipMemcpy(e->d_pool_next, next, 16, hipMemcpyHostToDevice));
+        e->h_pool_next[PC_NEXT] = e->h_pool_next[PC_FLOOR] = nbkt;
     }
     e->pmap_key = keys;
     e->pmap_index.clear();
@@ -1832,13 +1855,17 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
     e->tmaps = tmaps;
     if (keys.size() > e->pmoves_cap) {  // (the stream is drained: rebuild_pmaps synchronised it above)
         dfree(e->d_pmoves);
-        dfree(e->d_pcwork);
         e->pmoves_cap = keys.size();
         HIPCHK(hipMalloc(&e->d_pmoves, (e->pmoves_cap + 1) * sizeof(uint4)));
     }
-    dfree(e->d_pbkt2);  // (sized by the pool: compact_pmaps allocates it again)
-    dfree(e->d_pdat2);
     return SG_OK;
+}
+
+// The second pool of the compactions and their scratch exist whenever the pool does: laid out with the maps
+// (rebuild_pmaps), so a compaction never allocates
+static int ensure_pool2(sg_engine* e) {
+    if (!e->pool_nb || (e->pool2_nb == e->pool_nb && e->d_pcwork)) return SG_OK;
+    return fail(SG_ESTATE, "the hot-parameter map pool has no compaction copy");
 }
 
 // The pool's compaction between batches (drained): on the device, every map's region back to back into the
@@ -1847,27 +1874,15 @@ static int rebuild_pmaps(sg_engine* e, const std::map<uint32_t, uint32_t>& rcap,
 static int compact_pmaps(sg_engine* e) {
     const uint32_t nm = (uint32_t)e->pmap_key.size();
     if (!nm) return SG_OK;
-    if (!e->d_pbkt2) {
-        if (hipMalloc(&e->d_pbkt2, e->pool_nb * sizeof(PBucket)) != hipSuccess ||
-            hipMalloc(&e->d_pdat2, e->pool_nb * PM_BKT * sizeof(PData)) != hipSuccess) {
-            (void)hipGetLastError();
-            dfree(e->d_pbkt2);
-            dfree(e->d_pdat2);
-            return rebuild_pmaps(e, e->rmap_cap, e->tmaps);
-        }
-    }
-    if (!e->d_pcwork) HIPCHK(hipMalloc(&e->d_pcwork, (3ull * e->pmoves_cap + 4096) * 4));
+    if (int rc = ensure_pool2(e)) return rc;
     hipStream_t st = e->stream;
     HIPCHK(hipMemsetAsync(e->d_pbkt2, 0xFF, e->pool_nb * sizeof(PBucket), st));  // PK_EMPTY: regions grow into it
     HIPCHK(launch_pm_compact(e->d_pmap, nm, e->d_pbkt, e->d_pdat, e->d_pbkt2, e->d_pdat2, e->d_pcwork,
                              e->d_pcwork + e->pmoves_cap, e->d_pcwork + 2 * e->pmoves_cap, e->d_pool_next, launch_scan, st));
-    unsigned long long next = 0;
-    HIPCHK(hipMemcpyAsync(&next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, PC_WORDS * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     std::swap(e->d_pbkt, e->d_pbkt2);
     std::swap(e->d_pdat, e->d_pdat2);
-    e->pool_floor = next;
-    *e->h_pool_next = next;
     return SG_OK;
 }
 
@@ -2097,9 +2112,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const int k = e->cur;
     rc = collect(e, k);  // the batch that last used this slot (two batches ago) is decided
     if (rc) return rc;
-    // the param map pool: the regions maps grew out of are dropped by a relayout once the growth since the last
-    // layout took half of what was free (the count is a batch or two old)
-    if (e->pool_nb && *e->h_pool_next > e->pool_floor + (e->pool_nb - e->pool_floor) / 2) {
+    // the param map pool: the regions maps grew out of are dropped by a compaction between batches once the growth
+    // since the last one took half of what was free (the counts are a batch or two old); a batch that finds the pool
+    // short before that compacts on the device itself (launch_pm_grow)
+    if (int prc = ensure_pool2(e)) return prc;
+    const unsigned long long pfloor = e->h_pool_next ? e->h_pool_next[PC_FLOOR] : 0;
+    if (e->pool_nb && e->h_pool_next[PC_NEXT] > pfloor + (e->pool_nb - pfloor) / 2) {
         if (int drc = drain(e)) return drc;
         if (int crc = compact_pmaps(e)) return crc;
         ++e->n_compact;
@@ -2271,42 +2289,14 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.max_ctx = SG_MAX_CONTEXTS;
     // ---- decide stage, in order after the previous batch's: references into earlier batches first
     HIPCHK(hipStreamWaitEvent(st, B.ev[1], 0));
-    // XF_MIX segments of the cooperative bins (and XF_PVPQ ones): their param checks first (the value-parallel pre
-    // pass, else k_pq's), the owners then decide the flow / degrade chain on them.  The pre pass runs on
-    // bin_stream[1] (whose J4 / J1 wait for it anyway); its extraction and sort touch no map, so they start now,
-    // beside the references' resolution and the maps' growth on the main stream; the rest waits for the growth.
     const uint32_t n_mix = e->has_mix ? head[6] : 0u, n_mixw = e->has_mix ? head[7] : 0u;
     // SG_DEBUG_FLAGS & 8 (diagnostics): every decide kernel on the main stream, one after the other
     const bool serial_bins = (e->dbg_flags & 8) != 0;
     const bool pre_split = (n_mix || n_mixw) && !serial_bins;
     hipStream_t ps = pre_split ? e->bin_stream[1] : st;
-    if (pre_split) {
-        HIPCHK(hipEventRecord(e->fork0, st));
-        HIPCHK(hipStreamWaitEvent(ps, e->fork0, 0));
-    }
-    if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
-        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
-        e->pv_last_m = n_mixw;
-    }
-    const bool pv_ran = n_mixw && e->pv_on && head[72];
-    if (pv_ran)
-        HIPCHK(launch_pv_a(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec, e->d_pvseg, e->pvb,
-                           head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, ps, launch_radix_hist_n,
-                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
     HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
-    // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
-    // compaction check of a later submit
-    if (e->pool_nb) {
-        DevState Sg{};
-        std::memset(&Sg, 0, sizeof(Sg));
-        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
-        Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
-        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, e->d_pmoves,
-                              e->d_pmoves ? reinterpret_cast<uint32_t*>(e->d_pmoves + e->pmoves_cap) : nullptr,
-                              (uint32_t)e->pmoves_cap, st));
-        HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, 8, hipMemcpyDeviceToHost, st));
-    }
-    // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY
+    // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY.  First on the decide stream: the
+    // pre pass's eligibility reads the chain flags (it ran beside the grants and raced them)
     if (e->cfg.switch_on && (e->cfg.max_slot_chain_size <= 0 || e->n_chains < (uint32_t)e->cfg.max_slot_chain_size)) {
         const bool grant_all = e->cfg.max_slot_chain_size <= 0;
         HIPCHK(launch_chain(e->d_recs, vin, e->d_segs, m, e->d_info, grant_all ? 1 : 0, e->d_bsmall + 2, e->d_cand,
@@ -2335,8 +2325,39 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
             }
         }
     }
+    // XF_MIX segments of the cooperative bins (and XF_PVPQ ones): their param checks first (the value-parallel pre
+    // pass, else k_pq's), the owners then decide the flow / degrade chain on them.  The pre pass runs on
+    // bin_stream[1] (whose J4 / J1 wait for it anyway); its extraction and sort touch no map region, so they start
+    // after the chain grants, beside the maps' growth on the main stream; the rest waits for the growth.
+    if (pre_split) {
+        HIPCHK(hipEventRecord(e->fork0, st));
+        HIPCHK(hipStreamWaitEvent(ps, e->fork0, 0));
+    }
+    if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
+        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
+        e->pv_last_m = n_mixw;
+    }
+    const bool pv_ran = n_mixw && e->pv_on && head[72];
+    if (pv_ran)
+        HIPCHK(launch_pv_a(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec, e->d_pvseg, e->pvb,
+                           head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, ps, launch_radix_hist_n,
+                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
+    // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
+    // compaction check of a later submit
+    if (e->pool_nb) {
+        DevState Sg{};
+        std::memset(&Sg, 0, sizeof(Sg));
+        Sg.prog = e->d_prog; Sg.rules = e->d_rules; Sg.tmid = e->d_tmid; Sg.prio = e->d_prio;
+        Sg.pmap = e->d_pmap; Sg.pbkt = e->d_pbkt; Sg.pdat = e->d_pdat; Sg.pbm = e->d_pbm;
+        const uint32_t nm = (uint32_t)e->pmap_key.size();
+        HIPCHK(launch_pm_grow(e->d_segs, e->d_bsmall + 1, mb, Sg, e->d_pool_next, e->pool_nb, e->d_bsmall + 0, e->d_pmoves,
+                              e->d_pmoves ? reinterpret_cast<uint32_t*>(e->d_pmoves + e->pmoves_cap) : nullptr,
+                              (uint32_t)e->pmoves_cap, e->epoch, nm, e->d_pbkt2, e->d_pdat2, e->d_pcwork,
+                              e->d_pcwork + e->pmoves_cap, e->d_pcwork + 2 * e->pmoves_cap, launch_scan, st));
+        HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, PC_WORDS * 8, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(hipEventRecord(B.ev[2], st));
-    if (pre_split) {  // every map-touching pre-pass kernel after the maps grew (they move) and the chains
+    if (pre_split) {  // every map-touching pre-pass kernel after the maps grew (they move)
         HIPCHK(hipEventRecord(e->grown, st));
         HIPCHK(hipStreamWaitEvent(ps, e->grown, 0));
     }

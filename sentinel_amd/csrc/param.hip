@@ -1584,8 +1584,11 @@ __device__ void pm_move(const DevState& S, uint32_t id, PMap m, uint64_t nbase, 
 // the map before up to `adds` more keys arrive: at most half its slots used, else a region twice as large (or
 // large enough), up to map_buckets(cap)
 // mv (k_pm_grow): the move is listed for k_pm_move_list (a workgroup per map) instead of done by this lane
+// pool_next = the pool's control words (PC_*).  rescue != 0: a region the pool cannot hold yet is a request for the
+// batch's on-device compaction (PC_RESCUE = rescue, the map keeps its region for now); 0: the pool is used up
 __device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned long long* pool_next, uint64_t pool_nb,
-                        uint32_t* bflags, uint4* mv = nullptr, uint32_t* nmv = nullptr, uint32_t mcap = 0) {
+                        uint32_t* bflags, uint4* mv = nullptr, uint32_t* nmv = nullptr, uint32_t mcap = 0,
+                        uint32_t rescue = 0) {
     const PMap m = S.pmap[id];
     uint64_t need = (uint64_t)m.live + adds;
     if (need > m.cap) need = m.cap;
@@ -1594,7 +1597,11 @@ __device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned 
     uint32_t nn = want > 2 * m.nb ? want : 2 * m.nb;
     if (nn > full) nn = full;
     const uint64_t nbase = atomicAdd(pool_next, (unsigned long long)nn);
-    if (nbase + nn > pool_nb) { atomicOr(bflags, BF_POOL_FULL); return; }
+    if (nbase + nn > pool_nb) {
+        if (rescue) pool_next[PC_RESCUE] = rescue;
+        else atomicOr(bflags, BF_POOL_FULL);
+        return;
+    }
     if (mv) {
         const uint32_t k = atomicAdd(nmv, 1u);
         if (k < mcap) { mv[k] = make_uint4(id, (uint32_t)nbase, (uint32_t)(nbase >> 32), nn); return; }
@@ -1687,10 +1694,13 @@ __global__ __launch_bounds__(256) void k_pm_move_list(const uint4* __restrict__ 
 // Decide stage, before every kernel that touches the maps: the maps a segment may add keys to -- its QPS rules'
 // maps and its thread-count maps -- grown for the segment's events (an upper bound of its accesses); one lane each.
 // (Maps of STRATEGY_RELATE members, whose events sort under another resource, are grown to capacity at rule load.)
+// Two passes a batch: the first asks for the on-device compaction when the pool runs short (rescue = the batch's
+// epoch), the second runs only after one (PC_RESCUE = epoch) and finds the pool used up for real.
 __global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, const uint32_t* __restrict__ mp, DevState S,
                                                  unsigned long long* pool_next, uint64_t pool_nb, uint32_t* bflags,
-                                                 uint4* mv, uint32_t* nmv, uint32_t mcap) {
+                                                 uint4* mv, uint32_t* nmv, uint32_t mcap, uint32_t epoch, uint32_t second) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (second && pool_next[PC_RESCUE] != epoch) return;
     if (s >= *mp) return;
     const Seg sg = segs[s];
     const Prog pg = S.prog[sg.res];
@@ -1699,12 +1709,13 @@ __global__ __launch_bounds__(256) void k_pm_grow(const Seg* __restrict__ segs, c
     const uint64_t adds = (S.prio && (S.prio[sg.res] & PM_ARGL)) ? 0xFFFFFFFFull : (uint64_t)sg.len;
     for (int k = 0; k < pg.n_param; ++k) {
         const DRule& r = S.rules[pg.rule_off + k];
-        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS) pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags, mv, nmv, mcap);
+        if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS)
+            pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags, mv, nmv, mcap, second ? 0u : epoch);
     }
     if (pg.tm_base != NO_ID)
         for (int i = 0; i < SG_MAX_ARGS; ++i) {
             const uint32_t id = S.tmid[pg.tm_base + i];
-            if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags, mv, nmv, mcap);
+            if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags, mv, nmv, mcap, second ? 0u : epoch);
         }
 }
 // listed maps to full size (rule load: STRATEGY_RELATE members)
@@ -1715,8 +1726,13 @@ __global__ void k_pm_grow_ids(const uint32_t* __restrict__ ids, uint32_t n, DevS
 }
 
 // ---- pool compaction on the device: every map's region, back to back in map order, into the other pool (the
-// regions maps grew out of are dropped); the rings stay where they are
-__global__ void k_pc_nb(const PMap* __restrict__ pm, uint32_t n, uint32_t* __restrict__ sz) {
+// regions maps grew out of are dropped); the rings stay where they are.  Between batches (engine.cpp compact_pmaps,
+// ctl = null) the pools then swap; inside a batch whose growth found the pool short (ctl[PC_RESCUE] = epoch: every
+// kernel of the chain returns at once otherwise) the compacted prefix is copied back (k_pc_back), so the kernels
+// already queued with this pool's address see the maps in place.
+__global__ void k_pc_nb(const PMap* __restrict__ pm, uint32_t n, uint32_t* __restrict__ sz,
+                        const unsigned long long* __restrict__ ctl, uint32_t epoch) {
+    if (ctl && ctl[PC_RESCUE] != epoch) return;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) sz[i] = pm[i].nb;
 }
@@ -1724,7 +1740,9 @@ __global__ void k_pc_nb(const PMap* __restrict__ pm, uint32_t n, uint32_t* __res
 __global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t n, const uint32_t* __restrict__ off,
                                                  const PBucket* __restrict__ ob, const PData* __restrict__ od,
                                                  PBucket* __restrict__ nbk, PData* __restrict__ nd,
-                                                 unsigned long long* __restrict__ pool_next) {
+                                                 unsigned long long* __restrict__ pool_next, uint32_t cond,
+                                                 uint32_t epoch) {
+    if (cond && pool_next[PC_RESCUE] != epoch) return;
     const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
     if (i >= n) return;
     const PMap m = pm[i];
@@ -1737,23 +1755,59 @@ __global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t
     for (uint32_t w = l; w < m.nb * PM_BKT; w += 64) dd[w] = sd[w];  // (PData: 16 B)
     if (l == 0) {
         pm[i].base = nb;
-        if (i == n - 1) *pool_next = nb + m.nb;
+        if (i == n - 1) {
+            pool_next[PC_NEXT] = nb + m.nb;
+            pool_next[PC_FLOOR] = nb + m.nb;
+        }
     }
+}
+// the rescue's copy back: the compacted prefix [0, ctl[PC_NEXT]) of the other pool over this one
+__global__ __launch_bounds__(256) void k_pc_back(PBucket* __restrict__ b1, PData* __restrict__ d1,
+                                                 const PBucket* __restrict__ b2, const PData* __restrict__ d2,
+                                                 unsigned long long* __restrict__ ctl, uint32_t epoch) {
+    if (ctl[PC_RESCUE] != epoch) return;
+    const uint64_t nb = ctl[PC_NEXT];
+    const uint64_t nw = nb * 8, stride = (uint64_t)gridDim.x * blockDim.x;  // (PBucket: 8 x 16 B; PData: 16 B a slot)
+    const uint4* sb = reinterpret_cast<const uint4*>(b2);
+    uint4* db = reinterpret_cast<uint4*>(b1);
+    const uint4* sd = reinterpret_cast<const uint4*>(d2);
+    uint4* dd = reinterpret_cast<uint4*>(d1);
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        db[w] = sb[w];
+        dd[w] = sd[w];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctl[PC_RESCUES] += 1;
 }
 
 namespace sg {
 // mv / nmv / mcap: the move list (null: each lane moves its maps itself)
+// The batch's map growth (pool_next = the pool's control words): a first pass; then, only if that pass found the pool
+// short, the compaction into the other pool (b2 / d2), its copy back and a second pass (every kernel of the rescue
+// returns at once otherwise: no host round trip in the decide stage).  nm maps; sz / off / part: compaction scratch.
 hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, const DevState& S, unsigned long long* pool_next,
-                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, hipStream_t st) {
+                          uint64_t pool_nb, uint32_t* bflags, uint4* mv, uint32_t* nmv, uint32_t mcap, uint32_t epoch,
+                          uint32_t nm, PBucket* b2, PData* d2, uint32_t* sz, uint32_t* off, uint32_t* part,
+                          hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                          hipStream_t st) {
     if (!mb) return hipSuccess;
     if (!mcap) mv = nullptr;
-    if (mv) {
-        const hipError_t e = hipMemsetAsync(nmv, 0, 4, st);
+    for (uint32_t second = 0; second < 2; ++second) {
+        if (mv) {
+            const hipError_t e = hipMemsetAsync(nmv, 0, 4, st);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags,
+                           mv, nmv, mcap, epoch, second);
+        if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 16384 ? (mcap + 3) / 4 : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
+        if (second || !nm || !b2) break;
+        hipLaunchKernelGGL(k_pc_nb, dim3((nm + 255) / 256), dim3(256), 0, st, S.pmap, nm, sz,
+                           (const unsigned long long*)pool_next, epoch);
+        const hipError_t e = scan(sz, off, nm, part, nullptr, st);
         if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_pc_copy, dim3((nm + 3) / 4), dim3(256), 0, st, S.pmap, nm, off, S.pbkt, S.pdat, b2, d2,
+                           pool_next, 1u, epoch);
+        hipLaunchKernelGGL(k_pc_back, dim3(2048), dim3(256), 0, st, S.pbkt, S.pdat, b2, d2, pool_next, epoch);
     }
-    hipLaunchKernelGGL(k_pm_grow, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, S, pool_next, pool_nb, bflags,
-                       mv, nmv, mcap);
-    if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 16384 ? (mcap + 3) / 4 : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
     return hipGetLastError();
 }
 // sz / off: n words each; part: scan partials
@@ -1762,10 +1816,10 @@ hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PDat
                              hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                              hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pc_nb, dim3((n + 255) / 256), dim3(256), 0, st, pm, n, sz);
+    hipLaunchKernelGGL(k_pc_nb, dim3((n + 255) / 256), dim3(256), 0, st, pm, n, sz, (const unsigned long long*)nullptr, 0u);
     const hipError_t e = scan(sz, off, n, part, nullptr, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pc_copy, dim3((n + 3) / 4), dim3(256), 0, st, pm, n, off, ob, od, nbk, nd, pool_next);
+    hipLaunchKernelGGL(k_pc_copy, dim3((n + 3) / 4), dim3(256), 0, st, pm, n, off, ob, od, nbk, nd, pool_next, 0u, 0u);
     return hipGetLastError();
 }
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,

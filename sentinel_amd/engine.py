@@ -246,15 +246,16 @@ class Engine:
                 "walk_max": int(out[6])}
 
     def param_pool(self) -> dict:
-        """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last layout,
-        compactions."""
+        """The param map bucket pool (diagnostics export sgx_param_pool): size, taken, taken at the last compaction,
+        compactions between batches, compactions a batch ran on the device when its growth found the pool short."""
         fn = lib().sgx_param_pool
         fn.restype = C.c_int
         fn.argtypes = [C.c_void_p, C.c_void_p]
-        out = np.zeros(4, dtype=np.uint64)
+        out = np.zeros(5, dtype=np.uint64)
         if fn(self.h, out.ctypes.data) != 0:
             raise SentinelError(A.SG_EDEVICE, "sgx_param_pool failed")
-        return {"buckets": int(out[0]), "taken": int(out[1]), "floor": int(out[2]), "compactions": int(out[3])}
+        return {"buckets": int(out[0]), "taken": int(out[1]), "floor": int(out[2]), "compactions": int(out[3]),
+                "device_compactions": int(out[4])}
 
     def param_thread_count(self, res: int, idx: int, key: int, with_presence: bool = False):
         """ParameterMetric.getThreadCount (sg_param_thread_count): the value's count in the thread-count map of

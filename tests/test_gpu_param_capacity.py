@@ -100,6 +100,32 @@ def test_pool_used_up_fails_the_batch_and_the_engine():
         eng.submit(_entries(rid, [_long(1)], t=T0 + 20))
 
 
+def test_batch_that_finds_the_pool_short_compacts_on_the_device():
+    # the between-batch compaction runs at half of the free space on counts a batch or two old, so one
+    # batch can still find the pool short.  It then compacts on the device and grows again (param.hip
+    # launch_pm_grow).  2^12 slots = 512 buckets: batch 1 grows a's two maps to 25 buckets each, batch 2 to 75
+    # (54 buckets grown out of, under the host's trigger), batch 3 asks 2 x 175 with 304 free -- short; the live
+    # regions compacted (154 buckets) leave room.  Every decision against the oracle, then a's maps still hold
+    # their keys (thread counts read back).
+    eng = E.Engine(max_resources=64, max_slot_chain_size=0, param_table_log2=12)
+    orc = O.Oracle(max_slot_chain_size=0)
+    for n in ("a", "b"):
+        assert eng.register(n) == orc.register(n)
+    rules = [A.param_rule("a", 0, 50), A.param_rule("b", 0, 50)]
+    assert eng.load_param_rules(rules) == 2 and orc.load_param_rules(rules) == 2
+    v0 = 0
+    for b, n in enumerate((100, 200, 400)):
+        ev = _entries(0, [_long(v) for v in range(v0, v0 + n)], t=T0 + 100 * b)
+        v0 += n
+        dg, do = eng.submit(ev), orc.submit(ev)
+        np.testing.assert_array_equal(dg, do, err_msg="batch %d" % b)
+    pool = eng.param_pool()
+    assert pool["device_compactions"] == 1 and pool["compactions"] == 0, pool
+    assert pool["taken"] <= pool["buckets"], pool
+    for v in (0, 99, 100, 350, 699):
+        assert eng.param_thread_count(0, 0, _long(v)) == orc.param_thread_count(0, 0, _long(v)) == 1, v
+
+
 def test_regions_grow_and_the_pool_compacts():
     # 300 resources, each map growing over 12 batches from 2 buckets towards full size, in a pool a little larger
     # than the final regions: the regions grown out of fill it and are dropped by relayouts between batches

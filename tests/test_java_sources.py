@@ -169,6 +169,28 @@ def test_init_failure_refuses_entries_instead_of_throwing():
     assert "GpuChainInit.fail(" in body and body.count("throw new GpuUnavailableException") == 2
 
 
+def test_runtime_engine_failure_fails_closed():
+    # once the engine dies at run time (a batch failed: e->fatal, BF_POOL_FULL, a poisoned
+    # batcher) GpuEngine.decide throws a RuntimeException; CtSph.entryWithPriority catches anything that is not a
+    # BlockException and lets the entry pass unchecked (core/CtSph.java:163-166).  The slot must record the failure
+    # (every later entry refused by the poison check) and throw GpuUnavailableException (a BlockException)
+    ref = "/root/reference/sentinel-core/src/main/java/com/alibaba/csp/sentinel/CtSph.java"
+    if os.path.exists(ref):
+        txt = open(ref).read()
+        assert "catch (BlockException e1)" in txt and "catch (Throwable e1)" in txt
+    slot = _code(open(os.path.join(JAVA, "GpuDecisionSlot.java")).read())
+    body = slot[slot.index("public void entry("):slot.index("public void exit(")]
+    m = re.search(r"try\s*\{\s*d = eng\.decide\(op\);\s*\}\s*catch \(RuntimeException (\w+)\)\s*\{(.*?)\}", body, re.S)
+    assert m, "eng.decide is not guarded"
+    handler = m.group(2)
+    assert "GpuChainInit.fail(" in handler and "throw new GpuUnavailableException(GpuChainInit.failure())" in handler
+    assert body.count("eng.decide(") == 1
+    # GpuEngine.decide reports a dead engine with a RuntimeException (not an Error the guard would miss)
+    eng = _code(open(os.path.join(JAVA, "GpuEngine.java")).read())
+    dec = eng[eng.index("int decide(Op op)"):]
+    assert "throw new IllegalStateException" in dec[:dec.index("\n    }")]
+
+
 def test_java_sources_are_balanced():
     for root, _, files in os.walk(os.path.join(ROOT, "java", "src")):
         for f in files:

@@ -45,6 +45,38 @@ def test_launch_failing_rank_stops_the_others():
     assert time.time() - t < 30
 
 
+def test_launch_escalates_to_sigkill():
+    # a rank that ignores SIGTERM (stuck in a collective) is killed after the grace period
+    code = ("import os, signal, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\n"
+            "signal.signal(signal.SIGTERM, signal.SIG_IGN)\ntime.sleep(120)")
+    import time
+    t = time.time()
+    rc = L.launch_ranks(2, [sys.executable, "-c", code], poll_s=0.05, grace_s=1.0)
+    assert rc == 3
+    assert time.time() - t < 30
+
+
+def test_launch_parent_interrupt_stops_ranks(monkeypatch):
+    # an exception in the parent (Ctrl-C) stops every rank before it propagates: no orphan keeps a GPU
+    started = []
+    real = L.subprocess.Popen
+
+    def popen(*a, **k):
+        p = real(*a, **k)
+        started.append(p)
+        return p
+
+    def boom(_):
+        raise KeyboardInterrupt
+
+    import types
+    monkeypatch.setattr(L.subprocess, "Popen", popen)
+    monkeypatch.setattr(L, "time", types.SimpleNamespace(sleep=boom, monotonic=L.time.monotonic))
+    with pytest.raises(KeyboardInterrupt):
+        L.launch_ranks(2, [sys.executable, "-c", "import time; time.sleep(120)"], grace_s=2.0)
+    assert len(started) == 2 and all(p.poll() is not None for p in started)
+
+
 def test_launch_ranks_rendezvous_gloo():
     # the environment is enough for torch.distributed's env:// rendezvous (what bench.py's ranks do)
     code = ("import torch, torch.distributed as d; d.init_process_group('gloo'); t = torch.ones(1); "
