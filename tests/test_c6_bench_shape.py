@@ -6,11 +6,10 @@ two-stage pipeline, param_table_log2 = 29, max_rules = 1 << 22.  At that size th
 run reaches all run: the value-parallel pre / post passes over multi-million-event head segments
 (pvalue.hip), the k_lite<true> lanes of ~700k cold resources, param maps growing inside the 2^29-slot pool and
 the pool's device compaction between batches (engine.cpp compact_pmaps).  This test replays the first two
-global batches of that exact trace plus a time-shifted copy of the first one (built on the device as bench.py
-builds its fresh batches), then a second shifted copy, through the engine and through the resource-partitioned
-oracle, and compares every decision, the node windows of the 50 hottest and 300 random resources and
-ParameterMetric.getThreadCount of the hot resources' values.  A pool with a lower compaction point
-(SG_POOL_COMPACT_FRAC) makes sure at least one compaction happens inside the run.
+global batches of that exact trace, then time-shifted copies of them (built on the device as bench.py builds its
+fresh batches) until the param map pool has been compacted at least once, through the engine and through the
+resource-partitioned oracle, and compares every decision, the node windows of the 50 hottest and 300 random
+resources and ParameterMetric.getThreadCount of the hot resources' values.
 
 Reference: param/slots/HotParamSlotChainBuilder.java:38-51 (slot order), param/slots/block/flow/param/
 ParameterMetric.java:37-39 (map capacities), ParamFlowChecker.java:121-196 (passDefaultLocalCheck).
@@ -44,37 +43,47 @@ def test_c6_bench_shape():
     dev = torch.device("cuda", 0)
     base = torch.from_numpy(np.ascontiguousarray(ev).view(np.uint8).copy()).to(dev)
     base64 = base.view(torch.int64).view(-1, 3)
-    copies = [torch.empty((GB, 3), dtype=torch.int64, device=dev) for _ in range(2)]
-    host = []
-    for k, (c, (a, e)) in enumerate(zip(copies, ((0, GB), (GB, 2 * GB)))):
-        bench.shifted_batch(base64, a, e, 1, tspan, n_base, c)
-        h = ev[a:e].copy()
-        h["ts"] += tspan
+
+    def shifted(k, b):
+        """Copy k of base batch b: on the device as bench.py builds it, on the host for the oracle."""
+        c = torch.empty((GB, 3), dtype=torch.int64, device=dev)
+        bench.shifted_batch(base64, b * GB, (b + 1) * GB, k, tspan, n_base, c)
+        h = ev[b * GB:(b + 1) * GB].copy()
+        h["ts"] += k * tspan
         isref = (h["kind"] != A.EV_ENTRY) & ((h["aux"] & np.uint64(A.REF_NONE)) != np.uint64(A.REF_NONE))
-        h["aux"] = np.where(isref, h["aux"] + np.uint64(n_base), h["aux"])
-        assert np.array_equal(c.cpu().numpy().view(np.uint8).reshape(-1), h.view(np.uint8)), k
-        host.append(h)
+        h["aux"] = np.where(isref, h["aux"] + np.uint64(k * n_base), h["aux"])
+        assert np.array_equal(c.cpu().numpy().view(np.uint8).reshape(-1), h.view(np.uint8)), (k, b)
+        return c, h
 
     eng = E.Engine(device=0, max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0, max_batch_events=GB,
                    aux_node_capacity=1 << 20, **kw)
     w.install(eng)
-    outs = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(4)]
-    ptrs = [base.data_ptr(), base.data_ptr() + GB * 24, copies[0].data_ptr(), copies[1].data_ptr()]
-    pv = []
-    for p, o in zip(ptrs, outs):  # back to back through the pipeline, as bench.py submits
-        eng.submit_ptr(p, GB, o.data_ptr(), sync=False)
-    eng.sync()
-    pool = eng.param_pool()
-    pv.append(eng.pv_last())
-    dg = np.concatenate([o.cpu().numpy().view(np.uint32) for o in outs])
-
     threads = min(16, len(os.sched_getaffinity(0)))
     po = O.PartitionedOracle(w, threads, max_slot_chain_size=0)
-    do = np.concatenate([po.submit(ev[:GB]), po.submit(ev[GB:]), po.submit(host[0]), po.submit(host[1])])
-    allev = np.concatenate([ev, host[0], host[1]])
+    # global batches in pairs, each pair back to back through the pipeline as bench.py submits: the two base batches,
+    # then time-shifted copies of them (fresh to the engine: windows roll, breakers trip and reset, the maps keep
+    # growing) until the pool has been compacted at least once (at most 4 pairs)
+    dg, do, allev, pv, pool = [], [], [], None, None
+    out = [torch.empty(GB, dtype=torch.int32, device=dev) for _ in range(2)]
+    for k in range(4):
+        pair = [(base[b * GB * 24:], ev[b * GB:(b + 1) * GB]) for b in range(2)] if k == 0 else \
+               [shifted(k, b) for b in range(2)]
+        for (d, _), o in zip(pair, out):
+            eng.submit_ptr(d.data_ptr(), GB, o.data_ptr(), sync=False)
+        eng.sync()
+        if k == 0:
+            pv = eng.pv_last()
+        dg += [o.cpu().numpy().view(np.uint32).copy() for o in out]
+        do += [po.submit(h) for _, h in pair]
+        allev += [h for _, h in pair]
+        pool = eng.param_pool()
+        if pool["compactions"] + pool["device_compactions"] >= 1:
+            break
+    dg, do, allev = np.concatenate(dg), np.concatenate(do), np.concatenate(allev)
     bad = np.nonzero(dg != do)[0]
     assert len(bad) == 0, "decision mismatch at event %d (%s): gpu=%08x oracle=%08x; %d mismatches" % (
         bad[0], allev[bad[0]], dg[bad[0]], do[bad[0]], len(bad))
+    print("C6 bench shape: %d global batches, pool %s, pv %s" % (len(allev) // GB, pool, pv))
 
     cnt = np.bincount(ev["res_id"], minlength=w.n_res)
     rng = np.random.default_rng(7)
@@ -103,7 +112,7 @@ def test_c6_bench_shape():
     st = dg[allev["kind"] == A.EV_ENTRY] & 0xFF
     for s in (A.BLOCK_PARAM, A.BLOCK_FLOW, A.BLOCK_DEGRADE, A.PASS):
         assert (st == s).sum() > 0, s
-    assert pv[0]["segments"] > 0 and pv[0]["accesses"] > 1_000_000, pv
-    assert pool["compactions"] + pool["device_compactions"] >= 1, pool
+    assert pv["segments"] > 0 and pv["accesses"] > 1_000_000, pv
+    assert pool["compactions"] + pool["device_compactions"] >= 1, str(pool)
     po.close()
     eng.close()
