@@ -55,11 +55,12 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 #define J8_MAX (1u << 23)  // longest segment of a QPS-DefaultController program on the 512-lane owner
 #define SEG_ITEMS 16
 #define SEG_TILE (256 * SEG_ITEMS)
+// (keys[lo, n) only: lo = the hot / cold group stage's cold region, whose first key starts a segment)
 __device__ __forceinline__ uint32_t seg_flags16(const uint32_t* __restrict__ keys, uint64_t n, uint64_t i0,
-                                                uint32_t* kout) {
+                                                uint32_t* kout, uint64_t lo = 0) {
     uint32_t f = 0;
-    if (i0 >= n) return 0;
-    uint32_t prev = i0 == 0 ? 0xFFFFFFFFu : keys[i0 - 1];
+    if (i0 >= n || i0 + SEG_ITEMS <= lo) return 0;
+    uint32_t prev = i0 <= lo ? 0xFFFFFFFFu : keys[i0 - 1];
     if (i0 + SEG_ITEMS <= n) {
         const uint4* v = reinterpret_cast<const uint4*>(keys + i0);
 #pragma unroll
@@ -73,10 +74,10 @@ __device__ __forceinline__ uint32_t seg_flags16(const uint32_t* __restrict__ key
     }
 #pragma unroll
     for (int j = 0; j < SEG_ITEMS; ++j) {
-        const bool valid = i0 + j < n;
-        const bool st = valid && (i0 + j == 0 || kout[j] != prev);
+        const bool valid = i0 + j < n && i0 + j >= lo;
+        const bool st = valid && (i0 + j == lo || kout[j] != prev);
         f |= (st ? 1u : 0u) << j;
-        prev = kout[j];
+        prev = valid ? kout[j] : 0xFFFFFFFFu;
     }
     return f;
 }
@@ -97,21 +98,32 @@ __device__ __forceinline__ uint32_t seg_block_excl_scan(uint32_t v, uint32_t* to
     *total = tot;
     return pre + x - v;
 }
-__global__ __launch_bounds__(256) void k_seg_count(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ cnt) {
+// lo (optional, on the device): the first position of the keys (the cold region); sbase (optional): segments written
+// from segs[*sbase] on (after the hot ones)
+__global__ __launch_bounds__(256) void k_seg_count(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ cnt,
+                                                   const uint32_t* __restrict__ lo) {
+    const uint64_t b = lo ? *lo : 0u;
+    if ((uint64_t)(blockIdx.x + 1) * SEG_TILE <= b) {  // a tile wholly before the region
+        if (threadIdx.x == 0) cnt[blockIdx.x] = 0;
+        return;
+    }
     uint32_t kk[SEG_ITEMS];
     const uint64_t i0 = (uint64_t)blockIdx.x * SEG_TILE + (uint64_t)threadIdx.x * SEG_ITEMS;
-    const uint32_t f = seg_flags16(keys, n, i0, kk);
+    const uint32_t f = seg_flags16(keys, n, i0, kk, b);
     uint32_t tot;
     (void)seg_block_excl_scan((uint32_t)__popc(f), &tot);
     if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
 }
 __global__ __launch_bounds__(256) void k_seg_emit(const uint32_t* __restrict__ keys, uint64_t n,
-                                                  const uint32_t* __restrict__ off, Seg* __restrict__ segs) {
+                                                  const uint32_t* __restrict__ off, Seg* __restrict__ segs,
+                                                  const uint32_t* __restrict__ lo, const uint32_t* __restrict__ sbase) {
+    const uint64_t b = lo ? *lo : 0u;
+    if ((uint64_t)(blockIdx.x + 1) * SEG_TILE <= b) return;
     uint32_t kk[SEG_ITEMS];
     const uint64_t i0 = (uint64_t)blockIdx.x * SEG_TILE + (uint64_t)threadIdx.x * SEG_ITEMS;
-    uint32_t f = seg_flags16(keys, n, i0, kk);
+    uint32_t f = seg_flags16(keys, n, i0, kk, b);
     uint32_t tot;
-    uint32_t pos = off[blockIdx.x] + seg_block_excl_scan((uint32_t)__popc(f), &tot);
+    uint32_t pos = (sbase ? *sbase : 0u) + off[blockIdx.x] + seg_block_excl_scan((uint32_t)__popc(f), &tot);
 #pragma unroll
     for (int j = 0; j < SEG_ITEMS; ++j) {
         if ((f >> j) & 1u) {
@@ -295,6 +307,7 @@ __global__ __launch_bounds__(256) void k_scatter_rec(const SEv* __restrict__ rec
 // EXIT (or TRACE) named the same ENTRY (BF_MULTI_LINK: frozen-stretch skipping is off for the batch).
 // A reference must also name an ENTRY of its own resource: the two carry the same sort key (inside a
 // STRATEGY_RELATE component the key is the component's).
+// skeys (optional: the radix group stage; the hot / cold one checks the resource in k_grp_records)
 __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, const uint32_t* __restrict__ skeys,
                                                     uint64_t n, uint32_t* __restrict__ bst, Link* __restrict__ link,
                                                     uint32_t epoch, uint32_t* __restrict__ bflags) {
@@ -315,7 +328,7 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
                     r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
                 const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
                 if ((uint32_t)(old >> 32) == epoch) multi = true;
-                if (skeys[r.x] != skeys[p]) bad = true;
+                if (skeys && skeys[r.x] != skeys[p]) bad = true;
             }
         }
     }
@@ -3314,10 +3327,35 @@ hipError_t launch_seg(const uint32_t* keys, uint64_t n, uint32_t* flag, uint32_t
                       uint32_t* part, uint32_t* nseg) {
     // flag/pos are scratch of >= n words: tile counts in flag, their offsets in pos
     const uint32_t nt = (uint32_t)((n + SEG_TILE - 1) / SEG_TILE);
-    hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag);
+    hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag, (const uint32_t*)nullptr);
     hipError_t e = scan(flag, pos, nt, part, nseg, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs);
+    hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+__global__ void k_add2(uint32_t* __restrict__ dst, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
+    if (threadIdx.x == 0) *dst = *a + *b;
+}
+// the cold segments of the hot / cold group stage: keys[*lo, n), written after the *sbase hot ones; nseg = both.
+// flag / pos: scratch of >= n / SEG_TILE + 1 words each; ccount: one device word
+hipError_t launch_seg_cold(const uint32_t* keys, uint64_t n, const uint32_t* lo, const uint32_t* sbase, uint32_t* flag,
+                           uint32_t* pos, Seg* segs, hipStream_t st,
+                           hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                           uint32_t* part, uint32_t* ccount, uint32_t* nseg) {
+    const uint32_t nt = (uint32_t)((n + SEG_TILE - 1) / SEG_TILE);
+    hipLaunchKernelGGL(k_seg_count, dim3(nt), dim3(256), 0, st, keys, n, flag, lo);
+    hipError_t e = scan(flag, pos, nt, part, ccount, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_emit, dim3(nt), dim3(256), 0, st, keys, n, pos, segs, lo, sbase);
+    hipLaunchKernelGGL(k_add2, dim3(1), dim3(64), 0, st, nseg, sbase, ccount);
+    return hipGetLastError();
+}
+// the sorted-order side tables (bst sums, forward links) of the hot / cold group stage (its records are in place)
+hipError_t launch_block_sums(const SEv* recs, uint64_t n, uint32_t* bst, Link* link, uint32_t epoch, uint32_t* bflags,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs,
+                       (const uint32_t*)nullptr, n, bst, link, epoch, bflags);
     return hipGetLastError();
 }
 // mp: the segment count on the device; mb: an upper bound of it (the grid)

@@ -37,6 +37,32 @@ hipError_t launch_radix_hist_n(const uint32_t* keys, uint64_t n, const uint32_t*
                                uint32_t nblocks, hipStream_t st);
 hipError_t launch_radix_scatter_n(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev, int shift,
                                   const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st);
+hipError_t launch_radix_scatter_x(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev,
+                                  const uint32_t* tcnt, const uint32_t* dbase, int shift, const uint32_t* goff,
+                                  uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
+hipError_t launch_grp_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
+                            uint32_t* bflags, int64_t* t0_out, uint32_t* prio, uint64_t* key_ring, const uint32_t* comp,
+                            const sg_event_ext* ext, const sg_arg* args, uint64_t n_args, uint32_t max_ctx,
+                            const uint16_t* hot_tab, uint32_t nhot, uint32_t nblocks, uint32_t* words,
+                            uint32_t* hot_hist, uint32_t* ckeys, uint32_t* cvals, uint32_t* ccnt, uint32_t* chist,
+                            hipStream_t st);
+hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
+                              int32_t max_rt, const uint32_t* words, const uint32_t* hot_off, uint32_t nblocks,
+                              uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev, uint32_t* nprev,
+                              uint32_t* bst, uint32_t* bflags, const uint32_t* comp, const sg_event_ext* ext,
+                              const sg_arg* args, uint32_t max_ctx, hipStream_t st);
+hipError_t launch_hot_segs(const uint32_t* hot_off, uint32_t nhot, uint32_t nblocks, const uint32_t* hot_total,
+                           const uint32_t* hot_list, Seg* segs, uint32_t* out, hipStream_t st);
+hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
+                            uint32_t* hot_list, uint32_t nhot_old, uint32_t* hot_n, hipStream_t st);
+hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, hipStream_t st);
+uint32_t hot_max();
+hipError_t launch_seg_cold(const uint32_t* keys, uint64_t n, const uint32_t* lo, const uint32_t* sbase, uint32_t* flag,
+                           uint32_t* pos, Seg* segs, hipStream_t st,
+                           hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                           uint32_t* part, uint32_t* ccount, uint32_t* nseg);
+hipError_t launch_block_sums(const SEv* recs, uint64_t n, uint32_t* bst, Link* link, uint32_t epoch, uint32_t* bflags,
+                             hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
 uint32_t radix_tile();
@@ -522,6 +548,7 @@ struct sg_engine {
         uint32_t *d_hist = nullptr, *d_part = nullptr, *d_flag = nullptr, *d_pos = nullptr, *d_order = nullptr;
         uint32_t *d_posof = nullptr, *d_dec = nullptr, *d_blkcnt = nullptr, *d_prev = nullptr;
         SEv *d_recs = nullptr, *d_rec_o = nullptr;
+        uint32_t* d_ccnt = nullptr;    // hot / cold group stage: per-tile cold counts, the cold segments' tile scratch
         Seg* d_segs = nullptr;
         uint64_t* d_cand = nullptr;
         uint32_t* d_bsmall = nullptr;  // [0] bflags [1] nseg [2] ncand [3] nprev [4..5] t0 [8..8+N_BINS] bin offsets
@@ -547,6 +574,12 @@ struct sg_engine {
     std::vector<std::array<double, 4>> tlog;  // per batch [group, decide, post, total] ms, by collect()
     std::string fatal;           // non-empty: a batch left device state inconsistent; every later submit fails
     uint32_t* d_prio = nullptr;  // [res] sticky PM_* marks (DevState.prio)
+    // hot / cold group stage (kernels.hip k_grp_*): [sort key] -> hot id of the next batch (0xFFFF: cold), the ids'
+    // keys, and how many (the host learns it with the batch's head)
+    uint16_t* d_hot_tab = nullptr;
+    uint32_t* d_hot_list = nullptr;
+    uint32_t nhot = 0;
+    bool radix_group = false;    // SG_DEBUG_FLAGS & 8192: the all-radix group stage (A/B)
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
     AuxNode* d_auxtab = nullptr;
     uint32_t* d_auxcnt = nullptr;
@@ -666,7 +699,8 @@ static void free_slot(sg_engine::BatchSlot& B) {
     dfree(B.d_ev); dfree(B.d_out); dfree(B.d_k0); dfree(B.d_v0); dfree(B.d_k1); dfree(B.d_v1);
     dfree(B.d_hist); dfree(B.d_part); dfree(B.d_flag); dfree(B.d_pos); dfree(B.d_order); dfree(B.d_segs);
     dfree(B.d_cand); dfree(B.d_posof); dfree(B.d_dec); dfree(B.d_recs); dfree(B.d_rec_o); dfree(B.d_blkcnt);
-    dfree(B.d_prev); dfree(B.d_bsmall);
+    dfree(B.d_prev); dfree(B.d_bsmall); dfree(B.d_ccnt);
+    B.d_ccnt = nullptr;
     dfree(B.d_link); dfree(B.d_bst); dfree(B.d_pend); dfree(B.d_spans); dfree(B.d_ext); dfree(B.d_args);
     dfree(B.d_ashort); dfree(B.d_apiece); dfree(B.d_amulti); dfree(B.d_along); dfree(B.d_mix);
     B.d_mix = nullptr;
@@ -701,7 +735,8 @@ int ensure_batch(sg_engine* e, uint64_t n) {
         HIPCHK(hipMalloc(&B.d_posof, c * 4));
         HIPCHK(hipMalloc(&B.d_dec, c * 4));
         HIPCHK(hipMalloc(&B.d_recs, c * sizeof(SEv)));
-        HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));
+        if (e->radix_group) HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));  // (the hot / cold stage has none)
+        HIPCHK(hipMalloc(&B.d_ccnt, 3 * (nblocks + 64) * 4));
         HIPCHK(hipMalloc(&B.d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));
         HIPCHK(hipMalloc(&B.d_prev, c * 4));
         HIPCHK(hipMalloc(&B.d_bsmall, 256 * 4));
@@ -1180,7 +1215,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         hipMalloc(&e->d_info, R * sizeof(NodeInfo)) != hipSuccess || hipMalloc(&e->d_prog, R * sizeof(Prog)) != hipSuccess ||
         hipMalloc(&e->d_ring, 1ull << cfg.status_ring_log2) != hipSuccess || hipMalloc(&e->d_small, 256 * 4) != hipSuccess ||
         hipMalloc(&e->d_sink, 1024 * 4) != hipSuccess || hipMalloc(&e->d_borrow, R * 4 * sizeof(int64_t)) != hipSuccess ||
-        hipMalloc(&e->d_prio, R * 4) != hipSuccess)
+        hipMalloc(&e->d_prio, R * 4) != hipSuccess || hipMalloc(&e->d_hot_tab, R * 2) != hipSuccess ||
+        hipMalloc(&e->d_hot_list, hot_max() * 4) != hipSuccess)
         return bad(fail(SG_ENOMEM, "device allocation of the engine state failed"));
     {   // origin / context node table (open addressing, load <= 2/3 at capacity, power of two)
         const uint64_t cap = std::max<uint32_t>(cfg.aux_node_capacity, 16u);
@@ -1196,6 +1232,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (hipMemsetAsync(e->d_prog, 0, R * sizeof(Prog), e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_ring, 0xFF, 1ull << cfg.status_ring_log2, e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_prio, 0, R * 4, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_hot_tab, 0xFF, R * 2, e->stream) != hipSuccess ||
         launch_init_state(e->d_sec, e->d_minb, e->d_info, e->d_borrow, (uint32_t)R, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
         return bad(fail(SG_EDEVICE, "device initialisation failed"));
@@ -1211,6 +1248,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
         if (d[0] == '1' && hipMalloc(&e->d_dbg, 64 * 8) == hipSuccess) (void)hipMemset(e->d_dbg, 0, 64 * 8);
     }
     if (const char* f = std::getenv("SG_DEBUG_FLAGS")) e->dbg_flags = (uint32_t)std::strtoul(f, nullptr, 0);
+    e->radix_group = (e->dbg_flags & 8192) != 0;
     if (const char* f = std::getenv("SG_PROF_BIN")) e->prof_bin = std::atoi(f);  // SG_DEBUG counters of J16/J4/J1
     // decide-bin thresholds (segment lengths); tuning knobs, the defaults are the measured best
     if (const char* v = std::getenv("SG_LANE_MAX")) { e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
@@ -1342,7 +1380,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot); dfree(e->d_pvrest);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
-    dfree(e->d_prio); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
+    dfree(e->d_prio); dfree(e->d_hot_tab); dfree(e->d_hot_list); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
     dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
@@ -2173,23 +2211,56 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     uint32_t nblocks = (uint32_t)((n + radix_tile() - 1) / radix_tile());
     HIPCHK(hipMemsetAsync(e->d_bsmall, 0, 256 * 4, gs));
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
-    HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o, e->d_k1,
-                           e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring, e->d_comp, dev_ext,
-                           dev_args, n_args, SG_MAX_CONTEXTS, gs));
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
-    for (int p = 0; p < passes; ++p) {
-        if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * db, e->d_hist, nblocks, gs));
-        HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks << db, e->d_part, nullptr, gs));
-        HIPCHK(launch_radix_scatter(kin, vin, n, p * db, e->d_hist, nblocks, kout, vout,
-                                    p == passes - 1 ? e->d_posof : nullptr, gs));
-        std::swap(kin, kout);
-        std::swap(vin, vout);
-    }
-    // ---- 2. segments + 16-byte sorted records
-    HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, gs, launch_scan, e->d_part, e->d_bsmall + 1));
     if (++e->epoch == 0) e->epoch = 1;
-    HIPCHK(launch_gather(e->d_rec_o, vin, kin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link, e->d_bst,
-                         e->epoch, e->d_bsmall + 0, gs));
+    if (e->radix_group) {  // every event through the radix passes (SG_DEBUG_FLAGS & 8192; A/B of the group stage)
+        HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o,
+                               e->d_k1, e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,
+                               e->d_comp, dev_ext, dev_args, n_args, SG_MAX_CONTEXTS, gs));
+        for (int p = 0; p < passes; ++p) {
+            if (p > 0) HIPCHK(launch_radix_hist(kin, n, p * db, e->d_hist, nblocks, gs));
+            HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks << db, e->d_part, nullptr, gs));
+            HIPCHK(launch_radix_scatter(kin, vin, n, p * db, e->d_hist, nblocks, kout, vout,
+                                        p == passes - 1 ? e->d_posof : nullptr, gs));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        HIPCHK(launch_seg(kin, n, e->d_flag, e->d_pos, e->d_segs, gs, launch_scan, e->d_part, e->d_bsmall + 1));
+        HIPCHK(launch_gather(e->d_rec_o, vin, kin, n, e->d_posof, e->d_recs, e->d_prev, e->d_bsmall + 3, e->d_link,
+                             e->d_bst, e->epoch, e->d_bsmall + 0, gs));
+    } else {
+        // ---- hot / cold group stage (kernels.hip k_grp_*): [77] hot_total (the cold region's start), [78] cold
+        // events, [80] hot segments, [81] (hot_total again), [82] cold segments, [76] the next batch's hot ids
+        const uint32_t nhot = e->nhot;
+        uint32_t* words = e->d_flag;    // per event: W_HOT | hot id << 12 | rank in its tile's hot id, else 0
+        uint32_t* hot_off = e->d_pos;   // [hot id][tile] counts, scanned in place: the runs' sorted positions
+        uint32_t* ccnt = B.d_ccnt;      // per tile: cold events (compacted at the tile's start in k1 / v1)
+        HIPCHK(launch_grp_first(dev_ev, n, R, e->gbase, ring_mask, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,
+                                e->d_comp, dev_ext, dev_args, n_args, SG_MAX_CONTEXTS, e->d_hot_tab, nhot, nblocks,
+                                words, hot_off, e->d_k1, e->d_v1, ccnt, e->d_hist, gs));
+        if (nhot) HIPCHK(launch_scan(hot_off, hot_off, (uint64_t)nhot * nblocks, e->d_part, e->d_bsmall + 77, gs));
+        HIPCHK(launch_cold_n(n, e->d_bsmall + 77, e->d_bsmall + 78, gs));
+        for (int p = 0; p < passes; ++p) {  // the cold (key, index) pairs
+            if (p > 0) HIPCHK(launch_radix_hist_n(kin, n, e->d_bsmall + 78, p * db, e->d_hist, nblocks, gs));
+            HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks << db, e->d_part, nullptr, gs));
+            const bool last = p == passes - 1;
+            HIPCHK(launch_radix_scatter_x(kin, vin, n, p ? e->d_bsmall + 78 : nullptr, p ? nullptr : ccnt,
+                                          last ? e->d_bsmall + 77 : nullptr, p * db, e->d_hist, nblocks, kout, vout,
+                                          last ? e->d_posof : nullptr, gs));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        // segments: the hot ids' (in id order), then the cold keys' [hot_total, n)
+        HIPCHK(launch_hot_segs(hot_off, nhot, nblocks, e->d_bsmall + 77, e->d_hot_list, e->d_segs, e->d_bsmall + 80, gs));
+        const uint64_t sc = nblocks + 64;
+        HIPCHK(launch_seg_cold(kin, n, e->d_bsmall + 77, e->d_bsmall + 80, ccnt + sc, ccnt + 2 * sc, e->d_segs, gs,
+                               launch_scan, e->d_part, e->d_bsmall + 82, e->d_bsmall + 1));
+        HIPCHK(hipMemsetAsync(e->d_bst, 0, ((n + 1023) / 1024) * 4, gs));
+        HIPCHK(launch_grp_records(dev_ev, n, R, e->gbase, ring_mask, e->cfg.statistic_max_rt, words, hot_off, nblocks,
+                                  e->d_posof, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst, e->d_bsmall + 0,
+                                  e->d_comp, dev_ext, dev_args, SG_MAX_CONTEXTS, gs));
+        HIPCHK(launch_block_sums(e->d_recs, n, e->d_bst, e->d_link, e->epoch, e->d_bsmall + 0, gs));
+    }
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement), sized by an upper bound of
     // the segment count so that the group stage needs one host round trip
     const bool force_lane = !e->cfg.switch_on || (e->dbg_flags & 2);
@@ -2218,12 +2289,20 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                           (uint32_t)B.mix_cap, e->d_bsmall + 72, (e->pv_on || e->pvt_on) ? 0u : e->pq_wide, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
+    // the next batch's hot ids: this batch's resources of >= n / 8192 events (about one per 4096-event tile, so
+    // that a tile's run of one hot id is more than a random write), at least 64
+    const uint32_t hot_min = (uint32_t)std::max<uint64_t>(64, n / 8192);
+    if (!e->radix_group)
+        HIPCHK(launch_hot_build(e->d_segs, e->d_bsmall + 1, mb, hot_min, R, e->d_hot_tab, e->d_hot_list, e->nhot,
+                                e->d_bsmall + 76, gs));
     // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..8+N_BINS] bin offsets [72] wide XF_MIX events
-    uint32_t head[73];
+    // [76] the next batch's hot ids
+    uint32_t head[77];
     static_assert(8 + N_BINS + 1 <= 72, "head layout");
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
     HIPCHK(hipEventRecord(B.ev[1], gs));
     HIPCHK(hipStreamSynchronize(gs));
+    if (!e->radix_group) e->nhot = std::min<uint32_t>(head[76], hot_max());
     const uint32_t m = head[1];
     const uint32_t nprev = head[3];
     int64_t t0 = 0;

@@ -175,6 +175,335 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
     for (int b = threadIdx.x; b < NB; b += RS_THREADS) ghist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
 }
 
+// =================================================================================
+// 1b. grouping by a hot / cold split (the default group stage)
+// =================================================================================
+// Zipf traffic puts most of a batch on a few hundred resources (C4: the ~540 resources of >= 4096 events hold ~65 %
+// of a 2^25-event batch), and LSD radix passes over them move every event three times to end where one counting
+// split would put it.  The resources that were hot in the previous batch (k_hot_build, from its segments) get
+// dense ids h < nhot: their events go to their final sorted positions in ONE pass (per-tile counts per hot id, a
+// scan, a scatter), hot id by hot id, each in event order.  Only the cold rest takes the radix passes.  Every
+// resource's events end contiguous and in event order -- all the decide stage needs (segments are not in resource
+// order: hot ids first, then the cold keys sorted).
+//
+//   k_grp_first  : events read once in submission order: the batch's validation, marks and key ring (as
+//                  k_rs_first), the tile's stable rank of every hot event within its hot id (word[i] = W_HOT |
+//                  h << 12 | rank), the tile's hot-id counts, and the cold events' (key, index) compacted per
+//                  tile with the first radix digit's histogram
+//   radix passes : the cold (key, index) only (k_radix_scatter with per-tile counts on the first pass); the last
+//                  pass writes the sorted values and pos_of at hot_total + its position
+//   k_grp_records: events read again: every event's sorted position (hot: scanned tile offset + rank; cold:
+//                  pos_of), same-batch references mapped to sorted positions, the 16-byte record written there
+#define HOT_MAX 1024u
+#define HOT_NONE 0xFFFFu
+#define W_HOT 0x80000000u
+
+template <int DB>
+__global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
+                                                       uint64_t gbase, uint64_t ring_mask, uint32_t* __restrict__ bflags,
+                                                       int64_t* __restrict__ t0_out, uint32_t* __restrict__ prio,
+                                                       uint64_t* __restrict__ key_ring, const uint32_t* __restrict__ comp,
+                                                       const sg_event_ext* __restrict__ ext, const sg_arg* __restrict__ args,
+                                                       uint64_t n_args, uint32_t max_ctx,
+                                                       const uint16_t* __restrict__ hot_tab, uint32_t nhot,
+                                                       uint32_t nblocks, uint32_t* __restrict__ words,
+                                                       uint32_t* __restrict__ hot_hist, uint32_t* __restrict__ ckeys,
+                                                       uint32_t* __restrict__ cvals, uint32_t* __restrict__ ccnt,
+                                                       uint32_t* __restrict__ chist) {
+    constexpr int NB = 1 << DB;
+    __shared__ uint32_t wcnt[4][HOT_MAX];  // per-wave hot-id counts, then per-wave rank offsets
+    __shared__ uint32_t h[NB];
+    __shared__ uint32_t cw[4];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < NB; i += RS_THREADS) h[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 4 * HOT_MAX; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t t0 = ev[0].ts;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *t0_out = t0;
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t wbase = base + (uint64_t)w * (RS_TILE / 4);
+    const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
+    uint32_t fl = 0;
+    uint32_t kk[RS_ITEMS], rk[RS_ITEMS];  // key; hot: id << 16 | wave rank, cold: wave rank
+    uint32_t hotm = 0, entm = 0;          // per item: hot, ENTRY
+    uint32_t ccount = 0;                  // the wave's cold items so far
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {  // per-wave rounds of 64 consecutive events: coalesced, in event order
+        const uint64_t i = wbase + (uint64_t)it * WAVE + l;
+        const bool valid = i < n;
+        uint32_t key = 0, hid = HOT_NONE;
+        if (valid) {
+            const sg_event e = ev[i];
+            if (e.res_id >= max_res) fl |= BF_BAD_RES;
+            const int64_t dt = e.ts - t0;
+            if (dt < 0 || dt > 0x7FFFFFFFLL) fl |= (dt < 0 ? BF_BACKWARD : BF_TSPAN);
+            if (i > 0 && ev[i - 1].ts > e.ts) fl |= BF_BACKWARD;  // ABI: non-decreasing ts
+            uint32_t mark = 0;  // PM_* marks for the resource
+            uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+            bool own_args = false;
+            if (ext) {  // sg_submit_ex: validate the event's args; a NullContext event is k_lane's
+                const sg_event_ext x = ext[i];
+                if (x.n_args > SG_MAX_ARGS || (uint64_t)x.arg_off + x.n_args > n_args) fl |= BF_BAD_ARGS;
+                else if (x.n_args) {
+                    for (uint32_t k = 0; k < x.n_args; ++k) {
+                        const sg_arg a = args[x.arg_off + k];
+                        if (a.kind > SG_ARG_LIST || (a.kind == SG_ARG_LIST && (a.key > n_args || a.len > n_args - a.key)))
+                            fl |= BF_BAD_ARGS;
+                        else if (a.kind == SG_ARG_LIST) {
+                            mark |= PM_ARGL;
+                            for (uint32_t q = 0; q < a.len; ++q)
+                                if (args[a.key + q].kind > SG_ARG_SCALAR) fl |= BF_BAD_ARGS;
+                        }
+                    }
+                    const sg_arg a0 = args[x.arg_off];
+                    key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                    own_args = true;
+                }
+                if (x.context_id > max_ctx) mark |= PM_LANE;
+                else if (x.origin_id != 0 || x.context_id != 0) {
+                    mark |= PM_AUX;
+                    if (x.origin_id >> TAG_ORIGIN_BITS) mark |= PM_LANE;
+                }
+            }
+            if (own_args && e.kind == SG_EV_EXIT && (e.flags & SG_F_EXIT_ARGS)) mark |= PM_XARGS;
+            if (e.kind == SG_EV_ENTRY) {
+                if (key_ring) key_ring[(gbase + i) & ring_mask] = key0;
+                if (e.flags & SG_F_PRIORITIZED) mark |= PM_PRIO;
+                if (e.flags & SG_F_BLOCKED_UPSTREAM) mark |= PM_LANE;
+            } else if (e.kind == SG_EV_EXIT && own_args && key_ring) {
+                key_ring[(gbase + i) & ring_mask] = key0;
+            }
+            if (e.kind != SG_EV_ENTRY) {
+                const uint64_t ref = e.aux & SG_REF_NONE;
+                if (ref != SG_REF_NONE && ref >= gbase && ref - gbase >= i) fl |= BF_BAD_REF;  // must follow its ENTRY
+            }
+            if (mark && e.res_id < max_res && (prio[e.res_id] & mark) != mark) atomicOr(&prio[e.res_id], mark);
+            key = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
+            if (key < max_res) hid = hot_tab[key];
+            if (e.kind == SG_EV_ENTRY) entm |= 1u << it;
+        }
+        kk[it] = key;
+        const bool hot = valid && hid < nhot;
+        // hot: the rank among the wave's earlier items of the same id (peers by ballots over the id's bits)
+        uint64_t peers = __ballot(hot);
+#pragma unroll
+        for (int b = 0; b < 10; ++b) {
+            const uint64_t bb = __ballot((hid >> b) & 1);
+            peers &= ((hid >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t hrank = __popcll(peers & lt);
+        uint32_t* myc = wcnt[w];
+        const uint32_t old = hot ? myc[hid] : 0u;  // (read by every peer before its first one bumps it)
+        if (hot && hrank == 0) myc[hid] = old + (uint32_t)__popcll(peers);
+        const uint64_t cb = __ballot(valid && !hot);
+        if (hot) {
+            hotm |= 1u << it;
+            rk[it] = (hid << 16) | (old + hrank);
+        } else {
+            rk[it] = ccount + (uint32_t)__popcll(cb & lt);
+        }
+        ccount += (uint32_t)__popcll(cb);
+        hist_add<DB>(h, key & (NB - 1), valid && !hot);
+    }
+    if (l == 0) cw[w] = ccount;
+    if (fl) atomicOr(bflags, fl);
+    __syncthreads();
+    // per hot id: the waves' offsets (exclusive over waves) in place, the tile's count to the hot histogram
+    for (uint32_t d = threadIdx.x; d < nhot; d += RS_THREADS) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) { const uint32_t c = wcnt[ww][d]; wcnt[ww][d] = acc; acc += c; }
+        hot_hist[(uint64_t)d * nblocks + blockIdx.x] = acc;
+    }
+    uint32_t coff = 0;
+    for (int ww = 0; ww < w; ++ww) coff += cw[ww];
+    if (threadIdx.x == 0) ccnt[blockIdx.x] = cw[0] + cw[1] + cw[2] + cw[3];
+    for (int b = threadIdx.x; b < NB; b += RS_THREADS) chist[(uint64_t)b * nblocks + blockIdx.x] = h[b];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; ++it) {
+        const uint64_t i = wbase + (uint64_t)it * WAVE + l;
+        if (i >= n) continue;
+        if ((hotm >> it) & 1) {
+            const uint32_t hid = rk[it] >> 16;
+            words[i] = W_HOT | (hid << 12) | (wcnt[w][hid] + (rk[it] & 0xFFFFu));
+        } else {
+            words[i] = 0;
+            const uint64_t o = base + coff + rk[it];  // the tile's cold items, compacted in event order
+            ckeys[o] = kk[it];
+            cvals[o] = (uint32_t)i | (((entm >> it) & 1) ? 0x80000000u : 0u);
+        }
+    }
+}
+
+// The sorted position of event j (its word; cold: pos_of from the cold sort's last pass)
+__device__ __forceinline__ uint32_t grp_pos(uint64_t j, const uint32_t* __restrict__ words,
+                                            const uint32_t* __restrict__ hot_off, uint32_t nblocks,
+                                            const uint32_t* __restrict__ pos_of) {
+    const uint32_t wd = words[j];
+    if (wd & W_HOT) return hot_off[(uint64_t)((wd >> 12) & (HOT_MAX - 1)) * nblocks + j / RS_TILE] + (wd & 0xFFFu);
+    return pos_of[j] & 0x7FFFFFFFu;
+}
+
+// Every event's 16-byte record at its sorted position (one lane an event, in submission order).  References to
+// ENTRYs of this batch become the ENTRY's sorted position here: an EXIT sits ~RT of traffic after its ENTRY, so the
+// ENTRY's word / pos_of / event are recent lines (cache) -- a reference must name an earlier ENTRY of the same
+// resource (sort key); one that names a non-ENTRY resolves like an unknown entry.  References into earlier batches
+// are listed (prev) for k_resolve.  Hot events also get their pos_of entry and sorted value here.
+__global__ __launch_bounds__(256) void k_grp_records(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
+                                                     uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
+                                                     const uint32_t* __restrict__ words,
+                                                     const uint32_t* __restrict__ hot_off, uint32_t nblocks,
+                                                     uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
+                                                     uint32_t* __restrict__ svals, uint32_t* __restrict__ prev,
+                                                     uint32_t* __restrict__ nprev, uint32_t* __restrict__ bst,
+                                                     uint32_t* __restrict__ bflags, const uint32_t* __restrict__ comp,
+                                                     const sg_event_ext* __restrict__ ext,
+                                                     const sg_arg* __restrict__ args, uint32_t max_ctx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool is_prev = false, bad = false, zero = false;
+    uint32_t p = 0;
+    if (i < n) {
+        const int64_t t0 = ev[0].ts;
+        const sg_event e = ev[i];
+        const uint32_t wd = words[i];
+        const bool entry = e.kind == SG_EV_ENTRY;
+        p = (wd & W_HOT) ? hot_off[(uint64_t)((wd >> 12) & (HOT_MAX - 1)) * nblocks + i / RS_TILE] + (wd & 0xFFFu)
+                         : (pos_of[i] & 0x7FFFFFFFu);
+        SEv r;
+        r.dt = (int32_t)(e.ts - t0);
+        r.x = 0;
+        r.cnt = e.count;
+        r.rt = 0;
+        r.kind = e.kind;
+        r.flags = (uint8_t)(e.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
+        r.code = RC_NONE;
+        r.pad = 0;
+        uint32_t tag = 0;
+        bool own_args = false;
+        uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+        if (ext) {
+            const sg_event_ext x = ext[i];
+            if (x.n_args && x.n_args <= SG_MAX_ARGS) {
+                const sg_arg a0 = args[x.arg_off];
+                key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                own_args = true;
+            }
+            if (x.context_id <= max_ctx && (x.origin_id != 0 || x.context_id != 0) && !(x.origin_id >> TAG_ORIGIN_BITS))
+                tag = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
+        }
+        if (own_args) {
+            r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
+            if (e.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
+        }
+        r.x = tag;
+        if (entry) {
+            zero = e.count == 0;
+        } else {
+            if (e.kind == SG_EV_EXIT) {
+                const int64_t raw = (int64_t)(e.aux >> 48);
+                r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
+            }
+            const uint64_t ref = e.aux & SG_REF_NONE;
+            if (ref != SG_REF_NONE) {
+                if (ref >= gbase) {
+                    const uint64_t j = ref - gbase;
+                    if (j < i) {  // (k_grp_first flagged the others)
+                        const sg_event f = ev[j];
+                        if (f.kind == SG_EV_ENTRY) {
+                            const uint32_t ki = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
+                            const uint32_t kj = (comp && f.res_id < max_res) ? comp[f.res_id] : f.res_id;
+                            if (ki != kj) bad = true;
+                            r.code = RC_BATCH;
+                            r.x = grp_pos(j, words, hot_off, nblocks, pos_of);
+                        } else {
+                            r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+                        }
+                    }
+                } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve
+                    r.code = RC_PREV;
+                    r.x = (uint32_t)(ref & ring_mask);
+                    is_prev = true;
+                }
+            }
+            if (r.code == RC_NONE || r.code == RC_PREV) atomicOr(&bst[p >> 10], BST_STATIC);
+        }
+        recs[p] = r;
+        if (wd & W_HOT) {
+            const uint32_t v = (uint32_t)i | (entry ? 0x80000000u : 0u);
+            svals[p] = v;
+            pos_of[i] = p | (entry ? 0x80000000u : 0u);
+        }
+    }
+    // wave-aggregated flags and prev-list slots
+    const uint64_t pb = __ballot(is_prev);
+    if (pb) {
+        const int l = threadIdx.x & 63;
+        const int lead = __ffsll((long long)pb) - 1;
+        uint32_t b0 = 0;
+        if (l == lead) b0 = atomicAdd(nprev, (uint32_t)__popcll(pb));
+        b0 = __shfl(b0, lead, 64);
+        if (is_prev) prev[b0 + __popcll(pb & ((1ull << l) - 1))] = p;
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_BAD_REF);
+    if (__ballot(zero) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_ZERO_CNT);
+}
+
+// The hot ids' segments (hot id order, the non-empty ones) from the scanned per-tile counts: segs[0 .. k),
+// out[0] = k, out[1] = hot_total (the cold region's first position).  One workgroup of HOT_MAX lanes.
+__global__ __launch_bounds__(HOT_MAX) void k_hot_segs(const uint32_t* __restrict__ hot_off, uint32_t nhot,
+                                                      uint32_t nblocks, const uint32_t* __restrict__ hot_total,
+                                                      const uint32_t* __restrict__ hot_list, Seg* __restrict__ segs,
+                                                      uint32_t* __restrict__ out) {
+    __shared__ uint32_t ws[HOT_MAX / 64];
+    const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
+    const uint32_t tot = nhot ? *hot_total : 0u;
+    uint32_t s = 0, len = 0;
+    if (t < nhot) {
+        s = hot_off[(uint64_t)t * nblocks];
+        len = (t + 1 < nhot ? hot_off[(uint64_t)(t + 1) * nblocks] : tot) - s;
+    }
+    const uint32_t f = len ? 1u : 0u;
+    uint32_t x = f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x += y;
+    }
+    if (l == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+    for (uint32_t k = 0; k < HOT_MAX / 64; ++k) { if (k < wv) pre += ws[k]; all += ws[k]; }
+    if (f) {
+        Seg sg;
+        sg.res = hot_list[t];
+        sg.start = s;
+        sg.len = 0;
+        sg.bin = 0;
+        segs[pre + x - f] = sg;
+    }
+    if (t == 0) { out[0] = all; out[1] = tot; }
+}
+
+// The next batch's hot ids: the segments of this one with >= min_len events (at most HOT_MAX, first come); the
+// previous ids are cleared first (k_hot_clear).  hot_n = the new count (for the host with the batch's head).
+__global__ void k_hot_clear(uint16_t* __restrict__ hot_tab, const uint32_t* __restrict__ hot_list, uint32_t nhot) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nhot) hot_tab[hot_list[t]] = (uint16_t)HOT_NONE;
+}
+// (after k_seg_bin: Seg.len is set)
+__global__ __launch_bounds__(256) void k_hot_build(const Seg* __restrict__ segs, const uint32_t* __restrict__ mp,
+                                                   uint32_t min_len, uint32_t max_res, uint16_t* __restrict__ hot_tab,
+                                                   uint32_t* __restrict__ hot_list, uint32_t* __restrict__ hot_n) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *mp || segs[s].len < min_len || segs[s].res >= max_res) return;  // (a batch the host will refuse)
+    const uint32_t k = atomicAdd(hot_n, 1u);
+    if (k >= HOT_MAX) return;
+    const uint32_t r = segs[s].res;
+    hot_tab[r] = (uint16_t)k;
+    hot_list[k] = r;
+}
+
 template <int DB>
 // ndev (optional): the key count on the device, at most n (the grid is sized for n)
 __global__ __launch_bounds__(RS_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, uint64_t n, int shift,
@@ -210,10 +539,16 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
                                                            const uint32_t* __restrict__ vals_in, uint64_t n, int shift,
                                                            const uint32_t* __restrict__ goff, uint32_t nblocks,
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                           uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ ndev) {
+                                                           uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ ndev,
+                                                           const uint32_t* __restrict__ tcnt,
+                                                           const uint32_t* __restrict__ dbase) {
     constexpr int NB = 1 << DB;
     if (ndev && *ndev < n) n = *ndev;
     if ((uint64_t)blockIdx.x * RS_TILE >= n) return;  // (a tile past the device count: nothing to move)
+    // tcnt (optional): tile t holds tcnt[t] items at its start (k_grp_first's compacted cold items), the rest of
+    // its span is not input; dbase (optional): every destination is offset by *dbase
+    if (tcnt) n = (uint64_t)blockIdx.x * RS_TILE + tcnt[blockIdx.x];
+    const uint32_t ob = dbase ? *dbase : 0u;
     constexpr int DPT = NB / RS_THREADS;  // digits per thread in the offset scan
     static_assert(NB % RS_THREADS == 0, "whole digits per thread");
     __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
@@ -293,7 +628,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < cnt_tile; p += RS_THREADS) {  // digit runs: consecutive addresses
         const uint32_t k = sk[p], v = sv[p];
-        const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (NB - 1)] + (int64_t)p);
+        const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (NB - 1)] + (int64_t)p) + ob;
         keys_out[dst] = k;
         vals_out[dst] = v;
         if (pos_of) pos_of[v & 0x7FFFFFFFu] = (uint32_t)dst | (v & 0x80000000u);
@@ -500,15 +835,65 @@ hipError_t launch_radix_hist_n(const uint32_t* keys, uint64_t n, const uint32_t*
 hipError_t launch_radix_scatter_n(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev, int shift,
                                   const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, (uint32_t*)nullptr, ndev);
+                       kout, vout, (uint32_t*)nullptr, ndev, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, pos_of, (const uint32_t*)nullptr);
+                       kout, vout, pos_of, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
+// the cold passes of the hot / cold group stage: tcnt = per-tile counts (first pass), ndev = the cold count (later
+// passes), dbase = hot_total (last pass: sorted values and pos_of at their final positions)
+hipError_t launch_radix_scatter_x(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev,
+                                  const uint32_t* tcnt, const uint32_t* dbase, int shift, const uint32_t* goff,
+                                  uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
+                       kout, vout, pos_of, ndev, tcnt, dbase);
+    return hipGetLastError();
+}
+hipError_t launch_grp_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
+                            uint32_t* bflags, int64_t* t0_out, uint32_t* prio, uint64_t* key_ring, const uint32_t* comp,
+                            const sg_event_ext* ext, const sg_arg* args, uint64_t n_args, uint32_t max_ctx,
+                            const uint16_t* hot_tab, uint32_t nhot, uint32_t nblocks, uint32_t* words,
+                            uint32_t* hot_hist, uint32_t* ckeys, uint32_t* cvals, uint32_t* ccnt, uint32_t* chist,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_grp_first<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, ev, n, max_res, gbase, ring_mask, bflags,
+                       t0_out, prio, key_ring, comp, ext, args, n_args, max_ctx, hot_tab, nhot, nblocks, words, hot_hist,
+                       ckeys, cvals, ccnt, chist);
+    return hipGetLastError();
+}
+hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
+                              int32_t max_rt, const uint32_t* words, const uint32_t* hot_off, uint32_t nblocks,
+                              uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev, uint32_t* nprev,
+                              uint32_t* bst, uint32_t* bflags, const uint32_t* comp, const sg_event_ext* ext,
+                              const sg_arg* args, uint32_t max_ctx, hipStream_t st) {
+    hipLaunchKernelGGL(k_grp_records, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, ev, n, max_res, gbase,
+                       ring_mask, max_rt, words, hot_off, nblocks, pos_of, recs, svals, prev, nprev, bst, bflags, comp,
+                       ext, args, max_ctx);
+    return hipGetLastError();
+}
+hipError_t launch_hot_segs(const uint32_t* hot_off, uint32_t nhot, uint32_t nblocks, const uint32_t* hot_total,
+                           const uint32_t* hot_list, Seg* segs, uint32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_hot_segs, dim3(1), dim3(HOT_MAX), 0, st, hot_off, nhot, nblocks, hot_total, hot_list, segs, out);
+    return hipGetLastError();
+}
+hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
+                            uint32_t* hot_list, uint32_t nhot_old, uint32_t* hot_n, hipStream_t st) {
+    if (nhot_old) hipLaunchKernelGGL(k_hot_clear, dim3((nhot_old + 255) / 256), dim3(256), 0, st, hot_tab, hot_list, nhot_old);
+    if (mb) hipLaunchKernelGGL(k_hot_build, dim3((mb + 255) / 256), dim3(256), 0, st, segs, mp, min_len, max_res, hot_tab,
+                               hot_list, hot_n);
+    return hipGetLastError();
+}
+__global__ void k_cold_n(uint64_t n, const uint32_t* __restrict__ hot_total, uint32_t* __restrict__ out) {
+    if (threadIdx.x == 0) *out = (uint32_t)(n - *hot_total);
+}
+hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_cold_n, dim3(1), dim3(64), 0, st, n, hot_total, out);
+    return hipGetLastError();
+}
+uint32_t hot_max() { return HOT_MAX; }
 
 uint32_t radix_tile() { return RS_TILE; }
 
