@@ -307,10 +307,13 @@ __global__ __launch_bounds__(256) void k_scatter_rec(const SEv* __restrict__ rec
 // EXIT (or TRACE) named the same ENTRY (BF_MULTI_LINK: frozen-stretch skipping is off for the batch).
 // A reference must also name an ENTRY of its own resource: the two carry the same sort key (inside a
 // STRATEGY_RELATE component the key is the component's).
-// skeys (optional: the radix group stage; the hot / cold one checks the resource in k_grp_records)
+// skeys: the sorted keys of positions >= *lo (the hot / cold group stage's cold region: k_grp_records checked the
+// references of hot events; lo = null: every position, the radix group stage)
 __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs, const uint32_t* __restrict__ skeys,
                                                     uint64_t n, uint32_t* __restrict__ bst, Link* __restrict__ link,
-                                                    uint32_t epoch, uint32_t* __restrict__ bflags) {
+                                                    uint32_t epoch, uint32_t* __restrict__ bflags,
+                                                    const uint32_t* __restrict__ lo) {
+    const uint32_t kmin = lo ? *lo : 0u;
     __shared__ uint32_t wsum[4];
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
     uint32_t v = 0;
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
                     r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
                 const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
                 if ((uint32_t)(old >> 32) == epoch) multi = true;
-                if (skeys && skeys[r.x] != skeys[p]) bad = true;
+                if (p >= kmin && r.x >= kmin && skeys[r.x] != skeys[p]) bad = true;
             }
         }
     }
@@ -3353,9 +3356,9 @@ hipError_t launch_seg_cold(const uint32_t* keys, uint64_t n, const uint32_t* lo,
 }
 // the sorted-order side tables (bst sums, forward links) of the hot / cold group stage (its records are in place)
 hipError_t launch_block_sums(const SEv* recs, uint64_t n, uint32_t* bst, Link* link, uint32_t epoch, uint32_t* bflags,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs,
-                       (const uint32_t*)nullptr, n, bst, link, epoch, bflags);
+                             const uint32_t* skeys, const uint32_t* lo, hipStream_t st) {
+    hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, skeys, n, bst, link,
+                       epoch, bflags, lo);
     return hipGetLastError();
 }
 // mp: the segment count on the device; mb: an upper bound of it (the grid)
@@ -3387,7 +3390,7 @@ hipError_t launch_gather(const SEv* rec_o, const uint32_t* vals, const uint32_t*
     hipLaunchKernelGGL(k_scatter_rec, dim3(nb), dim3(256), 0, st, rec_o, n, pos_of, recs, prev, nprev, link, bst,
                        epoch, bflags);
     hipLaunchKernelGGL(k_block_sums, dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0, st, recs, skeys, n, bst, link,
-                       epoch, bflags);
+                       epoch, bflags, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, const SEv* recs, const Prog* prog,

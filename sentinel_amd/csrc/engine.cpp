@@ -46,13 +46,15 @@ hipError_t launch_grp_first(const sg_event* ev, uint64_t n, uint32_t max_res, ui
                             const uint16_t* hot_tab, uint32_t nhot, uint32_t nblocks, uint32_t* words,
                             uint32_t* hot_hist, uint32_t* ckeys, uint32_t* cvals, uint32_t* ccnt, uint32_t* chist,
                             hipStream_t st);
-hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
-                              int32_t max_rt, const uint32_t* words, const uint32_t* hot_off, uint32_t nblocks,
-                              uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev, uint32_t* nprev,
-                              uint32_t* bst, uint32_t* bflags, const uint32_t* comp, const sg_event_ext* ext,
+hipError_t launch_hot_scan(uint32_t* C, uint32_t nblocks, uint32_t nhot, uint32_t* part, uint32_t* hb, uint32_t* total,
+                           hipStream_t st);
+hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
+                              const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
+                              const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
+                              uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
                               const sg_arg* args, uint32_t max_ctx, hipStream_t st);
-hipError_t launch_hot_segs(const uint32_t* hot_off, uint32_t nhot, uint32_t nblocks, const uint32_t* hot_total,
-                           const uint32_t* hot_list, Seg* segs, uint32_t* out, hipStream_t st);
+hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,
+                           hipStream_t st);
 hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
                             uint32_t* hot_list, uint32_t nhot_old, uint32_t* hot_n, hipStream_t st);
 hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, hipStream_t st);
@@ -62,7 +64,7 @@ hipError_t launch_seg_cold(const uint32_t* keys, uint64_t n, const uint32_t* lo,
                            hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                            uint32_t* part, uint32_t* ccount, uint32_t* nseg);
 hipError_t launch_block_sums(const SEv* recs, uint64_t n, uint32_t* bst, Link* link, uint32_t epoch, uint32_t* bflags,
-                             hipStream_t st);
+                             const uint32_t* skeys, const uint32_t* lo, hipStream_t st);
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st);
 uint32_t radix_tile();
@@ -579,6 +581,8 @@ struct sg_engine {
     uint16_t* d_hot_tab = nullptr;
     uint32_t* d_hot_list = nullptr;
     uint32_t nhot = 0;
+    uint32_t* d_hot_part = nullptr;  // the hot scan's per-chunk partials ((max tiles / 64 + 2) x HOT_MAX words)
+    uint32_t* d_hot_hb = nullptr;    // per hot id: first sorted position, total (2 x HOT_MAX words)
     bool radix_group = false;    // SG_DEBUG_FLAGS & 8192: the all-radix group stage (A/B)
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
     AuxNode* d_auxtab = nullptr;
@@ -737,6 +741,12 @@ int ensure_batch(sg_engine* e, uint64_t n) {
         HIPCHK(hipMalloc(&B.d_recs, c * sizeof(SEv)));
         if (e->radix_group) HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));  // (the hot / cold stage has none)
         HIPCHK(hipMalloc(&B.d_ccnt, 3 * (nblocks + 64) * 4));
+    }
+    dfree(e->d_hot_part);
+    dfree(e->d_hot_hb);
+    HIPCHK(hipMalloc(&e->d_hot_part, (nblocks / 64 + 2) * hot_max() * 4));
+    HIPCHK(hipMalloc(&e->d_hot_hb, 2 * hot_max() * 4));
+    for (auto& B : e->slot) {
         HIPCHK(hipMalloc(&B.d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));
         HIPCHK(hipMalloc(&B.d_prev, c * 4));
         HIPCHK(hipMalloc(&B.d_bsmall, 256 * 4));
@@ -1380,7 +1390,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_pvseg); dfree(e->d_pvtseg); dfree(e->d_pvtot); dfree(e->d_pvrest);
     if (e->gstream) (void)hipStreamSynchronize(e->gstream);
     for (auto& B : e->slot) free_slot(B);
-    dfree(e->d_prio); dfree(e->d_hot_tab); dfree(e->d_hot_list); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
+    dfree(e->d_prio); dfree(e->d_hot_tab); dfree(e->d_hot_list); dfree(e->d_hot_part); dfree(e->d_hot_hb); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
     dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
     dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
@@ -2238,7 +2248,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(launch_grp_first(dev_ev, n, R, e->gbase, ring_mask, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,
                                 e->d_comp, dev_ext, dev_args, n_args, SG_MAX_CONTEXTS, e->d_hot_tab, nhot, nblocks,
                                 words, hot_off, e->d_k1, e->d_v1, ccnt, e->d_hist, gs));
-        if (nhot) HIPCHK(launch_scan(hot_off, hot_off, (uint64_t)nhot * nblocks, e->d_part, e->d_bsmall + 77, gs));
+        HIPCHK(launch_hot_scan(hot_off, nblocks, nhot, e->d_hot_part, e->d_hot_hb, e->d_bsmall + 77, gs));
         HIPCHK(launch_cold_n(n, e->d_bsmall + 77, e->d_bsmall + 78, gs));
         for (int p = 0; p < passes; ++p) {  // the cold (key, index) pairs
             if (p > 0) HIPCHK(launch_radix_hist_n(kin, n, e->d_bsmall + 78, p * db, e->d_hist, nblocks, gs));
@@ -2251,15 +2261,15 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
             std::swap(vin, vout);
         }
         // segments: the hot ids' (in id order), then the cold keys' [hot_total, n)
-        HIPCHK(launch_hot_segs(hot_off, nhot, nblocks, e->d_bsmall + 77, e->d_hot_list, e->d_segs, e->d_bsmall + 80, gs));
+        HIPCHK(launch_hot_segs(e->d_hot_hb, nhot, e->d_hot_list, e->d_segs, e->d_bsmall + 80, gs));
         const uint64_t sc = nblocks + 64;
         HIPCHK(launch_seg_cold(kin, n, e->d_bsmall + 77, e->d_bsmall + 80, ccnt + sc, ccnt + 2 * sc, e->d_segs, gs,
                                launch_scan, e->d_part, e->d_bsmall + 82, e->d_bsmall + 1));
         HIPCHK(hipMemsetAsync(e->d_bst, 0, ((n + 1023) / 1024) * 4, gs));
-        HIPCHK(launch_grp_records(dev_ev, n, R, e->gbase, ring_mask, e->cfg.statistic_max_rt, words, hot_off, nblocks,
-                                  e->d_posof, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst, e->d_bsmall + 0,
-                                  e->d_comp, dev_ext, dev_args, SG_MAX_CONTEXTS, gs));
-        HIPCHK(launch_block_sums(e->d_recs, n, e->d_bst, e->d_link, e->epoch, e->d_bsmall + 0, gs));
+        HIPCHK(launch_grp_records(dev_ev, n, e->gbase, ring_mask, e->cfg.statistic_max_rt, words, hot_off, nhot, nblocks,
+                                  e->d_hot_hb, e->d_posof, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst,
+                                  e->d_bsmall + 0, dev_ext, dev_args, SG_MAX_CONTEXTS, gs));
+        HIPCHK(launch_block_sums(e->d_recs, n, e->d_bst, e->d_link, e->epoch, e->d_bsmall + 0, kin, e->d_bsmall + 77, gs));
     }
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement), sized by an upper bound of
     // the segment count so that the group stage needs one host round trip

@@ -196,7 +196,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
 //                  pos_of), same-batch references mapped to sorted positions, the 16-byte record written there
 #define HOT_MAX 1024u
 #define HOT_NONE 0xFFFFu
-#define W_HOT 0x80000000u
+#define W_HOT 0x80000000u   // word: a hot event (W_HOT | W_ENT? | hot id << 12 | rank in its tile's run)
+#define W_ENT 0x40000000u   // word: an ENTRY (hot or cold)
 
 template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
@@ -308,12 +309,13 @@ __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __rest
     if (l == 0) cw[w] = ccount;
     if (fl) atomicOr(bflags, fl);
     __syncthreads();
-    // per hot id: the waves' offsets (exclusive over waves) in place, the tile's count to the hot histogram
+    // per hot id: the waves' offsets (exclusive over waves) in place, the tile's count to its row of the hot
+    // counts (tile-major: one contiguous row a tile; k_hot_scan_* turn them into the runs' positions)
     for (uint32_t d = threadIdx.x; d < nhot; d += RS_THREADS) {
         uint32_t acc = 0;
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) { const uint32_t c = wcnt[ww][d]; wcnt[ww][d] = acc; acc += c; }
-        hot_hist[(uint64_t)d * nblocks + blockIdx.x] = acc;
+        hot_hist[(uint64_t)blockIdx.x * nhot + d] = acc;
     }
     uint32_t coff = 0;
     for (int ww = 0; ww < w; ++ww) coff += cw[ww];
@@ -324,11 +326,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __rest
     for (int it = 0; it < RS_ITEMS; ++it) {
         const uint64_t i = wbase + (uint64_t)it * WAVE + l;
         if (i >= n) continue;
+        const uint32_t ent = ((entm >> it) & 1) ? W_ENT : 0u;
         if ((hotm >> it) & 1) {
             const uint32_t hid = rk[it] >> 16;
-            words[i] = W_HOT | (hid << 12) | (wcnt[w][hid] + (rk[it] & 0xFFFFu));
+            words[i] = W_HOT | ent | (hid << 12) | (wcnt[w][hid] + (rk[it] & 0xFFFFu));
         } else {
-            words[i] = 0;
+            words[i] = ent;
             const uint64_t o = base + coff + rk[it];  // the tile's cold items, compacted in event order
             ckeys[o] = kk[it];
             cvals[o] = (uint32_t)i | (((entm >> it) & 1) ? 0x80000000u : 0u);
@@ -336,133 +339,238 @@ __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __rest
     }
 }
 
-// The sorted position of event j (its word; cold: pos_of from the cold sort's last pass)
-__device__ __forceinline__ uint32_t grp_pos(uint64_t j, const uint32_t* __restrict__ words,
-                                            const uint32_t* __restrict__ hot_off, uint32_t nblocks,
-                                            const uint32_t* __restrict__ pos_of) {
-    const uint32_t wd = words[j];
-    if (wd & W_HOT) return hot_off[(uint64_t)((wd >> 12) & (HOT_MAX - 1)) * nblocks + j / RS_TILE] + (wd & 0xFFFu);
-    return pos_of[j] & 0x7FFFFFFFu;
+// ---- the hot runs' sorted positions: the tile-major counts C[tile][h] become P[tile][h] = the first position of
+// tile's run of hot id h = sum over h' < h of h''s total + sum over tiles < tile of C[.][h] (hot ids in order,
+// each in tile order).  Reduce-then-scan along the tiles, TC tiles a chunk, rows read and written contiguous.
+#define HS_TC 64u
+// partial sums of every chunk: part[chunk][h]
+__global__ __launch_bounds__(256) void k_hot_scan_a(const uint32_t* __restrict__ C, uint32_t nblocks, uint32_t nhot,
+                                                    uint32_t* __restrict__ part) {
+    const uint32_t c = blockIdx.x, t0 = c * HS_TC, t1 = min(nblocks, t0 + HS_TC);
+    for (uint32_t h = threadIdx.x; h < nhot; h += 256) {
+        uint32_t a = 0;
+        for (uint32_t t = t0; t < t1; ++t) a += C[(uint64_t)t * nhot + h];
+        part[(uint64_t)c * nhot + h] = a;
+    }
+}
+// one workgroup: every chunk's exclusive prefix per h (in place), the ids' totals and bases: hb[h] = first position of
+// id h, hb[HOT_MAX + h] = its total; out[0] = hot_total
+__global__ __launch_bounds__(HOT_MAX) void k_hot_scan_b(uint32_t* __restrict__ part, uint32_t nch, uint32_t nhot,
+                                                        uint32_t* __restrict__ hb, uint32_t* __restrict__ out) {
+    __shared__ uint32_t ws[HOT_MAX / 64];
+    const uint32_t h = threadIdx.x, l = h & 63, wv = h >> 6;
+    uint32_t tot = 0;
+    if (h < nhot)
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint32_t v = part[(uint64_t)c * nhot + h];
+            part[(uint64_t)c * nhot + h] = tot;
+            tot += v;
+        }
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x += y;
+    }
+    if (l == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+    for (uint32_t k = 0; k < HOT_MAX / 64; ++k) { if (k < wv) pre += ws[k]; all += ws[k]; }
+    if (h < nhot) { hb[h] = pre + x - tot; hb[HOT_MAX + h] = tot; }
+    if (h == 0) *out = all;
+}
+// P in place of C: chunk base (hb + part) and a running sum down the chunk's tiles
+__global__ __launch_bounds__(256) void k_hot_scan_c(uint32_t* __restrict__ C, uint32_t nblocks, uint32_t nhot,
+                                                    const uint32_t* __restrict__ part, const uint32_t* __restrict__ hb) {
+    const uint32_t c = blockIdx.x, t0 = c * HS_TC, t1 = min(nblocks, t0 + HS_TC);
+    for (uint32_t h = threadIdx.x; h < nhot; h += 256) {
+        uint32_t run = hb[h] + part[(uint64_t)c * nhot + h];
+        for (uint32_t t = t0; t < t1; ++t) {
+            const uint32_t v = C[(uint64_t)t * nhot + h];
+            C[(uint64_t)t * nhot + h] = run;
+            run += v;
+        }
+    }
 }
 
-// Every event's 16-byte record at its sorted position (one lane an event, in submission order).  References to
-// ENTRYs of this batch become the ENTRY's sorted position here: an EXIT sits ~RT of traffic after its ENTRY, so the
-// ENTRY's word / pos_of / event are recent lines (cache) -- a reference must name an earlier ENTRY of the same
-// resource (sort key); one that names a non-ENTRY resolves like an unknown entry.  References into earlier batches
-// are listed (prev) for k_resolve.  Hot events also get their pos_of entry and sorted value here.
-__global__ __launch_bounds__(256) void k_grp_records(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
-                                                     uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
-                                                     const uint32_t* __restrict__ words,
-                                                     const uint32_t* __restrict__ hot_off, uint32_t nblocks,
-                                                     uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
-                                                     uint32_t* __restrict__ svals, uint32_t* __restrict__ prev,
-                                                     uint32_t* __restrict__ nprev, uint32_t* __restrict__ bst,
-                                                     uint32_t* __restrict__ bflags, const uint32_t* __restrict__ comp,
-                                                     const sg_event_ext* __restrict__ ext,
-                                                     const sg_arg* __restrict__ args, uint32_t max_ctx) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool is_prev = false, bad = false, zero = false;
-    uint32_t p = 0;
-    if (i < n) {
-        const int64_t t0 = ev[0].ts;
-        const sg_event e = ev[i];
-        const uint32_t wd = words[i];
-        const bool entry = e.kind == SG_EV_ENTRY;
-        p = (wd & W_HOT) ? hot_off[(uint64_t)((wd >> 12) & (HOT_MAX - 1)) * nblocks + i / RS_TILE] + (wd & 0xFFFu)
-                         : (pos_of[i] & 0x7FFFFFFFu);
-        SEv r;
-        r.dt = (int32_t)(e.ts - t0);
-        r.x = 0;
-        r.cnt = e.count;
-        r.rt = 0;
-        r.kind = e.kind;
-        r.flags = (uint8_t)(e.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
-        r.code = RC_NONE;
-        r.pad = 0;
-        uint32_t tag = 0;
-        bool own_args = false;
-        uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
-        if (ext) {
-            const sg_event_ext x = ext[i];
-            if (x.n_args && x.n_args <= SG_MAX_ARGS) {
-                const sg_arg a0 = args[x.arg_off];
-                key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
-                own_args = true;
-            }
-            if (x.context_id <= max_ctx && (x.origin_id != 0 || x.context_id != 0) && !(x.origin_id >> TAG_ORIGIN_BITS))
-                tag = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
+// The sorted position of event j and whether it is an ENTRY (its word; cold: pos_of from the cold sort's last pass)
+__device__ __forceinline__ uint32_t grp_pos(uint64_t j, uint32_t wd, const uint32_t* __restrict__ P, uint32_t nhot,
+                                            const uint32_t* __restrict__ pos_of, bool& entry) {
+    if (wd & W_HOT) {
+        entry = (wd & W_ENT) != 0;
+        return P[(j / RS_TILE) * nhot + ((wd >> 12) & (HOT_MAX - 1))] + (wd & 0xFFFu);
+    }
+    const uint32_t po = pos_of[j];
+    entry = (po & 0x80000000u) != 0;
+    return po & 0x7FFFFFFFu;
+}
+
+// Every event's 16-byte record at its sorted position: a workgroup of 1024 lanes per 4096-event tile (4 events a
+// lane, in submission order).  The tile's hot runs are staged in LDS in (hot id, rank) order and leave as runs of
+// consecutive positions (records and sorted values); a cold event's record goes straight to its position (the cold
+// sort placed it).  References to ENTRYs of this batch become the ENTRY's sorted position: an EXIT sits ~RT of
+// traffic after its ENTRY, so the ENTRY's word and position are recent lines.  A reference must name an earlier ENTRY
+// of the same resource: two hot events by their ids here, two cold ones by their sort keys in k_block_sums (sorted
+// order); one naming a non-ENTRY resolves like an unknown entry.  References into earlier batches are listed (prev)
+// for k_resolve.
+#define GR_THREADS 1024
+#define GR_ITEMS (RS_TILE / GR_THREADS)
+__global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __restrict__ ev, uint64_t n,
+                                                            uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
+                                                            const uint32_t* __restrict__ words,
+                                                            const uint32_t* __restrict__ P, uint32_t nhot,
+                                                            uint32_t nblocks, const uint32_t* __restrict__ hb,
+                                                            uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
+                                                            uint32_t* __restrict__ svals, uint32_t* __restrict__ prev,
+                                                            uint32_t* __restrict__ nprev, uint32_t* __restrict__ bst,
+                                                            uint32_t* __restrict__ bflags,
+                                                            const sg_event_ext* __restrict__ ext,
+                                                            const sg_arg* __restrict__ args, uint32_t max_ctx) {
+    __shared__ uint4 srec[RS_TILE];          // the tile's hot records in (hot id, rank) order
+    __shared__ uint32_t spos[RS_TILE], sval[RS_TILE];
+    __shared__ uint32_t lo[HOT_MAX];         // the tile's run of id h starts at local slot lo[h] (then its position)
+    __shared__ uint32_t ws[GR_THREADS / 64];
+    __shared__ uint32_t nh_tile;
+    const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * RS_TILE;
+    // the tile's run lengths per hot id (next row, or the id's end for the last tile), their local offsets
+    {
+        uint32_t c = 0;
+        if (t < nhot) {
+            const uint32_t p0 = P[(uint64_t)tile * nhot + t];
+            const uint32_t p1 = tile + 1 < nblocks ? P[(uint64_t)(tile + 1) * nhot + t] : hb[t] + hb[HOT_MAX + t];
+            c = p1 - p0;
         }
-        if (own_args) {
-            r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
-            if (e.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if ((int)l >= o) x += y;
         }
-        r.x = tag;
-        if (entry) {
-            zero = e.count == 0;
-        } else {
-            if (e.kind == SG_EV_EXIT) {
-                const int64_t raw = (int64_t)(e.aux >> 48);
-                r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
-            }
-            const uint64_t ref = e.aux & SG_REF_NONE;
-            if (ref != SG_REF_NONE) {
-                if (ref >= gbase) {
-                    const uint64_t j = ref - gbase;
-                    if (j < i) {  // (k_grp_first flagged the others)
-                        const sg_event f = ev[j];
-                        if (f.kind == SG_EV_ENTRY) {
-                            const uint32_t ki = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
-                            const uint32_t kj = (comp && f.res_id < max_res) ? comp[f.res_id] : f.res_id;
-                            if (ki != kj) bad = true;
-                            r.code = RC_BATCH;
-                            r.x = grp_pos(j, words, hot_off, nblocks, pos_of);
-                        } else {
-                            r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-                        }
-                    }
-                } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve
-                    r.code = RC_PREV;
-                    r.x = (uint32_t)(ref & ring_mask);
-                    is_prev = true;
+        if (l == 63) ws[wv] = x;
+        __syncthreads();
+        uint32_t pre = 0, all = 0;
+        for (uint32_t k = 0; k < GR_THREADS / 64; ++k) { if (k < wv) pre += ws[k]; all += ws[k]; }
+        if (t < nhot) lo[t] = pre + x - c;
+        if (t == 0) nh_tile = all;
+    }
+    __syncthreads();
+    const int64_t t0 = ev[0].ts;
+    bool bad = false, zero = false;
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * GR_THREADS + t;
+        bool is_prev = false;
+        uint32_t p = 0;
+        if (i < n) {
+            const sg_event e = ev[i];
+            const uint32_t wd = words[i];
+            const bool hot = (wd & W_HOT) != 0;
+            const bool entry = e.kind == SG_EV_ENTRY;
+            const uint32_t hid = (wd >> 12) & (HOT_MAX - 1);
+            p = hot ? P[(uint64_t)tile * nhot + hid] + (wd & 0xFFFu) : (pos_of[i] & 0x7FFFFFFFu);
+            SEv r;
+            r.dt = (int32_t)(e.ts - t0);
+            r.x = 0;
+            r.cnt = e.count;
+            r.rt = 0;
+            r.kind = e.kind;
+            r.flags = (uint8_t)(e.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
+            r.code = RC_NONE;
+            r.pad = 0;
+            uint32_t tag = 0;
+            bool own_args = false;
+            uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+            if (ext) {
+                const sg_event_ext x = ext[i];
+                if (x.n_args && x.n_args <= SG_MAX_ARGS) {
+                    const sg_arg a0 = args[x.arg_off];
+                    key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                    own_args = true;
                 }
+                if (x.context_id <= max_ctx && (x.origin_id != 0 || x.context_id != 0) && !(x.origin_id >> TAG_ORIGIN_BITS))
+                    tag = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
             }
-            if (r.code == RC_NONE || r.code == RC_PREV) atomicOr(&bst[p >> 10], BST_STATIC);
+            if (own_args) {
+                r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
+                if (e.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
+            }
+            r.x = tag;
+            if (entry) {
+                zero |= e.count == 0;
+            } else {
+                if (e.kind == SG_EV_EXIT) {
+                    const int64_t raw = (int64_t)(e.aux >> 48);
+                    r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
+                }
+                const uint64_t ref = e.aux & SG_REF_NONE;
+                if (ref != SG_REF_NONE) {
+                    if (ref >= gbase) {
+                        const uint64_t j = ref - gbase;
+                        if (j < i) {  // (k_grp_first flagged the others)
+                            const uint32_t wj = words[j];
+                            bool ej;
+                            const uint32_t pj = grp_pos(j, wj, P, nhot, pos_of, ej);
+                            if (ej) {
+                                // one hot and one cold, or two hot ids: not the same resource (two cold: k_block_sums)
+                                if (((wj ^ wd) & W_HOT) || (hot && ((wj >> 12) & (HOT_MAX - 1)) != hid)) bad = true;
+                                r.code = RC_BATCH;
+                                r.x = pj;
+                            } else {
+                                r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+                            }
+                        }
+                    } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve
+                        r.code = RC_PREV;
+                        r.x = (uint32_t)(ref & ring_mask);
+                        is_prev = true;
+                    }
+                }
+                if (r.code == RC_NONE || r.code == RC_PREV) atomicOr(&bst[p >> 10], BST_STATIC);
+            }
+            uint4 rv;
+            __builtin_memcpy(&rv, &r, sizeof(rv));
+            if (hot) {
+                const uint32_t slot = lo[hid] + (wd & 0xFFFu);
+                srec[slot] = rv;
+                spos[slot] = p;
+                sval[slot] = (uint32_t)i | (entry ? 0x80000000u : 0u);
+                pos_of[i] = p | (entry ? 0x80000000u : 0u);
+            } else {
+                reinterpret_cast<uint4*>(recs)[p] = rv;
+            }
         }
-        recs[p] = r;
-        if (wd & W_HOT) {
-            const uint32_t v = (uint32_t)i | (entry ? 0x80000000u : 0u);
-            svals[p] = v;
-            pos_of[i] = p | (entry ? 0x80000000u : 0u);
+        // wave-aggregated prev-list slots
+        const uint64_t pb = __ballot(is_prev);
+        if (pb) {
+            const int lead = __ffsll((long long)pb) - 1;
+            uint32_t b0 = 0;
+            if ((int)l == lead) b0 = atomicAdd(nprev, (uint32_t)__popcll(pb));
+            b0 = __shfl(b0, lead, 64);
+            if (is_prev) prev[b0 + __popcll(pb & ((1ull << l) - 1))] = p;
         }
     }
-    // wave-aggregated flags and prev-list slots
-    const uint64_t pb = __ballot(is_prev);
-    if (pb) {
-        const int l = threadIdx.x & 63;
-        const int lead = __ffsll((long long)pb) - 1;
-        uint32_t b0 = 0;
-        if (l == lead) b0 = atomicAdd(nprev, (uint32_t)__popcll(pb));
-        b0 = __shfl(b0, lead, 64);
-        if (is_prev) prev[b0 + __popcll(pb & ((1ull << l) - 1))] = p;
+    if (__ballot(bad) && l == 0) atomicOr(bflags, BF_BAD_REF);
+    if (__ballot(zero) && l == 0) atomicOr(bflags, BF_ZERO_CNT);
+    __syncthreads();
+    // the hot runs leave in slot order: consecutive slots of one id are consecutive positions
+    const uint32_t nh = nh_tile;
+    for (uint32_t k = t; k < nh; k += GR_THREADS) {
+        const uint32_t q = spos[k];
+        reinterpret_cast<uint4*>(recs)[q] = srec[k];
+        svals[q] = sval[k];
     }
-    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_BAD_REF);
-    if (__ballot(zero) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_ZERO_CNT);
 }
 
-// The hot ids' segments (hot id order, the non-empty ones) from the scanned per-tile counts: segs[0 .. k),
-// out[0] = k, out[1] = hot_total (the cold region's first position).  One workgroup of HOT_MAX lanes.
-__global__ __launch_bounds__(HOT_MAX) void k_hot_segs(const uint32_t* __restrict__ hot_off, uint32_t nhot,
-                                                      uint32_t nblocks, const uint32_t* __restrict__ hot_total,
+// The hot ids' segments (hot id order, the non-empty ones) from their bases and totals (hb): segs[0 .. k),
+// out[0] = k.  One workgroup of HOT_MAX lanes.
+__global__ __launch_bounds__(HOT_MAX) void k_hot_segs(const uint32_t* __restrict__ hb, uint32_t nhot,
                                                       const uint32_t* __restrict__ hot_list, Seg* __restrict__ segs,
                                                       uint32_t* __restrict__ out) {
     __shared__ uint32_t ws[HOT_MAX / 64];
     const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
-    const uint32_t tot = nhot ? *hot_total : 0u;
-    uint32_t s = 0, len = 0;
-    if (t < nhot) {
-        s = hot_off[(uint64_t)t * nblocks];
-        len = (t + 1 < nhot ? hot_off[(uint64_t)(t + 1) * nblocks] : tot) - s;
-    }
+    const uint32_t len = t < nhot ? hb[HOT_MAX + t] : 0u;
     const uint32_t f = len ? 1u : 0u;
     uint32_t x = f;
 #pragma unroll
@@ -477,12 +585,12 @@ __global__ __launch_bounds__(HOT_MAX) void k_hot_segs(const uint32_t* __restrict
     if (f) {
         Seg sg;
         sg.res = hot_list[t];
-        sg.start = s;
+        sg.start = hb[t];
         sg.len = 0;
         sg.bin = 0;
         segs[pre + x - f] = sg;
     }
-    if (t == 0) { out[0] = all; out[1] = tot; }
+    if (t == 0) out[0] = all;
 }
 
 // The next batch's hot ids: the segments of this one with >= min_len events (at most HOT_MAX, first come); the
@@ -864,19 +972,27 @@ hipError_t launch_grp_first(const sg_event* ev, uint64_t n, uint32_t max_res, ui
                        ckeys, cvals, ccnt, chist);
     return hipGetLastError();
 }
-hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
-                              int32_t max_rt, const uint32_t* words, const uint32_t* hot_off, uint32_t nblocks,
-                              uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev, uint32_t* nprev,
-                              uint32_t* bst, uint32_t* bflags, const uint32_t* comp, const sg_event_ext* ext,
-                              const sg_arg* args, uint32_t max_ctx, hipStream_t st) {
-    hipLaunchKernelGGL(k_grp_records, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, ev, n, max_res, gbase,
-                       ring_mask, max_rt, words, hot_off, nblocks, pos_of, recs, svals, prev, nprev, bst, bflags, comp,
-                       ext, args, max_ctx);
+hipError_t launch_hot_scan(uint32_t* C, uint32_t nblocks, uint32_t nhot, uint32_t* part, uint32_t* hb, uint32_t* total,
+                           hipStream_t st) {
+    if (!nhot) return hipMemsetAsync(total, 0, 4, st);
+    const uint32_t nch = (nblocks + HS_TC - 1) / HS_TC;
+    hipLaunchKernelGGL(k_hot_scan_a, dim3(nch), dim3(256), 0, st, C, nblocks, nhot, part);
+    hipLaunchKernelGGL(k_hot_scan_b, dim3(1), dim3(HOT_MAX), 0, st, part, nch, nhot, hb, total);
+    hipLaunchKernelGGL(k_hot_scan_c, dim3(nch), dim3(256), 0, st, C, nblocks, nhot, part, hb);
     return hipGetLastError();
 }
-hipError_t launch_hot_segs(const uint32_t* hot_off, uint32_t nhot, uint32_t nblocks, const uint32_t* hot_total,
-                           const uint32_t* hot_list, Seg* segs, uint32_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_hot_segs, dim3(1), dim3(HOT_MAX), 0, st, hot_off, nhot, nblocks, hot_total, hot_list, segs, out);
+hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
+                              const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
+                              const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
+                              uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
+                              const sg_arg* args, uint32_t max_ctx, hipStream_t st) {
+    hipLaunchKernelGGL(k_grp_records, dim3(nblocks), dim3(GR_THREADS), 0, st, ev, n, gbase, ring_mask, max_rt, words, P,
+                       nhot, nblocks, hb, pos_of, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx);
+    return hipGetLastError();
+}
+hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_hot_segs, dim3(1), dim3(HOT_MAX), 0, st, hb, nhot, hot_list, segs, out);
     return hipGetLastError();
 }
 hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
