@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
                                                     uint32_t epoch, uint32_t* __restrict__ bflags,
                                                     const uint32_t* __restrict__ lo) {
     const uint32_t kmin = lo ? *lo : 0u;
+    if ((uint64_t)(blockIdx.x + 1) * 1024 <= kmin) return;  // (the hot region: k_grp_records)
     __shared__ uint32_t wsum[4];
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
     uint32_t v = 0;
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
-        if (p < n) {
+        if (p < n && p >= kmin) {
             const uint4 w = reinterpret_cast<const uint4*>(recs)[p];
             SEv r;
             __builtin_memcpy(&r, &w, sizeof(r));

@@ -52,7 +52,7 @@ hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, ui
                               const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
                               const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
                               uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
-                              const sg_arg* args, uint32_t max_ctx, hipStream_t st);
+                              const sg_arg* args, uint32_t max_ctx, Link* link, uint32_t epoch, hipStream_t st);
 hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,
                            hipStream_t st);
 hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
@@ -2268,7 +2268,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(hipMemsetAsync(e->d_bst, 0, ((n + 1023) / 1024) * 4, gs));
         HIPCHK(launch_grp_records(dev_ev, n, e->gbase, ring_mask, e->cfg.statistic_max_rt, words, hot_off, nhot, nblocks,
                                   e->d_hot_hb, e->d_posof, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst,
-                                  e->d_bsmall + 0, dev_ext, dev_args, SG_MAX_CONTEXTS, gs));
+                                  e->d_bsmall + 0, dev_ext, dev_args, SG_MAX_CONTEXTS, e->d_link, e->epoch, gs));
         HIPCHK(launch_block_sums(e->d_recs, n, e->d_bst, e->d_link, e->epoch, e->d_bsmall + 0, kin, e->d_bsmall + 77, gs));
     }
     // bins + bin-ordered dispatch list (per-block counts -> scan -> placement), sized by an upper bound of

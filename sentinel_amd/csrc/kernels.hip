@@ -425,7 +425,8 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                                                             uint32_t* __restrict__ nprev, uint32_t* __restrict__ bst,
                                                             uint32_t* __restrict__ bflags,
                                                             const sg_event_ext* __restrict__ ext,
-                                                            const sg_arg* __restrict__ args, uint32_t max_ctx) {
+                                                            const sg_arg* __restrict__ args, uint32_t max_ctx,
+                                                            Link* __restrict__ link, uint32_t epoch) {
     __shared__ uint4 srec[RS_TILE];          // the tile's hot records in (hot id, rank) order
     __shared__ uint32_t spos[RS_TILE], sval[RS_TILE];
     __shared__ uint32_t lo[HOT_MAX];         // the tile's run of id h starts at local slot lo[h] (then its position)
@@ -554,13 +555,46 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
     if (__ballot(bad) && l == 0) atomicOr(bflags, BF_BAD_REF);
     if (__ballot(zero) && l == 0) atomicOr(bflags, BF_ZERO_CNT);
     __syncthreads();
-    // the hot runs leave in slot order: consecutive slots of one id are consecutive positions
+    // the hot runs leave in slot order: consecutive slots of one id are consecutive positions.  On the way, the
+    // sorted-order side tables of the hot region (k_block_sums does the cold one): each 1024-position block's ENTRY
+    // count sum (a segmented wave sum over equal blocks: a run's positions are consecutive) and the forward link of
+    // every referenced ENTRY (an EXIT run names an earlier tile's run of ENTRYs: nearby link slots).
     const uint32_t nh = nh_tile;
-    for (uint32_t k = t; k < nh; k += GR_THREADS) {
-        const uint32_t q = spos[k];
-        reinterpret_cast<uint4*>(recs)[q] = srec[k];
-        svals[q] = sval[k];
+    bool multi = false;
+    for (uint32_t k0 = 0; k0 < nh; k0 += GR_THREADS) {  // (wave-uniform trip count)
+        const uint32_t k = k0 + t;
+        uint32_t key = 0xFFFFFFFFu, v = 0;
+        if (k < nh) {
+            const uint32_t q = spos[k];
+            const uint4 rv = srec[k];
+            reinterpret_cast<uint4*>(recs)[q] = rv;
+            svals[q] = sval[k];
+            key = q >> 10;
+            const uint32_t kind = rv.w & 0xFFu, code = (rv.w >> 16) & 0xFFu;
+            if (kind == SG_EV_ENTRY) v = rv.z & 0xFFFFu;
+            else if (code == RC_BATCH) {
+                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
+                    kind == SG_EV_EXIT ? &link[rv.y].exit_l : &link[rv.y].trace_l);
+                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | q);
+                if ((uint32_t)(old >> 32) == epoch) multi = true;
+            }
+        }
+        // segmented inclusive sum over runs of equal blocks; the last lane of each run adds it
+        const uint32_t kp = __shfl_up(key, 1, 64), kn = __shfl_down(key, 1, 64);
+        bool f = l == 0 || kp != key;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            const bool g = __shfl_up(f ? 1 : 0, o, 64) != 0;
+            if ((int)l >= o) {
+                if (!f) x += y;
+                f = f || g;
+            }
+        }
+        if ((l == 63 || kn != key) && key != 0xFFFFFFFFu && x) atomicAdd(&bst[key], x);
     }
+    if (__ballot(multi) && l == 0) atomicOr(bflags, BF_MULTI_LINK);
 }
 
 // The hot ids' segments (hot id order, the non-empty ones) from their bases and totals (hb): segs[0 .. k),
@@ -985,9 +1019,9 @@ hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, ui
                               const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
                               const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
                               uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
-                              const sg_arg* args, uint32_t max_ctx, hipStream_t st) {
+                              const sg_arg* args, uint32_t max_ctx, Link* link, uint32_t epoch, hipStream_t st) {
     hipLaunchKernelGGL(k_grp_records, dim3(nblocks), dim3(GR_THREADS), 0, st, ev, n, gbase, ring_mask, max_rt, words, P,
-                       nhot, nblocks, hb, pos_of, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx);
+                       nhot, nblocks, hb, pos_of, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx, link, epoch);
     return hipGetLastError();
 }
 hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,
