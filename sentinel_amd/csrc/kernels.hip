@@ -429,12 +429,22 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                                                             Link* __restrict__ link, uint32_t epoch) {
     __shared__ uint4 srec[RS_TILE];          // the tile's hot records in (hot id, rank) order
     __shared__ uint32_t spos[RS_TILE], sval[RS_TILE];
-    __shared__ uint32_t lo[HOT_MAX];         // the tile's run of id h starts at local slot lo[h] (then its position)
+    __shared__ uint32_t lo[HOT_MAX];         // the tile's run of id h starts at local slot lo[h]
+    __shared__ uint32_t prow[HOT_MAX];       // ... and at sorted position prow[h]
     __shared__ uint32_t ws[GR_THREADS / 64];
     __shared__ uint32_t nh_tile;
     const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * RS_TILE;
+    // the tile's events and words first (their loads in flight across the setup below)
+    sg_event e[GR_ITEMS];
+    uint32_t wd[GR_ITEMS];
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * GR_THREADS + t;
+        if (i < n) { e[it] = ev[i]; wd[it] = words[i]; }
+        else { e[it].kind = 0xFF; wd[it] = 0; }
+    }
     // the tile's run lengths per hot id (next row, or the id's end for the last tile), their local offsets
     {
         uint32_t c = 0;
@@ -442,6 +452,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             const uint32_t p0 = P[(uint64_t)tile * nhot + t];
             const uint32_t p1 = tile + 1 < nblocks ? P[(uint64_t)(tile + 1) * nhot + t] : hb[t] + hb[HOT_MAX + t];
             c = p1 - p0;
+            prow[t] = p0;
         }
         uint32_t x = c;
 #pragma unroll
@@ -458,31 +469,61 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
     }
     __syncthreads();
     const int64_t t0 = ev[0].ts;
+    // stage 2: every item's own position (hot: its run's start in LDS; cold: pos_of) and its reference's word,
+    // all loads issued before any is used (each item's chain is a few dependent cache lines: overlap them)
+    uint32_t p[GR_ITEMS], wj[GR_ITEMS];
+    uint64_t jj[GR_ITEMS];
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint64_t i = base + (uint64_t)it * GR_THREADS + t;
+        jj[it] = ~0ull;
+        wj[it] = 0;
+        p[it] = 0;
+        if (i >= n) continue;
+        if (!(wd[it] & W_HOT)) p[it] = pos_of[i] & 0x7FFFFFFFu;
+        if (e[it].kind != SG_EV_ENTRY) {
+            const uint64_t ref = e[it].aux & SG_REF_NONE;
+            if (ref != SG_REF_NONE && ref >= gbase && ref - gbase < i) {  // (k_grp_first flagged the others)
+                jj[it] = ref - gbase;
+                wj[it] = words[ref - gbase];
+            }
+        }
+    }
+    // stage 3: the referenced ENTRYs' positions
+    uint32_t pj[GR_ITEMS];
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        pj[it] = 0;
+        if (jj[it] == ~0ull) continue;
+        if (wj[it] & W_HOT) pj[it] = P[(jj[it] / RS_TILE) * nhot + ((wj[it] >> 12) & (HOT_MAX - 1))] + (wj[it] & 0xFFFu);
+        else pj[it] = pos_of[jj[it]];  // (bit 31: an ENTRY)
+    }
+    // stage 4: the records
     bool bad = false, zero = false;
 #pragma unroll
     for (int it = 0; it < GR_ITEMS; ++it) {
         const uint64_t i = base + (uint64_t)it * GR_THREADS + t;
         bool is_prev = false;
-        uint32_t p = 0;
+        uint32_t q = 0;
         if (i < n) {
-            const sg_event e = ev[i];
-            const uint32_t wd = words[i];
-            const bool hot = (wd & W_HOT) != 0;
-            const bool entry = e.kind == SG_EV_ENTRY;
-            const uint32_t hid = (wd >> 12) & (HOT_MAX - 1);
-            p = hot ? P[(uint64_t)tile * nhot + hid] + (wd & 0xFFFu) : (pos_of[i] & 0x7FFFFFFFu);
+            const sg_event& ee = e[it];
+            const uint32_t w = wd[it];
+            const bool hot = (w & W_HOT) != 0;
+            const bool entry = ee.kind == SG_EV_ENTRY;
+            const uint32_t hid = (w >> 12) & (HOT_MAX - 1);
+            q = hot ? prow[hid] + (w & 0xFFFu) : p[it];
             SEv r;
-            r.dt = (int32_t)(e.ts - t0);
+            r.dt = (int32_t)(ee.ts - t0);
             r.x = 0;
-            r.cnt = e.count;
+            r.cnt = ee.count;
             r.rt = 0;
-            r.kind = e.kind;
-            r.flags = (uint8_t)(e.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
+            r.kind = ee.kind;
+            r.flags = (uint8_t)(ee.flags & 0x3Fu);  // the ABI's SG_F_* bits only (RF_* are internal)
             r.code = RC_NONE;
             r.pad = 0;
             uint32_t tag = 0;
             bool own_args = false;
-            uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+            uint64_t key0 = (ee.flags & SG_F_HAS_ARG) ? ee.aux : NO_KEY;
             if (ext) {
                 const sg_event_ext x = ext[i];
                 if (x.n_args && x.n_args <= SG_MAX_ARGS) {
@@ -495,51 +536,45 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             }
             if (own_args) {
                 r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
-                if (e.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
+                if (ee.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
             }
             r.x = tag;
             if (entry) {
-                zero |= e.count == 0;
+                zero |= ee.count == 0;
             } else {
-                if (e.kind == SG_EV_EXIT) {
-                    const int64_t raw = (int64_t)(e.aux >> 48);
+                if (ee.kind == SG_EV_EXIT) {
+                    const int64_t raw = (int64_t)(ee.aux >> 48);
                     r.rt = (uint16_t)(raw > max_rt ? max_rt : raw);
                 }
-                const uint64_t ref = e.aux & SG_REF_NONE;
-                if (ref != SG_REF_NONE) {
-                    if (ref >= gbase) {
-                        const uint64_t j = ref - gbase;
-                        if (j < i) {  // (k_grp_first flagged the others)
-                            const uint32_t wj = words[j];
-                            bool ej;
-                            const uint32_t pj = grp_pos(j, wj, P, nhot, pos_of, ej);
-                            if (ej) {
-                                // one hot and one cold, or two hot ids: not the same resource (two cold: k_block_sums)
-                                if (((wj ^ wd) & W_HOT) || (hot && ((wj >> 12) & (HOT_MAX - 1)) != hid)) bad = true;
-                                r.code = RC_BATCH;
-                                r.x = pj;
-                            } else {
-                                r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
-                            }
-                        }
-                    } else {  // an ENTRY of an earlier batch: its status is read from the ring by k_resolve
-                        r.code = RC_PREV;
-                        r.x = (uint32_t)(ref & ring_mask);
-                        is_prev = true;
+                const uint64_t ref = ee.aux & SG_REF_NONE;
+                if (jj[it] != ~0ull) {
+                    const bool ej = (wj[it] & W_HOT) ? (wj[it] & W_ENT) != 0 : (pj[it] & 0x80000000u) != 0;
+                    if (ej) {
+                        // one hot and one cold, or two hot ids: not the same resource (two cold: k_block_sums)
+                        if (((wj[it] ^ w) & W_HOT) || (hot && ((wj[it] >> 12) & (HOT_MAX - 1)) != hid)) bad = true;
+                        r.code = RC_BATCH;
+                        r.x = pj[it] & 0x7FFFFFFFu;
+                    } else {
+                        r.code = ee.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
                     }
+                } else if (ref != SG_REF_NONE && ref < gbase) {
+                    // an ENTRY of an earlier batch: its status is read from the ring by k_resolve
+                    r.code = RC_PREV;
+                    r.x = (uint32_t)(ref & ring_mask);
+                    is_prev = true;
                 }
-                if (r.code == RC_NONE || r.code == RC_PREV) atomicOr(&bst[p >> 10], BST_STATIC);
+                if (r.code == RC_NONE || r.code == RC_PREV) atomicOr(&bst[q >> 10], BST_STATIC);
             }
             uint4 rv;
             __builtin_memcpy(&rv, &r, sizeof(rv));
             if (hot) {
-                const uint32_t slot = lo[hid] + (wd & 0xFFFu);
+                const uint32_t slot = lo[hid] + (w & 0xFFFu);
                 srec[slot] = rv;
-                spos[slot] = p;
+                spos[slot] = q;
                 sval[slot] = (uint32_t)i | (entry ? 0x80000000u : 0u);
-                pos_of[i] = p | (entry ? 0x80000000u : 0u);
+                pos_of[i] = q | (entry ? 0x80000000u : 0u);
             } else {
-                reinterpret_cast<uint4*>(recs)[p] = rv;
+                reinterpret_cast<uint4*>(recs)[q] = rv;
             }
         }
         // wave-aggregated prev-list slots
@@ -549,7 +584,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             uint32_t b0 = 0;
             if ((int)l == lead) b0 = atomicAdd(nprev, (uint32_t)__popcll(pb));
             b0 = __shfl(b0, lead, 64);
-            if (is_prev) prev[b0 + __popcll(pb & ((1ull << l) - 1))] = p;
+            if (is_prev) prev[b0 + __popcll(pb & ((1ull << l) - 1))] = q;
         }
     }
     if (__ballot(bad) && l == 0) atomicOr(bflags, BF_BAD_REF);
