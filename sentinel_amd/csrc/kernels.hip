@@ -405,16 +405,18 @@ __device__ __forceinline__ uint32_t grp_pos(uint64_t j, uint32_t wd, const uint3
     return po & 0x7FFFFFFFu;
 }
 
-// Every event's 16-byte record at its sorted position: a workgroup of 1024 lanes per 4096-event tile (4 events a
-// lane, in submission order).  The tile's hot runs are staged in LDS in (hot id, rank) order and leave as runs of
-// consecutive positions (records and sorted values); a cold event's record goes straight to its position (the cold
-// sort placed it).  References to ENTRYs of this batch become the ENTRY's sorted position: an EXIT sits ~RT of
-// traffic after its ENTRY, so the ENTRY's word and position are recent lines.  A reference must name an earlier ENTRY
-// of the same resource: two hot events by their ids here, two cold ones by their sort keys in k_block_sums (sorted
-// order); one naming a non-ENTRY resolves like an unknown entry.  References into earlier batches are listed (prev)
-// for k_resolve.
-#define GR_THREADS 1024
-#define GR_ITEMS (RS_TILE / GR_THREADS)
+// Every event's 16-byte record at its sorted position: a workgroup of 256 lanes per quarter of a 4096-event tile
+// (4 events a lane, in submission order; four workgroups a CU).  The quarter's hot events are staged in LDS in
+// (hot id, rank) order -- a quarter's events of one id hold consecutive ranks of the tile's run, r0 .. r0 + c -- and
+// leave as runs of consecutive positions (records and sorted values); a cold event's record goes straight to its
+// position (the cold sort placed it).  References to ENTRYs of this batch become the ENTRY's sorted position: an
+// EXIT sits ~RT of traffic after its ENTRY, so the ENTRY's word and position are recent lines.  A reference must
+// name an earlier ENTRY of the same resource: two hot events by their ids here, two cold ones by their sort keys in
+// k_block_sums (sorted order); one naming a non-ENTRY resolves like an unknown entry.  References into earlier
+// batches are listed (prev) for k_resolve.
+#define GR_THREADS 256
+#define GR_EVENTS (RS_TILE / 4)
+#define GR_ITEMS (GR_EVENTS / GR_THREADS)
 __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __restrict__ ev, uint64_t n,
                                                             uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
                                                             const uint32_t* __restrict__ words,
@@ -427,16 +429,17 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                                                             const sg_event_ext* __restrict__ ext,
                                                             const sg_arg* __restrict__ args, uint32_t max_ctx,
                                                             Link* __restrict__ link, uint32_t epoch) {
-    __shared__ uint4 srec[RS_TILE];          // the tile's hot records in (hot id, rank) order
-    __shared__ uint32_t spos[RS_TILE], sval[RS_TILE];
-    __shared__ uint32_t lo[HOT_MAX];         // the tile's run of id h starts at local slot lo[h]
-    __shared__ uint32_t prow[HOT_MAX];       // ... and at sorted position prow[h]
+    __shared__ uint4 srec[GR_EVENTS];        // the quarter's hot records in (hot id, rank) order
+    __shared__ uint32_t spos[GR_EVENTS], sval[GR_EVENTS];
+    __shared__ uint32_t lo[HOT_MAX];         // per hot id: the quarter's count, then its first local slot
+    __shared__ uint32_t r0[HOT_MAX];         // ... its first rank in the tile's run
+    __shared__ uint32_t prow[HOT_MAX];       // ... the tile's run's first sorted position
     __shared__ uint32_t ws[GR_THREADS / 64];
-    __shared__ uint32_t nh_tile;
+    __shared__ uint32_t nh_q;
     const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
-    const uint32_t tile = blockIdx.x;
-    const uint64_t base = (uint64_t)tile * RS_TILE;
-    // the tile's events and words first (their loads in flight across the setup below)
+    const uint32_t tile = blockIdx.x >> 2;
+    const uint64_t base = (uint64_t)tile * RS_TILE + (uint64_t)(blockIdx.x & 3) * GR_EVENTS;
+    // the quarter's events and words first (their loads in flight across the setup below)
     sg_event e[GR_ITEMS];
     uint32_t wd[GR_ITEMS];
 #pragma unroll
@@ -445,16 +448,30 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         if (i < n) { e[it] = ev[i]; wd[it] = words[i]; }
         else { e[it].kind = 0xFF; wd[it] = 0; }
     }
-    // the tile's run lengths per hot id (next row, or the id's end for the last tile), their local offsets
-    {
-        uint32_t c = 0;
-        if (t < nhot) {
-            const uint32_t p0 = P[(uint64_t)tile * nhot + t];
-            const uint32_t p1 = tile + 1 < nblocks ? P[(uint64_t)(tile + 1) * nhot + t] : hb[t] + hb[HOT_MAX + t];
-            c = p1 - p0;
-            prow[t] = p0;
+    for (uint32_t h = t; h < nhot; h += GR_THREADS) {
+        lo[h] = 0;
+        r0[h] = 0xFFFFFFFFu;
+        prow[h] = P[(uint64_t)tile * nhot + h];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it)
+        if (wd[it] & W_HOT) {
+            const uint32_t h = (wd[it] >> 12) & (HOT_MAX - 1);
+            atomicAdd(&lo[h], 1u);
+            atomicMin(&r0[h], wd[it] & 0xFFFu);
         }
-        uint32_t x = c;
+    __syncthreads();
+    {   // local slots: exclusive scan of the counts over the ids (4 ids a lane)
+        constexpr uint32_t PER = HOT_MAX / GR_THREADS;
+        uint32_t c[PER], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t h = t * PER + k;
+            c[k] = h < nhot ? lo[h] : 0u;
+            sum += c[k];
+        }
+        uint32_t x = sum;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
@@ -464,13 +481,19 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         __syncthreads();
         uint32_t pre = 0, all = 0;
         for (uint32_t k = 0; k < GR_THREADS / 64; ++k) { if (k < wv) pre += ws[k]; all += ws[k]; }
-        if (t < nhot) lo[t] = pre + x - c;
-        if (t == 0) nh_tile = all;
+        uint32_t run = pre + x - sum;
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t h = t * PER + k;
+            if (h < nhot) lo[h] = run;
+            run += c[k];
+        }
+        if (t == 0) nh_q = all;
     }
     __syncthreads();
     const int64_t t0 = ev[0].ts;
-    // stage 2: every item's own position (hot: its run's start in LDS; cold: pos_of) and its reference's word,
-    // all loads issued before any is used (each item's chain is a few dependent cache lines: overlap them)
+    // every item's own position (hot: its run's start in LDS; cold: pos_of) and its reference's word, all loads
+    // issued before any is used (each item's chain is a few dependent cache lines: overlap them)
     uint32_t p[GR_ITEMS], wj[GR_ITEMS];
     uint64_t jj[GR_ITEMS];
 #pragma unroll
@@ -489,7 +512,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             }
         }
     }
-    // stage 3: the referenced ENTRYs' positions
+    // the referenced ENTRYs' positions
     uint32_t pj[GR_ITEMS];
 #pragma unroll
     for (int it = 0; it < GR_ITEMS; ++it) {
@@ -498,7 +521,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         if (wj[it] & W_HOT) pj[it] = P[(jj[it] / RS_TILE) * nhot + ((wj[it] >> 12) & (HOT_MAX - 1))] + (wj[it] & 0xFFFu);
         else pj[it] = pos_of[jj[it]];  // (bit 31: an ENTRY)
     }
-    // stage 4: the records
+    // the records
     bool bad = false, zero = false;
 #pragma unroll
     for (int it = 0; it < GR_ITEMS; ++it) {
@@ -568,7 +591,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             uint4 rv;
             __builtin_memcpy(&rv, &r, sizeof(rv));
             if (hot) {
-                const uint32_t slot = lo[hid] + (w & 0xFFFu);
+                const uint32_t slot = lo[hid] + (w & 0xFFFu) - r0[hid];
                 srec[slot] = rv;
                 spos[slot] = q;
                 sval[slot] = (uint32_t)i | (entry ? 0x80000000u : 0u);
@@ -594,7 +617,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
     // sorted-order side tables of the hot region (k_block_sums does the cold one): each 1024-position block's ENTRY
     // count sum (a segmented wave sum over equal blocks: a run's positions are consecutive) and the forward link of
     // every referenced ENTRY (an EXIT run names an earlier tile's run of ENTRYs: nearby link slots).
-    const uint32_t nh = nh_tile;
+    const uint32_t nh = nh_q;
     bool multi = false;
     for (uint32_t k0 = 0; k0 < nh; k0 += GR_THREADS) {  // (wave-uniform trip count)
         const uint32_t k = k0 + t;
@@ -1055,7 +1078,7 @@ hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, ui
                               const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
                               uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
                               const sg_arg* args, uint32_t max_ctx, Link* link, uint32_t epoch, hipStream_t st) {
-    hipLaunchKernelGGL(k_grp_records, dim3(nblocks), dim3(GR_THREADS), 0, st, ev, n, gbase, ring_mask, max_rt, words, P,
+    hipLaunchKernelGGL(k_grp_records, dim3(nblocks * 4), dim3(GR_THREADS), 0, st, ev, n, gbase, ring_mask, max_rt, words, P,
                        nhot, nblocks, hb, pos_of, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx, link, epoch);
     return hipGetLastError();
 }
