@@ -1375,6 +1375,16 @@ extern "C" int sgx_param_pool(sg_engine* e, unsigned long long* out) {
     return 0;
 }
 
+static int compact_pmaps(sg_engine* e);
+// diagnostics export: compact the param map pool now, between batches (tests run the compaction at full size)
+extern "C" int sgx_param_compact(sg_engine* e) {
+    if (!e || drain(e) != SG_OK) return -1;
+    if (!e->pool_nb) return 0;
+    if (compact_pmaps(e) != SG_OK) return -1;
+    ++e->n_compact;
+    return 0;
+}
+
 static void free_pv(sg_engine* e);
 
 int sg_engine_destroy(sg_engine* e) {

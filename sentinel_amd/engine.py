@@ -257,6 +257,15 @@ class Engine:
         return {"buckets": int(out[0]), "taken": int(out[1]), "floor": int(out[2]), "compactions": int(out[3]),
                 "device_compactions": int(out[4])}
 
+    def param_compact(self):
+        """Compact the param map pool now, between batches (diagnostics export sgx_param_compact: the same
+        on-device compaction a submit runs once growth took half of the free pool)."""
+        fn = lib().sgx_param_compact
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p]
+        if fn(self.h) != 0:
+            raise SentinelError(A.SG_EDEVICE, "sgx_param_compact failed")
+
     def param_thread_count(self, res: int, idx: int, key: int, with_presence: bool = False):
         """ParameterMetric.getThreadCount (sg_param_thread_count): the value's count in the thread-count map of
         paramIdx idx, 0 if absent; with_presence: (count, present).  Does not reorder the map's LRU."""
