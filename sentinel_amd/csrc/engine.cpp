@@ -50,7 +50,7 @@ hipError_t launch_hot_scan(uint32_t* C, uint32_t nblocks, uint32_t nhot, uint32_
                            hipStream_t st);
 hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
                               const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
-                              const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
+                              const uint32_t* hb, SEv* recs, uint32_t* svals, uint32_t* prev,
                               uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
                               const sg_arg* args, uint32_t max_ctx, Link* link, uint32_t epoch, hipStream_t st);
 hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,
@@ -138,6 +138,8 @@ hipError_t launch_fill(const Span* spans, const uint32_t* nspan, uint32_t cap, c
                        const DRule* rules, uint32_t* dec, hipStream_t st);
 hipError_t launch_resolve(const uint32_t* prev, uint32_t np, const uint8_t* ring, SEv* recs, const uint32_t* vals,
                           const sg_event_ext* ext, hipStream_t st);
+hipError_t launch_post_w(const uint32_t* words, const uint32_t* P, uint32_t nhot, const uint32_t* dec, uint64_t n,
+                         uint64_t gbase, uint8_t* ring, uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, uint64_t gbase, uint8_t* ring,
                        uint64_t ring_mask, uint32_t* out, hipStream_t st);
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
@@ -551,6 +553,8 @@ struct sg_engine {
         uint32_t *d_posof = nullptr, *d_dec = nullptr, *d_blkcnt = nullptr, *d_prev = nullptr;
         SEv *d_recs = nullptr, *d_rec_o = nullptr;
         uint32_t* d_ccnt = nullptr;    // hot / cold group stage: per-tile cold counts, the cold segments' tile scratch
+        bool radix = false;            // this batch took the radix group stage (d_posof), else the hot / cold one
+        uint32_t nhot = 0;             // ... with these hot ids (its words and P in d_flag / d_pos)
         Seg* d_segs = nullptr;
         uint64_t* d_cand = nullptr;
         uint32_t* d_bsmall = nullptr;  // [0] bflags [1] nseg [2] ncand [3] nprev [4..5] t0 [8..8+N_BINS] bin offsets
@@ -739,7 +743,7 @@ int ensure_batch(sg_engine* e, uint64_t n) {
         HIPCHK(hipMalloc(&B.d_posof, c * 4));
         HIPCHK(hipMalloc(&B.d_dec, c * 4));
         HIPCHK(hipMalloc(&B.d_recs, c * sizeof(SEv)));
-        if (e->radix_group) HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));  // (the hot / cold stage has none)
+        if (e->radix_group || c >= (1ull << 30)) HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));  // (radix stage only)
         HIPCHK(hipMalloc(&B.d_ccnt, 3 * (nblocks + 64) * 4));
     }
     dfree(e->d_hot_part);
@@ -2233,7 +2237,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     int64_t* d_t0 = reinterpret_cast<int64_t*>(e->d_bsmall + 4);  // [4..5]
     uint32_t *kin = e->d_k1, *vin = e->d_v1, *kout = e->d_k0, *vout = e->d_v0;
     if (++e->epoch == 0) e->epoch = 1;
-    if (e->radix_group) {  // every event through the radix passes (SG_DEBUG_FLAGS & 8192; A/B of the group stage)
+    // every event through the radix passes: SG_DEBUG_FLAGS & 8192 (A/B of the group stage), or a batch of 2^30 events
+    // or more (the hot / cold stage's words hold a position in 30 bits)
+    B.radix = e->radix_group || n >= (1ull << 30);
+    if (B.radix) {
         HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o,
                                e->d_k1, e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,
                                e->d_comp, dev_ext, dev_args, n_args, SG_MAX_CONTEXTS, gs));
@@ -2252,7 +2259,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         // ---- hot / cold group stage (kernels.hip k_grp_*): [77] hot_total (the cold region's start), [78] cold
         // events, [80] hot segments, [81] (hot_total again), [82] cold segments, [76] the next batch's hot ids
         const uint32_t nhot = e->nhot;
-        uint32_t* words = e->d_flag;    // per event: W_HOT | hot id << 12 | rank in its tile's hot id, else 0
+        B.nhot = nhot;
+        uint32_t* words = e->d_flag;    // per event: W_HOT | W_ENT? | hot id << 12 | rank in its tile's run of the id;
+                                        // cold: W_ENT? | sorted position (the last cold pass)
         uint32_t* hot_off = e->d_pos;   // [hot id][tile] counts, scanned in place: the runs' sorted positions
         uint32_t* ccnt = B.d_ccnt;      // per tile: cold events (compacted at the tile's start in k1 / v1)
         HIPCHK(launch_grp_first(dev_ev, n, R, e->gbase, ring_mask, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,
@@ -2266,7 +2275,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
             const bool last = p == passes - 1;
             HIPCHK(launch_radix_scatter_x(kin, vin, n, p ? e->d_bsmall + 78 : nullptr, p ? nullptr : ccnt,
                                           last ? e->d_bsmall + 77 : nullptr, p * db, e->d_hist, nblocks, kout, vout,
-                                          last ? e->d_posof : nullptr, gs));
+                                          last ? words : nullptr, gs));
             std::swap(kin, kout);
             std::swap(vin, vout);
         }
@@ -2277,7 +2286,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                                launch_scan, e->d_part, e->d_bsmall + 82, e->d_bsmall + 1));
         HIPCHK(hipMemsetAsync(e->d_bst, 0, ((n + 1023) / 1024) * 4, gs));
         HIPCHK(launch_grp_records(dev_ev, n, e->gbase, ring_mask, e->cfg.statistic_max_rt, words, hot_off, nhot, nblocks,
-                                  e->d_hot_hb, e->d_posof, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst,
+                                  e->d_hot_hb, e->d_recs, vin, e->d_prev, e->d_bsmall + 3, e->d_bst,
                                   e->d_bsmall + 0, dev_ext, dev_args, SG_MAX_CONTEXTS, e->d_link, e->epoch, gs));
         HIPCHK(launch_block_sums(e->d_recs, n, e->d_bst, e->d_link, e->epoch, e->d_bsmall + 0, kin, e->d_bsmall + 77, gs));
     }
@@ -2312,7 +2321,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // the next batch's hot ids: this batch's resources of >= n / 8192 events (about one per 4096-event tile, so
     // that a tile's run of one hot id is more than a random write), at least 64
     const uint32_t hot_min = (uint32_t)std::max<uint64_t>(64, n / 8192);
-    if (!e->radix_group)
+    if (!B.radix)
         HIPCHK(launch_hot_build(e->d_segs, e->d_bsmall + 1, mb, hot_min, R, e->d_hot_tab, e->d_hot_list, e->nhot,
                                 e->d_bsmall + 76, gs));
     // [0] bflags [1] nseg [3] nprev [4..5] t0 [6..7] XF_MIX lists [8..8+N_BINS] bin offsets [72] wide XF_MIX events
@@ -2322,7 +2331,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     HIPCHK(hipMemcpyAsync(head, e->d_bsmall, sizeof(head), hipMemcpyDeviceToHost, gs));
     HIPCHK(hipEventRecord(B.ev[1], gs));
     HIPCHK(hipStreamSynchronize(gs));
-    if (!e->radix_group) e->nhot = std::min<uint32_t>(head[76], hot_max());
+    if (!B.radix) e->nhot = std::min<uint32_t>(head[76], hot_max());
     const uint32_t m = head[1];
     const uint32_t nprev = head[3];
     int64_t t0 = 0;
@@ -2561,7 +2570,8 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                           st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
-    HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
+    if (B.radix) HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
+    else HIPCHK(launch_post_w(e->d_flag, e->d_pos, B.nhot, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
     if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(B.ev[4], st));
     B.pending = true;

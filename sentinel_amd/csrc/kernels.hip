@@ -197,7 +197,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_first(const sg_event* __restr
 #define HOT_MAX 1024u
 #define HOT_NONE 0xFFFFu
 #define W_HOT 0x80000000u   // word: a hot event (W_HOT | W_ENT? | hot id << 12 | rank in its tile's run)
-#define W_ENT 0x40000000u   // word: an ENTRY (hot or cold)
+#define W_ENT 0x40000000u   // word: an ENTRY (hot or cold); a cold event's word is W_ENT? | its sorted position
+#define W_POS 0x3FFFFFFFu   // (the last cold radix pass writes it: batches of < 2^30 events)
 
 template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __restrict__ ev, uint64_t n, uint32_t max_res,
@@ -393,16 +394,10 @@ __global__ __launch_bounds__(256) void k_hot_scan_c(uint32_t* __restrict__ C, ui
     }
 }
 
-// The sorted position of event j and whether it is an ENTRY (its word; cold: pos_of from the cold sort's last pass)
-__device__ __forceinline__ uint32_t grp_pos(uint64_t j, uint32_t wd, const uint32_t* __restrict__ P, uint32_t nhot,
-                                            const uint32_t* __restrict__ pos_of, bool& entry) {
-    if (wd & W_HOT) {
-        entry = (wd & W_ENT) != 0;
-        return P[(j / RS_TILE) * nhot + ((wd >> 12) & (HOT_MAX - 1))] + (wd & 0xFFFu);
-    }
-    const uint32_t po = pos_of[j];
-    entry = (po & 0x80000000u) != 0;
-    return po & 0x7FFFFFFFu;
+// The sorted position of event j from its word (hot: the tile's run start + rank; cold: the word itself)
+__device__ __forceinline__ uint32_t grp_pos(uint64_t j, uint32_t wd, const uint32_t* __restrict__ P, uint32_t nhot) {
+    if (wd & W_HOT) return P[(j / RS_TILE) * nhot + ((wd >> 12) & (HOT_MAX - 1))] + (wd & 0xFFFu);
+    return wd & W_POS;
 }
 
 // Every event's 16-byte record at its sorted position: a workgroup of 256 lanes per quarter of a 4096-event tile
@@ -422,7 +417,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                                                             const uint32_t* __restrict__ words,
                                                             const uint32_t* __restrict__ P, uint32_t nhot,
                                                             uint32_t nblocks, const uint32_t* __restrict__ hb,
-                                                            uint32_t* __restrict__ pos_of, SEv* __restrict__ recs,
+                                                            SEv* __restrict__ recs,
                                                             uint32_t* __restrict__ svals, uint32_t* __restrict__ prev,
                                                             uint32_t* __restrict__ nprev, uint32_t* __restrict__ bst,
                                                             uint32_t* __restrict__ bflags,
@@ -503,7 +498,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         wj[it] = 0;
         p[it] = 0;
         if (i >= n) continue;
-        if (!(wd[it] & W_HOT)) p[it] = pos_of[i] & 0x7FFFFFFFu;
+        if (!(wd[it] & W_HOT)) p[it] = wd[it] & W_POS;
         if (e[it].kind != SG_EV_ENTRY) {
             const uint64_t ref = e[it].aux & SG_REF_NONE;
             if (ref != SG_REF_NONE && ref >= gbase && ref - gbase < i) {  // (k_grp_first flagged the others)
@@ -515,12 +510,7 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
     // the referenced ENTRYs' positions
     uint32_t pj[GR_ITEMS];
 #pragma unroll
-    for (int it = 0; it < GR_ITEMS; ++it) {
-        pj[it] = 0;
-        if (jj[it] == ~0ull) continue;
-        if (wj[it] & W_HOT) pj[it] = P[(jj[it] / RS_TILE) * nhot + ((wj[it] >> 12) & (HOT_MAX - 1))] + (wj[it] & 0xFFFu);
-        else pj[it] = pos_of[jj[it]];  // (bit 31: an ENTRY)
-    }
+    for (int it = 0; it < GR_ITEMS; ++it) pj[it] = jj[it] == ~0ull ? 0u : grp_pos(jj[it], wj[it], P, nhot);
     // the records
     bool bad = false, zero = false;
 #pragma unroll
@@ -571,12 +561,11 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                 }
                 const uint64_t ref = ee.aux & SG_REF_NONE;
                 if (jj[it] != ~0ull) {
-                    const bool ej = (wj[it] & W_HOT) ? (wj[it] & W_ENT) != 0 : (pj[it] & 0x80000000u) != 0;
-                    if (ej) {
+                    if (wj[it] & W_ENT) {
                         // one hot and one cold, or two hot ids: not the same resource (two cold: k_block_sums)
                         if (((wj[it] ^ w) & W_HOT) || (hot && ((wj[it] >> 12) & (HOT_MAX - 1)) != hid)) bad = true;
                         r.code = RC_BATCH;
-                        r.x = pj[it] & 0x7FFFFFFFu;
+                        r.x = pj[it];
                     } else {
                         r.code = ee.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
                     }
@@ -595,7 +584,6 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
                 srec[slot] = rv;
                 spos[slot] = q;
                 sval[slot] = (uint32_t)i | (entry ? 0x80000000u : 0u);
-                pos_of[i] = q | (entry ? 0x80000000u : 0u);
             } else {
                 reinterpret_cast<uint4*>(recs)[q] = rv;
             }
@@ -653,6 +641,42 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         if ((l == 63 || kn != key) && key != 0xFFFFFFFFu && x) atomicAdd(&bst[key], x);
     }
     if (__ballot(multi) && l == 0) atomicOr(bflags, BF_MULTI_LINK);
+}
+
+// Decisions back to submission order from the words (the hot / cold stage's inverse permutation): only ENTRYs are
+// gathered (every other event's word is mk_dec(ST_NOT_ENTRY, 0, 0)); the status ring keeps every event's status
+// for references from later batches.  The hot positions read their tile's row of P (a few lines a tile).
+#define POSTW_ITEMS 4
+__global__ __launch_bounds__(256) void k_post_w(const uint32_t* __restrict__ words, const uint32_t* __restrict__ P,
+                                                uint32_t nhot, const uint32_t* __restrict__ dec, uint64_t n,
+                                                uint64_t gbase, uint8_t* __restrict__ ring, uint64_t ring_mask,
+                                                uint32_t* __restrict__ out) {
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * POSTW_ITEMS) + threadIdx.x;
+    uint32_t w[POSTW_ITEMS], d[POSTW_ITEMS];
+#pragma unroll
+    for (int k = 0; k < POSTW_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256;
+        w[k] = i < n ? words[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < POSTW_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256;
+        d[k] = (w[k] & W_ENT) ? dec[grp_pos(i, w[k], P, nhot)] : (uint32_t)ST_NOT_ENTRY;  // (= mk_dec(ST_NOT_ENTRY, 0, 0))
+    }
+#pragma unroll
+    for (int k = 0; k < POSTW_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * 256;
+        if (i < n) {
+            out[i] = d[k];
+            ring[(gbase + i) & ring_mask] = (uint8_t)(d[k] & 0xFF);
+        }
+    }
+}
+hipError_t launch_post_w(const uint32_t* words, const uint32_t* P, uint32_t nhot, const uint32_t* dec, uint64_t n,
+                         uint64_t gbase, uint8_t* ring, uint64_t ring_mask, uint32_t* out, hipStream_t st) {
+    const uint32_t nb = (uint32_t)((n + 256 * POSTW_ITEMS - 1) / (256 * POSTW_ITEMS));
+    hipLaunchKernelGGL(k_post_w, dim3(nb), dim3(256), 0, st, words, P, nhot, dec, n, gbase, ring, ring_mask, out);
+    return hipGetLastError();
 }
 
 // The hot ids' segments (hot id order, the non-empty ones) from their bases and totals (hb): segs[0 .. k),
@@ -741,7 +765,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
                                                            uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                            uint32_t* __restrict__ pos_of, const uint32_t* __restrict__ ndev,
                                                            const uint32_t* __restrict__ tcnt,
-                                                           const uint32_t* __restrict__ dbase) {
+                                                           const uint32_t* __restrict__ dbase, uint32_t wfmt) {
     constexpr int NB = 1 << DB;
     if (ndev && *ndev < n) n = *ndev;
     if ((uint64_t)blockIdx.x * RS_TILE >= n) return;  // (a tile past the device count: nothing to move)
@@ -831,7 +855,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint32_t* __
         const uint64_t dst = (uint64_t)(gdst[(k >> shift) & (NB - 1)] + (int64_t)p) + ob;
         keys_out[dst] = k;
         vals_out[dst] = v;
-        if (pos_of) pos_of[v & 0x7FFFFFFFu] = (uint32_t)dst | (v & 0x80000000u);
+        // the inverse permutation: pos_of[index] = position | ENTRY << 31, or (wfmt: the hot / cold stage's word of
+        // a cold event) position | ENTRY << 30 (W_ENT)
+        if (pos_of) pos_of[v & 0x7FFFFFFFu] = (uint32_t)dst | (wfmt ? (v >> 1) & 0x40000000u : (v & 0x80000000u));
     }
 }
 
@@ -1035,22 +1061,23 @@ hipError_t launch_radix_hist_n(const uint32_t* keys, uint64_t n, const uint32_t*
 hipError_t launch_radix_scatter_n(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev, int shift,
                                   const uint32_t* goff, uint32_t nblocks, uint32_t* kout, uint32_t* vout, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, (uint32_t*)nullptr, ndev, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+                       kout, vout, (uint32_t*)nullptr, ndev, (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u);
     return hipGetLastError();
 }
 hipError_t launch_radix_scatter(const uint32_t* kin, const uint32_t* vin, uint64_t n, int shift, const uint32_t* goff,
                                 uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, pos_of, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+                       kout, vout, pos_of, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u);
     return hipGetLastError();
 }
 // the cold passes of the hot / cold group stage: tcnt = per-tile counts (first pass), ndev = the cold count (later
-// passes), dbase = hot_total (last pass: sorted values and pos_of at their final positions)
+// passes), dbase = hot_total (last pass: sorted values at their final positions, and the cold events' words =
+// position | W_ENT into pos_of = the words array)
 hipError_t launch_radix_scatter_x(const uint32_t* kin, const uint32_t* vin, uint64_t n, const uint32_t* ndev,
                                   const uint32_t* tcnt, const uint32_t* dbase, int shift, const uint32_t* goff,
                                   uint32_t nblocks, uint32_t* kout, uint32_t* vout, uint32_t* pos_of, hipStream_t st) {
     hipLaunchKernelGGL(k_radix_scatter<8>, dim3(nblocks), dim3(RS_THREADS), 0, st, kin, vin, n, shift, goff, nblocks,
-                       kout, vout, pos_of, ndev, tcnt, dbase);
+                       kout, vout, pos_of, ndev, tcnt, dbase, 1u);
     return hipGetLastError();
 }
 hipError_t launch_grp_first(const sg_event* ev, uint64_t n, uint32_t max_res, uint64_t gbase, uint64_t ring_mask,
@@ -1075,11 +1102,11 @@ hipError_t launch_hot_scan(uint32_t* C, uint32_t nblocks, uint32_t nhot, uint32_
 }
 hipError_t launch_grp_records(const sg_event* ev, uint64_t n, uint64_t gbase, uint64_t ring_mask, int32_t max_rt,
                               const uint32_t* words, const uint32_t* P, uint32_t nhot, uint32_t nblocks,
-                              const uint32_t* hb, uint32_t* pos_of, SEv* recs, uint32_t* svals, uint32_t* prev,
+                              const uint32_t* hb, SEv* recs, uint32_t* svals, uint32_t* prev,
                               uint32_t* nprev, uint32_t* bst, uint32_t* bflags, const sg_event_ext* ext,
                               const sg_arg* args, uint32_t max_ctx, Link* link, uint32_t epoch, hipStream_t st) {
     hipLaunchKernelGGL(k_grp_records, dim3(nblocks * 4), dim3(GR_THREADS), 0, st, ev, n, gbase, ring_mask, max_rt, words, P,
-                       nhot, nblocks, hb, pos_of, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx, link, epoch);
+                       nhot, nblocks, hb, recs, svals, prev, nprev, bst, bflags, ext, args, max_ctx, link, epoch);
     return hipGetLastError();
 }
 hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* hot_list, Seg* segs, uint32_t* out,

@@ -8,8 +8,8 @@ are coalesced streams (STREAMING below); the reads of the random-access kernels 
 gathers) are uncalibrated and taken as counted.  Reads and writes are reported separately, and the
 all-doubled figure of earlier rounds is kept as traffic_upper_bytes_per_batch.
 Totals are summed over every dispatch of the run and divided by the number of batches (one
-k_rs_first dispatch per batch), so kernels launched several times per batch (radix passes, scans)
-count every launch.  The JSON is stamped with bench.src_sha() of the sources it was measured on;
+k_grp_first or k_rs_first dispatch per batch), so kernels launched several times per batch (radix passes, scans)
+count every launch (k_grp_first, the hot / cold group stage's first pass, or k_rs_first, the radix one).  The JSON is stamped with bench.src_sha() of the sources it was measured on;
 bench.py reports its traffic only when that stamp matches the sources it runs.
 """
 import csv
@@ -23,7 +23,7 @@ import bench  # noqa: E402
 
 DECIDE = ("k_jac", "k_lane", "k_lite", "k_fill", "k_resolve", "k_chain", "k_pq")
 # kernels whose loads are wide coalesced streams (events, keys, sorted records, histograms)
-STREAMING = ("k_rs_first", "k_radix_hist", "k_radix_scatter", "k_scan_", "k_seg_count", "k_seg_emit", "k_block_sums",
+STREAMING = ("k_grp_first", "k_grp_records", "k_hot_scan", "k_rs_first", "k_radix_hist", "k_radix_scatter", "k_scan_", "k_seg_count", "k_seg_emit", "k_block_sums",
              "k_scatter_rec", "k_fill", "k_jac")
 SKIP = ("k_init_state", "k_snap_", "k_set_flags")
 
@@ -46,7 +46,7 @@ def load(path, counter):
 def main():
     fetch, fcnt = load(sys.argv[1], "FETCH_SIZE")
     write, _ = load(sys.argv[2], "WRITE_SIZE")
-    nb = max(1, sum(v for k, v in fcnt.items() if k.startswith("k_rs_first")))
+    nb = max(1, sum(v for k, v in fcnt.items() if k.startswith(("k_rs_first", "k_grp_first"))))
     names = sorted(set(fetch) | set(write))
     kern = {}
     for n in names:
