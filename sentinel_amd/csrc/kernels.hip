@@ -672,12 +672,6 @@ __global__ __launch_bounds__(256) void k_post_w(const uint32_t* __restrict__ wor
         }
     }
 }
-hipError_t launch_post_w(const uint32_t* words, const uint32_t* P, uint32_t nhot, const uint32_t* dec, uint64_t n,
-                         uint64_t gbase, uint8_t* ring, uint64_t ring_mask, uint32_t* out, hipStream_t st) {
-    const uint32_t nb = (uint32_t)((n + 256 * POSTW_ITEMS - 1) / (256 * POSTW_ITEMS));
-    hipLaunchKernelGGL(k_post_w, dim3(nb), dim3(256), 0, st, words, P, nhot, dec, n, gbase, ring, ring_mask, out);
-    return hipGetLastError();
-}
 
 // The hot ids' segments (hot id order, the non-empty ones) from their bases and totals (hb): segs[0 .. k),
 // out[0] = k.  One workgroup of HOT_MAX lanes.
@@ -1129,6 +1123,12 @@ hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, h
     return hipGetLastError();
 }
 uint32_t hot_max() { return HOT_MAX; }
+hipError_t launch_post_w(const uint32_t* words, const uint32_t* P, uint32_t nhot, const uint32_t* dec, uint64_t n,
+                         uint64_t gbase, uint8_t* ring, uint64_t ring_mask, uint32_t* out, hipStream_t st) {
+    const uint32_t nb = (uint32_t)((n + 256 * POSTW_ITEMS - 1) / (256 * POSTW_ITEMS));
+    hipLaunchKernelGGL(k_post_w, dim3(nb), dim3(256), 0, st, words, P, nhot, dec, n, gbase, ring, ring_mask, out);
+    return hipGetLastError();
+}
 
 uint32_t radix_tile() { return RS_TILE; }
 
