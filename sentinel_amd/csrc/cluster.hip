@@ -10,13 +10,18 @@
 //
 // A batch of requests (time-ordered) is decided in three device steps:
 //   1. k_tok_classify  (parallel)  BAD_REQUEST / NO_RULE_EXISTS, flowId -> flow index (hash table);
-//   2. k_tok_limiter   (one wave)  the namespace's GlobalRequestLimiter, in request order.  Inside one
-//                                  100 ms bucket the set of valid buckets is fixed, so the passes of a
-//                                  bucket are a prefix of its requests: one step per bucket, not per
-//                                  request;
-//   3. stable radix sort of the limiter-passed requests by flow index (kernels.hip), then
-//      k_tok_flow (one lane per flowId) runs acquireClusterToken over the flow's requests in order
-//      against the flow's ClusterMetric, kept in HBM between batches.
+//   2. the namespace's GlobalRequestLimiter, in request order.  Inside one 100 ms bucket the set of valid
+//      buckets is fixed, so the passes of a bucket are a prefix of its candidates: k_lim_walk takes one
+//      step per bucket (their candidate counts from a scan), k_lim_apply ranks every request in its
+//      bucket (parallel);
+//   3. stable radix sort of the limiter-passed requests by flow index (kernels.hip), then k_tok_flow_wg
+//      (a workgroup per flowId) runs acquireClusterToken over the flow's requests in time order against
+//      the flow's ClusterMetric, kept in HBM between batches.  Inside one window sub-bucket the valid
+//      buckets are fixed too, and a request passes iff threshold - (S + P) / intervalSec - acquire >= 0
+//      with S the sub-bucket's starting PASS_REQUEST sum and P the passes before it: per request the largest
+//      such P (L_j, by bisection on the exact double expression), and the passes follow in a few block-wide
+//      phases (one per distinct L_j).  Prioritized requests that fail then try tryOccupyNext in order (one
+//      lane: each step is O(1) from prefix sums of the passes).
 // Every flowId's window is touched only by its own requests, so step 3 is independent per flowId.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -247,6 +252,309 @@ __global__ void k_tok_flow(const uint32_t* __restrict__ skeys, const uint32_t* _
     }
 }
 
+// ---- 2. the limiter, parallel over requests and sequential over 100 ms buckets
+// per request: its bucket starts here (first request of its 100 ms bucket), and it is a limiter candidate
+__global__ void k_lim_flags(const sg_token_req* __restrict__ req, uint64_t n, const uint32_t* __restrict__ fidx,
+                            uint32_t* __restrict__ bflag, uint32_t* __restrict__ cflag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = req[i].ts / NS_WLEN;
+    bflag[i] = (i == 0 || req[i - 1].ts / NS_WLEN != b) ? 1u : 0u;
+    cflag[i] = fidx[i] != NO_FLOW ? 1u : 0u;
+}
+// bucket starts: bstart[k] = first request of the k-th bucket (bflag scanned exclusively: its bucket index)
+__global__ void k_lim_starts(const uint32_t* __restrict__ bidx, const uint32_t* __restrict__ bflag0, uint64_t n,
+                             uint32_t* __restrict__ bstart) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (bflag0[i]) bstart[bidx[i]] = (uint32_t)i;
+}
+// one lane walks the buckets in order: RequestLimiter.canPass = sum(valid buckets) + 1 <= qpsAllowed, then add(1)
+// -- the passes of a bucket are its first kpass[k] candidates (cexcl: candidates before a request)
+__global__ void k_lim_walk(const sg_token_req* __restrict__ req, uint64_t n, const uint32_t* __restrict__ bstart,
+                           const uint32_t* __restrict__ nbk, const uint32_t* __restrict__ cexcl,
+                           const uint32_t* __restrict__ ctot, NsLimiter* __restrict__ lim, double allowed,
+                           uint32_t* __restrict__ kpass) {
+    if (threadIdx.x != 0) return;
+    NsLimiter L = *lim;
+    const uint32_t nb = *nbk;
+    for (uint32_t k = 0; k < nb; ++k) {
+        const uint32_t a = bstart[k];
+        const uint32_t m = (k + 1 < nb ? cexcl[bstart[k + 1]] : *ctot) - cexcl[a];
+        if (!m) { kpass[k] = 0; continue; }
+        const int64_t tb = req[a].ts;  // (every candidate of the bucket: the same bucket, the same valid set)
+        const int64_t wsb = tb - tb % NS_WLEN;
+        const int idx = (int)((tb / NS_WLEN) % NS_BUCKETS);
+        if (L.ws[idx] < 0 || wsb > L.ws[idx]) { L.ws[idx] = wsb; L.cnt[idx] = 0; }
+        int64_t s = 0;
+        for (int j = 0; j < NS_BUCKETS; ++j)
+            if (L.ws[j] >= 0 && tb - L.ws[j] <= NS_INTERVAL) s += L.cnt[j];
+        int64_t kp = 0;
+        if ((double)s + 1.0 <= allowed) {  // the j-th candidate passes iff (double)(s + j) + 1 <= allowed
+            int64_t lo = 0, hi = m;  // largest count kp <= m with (double)(s + kp - 1) + 1 <= allowed
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) / 2;
+                if ((double)(s + mid - 1) + 1.0 <= allowed) lo = mid; else hi = mid - 1;
+            }
+            kp = lo;
+        }
+        L.cnt[idx] += kp;
+        kpass[k] = (uint32_t)kp;
+    }
+    *lim = L;
+}
+// every candidate: passes iff its rank among its bucket's candidates < kpass (else TOO_MANY_REQUEST); the sort key
+__global__ void k_lim_apply(const uint64_t n, const uint32_t* __restrict__ fidx, const uint32_t* __restrict__ bidx,
+                            const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ cexcl,
+                            const uint32_t* __restrict__ kpass, uint32_t nflows, uint32_t* __restrict__ keys,
+                            uint32_t* __restrict__ vals, sg_token_result* __restrict__ res) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t f = fidx[i];
+    uint32_t key = nflows;
+    if (f != NO_FLOW) {
+        const uint32_t k = bidx[i];
+        if (cexcl[i] - cexcl[bstart[k]] < kpass[k]) key = f;
+        else res[i].status = SG_TOKEN_TOO_MANY_REQUEST;
+    }
+    keys[i] = key;
+    vals[i] = (uint32_t)i;
+}
+
+// ---- 3. one flowId's requests, a workgroup of TF_T lanes, chunks of TF_T requests in time order
+#define TF_T 1024
+__device__ __forceinline__ uint32_t tf_scan_excl(uint32_t v, uint32_t* red, uint32_t* total) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x += y;
+    }
+    __syncthreads();
+    if (l == 63) red[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t k = 0; k < TF_T / 64; ++k) { const uint32_t c = red[k]; if (k < w) pre += c; tot += c; }
+    *total = tot;
+    return pre + x - v;
+}
+__device__ __forceinline__ int64_t tf_min(int64_t v, int64_t* red) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const int64_t y = __shfl_xor(v, o, 64); v = y < v ? y : v; }
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    int64_t m = red[0];
+    for (uint32_t k = 1; k < TF_T / 64; ++k) m = red[k] < m ? red[k] : m;
+    return m;
+}
+__device__ __forceinline__ int64_t tf_sum(int64_t v, int64_t* red) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    int64_t m = 0;
+    for (uint32_t k = 0; k < TF_T / 64; ++k) m += red[k];
+    return m;
+}
+#define TF_NONE ((int64_t)1 << 62)
+enum : uint8_t { TS_BLOCK = 0, TS_PASS = 1, TS_WAIT = 2 };
+__global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict__ skeys,
+                                                      const uint32_t* __restrict__ svals, uint64_t n,
+                                                      const sg_token_req* __restrict__ req, CFlow* __restrict__ flows,
+                                                      uint32_t nflows, CBkt* __restrict__ bkts, double exceed,
+                                                      double max_occ_ratio, sg_token_result* __restrict__ res) {
+    __shared__ uint32_t ured[TF_T / 64];
+    __shared__ int64_t lred[TF_T / 64];
+    __shared__ uint8_t sst[TF_T];     // per position of the chunk: TS_*
+    __shared__ int64_t spass[TF_T];   // acquire sum of the run's passes before the position
+    __shared__ uint32_t flist[TF_T];  // the run's prioritized requests that failed the normal check, in order
+    __shared__ int32_t sacq[TF_T];
+    __shared__ int64_t sh_S, sh_W0, sh_PS0, sh_head, sh_cur0, sh_wadd;
+    __shared__ uint32_t sh_seq, sh_lo, sh_hi, sh_headcur;
+    const uint32_t f = blockIdx.x, t = threadIdx.x;
+    if (f >= nflows) return;
+    if (t == 0) {  // lower_bound(skeys, f), lower_bound(skeys, f + 1)
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) { const uint64_t mid = (lo + hi) / 2; if (skeys[mid] < f) lo = mid + 1; else hi = mid; }
+        uint64_t e = lo, h2 = n;
+        while (e < h2) { const uint64_t mid = (e + h2) / 2; if (skeys[mid] <= f) e = mid + 1; else h2 = mid; }
+        sh_lo = (uint32_t)lo;
+        sh_hi = (uint32_t)e;
+    }
+    __syncthreads();
+    const uint32_t lo = sh_lo, hi = sh_hi;
+    if (lo == hi) return;
+    CMetric M;
+    M.f = &flows[f];
+    M.b = bkts + M.f->boff;
+    M.wlen = M.f->interval / M.f->n;
+    const double thr = M.f->thr_type == SG_CLUSTER_THRESHOLD_GLOBAL ? M.f->count : M.f->count * (double)M.f->connected;
+    const double gthr = thr * exceed;  // calcGlobalThreshold * exceedCount
+    const double isec = M.f->interval / 1000.0;
+    const int wait = 1000 / M.f->n;
+    for (uint32_t c0 = lo; c0 < hi; c0 += TF_T) {
+        const uint32_t cn = min((uint32_t)TF_T, hi - c0);
+        uint32_t i = 0;
+        int64_t now = 0;
+        int32_t acq = 0;
+        bool prio = false;
+        if (t < cn) {
+            i = svals[c0 + t];
+            const sg_token_req q = req[i];
+            now = q.ts;
+            acq = q.acquire_count;
+            prio = q.prioritized != 0;
+        }
+        const int64_t sb = t < cn ? now / M.wlen : -1;
+        if (t < cn) sacq[t] = acq;
+        // the chunk's sub-bucket runs, one after the other (usually one)
+        uint32_t a = 0;
+        while (a < cn) {
+            __syncthreads();
+            if (t == a) {  // the run's window: LeapArray.currentWindow (reset / occupy transfer), then every sum over
+                           // the sub-bucket's valid buckets (constant inside it)
+                CBkt* cur = cm_current(M, now);
+                sh_seq = cur == &M.scratch ? 1u : 0u;  // a time before the slot's window: the sequential path
+                sh_S = cm_sum(M, now, CF_PASS_REQ);
+                sh_W0 = cm_sum(M, now, CF_WAITING);
+                sh_PS0 = cm_sum(M, now, CF_PASS);
+                const int hidx = (int)(((now + M.wlen) / M.wlen) % M.f->n);
+                const CBkt& hw = M.b[hidx];
+                sh_head = (hw.ws >= 0 && !(now - hw.ws > M.f->interval)) ? hw.c[CF_PASS] : 0;
+                sh_headcur = &hw == cur ? 1u : 0u;  // (one sample: the head window is the current one)
+                sh_cur0 = cur->c[CF_PASS];
+                sh_wadd = 0;
+                lred[0] = sb;
+            }
+            __syncthreads();
+            const int64_t sba = lred[0];
+            uint32_t nrun;
+            (void)tf_scan_excl(t < cn && t >= a && sb == sba ? 1u : 0u, ured, &nrun);
+            const uint32_t b = a + nrun;  // (positions are time ordered: the run is [a, b))
+            const bool in = t >= a && t < b;
+            if (sh_seq) {  // the reference's order, request by request
+                for (uint32_t c = a; c < b; ++c) {
+                    __syncthreads();
+                    if (t != c) continue;
+                    sg_token_result o;
+                    o.status = SG_TOKEN_BLOCKED; o.remaining = 0; o.wait_in_ms = 0; o.reserved = 0;
+                    const double nr = gthr - cm_avg(M, now, CF_PASS_REQ) - acq;
+                    if (nr >= 0) {
+                        cm_add(M, now, CF_PASS, acq);
+                        cm_add(M, now, CF_PASS_REQ, 1);
+                        if (prio) cm_add(M, now, CF_OCC_PASS, acq);
+                        o.status = SG_TOKEN_OK;
+                        o.remaining = j_d2i(nr);
+                    } else {
+                        cm_add(M, now, CF_BLOCK, acq);
+                        cm_add(M, now, CF_BLOCK_REQ, 1);
+                        if (prio) cm_add(M, now, CF_OCC_BLOCK, acq);
+                    }
+                    res[i] = o;
+                }
+                a = b;
+                continue;
+            }
+            const int64_t S = sh_S;
+            // L: the largest P >= 0 with gthr - (double)(S + P) / isec - acq >= 0 (-1: none), by bisection on the
+            // reference's expression (monotone in P)
+            int64_t L = -1;
+            if (in && gthr - (double)S / isec - acq >= 0) {
+                int64_t l2 = 0, h2 = (int64_t)1 << 50;
+                while (l2 < h2) {
+                    const int64_t mid = (l2 + h2 + 1) / 2;
+                    if (gthr - (double)(S + mid) / isec - acq >= 0) l2 = mid; else h2 = mid - 1;
+                }
+                L = l2;
+            }
+            // the passes, phase by phase: with P passes so far a request of L < P never passes; the undecided
+            // rest pass in order while P <= their smallest L (one phase per distinct L)
+            int64_t P = 0, myP = 0;
+            bool undec = in, pass = false;
+            for (;;) {
+                if (undec && L < P) undec = false;
+                const int64_t V = tf_min(undec ? L : TF_NONE, lred);
+                if (V == TF_NONE) break;
+                const int64_t need = V - P + 1;
+                uint32_t nu;
+                const uint32_t rk = tf_scan_excl(undec ? 1u : 0u, ured, &nu);
+                if (undec && (int64_t)rk < need) { pass = true; myP = P + rk; undec = false; }
+                if ((int64_t)nu <= need) break;
+                P = V + 1;
+            }
+            // the PASS sum each position sees (acquire prefix of the passes: 2 x 16-bit halves, a run < 2^10)
+            {
+                const uint32_t pa = pass ? (uint32_t)acq : 0u;
+                uint32_t tl, th;
+                const uint32_t el = tf_scan_excl(pa & 0xFFFFu, ured, &tl);
+                const uint32_t eh = tf_scan_excl(pa >> 16, ured, &th);
+                if (in) spass[t] = (int64_t)el + ((int64_t)eh << 16);
+            }
+            const bool fp = in && !pass && prio;  // tries tryOccupyNext
+            uint32_t nfp;
+            const uint32_t fr = tf_scan_excl(fp ? 1u : 0u, ured, &nfp);
+            if (fp) flist[fr] = t;
+            if (in) sst[t] = pass ? TS_PASS : TS_BLOCK;
+            __syncthreads();
+            if (t == 0 && nfp) {  // tryOccupyNext in request order (ClusterMetric.java:78-98)
+                int64_t wadd = 0;
+                for (uint32_t k = 0; k < nfp; ++k) {
+                    const uint32_t c = flist[k];
+                    const double occupy_avg = (double)(sh_W0 + wadd) / isec;
+                    if (!(occupy_avg <= max_occ_ratio * gthr)) break;  // (WAITING only grows inside the run)
+                    const double lq = (double)(sh_PS0 + spass[c]) / isec;
+                    const int64_t head_pass = sh_headcur ? sh_cur0 + spass[c] : sh_head;
+                    const int64_t qa = sacq[c];
+                    // lq and occupied only grow inside the run and head_pass is fixed (unless the head window is the
+                    // current one): once even an acquire of 1 cannot occupy, no later request can
+                    if (!sh_headcur && lq + (double)(1 + M.f->occ_pass) - (double)head_pass > gthr) break;
+                    if (lq + (double)(qa + M.f->occ_pass) - (double)head_pass <= gthr) {
+                        M.f->occ_pass += qa;  // addOccupyPass
+                        M.f->occ_req += 1;
+                        M.f->has_occ = 1;
+                        wadd += qa;
+                        if (wait > 0) sst[c] = TS_WAIT;
+                    }
+                }
+                sh_wadd = wadd;
+            }
+            __syncthreads();
+            const uint8_t st = in ? sst[t] : (uint8_t)0xFF;
+            if (in) {
+                sg_token_result o;
+                o.status = st == TS_PASS ? SG_TOKEN_OK : st == TS_WAIT ? SG_TOKEN_SHOULD_WAIT : SG_TOKEN_BLOCKED;
+                o.remaining = st == TS_PASS ? j_d2i(gthr - (double)(S + myP) / isec - acq) : 0;
+                o.wait_in_ms = st == TS_WAIT ? wait : 0;
+                o.reserved = 0;
+                res[i] = o;
+            }
+            // the window's counts of the run
+            const int64_t pas = tf_sum(st == TS_PASS ? acq : 0, lred);
+            const int64_t pasr = tf_sum(st == TS_PASS ? 1 : 0, lred);
+            const int64_t opas = tf_sum(st == TS_PASS && prio ? acq : 0, lred);
+            const int64_t blk = tf_sum(st == TS_BLOCK ? acq : 0, lred);
+            const int64_t blkr = tf_sum(st == TS_BLOCK ? 1 : 0, lred);
+            const int64_t oblk = tf_sum(st == TS_BLOCK && prio ? acq : 0, lred);
+            if (t == 0) {
+                CBkt* cur = cm_current(M, sba * M.wlen);
+                cur->c[CF_PASS] += pas;
+                cur->c[CF_PASS_REQ] += pasr;
+                cur->c[CF_OCC_PASS] += opas;
+                cur->c[CF_WAITING] += sh_wadd;
+                cur->c[CF_BLOCK] += blk;
+                cur->c[CF_BLOCK_REQ] += blkr;
+                cur->c[CF_OCC_BLOCK] += oblk;
+            }
+            a = b;
+        }
+    }
+}
+
 hipError_t launch_tok_classify(const sg_token_req* req, uint64_t n, const CSlot* tab, uint32_t mask, uint32_t* fidx,
                                sg_token_result* res, uint32_t* flags, hipStream_t st) {
     if (!n) return hipSuccess;
@@ -265,8 +573,27 @@ hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_
                            CFlow* flows, uint32_t nflows, CBkt* bkts, double exceed, double max_occ_ratio,
                            sg_token_result* res, hipStream_t st) {
     if (!n || !nflows) return hipSuccess;
-    hipLaunchKernelGGL(k_tok_flow, dim3((nflows + 255) / 256), dim3(256), 0, st, skeys, svals, n, req, flows, nflows,
-                       bkts, exceed, max_occ_ratio, res);
+    hipLaunchKernelGGL(k_tok_flow_wg, dim3(nflows), dim3(TF_T), 0, st, skeys, svals, n, req, flows, nflows, bkts, exceed,
+                       max_occ_ratio, res);
+    return hipGetLastError();
+}
+// the limiter: bflag / cflag / bidx / cexcl / bstart / kpass are n-word scratch arrays, part the scan partials,
+// small = 2 device words (bucket count, candidate count)
+hipError_t launch_tok_limiter_par(const sg_token_req* req, uint64_t n, const uint32_t* fidx, uint32_t nflows,
+                                  NsLimiter* lim, double allowed, uint32_t* keys, uint32_t* vals, sg_token_result* res,
+                                  uint32_t* bflag, uint32_t* cflag, uint32_t* bidx, uint32_t* cexcl, uint32_t* bstart,
+                                  uint32_t* kpass, uint32_t* part, uint32_t* small,
+                                  hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                                  hipStream_t st) {
+    if (!n) return hipSuccess;
+    const uint32_t g = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_lim_flags, dim3(g), dim3(256), 0, st, req, n, fidx, bflag, cflag);
+    hipError_t e = scan(bflag, bidx, n, part, small, st);
+    if (e == hipSuccess) e = scan(cflag, cexcl, n, part, small + 1, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lim_starts, dim3(g), dim3(256), 0, st, bidx, bflag, n, bstart);
+    hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, st, req, n, bstart, small, cexcl, small + 1, lim, allowed, kpass);
+    hipLaunchKernelGGL(k_lim_apply, dim3(g), dim3(256), 0, st, n, fidx, bidx, bstart, cexcl, kpass, nflows, keys, vals, res);
     return hipGetLastError();
 }
 

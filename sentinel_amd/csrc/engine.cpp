@@ -151,6 +151,12 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
 // cluster.hip
 hipError_t launch_tok_classify(const sg_token_req* req, uint64_t n, const CSlot* tab, uint32_t mask, uint32_t* fidx,
                                sg_token_result* res, uint32_t* flags, hipStream_t st);
+hipError_t launch_tok_limiter_par(const sg_token_req* req, uint64_t n, const uint32_t* fidx, uint32_t nflows,
+                                  NsLimiter* lim, double allowed, uint32_t* keys, uint32_t* vals, sg_token_result* res,
+                                  uint32_t* bflag, uint32_t* cflag, uint32_t* bidx, uint32_t* cexcl, uint32_t* bstart,
+                                  uint32_t* kpass, uint32_t* part, uint32_t* small,
+                                  hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
+                                  hipStream_t st);
 hipError_t launch_tok_limiter(const sg_token_req* req, uint64_t n, const uint32_t* fidx, uint32_t nflows,
                               NsLimiter* lim, double allowed, uint32_t* keys, uint32_t* vals, sg_token_result* res,
                               hipStream_t st);
@@ -2826,7 +2832,10 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
     if (flags & 1) return fail(SG_EINVAL, "token requests must be ordered by ts (the replay clock)");
     // GlobalRequestLimiter: a negative qpsAllowed stands for "no limiter registered" (tryPass -> true)
     const double allowed = e->cfg.cluster_max_allowed_qps < 0 ? 1.0 / 0.0 : (double)e->cfg.cluster_max_allowed_qps;
-    HIPCHK(launch_tok_limiter(e->d_treq, n, e->d_tfidx, nflows, e->d_nslim, allowed, e->d_k0, e->d_v0, e->d_tres, st));
+    // the limiter (parallel per 100 ms bucket; the drained batch slot's arrays are its scratch), then the flows
+    HIPCHK(launch_tok_limiter_par(e->d_treq, n, e->d_tfidx, nflows, e->d_nslim, allowed, e->d_k0, e->d_v0, e->d_tres,
+                                  e->d_flag, e->d_pos, e->d_order, e->d_prev, e->d_dec, e->d_posof, e->d_part,
+                                  e->d_small + 8, launch_scan, st));
     if (nflows) {
         int bits = 1;
         while (bits < 32 && (1ull << bits) <= nflows) ++bits;  // keys 0..nflows (nflows = not for a flow)
