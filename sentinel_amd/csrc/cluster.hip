@@ -304,7 +304,9 @@ __global__ void k_lim_walk(const sg_token_req* __restrict__ req, uint64_t n, con
     *lim = L;
 }
 // every candidate: passes iff its rank among its bucket's candidates < kpass (else TOO_MANY_REQUEST); the sort key
-__global__ void k_lim_apply(const uint64_t n, const uint32_t* __restrict__ fidx, const uint32_t* __restrict__ bidx,
+// (bidx = the exclusive scan of the bucket-start flags: a request's bucket is bidx + bflag - 1)
+__global__ void k_lim_apply(const uint64_t n, const uint32_t* __restrict__ fidx, const uint32_t* __restrict__ bflag,
+                            const uint32_t* __restrict__ bidx,
                             const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ cexcl,
                             const uint32_t* __restrict__ kpass, uint32_t nflows, uint32_t* __restrict__ keys,
                             uint32_t* __restrict__ vals, sg_token_result* __restrict__ res) {
@@ -313,7 +315,7 @@ __global__ void k_lim_apply(const uint64_t n, const uint32_t* __restrict__ fidx,
     const uint32_t f = fidx[i];
     uint32_t key = nflows;
     if (f != NO_FLOW) {
-        const uint32_t k = bidx[i];
+        const uint32_t k = bidx[i] + bflag[i] - 1;
         if (cexcl[i] - cexcl[bstart[k]] < kpass[k]) key = f;
         else res[i].status = SG_TOKEN_TOO_MANY_REQUEST;
     }
@@ -593,7 +595,8 @@ hipError_t launch_tok_limiter_par(const sg_token_req* req, uint64_t n, const uin
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lim_starts, dim3(g), dim3(256), 0, st, bidx, bflag, n, bstart);
     hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, st, req, n, bstart, small, cexcl, small + 1, lim, allowed, kpass);
-    hipLaunchKernelGGL(k_lim_apply, dim3(g), dim3(256), 0, st, n, fidx, bidx, bstart, cexcl, kpass, nflows, keys, vals, res);
+    hipLaunchKernelGGL(k_lim_apply, dim3(g), dim3(256), 0, st, n, fidx, bflag, bidx, bstart, cexcl, kpass, nflows, keys,
+                       vals, res);
     return hipGetLastError();
 }
 
