@@ -467,11 +467,11 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
             // reference's expression (monotone in P)
             int64_t L = -1;
             if (in && gthr - (double)S / isec - acq >= 0) {
-                int64_t l2 = 0, h2 = (int64_t)1 << 50;
-                while (l2 < h2) {
-                    const int64_t mid = (l2 + h2 + 1) / 2;
-                    if (gthr - (double)(S + mid) / isec - acq >= 0) l2 = mid; else h2 = mid - 1;
-                }
+                // near (gthr - acq) * isec - S, then stepped to the exact boundary of the reference's expression
+                const double g = (gthr - acq) * isec - (double)S;
+                int64_t l2 = g >= 9.0e15 ? ((int64_t)1 << 53) : (g < 0 ? 0 : (int64_t)g);
+                while (l2 > 0 && !(gthr - (double)(S + l2) / isec - acq >= 0)) --l2;
+                while (l2 < ((int64_t)1 << 53) && gthr - (double)(S + l2 + 1) / isec - acq >= 0) ++l2;
                 L = l2;
             }
             // the passes, phase by phase: with P passes so far a request of L < P never passes; the undecided
