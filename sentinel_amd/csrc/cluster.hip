@@ -181,77 +181,6 @@ __device__ double cm_avg(CMetric& M, int64_t now, int ev) {
 }
 __device__ void cm_add(CMetric& M, int64_t now, int ev, int64_t v) { cm_current(M, now)->c[ev] += v; }
 
-// 3. ClusterFlowChecker.acquireClusterToken over one flow's requests (sorted positions [lo, hi))
-__global__ void k_tok_flow(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals, uint64_t n,
-                           const sg_token_req* __restrict__ req, CFlow* __restrict__ flows, uint32_t nflows,
-                           CBkt* __restrict__ bkts, double exceed, double max_occ_ratio,
-                           sg_token_result* __restrict__ res) {
-    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nflows) return;
-    // lower_bound(skeys, f), lower_bound(skeys, f + 1)
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) { const uint64_t mid = (lo + hi) / 2; if (skeys[mid] < f) lo = mid + 1; else hi = mid; }
-    uint64_t e = lo, h2 = n;
-    while (e < h2) { const uint64_t mid = (e + h2) / 2; if (skeys[mid] <= f) e = mid + 1; else h2 = mid; }
-    if (lo == e) return;
-    CMetric M;
-    M.f = &flows[f];
-    M.b = bkts + M.f->boff;
-    M.wlen = M.f->interval / M.f->n;
-    const double thr = M.f->thr_type == SG_CLUSTER_THRESHOLD_GLOBAL ? M.f->count : M.f->count * (double)M.f->connected;
-    const double global_threshold = thr * exceed;  // calcGlobalThreshold * exceedCount
-    for (uint64_t p = lo; p < e; ++p) {
-        const uint32_t i = svals[p];
-        const sg_token_req q = req[i];
-        const int64_t now = q.ts;
-        sg_token_result o;
-        o.status = SG_TOKEN_BLOCKED; o.remaining = 0; o.wait_in_ms = 0; o.reserved = 0;
-        const double latest_qps = cm_avg(M, now, CF_PASS_REQ);
-        const double next_remaining = global_threshold - latest_qps - q.acquire_count;
-        if (next_remaining >= 0) {
-            cm_add(M, now, CF_PASS, q.acquire_count);
-            cm_add(M, now, CF_PASS_REQ, 1);
-            if (q.prioritized) cm_add(M, now, CF_OCC_PASS, q.acquire_count);
-            o.status = SG_TOKEN_OK;
-            o.remaining = j_d2i(next_remaining);  // (int) nextRemaining
-            res[i] = o;
-            continue;
-        }
-        if (q.prioritized) {
-            const double occupy_avg = cm_avg(M, now, CF_WAITING);
-            if (occupy_avg <= max_occ_ratio * global_threshold) {
-                // ClusterMetric.tryOccupyNext / canOccupy (ClusterMetric.java:78-98)
-                const double lq = cm_avg(M, now, CF_PASS);
-                cm_current(M, now);
-                int64_t head_pass = 0;  // getFirstCountOfWindow: LeapArray.getValidHead
-                {
-                    const int hidx = (int)(((now + M.wlen) / M.wlen) % M.f->n);
-                    const CBkt& w = M.b[hidx];
-                    if (w.ws >= 0 && !(now - w.ws > M.f->interval)) head_pass = w.c[CF_PASS];
-                }
-                const int64_t occupied = M.f->occ_pass;
-                if (lq + (double)((int64_t)q.acquire_count + occupied) - (double)head_pass <= global_threshold) {
-                    M.f->occ_pass += q.acquire_count;  // addOccupyPass
-                    M.f->occ_req += 1;
-                    M.f->has_occ = 1;
-                    cm_add(M, now, CF_WAITING, q.acquire_count);
-                    const int wait = 1000 / M.f->n;
-                    if (wait > 0) {
-                        o.status = SG_TOKEN_SHOULD_WAIT;
-                        o.wait_in_ms = wait;
-                        res[i] = o;
-                        continue;
-                    }
-                }
-            }
-        }
-        cm_add(M, now, CF_BLOCK, q.acquire_count);
-        cm_add(M, now, CF_BLOCK_REQ, 1);
-        if (q.prioritized) cm_add(M, now, CF_OCC_BLOCK, q.acquire_count);
-        res[i] = o;
-    }
-}
-
 // ---- 2. the limiter, parallel over requests and sequential over 100 ms buckets
 // per request: its bucket starts here (first request of its 100 ms bucket), and it is a limiter candidate
 __global__ void k_lim_flags(const sg_token_req* __restrict__ req, uint64_t n, const uint32_t* __restrict__ fidx,
@@ -352,18 +281,42 @@ __device__ __forceinline__ int64_t tf_min(int64_t v, int64_t* red) {
     for (uint32_t k = 1; k < TF_T / 64; ++k) m = red[k] < m ? red[k] : m;
     return m;
 }
-__device__ __forceinline__ int64_t tf_sum(int64_t v, int64_t* red) {
+// six 64-bit sums at once: one wave reduction each, one barrier
+__device__ __forceinline__ void tf_sum6(int64_t v[6], int64_t (*red)[6]) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
     __syncthreads();
-    if (l == 0) red[w] = v;
+    if (l == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[w][k] = v[k];
     __syncthreads();
-    int64_t m = 0;
-    for (uint32_t k = 0; k < TF_T / 64; ++k) m += red[k];
-    return m;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int64_t m = 0;
+        for (uint32_t j = 0; j < TF_T / 64; ++j) m += red[j][k];
+        v[k] = m;
+    }
+}
+__device__ __forceinline__ int64_t tf_scan64_excl(int64_t v, int64_t* red) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x += y;
+    }
+    __syncthreads();
+    if (l == 63) red[w] = x;
+    __syncthreads();
+    int64_t pre = 0;
+    for (uint32_t k = 0; k < w; ++k) pre += red[k];
+    return pre + x - v;
 }
 #define TF_NONE ((int64_t)1 << 62)
+#define TF_NB 64  // ClusterMetric windows kept in LDS for the workgroup's life (more samples: in HBM)
 enum : uint8_t { TS_BLOCK = 0, TS_PASS = 1, TS_WAIT = 2 };
 __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals, uint64_t n,
@@ -376,6 +329,9 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
     __shared__ int64_t spass[TF_T];   // acquire sum of the run's passes before the position
     __shared__ uint32_t flist[TF_T];  // the run's prioritized requests that failed the normal check, in order
     __shared__ int32_t sacq[TF_T];
+    __shared__ int64_t red6[TF_T / 64][6];
+    __shared__ CFlow lflow;
+    __shared__ CBkt lbkt[TF_NB];
     __shared__ int64_t sh_S, sh_W0, sh_PS0, sh_head, sh_cur0, sh_wadd;
     __shared__ uint32_t sh_seq, sh_lo, sh_hi, sh_headcur;
     const uint32_t f = blockIdx.x, t = threadIdx.x;
@@ -391,9 +347,15 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
     __syncthreads();
     const uint32_t lo = sh_lo, hi = sh_hi;
     if (lo == hi) return;
+    // the flow's metric: its view and windows in LDS while the workgroup runs (lane 0 works on them; written back)
+    const CFlow gf = flows[f];
+    const bool in_lds = gf.n <= TF_NB;
+    if (t == 0) lflow = gf;
+    if (in_lds && t < (uint32_t)gf.n) lbkt[t] = bkts[gf.boff + t];
+    __syncthreads();
     CMetric M;
-    M.f = &flows[f];
-    M.b = bkts + M.f->boff;
+    M.f = &lflow;
+    M.b = in_lds ? lbkt : bkts + gf.boff;
     M.wlen = M.f->interval / M.f->n;
     const double thr = M.f->thr_type == SG_CLUSTER_THRESHOLD_GLOBAL ? M.f->count : M.f->count * (double)M.f->connected;
     const double gthr = thr * exceed;  // calcGlobalThreshold * exceedCount
@@ -489,13 +451,10 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
                 if ((int64_t)nu <= need) break;
                 P = V + 1;
             }
-            // the PASS sum each position sees (acquire prefix of the passes: 2 x 16-bit halves, a run < 2^10)
+            // the PASS sum each position sees (the acquire prefix of the run's passes)
             {
-                const uint32_t pa = pass ? (uint32_t)acq : 0u;
-                uint32_t tl, th;
-                const uint32_t el = tf_scan_excl(pa & 0xFFFFu, ured, &tl);
-                const uint32_t eh = tf_scan_excl(pa >> 16, ured, &th);
-                if (in) spass[t] = (int64_t)el + ((int64_t)eh << 16);
+                const int64_t ex = tf_scan64_excl(pass ? (int64_t)acq : 0, lred);
+                if (in) spass[t] = ex;
             }
             const bool fp = in && !pass && prio;  // tries tryOccupyNext
             uint32_t nfp;
@@ -536,25 +495,25 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
                 res[i] = o;
             }
             // the window's counts of the run
-            const int64_t pas = tf_sum(st == TS_PASS ? acq : 0, lred);
-            const int64_t pasr = tf_sum(st == TS_PASS ? 1 : 0, lred);
-            const int64_t opas = tf_sum(st == TS_PASS && prio ? acq : 0, lred);
-            const int64_t blk = tf_sum(st == TS_BLOCK ? acq : 0, lred);
-            const int64_t blkr = tf_sum(st == TS_BLOCK ? 1 : 0, lred);
-            const int64_t oblk = tf_sum(st == TS_BLOCK && prio ? acq : 0, lred);
+            int64_t cs[6] = {st == TS_PASS ? acq : 0, st == TS_PASS ? 1 : 0, st == TS_PASS && prio ? acq : 0,
+                             st == TS_BLOCK ? acq : 0, st == TS_BLOCK ? 1 : 0, st == TS_BLOCK && prio ? acq : 0};
+            tf_sum6(cs, red6);
             if (t == 0) {
                 CBkt* cur = cm_current(M, sba * M.wlen);
-                cur->c[CF_PASS] += pas;
-                cur->c[CF_PASS_REQ] += pasr;
-                cur->c[CF_OCC_PASS] += opas;
+                cur->c[CF_PASS] += cs[0];
+                cur->c[CF_PASS_REQ] += cs[1];
+                cur->c[CF_OCC_PASS] += cs[2];
                 cur->c[CF_WAITING] += sh_wadd;
-                cur->c[CF_BLOCK] += blk;
-                cur->c[CF_BLOCK_REQ] += blkr;
-                cur->c[CF_OCC_BLOCK] += oblk;
+                cur->c[CF_BLOCK] += cs[3];
+                cur->c[CF_BLOCK_REQ] += cs[4];
+                cur->c[CF_OCC_BLOCK] += cs[5];
             }
             a = b;
         }
     }
+    __syncthreads();
+    if (in_lds && t < (uint32_t)gf.n) bkts[gf.boff + t] = lbkt[t];
+    if (t == 0) flows[f] = lflow;
 }
 
 hipError_t launch_tok_classify(const sg_token_req* req, uint64_t n, const CSlot* tab, uint32_t mask, uint32_t* fidx,
@@ -601,7 +560,7 @@ hipError_t launch_tok_limiter_par(const sg_token_req* req, uint64_t n, const uin
 }
 
 // ---- ClusterParamFlowChecker.acquireClusterToken (csrv/flow/ClusterParamFlowChecker.java:42-88)
-// One lane per param flow over its requests in time order (sorted positions), like k_tok_flow.  The
+// One lane per param flow over its requests in time order (sorted positions).  The
 // flow's ClusterParameterLeapArray keeps per-bucket value maps; here a value's counts live in a PVal
 // slot of an open-addressing table shared by all flows (claimed by CAS on PVal.flow; a lane only ever
 // looks up its own flow's values, which it inserted itself, so a lookup never races an insert it needs).
