@@ -561,10 +561,12 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
     return rows
 
 
-def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60):
+def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60, cpu_requests=2_000_000):
     """C5's cluster half: the token server over 10k GLOBAL flowIds (thresholds 10^3..10^5 per
     window, 1-10 samples of 0.5-2 s), Zipf(1.1) requests in time order, requests and results in HBM
-    (sg_cluster_request_tokens with device buffers, as dist.request_tokens_tensor calls it); first batch untimed."""
+    (sg_cluster_request_tokens with device buffers, as dist.request_tokens_tensor calls it); first batch untimed.
+    cpu_baseline: the oracle (ClusterFlowChecker restated in C, one thread: the token server is one sequential
+    state machine per namespace) on the first cpu_requests requests, which the GPU result is checked against."""
     import torch
     from sentinel_amd import _abi as A
     from sentinel_amd import engine as E
@@ -577,6 +579,14 @@ def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60)
                          cluster_sample_count=int(rng.choice([1, 2, 5, 10])),
                          cluster_window_interval_ms=int(rng.choice([500, 1000, 2000]))) for f in fids]
     eng.load_flow_rules(rules)
+    orc = None
+    if cpu_requests:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as O
+        orc = O.Oracle(cluster_max_allowed_qps=10 ** 9)
+        for f in fids:
+            orc.register("r%d" % f)
+        orc.load_flow_rules(rules)
     p = 1.0 / np.arange(1, n_flows + 1) ** 1.1
     p /= p.sum()
     reqs = np.zeros(n_req, dtype=A.TOKEN_REQ_DTYPE)
@@ -595,15 +605,29 @@ def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60)
         eng.cluster_request_ptr(dq.data_ptr() + a * rq, b - a, dr.data_ptr() + a * rs)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    st = dr.view(torch.int32).view(-1, 4)[:, 0].cpu().numpy()
+    res = dr.view(torch.int32).view(-1, 4).cpu().numpy()
+    st = res[:, 0]
     n_t = n_req - cuts[1]
     eng.close()
     del dq, dr
     torch.cuda.empty_cache()
+    cpu = None
+    if orc is not None:
+        m = min(cpu_requests, n_req)
+        t1 = time.perf_counter()
+        want = orc.cluster_request_array(reqs[:m])
+        dt1 = time.perf_counter() - t1
+        got = res[:m].copy().view(A.TOKEN_RES_DTYPE).reshape(-1)
+        same = bool(np.array_equal(np.asarray(want).view(np.uint8), got.view(np.uint8)))
+        cpu = {"value": m / dt1, "unit": "token requests/s", "cores": 1, "kind": "port",
+               "sample": "first %d requests of the same stream, oracle/liboracle.so (ClusterFlowChecker / "
+                         "GlobalRequestLimiter restated), one thread" % m, "gpu_results_equal": same}
+        orc.close()
     return {"config": "C5 cluster half: token server, %d GLOBAL flowIds (counts 1e3-1e5), Zipf(1.1) requests over %d s, "
                       "buffers in HBM, %d-request calls" % (n_flows, seconds, batch),
             "value": n_t / dt, "unit": "token requests/s", "requests_timed": n_t, "ms_per_call": dt / (len(cuts) - 2) * 1e3,
-            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+            "cpu_baseline": cpu}
 
 
 def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400):
