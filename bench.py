@@ -557,8 +557,48 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
         w.close()
     if c4 is not None:
         rows.append(dropin_line(dev, *c4))
+        rows.append(latency_line(dev, *c4))
     rows.append(token_line(dev))
     return rows
+
+
+def latency_line(dev, w, ev, sizes=(1, 64, 1024), calls=2000, warm=200):
+    """The drop-in under light load: every SphU.entry is synchronous (core/CtSph.java:117-168), so a
+    lightly loaded service pays one engine call per few events.  Synchronous sg_submit_ex of 1, 64 and 1,024 events of
+    the C4 trace from pageable host memory (contexts and origins on every event, as the Java batcher sends them):
+    p50 / p99 / mean host wall time per call."""
+    import torch
+    from sentinel_amd import engine as E
+    from sentinel_amd import tracegen as T
+    eng = E.Engine(device=dev.index, max_resources=1 << 20, max_slot_chain_size=0, param_table_log2=16,
+                   status_ring_log2=28, max_batch_events=max(sizes), aux_node_capacity=1 << 22)
+    w.install(eng)
+    io, ic = w.intern_names(eng)
+    out = {}
+    off = 0
+    total = sum(n * (calls + warm) for n in sizes)  # one prefix of the trace, in order (the engine's event indices)
+    ext_all = T.ext_for(np.ascontiguousarray(ev[:total]), io, ic, seed=T.SEED_BASE + 47)
+    for n in sizes:
+        need = n * (calls + warm)
+        sub = np.ascontiguousarray(ev[off:off + need])
+        ext = ext_all[off:off + need]
+        lat = []
+        for b in range(calls + warm):
+            e, x = sub[b * n:(b + 1) * n], ext[b * n:(b + 1) * n]
+            t = time.perf_counter()
+            eng.submit_ex(e, x)
+            dt = time.perf_counter() - t
+            if b >= warm:
+                lat.append(dt)
+        lat = np.array(lat) * 1e3
+        out[str(n)] = {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+                       "mean_ms": float(lat.mean()), "calls": calls}
+        off += need
+    eng.close()
+    torch.cuda.empty_cache()
+    return {"config": "drop-in latency floor: synchronous sg_submit_ex of 1 / 64 / 1024 C4 events from pageable host "
+                      "memory, contexts + origins", "unit": "ms per call", "latency": out,
+            "note": "each call: the group stage, one host round trip for the bins, the decide stage, the decisions back"}
 
 
 def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60, cpu_requests=2_000_000):
