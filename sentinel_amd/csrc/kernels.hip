@@ -881,8 +881,15 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* total) {
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(SC_THREADS) void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ part) {
+// ndev (optional): the element count on the device, at most n (the grid covers n): tiles past it add nothing
+__global__ __launch_bounds__(SC_THREADS) void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ part,
+                                                         const uint32_t* __restrict__ ndev) {
+    if (ndev && *ndev < n) n = *ndev;
     uint64_t base = (uint64_t)blockIdx.x * SC_TILE;
+    if (base >= n) {
+        if (threadIdx.x == 0) part[blockIdx.x] = 0;
+        return;
+    }
     uint32_t s = 0;
     for (int it = 0; it < SC_ITEMS; ++it) {
         uint64_t i = base + (uint64_t)it * SC_THREADS + threadIdx.x;
@@ -909,7 +916,9 @@ __global__ __launch_bounds__(SC_THREADS) void k_scan_top(uint32_t* __restrict__ 
 }
 
 __global__ __launch_bounds__(SC_THREADS) void k_scan_down(const uint32_t* __restrict__ in, uint64_t n, const uint32_t* __restrict__ part,
-                                                       uint32_t* __restrict__ out) {
+                                                       uint32_t* __restrict__ out, const uint32_t* __restrict__ ndev) {
+    if (ndev && *ndev < n) n = *ndev;
+    if ((uint64_t)blockIdx.x * SC_TILE >= n) return;
     // each thread owns SC_ITEMS consecutive items (blocked) for a sequential local scan
     uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
     uint32_t loc[SC_ITEMS];
@@ -1154,9 +1163,19 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* 
                        hipStream_t st) {
     uint32_t nb = (uint32_t)((n + SC_TILE - 1) / SC_TILE);
     if (nb == 0) nb = 1;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, (const uint32_t*)nullptr);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SC_THREADS), 0, st, part, nb, total);
-    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, out);
+    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, out, (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+// the same over the first min(n, *ndev) elements only (a count known on the device; the rest of out is untouched)
+hipError_t launch_scan_n(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* ndev, uint32_t* part,
+                         uint32_t* total, hipStream_t st) {
+    uint32_t nb = (uint32_t)((n + SC_TILE - 1) / SC_TILE);
+    if (nb == 0) nb = 1;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, ndev);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SC_THREADS), 0, st, part, nb, total);
+    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, out, ndev);
     return hipGetLastError();
 }
 

@@ -385,8 +385,8 @@ __device__ int32_t pv_count_gt(const PvBuf& B, int64_t lo, int64_t hi, int32_t r
 //     < cap; that count lies between the segment's earlier new values (NN) and earlier first accesses (NF).
 __global__ void k_pv_fflags(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= cap) return;
-    const int32_t w = g < *tot ? B.w[g] : -1;
+    if (g >= cap || g >= *tot) return;  // (the scans run over the accesses only)
+    const int32_t w = B.w[g];
     reinterpret_cast<uint32_t*>(B.gdt)[g] = w >= 0 ? 1u : 0u;  // -> NF (scan)
     B.gaw[g] = w == PV_INF ? 1u : 0u;                          // -> NN (scan)
 }
@@ -487,8 +487,8 @@ __global__ void k_pv_gather(const Seg* __restrict__ segs, const uint32_t* __rest
 // the value groups of the sorted accesses, densely: F[q] = q starts a group (scan -> its index), list G[index] = q
 __global__ void k_pv_gflags(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap, uint32_t* __restrict__ F) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= cap) return;
-    F[q] = q < *tot && (q == 0 || B.gid[q] != B.gid[q - 1]) ? 1u : 0u;
+    if (q >= cap || q >= *tot) return;  // (the scans run over the accesses only)
+    F[q] = q == 0 || B.gid[q] != B.gid[q - 1] ? 1u : 0u;
 }
 __global__ void k_pv_glist(PvBuf B, const uint32_t* __restrict__ tot, const uint32_t* __restrict__ X,
                            uint32_t* __restrict__ G) {
@@ -930,7 +930,7 @@ __device__ __forceinline__ bool pv_commits(const PvSeg& ps, const PMap& mp, uint
 }
 __global__ void k_pv_keepw(PvBuf B, const uint32_t* __restrict__ tot, uint32_t cap) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < cap) B.tc[g] = g < *tot ? (uint32_t)B.keep[g] : 0u;
+    if (g < cap && g < *tot) B.tc[g] = (uint32_t)B.keep[g];  // (the scans run over the accesses only)
 }
 // X = exclusive scan of keep (the flagged last accesses): the list L[X[g]] = g (segment-major, last-access order
 // within a segment); and the old stamps of the values live at the start and accessed (first accesses: w a rank)
@@ -1167,6 +1167,10 @@ static hipError_t pv_sort(PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* hist, 
     return hipSuccess;
 }
 
+// the scans below run over the accesses only (tot[0] on the device), not the scratch capacity (kernels.hip)
+hipError_t launch_scan_n(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* ndev, uint32_t* part,
+                         uint32_t* total, hipStream_t st);
+
 // residency (after k_pv_prev / k_pv_blocks): NF / NN prefix counts in gdt / gaw, horizons in gpos
 static hipError_t pv_resid(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv, const DevState& S, uint32_t* part,
                            hipStream_t st,
@@ -1174,8 +1178,8 @@ static hipError_t pv_resid(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv
     const uint32_t nb = (cap + 255) / 256, nblk = (cap + PV_B - 1) / PV_B;
     uint32_t* nf = reinterpret_cast<uint32_t*>(B.gdt);
     hipLaunchKernelGGL(k_pv_fflags, dim3(nb), dim3(256), 0, st, B, tot, cap);
-    hipError_t e = scan(nf, nf, cap, part, nullptr, st);
-    if (e == hipSuccess) e = scan(B.gaw, B.gaw, cap, part, nullptr, st);
+    hipError_t e = launch_scan_n(nf, nf, cap, tot, part, nullptr, st);
+    if (e == hipSuccess) e = launch_scan_n(B.gaw, B.gaw, cap, tot, part, nullptr, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_horizon, dim3((nblk + 3) / 4), dim3(256), 0, st, B, tot, pv, S, B.gpos);
     hipLaunchKernelGGL(k_pv_resid, dim3(nb), dim3(256), 0, st, B, tot, pv, S, nf, B.gaw, B.gpos);
@@ -1188,8 +1192,8 @@ static hipError_t pv_klist(PvBuf B, uint32_t cap, uint32_t* tot, const PvSeg* pv
                            hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t)) {
     const uint32_t nb = (cap + 255) / 256;
     hipLaunchKernelGGL(k_pv_keepw, dim3(nb), dim3(256), 0, st, B, tot, cap);
-    const hipError_t e = scan(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, part,
-                              nullptr, st);
+    const hipError_t e = launch_scan_n(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap,
+                                       tot, part, nullptr, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_klist, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.gdt), B.idx2, tot,
                        pv, S, tmode);
@@ -1238,12 +1242,12 @@ hipError_t launch_pv_b(SEv* recs, Seg* segs, const uint32_t* list, uint32_t m, c
     hipLaunchKernelGGL(k_pv_gather, dim3(nb), dim3(256), 0, st, segs, list, B, tot);
     {   // MC in place (its values up to tot read only the flags before them)
         uint32_t* mc = reinterpret_cast<uint32_t*>(B.sw);
-        e = scan(mc, mc, cap, part, nullptr, st);
+        e = launch_scan_n(mc, mc, cap, tot, part, nullptr, st);
         if (e != hipSuccess) return e;
     }
     // the groups' starts, densely (flags in gid2, scanned in place, count in tot[8]; list in idx2)
     hipLaunchKernelGGL(k_pv_gflags, dim3(nb), dim3(256), 0, st, B, tot, cap, B.gid2);
-    e = scan(B.gid2, B.gid2, cap, part, tot + 8, st);
+    e = launch_scan_n(B.gid2, B.gid2, cap, tot, part, tot + 8, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pv_glist, dim3(nb), dim3(256), 0, st, B, tot, B.gid2, B.idx2);
     hipLaunchKernelGGL(k_pv_walk, dim3(nb), dim3(256), 0, st, recs, segs, list, B, tot, pv, S, t0, dec, jumps, cap, bflags,
@@ -1288,7 +1292,8 @@ hipError_t launch_pvt(SEv* recs, const sg_event* ev, const uint32_t* vals, Seg* 
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pvt_walk, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     // (the peak of the segments with releases; the scan's output in gdt: free in the post pass)
-    e = scan(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, part, nullptr, st);
+    e = launch_scan_n(reinterpret_cast<const uint32_t*>(B.tc), reinterpret_cast<uint32_t*>(B.gdt), cap, tot, part,
+                      nullptr, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pvt_peak, dim3(nb), dim3(256), 0, st, B, reinterpret_cast<const uint32_t*>(B.gdt), tot, pv);
     e = pv_klist(B, cap, tot, pv, S, 1u, part, st, scan);
