@@ -1,12 +1,15 @@
-"""Parity of the engine's alternative group-stage paths, selected by environment knobs that the
-library reads once per process (so each runs in a child process):
+"""Parity of the engine's non-default paths, selected by environment knobs that the library reads once per
+engine (each runs in a child process; DESIGN.md §10 lists every switch):
 
   SG_PIPELINE=0            group and decide stages back to back (no overlap of batch k+1's grouping)
-  SG_STREAM_PRIO=1         the decide streams at the higher priority (default: the group stream)
-  SG_STREAM_PRIO=0         default stream priorities
+  SG_STREAM_PRIO=1 / 0     the decide streams at the higher priority / default stream priorities
+  SG_DEBUG_FLAGS=8192      the all-radix group stage (k_rs_first / k_scatter_rec) instead of the hot / cold split
+  SG_PQ=0                  hot-parameter resources on the per-lane kernel (no k_pq)
+  SG_MIX=0 / SG_MIX_PQ=0   mixed flow / degrade / param resources on one lane (no cooperative passes)
+  SG_PV=0, SG_PVT=0        the value-parallel pre pass without its post pass, and the reverse
 
-Each child replays a seeded C4 trace (DegradeRules + QPS rules, several batches) through the HIP
-engine and the oracle and requires bit-identical decisions and node state.
+Each child replays a seeded trace (C4: DegradeRules + QPS rules; C5: hot-parameter rules; C6: mixed rules;
+several batches) through the HIP engine and the oracle and requires bit-identical decisions and node state.
 """
 import os
 import subprocess
@@ -25,8 +28,11 @@ import numpy as np
 import pyoracle as O
 from sentinel_amd import engine as E
 from sentinel_amd import tracegen as T
-w = T.Workload(4, n_entries=300_000, n_res=30_000)
-eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, status_ring_log2=24)
+cfg = %(cfg)d
+w = T.Workload(cfg, n_entries=300_000, n_res={4: 30_000, 5: 1_000, 6: 3_000}[cfg],
+               **({"n_param_values": 200_000} if cfg != 4 else {}))
+eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, status_ring_log2=24,
+               **({"param_table_log2": 24} if cfg != 4 else {}))
 orc = O.Oracle(max_slot_chain_size=0)
 w.install(eng); w.install(orc)
 ev = w.events
@@ -43,10 +49,14 @@ print("ok", len(ev))
 """
 
 
-@pytest.mark.parametrize("env", ["SG_PIPELINE=0", "SG_STREAM_PRIO=1", "SG_STREAM_PRIO=0"])
-def test_alternative_path_parity(env):
-    k, v = env.split("=")
-    child_env = dict(os.environ, **{k: v})
-    p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT}], env=child_env, capture_output=True,
+@pytest.mark.parametrize("env,cfg", [("SG_PIPELINE=0", 4), ("SG_STREAM_PRIO=1", 4), ("SG_STREAM_PRIO=0", 4),
+                                     ("SG_DEBUG_FLAGS=8192", 4), ("SG_DEBUG_FLAGS=8192", 6), ("SG_PQ=0", 5),
+                                     ("SG_MIX=0", 6), ("SG_MIX_PQ=0", 6), ("SG_PVT=0", 6), ("SG_PV=0 SG_PVT=1", 6)])
+def test_alternative_path_parity(env, cfg):
+    child_env = dict(os.environ)
+    for kv in env.split():
+        k, v = kv.split("=")
+        child_env[k] = v
+    p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "cfg": cfg}], env=child_env, capture_output=True,
                        text=True, timeout=110)
     assert p.returncode == 0 and p.stdout.startswith("ok"), p.stdout[-2000:] + p.stderr[-2000:]
