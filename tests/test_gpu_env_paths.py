@@ -7,8 +7,11 @@ engine (each runs in a child process; DESIGN.md §10 lists every switch):
   SG_PQ=0                  hot-parameter resources on the per-lane kernel (no k_pq)
   SG_MIX=0 / SG_MIX_PQ=0   mixed flow / degrade / param resources on one lane (no cooperative passes)
   SG_PV=0, SG_PVT=0        the value-parallel pre pass without its post pass, and the reverse
+  SG_DEBUG_FLAGS=4 / 8 / 16 / 128   no frozen-stretch skipping / the decide bins one after another on one stream /
+                           no closed-form guesses in the cooperative owners / the 512-lane k_pq for wide segments
+  SG_DEBUG_FLAGS=288       k_pq's map phases: sequential key walks (32) and the thread-count map sorted again (256)
 
-Each child replays a seeded trace (C4: DegradeRules + QPS rules; C5: hot-parameter rules; C6: mixed rules;
+Each child replays a seeded trace (C3: THREAD + rate-limiter rules with warm-up rate limiters; C4: DegradeRules + QPS rules; C5: hot-parameter rules; C6: mixed rules;
 several batches) through the HIP engine and the oracle and requires bit-identical decisions and node state.
 """
 import os
@@ -29,10 +32,10 @@ import pyoracle as O
 from sentinel_amd import engine as E
 from sentinel_amd import tracegen as T
 cfg = %(cfg)d
-w = T.Workload(cfg, n_entries=300_000, n_res={4: 30_000, 5: 1_000, 6: 3_000}[cfg],
-               **({"n_param_values": 200_000} if cfg != 4 else {}))
+w = T.Workload(cfg, n_entries=300_000, n_res={3: 2_000, 4: 30_000, 5: 1_000, 6: 3_000}[cfg],
+               **({"n_param_values": 200_000} if cfg in (5, 6) else {"variant": T.V_WARM_RL} if cfg == 3 else {}))
 eng = E.Engine(max_resources=w.n_res, max_slot_chain_size=0, status_ring_log2=24,
-               **({"param_table_log2": 24} if cfg != 4 else {}))
+               **({"param_table_log2": 24} if cfg in (5, 6) else {}))
 orc = O.Oracle(max_slot_chain_size=0)
 w.install(eng); w.install(orc)
 ev = w.events
@@ -51,7 +54,10 @@ print("ok", len(ev))
 
 @pytest.mark.parametrize("env,cfg", [("SG_PIPELINE=0", 4), ("SG_STREAM_PRIO=1", 4), ("SG_STREAM_PRIO=0", 4),
                                      ("SG_DEBUG_FLAGS=8192", 4), ("SG_DEBUG_FLAGS=8192", 6), ("SG_PQ=0", 5),
-                                     ("SG_MIX=0", 6), ("SG_MIX_PQ=0", 6), ("SG_PVT=0", 6), ("SG_PV=0 SG_PVT=1", 6)])
+                                     ("SG_MIX=0", 6), ("SG_MIX_PQ=0", 6), ("SG_PVT=0", 6), ("SG_PV=0 SG_PVT=1", 6),
+                                     ("SG_DEBUG_FLAGS=4", 3), ("SG_DEBUG_FLAGS=8", 4), ("SG_DEBUG_FLAGS=16", 3),
+                                     ("SG_DEBUG_FLAGS=128 SG_PQ_WIDE=512", 5),
+                                     ("SG_DEBUG_FLAGS=288", 5)])
 def test_alternative_path_parity(env, cfg):
     child_env = dict(os.environ)
     for kv in env.split():
