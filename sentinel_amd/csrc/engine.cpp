@@ -111,7 +111,7 @@ hipError_t launch_pv_a(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_
                        hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                    const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                        hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                       uint32_t tile, uint32_t* rest);
+                       uint32_t tile, uint32_t* rest, uint32_t grant_all);
 hipError_t launch_pv_b(SEv* recs, Seg* segs, const uint32_t* list, uint32_t m, const DevState& S, int64_t t0,
                        uint32_t* dec, uint32_t* bflags, PvSeg* pv, PvBuf B, uint32_t cap, uint32_t* tot, uint32_t* part,
                        uint32_t jumps, hipStream_t st,
@@ -654,7 +654,10 @@ struct sg_engine {
     bool pv_pq = true;          // SG_PV_PQ (default 1): XF_PVPQ programs' long segments through the value-parallel passes
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
     bool pv_on = true;          // SG_PV (default 1): the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
-    PvBuf pvb{};                // its scratch (decide stage only: one set)
+    PvBuf pvb{};                // its scratch: the pre pass's (launch_pv_a / _b) ...
+    PvBuf pvbt{};               // ... and the post pass's (launch_pvt), so that the next batch's extraction and sort
+                                // (launch_pv_a, early on bin_stream[1]) can run beside this batch's post pass
+    bool has_multi = false;     // some STRATEGY_RELATE component exists (PX_MULTI): launch_pv_a waits for the grants
     uint64_t pv_cap = 0;
     PvSeg* d_pvseg = nullptr;
     PvSeg* d_pvtseg = nullptr;  // the post pass's (pvalue.hip launch_pvt)
@@ -662,7 +665,7 @@ struct sg_engine {
     bool pvt_on = false;        // SG_PVT (default: SG_PV): the value-parallel post pass (thread-count maps)
     uint64_t pvseg_cap = 0;
     uint64_t pvch_cap = 0;      // pvalue.hip's extraction chunk arrays
-    uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr;
+    uint32_t *d_pvtot = nullptr, *d_pvhist = nullptr, *d_pvpart = nullptr, *d_pvthist = nullptr, *d_pvtpart = nullptr;
     uint32_t pv_last_m = 0;     // listed segments of the last batch that ran it (diagnostics)
     bool skip_pinned = false;   // SG_SKIP_MIN set: no per-batch adaptation
     // token server (cluster.hip): flowId table and ClusterMetric state in HBM, host mirror of the
@@ -1063,6 +1066,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
     // STRATEGY_RELATE components (co-locate the rule graph's connected components):
     // union-find over the references; every member sorts under the representative, one segment
     std::vector<uint32_t> comp;
+    bool any_multi = false;
     if (!relate.empty()) {
         comp.resize(R);
         for (uint32_t x = 0; x < R; ++x) comp[x] = x;
@@ -1080,6 +1084,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
         for (uint32_t x : members) {
             if (comp[x] == x) { prog[x].multi |= PX_MULTI; prog[x].pflags |= PF_SERIAL; }
         }
+        any_multi = !members.empty();
         // ClusterNode existence of the members from here on: NI_TOUCHED (a chain grant means an ENTRY of
         // the resource was decided in a finished batch: no batch is in flight during a rule load)
         std::vector<NodeInfo> ni(members.size());
@@ -1141,6 +1146,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
     HIPCHK(hipMemcpy(e->d_prog, prog.data(), R * sizeof(Prog), hipMemcpyHostToDevice));
     e->n_dev_rules = (uint32_t)rules.size();
     e->has_mix = any_mix;
+    e->has_multi = any_multi;
     if (comp.empty()) {
         dfree(e->d_comp);
         e->d_comp = nullptr;
@@ -2065,21 +2071,32 @@ int sg_load_param_rules(sg_engine* e, const sg_param_rule* rules, uint32_t n, ui
 
 // pvalue.hip's scratch for up to cap accesses of up to m listed segments (the decide stage's: a batch in flight may
 // still use the old arrays, so the stream drains first)
-static void free_pv(sg_engine* e) {
-    PvBuf& B = e->pvb;
+static void free_pvbuf(PvBuf& B) {
     dfree(B.key); dfree(B.pos); dfree(B.dt); dfree(B.acq); dfree(B.tc); dfree(B.seg); dfree(B.gid); dfree(B.idx);
     dfree(B.gid2); dfree(B.idx2); dfree(B.prev); dfree(B.w); dfree(B.sprev); dfree(B.sw); dfree(B.fslot); dfree(B.hit);
     dfree(B.keep); dfree(B.flast); dfree(B.ftok); dfree(B.htab); dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
-    dfree(B.gdt); dfree(B.gaw); dfree(B.gpos); dfree(B.range); dfree(e->d_pvhist); dfree(e->d_pvpart);
+    dfree(B.gdt); dfree(B.gaw); dfree(B.gpos); dfree(B.range);
     B = PvBuf{};
-    e->d_pvhist = e->d_pvpart = nullptr;
+}
+static void free_pv(sg_engine* e) {
+    free_pvbuf(e->pvb);
+    free_pvbuf(e->pvbt);
+    dfree(e->d_pvhist); dfree(e->d_pvpart); dfree(e->d_pvthist); dfree(e->d_pvtpart);
+    e->d_pvhist = e->d_pvpart = e->d_pvthist = e->d_pvtpart = nullptr;
     e->pv_cap = 0;
     e->pvch_cap = 0;
+}
+// every stream that may still read the scratch: the decide stream and the pre pass's
+static hipError_t drain_decide(sg_engine* e) {
+    hipError_t r = hipStreamSynchronize(e->stream);
+    for (auto s : e->bin_stream)
+        if (r == hipSuccess && s) r = hipStreamSynchronize(s);
+    return r;
 }
 // (grown with headroom: a reallocation drains the stream, so it must stay rare)
 static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
     if (m > e->pvseg_cap) {
-        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(drain_decide(e));
         dfree(e->d_pvseg);
         dfree(e->d_pvtseg);
         e->pvseg_cap = std::max<uint64_t>(m + m / 2, 1024);
@@ -2089,33 +2106,40 @@ static int ensure_pv(sg_engine* e, uint64_t cap, uint64_t m) {
         HIPCHK(hipMalloc(&e->d_pvrest, 2 * (e->pvseg_cap + 1) * 4));
     }
     if (!e->d_pvtot) HIPCHK(hipMalloc(&e->d_pvtot, 64));
-    PvBuf& B = e->pvb;
     if (cap > e->pv_cap) {
-        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(drain_decide(e));
         free_pv(e);
         const uint64_t c = std::max<uint64_t>(cap + cap / 4, 1u << 16);
-        HIPCHK(hipMalloc(&B.key, c * 8)); HIPCHK(hipMalloc(&B.pos, c * 4)); HIPCHK(hipMalloc(&B.dt, c * 4));
-        HIPCHK(hipMalloc(&B.acq, c * 4)); HIPCHK(hipMalloc(&B.tc, c * 4)); HIPCHK(hipMalloc(&B.seg, c * 4));
-        HIPCHK(hipMalloc(&B.gid, c * 4)); HIPCHK(hipMalloc(&B.idx, c * 4)); HIPCHK(hipMalloc(&B.gid2, c * 4));
-        HIPCHK(hipMalloc(&B.idx2, c * 4)); HIPCHK(hipMalloc(&B.prev, c * 4)); HIPCHK(hipMalloc(&B.w, c * 4));
-        HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
-        HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
-        HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
-        HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
-        HIPCHK(hipMalloc(&B.range, c * 16));
+        for (PvBuf* Bp : {&e->pvb, &e->pvbt}) {
+            PvBuf& B = *Bp;
+            HIPCHK(hipMalloc(&B.key, c * 8)); HIPCHK(hipMalloc(&B.pos, c * 4)); HIPCHK(hipMalloc(&B.dt, c * 4));
+            HIPCHK(hipMalloc(&B.acq, c * 4)); HIPCHK(hipMalloc(&B.tc, c * 4)); HIPCHK(hipMalloc(&B.seg, c * 4));
+            HIPCHK(hipMalloc(&B.gid, c * 4)); HIPCHK(hipMalloc(&B.idx, c * 4)); HIPCHK(hipMalloc(&B.gid2, c * 4));
+            HIPCHK(hipMalloc(&B.idx2, c * 4)); HIPCHK(hipMalloc(&B.prev, c * 4)); HIPCHK(hipMalloc(&B.w, c * 4));
+            HIPCHK(hipMalloc(&B.sprev, c * 4)); HIPCHK(hipMalloc(&B.sw, c * 4)); HIPCHK(hipMalloc(&B.fslot, c * 4));
+            HIPCHK(hipMalloc(&B.hit, c)); HIPCHK(hipMalloc(&B.keep, c)); HIPCHK(hipMalloc(&B.flast, c * 8));
+            HIPCHK(hipMalloc(&B.ftok, c * 4)); HIPCHK(hipMalloc(&B.htab, c * 16));
+            HIPCHK(hipMalloc(&B.gdt, c * 4)); HIPCHK(hipMalloc(&B.gaw, c * 4)); HIPCHK(hipMalloc(&B.gpos, c * 4));
+            HIPCHK(hipMalloc(&B.range, c * 16));
+        }
         const uint64_t nblocks = (c + radix_tile() - 1) / radix_tile();
         HIPCHK(hipMalloc(&e->d_pvhist, nblocks * 256 * 4));
         HIPCHK(hipMalloc(&e->d_pvpart, nblocks * 256 * 4 + 4096));
+        HIPCHK(hipMalloc(&e->d_pvthist, nblocks * 256 * 4));
+        HIPCHK(hipMalloc(&e->d_pvtpart, nblocks * 256 * 4 + 4096));
         e->pv_cap = c;
     }
     // chunks: cap / PV_CH (4096) + one per segment (launch_pv's grid: pv_cap / 4096 + m + 1)
     const uint64_t nch = e->pv_cap / 4096 + m + 16;
     if (nch > e->pvch_cap) {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
+        HIPCHK(drain_decide(e));
         e->pvch_cap = nch + nch / 2;
-        HIPCHK(hipMalloc(&B.chunk, e->pvch_cap * 8)); HIPCHK(hipMalloc(&B.ccnt, e->pvch_cap * 4));
-        HIPCHK(hipMalloc(&B.cof, e->pvch_cap * 4 + 4));
+        for (PvBuf* Bp : {&e->pvb, &e->pvbt}) {
+            PvBuf& B = *Bp;
+            dfree(B.chunk); dfree(B.ccnt); dfree(B.cof);
+            HIPCHK(hipMalloc(&B.chunk, e->pvch_cap * 8)); HIPCHK(hipMalloc(&B.ccnt, e->pvch_cap * 4));
+            HIPCHK(hipMalloc(&B.cof, e->pvch_cap * 4 + 4));
+        }
     }
     return SG_OK;
 }
@@ -2408,6 +2432,22 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const bool serial_bins = (e->dbg_flags & 8) != 0;
     const bool pre_split = (n_mix || n_mixw) && !serial_bins;
     hipStream_t ps = pre_split ? e->bin_stream[1] : st;
+    // the value-parallel pre pass's extraction and sort (launch_pv_a) read only this batch's records and the rules,
+    // so with every chain granted (k_pv_prep then knows the grants' outcome) they start as soon as this batch is
+    // grouped, on bin_stream[1] beside the previous batch's post pass (their own scratch, pvb; the post pass has pvbt)
+    const uint32_t grant_all = (e->cfg.switch_on && e->cfg.max_slot_chain_size <= 0) ? 1u : 0u;
+    if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
+        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
+        e->pv_last_m = n_mixw;
+    }
+    const bool pv_ran = n_mixw && e->pv_on && head[72];
+    const bool pv_early = pv_ran && pre_split && grant_all && !e->has_multi;
+    if (pv_early) {
+        HIPCHK(hipStreamWaitEvent(ps, B.ev[1], 0));
+        HIPCHK(launch_pv_a(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec, e->d_pvseg, e->pvb,
+                           head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, ps, launch_radix_hist_n,
+                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest, grant_all));
+    }
     HIPCHK(launch_resolve(e->d_prev, nprev, e->d_ring, e->d_recs, vin, dev_ext, st));
     // ---- chain cap (CtSph.lookProcessChain): grant chains in order of first ENTRY.  First on the decide stream: the
     // pre pass's eligibility reads the chain flags (it ran beside the grants and raced them)
@@ -2447,15 +2487,10 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         HIPCHK(hipEventRecord(e->fork0, st));
         HIPCHK(hipStreamWaitEvent(ps, e->fork0, 0));
     }
-    if (n_mixw && (e->pv_on || e->pvt_on) && head[72]) {
-        if (int prc = ensure_pv(e, head[72], n_mixw)) return prc;
-        e->pv_last_m = n_mixw;
-    }
-    const bool pv_ran = n_mixw && e->pv_on && head[72];
-    if (pv_ran)
+    if (pv_ran && !pv_early)
         HIPCHK(launch_pv_a(e->d_recs, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec, e->d_pvseg, e->pvb,
                            head[72], e->d_pvtot, e->d_pvhist, e->d_pvpart, ps, launch_radix_hist_n,
-                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest));
+                           launch_radix_scatter_n, launch_scan, radix_tile(), e->d_pvrest, grant_all));
     // param map regions grown for this batch's segments before anything touches a map; the pool's use, for the
     // compaction check of a later submit
     if (e->pool_nb) {
@@ -2561,7 +2596,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // where the maps do not overflow, pvalue.hip; the rest by k_pq's post pass)
     if (n_mixw && e->pvt_on && head[72])
         HIPCHK(launch_pvt(e->d_recs, dev_ev, vin, e->d_segs, B.d_mix + B.mix_cap, n_mixw, S, dc, e->d_dec,
-                          e->d_bsmall + 0, e->d_pvtseg, e->pvb, head[72], e->d_pvtot + 4, e->d_pvhist, e->d_pvpart, st,
+                          e->d_bsmall + 0, e->d_pvtseg, e->pvbt, head[72], e->d_pvtot + 4, e->d_pvthist, e->d_pvtpart, st,
                           launch_radix_hist_n, launch_radix_scatter_n, launch_scan, radix_tile(),
                           e->d_pvrest + e->pvseg_cap + 1));
     const bool pvt_ran = n_mixw && e->pvt_on && head[72];

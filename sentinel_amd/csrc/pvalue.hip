@@ -111,23 +111,40 @@ __device__ void pv_ring_prefix(const DevState& S, const PMap& mp, uint32_t* red)
         }
 }
 
-// ---- prep: one workgroup per listed segment: eligibility, the map's ring prefix counts, extraction chunks
+// ---- prep: one workgroup per listed segment: eligibility, extraction chunks (the map's ring prefix counts: k_pv_rpre)
+// The chain test is the state after this batch's grants (CtSph.lookProcessChain): with every chain granted
+// (grant_all, no STRATEGY_RELATE component in the list) a resource without NI_CHAIN gets one in this batch iff the
+// segment holds an ENTRY that looks its chain up (k_chain), so prep may run beside the grants (launch_pv_a early,
+// beside the previous batch's decide stage) and still routes every segment the same way.
 #define PV_CH 4096u  // positions per extraction chunk
-__global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
-                                                 DevState S, PvSeg* __restrict__ pv, uint32_t* __restrict__ rest) {
-    __shared__ uint32_t red[4];
-    __shared__ uint32_t okf;
+__global__ __launch_bounds__(256) void k_pv_prep(const SEv* __restrict__ recs, const uint32_t* __restrict__ vals,
+                                                 Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
+                                                 DevState S, PvSeg* __restrict__ pv, uint32_t* __restrict__ rest,
+                                                 uint32_t grant_all) {
+    __shared__ uint32_t okf, look;
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
     if (i >= m) return;
     const Seg sg = segs[list[i]];
     const Prog pg = S.prog[sg.res];
     const int k1 = pv_rule(S, pg);
-    if (tid == 0) {
-        // eligible: one checked rule, its map within the commit's LDS (<= PQ_MAX_CAP), no argument lists, a chain
-        uint32_t ok = k1 >= 0 && !(S.prio && (S.prio[sg.res] & PM_ARGL)) && (S.info[sg.res].flags & NI_CHAIN);
-        if (ok && S.pmap[S.rules[pg.rule_off + k1].pmap].cap > PQ_MAX_CAP) ok = 0;
-        okf = ok;
+    const uint32_t f = S.info[sg.res].flags;
+    // eligible: one checked rule, its map within the commit's LDS (<= PQ_MAX_CAP), no argument lists, a chain
+    uint32_t ok = k1 >= 0 && !(S.prio && (S.prio[sg.res] & PM_ARGL));
+    if (ok && S.pmap[S.rules[pg.rule_off + k1].pmap].cap > PQ_MAX_CAP) ok = 0;
+    bool chain = (f & NI_CHAIN) != 0;
+    if (ok && !chain && grant_all && !(f & NI_REJECTED) && !(pg.multi & PX_MULTI)) {
+        if (tid == 0) look = 0;
+        __syncthreads();
+        for (uint32_t p0 = 0; p0 < sg.len; p0 += 256) {  // (uniform trip count; the first ENTRY is near the start)
+            const uint32_t p = p0 + tid;
+            if (p < sg.len && recs[sg.start + p].kind == SG_EV_ENTRY &&
+                (!S.ext || S.ext[vals[sg.start + p] & 0x7FFFFFFFu].context_id <= S.max_ctx))
+                look = 1;
+            if (__syncthreads_or(look)) break;
+        }
+        chain = look != 0;
     }
+    if (tid == 0) okf = ok && chain;
     __syncthreads();
     if (!okf) {  // k_pq's pre pass: rest[1 + k], count rest[0] (an XF_PVPQ segment: k_pq's full pass decides it)
         if (tid == 0) {
@@ -139,13 +156,20 @@ __global__ __launch_bounds__(256) void k_pv_prep(Seg* __restrict__ segs, const u
         return;
     }
     const DRule& r = S.rules[pg.rule_off + k1];
-    pv_ring_prefix(S, S.pmap[r.pmap], red);
     if (tid == 0) {
         PvSeg o{};
         o.ok = 1; o.mid = r.pmap; o.rk = (uint32_t)k1; o.nch = (sg.len + PV_CH - 1) / PV_CH;
         pv[i] = o;
         segs[list[i]].bin = sg.bin | SEG_PV;  // (k_pq's pre pass leaves it)
     }
+}
+
+// the maps' ring prefix counts of the eligible segments (after the maps' growth: a map region moves)
+__global__ __launch_bounds__(256) void k_pv_rpre(const PvSeg* __restrict__ pv, uint32_t m, DevState S) {
+    __shared__ uint32_t red[4];
+    const uint32_t i = blockIdx.x;
+    if (i >= m || !pv[i].ok) return;
+    pv_ring_prefix(S, S.pmap[pv[i].mid], red);
 }
 
 // the chunk table: (listed segment, first position) of every chunk, segment by segment; tot[1] = chunks
@@ -1212,7 +1236,7 @@ hipError_t launch_pv_a(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_
                        hipError_t (*radix_scatter)(const uint32_t*, const uint32_t*, uint64_t, const uint32_t*, int,
                                                    const uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t),
                        hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
-                       uint32_t tile, uint32_t* rest) {
+                       uint32_t tile, uint32_t* rest, uint32_t grant_all) {
     if (!m || !cap) return hipSuccess;
     const uint32_t nchunk = cap / PV_CH + m + 1;
     hipError_t e = hipMemsetAsync(tot, 0, 16, st);
@@ -1220,7 +1244,7 @@ hipError_t launch_pv_a(SEv* recs, const uint32_t* vals, Seg* segs, const uint32_
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(rest, 0, 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, segs, list, m, S, pv, rest);
+    hipLaunchKernelGGL(k_pv_prep, dim3(m), dim3(256), 0, st, recs, vals, segs, list, m, S, pv, rest, grant_all);
     hipLaunchKernelGGL(k_pv_chunks, dim3(1), dim3(256), 0, st, pv, m, B, tot);
     hipLaunchKernelGGL(k_pv_count, dim3(nchunk), dim3(256), 0, st, recs, vals, segs, list, S, cfg, pv, B, tot, dec);
     hipLaunchKernelGGL(k_pv_offsets, dim3(1), dim3(256), 0, st, pv, m, B, tot);
@@ -1235,6 +1259,7 @@ hipError_t launch_pv_b(SEv* recs, Seg* segs, const uint32_t* list, uint32_t m, c
     if (!m || !cap) return hipSuccess;
     hipError_t e = hipSuccess;
     const uint32_t nb = (cap + 255) / 256;
+    hipLaunchKernelGGL(k_pv_rpre, dim3(m), dim3(256), 0, st, pv, m, S);
     hipLaunchKernelGGL(k_pv_prev, dim3(nb), dim3(256), 0, st, B, tot, pv, S);
     hipLaunchKernelGGL(k_pv_blocks, dim3((cap + PV_B - 1) / PV_B), dim3(PV_B), 0, st, B, tot);
     e = pv_resid(B, cap, tot, pv, S, part, st, scan);
