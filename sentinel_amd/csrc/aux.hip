@@ -584,12 +584,18 @@ hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, con
                       const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
                       int64_t t0, const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
                       uint32_t* bflags, hipStream_t st) {
-    hipLaunchKernelGGL(k_aux_cold, dim3(2048), dim3(256), 0, st, recs, segs, ashort, aux + 0, S, cfg, t0, dec, bflags);
+    if (ashort) hipLaunchKernelGGL(k_aux_cold, dim3(2048), dim3(256), 0, st, recs, segs, ashort, aux + 0, S, cfg, t0, dec, bflags);
     hipLaunchKernelGGL(k_aux_expand, dim3(512), dim3(256), 0, st, segs, along, aux + 3, apiece);
     hipLaunchKernelGGL(k_aux_piece, dim3(2048), dim3(256), 0, st, recs, segs, apiece, aux + 1, S, cfg, t0, dec, pool,
                        pool_cap, pool_n, meta, bflags);
     hipLaunchKernelGGL(k_aux_merge, dim3(256), dim3(256), 0, st, recs, segs, amulti, aux + 2, S, cfg, t0, dec, pool, meta,
                        bflags);
+    return hipGetLastError();
+}
+// the short segments' part alone (launch_aux then gets ashort = null)
+hipError_t launch_aux_cold(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort, const DevState& S,
+                           const DevCfg& cfg, int64_t t0, const uint32_t* dec, uint32_t* bflags, hipStream_t st) {
+    hipLaunchKernelGGL(k_aux_cold, dim3(2048), dim3(256), 0, st, recs, segs, ashort, aux + 0, S, cfg, t0, dec, bflags);
     return hipGetLastError();
 }
 } // namespace sg

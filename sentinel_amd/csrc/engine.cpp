@@ -89,6 +89,8 @@ hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, con
                       const uint64_t* along, uint64_t* apiece, const uint64_t* amulti, const DevState& S, const DevCfg& cfg,
                       int64_t t0, const uint32_t* dec, AuxAcc* pool, uint32_t pool_cap, uint32_t* pool_n, uint64_t* meta,
                       uint32_t* bflags, hipStream_t st);
+hipError_t launch_aux_cold(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort, const DevState& S,
+                           const DevCfg& cfg, int64_t t0, const uint32_t* dec, uint32_t* bflags, hipStream_t st);
 // param.hip
 hipError_t launch_pq(int wide, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                      const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* dec,
@@ -644,6 +646,8 @@ struct sg_engine {
     hipEvent_t fork0 = nullptr;  // XF_MIX batches: the pre passes on bin_stream[1] start here, beside the lane bins
     hipEvent_t grown = nullptr;  // ... and their map-touching part after the maps' growth
     bool pipeline = true;   // the group stage of batch k+1 overlaps the decide stage of batch k (SG_PIPELINE=0: off)
+    int j1_stream = -1;     // SG_J1_STREAM=1 / 0: J1 after J16 / J8 on bin_stream[0] / after the lane bins (default:
+                            // bin_stream[0] when the short aux nodes take the main stream, else the main stream)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
     bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
@@ -1281,6 +1285,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J1_MAX")) { e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
+    if (const char* v = std::getenv("SG_J1_STREAM")) e->j1_stream = std::atoi(v);
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX_PQ")) e->mix_pq = v[0] != '0';
@@ -2580,14 +2585,26 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     }
     if (!pre_split)
         if (int lrc = lane_bins()) return lrc;
+    // sg_submit_ex: the short segments' origin / context nodes (aux.hip k_aux_cold) need only the lane bins' verdicts
+    // when every short segment (<= AUX_SHORT = 256 events, decide.hip) is a lane one -- lane bins up to 256 events and
+    // no k_pq<4> segment -- so they go right after them, beside the owners
+    const bool aux_early = ext && !bin_n[BIN_PQ4] && !serial_bins && (force_lane || lane_max >= 256u);
+    if (aux_early)
+        HIPCHK(launch_aux_cold(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
+    // J1: after the lane bins on the main stream, or (SG_J1_STREAM=1, and with the short aux nodes on the main stream)
+    // after J16 / J8 on bin_stream[0]
+    const bool j1_b0 = bin_n[BIN_J1] && !serial_bins && (e->j1_stream == 1 || (e->j1_stream < 0 && aux_early));
     if (bin_n[BIN_J1]) {
         DevState Sj = S;
         Sj.dbg = (e->prof_bin == 2 && e->d_dbg) ? e->d_dbg : nullptr;
+        hipStream_t bs = j1_b0 ? e->bin_stream[0] : st;
+        if (j1_b0 && !(bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_PQ16])) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
         HIPCHK(launch_decide_bin(BIN_J1, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J1], bin_n[BIN_J1], Sj, dc,
-                                 t0, e->d_dec, e->d_bsmall + 0, st));
+                                 t0, e->d_dec, e->d_bsmall + 0, bs));
+        if (j1_b0) HIPCHK(hipEventRecord(e->join[0], bs));
     }
     for (int c = 0; c < 2; ++c)
-        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4] || (c == 0 && j8_own))
+        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4] || (c == 0 && (j8_own || j1_b0)))
             HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))
@@ -2606,9 +2623,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                              e->d_dec, e->d_bsmall + 0, st, pvt_ran ? prest + 1 : nullptr, prest));
     // origin / context nodes of the segments decided off k_lane<16>, from the committed verdicts (aux.hip)
     if (ext)
-        HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, B.d_along, B.d_apiece, B.d_amulti, S, dc,
-                          t0, e->d_dec, e->d_auxpool, e->auxpool_cap, e->d_bsmall + 134, e->d_auxmeta, e->d_bsmall + 0,
-                          st));
+        HIPCHK(launch_aux(e->d_recs, e->d_segs, e->d_bsmall + 130, aux_early ? nullptr : B.d_ashort, B.d_along, B.d_apiece,
+                          B.d_amulti, S, dc, t0, e->d_dec, e->d_auxpool, e->auxpool_cap, e->d_bsmall + 134, e->d_auxmeta,
+                          e->d_bsmall + 0, st));
     HIPCHK(hipEventRecord(B.ev[3], st));
     // ---- 4. decisions back to submission order + status ring
     if (B.radix) HIPCHK(launch_post(e->d_posof, e->d_dec, n, e->gbase, e->d_ring, ring_mask, dev_out, st));
