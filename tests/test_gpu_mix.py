@@ -211,3 +211,33 @@ def test_mix_ext_contexts():
     for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         _cmp(eng, orc, ev[a:b], "ext batch %d" % i, ext=ext[a:b])
     _nodes(eng, orc, range(n_res))
+
+
+@pytest.mark.parametrize("chain_cap", [0, 3])
+def test_mix_first_seen_wide_resource(chain_cap):
+    # The value-parallel pre pass's extraction runs beside the chain grants of its own batch (and beside the previous
+    # batch's post pass) when every chain is granted (chain_cap 0): k_pv_prep then decides the grant's outcome itself.
+    # x0 is absent from the first batch and a wide segment with no chain yet in the second; with chain_cap 3 the grants
+    # are host-side (CtSph's chain cap: some resources never get one) and the pre pass waits for them.
+    eng = E.Engine(max_resources=64, max_slot_chain_size=chain_cap, param_table_log2=22, status_ring_log2=24)
+    orc = O.Oracle(max_slot_chain_size=chain_cap)
+    for nm in NAMES:
+        assert eng.register(nm) == orc.register(nm)
+    f, d, p = _mix_rules(1e5)
+    for x in (eng, orc):
+        x.load_flow_rules(f)
+        x.load_degrade_rules(d)
+        x.load_param_rules(p)
+    t, gbase, pv = T0, 0, []
+    for b in range(3):
+        ev = _synthetic(300 + b, 40_000, gbase, len(NAMES), t=t)
+        if b == 0:
+            ev["res_id"][ev["res_id"] == 0] = 1  # (x1 takes x0's events: every reference stays one resource's)
+        gbase += len(ev)
+        _cmp(eng, orc, ev, "batch %d" % b)
+        pv.append(eng.pv_last())
+        t = int(ev["ts"].max()) + 1
+    _nodes(eng, orc, range(len(NAMES)))
+    _thread_maps(eng, orc, ev, [0, 1, 2])
+    if chain_cap == 0:  # x0's first batch went through the value-parallel pass
+        assert pv[1]["segments"] >= 1 and pv[1]["accesses"] > 10_000, pv
