@@ -24,8 +24,9 @@ resources partitioned over the ranks (strong scaling).  Every rank generates the
 keeps its shard (EXIT/TRACE references rewritten to its own numbering).  The partition is a resource ->
 rank table balanced by the event counts of a history window, the first global batch
 (sentinel_amd/dist.py balanced_table; --sharding
-hash: splitmix64(res_id) % N), and each rank submits its shard in rank-local batches of ~--batch-events
-events (a step is S / N of them per rank), so the ranks advance independently: the decision path has
+hash: splitmix64(res_id) % N), and each rank submits its shard either as one batch per global batch (~--batch-events
+/ N events, S a step: --rank-batches global, the default above N = 2) or in rank-local batches of ~--batch-events
+events (S / N a step: --rank-batches local, the default at N = 2), so the ranks advance independently: the decision path has
 no collective, and only the per-second MetricNode all-gather (RCCL) inside the timed chunks and the
 chunk barriers synchronise them.  The step time is the max over ranks and value = every rank's
 entries / that time.
@@ -77,6 +78,10 @@ def parse():
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
     p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rank-batches", choices=("auto", "local", "global"), default="auto",
+                   help="N > 1: 'local' = a rank submits its shard in batches of ~--batch-events (each spanning N global "
+                        "batches' time); 'global' = each global batch's shard is one batch of ~batch-events / N; 'auto' = "
+                        "local for N <= 2, global above (tools/shard_rehearsal.sh, DESIGN.md §7)")
     p.add_argument("--shard", default="", metavar="R/N",
                    help="rehearsal: run rank R's shard of an N-GPU run alone on this GPU (no collectives; "
                         "the per-rank step time of the N-GPU run, NOT a measurement of it)")
@@ -182,6 +187,11 @@ def main():
     LB = max(1, B // nparts)
     per_step = max(1, S // nparts)
     cuts = np.linspace(0, n_base, LB + 1).astype(np.int64)
+    rank_batches = args.rank_batches if args.rank_batches != "auto" else ("local" if nparts <= 2 else "global")
+    if nparts > 1 and rank_batches == "global":  # every global batch's shard as its own batch (S a step)
+        LB, per_step = B, S
+        cuts = np.searchsorted(pos, np.arange(B + 1, dtype=np.int64) * gb).astype(np.int64)
+        cuts[-1] = n_base
     sizes = np.diff(cuts)
     ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(LB)])
     res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(LB)])
@@ -362,6 +372,7 @@ def main():
                        "events_per_step": events / steps, "entries_per_step": entries / steps,
                        "resources_touched_per_batch": touched / nb, "base_batches": B,
                        "timed_chunks": chunks, "rank_local_batches_per_step": per_step,
+                       "rank_batches": rank_batches if nparts > 1 else None,
                        "parallelism": ("resource-sharded x%d (%s)" % (world, "balanced by the event counts of a "
                                                                       "history window: base batch 0 of %d" % B
                                                                       if args.sharding == "balanced" else
