@@ -25,8 +25,8 @@ keeps its shard (EXIT/TRACE references rewritten to its own numbering).  The par
 rank table balanced by the event counts of a history window, the first global batch
 (sentinel_amd/dist.py balanced_table; --sharding
 hash: splitmix64(res_id) % N), and each rank submits its shard either as one batch per global batch (~--batch-events
-/ N events, S a step: --rank-batches global, the default above N = 2) or in rank-local batches of ~--batch-events
-events (S / N a step: --rank-batches local, the default at N = 2), so the ranks advance independently: the decision path has
+/ N events, S a step: --rank-batches global, the default) or in rank-local batches of ~--batch-events
+events (S / N a step: --rank-batches local), so the ranks advance independently: the decision path has
 no collective, and only the per-second MetricNode all-gather (RCCL) inside the timed chunks and the
 chunk barriers synchronise them.  The step time is the max over ranks and value = every rank's
 entries / that time.
@@ -78,10 +78,10 @@ def parse():
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
     p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--rank-batches", choices=("auto", "local", "global"), default="auto",
-                   help="N > 1: 'local' = a rank submits its shard in batches of ~--batch-events (each spanning N global "
-                        "batches' time); 'global' = each global batch's shard is one batch of ~batch-events / N; 'auto' = "
-                        "local for N <= 2, global above (tools/shard_rehearsal.sh, DESIGN.md §7)")
+    p.add_argument("--rank-batches", default="auto",
+                   help="N > 1: global batches per rank batch -- an integer k (a rank's batch = its shard of k consecutive "
+                        "global batches, ~k * batch-events / N events), 'local' (k = N: batches of ~--batch-events), "
+                        "'global' (k = 1) or 'auto' (tools/shard_rehearsal.sh, DESIGN.md §7)")
     p.add_argument("--shard", default="", metavar="R/N",
                    help="rehearsal: run rank R's shard of an N-GPU run alone on this GPU (no collectives; "
                         "the per-rank step time of the N-GPU run, NOT a measurement of it)")
@@ -99,6 +99,11 @@ def src_sha() -> str:
                 with open(os.path.join(ROOT, d, f), "rb") as fh:
                     h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+# global batches per rank batch by N (bench --rank-batches auto): one at every N measured (tools/shard_rehearsal.sh,
+# N = 2 / 4 / 8 slowest rank 2.30 / 1.83 / 1.46 ms per global batch, against 2.45 / 2.16 / 1.90 with two)
+AUTO_RANK_BATCHES = {}
 
 
 def make_trace(n_res: int, batch_events: int, base_batches: int, seed: int):
@@ -187,10 +192,13 @@ def main():
     LB = max(1, B // nparts)
     per_step = max(1, S // nparts)
     cuts = np.linspace(0, n_base, LB + 1).astype(np.int64)
-    rank_batches = args.rank_batches if args.rank_batches != "auto" else ("local" if nparts <= 2 else "global")
-    if nparts > 1 and rank_batches == "global":  # every global batch's shard as its own batch (S a step)
-        LB, per_step = B, S
-        cuts = np.searchsorted(pos, np.arange(B + 1, dtype=np.int64) * gb).astype(np.int64)
+    rb = args.rank_batches
+    kb = nparts if rb == "local" else 1 if rb == "global" else AUTO_RANK_BATCHES.get(nparts, 1) if rb == "auto" else int(rb)
+    rank_batches = kb
+    if nparts > 1 and kb != nparts:  # a rank batch = the shard of kb consecutive global batches (S / kb a step)
+        assert kb >= 1 and B % kb == 0 and S % kb == 0, "--rank-batches k must divide --base-batches and --sub-batches"
+        LB, per_step = B // kb, S // kb
+        cuts = np.searchsorted(pos, np.arange(0, B + 1, kb, dtype=np.int64) * gb).astype(np.int64)
         cuts[-1] = n_base
     sizes = np.diff(cuts)
     ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(LB)])

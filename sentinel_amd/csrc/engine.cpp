@@ -706,6 +706,8 @@ struct sg_engine {
 
 namespace {
 
+constexpr uint64_t SHARD_BATCH = 3ull << 21;  // batches of fewer events take the shard-sized bins and skip threshold
+
 static void activate(sg_engine* e, int k) {
     auto& B = e->slot[k];
     e->d_ev = B.d_ev; e->d_out = B.d_out;
@@ -2332,11 +2334,13 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     const uint32_t nblk = (mb + 255) / 256;
     // Bin thresholds by batch size: a full batch (C4: 2^25 events) keeps the decide stage busy with event
     // throughput, and wider owners for shorter segments cost more than they save (measured); in a batch of
-    // fewer than 2^24 events -- one rank's shard of a multi-GPU step -- the longest owner chains bound it
+    // fewer than SHARD_BATCH (6.3M) events -- one rank's shard of a multi-GPU step -- the longest owner chains bound it
     // instead, so segments get wider owners sooner (tools/shard_rehearsal.sh: 8-way shards of C4, mean
     // rank step 1.70 -> 1.33 ms, slowest 1.85 -> 1.73 ms).
     uint32_t lane_max = e->lane_max, j1_max = e->j1_max, j4_max = e->j4_max;
-    if (!e->bins_pinned && n < (1ull << 24)) {
+    // (below SHARD_BATCH events: an 8-way shard of a 2^25-event global batch is ~2^22; a 4-way shard's 2^23 runs
+    // faster with the full-batch bins: 4-way rehearsal 2.24 -> 1.79 ms per global batch)
+    if (!e->bins_pinned && n < SHARD_BATCH) {
         lane_max = std::min<uint32_t>(lane_max, 128);
         j1_max = std::min<uint32_t>(j1_max, 1024);
         j4_max = std::min<uint32_t>(j4_max, 4096);
@@ -2422,7 +2426,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     S.skip_ok = !(bflags & (BF_MULTI_LINK | BF_ZERO_CNT)) && !(e->dbg_flags & 4) ? 1u : 0u;
     // a shard-sized batch (see the bins above) is bound by its longest owners, whose frozen stretches are
     // cheaper skipped than streamed from 8192 positions on (8-way C4 shards: slowest rank 1.79 -> 1.69 ms)
-    S.skip_min = (!e->skip_pinned && n < (1ull << 24)) ? std::min<uint32_t>(e->skip_min, 8192) : e->skip_min;
+    S.skip_min = (!e->skip_pinned && n < SHARD_BATCH) ? std::min<uint32_t>(e->skip_min, 8192) : e->skip_min;
     S.ext = dev_ext;
     S.args = dev_args;
     S.aux_tab = e->d_auxtab;

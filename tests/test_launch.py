@@ -92,14 +92,16 @@ def test_bench_rejects_a_world_that_is_not_gpus():
 
 
 @pytest.mark.gpu
-def test_bench_gpus2_launches_two_ranks():
+@pytest.mark.parametrize("rank_batches,k", [("auto", 1), ("local", 2)])
+def test_bench_gpus2_launches_two_ranks(rank_batches, k):
+    # each global batch's shard as one batch (the default) and rank-local batches of ~--batch-events
     env = dict(os.environ, SG_BENCH_GLOO="1")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)
+    for key in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(key, None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--resources", "20000",
                         "--batch-events", str(1 << 20), "--base-batches", "2", "--sub-batches", "2", "--steps", "2",
-                        "--warmup", "1", "--no-configs", "--no-cpu-baseline"], env=env, capture_output=True,
-                       text=True, timeout=600)
+                        "--warmup", "1", "--no-configs", "--no-cpu-baseline", "--rank-batches", rank_batches], env=env,
+                       capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-4000:]
@@ -108,3 +110,4 @@ def test_bench_gpus2_launches_two_ranks():
     assert len(j["config"]["rank_event_shares"]) == 2
     assert j["metric_gathers"]["count"] >= 1
     assert j["value"] > 0
+    assert j["config"]["rank_batches"] == k and j["config"]["rank_local_batches_per_step"] == 2 // k
