@@ -763,7 +763,7 @@ int ensure_batch(sg_engine* e, uint64_t n) {
     }
     dfree(e->d_hot_part);
     dfree(e->d_hot_hb);
-    HIPCHK(hipMalloc(&e->d_hot_part, (nblocks / 64 + 2) * hot_max() * 4));
+    HIPCHK(hipMalloc(&e->d_hot_part, (nblocks / 16 + 2) * hot_max() * 4));  // (HS_TC >= 16 tiles a chunk)
     HIPCHK(hipMalloc(&e->d_hot_hb, 2 * hot_max() * 4));
     for (auto& B : e->slot) {
         HIPCHK(hipMalloc(&B.d_blkcnt, ((c + 255) / 256 + 1) * N_BINS * 4));

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_grp_first(const sg_event* __rest
 // ---- the hot runs' sorted positions: the tile-major counts C[tile][h] become P[tile][h] = the first position of
 // tile's run of hot id h = sum over h' < h of h''s total + sum over tiles < tile of C[.][h] (hot ids in order,
 // each in tile order).  Reduce-then-scan along the tiles, TC tiles a chunk, rows read and written contiguous.
-#define HS_TC 64u
+#define HS_TC 16u  // (16 tiles a chunk: 512 chunks of a 2^25-event batch; 64 measured ~1 % slower in the pipeline)
 // partial sums of every chunk: part[chunk][h]
 __global__ __launch_bounds__(256) void k_hot_scan_a(const uint32_t* __restrict__ C, uint32_t nblocks, uint32_t nhot,
                                                     uint32_t* __restrict__ part) {
