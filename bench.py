@@ -106,6 +106,32 @@ def src_sha() -> str:
 AUTO_RANK_BATCHES = {}
 
 
+def rank_batch_k(spec: str, nparts: int) -> int:
+    """--rank-batches: global batches per rank batch (local = N, global = 1, auto by N, or an integer)."""
+    if spec == "local":
+        return nparts
+    if spec == "global":
+        return 1
+    if spec == "auto":
+        return AUTO_RANK_BATCHES.get(nparts, 1)
+    return int(spec)
+
+
+def rank_batch_cuts(pos, n_base: int, gb: int, B: int, S: int, nparts: int, kb: int):
+    """A rank's batches of its shard of the B base batches: (batches LB, batches a step, event cuts [LB + 1]).
+
+    k = N (or one GPU): B / N batches of ~gb events cut evenly (each spans N global batches' time, S / N a step);
+    otherwise the shard of kb consecutive global batches each (pos: the shard's global event positions), S / kb a step.
+    """
+    if nparts <= 1 or kb == nparts:
+        LB = max(1, B // nparts)
+        return LB, max(1, S // nparts), np.linspace(0, n_base, LB + 1).astype(np.int64)
+    assert kb >= 1 and B % kb == 0 and S % kb == 0, "--rank-batches k must divide --base-batches and --sub-batches"
+    cuts = np.searchsorted(pos, np.arange(0, B + 1, kb, dtype=np.int64) * gb).astype(np.int64)
+    cuts[-1] = n_base
+    return B // kb, S // kb, cuts
+
+
 def make_trace(n_res: int, batch_events: int, base_batches: int, seed: int):
     """The C4 trace, cut to base_batches whole global batches (the Workload owns the memory)."""
     from sentinel_amd import tracegen as T
@@ -188,18 +214,9 @@ def main():
     else:
         mine = ev
     n_base = len(mine)
-    # rank-local batches: the shard of the B base batches in B / N batches of ~gb events (a step is S / N of them)
-    LB = max(1, B // nparts)
-    per_step = max(1, S // nparts)
-    cuts = np.linspace(0, n_base, LB + 1).astype(np.int64)
-    rb = args.rank_batches
-    kb = nparts if rb == "local" else 1 if rb == "global" else AUTO_RANK_BATCHES.get(nparts, 1) if rb == "auto" else int(rb)
+    kb = rank_batch_k(args.rank_batches, nparts)
     rank_batches = kb
-    if nparts > 1 and kb != nparts:  # a rank batch = the shard of kb consecutive global batches (S / kb a step)
-        assert kb >= 1 and B % kb == 0 and S % kb == 0, "--rank-batches k must divide --base-batches and --sub-batches"
-        LB, per_step = B // kb, S // kb
-        cuts = np.searchsorted(pos, np.arange(0, B + 1, kb, dtype=np.int64) * gb).astype(np.int64)
-        cuts[-1] = n_base
+    LB, per_step, cuts = rank_batch_cuts(pos if nparts > 1 else None, n_base, gb, B, S, nparts, kb)
     sizes = np.diff(cuts)
     ent_b = np.array([int((mine["kind"][cuts[b]:cuts[b + 1]] == 0).sum()) for b in range(LB)])
     res_b = np.array([len(np.unique(mine["res_id"][cuts[b]:cuts[b + 1]])) for b in range(LB)])
