@@ -58,6 +58,8 @@ hipError_t launch_hot_segs(const uint32_t* hb, uint32_t nhot, const uint32_t* ho
 hipError_t launch_hot_build(const Seg* segs, const uint32_t* mp, uint32_t mb, uint32_t min_len, uint32_t max_res, uint16_t* hot_tab,
                             uint32_t* hot_list, uint32_t nhot_old, uint32_t* hot_n, hipStream_t st);
 hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, hipStream_t st);
+hipError_t launch_cold_small(const uint32_t* kin, const uint32_t* vin, const uint32_t* cnt, const uint32_t* dbase,
+                             uint32_t* kout, uint32_t* vout, uint32_t* words, hipStream_t st);
 uint32_t hot_max();
 hipError_t launch_seg_cold(const uint32_t* keys, uint64_t n, const uint32_t* lo, const uint32_t* sbase, uint32_t* flag,
                            uint32_t* pos, Seg* segs, hipStream_t st,
@@ -2306,7 +2308,12 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
                                 words, hot_off, e->d_k1, e->d_v1, ccnt, e->d_hist, gs));
         HIPCHK(launch_hot_scan(hot_off, nblocks, nhot, e->d_hot_part, e->d_hot_hb, e->d_bsmall + 77, gs));
         HIPCHK(launch_cold_n(n, e->d_bsmall + 77, e->d_bsmall + 78, gs));
-        for (int p = 0; p < passes; ++p) {  // the cold (key, index) pairs
+        if (nblocks == 1) {  // one tile: the cold pairs sorted by one workgroup (k_cold_small), into k0 / v0
+            HIPCHK(launch_cold_small(kin, vin, ccnt, e->d_bsmall + 77, kout, vout, words, gs));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        for (int p = 0; p < passes && nblocks > 1; ++p) {  // the cold (key, index) pairs
             if (p > 0) HIPCHK(launch_radix_hist_n(kin, n, e->d_bsmall + 78, p * db, e->d_hist, nblocks, gs));
             HIPCHK(launch_scan(e->d_hist, e->d_hist, (uint64_t)nblocks << db, e->d_part, nullptr, gs));
             const bool last = p == passes - 1;

@@ -1132,6 +1132,45 @@ hipError_t launch_cold_n(uint64_t n, const uint32_t* hot_total, uint32_t* out, h
     return hipGetLastError();
 }
 uint32_t hot_max() { return HOT_MAX; }
+
+// A batch of one tile (n <= RS_TILE, the drop-in's synchronous calls): its cold (key, index) pairs -- compacted at
+// the tile's start by k_grp_first, *cnt of them -- sorted in one workgroup instead of the radix passes' ~14 launches.
+// A bitonic sort of (key << 32 | input position) is the stable sort by key the passes make; the outputs are the last
+// pass's: sorted keys and values at *dbase + rank, and each cold event's word = its position | W_ENT.
+__global__ __launch_bounds__(1024) void k_cold_small(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ dbase,
+                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                     uint32_t* __restrict__ words) {
+    __shared__ unsigned long long s[RS_TILE];
+    const uint32_t cnt = *cnt_p, ob = *dbase, t = threadIdx.x;
+    uint32_t n2 = 1;
+    while (n2 < cnt) n2 <<= 1;
+    for (uint32_t i = t; i < n2; i += blockDim.x)
+        s[i] = i < cnt ? (((unsigned long long)kin[i] << 32) | i) : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < n2; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const unsigned long long a = s[i], b = s[l];
+                    if (((i & k) == 0) == (a > b)) { s[i] = b; s[l] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t i = t; i < cnt; i += blockDim.x) {
+        const uint32_t idx = (uint32_t)s[i], key = (uint32_t)(s[i] >> 32), v = vin[idx], dst = ob + i;
+        kout[dst] = key;
+        vout[dst] = v;
+        words[v & 0x7FFFFFFFu] = dst | ((v >> 1) & W_ENT);
+    }
+}
+hipError_t launch_cold_small(const uint32_t* kin, const uint32_t* vin, const uint32_t* cnt, const uint32_t* dbase,
+                             uint32_t* kout, uint32_t* vout, uint32_t* words, hipStream_t st) {
+    hipLaunchKernelGGL(k_cold_small, dim3(1), dim3(1024), 0, st, kin, vin, cnt, dbase, kout, vout, words);
+    return hipGetLastError();
+}
 hipError_t launch_post_w(const uint32_t* words, const uint32_t* P, uint32_t nhot, const uint32_t* dec, uint64_t n,
                          uint64_t gbase, uint8_t* ring, uint64_t ring_mask, uint32_t* out, hipStream_t st) {
     const uint32_t nb = (uint32_t)((n + 256 * POSTW_ITEMS - 1) / (256 * POSTW_ITEMS));
@@ -1159,8 +1198,34 @@ hipError_t launch_region_copy(const uint64_t* src, uint64_t* dst, const uint64_t
 }
 
 // exclusive scan in -> out (may alias); part must hold ceil(n / SC_TILE) + 1 words
+// one tile (n <= SC_TILE): the whole exclusive scan in one workgroup (small batches' scans: one launch, not three)
+__global__ __launch_bounds__(SC_THREADS) void k_scan_one(const uint32_t* __restrict__ in, uint64_t n,
+                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ total) {
+    const uint64_t base = (uint64_t)threadIdx.x * SC_ITEMS;
+    uint32_t loc[SC_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const uint64_t i = base + k;
+        loc[k] = i < n ? in[i] : 0;
+        s += loc[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(s, &tot);  // (its barriers: every item is read before any is written, in == out)
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) {
+        const uint64_t i = base + k;
+        if (i < n) out[i] = ex;
+        ex += loc[k];
+    }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* part, uint32_t* total,
                        hipStream_t st) {
+    if (n <= SC_TILE) {
+        hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(SC_THREADS), 0, st, in, n, out, total);
+        return hipGetLastError();
+    }
     uint32_t nb = (uint32_t)((n + SC_TILE - 1) / SC_TILE);
     if (nb == 0) nb = 1;
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SC_THREADS), 0, st, in, n, part, (const uint32_t*)nullptr);

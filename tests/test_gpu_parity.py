@@ -198,7 +198,7 @@ def test_many_small_batches_and_single_events(bin_mode):
     ev = w.events
     dg, do = [], []
     i = 0
-    sizes = [1, 2, 3, 64, 65, 127, 1000, 4097]
+    sizes = [1, 2, 3, 64, 65, 127, 1000, 4097, 4096, 4095]  # (one tile: k_cold_small; more: the radix passes)
     k = 0
     while i < len(ev):
         s = sizes[k % len(sizes)]
