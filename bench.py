@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--cpu-sample-events", type=int, default=24_000_000)
     p.add_argument("--cpu-single-events", type=int, default=6_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--balance-alpha", type=float, default=0.9,
+                   help="--sharding balanced: a resource's load = its history-window events ** alpha")
     p.add_argument("--rank-batches", default="auto",
                    help="N > 1: global batches per rank batch -- an integer k (a rank's batch = its shard of k consecutive "
                         "global batches, ~k * batch-events / N events), 'local' (k = N: batches of ~--batch-events), "
@@ -209,7 +211,8 @@ def main():
         # global batch only (a router knows past load, not the future), so 7/8 of the timed events are
         # batches the partition never saw (not the timed trace)
         if args.sharding == "balanced":
-            table = D.balanced_table(np.bincount(ev["res_id"][:gb], minlength=args.resources), nparts)
+            table = D.balanced_table(np.bincount(ev["res_id"][:gb], minlength=args.resources), nparts,
+                                     args.balance_alpha)
         mine, pos = D.shard_stream(ev, nparts, me, table)
     else:
         mine = ev

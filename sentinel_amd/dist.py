@@ -45,17 +45,19 @@ def shard_of(res_ids, world: int, table=None) -> np.ndarray:
     return np.where(t >= 0, t, h)
 
 
-def balanced_table(counts, world: int) -> np.ndarray:
+def balanced_table(counts, world: int, alpha: float = 1.0) -> np.ndarray:
     """A resource -> rank table from per-resource event counts: largest first onto the least loaded rank
-    (longest-processing-time greedy); resources with no events stay on their hash rank (-1)."""
+    (longest-processing-time greedy) with a resource's load counts**alpha (alpha < 1: a long segment costs less per
+    event -- its owner skips the frozen rest of each round); resources with no events stay on their hash rank (-1)."""
     counts = np.asarray(counts, dtype=np.int64)
     table = np.full(len(counts), -1, dtype=np.int64)
-    load = np.zeros(world, dtype=np.int64)
+    load = np.zeros(world, dtype=np.float64)
     seen = np.nonzero(counts)[0]
+    cost = counts.astype(np.float64) ** alpha
     for r in seen[np.argsort(-counts[seen], kind="stable")]:
         k = int(np.argmin(load))
         table[r] = k
-        load[k] += counts[r]
+        load[k] += cost[r]
     return table
 
 

@@ -42,3 +42,15 @@ def test_k_must_divide():
     pos = _shard(8000, 4, 0)
     with pytest.raises(AssertionError):
         bench.rank_batch_cuts(pos, len(pos), 1000, 8, 16, 4, 3)
+
+
+def test_balanced_table_alpha():
+    # a resource's load = its events ** alpha: below 1 the hottest resource's rank takes more of the others
+    from sentinel_amd import dist as D
+    counts = np.array([10_000] + [100] * 400)
+    t1 = D.balanced_table(counts, 4)
+    t9 = D.balanced_table(counts, 4, 0.5)
+    assert t1[0] == t9[0]
+    assert (t9 == t9[0]).sum() > (t1 == t1[0]).sum()
+    for t in (t1, t9):
+        assert set(np.unique(t)) == {0, 1, 2, 3}

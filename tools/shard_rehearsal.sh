@@ -2,14 +2,14 @@
 # Per-rank step time of an N-GPU strong-scaling bench, rehearsed on one GPU: every rank's shard of the
 # C4 trace (bench.py --shard R/N) run alone, one after another.  The N-GPU step is the slowest rank's
 # (plus the MetricNode all-gather); this is a prediction, never a measurement of the N-GPU run.
-# usage: [SHARDING=hash] [RANKB=global] tools/shard_rehearsal.sh TAG N [N ...]   (default: the balanced resource table)
+# usage: [SHARDING=hash] [RANKB=global] [ALPHA=0.9] tools/shard_rehearsal.sh TAG N [N ...]   (default: the balanced resource table)
 set -e
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for N in "$@"; do
     for R in $(seq 0 $((N - 1))); do
-        timeout -k 10 200 python bench.py --shard $R/$N --steps 3 --warmup 1 --no-cpu-baseline --no-configs --sub-batches 16 --base-batches 8 ${SHARDING:+--sharding $SHARDING} ${RANKB:+--rank-batches $RANKB} > $OUT/s${R}_of_$N.json 2> $OUT/s${R}_of_$N.err
+        timeout -k 10 200 python bench.py --shard $R/$N --steps 3 --warmup 1 --no-cpu-baseline --no-configs --sub-batches 16 --base-batches 8 ${SHARDING:+--sharding $SHARDING} ${RANKB:+--rank-batches $RANKB} ${ALPHA:+--balance-alpha $ALPHA} > $OUT/s${R}_of_$N.json 2> $OUT/s${R}_of_$N.err
     done
     python3 - $OUT $N <<'PY'
 import json, sys
