@@ -58,7 +58,8 @@ print("ok", len(ev))
                                      ("SG_MIX=0", 6), ("SG_MIX_PQ=0", 6), ("SG_PVT=0", 6), ("SG_PV=0 SG_PVT=1", 6),
                                      ("SG_DEBUG_FLAGS=4", 3), ("SG_DEBUG_FLAGS=8", 4), ("SG_DEBUG_FLAGS=16", 3),
                                      ("SG_DEBUG_FLAGS=128 SG_PQ_WIDE=512", 5),
-                                     ("SG_DEBUG_FLAGS=288", 5), ("SG_J1_STREAM=1", 4), ("SG_J1_STREAM=1", 3)])
+                                     ("SG_DEBUG_FLAGS=288", 5), ("SG_J1_STREAM=1", 4), ("SG_J1_STREAM=1", 3),
+                                     ("SG_PIPELINE=0", 6), ("SG_STREAM_PRIO=0", 6)])
 def test_alternative_path_parity(env, cfg):
     child_env = dict(os.environ)
     for kv in env.split():
