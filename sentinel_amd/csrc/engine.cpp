@@ -2599,7 +2599,9 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // sg_submit_ex: the short segments' origin / context nodes (aux.hip k_aux_cold) need only the lane bins' verdicts
     // when every short segment (<= AUX_SHORT = 256 events, decide.hip) is a lane one -- lane bins up to 256 events and
     // no k_pq<4> segment -- so they go right after them, beside the owners
-    const bool aux_early = ext && !bin_n[BIN_PQ4] && !serial_bins && (force_lane || lane_max >= 256u);
+    // (a short PF_PQ segment on k_pq<16>, SG_PQ_WIDE below 256, is not a lane one either: ADVICE r5)
+    const bool aux_early = ext && !bin_n[BIN_PQ4] && !serial_bins && (force_lane || lane_max >= 256u) &&
+                           (!bin_n[BIN_PQ16] || e->pq_wide >= 256u);
     if (aux_early)
         HIPCHK(launch_aux_cold(e->d_recs, e->d_segs, e->d_bsmall + 130, B.d_ashort, S, dc, t0, e->d_dec, e->d_bsmall + 0, st));
     // J1: after the lane bins on the main stream, or (SG_J1_STREAM=1, and with the short aux nodes on the main stream)

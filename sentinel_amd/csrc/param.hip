@@ -1730,11 +1730,14 @@ __global__ void k_pm_grow_ids(const uint32_t* __restrict__ ids, uint32_t n, DevS
 // ctl = null) the pools then swap; inside a batch whose growth found the pool short (ctl[PC_RESCUE] = epoch: every
 // kernel of the chain returns at once otherwise) the compacted prefix is copied back (k_pc_back), so the kernels
 // already queued with this pool's address see the maps in place.
+// (grid-stride over the maps: inside a batch the chain is launched every time and must cost a few microseconds when
+// no rescue is due; cnt (optional): the scan's device count, n on a rescue and 0 otherwise)
 __global__ void k_pc_nb(const PMap* __restrict__ pm, uint32_t n, uint32_t* __restrict__ sz,
-                        const unsigned long long* __restrict__ ctl, uint32_t epoch) {
-    if (ctl && ctl[PC_RESCUE] != epoch) return;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) sz[i] = pm[i].nb;
+                        const unsigned long long* __restrict__ ctl, uint32_t epoch, uint32_t* __restrict__ cnt) {
+    const bool go = !ctl || ctl[PC_RESCUE] == epoch;
+    if (cnt && blockIdx.x == 0 && threadIdx.x == 0) *cnt = go ? n : 0u;
+    if (!go) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) sz[i] = pm[i].nb;
 }
 // a wavefront per map: buckets (128 B) and values (8 x 16 B a bucket) as 16-byte words; the header's base last
 __global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t n, const uint32_t* __restrict__ off,
@@ -1743,8 +1746,8 @@ __global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t
                                                  unsigned long long* __restrict__ pool_next, uint32_t cond,
                                                  uint32_t epoch) {
     if (cond && pool_next[PC_RESCUE] != epoch) return;
-    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
-    if (i >= n) return;
+    const uint32_t l = threadIdx.x & 63;
+    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {  // (a wavefront per map)
     const PMap m = pm[i];
     const uint64_t nb = off[i];
     const uint4* sb = reinterpret_cast<const uint4*>(ob + m.base);
@@ -1759,6 +1762,7 @@ __global__ __launch_bounds__(256) void k_pc_copy(PMap* __restrict__ pm, uint32_t
             pool_next[PC_NEXT] = nb + m.nb;
             pool_next[PC_FLOOR] = nb + m.nb;
         }
+    }
     }
 }
 // the rescue's copy back: the compacted prefix [0, ctl[PC_NEXT]) of the other pool over this one
@@ -1780,6 +1784,8 @@ __global__ __launch_bounds__(256) void k_pc_back(PBucket* __restrict__ b1, PData
 }
 
 namespace sg {
+hipError_t launch_scan_n(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* ndev, uint32_t* part,
+                         uint32_t* total, hipStream_t st);  // kernels.hip
 // mv / nmv / mcap: the move list (null: each lane moves its maps itself)
 // The batch's map growth (pool_next = the pool's control words): a first pass; then, only if that pass found the pool
 // short, the compaction into the other pool (b2 / d2), its copy back and a second pass (every kernel of the rescue
@@ -1800,11 +1806,15 @@ hipError_t launch_pm_grow(const Seg* segs, const uint32_t* mp, uint32_t mb, cons
                            mv, nmv, mcap, epoch, second);
         if (mv) hipLaunchKernelGGL(k_pm_move_list, dim3(mcap < 16384 ? (mcap + 3) / 4 : 4096), dim3(256), 0, st, mv, nmv, mcap, S, bflags);
         if (second || !nm || !b2) break;
-        hipLaunchKernelGGL(k_pc_nb, dim3((nm + 255) / 256), dim3(256), 0, st, S.pmap, nm, sz,
-                           (const unsigned long long*)pool_next, epoch);
-        const hipError_t e = scan(sz, off, nm, part, nullptr, st);
+        // (a fixed small grid each: a batch without a rescue pays a few microseconds for the chain, not a grid over
+        // every map; the scan runs over the device count, 0 then)
+        uint32_t* cnt = part + mcap + 4095;  // (part: mcap + 4096 words, the scan uses nm / 4096 + 2 of them)
+        const uint32_t gnb = std::min<uint32_t>((nm + 255) / 256, 1024u), gcp = std::min<uint32_t>((nm + 3) / 4, 2048u);
+        hipLaunchKernelGGL(k_pc_nb, dim3(gnb), dim3(256), 0, st, S.pmap, nm, sz, (const unsigned long long*)pool_next,
+                           epoch, cnt);
+        const hipError_t e = launch_scan_n(sz, off, nm, cnt, part, nullptr, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_pc_copy, dim3((nm + 3) / 4), dim3(256), 0, st, S.pmap, nm, off, S.pbkt, S.pdat, b2, d2,
+        hipLaunchKernelGGL(k_pc_copy, dim3(gcp), dim3(256), 0, st, S.pmap, nm, off, S.pbkt, S.pdat, b2, d2,
                            pool_next, 1u, epoch);
         hipLaunchKernelGGL(k_pc_back, dim3(2048), dim3(256), 0, st, S.pbkt, S.pdat, b2, d2, pool_next, epoch);
     }
@@ -1816,10 +1826,12 @@ hipError_t launch_pm_compact(PMap* pm, uint32_t n, const PBucket* ob, const PDat
                              hipError_t (*scan)(const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t*, hipStream_t),
                              hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pc_nb, dim3((n + 255) / 256), dim3(256), 0, st, pm, n, sz, (const unsigned long long*)nullptr, 0u);
+    hipLaunchKernelGGL(k_pc_nb, dim3(std::min<uint32_t>((n + 255) / 256, 1024u)), dim3(256), 0, st, pm, n, sz,
+                       (const unsigned long long*)nullptr, 0u, (uint32_t*)nullptr);
     const hipError_t e = scan(sz, off, n, part, nullptr, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pc_copy, dim3((n + 3) / 4), dim3(256), 0, st, pm, n, off, ob, od, nbk, nd, pool_next, 0u, 0u);
+    hipLaunchKernelGGL(k_pc_copy, dim3(std::min<uint32_t>((n + 3) / 4, 2048u)), dim3(256), 0, st, pm, n, off, ob, od, nbk,
+                       nd, pool_next, 0u, 0u);
     return hipGetLastError();
 }
 hipError_t launch_pm_grow_ids(const uint32_t* ids, uint32_t n, const DevState& S, unsigned long long* pool_next,

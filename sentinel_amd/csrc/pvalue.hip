@@ -121,20 +121,27 @@ __global__ __launch_bounds__(256) void k_pv_prep(const SEv* __restrict__ recs, c
                                                  Seg* __restrict__ segs, const uint32_t* __restrict__ list, uint32_t m,
                                                  DevState S, PvSeg* __restrict__ pv, uint32_t* __restrict__ rest,
                                                  uint32_t grant_all) {
-    __shared__ uint32_t okf, look;
+    __shared__ uint32_t okf, look, scan_f;
     const uint32_t i = blockIdx.x, tid = threadIdx.x;
     if (i >= m) return;
     const Seg sg = segs[list[i]];
     const Prog pg = S.prog[sg.res];
     const int k1 = pv_rule(S, pg);
-    const uint32_t f = S.info[sg.res].flags;
-    // eligible: one checked rule, its map within the commit's LDS (<= PQ_MAX_CAP), no argument lists, a chain
-    uint32_t ok = k1 >= 0 && !(S.prio && (S.prio[sg.res] & PM_ARGL));
-    if (ok && S.pmap[S.rules[pg.rule_off + k1].pmap].cap > PQ_MAX_CAP) ok = 0;
-    bool chain = (f & NI_CHAIN) != 0;
-    if (ok && !chain && grant_all && !(f & NI_REJECTED) && !(pg.multi & PX_MULTI)) {
-        if (tid == 0) look = 0;
-        __syncthreads();
+    // The node's flags are read ONCE (thread 0) and broadcast: with the early pre pass k_chain may set NI_CHAIN
+    // beside this kernel, and every wave must take the same branch around the barriers below.
+    if (tid == 0) {
+        const uint32_t f = S.info[sg.res].flags;
+        // eligible: one checked rule, its map within the commit's LDS (<= PQ_MAX_CAP), no argument lists, a chain
+        uint32_t ok = k1 >= 0 && !(S.prio && (S.prio[sg.res] & PM_ARGL));
+        if (ok && S.pmap[S.rules[pg.rule_off + k1].pmap].cap > PQ_MAX_CAP) ok = 0;
+        const bool chain = (f & NI_CHAIN) != 0;
+        const bool scan = ok && !chain && grant_all && !(f & NI_REJECTED) && !(pg.multi & PX_MULTI);
+        okf = ok && chain;  // final unless the ENTRY scan below runs
+        scan_f = scan ? 1u : 0u;
+        look = 0;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane((int)scan_f)) {
         for (uint32_t p0 = 0; p0 < sg.len; p0 += 256) {  // (uniform trip count; the first ENTRY is near the start)
             const uint32_t p = p0 + tid;
             if (p < sg.len && recs[sg.start + p].kind == SG_EV_ENTRY &&
@@ -142,11 +149,10 @@ __global__ __launch_bounds__(256) void k_pv_prep(const SEv* __restrict__ recs, c
                 look = 1;
             if (__syncthreads_or(look)) break;
         }
-        chain = look != 0;
+        if (tid == 0) okf = look != 0;  // (ok held: the scan runs only for an eligible segment)
+        __syncthreads();
     }
-    if (tid == 0) okf = ok && chain;
-    __syncthreads();
-    if (!okf) {  // k_pq's pre pass: rest[1 + k], count rest[0] (an XF_PVPQ segment: k_pq's full pass decides it)
+    if (!__builtin_amdgcn_readfirstlane((int)okf)) {  // k_pq's pre pass: rest[1 + k], count rest[0] (an XF_PVPQ segment: k_pq's full pass decides it)
         if (tid == 0) {
             PvSeg z{};
             z.ok = 0;

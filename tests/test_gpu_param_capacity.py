@@ -170,3 +170,38 @@ def test_c5_five_million_distinct_values():
         assert not len(bad), ("event", int(a + bad[0]), hex(dg[bad[0]]), hex(do[bad[0]]), len(bad))
         blocked += int(((dg & 0xFF) == A.BLOCK_PARAM).sum())
     assert blocked > 100_000
+
+
+def test_largest_pool_that_fits_loads():
+    # the compaction's second pool is allocated with the pool, so the maps take 2 x 2^k x 32 B of HBM at
+    # rule load.  8192 rules of durationInSec 50 (200,000 values each) could use more than 2^32 slots, so the pool is
+    # the full 2^k: param_table_log2 from 34 down, each load either refused with SG_ECAPACITY (nothing loaded) or
+    # taken; the largest k taken decides a batch exactly as the oracle, and every k the device memory holds loads
+    # (2^31 slots: 2 x 68.7 GB on one MI355X)
+    n_res = 8192
+    names = ["big%d" % i for i in range(n_res)]
+    rules = [A.param_rule(nm, 0, 5, duration_in_sec=50) for nm in names]
+    got = None
+    for k in (34, 33, 32, 31, 30):
+        eng = E.Engine(max_resources=n_res, max_slot_chain_size=0, param_table_log2=k)
+        eng.register_many(names)
+        try:
+            assert eng.load_param_rules(rules) == n_res
+        except E.SentinelError as ex:
+            assert ex.code == A.SG_ECAPACITY and "param_table_log2" in str(ex), str(ex)
+            eng.close()
+            continue
+        got = k
+        orc = O.Oracle(max_slot_chain_size=0)
+        for nm in names[:4]:
+            orc.register(nm)
+        assert orc.load_param_rules(rules[:4]) == 4
+        ev = np.concatenate([_entries(r, [_long(v % 7) for v in range(40)], t=T0 + 10 * r) for r in range(4)])
+        ev = ev[np.argsort(ev["ts"], kind="stable")]
+        np.testing.assert_array_equal(eng.submit(ev), orc.submit(ev))
+        pool = eng.param_pool()
+        assert pool["buckets"] * 8 == 1 << k, pool
+        orc.close()
+        eng.close()
+        break
+    assert got is not None and got >= 31, got
