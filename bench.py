@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--sharding", choices=("balanced", "hash"), default="balanced",
                    help="resource -> GPU partition: balanced by event counts, or splitmix64(res_id) %% N")
     p.add_argument("--no-configs", action="store_true", help="skip the C2 / C3 / C5 / C6 sub-lines")
+    p.add_argument("--only-config", default="", metavar="C2|C3|C5|C5-ext|C6",
+                   help="measure only that config sub-line (no headline; tools/pmc_configs.py profiles it)")
     p.add_argument("--resources", type=int, default=1_000_000)
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="partitioned oracle threads (0: this job's CPU share -- cgroup cpu.max, else min(16, cores))")
@@ -167,6 +169,12 @@ def main():
         # torch -- this parent never touches a GPU; rank 0 prints the JSON line
         from sentinel_amd.launch import launch_ranks
         sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    if args.only_config:
+        import torch
+        dev = torch.device("cuda", 0)
+        rows = config_lines(dev, None, 0, only=[args.only_config])
+        print(json.dumps({"only_config": args.only_config, "configs": rows, "src_sha": src_sha()}), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -475,7 +483,42 @@ EXT_NOTE = ("sg_submit_ex, the Java drop-in's call: every event in one of 4 name
             "DefaultNodes kept on the device")
 
 
-def run_batches(eng, ev, gb, dev, ext=None, args=None):
+def alg_bytes(ev, args_keyed: bool) -> float:
+    """SURVEY.md §8(d) algorithmic bytes of one batch: 24 B per event record, 4 B per ENTRY decision, 608 B of state
+    (S_r + S_w) per touched resource, and for hot-parameter rules 2 x 16 B per distinct (resource, args[0]) pair of
+    the batch's ENTRYs (the param term 2 * 16 * U_b; one param rule per resource in C5 / C6)."""
+    from sentinel_amd import _abi as A
+    ent = ev["kind"] == A.EV_ENTRY
+    b = len(ev) * EVENT_B + int(ent.sum()) * DECISION_B + len(np.unique(ev["res_id"])) * STATE_RW_B
+    if args_keyed:
+        has = ent & ((ev["flags"] & A.F_HAS_ARG) != 0)
+        pairs = np.empty(int(has.sum()), dtype=[("r", np.uint32), ("k", np.uint64)])
+        pairs["r"], pairs["k"] = ev["res_id"][has], ev["aux"][has]
+        b += 2 * 16 * len(np.unique(pairs))
+    return float(b)
+
+
+def config_roofline(cfg_key: str, ms_per_batch: float, alg: float, gb: int) -> dict:
+    """roofline of a config sub-line: its algorithmic bytes per batch over the wall time per batch; traffic = the
+    rocprofv3 FETCH / WRITE passes of that config (profiles/pmc_configs.json, tools/pmc_configs.py) when they were
+    measured on these sources."""
+    traffic, src = None, None
+    pj = os.path.join(ROOT, "profiles", "pmc_configs.json")
+    if os.path.exists(pj):
+        with open(pj) as f:
+            rec = json.load(f).get(cfg_key)
+        if rec and rec.get("src_sha") == src_sha() and rec.get("batch_events") == gb:
+            traffic = rec["traffic_bytes_per_batch"]
+            src = "profiles/pmc_configs.json[%s] (src_sha %s)" % (cfg_key, rec["src_sha"])
+        elif rec:
+            src = "profiles/pmc_configs.json[%s] is for other sources (src_sha %s): not used" % (cfg_key, rec.get("src_sha"))
+    ach = alg / (ms_per_batch / 1e3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "alg_bytes_per_batch": alg, "traffic": traffic, "traffic_source": src,
+            "kernel": "one batch through the whole pipeline (group, decide, post)"}
+
+
+def run_batches(eng, ev, gb, dev, ext=None, args=None, cfg_key=None, args_keyed=False):
     """Batch 0 untimed, the rest back to back through the pipeline; inputs (events, ext, args) in HBM."""
     import torch
     nb = (len(ev) + gb - 1) // gb
@@ -506,10 +549,14 @@ def run_batches(eng, ev, gb, dev, ext=None, args=None):
     ent = int((ev[cuts[1]:]["kind"] == 0).sum())
     del buf, xb, ab, out
     torch.cuda.empty_cache()
-    return {"value": ent / dt, "unit": "entries/s", "batches_timed": nb - 1, "batch_events": gb, "entries_timed": ent,
-            "ms_per_batch": dt / (nb - 1) * 1e3, "stage_ms_mean": {"group": float(st[:, 0].mean()),
-                                                                   "decide": float(st[:, 1].mean()),
-                                                                   "post": float(st[:, 2].mean())}}
+    r = {"value": ent / dt, "unit": "entries/s", "batches_timed": nb - 1, "batch_events": gb, "entries_timed": ent,
+         "ms_per_batch": dt / (nb - 1) * 1e3, "stage_ms_mean": {"group": float(st[:, 0].mean()),
+                                                                "decide": float(st[:, 1].mean()),
+                                                                "post": float(st[:, 2].mean())}}
+    if cfg_key:
+        alg = float(np.mean([alg_bytes(ev[cuts[b]:cuts[b + 1]], args_keyed) for b in range(1, nb)]))
+        r["roofline"] = config_roofline(cfg_key, r["ms_per_batch"], alg, gb)
+    return r
 
 
 def param_args(ev):
@@ -542,7 +589,7 @@ def config_cpu_baseline(w, ev, n_events):
                       "by splitmix64(res_id) %% %d (routing excluded)" % (len(sample), n_ent, T, T)}
 
 
-def config_lines(dev, c4=None, cpu_events=4_000_000):
+def config_lines(dev, c4=None, cpu_events=4_000_000, only=None):
     """The SURVEY.md configs besides the headline: C2, C3, C5, C6 (mixed rules); with c4 = (workload, events) of the headline trace,
     C4 and C4-ext on its first 3 global batches (the same events through sg_submit and sg_submit_ex), C5-ext, and
     the drop-in's operating point (dropin_line)."""
@@ -562,7 +609,7 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
             if ext_on:
                 io, ic = w.intern_names(eng)
                 ext = T.ext_for(sub, io, ic, seed=T.SEED_BASE + 44)
-            r = run_batches(eng, sub, gb, dev, ext=ext)
+            r = run_batches(eng, sub, gb, dev, ext=ext, cfg_key="C4-ext" if ext_on else "C4")
             r.update({"config": "C4%s: 1M resources, QPS DefaultController + DegradeRule, first 3 batches of the "
                                 "headline trace" % ("-ext" if ext_on else ""), "resources": w.n_res})
             if ext_on:
@@ -571,9 +618,14 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
             eng.close()
             torch.cuda.empty_cache()
     for cfg, n_entries, gb, kw, var, name in CONFIGS:
+        if only and not any(o.split("-")[0] == "C%d" % cfg for o in only):
+            continue
         w = T.Workload(cfg, seed=T.SEED_BASE + cfg, n_entries=n_entries, variant=var)
         ev = w.events
-        for ext_on in ((False, True) if cfg == 5 else (False,)):
+        ext_ons = (False, True) if cfg == 5 else (False,)
+        if only:
+            ext_ons = tuple(e for e in ext_ons if ("C%d%s" % (cfg, "-ext" if e else "")) in only)
+        for ext_on in ext_ons:
             eng = E.Engine(device=dev.index, max_resources=max(w.n_res, 1 << 10), max_slot_chain_size=0,
                            max_batch_events=gb, aux_node_capacity=1 << 20, **kw)
             w.install(eng)
@@ -583,7 +635,8 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
                 ext, args = param_args(ev)
                 oc = T.ext_for(ev, io, ic, seed=T.SEED_BASE + 45)
                 ext["origin_id"], ext["context_id"] = oc["origin_id"], oc["context_id"]
-            r = run_batches(eng, ev, gb, dev, ext=ext, args=args)
+            r = run_batches(eng, ev, gb, dev, ext=ext, args=args, cfg_key="C%d%s" % (cfg, "-ext" if ext_on else ""),
+                            args_keyed=cfg in (5, 6))
             r.update({"config": name if not ext_on else name.replace("C5:", "C5-ext:") + "; args[0] from the table",
                       "resources": w.n_res})
             if ext_on:
@@ -594,6 +647,8 @@ def config_lines(dev, c4=None, cpu_events=4_000_000):
                 r["cpu_baseline"] = config_cpu_baseline(w, ev, cpu_events)
             rows.append(r)
         w.close()
+    if only:  # (tools/pmc_configs.py: one config's batches under rocprofv3)
+        return rows
     if c4 is not None:
         rows.append(dropin_line(dev, *c4))
         rows.append(latency_line(dev, *c4))

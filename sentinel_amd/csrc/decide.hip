@@ -1608,6 +1608,8 @@ enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR
 
 template <int NW, int MF, int MD>
 struct JacSh {
+    Bkt minl[60];  // the resource's minute window, held in LDS for the owner's lifetime (the round's leader reads and
+                   // writes it every second: from HBM that was a dependent round trip or two per round)
     Node node;
     DRule rules[MF + MD];
     RState rs[MF + MD];
@@ -1636,9 +1638,22 @@ struct JacSh {
     unsigned long long fl[NW]; // flagged-block ballots
     uint32_t cg[NW][3];        // closed-form guesses: per-wave totals (entries, effective exits | last entry time, others)
     uint32_t cgm[NW];          // ... per-wave minimum of the thread-grade admission bound
-    // open stretches: the stop's evaluated outcome and the RT breakers' segmented passCount state before it
+    // open stretches: the stop's evaluated outcome and the RT breakers' segmented passCount state before it; the
+    // round machine: the stop's time and the round's pass count at it
     uint32_t os_o;
     uint32_t os_seg[MD];
+    int32_t os_t;
+    int64_t os_P;
+    // the round machine's state (written by the leader, read by every lane after a barrier): the open view before the
+    // current chunk (passes, successes, RT sum, exceptions, minute exceptions, blocks), the RT stages' segmented
+    // passCount carry and base, the round's event times, the open round's first position, frozen mode, the mode
+    int64_t mv[6];
+    uint32_t mksg[MD];
+    int32_t mpcb[MD];
+    int64_t mfzP;
+    int32_t mrlo, mrhi;
+    uint32_t molo, mfz0, mfcut, mmode;
+    double mflim[MF];
 };
 
 // leader: fold the round's committed deltas into the node (StatisticSlot bookkeeping of every
@@ -1669,7 +1684,7 @@ template <class SH>
 __device__ void round_setup(SH& sh, const Ctx& C, int nf, int nd, int64_t tn) {
     Node& N = sh.node;
     const int64_t b0 = tn / 500, T = tn - tn % 1000;
-    min_flush(N, C.minb);  // HBM holds the current minute bucket from here on
+    min_flush(N, C.minb);  // the window (sh.minl) holds the current minute bucket from here on
     int64_t next_reset = INT64_MAX;
     for (int k = 0; k < nd; ++k) {  // ResetTask due (Q12)
         RState& s = sh.rs[nf + k];
@@ -1722,6 +1737,15 @@ __device__ void round_setup(SH& sh, const Ctx& C, int nf, int nd, int64_t tn) {
     sh.cminrt = NO_LANE;
     sh.ctouch = 0;
     sh.round_open = 1;
+}
+
+// leader: the round ends (fold) and the round of tn opens (setup) -- kept out of line: the round machine calls it with a
+// chunk of records and its prefetch live in registers, and inlined the set-up's own temporaries spilled the 512-lane
+// owner's per-chunk loop (a call per round costs less than scratch traffic per chunk)
+template <class SH>
+__device__ __attribute__((noinline)) void round_next_leader(SH& sh, const Ctx& C, int nf, int nd, int64_t tn) {
+    round_fold(sh, C, nf);
+    round_setup(sh, C, nf, nd, tn);
 }
 
 __device__ __forceinline__ uint32_t out_to_dec(const DRule* rules, int nr, int nf, uint32_t o, int64_t wait) {
@@ -1784,7 +1808,10 @@ __device__ __forceinline__ bool rl_upd(const DRule& r, uint32_t c, uint32_t g, i
 // CLS: 0 every segment of the dispatch list; 1 only QPS-DefaultController programs (PF_FROZEN), 2 only the others
 // (one bin's list decided by two instantiations, each with the registers its own kind of segment needs)
 template <int NW, int EP, int WINLOG, int MF, int MD, bool RL, bool SKIP, int CLS = 0>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? (EP == 1 ? 4 : 2) : (EP == 1 ? 1 : 2)))) void k_jac(
+#ifndef J4_WAVES
+#define J4_WAVES 1  // waves per SIMD the 256-lane owner is compiled for (A/B builds: -DJ4_WAVES=2 caps it at 256 VGPRs)
+#endif
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? (EP == 1 ? 4 : 2) : (EP == 1 ? (NW == 4 ? J4_WAVES : 1) : 2)))) void k_jac(
     const SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t m,
     DevState S, DevCfg cfg, int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     constexpr uint32_t HW = NW * 64;
@@ -1804,7 +1831,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const Prog pg = S.prog[res];
     if (CLS != 0 && (((pg.pflags & PF_FROZEN) != 0) != (CLS == 1))) return;  // the other instantiation's segment
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
-    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    // the minute window in LDS (sh.minl): loaded here, written back at the segment's end; no other kernel of the
+    // decide stage touches this resource's minute buckets while its owner runs
+    for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
+        reinterpret_cast<uint4*>(sh.minl)[i] = reinterpret_cast<const uint4*>(S.minb + (uint64_t)res * 60)[i];
+    const Ctx C{sh.minl, cfg.max_rt, pg.pflags};
     // XF_MIX: the param rules come first in the program and k_pq's pre pass has decided them: an ENTRY one of them
     // blocked carries RF_PBLK (its dec[] word is final) and is a block here, nothing more
     const uint32_t roff = pg.rule_off + pg.n_param;
@@ -1876,7 +1907,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     uint32_t n_it = 0, n_round = 0, n_tile = 0, n_mm = 0, n_frz = 0, n_opn = 0;
 #ifdef SG_KPROF
     const bool prof0 = prof && tid == 0;  // every block times itself; the longest segment reports
-    unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tmA = prof0 ? __builtin_amdgcn_s_memtime() : 0, tph[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t m_nopen = 0, m_nfrz = 0, m_nround = 0;  // the round machine's steps (the slowest segment's, dbg[56..58])
     const unsigned long long tm_start = tmA;
 #define PROF_MARK(k)                                          \
     if (prof0) {                                              \
@@ -2023,18 +2055,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             // each flow stage's limit in this round: DefaultController count; WarmUp: warningQps above the
             // warning token, else count (the synced state of the round's second)
             double flim[MF];
+            auto calc_flim = [&]() {
 #pragma unroll
-            for (int s = 0; s < MF; ++s) {
-                flim[s] = 0.0;
-                if (s < nf) {
-                    const DRule& r = sh.rules[s];
-                    flim[s] = r.count;
-                    if ((warmm >> s) & 1) {
-                        const RState& st = ((sh.has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
-                        if (st.a >= r.warning_token) flim[s] = warm_qps(r, st.a);
+                for (int s = 0; s < MF; ++s) {
+                    flim[s] = 0.0;
+                    if (s < nf) {
+                        const DRule& r = sh.rules[s];
+                        flim[s] = r.count;
+                        if ((warmm >> s) & 1) {
+                            const RState& st = ((sh.has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                            if (st.a >= r.warning_token) flim[s] = warm_qps(r, st.a);
+                        }
                     }
                 }
-            }
+            };
+            calc_flim();
             // stage s blocks an acquire of c at the round's pass count P
             auto fblock = [&](int s, int64_t P, int c) -> bool {
                 return ((warmm >> s) & 1) ? !((double)(P + c) <= flim[s])
@@ -2377,7 +2412,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 continue;
             }
 
-            // ================= open stretch =================
+            // ================= open stretch / round machine =================
             // Same program shape, nothing saturated, no breaker cut, and the last committed ENTRY passed:
             // guess that every ENTRY from here on passes.  Under that guess the pass count, the window's
             // success / RT / exception sums and the RT breakers' passCount before an ENTRY are prefix sums
@@ -2385,9 +2420,27 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
             // (one chain of scans and barriers per chunk instead of one per tile of Jacobi iterations): every
             // ENTRY is checked against its prefix view in FlowRuleChecker / DegradeRule order, and the first
             // one that does not pass, the first event past the round, or the segment end stops the stretch.
-            // Everything before the stop is exact (every earlier ENTRY did pass); the stop re-enters the
-            // Jacobi iteration with its evaluated outcome as the guess.  A long unsaturated segment (C4's J4
-            // body: 47k events under a 5250 QPS limit, no mismatch in 201 iterations) is a map + scan.
+            // Everything before the stop is exact (every earlier ENTRY did pass).
+            //
+            // The owner's round chain: a hot segment's round is "open until the quota is
+            // spent, then frozen until the round ends", and each of those switches used to leave the stretch --
+            // a re-entry into the Jacobi tile (its records loaded again), full fences, the next stretch's first
+            // chunk loaded again, the leader's round set-up: ~10 dependent memory round trips a round.  Here the
+            // stretch keeps going with the chunk already in registers:
+            //   * an open stop that is a flow block at a saturated pass count (no acquire of 1 passes any more:
+            //     DefaultController.canPass, DefaultController.java:49-81; nothing passes, so the pass count stays)
+            //     switches to frozen mode at the stop: every later ENTRY of the round blocks (FlowSlot runs before
+            //     DegradeSlot, FlowSlot.java:146-158), a pure map + reduction;
+            //   * the first event past the round ends the round in place: the lanes' committed totals are reduced,
+            //     the leader folds the round and opens the next one (LDS only: the minute window is in sh.minl),
+            //     and the next round goes on frozen (saturated, or the first breaker cut: DegradeRule.java:172-223)
+            //     or open (nothing cut) from that event, in the same chunk.
+            // Anything else -- a degrade block, a breaker trip, an ENTRY a frozen round could pass, a round that is
+            // neither -- leaves the machine into the Jacobi iteration exactly as before, and so does a frozen round
+            // that may be longer than the skip threshold, for the frozen-stretch code to skip.  The machine's state
+            // lives in LDS (sh.m*: the leader writes it, every lane reads it after a barrier), not in registers.
+            // Chunks: open mode reads a chunk lane-blocked (a lane folds OPEN_EPL consecutive events), frozen mode
+            // strided (each load instruction one contiguous run of records, as the frozen-stretch loop).
             bool anycut = false;
             if (OPEN) {  // (nothing of this in the owners without open stretches: it sits on every iteration's chain)
 #pragma unroll
@@ -2401,278 +2454,571 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 flush(tbase);
                 __syncthreads();  // full fence at every stretch start (see lds_barrier)
                 const uint32_t fpos0 = tbase + c0;
-                // the view before the stretch: round base + committed (uniform)
-                const int64_t P0 = uni64(sh.bP + sh.cP), S0 = uni64(sh.bS + sh.cS), RT0 = uni64(sh.bRT + sh.cRT);
-                const int64_t E0 = uni64(sh.bE + sh.cE), EM0 = uni64(sh.bEM + sh.cE), B0 = uni64(sh.bB + sh.cB);
-                int64_t kP = 0, kS = 0, kRT = 0, kE = 0;  // carried over the stretch's earlier chunks (uniform)
-                uint32_t ksg[MD];                         // RT stages: segmented passCount carry
-                int32_t pcb0[MD];                         // ... and the breaker's passCount at the stretch start
+                // the owners skip a frozen round from skip_min positions on (the frozen-stretch code does)
+                const uint32_t skip_min = S.skip_min * NW / 16 > 0 ? S.skip_min * NW / 16 : 1u;
+                // a flow stage's limit in the machine's round (sh.mflim), and whether it blocks an acquire of c at P
+                auto mlim = [&](int s) -> double {
+                    const uint64_t b = (uint64_t)uni64((int64_t)__builtin_bit_cast(uint64_t, sh.mflim[s]));
+                    return __builtin_bit_cast(double, b);
+                };
+                auto mblock = [&](int s, int64_t P, int c) -> bool {
+                    return ((warmm >> s) & 1) ? !((double)(P + c) <= mlim(s)) : (double)j_iadd(j_d2i((double)P), c) > mlim(s);
+                };
+                auto msat = [&](int64_t P) -> bool {
+                    bool r = false;
 #pragma unroll
-                for (int k = 0; k < MD; ++k) {
-                    ksg[k] = 0;
-                    pcb0[k] = k < nd ? (int32_t)sh.rs[nf + k].b : 0;
+                    for (int s = 0; s < MF; ++s)
+                        if (s < nf) r |= mblock(s, P, 1);
+                    return r;
+                };
+                // ---- leader: the machine's round (event times, flow limits), open mode, frozen mode
+                auto m_round = [&]() {
+                    const int64_t nlo = sh.bkt0 * 500 - t0, nrs = sh.next_reset - t0;
+                    const int64_t nhi = (nrs < nlo + 500) ? nrs : nlo + 500;
+                    sh.mrlo = (int32_t)nlo;
+                    sh.mrhi = nhi > (int64_t)INT32_MAX ? INT32_MAX : (int32_t)nhi;
+                    for (int s = 0; s < nf; ++s) {
+                        const DRule& r = sh.rules[s];
+                        double l = r.count;
+                        if ((warmm >> s) & 1) {
+                            const RState& st = ((sh.has_sync >> s) & 1) ? sh.syn[s] : sh.rs[s];
+                            if (st.a >= r.warning_token) l = warm_qps(r, st.a);
+                        }
+                        sh.mflim[s] = l;
+                    }
+                };
+                auto m_open = [&](uint32_t from) {
+                    sh.mv[0] = sh.bP + sh.cP; sh.mv[1] = sh.bS + sh.cS; sh.mv[2] = sh.bRT + sh.cRT;
+                    sh.mv[3] = sh.bE + sh.cE; sh.mv[4] = sh.bEM + sh.cE; sh.mv[5] = sh.bB + sh.cB;
+                    for (int k = 0; k < MD; ++k) {
+                        sh.mksg[k] = 0;
+                        sh.mpcb[k] = k < nd ? (int32_t)sh.rs[nf + k].b : 0;
+                    }
+                    sh.molo = from;
+                    sh.mmode = 0;
+                };
+                auto m_frozen = [&](uint32_t from, int64_t P) {
+                    sh.mfz0 = from;
+                    sh.mfzP = P;
+                    sh.mfcut = (nd > 0 && sh.rs[nf].a != 0) ? 1u : 0u;
+                    sh.mmode = 1;
+                };
+                auto m_seg = [&]() {  // an open stop's RT passCount state (sh.os_seg) into the breakers
+                    for (int k = 0; k < nd; ++k)
+                        if (sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                            const uint32_t x = sh.os_seg[k];
+                            const int32_t cc = (int32_t)(x & 0x7fffffffu);
+                            sh.rs[nf + k].b = (x & 0x80000000u) ? cc : sh.rs[nf + k].b + cc;
+                        }
+                };
+                PROF_MARK(0)
+                if (tid == 0) {
+                    m_round();
+                    m_open(fpos0);
                 }
-                int64_t kB = 0;                           // XF_MIX: param-blocked units of the earlier chunks
                 uint32_t aP = 0, aS = 0, aRT = 0, aE = 0, aTI = 0, aTH = 0, aMin = NO_LANE;  // committed (lane)
-                uint32_t aB = 0;    // XF_MIX: committed param-blocked units (lane)
-                bool oent = false;  // the lane committed an ENTRY
+                uint32_t aB = 0;     // committed blocked units (XF_MIX param blocks; frozen mode: every ENTRY)
+                bool oent = false;   // the lane committed a passing ENTRY (WarmUp: every flow stage reached)
+                uint32_t freach = 0; // frozen mode: WarmUp stages a committed ENTRY reached
+                bool seg_pending = false;  // sh.os_seg holds an open stop's passCount state not in sh.rs yet (uniform)
+                bool frz = false;          // the mode (uniform copy of sh.mmode)
+                uint32_t g_exit = (uint32_t)nr;
                 const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
                 const uint32_t qmax = sg.len - 1;
                 uint4 rr[OE], rn[OE];
                 uint32_t sb = fpos0, nst = 0, fend = 0;
-#pragma unroll
-                for (int k = 0; k < (int)OE; ++k) {
-                    const uint32_t q = sb + tid * OE + k;
-                    rr[k] = r4[q < qmax ? q : qmax];
-                }
-                for (;;) {
-#pragma unroll
-                    for (int k = 0; k < (int)OE; ++k) {  // prefetch the next chunk
-                        const uint32_t q = sb + OST + tid * OE + k;
-                        rn[k] = r4[q < qmax ? q : qmax];
-                    }
-                    // classes under the all-pass guess; 0x80: a stop before evaluation (past the round / segment)
-                    uint32_t cl[OE];
-                    uint32_t lp = 0, ls = 0, lrt = 0, le = 0, lb = 0;
+                uint32_t lay = 0, nlay = 0;  // layout of rr / rn: 0 lane-blocked (open), 1 strided (frozen)
+                // a layout's positions are affine in the item k: base + off + k * stride
+                auto qoff = [&](uint32_t l) -> uint32_t { return l ? tid : tid * OE; };
+                auto qstr = [&](uint32_t l) -> uint32_t { return l ? HW : 1u; };
+                auto qpos = [&](uint32_t l, int k) -> uint32_t { return sb + qoff(l) + (uint32_t)k * qstr(l); };
+                auto load_chunk = [&](uint4 (&dst)[OE], uint32_t base, uint32_t l) {
+                    const uint32_t o = base + qoff(l), st = qstr(l);
 #pragma unroll
                     for (int k = 0; k < (int)OE; ++k) {
-                        const uint32_t q = sb + tid * OE + k;
-                        const int32_t edt = (int32_t)rr[k].x;
-                        const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
-                        const uint32_t code = (rr[k].w >> 16) & 0xFFu;
-                        uint32_t c = 0;
-                        if (q >= sg.len || edt >= dhi || edt < dlo) c = 0x80u;
-                        else if (ek == SG_EV_ENTRY) c = ((rr[k].w >> 8) & RF_PBLK) ? JC_PB : JC_ENT;
-                        else {
-                            bool eff = code == RC_NONE || code == RC_PASSED;
-                            if (code == RC_BATCH) {
-                                const uint32_t rel = rr[k].y - sg.start;
-                                if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
-                                else if (rel >= fpos0)  // an ENTRY of this stretch: passed, unless a param rule blocked it
-                                    eff = !mixp || !((reinterpret_cast<const uint4*>(recs)[rr[k].y].w >> 8) & RF_PBLK);
-                                else if (rel + WIN >= sb + OST) eff = win[rel & (WIN - 1)] != 0;
-                                else eff = !in_span(rel) &&
-                                           st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
-                            }
-                            if (eff && ek == SG_EV_EXIT) c = JC_XE;
-                            else if (eff && ek == SG_EV_TRACE && ec > 0) c = JC_TE;
-                        }
-                        cl[k] = c;
-                        lp += (c & JC_ENT) ? ec : 0u;
-                        ls += (c & JC_XE) ? ec : 0u;
-                        lrt += (c & JC_XE) ? ert : 0u;
-                        le += (c & JC_TE) ? ec : 0u;
-                        lb += (c & JC_PB) ? ec : 0u;
+                        const uint32_t q = o + (uint32_t)k * st;
+                        dst[k] = r4[q < qmax ? q : qmax];
                     }
-                    // block-exclusive prefixes of the lane totals, and the chunk totals
-                    uint32_t xp = lp, xs = ls, xrt = lrt, xe = le, xb = lb;
-                    WAVE_SCAN(xp, 0u, op_add);
-                    WAVE_SCAN(xs, 0u, op_add);
-                    WAVE_SCAN(xrt, 0u, op_add);
-                    WAVE_SCAN(xe, 0u, op_add);
-                    if (mixp) WAVE_SCAN(xb, 0u, op_add);
-                    uint32_t tP, tS, tRT, tE, tB = 0;
-                    if (NW == 1) {
-                        tP = (uint32_t)__builtin_amdgcn_readlane((int)xp, 63);
-                        tS = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
-                        tRT = (uint32_t)__builtin_amdgcn_readlane((int)xrt, 63);
-                        tE = (uint32_t)__builtin_amdgcn_readlane((int)xe, 63);
-                        if (mixp) tB = (uint32_t)__builtin_amdgcn_readlane((int)xb, 63);
-                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le; xb -= lb;
-                    } else {
-                        if (lane == 63) {
-                            sh.part[wv][0] = xp; sh.part[wv][1] = xs; sh.part[wv][2] = xrt; sh.part[wv][3] = xe;
-                            sh.part[wv][4] = xb;
-                        }
-                        lds_barrier();
-                        // lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv and the chunk total
-                        uint32_t* const xs4[5] = {&xp, &xs, &xrt, &xe, &xb};
-                        uint32_t* const ts4[5] = {&tP, &tS, &tRT, &tE, &tB};
+                };
+                // the time of the record skip_min (+ a chunk) past the chunk: a frozen round entered in this chunk is
+                // long (left to the frozen-stretch code, which skips it) if that record is still in the round
+                auto probe_at = [&](uint32_t base) -> int32_t {
+                    const uint32_t q = base + OST + skip_min;
+                    return q < sg.len ? (int32_t)recs[sg.start + q].dt : INT32_MAX;
+                };
+                int32_t pr_dt = skip_on ? probe_at(sb) : INT32_MAX, pr_nx = INT32_MAX;
+                load_chunk(rr, sb, 0);
+                lds_barrier();  // the leader's machine state
+                // the lanes' committed totals into the round's (leader), WarmUp reach; accumulators restart
+                auto reduce_to_sh = [&]() {
+                    if (warmm) {
+                        if (__ballot(oent) && lane == 0) atomicOr(&sh.warm_reach, warmm);
 #pragma unroll
-                        for (int i = 0; i < 5; ++i) {
-                            if (i == 4 && !mixp) break;
-                            uint32_t v = lane < (uint32_t)NW ? sh.part[lane][i] : 0u;
-                            WAVE_SCAN(v, 0u, op_add);
-                            *xs4[i] += wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
-                            *ts4[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
-                        }
-                        xp -= lp; xs -= ls; xrt -= lrt; xe -= le; xb -= lb;
+                        for (int s = 0; s < MF; ++s)
+                            if (((warmm >> s) & 1) && __ballot((freach >> s) & 1) && lane == 0) atomicOr(&sh.warm_reach, 1u << s);
                     }
-                    // RT breakers: which ENTRYs see an average at the threshold, then the segmented passCount scan
-                    uint32_t badb = 0, segl[MD], segt[MD];
-#pragma unroll
-                    for (int k = 0; k < MD; ++k) segl[k] = segt[k] = 0;
-                    if (has_rt) {
-                        uint32_t agg[MD];
-#pragma unroll
-                        for (int k = 0; k < MD; ++k) agg[k] = 0;
-                        uint32_t rS = 0, rRT = 0;
-#pragma unroll
-                        for (int e = 0; e < (int)OE; ++e) {
-                            const int64_t vS = S0 + kS + (int64_t)(xs + rS), vRT = RT0 + kRT + (int64_t)(xrt + rRT);
-#pragma unroll
-                            for (int k = 0; k < MD; ++k) {
-                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                                    const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
-                                    const bool bad = !(avg < sh.rules[nf + k].count);
-                                    if (bad) badb |= 1u << (e * MD + k);
-                                    agg[k] = op_seg(agg[k], (cl[e] & JC_ENT) ? (bad ? 1u : 0x80000000u) : 0u);
-                                }
-                            }
-                            if (cl[e] & JC_XE) { rS += rr[e].z & 0xFFFFu; rRT += rr[e].z >> 16; }
-                        }
-#pragma unroll
-                        for (int k = 0; k < MD; ++k) {
-                            if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                                uint32_t v = agg[k];
-                                WAVE_SCAN(v, 0u, op_seg);
-                                segl[k] = shr1(v, 0u);
-                                if (NW == 1) segt[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-                                else if (lane == 63) sh.pseg[wv][k] = v;
-                            }
-                        }
-                        if (NW > 1) {
-                            lds_barrier();
-#pragma unroll
-                            for (int k = 0; k < MD; ++k) {
-                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                                    uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
-                                    WAVE_SCAN(v, 0u, op_seg);
-                                    const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
-                                    segl[k] = op_seg(pre, segl[k]);
-                                    segt[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
-                                }
-                            }
-                        }
+                    WAVE_SCAN(aP, 0u, op_add);
+                    WAVE_SCAN(aS, 0u, op_add);
+                    WAVE_SCAN(aRT, 0u, op_add);
+                    WAVE_SCAN(aE, 0u, op_add);
+                    WAVE_SCAN(aTI, 0u, op_add);
+                    WAVE_SCAN(aTH, 0u, op_add);
+                    WAVE_SCAN(aMin, NO_LANE, op_min);
+                    WAVE_SCAN(aB, 0u, op_add);
+                    lds_barrier();  // every wave is past its reads of sh.part
+                    if (lane == 63) {
+                        sh.part[wv][0] = aP; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
+                        sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin; sh.part[wv][7] = aB;
                     }
-                    // every ENTRY against its prefix view; the lane's first stop
-                    uint32_t mystop = NO_LANE, myo = (uint32_t)nr, sst[MD];
-                    uint32_t rp = 0, rs2 = 0, re = 0, rb = 0, rseg[MD];
-#pragma unroll
-                    for (int k = 0; k < MD; ++k) rseg[k] = sst[k] = 0;
-#pragma unroll
-                    for (int e = 0; e < (int)OE; ++e) {
-                        const uint32_t c = cl[e];
-                        const uint32_t ec = rr[e].z & 0xFFFFu;
-                        uint32_t o = (uint32_t)nr;
-                        if (c & 0x80u) o = NO_LANE;
-                        else if (c & JC_ENT) {
-                            const int64_t vP = P0 + kP + (int64_t)(xp + rp);
-                            const int64_t vS = S0 + kS + (int64_t)(xs + rs2);
-#pragma unroll
-                            for (int s = 0; s < MF; ++s)
-                                if (s < nf && o == (uint32_t)nr && fblock(s, vP, (int)ec)) o = (uint32_t)s;
-#pragma unroll
-                            for (int k = 0; k < MD; ++k) {
-                                if (k < nd && o == (uint32_t)nr) {
-                                    const DRule& r = sh.rules[nf + k];
-                                    bool ok = true;
-                                    if (r.grade == SG_DEGRADE_GRADE_RT) {
-                                        const uint32_t x = op_seg(ksg[k], op_seg(segl[k], rseg[k]));
-                                        const int32_t cc = (int32_t)(x & 0x7fffffffu);
-                                        const int32_t pcb = (x & 0x80000000u) ? cc : pcb0[k] + cc;
-                                        ok = !((badb >> (e * MD + k)) & 1) || (pcb + 1 < 5);
-                                    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
-                                        const double exc = (double)(E0 + kE + (int64_t)(xe + re)) / 1.0;
-                                        const double succ = (double)vS / 1.0;
-                                        const double total = (double)vP / 1.0 + (double)(B0 + kB + (int64_t)(xb + rb)) / 1.0;
-                                        if (total < 5) ok = true;
-                                        else if (succ - exc <= 0 && exc < 5) ok = true;
-                                        else ok = exc / succ < r.count;
-                                    } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) {
-                                        ok = (double)(EM0 + kE + (int64_t)(xe + re)) < r.count;
-                                    }
-                                    if (!ok) o = (uint32_t)(nf + k);
-                                }
-                            }
-                        }
-                        if (o != (uint32_t)nr && mystop == NO_LANE) {
-                            mystop = sb + tid * OE + (uint32_t)e;
-                            myo = o == NO_LANE ? (uint32_t)nr : o;
-#pragma unroll
-                            for (int k = 0; k < MD; ++k) sst[k] = rseg[k];
-                        }
-                        rp += (c & JC_ENT) ? ec : 0u;
-                        rs2 += (c & JC_XE) ? ec : 0u;
-                        re += (c & JC_TE) ? ec : 0u;
-                        rb += (c & JC_PB) ? ec : 0u;
-                        if (has_rt) {
-#pragma unroll
-                            for (int k = 0; k < MD; ++k)
-                                if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT)
-                                    rseg[k] = op_seg(rseg[k], (c & JC_ENT) ? (((badb >> (e * MD + k)) & 1) ? 1u : 0x80000000u) : 0u);
-                        }
-                    }
-                    uint32_t wmin = mystop;
-                    WAVE_SCAN(wmin, NO_LANE, op_min);
-                    if (lane == 63) sh.mism[mb][wv] = wmin;
                     lds_barrier();
-                    uint32_t f = NO_LANE;
-                    f = blk_min<NW>(sh.mism[mb]);
-                    f = uni(f);
-                    mb ^= 1;
-                    ++n_opn;
-                    // commit every position before the stop (unconditional stores: masked lanes hit the sink)
-                    uint32_t appm = 0;
-#pragma unroll
-                    for (int k = 0; k < (int)OE; ++k) {
-                        const uint32_t q = sb + tid * OE + k;
-                        const bool cm = q < f && q < sg.len;
-                        const uint32_t c = cl[k];
-                        uint32_t d = 0;
-                        if (cm) {
-                            const uint32_t ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
-                            if (c & JC_ENT) {
-                                d = mk_dec(ST_PASS, 0, 0);
-                                win[q & (WIN - 1)] = 1;
-                                aP += ec; aTI += 1; aTH += 1;
-                                oent = true;
-                                appm |= 1u << k;
-                            } else {
-                                d = mk_dec(ST_NOT_ENTRY, 0, 0);
-                                win[q & (WIN - 1)] = 0;
-                                if (c & JC_XE) { aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1; }
-                                else if (c & JC_TE) { aE += ec; aTI += 1; }
-                                else if (c & JC_PB) { aB += ec; aTI += 1; }
+                    if (tid == 0) {
+                        for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                            sh.cP += sh.part[w][0]; sh.cS += sh.part[w][1]; sh.cRT += sh.part[w][2]; sh.cE += sh.part[w][3];
+                            sh.ctouch += sh.part[w][4]; sh.cTH += (int32_t)sh.part[w][5];
+                            sh.cminrt = op_min(sh.cminrt, sh.part[w][6]);
+                            sh.cB += sh.part[w][7];
+                        }
+                        if (seg_pending) m_seg();
+                    }
+                    seg_pending = false;
+                    aP = aS = aRT = aE = aTI = aTH = aB = 0;
+                    aMin = NO_LANE;
+                    oent = false;
+                    freach = 0;
+                };
+                // the round of the event at p (time tp) after the current one ended at p: 0 = open from p, 1 = frozen
+                // from p, 2 = leave the machine at p
+                auto round_next = [&](uint32_t p, int32_t tp) -> uint32_t {
+                    reduce_to_sh();
+                    if (tid == 0) {
+                        round_next_leader(sh, C, nf, nd, t0 + tp);
+                        m_round();
+                        const int64_t P = sh.bP + sh.cP;
+                        bool sat = false, anyc = false;
+                        for (int s = 0; s < nf; ++s) {
+                            const double l = sh.mflim[s];
+                            sat |= ((warmm >> s) & 1) ? !((double)(P + 1) <= l) : (double)j_iadd(j_d2i((double)P), 1) > l;
+                        }
+                        for (int k = 0; k < nd; ++k) anyc |= sh.rs[nf + k].a != 0;
+                        const bool cut0 = nd > 0 && sh.rs[nf].a != 0;
+                        if (sat || cut0) {
+                            if (pr_dt < sh.mrhi) sh.mmode = 2;  // long: the frozen-stretch code skips it
+                            else m_frozen(p, P);
+                        } else if (!anyc) m_open(p);
+                        else sh.mmode = 2;
+                    }
+                    lds_barrier();
+                    const uint32_t md = uni(sh.mmode);
+                    frz = md == 1;
+#ifdef SG_KPROF
+                    ++m_nround;
+#endif
+                    PROF_MARK(12)
+                    return md;
+                };
+                for (;;) {
+                    nlay = frz ? 1u : 0u;
+                    load_chunk(rn, sb + OST, nlay);  // prefetch the next chunk in the current mode's layout
+                    if (skip_on) pr_nx = probe_at(sb + OST);
+                    bool leave = false;
+                    for (;;) {  // this chunk, in the current mode (again after a mode switch inside it)
+                        if (!frz) {
+                            // ---------- open mode
+                            if (lay) {  // a strided chunk (the round turned open inside it): lane-blocked again
+                                load_chunk(rr, sb, 0);
+                                lay = 0;
+                                if (nlay) { load_chunk(rn, sb + OST, 0); nlay = 0; }
                             }
-                        }
-                        *((cm && !(c & JC_PB)) ? &dec[sg.start + q] : &S.sink[tid]) = d;
-                    }
-                    if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
-                        const uint32_t na = (uint32_t)__popc(appm);
-                        uint32_t incl = na;
-                        WAVE_SCAN(incl, 0u, op_add);
-                        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                        if (tot) {
-                            uint32_t base = 0;
-                            if (lane == 0) base = atomicAdd(&sh.npend, tot);
-                            base = (uint32_t)__shfl((int)base, 0, 64) + incl - na;
+                            const uint32_t olo = uni(sh.molo);
+                            const int32_t rlo = (int32_t)uni((uint32_t)sh.mrlo), rhi = (int32_t)uni((uint32_t)sh.mrhi);
+                            // classes under the all-pass guess; 0x80: a stop before evaluation (past the round / segment);
+                            // 0: committed already (before olo) or nothing to count
+                            uint32_t cl[OE];
+                            uint32_t lp = 0, ls = 0, lrt = 0, le = 0, lb = 0;
 #pragma unroll
-                            for (int k = 0; k < (int)OE; ++k)
-                                if ((appm >> k) & 1) S.pend[sg.start + base++] = sb + tid * OE + k;
-                        }
-                    }
-                    if (f != NO_LANE) {
-                        if (f >= sb + tid * OE && f < sb + tid * OE + OE) {  // the lane holding the stop
-                            sh.os_o = myo;
+                            for (int k = 0; k < (int)OE; ++k) {
+                                const uint32_t q = sb + tid * OE + k;
+                                const int32_t edt = (int32_t)rr[k].x;
+                                const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu;
+                                const uint32_t code = (rr[k].w >> 16) & 0xFFu;
+                                uint32_t c = 0;
+                                if (q < olo) c = 0;
+                                else if (q >= sg.len || edt >= rhi || edt < rlo) c = 0x80u;
+                                else if (ek == SG_EV_ENTRY) c = ((rr[k].w >> 8) & RF_PBLK) ? JC_PB : JC_ENT;
+                                else {
+                                    bool eff = code == RC_NONE || code == RC_PASSED;
+                                    if (code == RC_BATCH) {
+                                        const uint32_t rel = rr[k].y - sg.start;
+                                        if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+                                        else if (rel >= olo)  // an ENTRY of this open round: passed, unless a param rule blocked it
+                                            eff = !mixp || !((reinterpret_cast<const uint4*>(recs)[rr[k].y].w >> 8) & RF_PBLK);
+                                        else if (rel + WIN >= sb + OST) eff = win[rel & (WIN - 1)] != 0;
+                                        else eff = !in_span(rel) &&
+                                                   st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                                    }
+                                    if (eff && ek == SG_EV_EXIT) c = JC_XE;
+                                    else if (eff && ek == SG_EV_TRACE && ec > 0) c = JC_TE;
+                                }
+                                cl[k] = c;
+                                lp += (c & JC_ENT) ? ec : 0u;
+                                ls += (c & JC_XE) ? ec : 0u;
+                                lrt += (c & JC_XE) ? (rr[k].z >> 16) : 0u;
+                                le += (c & JC_TE) ? ec : 0u;
+                                lb += (c & JC_PB) ? ec : 0u;
+                            }
+                            // block-exclusive prefixes of the lane totals, and the chunk totals
+                            uint32_t xp = lp, xs = ls, xrt = lrt, xe = le, xb = lb;
+                            WAVE_SCAN(xp, 0u, op_add);
+                            WAVE_SCAN(xs, 0u, op_add);
+                            WAVE_SCAN(xrt, 0u, op_add);
+                            WAVE_SCAN(xe, 0u, op_add);
+                            if (mixp) WAVE_SCAN(xb, 0u, op_add);
+                            uint32_t tP, tS, tRT, tE, tB = 0;
+                            lds_barrier();  // (sh.part may still be read by a reduction of this chunk)
+                            if (lane == 63) {
+                                sh.part[wv][0] = xp; sh.part[wv][1] = xs; sh.part[wv][2] = xrt; sh.part[wv][3] = xe;
+                                sh.part[wv][4] = xb;
+                            }
+                            lds_barrier();
+                            {   // lanes l < NW fetch wave l's totals; a DPP scan gives the waves before wv and the chunk total
+                                uint32_t* const xs4[5] = {&xp, &xs, &xrt, &xe, &xb};
+                                uint32_t* const ts4[5] = {&tP, &tS, &tRT, &tE, &tB};
 #pragma unroll
-                            for (int k = 0; k < MD; ++k) sh.os_seg[k] = op_seg(ksg[k], op_seg(segl[k], sst[k]));
+                                for (int i = 0; i < 5; ++i) {
+                                    if (i == 4 && !mixp) break;
+                                    uint32_t v = lane < (uint32_t)NW ? sh.part[lane][i] : 0u;
+                                    WAVE_SCAN(v, 0u, op_add);
+                                    *xs4[i] += wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                                    *ts4[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+                                }
+                                xp -= lp; xs -= ls; xrt -= lrt; xe -= le; xb -= lb;
+                            }
+                            // the view before the chunk (after the barriers: the leader's carry of the last chunk)
+                            const int64_t P0 = uni64(sh.mv[0]), S0 = uni64(sh.mv[1]), RT0 = uni64(sh.mv[2]);
+                            const int64_t E0 = uni64(sh.mv[3]), EM0 = uni64(sh.mv[4]), B0 = uni64(sh.mv[5]);
+                            // RT breakers: which ENTRYs see an average at the threshold, then the segmented passCount scan
+                            uint32_t badb = 0, segl[MD], segt[MD];
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) segl[k] = segt[k] = 0;
+                            if (has_rt) {
+                                uint32_t agg[MD];
+#pragma unroll
+                                for (int k = 0; k < MD; ++k) agg[k] = 0;
+                                uint32_t rS = 0, rRT = 0;
+#pragma unroll
+                                for (int e = 0; e < (int)OE; ++e) {
+                                    const int64_t vS = S0 + (int64_t)(xs + rS), vRT = RT0 + (int64_t)(xrt + rRT);
+#pragma unroll
+                                    for (int k = 0; k < MD; ++k) {
+                                        if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                            const double avg = vS == 0 ? 0.0 : (double)vRT * 1.0 / (double)vS;
+                                            const bool bad = !(avg < sh.rules[nf + k].count);
+                                            if (bad) badb |= 1u << (e * MD + k);
+                                            agg[k] = op_seg(agg[k], (cl[e] & JC_ENT) ? (bad ? 1u : 0x80000000u) : 0u);
+                                        }
+                                    }
+                                    if (cl[e] & JC_XE) { rS += rr[e].z & 0xFFFFu; rRT += rr[e].z >> 16; }
+                                }
+#pragma unroll
+                                for (int k = 0; k < MD; ++k) {
+                                    if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                        uint32_t v = agg[k];
+                                        WAVE_SCAN(v, 0u, op_seg);
+                                        segl[k] = shr1(v, 0u);
+                                        if (lane == 63) sh.pseg[wv][k] = v;
+                                    }
+                                }
+                                lds_barrier();
+#pragma unroll
+                                for (int k = 0; k < MD; ++k) {
+                                    if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
+                                        uint32_t v = lane < (uint32_t)NW ? sh.pseg[lane][k] : 0u;
+                                        WAVE_SCAN(v, 0u, op_seg);
+                                        const uint32_t pre = wv == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)v, (int)wv - 1);
+                                        segl[k] = op_seg(pre, segl[k]);
+                                        segt[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, NW - 1);
+                                    }
+                                }
+                            }
+                            // every ENTRY against its prefix view; the lane's first stop (myo: NO_LANE = past the
+                            // round / segment end, else the blocking stage) and the round's pass count before it
+                            uint32_t mystop = NO_LANE, myo = NO_LANE, sst[MD];
+                            int64_t myP = 0;
+                            int32_t myt = 0;
+                            uint32_t rp = 0, rs2 = 0, re = 0, rb = 0, rseg[MD];
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) rseg[k] = sst[k] = 0;
+#pragma unroll
+                            for (int e = 0; e < (int)OE; ++e) {
+                                const uint32_t c = cl[e];
+                                const uint32_t ec = rr[e].z & 0xFFFFu;
+                                const int64_t vP = P0 + (int64_t)(xp + rp);
+                                uint32_t o = (uint32_t)nr;
+                                if (c & 0x80u) o = NO_LANE;
+                                else if (c & JC_ENT) {
+                                    const int64_t vS = S0 + (int64_t)(xs + rs2);
+#pragma unroll
+                                    for (int s = 0; s < MF; ++s)
+                                        if (s < nf && o == (uint32_t)nr && mblock(s, vP, (int)ec)) o = (uint32_t)s;
+#pragma unroll
+                                    for (int k = 0; k < MD; ++k) {
+                                        if (k < nd && o == (uint32_t)nr) {
+                                            const DRule& r = sh.rules[nf + k];
+                                            bool ok = true;
+                                            if (r.grade == SG_DEGRADE_GRADE_RT) {
+                                                const uint32_t x = op_seg(uni(sh.mksg[k]), op_seg(segl[k], rseg[k]));
+                                                const int32_t cc = (int32_t)(x & 0x7fffffffu);
+                                                const int32_t pcb = (x & 0x80000000u) ? cc : (int32_t)uni((uint32_t)sh.mpcb[k]) + cc;
+                                                ok = !((badb >> (e * MD + k)) & 1) || (pcb + 1 < 5);
+                                            } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
+                                                const double exc = (double)(E0 + (int64_t)(xe + re)) / 1.0;
+                                                const double succ = (double)vS / 1.0;
+                                                const double total = (double)vP / 1.0 + (double)(B0 + (int64_t)(xb + rb)) / 1.0;
+                                                if (total < 5) ok = true;
+                                                else if (succ - exc <= 0 && exc < 5) ok = true;
+                                                else ok = exc / succ < r.count;
+                                            } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_COUNT) {
+                                                ok = (double)(EM0 + (int64_t)(xe + re)) < r.count;
+                                            }
+                                            if (!ok) o = (uint32_t)(nf + k);
+                                        }
+                                    }
+                                }
+                                if (o != (uint32_t)nr && mystop == NO_LANE) {
+                                    mystop = sb + tid * OE + (uint32_t)e;
+                                    myo = o;
+                                    myP = vP;
+                                    myt = (int32_t)rr[e].x;
+#pragma unroll
+                                    for (int k = 0; k < MD; ++k) sst[k] = rseg[k];
+                                }
+                                rp += (c & JC_ENT) ? ec : 0u;
+                                rs2 += (c & JC_XE) ? ec : 0u;
+                                re += (c & JC_TE) ? ec : 0u;
+                                rb += (c & JC_PB) ? ec : 0u;
+                                if (has_rt) {
+#pragma unroll
+                                    for (int k = 0; k < MD; ++k)
+                                        if (k < nd && sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT)
+                                            rseg[k] = op_seg(rseg[k], (c & JC_ENT) ? (((badb >> (e * MD + k)) & 1) ? 1u : 0x80000000u) : 0u);
+                                }
+                            }
+                            uint32_t wmin = mystop;
+                            WAVE_SCAN(wmin, NO_LANE, op_min);
+                            if (lane == 63) sh.mism[mb][wv] = wmin;
+                            lds_barrier();
+                            uint32_t f = NO_LANE;
+                            f = blk_min<NW>(sh.mism[mb]);
+                            f = uni(f);
+                            mb ^= 1;
+                            ++n_opn;
+                            // commit every position of the round before the stop (unconditional stores: masked lanes hit the sink)
+                            uint32_t appm = 0;
+#pragma unroll
+                            for (int k = 0; k < (int)OE; ++k) {
+                                const uint32_t q = sb + tid * OE + k;
+                                const bool cm = q >= olo && q < f && q < sg.len;
+                                const uint32_t c = cl[k];
+                                uint32_t d = 0;
+                                if (cm) {
+                                    const uint32_t ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
+                                    if (c & JC_ENT) {
+                                        d = mk_dec(ST_PASS, 0, 0);
+                                        win[q & (WIN - 1)] = 1;
+                                        aP += ec; aTI += 1; aTH += 1;
+                                        oent = true;
+                                        appm |= 1u << k;
+                                    } else {
+                                        d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                                        win[q & (WIN - 1)] = 0;
+                                        if (c & JC_XE) { aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1; }
+                                        else if (c & JC_TE) { aE += ec; aTI += 1; }
+                                        else if (c & JC_PB) { aB += ec; aTI += 1; }
+                                    }
+                                }
+                                *((cm && !(c & JC_PB)) ? &dec[sg.start + q] : &S.sink[tid]) = d;
+                            }
+                            if (skip_on) {  // committed passes join the pending list (their EXIT/TRACE may fall in a skipped span)
+                                const uint32_t na = (uint32_t)__popc(appm);
+                                uint32_t incl = na;
+                                WAVE_SCAN(incl, 0u, op_add);
+                                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                                if (tot) {
+                                    uint32_t base = 0;
+                                    if (lane == 0) base = atomicAdd(&sh.npend, tot);
+                                    base = (uint32_t)__shfl((int)base, 0, 64) + incl - na;
+#pragma unroll
+                                    for (int k = 0; k < (int)OE; ++k)
+                                        if ((appm >> k) & 1) S.pend[sg.start + base++] = sb + tid * OE + k;
+                                }
+                            }
+#ifdef SG_KPROF
+                            ++m_nopen;
+#endif
+                            PROF_MARK(10)
+                            if (f == NO_LANE) {  // the chunk is committed: the leader carries the view into the next one
+                                if (tid == 0) {
+                                    sh.mv[0] += tP; sh.mv[1] += tS; sh.mv[2] += tRT; sh.mv[3] += tE; sh.mv[4] += tE; sh.mv[5] += tB;
+#pragma unroll
+                                    for (int k = 0; k < MD; ++k)
+                                        if (k < nd) sh.mksg[k] = op_seg(sh.mksg[k], segt[k]);
+                                }
+                                break;
+                            }
+                            if (mystop == f) {  // the lane holding the stop
+                                sh.os_o = myo;
+                                sh.os_P = myP;
+                                sh.os_t = myt;
+#pragma unroll
+                                for (int k = 0; k < MD; ++k) sh.os_seg[k] = op_seg(uni(sh.mksg[k]), op_seg(segl[k], sst[k]));
+                            }
+                            lds_barrier();
+                            seg_pending = true;
+                            const uint32_t o_f = uni(sh.os_o);
+                            if (f >= sg.len) { fend = sg.len; g_exit = (uint32_t)nr; leave = true; break; }
+                            if (o_f == NO_LANE) {  // the round ended: the next one from f, in this chunk
+                                if (round_next(f, (int32_t)uni((uint32_t)sh.os_t)) == 2u) {
+                                    fend = f; g_exit = (uint32_t)nr; leave = true; break;
+                                }
+                                continue;
+                            }
+                            const int64_t Pf = uni64(sh.os_P);
+                            if (o_f < (uint32_t)nf && msat(Pf) && pr_dt >= (int32_t)uni((uint32_t)sh.mrhi)) {
+                                // the quota is spent: frozen until the round ends
+                                if (tid == 0) {
+                                    m_seg();
+                                    m_frozen(f, Pf);
+                                }
+                                seg_pending = false;
+                                frz = true;
+                                lds_barrier();
+                                continue;
+                            }
+                            fend = f;
+                            g_exit = o_f;
+                            leave = true;
+                            break;
                         }
-                        fend = f < sg.len ? f : sg.len;
+                        // ---------- frozen mode: positions [max(sb, fz0), sb + OST) of the round; a stop at the first
+                        // event past the round (or an ENTRY that could pass: an acquire of 0)
+                        const uint32_t fz0 = uni(sh.mfz0);
+                        const int64_t fzP = uni64(sh.mfzP);
+                        const bool fcut = uni(sh.mfcut) != 0;
+                        const int32_t rlo = (int32_t)uni((uint32_t)sh.mrlo), rhi = (int32_t)uni((uint32_t)sh.mrhi);
+                        const int32_t fzi = j_d2i((double)fzP);
+                        const double fzd = (double)fzP;
+                        double fl[MF];
+#pragma unroll
+                        for (int s = 0; s < MF; ++s) fl[s] = s < nf ? mlim(s) : 0.0;
+                        uint32_t mystop = NO_LANE, myk = 0;
+                        int32_t myt = 0;
+                        uint32_t fdv[OE], fbs[OE];
+#pragma unroll
+                        for (int k = 0; k < (int)OE; ++k) {
+                            const uint32_t q = qpos(lay, k);
+                            const int32_t edt = (int32_t)rr[k].x;
+                            const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu;
+                            const bool act = q >= fz0 && q < sg.len;
+                            const bool in = edt >= rlo && edt < rhi;
+                            const double curv = (double)j_iadd(fzi, (int)ec);
+                            uint32_t bs = (uint32_t)nf;  // the blocking flow stage (nf: none)
+#pragma unroll
+                            for (int s = MF - 1; s >= 0; --s)
+                                if (s < nf && (((warmm >> s) & 1) ? !(fzd + (double)ec <= fl[s]) : curv > fl[s])) bs = (uint32_t)s;
+                            uint32_t fd = bs < (uint32_t)nf ? mk_dec(ST_BLOCK_FLOW, sh.rules[bs].slot, 0)
+                                                            : (fcut ? mk_dec(ST_BLOCK_DEGRADE, sh.rules[nf].slot, 0) : 0u);
+                            if ((rr[k].w >> 8) & RF_PBLK) fd = 1u;  // blocked by a param rule: its word is written
+                            fdv[k] = fd;
+                            fbs[k] = bs;
+                            const bool stop = act && (!in || (ek == SG_EV_ENTRY && fd == 0));
+                            if (stop && q < mystop) { mystop = q; myk = in ? 1u : 0u; myt = edt; }
+                        }
+                        uint32_t wmin = mystop;
+                        WAVE_SCAN(wmin, NO_LANE, op_min);
+                        if (lane == 63) sh.mism[mb][wv] = wmin;
+                        lds_barrier();
+                        uint32_t f = NO_LANE;
+                        f = blk_min<NW>(sh.mism[mb]);
+                        f = uni(f);
+                        mb ^= 1;
+                        ++n_frz;
+#pragma unroll
+                        for (int k = 0; k < (int)OE; ++k) {
+                            const uint32_t q = qpos(lay, k);
+                            const bool cm = q >= fz0 && q < f && q < sg.len;
+                            uint32_t d = 0;
+                            if (cm) {
+                                const uint32_t ek = rr[k].w & 0xFFu, ec = rr[k].z & 0xFFFFu, ert = rr[k].z >> 16;
+                                const uint32_t code = (rr[k].w >> 16) & 0xFFu;
+                                d = mk_dec(ST_NOT_ENTRY, 0, 0);
+                                if (ek == SG_EV_ENTRY) {
+                                    d = fdv[k];
+                                    win[q & (WIN - 1)] = 0;
+                                    aB += ec;
+                                    aTI += 1;
+                                    // WarmUp: the stages up to the blocking one (every flow stage when a breaker blocks)
+                                    if (warmm && d != 1u) freach |= (2u << fbs[k]) - 1u;
+                                } else {
+                                    bool eff = code == RC_NONE || code == RC_PASSED;
+                                    if (code == RC_BATCH) {
+                                        const uint32_t rel = rr[k].y - sg.start;
+                                        if (rel >= q) { atomicOr(bflags, BF_BAD_REF); eff = false; }
+                                        else if (rel >= fz0) eff = false;  // an ENTRY of the frozen part: blocked
+                                        else if (rel + WIN >= sb + OST) eff = win[rel & (WIN - 1)] != 0;
+                                        else eff = !in_span(rel) &&
+                                                   st_passed(__hip_atomic_load(&dec[rr[k].y], __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT) & 0xFF);
+                                    }
+                                    win[q & (WIN - 1)] = 0;
+                                    if (eff && ek == SG_EV_EXIT) {
+                                        aS += ec; aRT += ert; aTH -= 1; aMin = op_min(aMin, ert); aTI += 1;
+                                    } else if (eff && ek == SG_EV_TRACE && ec > 0) {
+                                        aE += ec; aTI += 1;
+                                    }
+                                }
+                            }
+                            *((cm && d != 1u) ? &dec[sg.start + q] : &S.sink[tid]) = d;
+                        }
+#ifdef SG_KPROF
+                        ++m_nfrz;
+#endif
+                        PROF_MARK(11)
+                        if (f == NO_LANE) break;  // the chunk is committed
+                        if (mystop == f) { sh.os_o = myk; sh.os_t = myt; }
+                        lds_barrier();
+                        if (uni(sh.os_o) == 0u) {  // past the round: the next one from f, in this chunk
+                            if (round_next(f, (int32_t)uni((uint32_t)sh.os_t)) == 2u) {
+                                fend = f; g_exit = (uint32_t)nr; leave = true; break;
+                            }
+                            continue;
+                        }
+                        fend = f;  // an ENTRY that could pass: the Jacobi iteration from it
+                        g_exit = (uint32_t)nr;
+                        leave = true;
                         break;
                     }
-                    kP += tP; kS += tS; kRT += tRT; kE += tE; kB += tB;
-#pragma unroll
-                    for (int k = 0; k < MD; ++k) ksg[k] = op_seg(ksg[k], segt[k]);
+                    if (leave) break;
                     sb += OST;
+                    if (sb >= sg.len) {
+                        fend = sg.len;
+                        g_exit = frz ? ((uni(sh.mfcut) && !msat(uni64(sh.mfzP))) ? (uint32_t)nf : 0u) : (uint32_t)nr;
+                        break;
+                    }
 #pragma unroll
                     for (int k = 0; k < (int)OE; ++k) rr[k] = rn[k];
+                    lay = nlay;
+                    pr_dt = pr_nx;
                     if (++nst % FULL_FENCE_TILES == 0) __syncthreads();  // bound the visibility of dec[] stores
                 }
-                // every committed ENTRY passed every flow stage: a pending WarmUp token sync persists
-                if (warmm && __ballot(oent) && lane == 0) atomicOr(&sh.warm_reach, warmm);
-                // stretch end: lane accumulators into the round's committed totals
+                // leave the machine: lane accumulators into the round's committed totals, then re-enter the tile
+                // machinery at fend with the guess g_exit
+                if (warmm) {
+                    if (__ballot(oent) && lane == 0) atomicOr(&sh.warm_reach, warmm);
+#pragma unroll
+                    for (int s = 0; s < MF; ++s)
+                        if (((warmm >> s) & 1) && __ballot((freach >> s) & 1) && lane == 0) atomicOr(&sh.warm_reach, 1u << s);
+                }
                 WAVE_SCAN(aP, 0u, op_add);
                 WAVE_SCAN(aS, 0u, op_add);
                 WAVE_SCAN(aRT, 0u, op_add);
@@ -2680,14 +3026,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 WAVE_SCAN(aTI, 0u, op_add);
                 WAVE_SCAN(aTH, 0u, op_add);
                 WAVE_SCAN(aMin, NO_LANE, op_min);
-                if (mixp) WAVE_SCAN(aB, 0u, op_add);
+                WAVE_SCAN(aB, 0u, op_add);
                 lds_barrier();  // sh.part's chunk exchange is read; sh.os_* is written
                 if (lane == 63) {
                     sh.part[wv][0] = aP; sh.part[wv][1] = aS; sh.part[wv][2] = aRT; sh.part[wv][3] = aE;
                     sh.part[wv][4] = aTI; sh.part[wv][5] = aTH; sh.part[wv][6] = aMin; sh.part[wv][7] = aB;
                 }
-                const uint32_t g = uni(sh.os_o);
-                // re-enter the tile machinery at the stop; guesses = the stop's evaluated outcome
+                const uint32_t g = g_exit;
                 tbase = fend / TILE * TILE;
                 c0 = fend - tbase;
                 {
@@ -2709,16 +3054,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                         sh.cminrt = op_min(sh.cminrt, sh.part[w][6]);
                         sh.cB += sh.part[w][7];
                     }
-                    for (int k = 0; k < nd; ++k)
-                        if (sh.rules[nf + k].grade == SG_DEGRADE_GRADE_RT) {
-                            const uint32_t x = sh.os_seg[k];
-                            const int32_t cc = (int32_t)(x & 0x7fffffffu);
-                            sh.rs[nf + k].b = (x & 0x80000000u) ? cc : sh.rs[nf + k].b + cc;
-                        }
+                    if (seg_pending) m_seg();
                     sh.last_out = g;
                     sh.c0 = c0;
                 }
                 lds_barrier();
+                PROF_MARK(13)  // (SG_KPROF: the machine's exit into the tile machinery)
                 continue;
             }
         }
@@ -3293,6 +3634,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
         const unsigned long long tm_end = __builtin_amdgcn_s_memtime(), tot = tm_end - tm_start;
         if (atomicMax(&S.dbg[18], tot) < tot) {  // slowest segment so far: its phases, length, rounds
             for (int k = 0; k < 10; ++k) S.dbg[8 + k] = tph[k];
+            for (int k = 10; k < 14; ++k) S.dbg[52 + k - 10] = tph[k];
+            S.dbg[56] = m_nopen;
+            S.dbg[57] = m_nfrz;
+            S.dbg[58] = m_nround;
             S.dbg[5] = sg.len;
             S.dbg[19] = n_round;
             S.dbg[23] = n_it;
@@ -3319,6 +3664,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     }
     __syncthreads();
     if ((int)tid < nr) S.rstate[roff + tid] = sh.rs[tid];
+    const uint32_t res_u = uni(segs[order[blockIdx.x]].res);  // (recomputed: not held in registers over the kernel)
+    for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
+        reinterpret_cast<uint4*>(S.minb + (uint64_t)res_u * 60)[i] = reinterpret_cast<const uint4*>(sh.minl)[i];
 }
 
 // =================================================================================

@@ -54,3 +54,19 @@ def test_balanced_table_alpha():
     assert (t9 == t9[0]).sum() > (t1 == t1[0]).sum()
     for t in (t1, t9):
         assert set(np.unique(t)) == {0, 1, 2, 3}
+
+
+def test_config_alg_bytes_and_roofline(tmp_path, monkeypatch):
+    # 24 B per event, 4 B per ENTRY, 608 B per touched resource, 2 x 16 B per distinct
+    # (resource, args[0]) of the ENTRYs for the hot-parameter configs
+    from sentinel_amd import _abi as A
+    ev = np.zeros(6, dtype=A.EVENT_DTYPE)
+    ev["res_id"] = [1, 1, 2, 1, 2, 3]
+    ev["kind"] = [A.EV_ENTRY, A.EV_EXIT, A.EV_ENTRY, A.EV_ENTRY, A.EV_ENTRY, A.EV_TRACE]
+    ev["flags"] = [A.F_HAS_ARG, 0, A.F_HAS_ARG, A.F_HAS_ARG, 0, 0]
+    ev["aux"] = [7, 0, 7, 7, 9, 0]
+    base = 6 * 24 + 4 * 4 + 3 * 608
+    assert bench.alg_bytes(ev, False) == base
+    assert bench.alg_bytes(ev, True) == base + 2 * 16 * 2  # (1, 7) and (2, 7)
+    r = bench.config_roofline("C9", 2.0, 16e9, 1 << 20)
+    assert r["bound"] == "hbm" and abs(r["achieved"] - 8000.0) < 1e-6 and abs(r["frac"] - 1.0) < 1e-9

@@ -53,6 +53,9 @@ for i in range(nb):
     names = ["top", "phaseB", "B2wait", "evalC", "commitD", "B1wait", "round_setup", "frozen_stretch", "frozen_reduce", "unused"]
     print("  slowest segment (len %d, %d rounds, %d cycles) phase cycles:" % (v[5], v[19], v[18]),
           {k: "%.0f" % ph[j] for j, k in enumerate(names)})
+    mph = v[52:56].astype(np.float64)
+    print("  slowest segment's round machine: open steps %d, frozen steps %d, round transitions %d; cycles" % (v[56], v[57], v[58]),
+          {k: "%.0f" % mph[j] for j, k in enumerate(["open", "frozen", "round_next", "exit"])})
     print("  slowest: iterations %d mismatched %d frozen-tiles %d open-chunks %d prog %#x flow count %d "
           "first flow behaviour|grade<<8 %#x" % (v[23], v[24], v[27], v[29], v[25], v[26], v[28]))
     print("  open-stretch chunks (all segments of the bin): %d" % d[7])
