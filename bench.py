@@ -656,11 +656,11 @@ def config_lines(dev, c4=None, cpu_events=4_000_000, only=None):
     return rows
 
 
-def latency_line(dev, w, ev, sizes=(1, 64, 1024), calls=2000, warm=200):
+def latency_line(dev, w, ev, sizes=(1, 64, 256, 1024), calls=2000, warm=200):
     """The drop-in under light load: every SphU.entry is synchronous (core/CtSph.java:117-168), so a
-    lightly loaded service pays one engine call per few events.  Synchronous sg_submit_ex of 1, 64 and 1,024 events of
-    the C4 trace from pageable host memory (contexts and origins on every event, as the Java batcher sends them):
-    p50 / p99 / mean host wall time per call."""
+    lightly loaded service pays one engine call per few events.  Synchronous sg_submit_ex of 1, 64, 256 and 1,024 events
+    of the C4 trace from pageable host memory (contexts and origins on every event, as the Java batcher sends them):
+    p50 / p99 / mean host wall time per call.  Up to 256 events a call is one k_tiny launch (engine.cpp tiny_impl)."""
     import torch
     from sentinel_amd import engine as E
     from sentinel_amd import tracegen as T
@@ -690,9 +690,10 @@ def latency_line(dev, w, ev, sizes=(1, 64, 1024), calls=2000, warm=200):
         off += need
     eng.close()
     torch.cuda.empty_cache()
-    return {"config": "drop-in latency floor: synchronous sg_submit_ex of 1 / 64 / 1024 C4 events from pageable host "
-                      "memory, contexts + origins", "unit": "ms per call", "latency": out,
-            "note": "each call: the group stage, one host round trip for the bins, the decide stage, the decisions back"}
+    return {"config": "drop-in latency floor: synchronous sg_submit_ex of %s C4 events from pageable host memory, "
+                      "contexts + origins" % " / ".join(str(n) for n in sizes), "unit": "ms per call", "latency": out,
+            "note": "<= 256 events: the events in, one k_tiny launch (every stage in one workgroup), the decisions back; "
+                    "larger: the group stage, one host round trip for the bins, the decide stage, the decisions back"}
 
 
 def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60, cpu_requests=2_000_000):

@@ -179,20 +179,13 @@ __device__ __forceinline__ void exc_advance(Node& N, const Bkt* minb, int64_t T)
         }
         N.exc_sum = s;
     } else {
-        // the seconds that fall out of the window, four buckets' loads issued at once (a cold resource moves a few
-        // seconds per event, and one dependent HBM round trip per second sat on its lane's critical path)
+        // the seconds that fall out of the window (one bucket a round trip: issuing four at once measured slower in
+        // k_lite and k_jac<8>, profiles/r06 A/B)
         const int64_t x1 = T - 60000;
-        for (int64_t x = N.exc_sum_sec - 59000; x <= x1; x += 4000) {
-            int64_t ws[4], ex[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {  // (every slot is a valid bucket: the loads are unconditional)
-                const int sl = (int)(((x + 1000 * u) / 1000) % 60);
-                ws[u] = sl == N.pfslot ? N.pf.ws : minb[sl].ws;
-                ex[u] = sl == N.pfslot ? N.pf.exc : minb[sl].exc;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (x + 1000 * u <= x1 && ws[u] == x + 1000 * u) N.exc_sum -= ex[u];
+        for (int64_t x = N.exc_sum_sec - 59000; x <= x1; x += 1000) {
+            const int sl = (int)((x / 1000) % 60);
+            const Bkt b = sl == N.pfslot ? N.pf : minb[sl];
+            if (b.ws == x) N.exc_sum -= b.exc;
         }
     }
     N.exc_sum_sec = T;

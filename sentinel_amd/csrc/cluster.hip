@@ -252,8 +252,12 @@ __global__ void k_lim_apply(const uint64_t n, const uint32_t* __restrict__ fidx,
     vals[i] = (uint32_t)i;
 }
 
-// ---- 3. one flowId's requests, a workgroup of TF_T lanes, chunks of TF_T requests in time order
-#define TF_T 1024
+// ---- 3. one flowId's requests, a workgroup of TF_T lanes, chunks of TF_T requests in time order.  A flow's cost is
+// one step per chunk plus one per window sub-bucket its requests touch (~20 a flow, up to ~160, over 10k flows), each
+// a dozen block-wide scans: a 1024-lane workgroup for a flow with more than `light` requests in the call, a one-wave
+// workgroup (the same code, its barriers a single wave's) for the rest, both launches side by side (the engine's
+// tok_light, SG_TOK_LIGHT; default 8192).
+template <int TF_T>
 __device__ __forceinline__ uint32_t tf_scan_excl(uint32_t v, uint32_t* red, uint32_t* total) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
@@ -270,6 +274,7 @@ __device__ __forceinline__ uint32_t tf_scan_excl(uint32_t v, uint32_t* red, uint
     *total = tot;
     return pre + x - v;
 }
+template <int TF_T>
 __device__ __forceinline__ int64_t tf_min(int64_t v, int64_t* red) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -282,6 +287,7 @@ __device__ __forceinline__ int64_t tf_min(int64_t v, int64_t* red) {
     return m;
 }
 // six 64-bit sums at once: one wave reduction each, one barrier
+template <int TF_T>
 __device__ __forceinline__ void tf_sum6(int64_t v[6], int64_t (*red)[6]) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -300,6 +306,7 @@ __device__ __forceinline__ void tf_sum6(int64_t v[6], int64_t (*red)[6]) {
         v[k] = m;
     }
 }
+template <int TF_T>
 __device__ __forceinline__ int64_t tf_scan64_excl(int64_t v, int64_t* red) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     int64_t x = v;
@@ -318,8 +325,20 @@ __device__ __forceinline__ int64_t tf_scan64_excl(int64_t v, int64_t* red) {
 #define TF_NONE ((int64_t)1 << 62)
 #define TF_NB 64  // ClusterMetric windows kept in LDS for the workgroup's life (more samples: in HBM)
 enum : uint8_t { TS_BLOCK = 0, TS_PASS = 1, TS_WAIT = 2 };
-__global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict__ skeys,
-                                                      const uint32_t* __restrict__ svals, uint64_t n,
+// bounds[f] = the first sorted position of flow f (lower_bound of the keys), f = 0 .. nflows
+__global__ void k_tok_bounds(const uint32_t* __restrict__ skeys, uint64_t n, uint32_t nflows,
+                             uint32_t* __restrict__ bounds) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const int64_t prev = i == 0 ? -1 : (int64_t)skeys[i - 1];
+    const int64_t k = i == n ? (int64_t)nflows : (int64_t)skeys[i];
+    const int64_t top = k < (int64_t)nflows ? k : (int64_t)nflows;
+    for (int64_t f = prev + 1; f <= top; ++f) bounds[f] = (uint32_t)i;
+}
+// flows with lo_cnt < requests <= hi_cnt
+template <int TF_T>
+__global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict__ svals, const uint32_t* __restrict__ bounds,
+                                                      uint32_t lo_cnt, uint32_t hi_cnt,
                                                       const sg_token_req* __restrict__ req, CFlow* __restrict__ flows,
                                                       uint32_t nflows, CBkt* __restrict__ bkts, double exceed,
                                                       double max_occ_ratio, sg_token_result* __restrict__ res) {
@@ -333,20 +352,11 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
     __shared__ CFlow lflow;
     __shared__ CBkt lbkt[TF_NB];
     __shared__ int64_t sh_S, sh_W0, sh_PS0, sh_head, sh_cur0, sh_wadd;
-    __shared__ uint32_t sh_seq, sh_lo, sh_hi, sh_headcur;
+    __shared__ uint32_t sh_seq, sh_headcur;
     const uint32_t f = blockIdx.x, t = threadIdx.x;
     if (f >= nflows) return;
-    if (t == 0) {  // lower_bound(skeys, f), lower_bound(skeys, f + 1)
-        uint64_t lo = 0, hi = n;
-        while (lo < hi) { const uint64_t mid = (lo + hi) / 2; if (skeys[mid] < f) lo = mid + 1; else hi = mid; }
-        uint64_t e = lo, h2 = n;
-        while (e < h2) { const uint64_t mid = (e + h2) / 2; if (skeys[mid] <= f) e = mid + 1; else h2 = mid; }
-        sh_lo = (uint32_t)lo;
-        sh_hi = (uint32_t)e;
-    }
-    __syncthreads();
-    const uint32_t lo = sh_lo, hi = sh_hi;
-    if (lo == hi) return;
+    const uint32_t lo = bounds[f], hi = bounds[f + 1];
+    if (hi - lo <= lo_cnt || hi - lo > hi_cnt) return;
     // the flow's metric: its view and windows in LDS while the workgroup runs (lane 0 works on them; written back)
     const CFlow gf = flows[f];
     const bool in_lds = gf.n <= TF_NB;
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
             __syncthreads();
             const int64_t sba = lred[0];
             uint32_t nrun;
-            (void)tf_scan_excl(t < cn && t >= a && sb == sba ? 1u : 0u, ured, &nrun);
+            (void)tf_scan_excl<TF_T>(t < cn && t >= a && sb == sba ? 1u : 0u, ured, &nrun);
             const uint32_t b = a + nrun;  // (positions are time ordered: the run is [a, b))
             const bool in = t >= a && t < b;
             if (sh_seq) {  // the reference's order, request by request
@@ -442,23 +452,23 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
             bool undec = in, pass = false;
             for (;;) {
                 if (undec && L < P) undec = false;
-                const int64_t V = tf_min(undec ? L : TF_NONE, lred);
+                const int64_t V = tf_min<TF_T>(undec ? L : TF_NONE, lred);
                 if (V == TF_NONE) break;
                 const int64_t need = V - P + 1;
                 uint32_t nu;
-                const uint32_t rk = tf_scan_excl(undec ? 1u : 0u, ured, &nu);
+                const uint32_t rk = tf_scan_excl<TF_T>(undec ? 1u : 0u, ured, &nu);
                 if (undec && (int64_t)rk < need) { pass = true; myP = P + rk; undec = false; }
                 if ((int64_t)nu <= need) break;
                 P = V + 1;
             }
             // the PASS sum each position sees (the acquire prefix of the run's passes)
             {
-                const int64_t ex = tf_scan64_excl(pass ? (int64_t)acq : 0, lred);
+                const int64_t ex = tf_scan64_excl<TF_T>(pass ? (int64_t)acq : 0, lred);
                 if (in) spass[t] = ex;
             }
             const bool fp = in && !pass && prio;  // tries tryOccupyNext
             uint32_t nfp;
-            const uint32_t fr = tf_scan_excl(fp ? 1u : 0u, ured, &nfp);
+            const uint32_t fr = tf_scan_excl<TF_T>(fp ? 1u : 0u, ured, &nfp);
             if (fp) flist[fr] = t;
             if (in) sst[t] = pass ? TS_PASS : TS_BLOCK;
             __syncthreads();
@@ -497,7 +507,7 @@ __global__ __launch_bounds__(TF_T) void k_tok_flow_wg(const uint32_t* __restrict
             // the window's counts of the run
             int64_t cs[6] = {st == TS_PASS ? acq : 0, st == TS_PASS ? 1 : 0, st == TS_PASS && prio ? acq : 0,
                              st == TS_BLOCK ? acq : 0, st == TS_BLOCK ? 1 : 0, st == TS_BLOCK && prio ? acq : 0};
-            tf_sum6(cs, red6);
+            tf_sum6<TF_T>(cs, red6);
             if (t == 0) {
                 CBkt* cur = cm_current(M, sba * M.wlen);
                 cur->c[CF_PASS] += cs[0];
@@ -530,12 +540,27 @@ hipError_t launch_tok_limiter(const sg_token_req* req, uint64_t n, const uint32_
     hipLaunchKernelGGL(k_tok_limiter, dim3(1), dim3(64), 0, st, req, n, fidx, nflows, lim, allowed, keys, vals, res);
     return hipGetLastError();
 }
+// bounds: nflows + 1 device words.  The flows of more than `light` requests on hs (after `fork`, recording `join`),
+// the rest on st, which then waits for `join`
 hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_token_req* req,
                            CFlow* flows, uint32_t nflows, CBkt* bkts, double exceed, double max_occ_ratio,
-                           sg_token_result* res, hipStream_t st) {
+                           sg_token_result* res, uint32_t* bounds, uint32_t light, uint32_t wide, hipStream_t st,
+                           hipStream_t hs, hipEvent_t fork, hipEvent_t join) {
     if (!n || !nflows) return hipSuccess;
-    hipLaunchKernelGGL(k_tok_flow_wg, dim3(nflows), dim3(TF_T), 0, st, skeys, svals, n, req, flows, nflows, bkts, exceed,
-                       max_occ_ratio, res);
+    hipLaunchKernelGGL(k_tok_bounds, dim3((uint32_t)((n + 256) / 256)), dim3(256), 0, st, skeys, n, nflows, bounds);
+    hipError_t e = hipEventRecord(fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(hs, fork, 0);
+    if (e != hipSuccess) return e;
+    if (wide == 1024)
+        hipLaunchKernelGGL(k_tok_flow_wg<1024>, dim3(nflows), dim3(1024), 0, hs, svals, bounds, light, 0xFFFFFFFFu, req,
+                           flows, nflows, bkts, exceed, max_occ_ratio, res);
+    else
+        hipLaunchKernelGGL(k_tok_flow_wg<512>, dim3(nflows), dim3(512), 0, hs, svals, bounds, light, 0xFFFFFFFFu, req,
+                           flows, nflows, bkts, exceed, max_occ_ratio, res);
+    if ((e = hipEventRecord(join, hs)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tok_flow_wg<64>, dim3(nflows), dim3(64), 0, st, svals, bounds, 0u, light, req, flows, nflows,
+                       bkts, exceed, max_occ_ratio, res);
+    if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
     return hipGetLastError();
 }
 // the limiter: bflag / cflag / bidx / cexcl / bstart / kpass are n-word scratch arrays, part the scan partials,

@@ -214,9 +214,11 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
             int lb = 31 - __clz(sg.len | 1);
             if (lb > (int)LANE_BINS - 1) lb = LANE_BINS - 1;
             // k_lite: no param rules, <= 2 DefaultController flow stages (QPS or thread), <= 2 breakers
-            // (or one QPS DefaultController param rule on args[0] before them, scalar args: k_lite<true>)
+            // (or one QPS DefaultController param rule on args[0] before them, scalar args: k_lite<true>), every
+            // flow stage on the ClusterNode (PF_SERIAL: a rule of another strategy, e.g. one whose node is never
+            // selected, FlowRuleChecker.selectReferenceNode, is k_lane's)
             const bool lite = (p.n_param == 0 || ((p.xf & XF_PLITE) && !(pm & PM_ARGL))) && !p.multi && !lane_only &&
-                              (p.pflags & PF_J16) && !(p.pflags & PF_WARM);
+                              (p.pflags & PF_J16) && !(p.pflags & (PF_WARM | PF_SERIAL));
             bin = (lite ? BIN_LITE : (nr <= 4 && !inline_aux) ? BIN_LANE : BIN_LANE16) + (LANE_BINS - 1 - lb);
         }
         // k_lane<16> keeps a PM_AUX resource's nodes inline; on every other owner the post-pass does
@@ -317,25 +319,44 @@ __global__ __launch_bounds__(256) void k_block_sums(const SEv* __restrict__ recs
     if ((uint64_t)(blockIdx.x + 1) * 1024 <= kmin) return;  // (the hot region: k_grp_records)
     __shared__ uint32_t wsum[4];
     const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    // the four records as whole 16-byte loads (x = dt, y = x, z = cnt | rt << 16, w = kind | flags << 8 | code << 16),
+    // then the four exchanges and the four key pairs issued together: one round trip each, not one per item
+    uint4 w[4];
+    bool in[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // (unconditional loads, clamped into the batch: no wait between them)
+        const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
+        in[k] = p < n && p >= kmin;
+        w[k] = reinterpret_cast<const uint4*>(recs)[p < n ? p : n - 1];
+    }
     uint32_t v = 0;
-    bool multi = false, bad = false;
+    unsigned long long* xd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t kind = w[k].w & 0xFFu, code = (w[k].w >> 16) & 0xFFu;
+        if (in[k] && kind == SG_EV_ENTRY) v += w[k].z & 0xFFFFu;
+        xd[k] = nullptr;
+        if (in[k] && kind != SG_EV_ENTRY && code == RC_BATCH)
+            xd[k] = reinterpret_cast<unsigned long long*>(kind == SG_EV_EXIT ? &link[w[k].y].exit_l : &link[w[k].y].trace_l);
+    }
+    auto xch = [&](int k) -> uint32_t {
+        const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
+        return xd[k] ? (uint32_t)(atomicExch(xd[k], ((unsigned long long)epoch << 32) | (uint32_t)p) >> 32) : 0u;
+    };
+    const uint32_t o0 = xch(0), o1 = xch(1), o2 = xch(2), o3 = xch(3);
+    // a cold reference to a cold ENTRY: the same sort key (both keys loaded for every item, clamped)
+    uint32_t ka[4], kb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint64_t p = base + (uint64_t)k * 256 + threadIdx.x;
-        if (p < n && p >= kmin) {
-            const uint4 w = reinterpret_cast<const uint4*>(recs)[p];
-            SEv r;
-            __builtin_memcpy(&r, &w, sizeof(r));
-            if (r.kind == SG_EV_ENTRY) v += r.cnt;
-            else if (r.code == RC_BATCH) {
-                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
-                    r.kind == SG_EV_EXIT ? &link[r.x].exit_l : &link[r.x].trace_l);
-                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | (uint32_t)p);
-                if ((uint32_t)(old >> 32) == epoch) multi = true;
-                if (p >= kmin && r.x >= kmin && skeys[r.x] != skeys[p]) bad = true;
-            }
-        }
+        ka[k] = skeys[p < n ? p : n - 1];
+        kb[k] = skeys[w[k].y < n ? w[k].y : n - 1];
     }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (xd[k] && w[k].y >= kmin && ka[k] != kb[k]) bad = true;
+    const bool multi = o0 == epoch || o1 == epoch || o2 == epoch || o3 == epoch;  // (epochs start at 1)
     if (__ballot(multi) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_MULTI_LINK);
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(bflags, BF_BAD_REF);
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
@@ -1095,14 +1116,12 @@ __device__ void lane_multi(const SEv* __restrict__ recs, const sg_event* __restr
     }
 }
 
+// one segment on one lane (k_lane; the tiny batches' single kernel, k_tiny)
 template <int NRMAX>
-__global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
-                                              const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
-                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
-                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const Seg sg = segs[order[i]];
+__device__ __forceinline__ void lane_seg(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                         const uint32_t* __restrict__ vals, const Seg sg, const DevState& S,
+                                         const DevCfg& cfg, int64_t t0, uint32_t* __restrict__ dec,
+                                         uint32_t* __restrict__ bflags, uint32_t i) {
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
     if (NRMAX >= 16 && (pg.multi & PX_MULTI)) {
@@ -1216,6 +1235,15 @@ __global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, cons
     }
 #endif
 #undef LPROF
+}
+template <int NRMAX>
+__global__ __launch_bounds__(256) void k_lane(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+                                              const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
+                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    lane_seg<NRMAX>(recs, ev, vals, segs[order[i]], S, cfg, t0, dec, bflags, i);
 }
 
 // =================================================================================
@@ -1606,10 +1634,13 @@ enum { Q_P, Q_B, Q_S, Q_RT, Q_E, Q_TH, Q_MIN, Q_TI /* touch | inr << 16 */, Q_TR
 #define OPEN_EPL 4      // open stretches: events per lane per chunk
 #define TG_PASSES 2     // closed-form passes per Jacobi iteration of a THREAD-grade program
 
+// the wide owners hold the resource's minute window in LDS (sh.minl) for their lifetime: the round's leader reads and
+// writes it every second, from HBM a dependent round trip or two per round; the one-wave owner keeps it in HBM (its
+// LDS bounds how many run on a CU)
+#define JAC_MINL(NW) ((NW) >= 4)
 template <int NW, int MF, int MD>
 struct JacSh {
-    Bkt minl[60];  // the resource's minute window, held in LDS for the owner's lifetime (the round's leader reads and
-                   // writes it every second: from HBM that was a dependent round trip or two per round)
+    Bkt minl[JAC_MINL(NW) ? 60 : 1];
     Node node;
     DRule rules[MF + MD];
     RState rs[MF + MD];
@@ -1809,7 +1840,8 @@ __device__ __forceinline__ bool rl_upd(const DRule& r, uint32_t c, uint32_t g, i
 // (one bin's list decided by two instantiations, each with the registers its own kind of segment needs)
 template <int NW, int EP, int WINLOG, int MF, int MD, bool RL, bool SKIP, int CLS = 0>
 #ifndef J4_WAVES
-#define J4_WAVES 1  // waves per SIMD the 256-lane owner is compiled for (A/B builds: -DJ4_WAVES=2 caps it at 256 VGPRs)
+#define J4_WAVES 2  // waves per SIMD the 256-lane owner is compiled for: 2 caps it at 256 registers (the round machine
+                    // took it to ~300 and one workgroup a CU: J4 1.75 -> 2.57 ms per C4 batch; capped 1.47 ms)
 #endif
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1 ? (EP == 1 ? 4 : 2) : (EP == 1 ? (NW == 4 ? J4_WAVES : 1) : 2)))) void k_jac(
     const SEv* __restrict__ recs, const Seg* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t m,
@@ -1833,9 +1865,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
     // the minute window in LDS (sh.minl): loaded here, written back at the segment's end; no other kernel of the
     // decide stage touches this resource's minute buckets while its owner runs
-    for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
-        reinterpret_cast<uint4*>(sh.minl)[i] = reinterpret_cast<const uint4*>(S.minb + (uint64_t)res * 60)[i];
-    const Ctx C{sh.minl, cfg.max_rt, pg.pflags};
+    if (JAC_MINL(NW))
+        for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
+            reinterpret_cast<uint4*>(sh.minl)[i] = reinterpret_cast<const uint4*>(S.minb + (uint64_t)res * 60)[i];
+    const Ctx C{JAC_MINL(NW) ? sh.minl : S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
     // XF_MIX: the param rules come first in the program and k_pq's pre pass has decided them: an ENTRY one of them
     // blocked carries RF_PBLK (its dec[] word is final) and is a block here, nothing more
     const uint32_t roff = pg.rule_off + pg.n_param;
@@ -1892,6 +1925,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     // Jacobi iteration already fills, it spilled the iteration's registers and cost more than it saved)
     constexpr bool OPEN = NW == 4 || NW == 8;
     const bool open_on = OPEN && !(cfg.dbg_flags & 64);
+    // the round machine (open stretches going on frozen and into the next round in place): the 256-lane owner only --
+    // on the 512-lane one (256 registers a lane, two waves a SIMD) its state spilled the chunk loop (A/B: J8 1.40 ->
+    // 1.60 ms per C4 batch), so there an open stretch leaves at every stop as before
+#ifndef JAC_MACH8
+#define JAC_MACH8 0
+#endif
+    constexpr bool MACH = NW == 4 || (NW == 8 && JAC_MACH8);
     const uint32_t open_min = TILE;
     // single-stage programs with closed-form admission guesses (see the Jacobi iteration)
     // (not with param-blocked ENTRYs in the mix: the closed forms count every ENTRY as an acquire)
@@ -2546,7 +2586,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                     const uint32_t q = base + OST + skip_min;
                     return q < sg.len ? (int32_t)recs[sg.start + q].dt : INT32_MAX;
                 };
-                int32_t pr_dt = skip_on ? probe_at(sb) : INT32_MAX, pr_nx = INT32_MAX;
+                int32_t pr_dt = (MACH && skip_on) ? probe_at(sb) : INT32_MAX, pr_nx = INT32_MAX;
                 load_chunk(rr, sb, 0);
                 lds_barrier();  // the leader's machine state
                 // the lanes' committed totals into the round's (leader), WarmUp reach; accumulators restart
@@ -2619,7 +2659,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                 for (;;) {
                     nlay = frz ? 1u : 0u;
                     load_chunk(rn, sb + OST, nlay);  // prefetch the next chunk in the current mode's layout
-                    if (skip_on) pr_nx = probe_at(sb + OST);
+                    if (MACH && skip_on) pr_nx = probe_at(sb + OST);
                     bool leave = false;
                     for (;;) {  // this chunk, in the current mode (again after a mode switch inside it)
                         if (!frz) {
@@ -2697,6 +2737,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                             // the view before the chunk (after the barriers: the leader's carry of the last chunk)
                             const int64_t P0 = uni64(sh.mv[0]), S0 = uni64(sh.mv[1]), RT0 = uni64(sh.mv[2]);
                             const int64_t E0 = uni64(sh.mv[3]), EM0 = uni64(sh.mv[4]), B0 = uni64(sh.mv[5]);
+                            // (the round's flow limits and the RT stages' carry / base, read once a chunk, not per event)
+                            double ofl[MF];
+                            uint32_t oksg[MD];
+                            int32_t opcb[MD];
+#pragma unroll
+                            for (int s = 0; s < MF; ++s) ofl[s] = s < nf ? mlim(s) : 0.0;
+#pragma unroll
+                            for (int k = 0; k < MD; ++k) {
+                                oksg[k] = uni(sh.mksg[k]);
+                                opcb[k] = (int32_t)uni((uint32_t)sh.mpcb[k]);
+                            }
+                            auto oblock = [&](int s, int64_t P, int c) -> bool {
+                                return ((warmm >> s) & 1) ? !((double)(P + c) <= ofl[s])
+                                                          : (double)j_iadd(j_d2i((double)P), c) > ofl[s];
+                            };
                             // RT breakers: which ENTRYs see an average at the threshold, then the segmented passCount scan
                             uint32_t badb = 0, segl[MD], segt[MD];
 #pragma unroll
@@ -2760,16 +2815,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                     const int64_t vS = S0 + (int64_t)(xs + rs2);
 #pragma unroll
                                     for (int s = 0; s < MF; ++s)
-                                        if (s < nf && o == (uint32_t)nr && mblock(s, vP, (int)ec)) o = (uint32_t)s;
+                                        if (s < nf && o == (uint32_t)nr && oblock(s, vP, (int)ec)) o = (uint32_t)s;
 #pragma unroll
                                     for (int k = 0; k < MD; ++k) {
                                         if (k < nd && o == (uint32_t)nr) {
                                             const DRule& r = sh.rules[nf + k];
                                             bool ok = true;
                                             if (r.grade == SG_DEGRADE_GRADE_RT) {
-                                                const uint32_t x = op_seg(uni(sh.mksg[k]), op_seg(segl[k], rseg[k]));
+                                                const uint32_t x = op_seg(oksg[k], op_seg(segl[k], rseg[k]));
                                                 const int32_t cc = (int32_t)(x & 0x7fffffffu);
-                                                const int32_t pcb = (x & 0x80000000u) ? cc : (int32_t)uni((uint32_t)sh.mpcb[k]) + cc;
+                                                const int32_t pcb = (x & 0x80000000u) ? cc : opcb[k] + cc;
                                                 ok = !((badb >> (e * MD + k)) & 1) || (pcb + 1 < 5);
                                             } else if (r.grade == SG_DEGRADE_GRADE_EXCEPTION_RATIO) {
                                                 const double exc = (double)(E0 + (int64_t)(xe + re)) / 1.0;
@@ -2871,20 +2926,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 sh.os_P = myP;
                                 sh.os_t = myt;
 #pragma unroll
-                                for (int k = 0; k < MD; ++k) sh.os_seg[k] = op_seg(uni(sh.mksg[k]), op_seg(segl[k], sst[k]));
+                                for (int k = 0; k < MD; ++k) sh.os_seg[k] = op_seg(oksg[k], op_seg(segl[k], sst[k]));
                             }
                             lds_barrier();
                             seg_pending = true;
                             const uint32_t o_f = uni(sh.os_o);
                             if (f >= sg.len) { fend = sg.len; g_exit = (uint32_t)nr; leave = true; break; }
-                            if (o_f == NO_LANE) {  // the round ended: the next one from f, in this chunk
+                            if (MACH && o_f == NO_LANE) {  // the round ended: the next one from f, in this chunk
                                 if (round_next(f, (int32_t)uni((uint32_t)sh.os_t)) == 2u) {
                                     fend = f; g_exit = (uint32_t)nr; leave = true; break;
                                 }
                                 continue;
                             }
                             const int64_t Pf = uni64(sh.os_P);
-                            if (o_f < (uint32_t)nf && msat(Pf) && pr_dt >= (int32_t)uni((uint32_t)sh.mrhi)) {
+                            if (MACH && o_f < (uint32_t)nf && msat(Pf) && pr_dt >= (int32_t)uni((uint32_t)sh.mrhi)) {
                                 // the quota is spent: frozen until the round ends
                                 if (tid == 0) {
                                     m_seg();
@@ -2896,7 +2951,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
                                 continue;
                             }
                             fend = f;
-                            g_exit = o_f;
+                            g_exit = o_f == NO_LANE ? (uint32_t)nr : o_f;
                             leave = true;
                             break;
                         }
@@ -3664,9 +3719,238 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     }
     __syncthreads();
     if ((int)tid < nr) S.rstate[roff + tid] = sh.rs[tid];
-    const uint32_t res_u = uni(segs[order[blockIdx.x]].res);  // (recomputed: not held in registers over the kernel)
-    for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
-        reinterpret_cast<uint4*>(S.minb + (uint64_t)res_u * 60)[i] = reinterpret_cast<const uint4*>(sh.minl)[i];
+    if (JAC_MINL(NW)) {
+        const uint32_t res_u = uni(segs[order[blockIdx.x]].res);  // (recomputed: not held in registers over the kernel)
+        for (uint32_t i = tid; i < 60u * sizeof(Bkt) / 16u; i += HW)
+            reinterpret_cast<uint4*>(S.minb + (uint64_t)res_u * 60)[i] = reinterpret_cast<const uint4*>(sh.minl)[i];
+    }
+}
+
+// =================================================================================
+// k_tiny: a whole synchronous batch of at most TINY_MAX events in one workgroup (the drop-in's small calls)
+// =================================================================================
+// The drop-in calls sg_submit_ex synchronously (core/CtSph.java:117-168: every SphU.entry waits for its verdict), so a
+// lightly loaded service sends batches of a few events, and the batched pipeline's ~30 launches and its mid-batch host
+// round trip set the latency floor.  Here one workgroup runs every stage with a barrier (and an
+// agent-scope fence) between them: the group stage's checks, marks and key ring (k_grp_first), a bitonic sort of
+// (resource, index) in LDS, the sorted records with same-batch references as sorted positions (k_grp_records) and
+// earlier batches' from the status ring (k_resolve), the chain grants (k_chain), the param maps' growth (k_pm_grow),
+// the decide stage -- one lane per segment on k_lane<16>'s chain (every rule shape; origin / context nodes inline, as
+// k_lane<16> keeps them) -- and the post (decisions in submission order, the status ring: k_post_w).  A batch it
+// cannot take alone -- a chain grant under a finite cap (the host orders those), a param pool that must be compacted
+// first -- raises BF_TINY_FALLBACK before anything but the marks and the key ring (which the batched path writes the
+// same) and growth it would do anyway changed, and the host runs the batched path.
+#define TINY_MAX 256u
+__global__ __launch_bounds__(TINY_MAX) void k_tiny(const sg_event* __restrict__ ev, uint32_t n, DevState S, DevCfg cfg,
+                                                   uint32_t max_res, uint32_t* __restrict__ prio_w,
+                                                   const uint32_t* __restrict__ comp, uint64_t n_args, uint32_t grant_all,
+                                                   unsigned long long* __restrict__ pool_next, uint64_t pool_nb,
+                                                   uint32_t epoch, SEv* __restrict__ recs, uint32_t* __restrict__ vals,
+                                                   uint32_t* __restrict__ dec, Seg* __restrict__ segs,
+                                                   uint32_t* __restrict__ bflags, uint32_t* __restrict__ out) {
+    __shared__ unsigned long long sk[TINY_MAX];  // key << 32 | event index, sorted
+    __shared__ uint32_t posof[TINY_MAX];         // event index -> sorted position
+    __shared__ uint32_t segat[TINY_MAX + 1];     // segment -> its first position
+    __shared__ uint32_t sflags, nseg;
+    const uint32_t t = threadIdx.x;
+    const uint64_t gbase = S.gbase, ring_mask = cfg.ring_mask;
+    if (t == 0) { sflags = 0; nseg = 0; *bflags = 0; }
+    __syncthreads();
+    const int64_t t0 = ev[0].ts;
+    // ---- 1. every event: the batch's checks, the resources' marks, the key ring (k_grp_first)
+    uint32_t fl = 0, key = 0xFFFFFFFFu;
+    if (t < n) {
+        const sg_event e = ev[t];
+        if (e.res_id >= max_res) fl |= BF_BAD_RES;
+        const int64_t dt = e.ts - t0;
+        if (dt < 0 || dt > 0x7FFFFFFFLL) fl |= (dt < 0 ? BF_BACKWARD : BF_TSPAN);
+        if (t > 0 && ev[t - 1].ts > e.ts) fl |= BF_BACKWARD;  // ABI: non-decreasing ts
+        uint32_t mark = 0;
+        uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+        bool own_args = false;
+        if (S.ext) {
+            const sg_event_ext x = S.ext[t];
+            if (x.n_args > SG_MAX_ARGS || (uint64_t)x.arg_off + x.n_args > n_args) fl |= BF_BAD_ARGS;
+            else if (x.n_args) {
+                for (uint32_t k = 0; k < x.n_args; ++k) {
+                    const sg_arg a = S.args[x.arg_off + k];
+                    if (a.kind > SG_ARG_LIST || (a.kind == SG_ARG_LIST && (a.key > n_args || a.len > n_args - a.key)))
+                        fl |= BF_BAD_ARGS;
+                    else if (a.kind == SG_ARG_LIST) {
+                        mark |= PM_ARGL;
+                        for (uint32_t q = 0; q < a.len; ++q)
+                            if (S.args[a.key + q].kind > SG_ARG_SCALAR) fl |= BF_BAD_ARGS;
+                    }
+                }
+                const sg_arg a0 = S.args[x.arg_off];
+                key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                own_args = true;
+            }
+            if (x.context_id > S.max_ctx) mark |= PM_LANE;
+            else if (x.origin_id != 0 || x.context_id != 0) {
+                mark |= PM_AUX;
+                if (x.origin_id >> TAG_ORIGIN_BITS) mark |= PM_LANE;
+            }
+        }
+        if (own_args && e.kind == SG_EV_EXIT && (e.flags & SG_F_EXIT_ARGS)) mark |= PM_XARGS;
+        if (e.kind == SG_EV_ENTRY) {
+            if (S.key_ring) S.key_ring[(gbase + t) & ring_mask] = key0;
+            if (e.flags & SG_F_PRIORITIZED) mark |= PM_PRIO;
+            if (e.flags & SG_F_BLOCKED_UPSTREAM) mark |= PM_LANE;
+        } else {
+            if (e.kind == SG_EV_EXIT && own_args && S.key_ring) S.key_ring[(gbase + t) & ring_mask] = key0;
+            const uint64_t ref = e.aux & SG_REF_NONE;
+            if (ref != SG_REF_NONE && ref >= gbase && ref - gbase >= t) fl |= BF_BAD_REF;  // must follow its ENTRY
+        }
+        if (mark && e.res_id < max_res && (prio_w[e.res_id] & mark) != mark) atomicOr(&prio_w[e.res_id], mark);
+        key = (comp && e.res_id < max_res) ? comp[e.res_id] : e.res_id;
+    }
+    sk[t] = t < n ? (((unsigned long long)key << 32) | t) : ~0ull;
+    if (fl) atomicOr(&sflags, fl);
+    __syncthreads();
+    // ---- 2. (resource, index) sorted: every resource's events contiguous, in event order
+    for (uint32_t k = 2; k <= TINY_MAX; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t l = t ^ j;
+            if (l > t) {
+                const unsigned long long a = sk[t], b = sk[l];
+                if (((t & k) == 0) == (a > b)) { sk[t] = b; sk[l] = a; }
+            }
+            __syncthreads();
+        }
+    const bool first = t < n && (t == 0 || (sk[t] >> 32) != (sk[t - 1] >> 32));
+    if (t < n) posof[(uint32_t)sk[t]] = t;
+    if (first) segat[atomicAdd(&nseg, 1u)] = t;  // (segment ids in any order: each lane decides its own)
+    __syncthreads();
+    // ---- 3. the sorted records (k_grp_records, k_resolve)
+    if (t < n) {
+        const uint32_t i = (uint32_t)sk[t];
+        const sg_event e = ev[i];
+        SEv r;
+        r.dt = (int32_t)(e.ts - t0);
+        r.x = 0;
+        r.cnt = e.count;
+        r.rt = 0;
+        r.kind = e.kind;
+        r.flags = (uint8_t)(e.flags & 0x3Fu);
+        r.code = RC_NONE;
+        r.pad = 0;
+        uint32_t tag = 0;
+        bool own_args = false;
+        uint64_t key0 = (e.flags & SG_F_HAS_ARG) ? e.aux : NO_KEY;
+        if (S.ext) {
+            const sg_event_ext x = S.ext[i];
+            if (x.n_args && x.n_args <= SG_MAX_ARGS) {
+                const sg_arg a0 = S.args[x.arg_off];
+                key0 = a0.kind == SG_ARG_SCALAR ? a0.key : NO_KEY;
+                own_args = true;
+            }
+            if (x.context_id <= S.max_ctx && (x.origin_id != 0 || x.context_id != 0) && !(x.origin_id >> TAG_ORIGIN_BITS))
+                tag = x.origin_id | (x.context_id << TAG_ORIGIN_BITS);
+        }
+        if (own_args) {
+            r.flags = (uint8_t)((r.flags & ~SG_F_HAS_ARG) | (key0 != NO_KEY ? SG_F_HAS_ARG : 0));
+            if (e.kind == SG_EV_EXIT) r.flags |= RF_OWN_ARGS;
+        }
+        r.x = tag;
+        if (e.kind != SG_EV_ENTRY) {
+            if (e.kind == SG_EV_EXIT) {
+                const int64_t raw = (int64_t)(e.aux >> 48);
+                r.rt = (uint16_t)(raw > cfg.max_rt ? cfg.max_rt : raw);
+            }
+            const uint64_t ref = e.aux & SG_REF_NONE;
+            if (ref != SG_REF_NONE && ref >= gbase && ref - gbase < i) {
+                const uint32_t j = (uint32_t)(ref - gbase);
+                if (ev[j].kind == SG_EV_ENTRY) {
+                    const uint32_t pj = posof[j];
+                    if ((sk[pj] >> 32) != (sk[t] >> 32)) atomicOr(&sflags, (uint32_t)BF_BAD_REF);  // another resource's
+                    r.code = RC_BATCH;
+                    r.x = pj;
+                } else {
+                    r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;  // names a non-ENTRY: as an unknown entry
+                }
+            } else if (ref != SG_REF_NONE && ref < gbase) {  // an ENTRY of an earlier batch: its status in the ring
+                const uint8_t st = S.ring[ref & ring_mask];
+                if (st == ST_NOT_ENTRY) r.code = e.kind == SG_EV_EXIT ? RC_NONE : RC_NOT;
+                else r.code = (st == ST_PASS || st == ST_PASS_WAIT) ? RC_PASSED : RC_NOT;
+            }
+        }
+        recs[t] = r;
+        vals[t] = i | (e.kind == SG_EV_ENTRY ? 0x80000000u : 0u);
+    }
+    __syncthreads();
+    const uint32_t m = nseg;
+    // a segment's extent: its start and the next start in position order (starts sorted by a rank among them)
+    Seg sg{};
+    if (t < m) {
+        const uint32_t a = segat[t];
+        uint32_t b = n;
+        for (uint32_t q = 0; q < m; ++q) { const uint32_t c = segat[q]; if (c > a && c < b) b = c; }
+        sg.res = (uint32_t)(sk[a] >> 32);
+        sg.start = a;
+        sg.len = b - a;
+        sg.bin = 0;
+        segs[t] = sg;
+    }
+    if (sflags & (BF_BAD_RES | BF_BACKWARD | BF_TSPAN | BF_BAD_ARGS | BF_BAD_REF)) {  // rejected before any decision
+        if (t == 0) *bflags = sflags | BF_TINY_REJECTED;
+        return;
+    }
+    // ---- 4. chain grants (k_chain: CtSph.lookProcessChain) and the param maps' growth (k_pm_grow)
+    if (t < m && cfg.switch_on) {
+        auto looks_up = [&](uint32_t j) {
+            return recs[sg.start + j].kind == SG_EV_ENTRY &&
+                   (!S.ext || S.ext[vals[sg.start + j] & 0x7FFFFFFFu].context_id <= S.max_ctx);
+        };
+        const bool multi = (S.prog[sg.res].multi & PX_MULTI) != 0;
+        for (uint32_t j = 0; j < sg.len; ++j) {
+            if (!looks_up(j)) continue;
+            const uint32_t res = multi ? ev[vals[sg.start + j] & 0x7FFFFFFFu].res_id : sg.res;
+            const uint32_t f = S.info[res].flags;
+            if (f & (NI_CHAIN | NI_REJECTED)) { if (!multi) break; continue; }
+            // grant_all: 1 unbounded cap (grant in place), 0 finite cap not reached (the host grants in first-ENTRY
+            // order: fall back), 2 cap reached (no grants; the batched path skips k_chain)
+            if (grant_all == 1u) S.info[res].flags = f | NI_CHAIN;
+            else if (grant_all == 0u) atomicOr(&sflags, (uint32_t)BF_TINY_FALLBACK);
+            if (!multi) break;
+        }
+    }
+    __syncthreads();
+    if (t < m && pool_nb && !(sflags & BF_TINY_FALLBACK)) {
+        const Prog pg = S.prog[sg.res];
+        if (pg.tm_base != NO_ID || pg.n_param != 0) {
+            const uint64_t adds = (S.prio && (S.prio[sg.res] & PM_ARGL)) ? 0xFFFFFFFFull : (uint64_t)sg.len;
+            for (int k = 0; k < pg.n_param; ++k) {
+                const DRule& r = S.rules[pg.rule_off + k];
+                if (r.behavior != PB_INIT_ONLY && r.grade == SG_FLOW_GRADE_QPS)
+                    pm_grow(S, r.pmap, adds, pool_next, pool_nb, bflags, nullptr, nullptr, 0, epoch);
+            }
+            if (pg.tm_base != NO_ID)
+                for (int i = 0; i < SG_MAX_ARGS; ++i) {
+                    const uint32_t id = S.tmid[pg.tm_base + i];
+                    if (id != NO_ID) pm_grow(S, id, adds, pool_next, pool_nb, bflags, nullptr, nullptr, 0, epoch);
+                }
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    if (pool_nb && t == 0 && pool_next[PC_RESCUE] == epoch) atomicOr(&sflags, (uint32_t)BF_TINY_FALLBACK);
+    __syncthreads();
+    if (sflags & BF_TINY_FALLBACK) {
+        if (t == 0) atomicOr(bflags, sflags);
+        return;
+    }
+    // ---- 5. decide: one lane per segment (k_lane<16>)
+    if (t < m) lane_seg<16>(recs, ev, vals, sg, S, cfg, t0, dec, bflags, t);
+    __threadfence();
+    __syncthreads();
+    // ---- 6. decisions in submission order, the status ring (k_post_w)
+    if (t < n) {
+        const uint32_t d = ev[t].kind == SG_EV_ENTRY ? dec[posof[t]] : (uint32_t)ST_NOT_ENTRY;
+        out[t] = d;
+        S.ring[(gbase + t) & ring_mask] = (uint8_t)(d & 0xFF);
+    }
+    if (t == 0 && sflags) atomicOr(bflags, sflags);
 }
 
 // =================================================================================
@@ -3768,6 +4052,16 @@ hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, 
     return hipGetLastError();
 }
 // bin = BIN_J16 / BIN_J8 / BIN_J4 / BIN_J1 / BIN_LANE (range of lane bins, nr <= 4) / BIN_LANE16
+hipError_t launch_tiny(const sg_event* ev, uint32_t n, const DevState& S, const DevCfg& cfg, uint32_t max_res,
+                       uint32_t* prio_w, const uint32_t* comp, uint64_t n_args, uint32_t grant_all,
+                       unsigned long long* pool_next, uint64_t pool_nb, uint32_t epoch, SEv* recs, uint32_t* vals,
+                       uint32_t* dec, Seg* segs, uint32_t* bflags, uint32_t* out, hipStream_t st) {
+    if (n == 0 || n > TINY_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tiny, dim3(1), dim3(TINY_MAX), 0, st, ev, n, S, cfg, max_res, prio_w, comp, n_args, grant_all,
+                       pool_next, pool_nb, epoch, recs, vals, dec, segs, bflags, out);
+    return hipGetLastError();
+}
+uint32_t tiny_max() { return TINY_MAX; }
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st) {

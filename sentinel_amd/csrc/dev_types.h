@@ -457,7 +457,9 @@ enum : uint32_t { BF_PRIORITIZED = 1,
                   BF_AUX_FULL = 1024,   // the origin / context node pool is full
                   BF_POOL_FULL = 2048,  // a param map could not grow: the bucket pool (param_table_log2) is used up
                   BF_MULTI_LINK = 128,  // an ENTRY is referenced by two EXITs (or two TRACEs) of the batch
-                  BF_ZERO_CNT = 256 };  // an ENTRY acquires 0 (it may pass inside a saturated stretch)
+                  BF_ZERO_CNT = 256,    // an ENTRY acquires 0 (it may pass inside a saturated stretch)
+                  BF_TINY_FALLBACK = 4096,  // k_tiny: the batch needs the batched path (nothing decided)
+                  BF_TINY_REJECTED = 8192 };  // k_tiny: the batch's checks failed before any decision
 
 // One event in resource-sorted order (16 B), built by k_prep from the caller's 24-byte
 // sg_event so that every decide kernel streams its segment with coalesced loads.

@@ -149,6 +149,11 @@ hipError_t launch_post(const uint32_t* pos_of, const uint32_t* dec, uint64_t n, 
 hipError_t launch_chain(const SEv* recs, const uint32_t* vals, const Seg* segs, uint32_t m, NodeInfo* info,
                         uint32_t grant_all, uint32_t* ncand, uint64_t* cand, const sg_event* ev, const Prog* prog,
                         const sg_event_ext* ext, uint32_t max_ctx, hipStream_t st);
+hipError_t launch_tiny(const sg_event* ev, uint32_t n, const DevState& S, const DevCfg& cfg, uint32_t max_res,
+                       uint32_t* prio_w, const uint32_t* comp, uint64_t n_args, uint32_t grant_all,
+                       unsigned long long* pool_next, uint64_t pool_nb, uint32_t epoch, SEv* recs, uint32_t* vals,
+                       uint32_t* dec, Seg* segs, uint32_t* bflags, uint32_t* out, hipStream_t st);
+uint32_t tiny_max();
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st);
@@ -166,7 +171,8 @@ hipError_t launch_tok_limiter(const sg_token_req* req, uint64_t n, const uint32_
                               hipStream_t st);
 hipError_t launch_tok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_token_req* req,
                            CFlow* flows, uint32_t nflows, CBkt* bkts, double exceed, double max_occ_ratio,
-                           sg_token_result* res, hipStream_t st);
+                           sg_token_result* res, uint32_t* bounds, uint32_t light, uint32_t wide, hipStream_t st,
+                           hipStream_t hs, hipEvent_t fork, hipEvent_t join);
 hipError_t launch_ptok_flow(const uint32_t* skeys, const uint32_t* svals, uint64_t n, const sg_param_token_req* req,
                             const uint64_t* values, PFlow* flows, uint32_t nflows, const PHot* hot, PVal* tab,
                             uint32_t mask, sg_token_result* res, uint32_t* flags, hipStream_t st);
@@ -598,6 +604,9 @@ struct sg_engine {
     uint32_t* d_hot_part = nullptr;  // the hot scan's per-chunk partials ((max tiles / 64 + 2) x HOT_MAX words)
     uint32_t* d_hot_hb = nullptr;    // per hot id: first sorted position, total (2 x HOT_MAX words)
     bool radix_group = false;    // SG_DEBUG_FLAGS & 8192: the all-radix group stage (A/B)
+    uint32_t tok_light = 8192;   // SG_TOK_LIGHT: token flows of at most this many requests a call on one-wave workgroups
+    uint32_t tok_wide = 512;     // SG_TOK_WIDE: 512 or 1024 lanes for the other token flows
+    bool tiny_on = true;         // SG_TINY=0: synchronous batches of <= 256 events through the batched path too
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
     AuxNode* d_auxtab = nullptr;
     uint32_t* d_auxcnt = nullptr;
@@ -687,6 +696,8 @@ struct sg_engine {
     sg_token_req* d_treq = nullptr;
     sg_token_result* d_tres = nullptr;
     uint32_t* d_tfidx = nullptr;
+    uint32_t* d_tbounds = nullptr;  // the flows' first sorted positions (nflows + 1 words)
+    uint32_t tbounds_cap = 0;
     uint64_t tcap = 0;
     // cluster param flows (ClusterParamFlowRuleManager / ClusterParamMetricStatistics roles)
     std::vector<PFlow> pflows;                    // host copy of the config part
@@ -1289,6 +1300,9 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J1_MAX")) { e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
+    if (const char* v = std::getenv("SG_TINY")) e->tiny_on = v[0] != '0';
+    if (const char* v = std::getenv("SG_TOK_WIDE")) e->tok_wide = std::atoi(v) == 1024 ? 1024u : 512u;
+    if (const char* v = std::getenv("SG_TOK_LIGHT")) e->tok_light = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J1_STREAM")) e->j1_stream = std::atoi(v);
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
     if (const char* v = std::getenv("SG_MIX")) e->mix_on = v[0] != '0';
@@ -1428,7 +1442,7 @@ int sg_engine_destroy(sg_engine* e) {
     dfree(e->d_prio); dfree(e->d_hot_tab); dfree(e->d_hot_list); dfree(e->d_hot_part); dfree(e->d_hot_hb); dfree(e->d_comp); dfree(e->d_auxtab); dfree(e->d_auxpool); dfree(e->d_auxcnt); dfree(e->d_auxmeta);
     dfree(e->d_pflow); dfree(e->d_phot); dfree(e->d_pftab); dfree(e->d_pvtab); dfree(e->d_preq); dfree(e->d_pvals);
     dfree(e->d_cflow); dfree(e->d_cbkt); dfree(e->d_ctab); dfree(e->d_nslim); dfree(e->d_borrow); dfree(e->d_keyring);
-    dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx);
+    dfree(e->d_treq); dfree(e->d_tres); dfree(e->d_tfidx); dfree(e->d_tbounds);
     dfree(e->d_snap_cnt); dfree(e->d_snap_off); dfree(e->d_snap_out); dfree(e->d_dbg);
     for (auto& B : e->slot)
         for (auto& v : B.ev) if (v) (void)hipEventDestroy(v);
@@ -2652,6 +2666,111 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     return SG_OK;
 }
 
+// A synchronous batch of at most tiny_max() events in one kernel (decide.hip k_tiny: every stage in one workgroup):
+// the drop-in's small calls.  Returns SG_OK, an error (as the batched path's, at the same points: a malformed batch is
+// rejected before any decision), or TINY_FALLBACK when the batch needs the batched path (a chain grant under a finite
+// cap, which the host orders; a param pool that must be compacted first) -- nothing was decided then.
+constexpr int TINY_FALLBACK = 1;
+static int tiny_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
+                     uint64_t n_args, uint32_t* out) {
+    if (!e || !ev || !out) return fail(SG_EINVAL, "null argument");
+    if (n_args && !args) return fail(SG_EINVAL, "null args table");
+    if (!e->fatal.empty()) return fail(SG_ESTATE, e->fatal + " -- engine unusable, recreate it");
+    if (n > e->cfg.max_batch_events) return fail(SG_EINVAL, "batch larger than max_batch_events");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = ensure_batch(e, n);
+    if (rc) return rc;
+    if ((rc = drain(e))) return rc;  // every earlier batch decided: the status ring holds their verdicts
+    if ((rc = ensure_pool2(e))) return rc;
+    const unsigned long long pfloor = e->h_pool_next ? e->h_pool_next[PC_FLOOR] : 0;
+    if (e->pool_nb && e->h_pool_next[PC_NEXT] > pfloor + (e->pool_nb - pfloor) / 2) return TINY_FALLBACK;  // compaction due
+    const int k = e->cur;
+    activate(e, k);
+    auto& B = e->slot[k];
+    hipStream_t st = e->stream;
+    const sg_event* dev_ev = ev;
+    const bool host_out = !is_device_ptr(out);
+    if (!is_device_ptr(ev)) {
+        HIPCHK(hipMemcpyAsync(e->d_ev, ev, n * sizeof(sg_event), hipMemcpyHostToDevice, st));
+        dev_ev = e->d_ev;
+    }
+    uint32_t* dev_out = host_out ? e->d_out : out;
+    const sg_event_ext* dev_ext = ext;
+    const sg_arg* dev_args = n_args ? args : nullptr;
+    if (ext && !is_device_ptr(ext)) {
+        if (n > B.ext_cap) {
+            dfree(B.d_ext);
+            B.ext_cap = std::max<uint64_t>(n, 1u << 16);
+            HIPCHK(hipMalloc(&B.d_ext, B.ext_cap * sizeof(sg_event_ext)));
+        }
+        HIPCHK(hipMemcpyAsync(B.d_ext, ext, n * sizeof(sg_event_ext), hipMemcpyHostToDevice, st));
+        dev_ext = B.d_ext;
+    }
+    if (n_args && !is_device_ptr(args)) {
+        if (n_args > B.args_cap) {
+            dfree(B.d_args);
+            B.args_cap = std::max<uint64_t>(n_args, 1u << 16);
+            HIPCHK(hipMalloc(&B.d_args, B.args_cap * sizeof(sg_arg)));
+        }
+        HIPCHK(hipMemcpyAsync(B.d_args, args, n_args * sizeof(sg_arg), hipMemcpyHostToDevice, st));
+        dev_args = B.d_args;
+    }
+    if (++e->epoch == 0) e->epoch = 1;
+    DevCfg dc;
+    std::memset(&dc, 0, sizeof(dc));
+    dc.max_rt = e->cfg.statistic_max_rt;
+    dc.occupy_timeout = e->cfg.occupy_timeout_ms;
+    dc.max_chain = e->cfg.max_slot_chain_size;
+    dc.switch_on = e->cfg.switch_on;
+    dc.ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
+    dc.dbg_flags = e->dbg_flags;
+    DevState S{};
+    std::memset(&S, 0, sizeof(S));
+    S.sec = e->d_sec; S.minb = e->d_minb; S.info = e->d_info; S.prog = e->d_prog; S.rules = e->d_rules;
+    S.rstate = e->d_rstate; S.hot = e->d_hot; S.pmap = e->d_pmap; S.pbkt = e->d_pbkt; S.pdat = e->d_pdat;
+    S.pbm = e->d_pbm; S.ppre = e->d_ppre; S.tmid = e->d_tmid; S.ring = e->d_ring; S.sink = e->d_sink;
+    S.borrow = e->d_borrow; S.prio = e->d_prio; S.key_ring = e->d_keyring; S.gbase = e->gbase; S.link = e->d_link;
+    S.bst = e->d_bst; S.pend = e->d_pend; S.spans = e->d_spans; S.nspan = e->d_bsmall + 120; S.span_cap = e->span_cap;
+    S.epoch = e->epoch; S.skip_ok = 0; S.skip_min = e->skip_min; S.ext = dev_ext; S.args = dev_args;
+    S.aux_tab = e->d_auxtab; S.aux_count = e->d_auxcnt; S.aux_cap = e->cfg.aux_node_capacity; S.aux_mask = e->aux_mask;
+    S.max_ctx = SG_MAX_CONTEXTS;
+    // the chain grants: every one in place (no cap), none (a cap reached: CtSph.lookProcessChain then returns null),
+    // or the host's, in first-ENTRY order (the batched path)
+    const int cap = e->cfg.max_slot_chain_size;
+    const uint32_t grants = cap <= 0 ? 1u : e->n_chains >= (uint32_t)cap ? 2u : 0u;
+    HIPCHK(launch_tiny(dev_ev, (uint32_t)n, S, dc, e->cfg.max_resources, e->d_prio, e->d_comp, n_args, grants,
+                       e->d_pool_next, e->pool_nb, e->epoch, e->d_recs, e->d_v0, e->d_dec, e->d_segs, e->d_bsmall,
+                       dev_out, st));
+    uint32_t bflags = 0;
+    HIPCHK(hipMemcpyAsync(&bflags, e->d_bsmall, 4, hipMemcpyDeviceToHost, st));
+    if (host_out) HIPCHK(hipMemcpyAsync(out, dev_out, n * 4, hipMemcpyDeviceToHost, st));
+    if (e->pool_nb) HIPCHK(hipMemcpyAsync(e->h_pool_next, e->d_pool_next, PC_WORDS * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (bflags & BF_TINY_FALLBACK) return TINY_FALLBACK;
+    if (bflags & BF_TINY_REJECTED) {  // rejected before any decision: submit_impl's checks, in its order
+        if (bflags & BF_BAD_RES) return fail(SG_EINVAL, "event res_id >= max_resources");
+        if (bflags & BF_BAD_REF)
+            return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
+        if (bflags & BF_TSPAN) return fail(SG_EINVAL, "a batch must span less than 2^31 ms");
+        if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing (SURVEY Q3)");
+        return fail(SG_EINVAL, "an sg_event_ext names args outside the table (or more than SG_MAX_ARGS, or a bad kind)");
+    }
+    e->gbase += n;
+    // the decide stage's own flags (collect)
+    if (bflags & BF_BAD_REF)
+        return fail(SG_EINVAL, "an EXIT/TRACE references an event that is not an earlier ENTRY of the same resource");
+    if (bflags & BF_BACKWARD) return fail(SG_EINVAL, "event timestamps must be non-decreasing across batches (SURVEY Q3)");
+    if (bflags & BF_AUX_FULL) return fail(SG_ECAPACITY, "origin/context node pool full (raise aux_node_capacity)");
+    if (bflags & BF_PQ_INVARIANT)
+        e->fatal = "internal error: a k_pq tile's presorted key subset did not match its accesses";
+    else if (bflags & BF_POOL_FULL)
+        e->fatal = "the hot-parameter map pool is used up (raise param_table_log2)";
+    else if (bflags & BF_PTAB_FULL)
+        e->fatal = "a hot-parameter map table could not place a key (its map holds a ghost entry)";
+    if (bflags & (BF_PQ_INVARIANT | BF_PTAB_FULL | BF_POOL_FULL)) return fail(SG_ECAPACITY, e->fatal + " -- engine unusable");
+    return SG_OK;
+}
+
 int sg_submit_async(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
     return submit_impl(e, ev, nullptr, n, nullptr, 0, out);
 }
@@ -2663,6 +2782,10 @@ int sg_submit_ex_async(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
 
 int sg_submit_ex(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, uint64_t n, const sg_arg* args,
                  uint64_t n_args, uint32_t* out) {
+    if (e && e->tiny_on && n && n <= tiny_max() && !e->radix_group) {
+        const int trc = tiny_impl(e, ev, ext, n, args, n_args, out);
+        if (trc != TINY_FALLBACK) return trc;
+    }
     int rc = submit_impl(e, ev, ext, n, args, n_args, out);
     if (rc) {
         if (e) (void)drain(e);
@@ -2712,6 +2835,10 @@ int sg_sync(sg_engine* e) {
 }
 
 int sg_submit(sg_engine* e, const sg_event* ev, uint64_t n, uint32_t* out) {
+    if (e && e->tiny_on && n && n <= tiny_max() && !e->radix_group) {
+        const int trc = tiny_impl(e, ev, nullptr, n, nullptr, 0, out);
+        if (trc != TINY_FALLBACK) return trc;
+    }
     int rc = sg_submit_async(e, ev, n, out);
     if (rc) {
         if (e) (void)drain(e);
@@ -2914,8 +3041,15 @@ int sg_cluster_request_tokens(sg_engine* e, const sg_token_req* reqs, uint64_t n
             std::swap(kin, kout);
             std::swap(vin, vout);
         }
+        if (nflows + 1 > e->tbounds_cap) {
+            dfree(e->d_tbounds);
+            e->tbounds_cap = std::max<uint32_t>(nflows + 1, 1u << 12);
+            HIPCHK(hipMalloc(&e->d_tbounds, (uint64_t)e->tbounds_cap * 4));
+        }
+        // (the decide streams are idle: every batch was drained above)
         HIPCHK(launch_tok_flow(kin, vin, n, e->d_treq, e->d_cflow, nflows, e->d_cbkt, e->cfg.cluster_exceed_count,
-                               e->cfg.cluster_max_occupy_ratio, e->d_tres, st));
+                               e->cfg.cluster_max_occupy_ratio, e->d_tres, e->d_tbounds, e->tok_light, e->tok_wide, st,
+                               e->bin_stream[0], e->fork, e->join[0]));
     }
     HIPCHK(hipMemcpyAsync(out, e->d_tres, n * sizeof(sg_token_result), hipMemcpyDefault, st));
     HIPCHK(hipStreamSynchronize(st));

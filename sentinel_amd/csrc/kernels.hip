@@ -633,12 +633,6 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
             key = q >> 10;
             const uint32_t kind = rv.w & 0xFFu, code = (rv.w >> 16) & 0xFFu;
             if (kind == SG_EV_ENTRY) v = rv.z & 0xFFFFu;
-            else if (code == RC_BATCH) {
-                unsigned long long* dst = reinterpret_cast<unsigned long long*>(
-                    kind == SG_EV_EXIT ? &link[rv.y].exit_l : &link[rv.y].trace_l);
-                const unsigned long long old = atomicExch(dst, ((unsigned long long)epoch << 32) | q);
-                if ((uint32_t)(old >> 32) == epoch) multi = true;
-            }
         }
         // segmented inclusive sum over runs of equal blocks; the last lane of each run adds it
         const uint32_t kp = __shfl_up(key, 1, 64), kn = __shfl_down(key, 1, 64);
@@ -655,6 +649,28 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         }
         if ((l == 63 || kn != key) && key != 0xFFFFFFFFu && x) atomicAdd(&bst[key], x);
     }
+    // the links: every exchange of the quarter issued before any old value is looked at
+    unsigned long long* xd[GR_ITEMS];
+    unsigned long long xv[GR_ITEMS];
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint32_t k = (uint32_t)it * GR_THREADS + t;
+        xd[it] = nullptr;
+        xv[it] = 0;
+        if (k < nh) {
+            const uint4 rv = srec[k];
+            const uint32_t kind = rv.w & 0xFFu, code = (rv.w >> 16) & 0xFFu;
+            if (kind != SG_EV_ENTRY && code == RC_BATCH) {
+                xd[it] = reinterpret_cast<unsigned long long*>(kind == SG_EV_EXIT ? &link[rv.y].exit_l
+                                                                                  : &link[rv.y].trace_l);
+                xv[it] = ((unsigned long long)epoch << 32) | spos[k];
+            }
+        }
+    }
+    static_assert(GR_ITEMS == 4, "four exchanges a lane");
+    auto xch = [&](int it) -> uint32_t { return xd[it] ? (uint32_t)(atomicExch(xd[it], xv[it]) >> 32) : 0u; };
+    const uint32_t o0 = xch(0), o1 = xch(1), o2 = xch(2), o3 = xch(3);
+    if (o0 == epoch || o1 == epoch || o2 == epoch || o3 == epoch) multi = true;  // (epochs start at 1)
     if (__ballot(multi) && l == 0) atomicOr(bflags, BF_MULTI_LINK);
 }
 

@@ -1536,78 +1536,7 @@ __global__ __launch_bounds__(NW * 64) void k_pq_list(SEv* __restrict__ recs, con
     }
 }
 
-// ---- elastic map regions (dev_types.h PM_MIN_NB)
-// Move map id to a region of nn buckets at nbase (fresh pool buckets: every key PK_EMPTY): its live keys, with their
-// stamps and values, by two-choice cuckoo placement (every key of the new table is live: a slot is free iff empty).
-__device__ void pm_move(const DevState& S, uint32_t id, PMap m, uint64_t nbase, uint32_t nn, uint32_t* bflags) {
-    const PBucket* OB = S.pbkt + m.base;
-    const PData* OD = S.pdat + m.base * PM_BKT;
-    PBucket* NB = S.pbkt + nbase;
-    PData* ND = S.pdat + nbase * PM_BKT;
-    const uint64_t* bm = S.pbm + m.bm;
-    for (uint32_t b = 0; b < m.nb; ++b) {
-        for (int j = 0; j < PM_BKT; ++j) {
-            uint64_t ck = OB[b].key[j];
-            int64_t cs = OB[b].stamp[j];
-            if (ck == PK_EMPTY || !pm_live(m, bm, cs)) continue;
-            PData cd = OD[b * PM_BKT + j];
-            uint32_t b1, b2;
-            pm_buckets(nn, ck, b1, b2);
-            uint32_t c = b1;
-            bool placed = false;
-            for (int step = 0; step < 512 && !placed; ++step) {
-                for (int q = 0; q < PM_BKT; ++q) {  // a free slot in either candidate (the first step) or in c
-                    if (NB[c].key[q] == PK_EMPTY) { NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd; placed = true; break; }
-                }
-                if (placed) break;
-                if (step == 0) {
-                    for (int q = 0; q < PM_BKT; ++q) {
-                        if (NB[b2].key[q] == PK_EMPTY) { NB[b2].key[q] = ck; NB[b2].stamp[q] = cs; ND[b2 * PM_BKT + q] = cd; placed = true; break; }
-                    }
-                    if (placed) break;
-                }
-                const int q = (int)((cs + step * 5) & 7);  // displace one key of c to its other bucket
-                const uint64_t nk = NB[c].key[q];
-                const int64_t ns = NB[c].stamp[q];
-                const PData nd = ND[c * PM_BKT + q];
-                NB[c].key[q] = ck; NB[c].stamp[q] = cs; ND[c * PM_BKT + q] = cd;
-                ck = nk; cs = ns; cd = nd;
-                c = pm_alt(nn, ck, c);
-            }
-            if (!placed) atomicOr(bflags, BF_PTAB_FULL);  // (cannot happen at <= 50 % load)
-        }
-    }
-    PMap* h = &S.pmap[id];
-    h->base = nbase;
-    h->nb = nn;
-}
-// the map before up to `adds` more keys arrive: at most half its slots used, else a region twice as large (or
-// large enough), up to map_buckets(cap)
-// mv (k_pm_grow): the move is listed for k_pm_move_list (a workgroup per map) instead of done by this lane
-// pool_next = the pool's control words (PC_*).  rescue != 0: a region the pool cannot hold yet is a request for the
-// batch's on-device compaction (PC_RESCUE = rescue, the map keeps its region for now); 0: the pool is used up
-__device__ void pm_grow(const DevState& S, uint32_t id, uint64_t adds, unsigned long long* pool_next, uint64_t pool_nb,
-                        uint32_t* bflags, uint4* mv = nullptr, uint32_t* nmv = nullptr, uint32_t mcap = 0,
-                        uint32_t rescue = 0) {
-    const PMap m = S.pmap[id];
-    uint64_t need = (uint64_t)m.live + adds;
-    if (need > m.cap) need = m.cap;
-    const uint32_t want = map_buckets((uint32_t)need), full = map_buckets(m.cap);
-    if (want <= m.nb) return;
-    uint32_t nn = want > 2 * m.nb ? want : 2 * m.nb;
-    if (nn > full) nn = full;
-    const uint64_t nbase = atomicAdd(pool_next, (unsigned long long)nn);
-    if (nbase + nn > pool_nb) {
-        if (rescue) pool_next[PC_RESCUE] = rescue;
-        else atomicOr(bflags, BF_POOL_FULL);
-        return;
-    }
-    if (mv) {
-        const uint32_t k = atomicAdd(nmv, 1u);
-        if (k < mcap) { mv[k] = make_uint4(id, (uint32_t)nbase, (uint32_t)(nbase >> 32), nn); return; }
-    }
-    pm_move(S, id, m, nbase, nn, bflags);
-}
+// ---- elastic map regions (dev_types.h PM_MIN_NB): pm_move / pm_grow live in pmap.h (k_tiny grows maps too)
 // the listed moves, a wavefront per map: every live key of the old region into the new one (PK_EMPTY-filled pool),
 // claimed by compare-and-swap in either of its buckets; the rare key finding both full is placed afterwards by one
 // lane with pm_move's displacement walk.  The map's order lives in its stamps and ring, not in the slots, so the

@@ -103,8 +103,12 @@ def _random_requests(rng, n, fids, t0, bad_frac=0.02):
     return out
 
 
-@pytest.mark.parametrize("allowed", [-1, 400])
-def test_random_parity(allowed):
+@pytest.mark.parametrize("allowed,light", [(-1, None), (400, None), (-1, "0"), (400, "1000000")])
+def test_random_parity(allowed, light, monkeypatch):
+    # light: SG_TOK_LIGHT (cluster.hip: flows of more requests a call on a 1024-lane workgroup, the rest on one wave);
+    # "0" every flow on the wide one, "1000000" every flow on one wave
+    if light is not None:
+        monkeypatch.setenv("SG_TOK_LIGHT", light)
     rng = np.random.default_rng(20240601 + 5)
     eng, orc = _pair(cluster_max_allowed_qps=allowed)
     fids = list(range(101, 141))
