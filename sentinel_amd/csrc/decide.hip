@@ -688,6 +688,10 @@ struct PmLane {
     uint32_t mid, tid;  // the rule's map / the thread-count map of paramIdx 0 (NO_ID: not held)
     PMap mp, tm;
 };
+struct PmLaneRef {      // (k_lite<true>: the headers in LDS)
+    uint32_t mid, tid;
+    PMap &mp, &tm;
+};
 // param_check's passDefaultLocalCheck on the held rule map
 __device__ __forceinline__ bool param_default_lane(const DevState& S, const DRule& r, PMap& m, int acquire, uint64_t v,
                                                    int64_t t, uint32_t* bflags) {
@@ -1313,8 +1317,12 @@ __device__ __forceinline__ void lm_roll(LiteMin& L, Node& N, Bkt* minb, int64_t 
 // first (ParamFlowSlot.java:77-101, ParamFlowChecker.passDefaultLocalCheck), its map and the thread-count map of
 // paramIdx 0 held by the lane (PmLane), ParamFlowStatisticEntryCallback / ExitCallback on them
 // (ParameterMetric.java:117-241); args[0]'s key from the key ring (k_rs_first).
+#ifndef LITE_PL_WAVES
+#define LITE_PL_WAVES 1  // k_lite<true>'s occupancy target (1: 256 VGPRs + 36 AGPRs, no spill; 2: 41 VGPRs spilled,
+                         // C6 0.88 vs 0.92 G entries/s, profiles/r06)
+#endif
 template <bool PL>
-__global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? LITE_PL_WAVES : 2))) void k_lite(const SEv* __restrict__ recs, const sg_event* __restrict__ ev,
                                               const uint32_t* __restrict__ vals, const Seg* __restrict__ segs,
                                               const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                               int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
@@ -1326,9 +1334,12 @@ __global__ __launch_bounds__(256) void k_lite(const SEv* __restrict__ recs, cons
     if (((pg.xf & XF_PLITE) != 0) != PL) return;
     const int nf = pg.n_flow, nd = pg.n_degrade;  // <= 2 each (PF_J16)
     const DRule* rules = S.rules + pg.rule_off + (PL ? 1 : 0);  // (flow stages, then breakers)
-    PmLane PLM;
-    PLM.mid = PLM.tid = NO_ID;
-    DRule pr;
+    // PL: the param rule and the two held map headers live in LDS, one slot a lane (60 KB a workgroup), not in
+    // registers (256 VGPRs + 68 AGPRs -> + 36).  Two waves a SIMD still spill (LITE_PL_WAVES).
+    __shared__ DRule spr[PL ? 256 : 1];
+    __shared__ PMap smp[PL ? 256 : 1], stm[PL ? 256 : 1];
+    DRule& pr = spr[PL ? threadIdx.x : 0];
+    PmLaneRef PLM{NO_ID, NO_ID, smp[PL ? threadIdx.x : 0], stm[PL ? threadIdx.x : 0]};
     if (PL) {
         pr = S.rules[pg.rule_off];
         PLM.mid = pr.pmap;

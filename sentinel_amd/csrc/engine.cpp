@@ -604,8 +604,10 @@ struct sg_engine {
     uint32_t* d_hot_part = nullptr;  // the hot scan's per-chunk partials ((max tiles / 64 + 2) x HOT_MAX words)
     uint32_t* d_hot_hb = nullptr;    // per hot id: first sorted position, total (2 x HOT_MAX words)
     bool radix_group = false;    // SG_DEBUG_FLAGS & 8192: the all-radix group stage (A/B)
+    uint64_t radix_below = 1u << 18;  // SG_RADIX_BELOW: batches of fewer events take the radix group stage (the drop-in's
+                                      // 65,536-event batches: 36 vs 30-32 M entries/s on the hot / cold one)
     uint32_t tok_light = 8192;   // SG_TOK_LIGHT: token flows of at most this many requests a call on one-wave workgroups
-    uint32_t tok_wide = 512;     // SG_TOK_WIDE: 512 or 1024 lanes for the other token flows
+    uint32_t tok_wide = 1024;    // SG_TOK_WIDE: 1024 or 512 lanes for the other token flows (1024: 7.3 vs 8.0 ms a call)
     bool tiny_on = true;         // SG_TINY=0: synchronous batches of <= 256 events through the batched path too
     // sg_submit_ex: host-side ext / args are staged here (per batch slot, below); origin / context nodes
     AuxNode* d_auxtab = nullptr;
@@ -771,7 +773,9 @@ int ensure_batch(sg_engine* e, uint64_t n) {
         HIPCHK(hipMalloc(&B.d_posof, c * 4));
         HIPCHK(hipMalloc(&B.d_dec, c * 4));
         HIPCHK(hipMalloc(&B.d_recs, c * sizeof(SEv)));
-        if (e->radix_group || c >= (1ull << 30)) HIPCHK(hipMalloc(&B.d_rec_o, c * sizeof(SEv)));  // (radix stage only)
+        // (radix stage only: every batch, or those below radix_below)
+        const uint64_t co = (e->radix_group || c >= (1ull << 30)) ? c : std::min<uint64_t>(c, e->radix_below);
+        if (co) HIPCHK(hipMalloc(&B.d_rec_o, co * sizeof(SEv)));
         HIPCHK(hipMalloc(&B.d_ccnt, 3 * (nblocks + 64) * 4));
     }
     dfree(e->d_hot_part);
@@ -1301,7 +1305,8 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_TINY")) e->tiny_on = v[0] != '0';
-    if (const char* v = std::getenv("SG_TOK_WIDE")) e->tok_wide = std::atoi(v) == 1024 ? 1024u : 512u;
+    if (const char* v = std::getenv("SG_RADIX_BELOW")) e->radix_below = std::strtoull(v, nullptr, 0);
+    if (const char* v = std::getenv("SG_TOK_WIDE")) e->tok_wide = std::atoi(v) == 512 ? 512u : 1024u;
     if (const char* v = std::getenv("SG_TOK_LIGHT")) e->tok_light = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J1_STREAM")) e->j1_stream = std::atoi(v);
     if (const char* v = std::getenv("SG_PQ")) e->pq_on = v[0] != '0';
@@ -2292,7 +2297,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     if (++e->epoch == 0) e->epoch = 1;
     // every event through the radix passes: SG_DEBUG_FLAGS & 8192 (A/B of the group stage), or a batch of 2^30 events
     // or more (the hot / cold stage's words hold a position in 30 bits)
-    B.radix = e->radix_group || n >= (1ull << 30);
+    B.radix = e->radix_group || n >= (1ull << 30) || n < e->radix_below;
     if (B.radix) {
         HIPCHK(launch_rs_first(dev_ev, n, R, e->gbase, e->d_ring, ring_mask, e->cfg.statistic_max_rt, e->d_rec_o,
                                e->d_k1, e->d_v1, e->d_hist, nblocks, e->d_bsmall + 0, d_t0, e->d_prio, e->d_keyring,

@@ -80,6 +80,7 @@ def _trace(plan, seed=11):
 
 @pytest.mark.parametrize("mode", ["default", "skip"])
 def test_hot_cold_flips_cap_and_absent_ids(mode, monkeypatch):
+    monkeypatch.setenv("SG_RADIX_BELOW", "0")  # (every batch on the hot / cold stage, whatever its size)
     if mode == "skip":
         monkeypatch.setenv("SG_SKIP_MIN", "16")
     ev, cuts = _trace(_plan())

@@ -189,7 +189,13 @@ def test_chain_cap_reference_default():
     _run(2, batches=2, chain_cap=6000, n_entries=300_000)
 
 
-def test_many_small_batches_and_single_events(bin_mode):
+@pytest.mark.parametrize("path", ["default", "hot_cold"])
+def test_many_small_batches_and_single_events(bin_mode, path, monkeypatch):
+    # default: <= 256 events the one-workgroup k_tiny, larger the radix group stage (below SG_RADIX_BELOW);
+    # hot_cold: every batch through the batched pipeline's hot / cold group stage (k_cold_small for one tile)
+    if path == "hot_cold":
+        monkeypatch.setenv("SG_TINY", "0")
+        monkeypatch.setenv("SG_RADIX_BELOW", "0")
     w = T.Workload(4, n_entries=20_000, n_res=2_000)
     eng = _engine(max_resources=w.n_res, max_slot_chain_size=0)
     orc = O.Oracle(max_slot_chain_size=0)
