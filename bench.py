@@ -589,6 +589,38 @@ def config_cpu_baseline(w, ev, n_events):
                       "by splitmix64(res_id) %% %d (routing excluded)" % (len(sample), n_ent, T, T)}
 
 
+def ext_cpu_baseline(w, ev, ext, n_events):
+    """config_cpu_baseline through or_submit_ex: the same contexts / origins on every event (the oracle keeps each
+    entry's origin StatisticNode and context DefaultNode, as the device does)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    T = cpu_share()
+    sample = ev[:min(len(ev), n_events)]
+    po = O.PartitionedOracle(w, T, max_slot_chain_size=0)
+    for o in po.orcs:
+        w.intern_names(o)
+    spent = []
+    po.submit_ex(sample, ext[:len(sample)], timed=spent)
+    po.close()
+    n_ent = int((sample["kind"] == 0).sum())
+    return {"value": n_ent / spent[0], "unit": "entries/s", "cores": T, "kind": "port",
+            "sample": "first %d events (%d entries) of the line's trace with its contexts / origins, "
+                      "oracle/liboracle.so or_submit_ex, %d threads partitioned by splitmix64(res_id) %% %d "
+                      "(routing excluded)" % (len(sample), n_ent, T, T)}
+
+
+def _oracle_for(w, ev, eng_names=True):
+    """One oracle (one thread: a lone caller's view) holding the resources ev touches, names interned as the
+    engine's (w.intern_names)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    orc = O.Oracle(max_slot_chain_size=0)
+    w.install(orc, np.unique(ev["res_id"]))
+    if eng_names:
+        w.intern_names(orc)
+    return orc
+
+
 def config_lines(dev, c4=None, cpu_events=4_000_000, only=None):
     """The SURVEY.md configs besides the headline: C2, C3, C5, C6 (mixed rules); with c4 = (workload, events) of the headline trace,
     C4 and C4-ext on its first 3 global batches (the same events through sg_submit and sg_submit_ex), C5-ext, and
@@ -614,6 +646,8 @@ def config_lines(dev, c4=None, cpu_events=4_000_000, only=None):
                                 "headline trace" % ("-ext" if ext_on else ""), "resources": w.n_res})
             if ext_on:
                 r["note"] = EXT_NOTE
+                if cpu_events:
+                    r["cpu_baseline"] = ext_cpu_baseline(w, sub, ext, cpu_events)
             rows.append(r)
             eng.close()
             torch.cuda.empty_cache()
@@ -650,13 +684,13 @@ def config_lines(dev, c4=None, cpu_events=4_000_000, only=None):
     if only:  # (tools/pmc_configs.py: one config's batches under rocprofv3)
         return rows
     if c4 is not None:
-        rows.append(dropin_line(dev, *c4))
-        rows.append(latency_line(dev, *c4))
+        rows.append(dropin_line(dev, *c4, cpu=bool(cpu_events)))
+        rows.append(latency_line(dev, *c4, cpu=bool(cpu_events)))
     rows.append(token_line(dev))
     return rows
 
 
-def latency_line(dev, w, ev, sizes=(1, 64, 256, 1024), calls=2000, warm=200):
+def latency_line(dev, w, ev, sizes=(1, 64, 256, 1024), calls=2000, warm=200, cpu=False):
     """The drop-in under light load: every SphU.entry is synchronous (core/CtSph.java:117-168), so a
     lightly loaded service pays one engine call per few events.  Synchronous sg_submit_ex of 1, 64, 256 and 1,024 events
     of the C4 trace from pageable host memory (contexts and origins on every event, as the Java batcher sends them):
@@ -671,17 +705,20 @@ def latency_line(dev, w, ev, sizes=(1, 64, 256, 1024), calls=2000, warm=200):
     out = {}
     off = 0
     total = sum(n * (calls + warm) for n in sizes)  # one prefix of the trace, in order (the engine's event indices)
-    ext_all = T.ext_for(np.ascontiguousarray(ev[:total]), io, ic, seed=T.SEED_BASE + 47)
+    prefix = np.ascontiguousarray(ev[:total])
+    ext_all = T.ext_for(prefix, io, ic, seed=T.SEED_BASE + 47)
+    got = np.zeros(total, np.uint32)
     for n in sizes:
         need = n * (calls + warm)
-        sub = np.ascontiguousarray(ev[off:off + need])
+        sub = prefix[off:off + need]
         ext = ext_all[off:off + need]
         lat = []
         for b in range(calls + warm):
             e, x = sub[b * n:(b + 1) * n], ext[b * n:(b + 1) * n]
             t = time.perf_counter()
-            eng.submit_ex(e, x)
+            d = eng.submit_ex(e, x)
             dt = time.perf_counter() - t
+            got[off + b * n:off + (b + 1) * n] = d
             if b >= warm:
                 lat.append(dt)
         lat = np.array(lat) * 1e3
@@ -690,10 +727,31 @@ def latency_line(dev, w, ev, sizes=(1, 64, 256, 1024), calls=2000, warm=200):
         off += need
     eng.close()
     torch.cuda.empty_cache()
-    return {"config": "drop-in latency floor: synchronous sg_submit_ex of %s C4 events from pageable host memory, "
-                      "contexts + origins" % " / ".join(str(n) for n in sizes), "unit": "ms per call", "latency": out,
-            "note": "<= 256 events: the events in, one k_tiny launch (every stage in one workgroup), the decisions back; "
-                    "larger: the group stage, one host round trip for the bins, the decide stage, the decisions back"}
+    r = {"config": "drop-in latency floor: synchronous sg_submit_ex of %s C4 events from pageable host memory, "
+                   "contexts + origins" % " / ".join(str(n) for n in sizes), "unit": "ms per call", "latency": out,
+         "note": "<= 256 events: the events in, one k_tiny launch (every stage in one workgroup), the decisions back; "
+                 "larger: the group stage, one host round trip for the bins, the decide stage, the decisions back"}
+    if cpu:  # the same calls through the oracle, one thread (ctypes call overhead included)
+        orc = _oracle_for(w, prefix)
+        cl, off, want = {}, 0, np.zeros(total, np.uint32)
+        for n in sizes:
+            lat = []
+            for b in range(calls + warm):
+                a = off + b * n
+                t = time.perf_counter()
+                want[a:a + n] = orc.submit_ex(prefix[a:a + n], ext_all[a:a + n])
+                dt = time.perf_counter() - t
+                if b >= warm:
+                    lat.append(dt)
+            lat = np.array(lat) * 1e3
+            cl[str(n)] = {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99))}
+            off += n * (calls + warm)
+        orc.close()
+        r["cpu_baseline"] = {"latency": cl, "unit": "ms per call", "cores": 1, "kind": "port",
+                             "sample": "the same %d calls, oracle/liboracle.so or_submit_ex, one thread" % (
+                                 len(sizes) * (calls + warm)),
+                             "gpu_results_equal": bool(np.array_equal(got, want))}
+    return r
 
 
 def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60, cpu_requests=2_000_000):
@@ -765,7 +823,7 @@ def token_line(dev, n_flows=10_000, n_req=16_000_000, batch=1 << 21, seconds=60,
             "cpu_baseline": cpu}
 
 
-def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400):
+def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400, cpu=False, cpu_batches=20):
     """The Java batcher's operating point (java/.../GpuEngine.java): batches of <= 65,536 events
     from pageable host memory, sg_submit_ex synchronous (one batch decided and back before the next), contexts and
     origins on every event.  Entries/s and the per-batch latency distribution (host wall clock around each call)."""
@@ -780,23 +838,43 @@ def dropin_line(dev, w, ev, batch=1 << 16, n_batches=400):
     ext = T.ext_for(sub, io, ic, seed=T.SEED_BASE + 46)
     lat = []
     ent = 0
+    nc = 20 + cpu_batches
+    got = []
     for b in range(n_batches + 20):
         e = sub[b * batch:(b + 1) * batch]
         t = time.perf_counter()
-        eng.submit_ex(e, ext[b * batch:(b + 1) * batch])
+        d = eng.submit_ex(e, ext[b * batch:(b + 1) * batch])
         dt = time.perf_counter() - t
+        if b < nc:
+            got.append(d)
         if b >= 20:  # warm-up batches untimed
             lat.append(dt)
             ent += int((e["kind"] == 0).sum())
     lat = np.array(lat)
     eng.close()
     torch.cuda.empty_cache()
-    return {"config": "drop-in operating point: C4 trace, %d-event batches from pageable host memory, sg_submit_ex "
-                      "synchronous" % batch, "value": ent / lat.sum(), "unit": "entries/s", "batches_timed": n_batches,
-            "batch_events": batch, "latency_ms": {"p50": float(np.percentile(lat, 50) * 1e3),
-                                                  "p99": float(np.percentile(lat, 99) * 1e3),
-                                                  "mean": float(lat.mean() * 1e3)},
-            "note": EXT_NOTE + "; PCIe copies of events, ext and decisions inside every call"}
+    r = {"config": "drop-in operating point: C4 trace, %d-event batches from pageable host memory, sg_submit_ex "
+                   "synchronous" % batch, "value": ent / lat.sum(), "unit": "entries/s", "batches_timed": n_batches,
+         "batch_events": batch, "latency_ms": {"p50": float(np.percentile(lat, 50) * 1e3),
+                                               "p99": float(np.percentile(lat, 99) * 1e3),
+                                               "mean": float(lat.mean() * 1e3)},
+         "note": EXT_NOTE + "; PCIe copies of events, ext and decisions inside every call"}
+    if cpu:  # the oracle, one thread, on the same first batches (the last cpu_batches of them timed)
+        orc = _oracle_for(w, sub[:nc * batch])
+        spent, cent, want = 0.0, 0, []
+        for b in range(nc):
+            e = sub[b * batch:(b + 1) * batch]
+            t = time.perf_counter()
+            want.append(orc.submit_ex(e, ext[b * batch:(b + 1) * batch]))
+            if b >= 20:
+                spent += time.perf_counter() - t
+                cent += int((e["kind"] == 0).sum())
+        orc.close()
+        r["cpu_baseline"] = {"value": cent / spent, "unit": "entries/s", "cores": 1, "kind": "port",
+                             "sample": "batches 20-%d of the same calls, oracle/liboracle.so or_submit_ex, one thread"
+                                       % (nc - 1),
+                             "gpu_results_equal": bool(np.array_equal(np.concatenate(got), np.concatenate(want)))}
+    return r
 
 
 def cpu_share() -> int:

@@ -323,12 +323,16 @@ class PartitionedOracle:
         self.n_events += len(events)
         return out
 
-    def submit_ex(self, events: np.ndarray, ext: np.ndarray) -> np.ndarray:
+    def submit_ex(self, events: np.ndarray, ext: np.ndarray, timed: list = None) -> np.ndarray:
         """sg_submit_ex without an args table (contexts and origins only): each shard gets its events' ext rows."""
+        import time
         ev = np.ascontiguousarray(events, dtype=A.EVENT_DTYPE)
         parts, pos = self.router.route(ev)
         exs = [np.ascontiguousarray(ext[p]) for p in pos]
+        t = time.perf_counter()
         outs = list(self.pool.map(lambda r: self.orcs[r].submit_ex(parts[r], exs[r]), range(self.T)))
+        if timed is not None:
+            timed.append(time.perf_counter() - t)
         out = np.zeros(len(events), dtype=np.uint32)
         for p, o in zip(pos, outs):
             out[p] = o

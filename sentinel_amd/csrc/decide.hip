@@ -1393,7 +1393,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? LITE_P
     uint64_t pm0 = 0, pm1 = 0, pm2 = 0, pm3 = 0;  // passed bits of positions 0..255
     // records in chunks of 4 with the next chunk in flight: one memory round trip per 4 events (the
     // loads are unconditional with a clamped index, so the compiler's vmcnt waits cannot serialise them)
-    constexpr uint32_t CH = 4;
+#ifndef LITE_CH
+#define LITE_CH 4
+#endif
+    constexpr uint32_t CH = LITE_CH;
     const uint4* r4 = reinterpret_cast<const uint4*>(recs + sg.start);
     const uint32_t qmax = sg.len ? sg.len - 1 : 0;
     uint4 cur[CH], nxt[CH];
@@ -1406,9 +1409,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? LITE_P
 #pragma unroll 1
     for (uint32_t k = 0; k < CH; ++k) {
         const uint4 rw = cur[0];
-        cur[0] = cur[1];
-        cur[1] = cur[2];
-        cur[2] = cur[3];
+#pragma unroll
+        for (uint32_t m = 0; m + 1 < CH; ++m) cur[m] = cur[m + 1];
         const uint32_t j = j0 + k;
         if (j >= sg.len) break;
         const int32_t rdt = (int32_t)rw.x;

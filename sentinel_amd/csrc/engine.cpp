@@ -2626,7 +2626,22 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     // J1: after the lane bins on the main stream, or (SG_J1_STREAM=1, and with the short aux nodes on the main stream)
     // after J16 / J8 on bin_stream[0]
     const bool j1_b0 = bin_n[BIN_J1] && !serial_bins && (e->j1_stream == 1 || (e->j1_stream < 0 && aux_early));
-    if (bin_n[BIN_J1]) {
+    // SG_J1_STREAM=2: the J1 segments halved, one half after J16 / J8 on bin_stream[0], the other after J4 on
+    // bin_stream[1] (A/B)
+    const bool j1_split = bin_n[BIN_J1] > 1 && !serial_bins && e->j1_stream == 2;
+    if (j1_split) {
+        const uint32_t h = bin_n[BIN_J1] / 2;
+        for (int c = 0; c < 2; ++c) {
+            DevState Sj = S;
+            Sj.dbg = nullptr;
+            hipStream_t bs = e->bin_stream[c];
+            const bool ran = c == 0 ? (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_PQ16]) : (bin_n[BIN_J4] || bin_n[BIN_PQ4]);
+            if (!ran) HIPCHK(hipStreamWaitEvent(bs, e->fork, 0));
+            HIPCHK(launch_decide_bin(BIN_J1, e->d_recs, dev_ev, vin, e->d_segs, e->d_order + off[BIN_J1] + (c ? h : 0),
+                                     c ? bin_n[BIN_J1] - h : h, Sj, dc, t0, e->d_dec, e->d_bsmall + 0, bs));
+            HIPCHK(hipEventRecord(e->join[c], bs));
+        }
+    } else if (bin_n[BIN_J1]) {
         DevState Sj = S;
         Sj.dbg = (e->prof_bin == 2 && e->d_dbg) ? e->d_dbg : nullptr;
         hipStream_t bs = j1_b0 ? e->bin_stream[0] : st;
@@ -2636,7 +2651,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
         if (j1_b0) HIPCHK(hipEventRecord(e->join[0], bs));
     }
     for (int c = 0; c < 2; ++c)
-        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4] || (c == 0 && (j8_own || j1_b0)))
+        if (bin_n[coop[c]] || bin_n[c == 0 ? BIN_PQ16 : BIN_PQ4] || (c == 0 && (j8_own || j1_b0)) || j1_split)
             HIPCHK(hipStreamWaitEvent(st, e->join[c], 0));
     // verdicts of the frozen spans the cooperative kernels skipped
     if (S.skip_ok && (bin_n[BIN_J16] || bin_n[BIN_J8] || bin_n[BIN_J4]))

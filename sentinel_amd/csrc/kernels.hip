@@ -453,11 +453,15 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
     sg_event e[GR_ITEMS];
     uint32_t wd[GR_ITEMS];
 #pragma unroll
-    for (int it = 0; it < GR_ITEMS; ++it) {
+    for (int it = 0; it < GR_ITEMS; ++it) {  // (clamped, unconditional loads: no wait between them)
         const uint64_t i = base + (uint64_t)it * GR_THREADS + t;
-        if (i < n) { e[it] = ev[i]; wd[it] = words[i]; }
-        else { e[it].kind = 0xFF; wd[it] = 0; }
+        const uint64_t ic = i < n ? i : n - 1;
+        e[it] = ev[ic];
+        wd[it] = words[ic];
     }
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it)
+        if (base + (uint64_t)it * GR_THREADS + t >= n) { e[it].kind = 0xFF; wd[it] = 0; }
     for (uint32_t h = t; h < nhot; h += GR_THREADS) {
         lo[h] = 0;
         r0[h] = 0xFFFFFFFFu;
@@ -516,16 +520,25 @@ __global__ __launch_bounds__(GR_THREADS) void k_grp_records(const sg_event* __re
         if (!(wd[it] & W_HOT)) p[it] = wd[it] & W_POS;
         if (e[it].kind != SG_EV_ENTRY) {
             const uint64_t ref = e[it].aux & SG_REF_NONE;
-            if (ref != SG_REF_NONE && ref >= gbase && ref - gbase < i) {  // (k_grp_first flagged the others)
-                jj[it] = ref - gbase;
-                wj[it] = words[ref - gbase];
-            }
+            if (ref != SG_REF_NONE && ref >= gbase && ref - gbase < i) jj[it] = ref - gbase;  // (k_grp_first flagged the others)
         }
     }
-    // the referenced ENTRYs' positions
+    // the referenced ENTRYs' words, then the hot ones' run starts: clamped, unconditional loads, each kind issued
+    // together (a load under a per-lane condition gets its own wait)
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint32_t x = words[jj[it] == ~0ull ? 0ull : jj[it]];
+        wj[it] = jj[it] == ~0ull ? 0u : x;
+    }
     uint32_t pj[GR_ITEMS];
 #pragma unroll
-    for (int it = 0; it < GR_ITEMS; ++it) pj[it] = jj[it] == ~0ull ? 0u : grp_pos(jj[it], wj[it], P, nhot);
+    for (int it = 0; it < GR_ITEMS; ++it) {
+        const uint64_t j = jj[it] == ~0ull ? 0ull : jj[it];
+        pj[it] = P[(wj[it] & W_HOT) ? (j / RS_TILE) * nhot + ((wj[it] >> 12) & (HOT_MAX - 1)) : 0];
+    }
+#pragma unroll
+    for (int it = 0; it < GR_ITEMS; ++it)  // (= grp_pos)
+        pj[it] = jj[it] == ~0ull ? 0u : (wj[it] & W_HOT) ? pj[it] + (wj[it] & 0xFFFu) : (wj[it] & W_POS);
     // the records
     bool bad = false, zero = false;
 #pragma unroll
@@ -689,10 +702,19 @@ __global__ __launch_bounds__(256) void k_post_w(const uint32_t* __restrict__ wor
         const uint64_t i = base + (uint64_t)k * 256;
         w[k] = i < n ? words[i] : 0u;
     }
+    // (the hot rows' positions, then the decisions: clamped, unconditional loads, each kind issued together -- a
+    // load under a per-lane condition gets its own wait)
+    uint32_t pr[POSTW_ITEMS];
 #pragma unroll
     for (int k = 0; k < POSTW_ITEMS; ++k) {
         const uint64_t i = base + (uint64_t)k * 256;
-        d[k] = (w[k] & W_ENT) ? dec[grp_pos(i, w[k], P, nhot)] : (uint32_t)ST_NOT_ENTRY;  // (= mk_dec(ST_NOT_ENTRY, 0, 0))
+        pr[k] = P[(w[k] & W_HOT) ? (i / RS_TILE) * nhot + ((w[k] >> 12) & (HOT_MAX - 1)) : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < POSTW_ITEMS; ++k) {
+        const uint32_t q = (w[k] & W_HOT) ? pr[k] + (w[k] & 0xFFFu) : (w[k] & W_POS);
+        const uint32_t x = dec[(w[k] & W_ENT) ? q : 0u];
+        d[k] = (w[k] & W_ENT) ? x : (uint32_t)ST_NOT_ENTRY;  // (= mk_dec(ST_NOT_ENTRY, 0, 0))
     }
 #pragma unroll
     for (int k = 0; k < POSTW_ITEMS; ++k) {

@@ -200,8 +200,10 @@ def _check(eng, orc, ev, dg, do, n_res):
         np.testing.assert_array_equal(g["minute"], o["minute"], err_msg="minute window of res %d" % r)
 
 
-@pytest.mark.parametrize("intern_first", [True, False])
-def test_origin_context_args_parity(intern_first):
+@pytest.mark.parametrize("intern_first,group", [(True, "default"), (False, "default"), (True, "hot_cold")])
+def test_origin_context_args_parity(intern_first, group, monkeypatch):
+    if group == "hot_cold":  # (these batches are below SG_RADIX_BELOW: the hot / cold stage's argument checks too)
+        monkeypatch.setenv("SG_RADIX_BELOW", "0")
     n_res = 36
     eng, orc, io, ic, _ = _pair(n_res, intern_first)
     ev, ext, table = _trace(7, n_res, 12_000, io, ic)

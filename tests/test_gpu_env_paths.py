@@ -2,7 +2,9 @@
 engine (each runs in a child process; DESIGN.md §10 lists every switch):
 
   SG_PIPELINE=0            group and decide stages back to back (no overlap of batch k+1's grouping)
-  SG_J1_STREAM=1           the J1 owners after J16 / J8 on bin_stream[0] instead of after the lane bins
+  SG_J1_STREAM=1 / 2       the J1 owners after J16 / J8 on bin_stream[0] instead of after the lane bins / halved over
+                           both bin streams
+  SG_RADIX_BELOW=0         the hot / cold group stage for batches of every size
   SG_STREAM_PRIO=1 / 0     the decide streams at the higher priority / default stream priorities
   SG_DEBUG_FLAGS=8192      the all-radix group stage (k_rs_first / k_scatter_rec) instead of the hot / cold split
   SG_PQ=0                  hot-parameter resources on the per-lane kernel (no k_pq)
@@ -59,6 +61,7 @@ print("ok", len(ev))
                                      ("SG_DEBUG_FLAGS=4", 3), ("SG_DEBUG_FLAGS=8", 4), ("SG_DEBUG_FLAGS=16", 3),
                                      ("SG_DEBUG_FLAGS=128 SG_PQ_WIDE=512", 5),
                                      ("SG_DEBUG_FLAGS=288", 5), ("SG_J1_STREAM=1", 4), ("SG_J1_STREAM=1", 3),
+                                     ("SG_J1_STREAM=2", 4), ("SG_J1_STREAM=2", 3), ("SG_RADIX_BELOW=0", 6),
                                      ("SG_PIPELINE=0", 6), ("SG_STREAM_PRIO=0", 6)])
 def test_alternative_path_parity(env, cfg):
     child_env = dict(os.environ)
