@@ -1875,6 +1875,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
     if (CLS != 0 && (((pg.pflags & PF_FROZEN) != 0) != (CLS == 1))) return;  // the other instantiation's segment
+    if ((NW == 16 || NW == 4) && (pg.xf & (XF_HEADT | XF_HEADR)) && !(cfg.dbg_flags & HEAD_OFF)) return;  // k_head's
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
     // the minute window in LDS (sh.minl): loaded here, written back at the segment's end; no other kernel of the
     // decide stage touches this resource's minute buckets while its owner runs
@@ -4075,10 +4076,18 @@ hipError_t launch_tiny(const sg_event* ev, uint32_t n, const DevState& S, const 
     return hipGetLastError();
 }
 uint32_t tiny_max() { return TINY_MAX; }
+hipError_t launch_head(const SEv* recs, const Seg* segs, const uint32_t* order, uint32_t m, const DevState& S,
+                       const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st);
 hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const uint32_t* vals, const Seg* segs,
                              const uint32_t* order, uint32_t m, const DevState& S, const DevCfg& cfg, int64_t t0,
                              uint32_t* dec, uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
+    // single-rule THREAD-grade / RateLimiter heads (XF_HEADT / XF_HEADR): the event-driven owner, before the
+    // cooperative one (which leaves those segments)
+    if ((bin == BIN_J16 || bin == BIN_J4) && !(cfg.dbg_flags & HEAD_OFF)) {
+        const hipError_t he = launch_head(recs, segs, order, m, S, cfg, t0, dec, bflags, st);
+        if (he != hipSuccess) return he;
+    }
     switch (bin) {
     case BIN_J16:  // programs of the J16 shape only (PF_J16): <= 2 flow, <= 2 degrade stages, no rate limiter;
                    // a 128 KiB status window (one workgroup per CU) keeps EXIT references in LDS

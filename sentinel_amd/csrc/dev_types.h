@@ -108,8 +108,11 @@ enum : uint16_t {
                          // blocks), the Jacobi owner the flow / degrade chain with those verdicts as inputs, and
                          // k_pq's post pass the thread-count map from the final verdicts
     XF_PLITE = 4,        // XF_MIX with exactly one (checked) param rule: its short segments take k_lite<true>
-    XF_PVPQ = 8          // PF_PQ with one QPS rule (DefaultController or throttle) on paramIdx 0: its long segments'
+    XF_PVPQ = 8,         // PF_PQ with one QPS rule (DefaultController or throttle) on paramIdx 0: its long segments'
                          // checks by pvalue.hip's passes, k_pq then folding the statistics only (SG_PV_PQ)
+    XF_HEADT = 16,       // the only rule is one THREAD-grade DefaultController flow rule on the ClusterNode (DIRECT,
+                         // limitApp default): its J16 / J4 segments take the event-driven head owner (head.hip)
+    XF_HEADR = 32        // ... one QPS RateLimiter flow rule likewise
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)
@@ -226,6 +229,7 @@ static_assert(sizeof(PMap) == 64, "PMap must be 64 B");
 enum : uint8_t { ST_PASS = 0, ST_PASS_WAIT = 1, ST_BLOCK_FLOW = 2, ST_BLOCK_DEGRADE = 3, ST_BLOCK_PARAM = 4,
                  ST_NO_CHECK = 5, ST_BLOCK_UPSTREAM = 6, ST_NOT_ENTRY = 0xFF };
 
+#define HEAD_OFF 16384u  // DevCfg.dbg_flags: the cooperative owner decides XF_HEADT / XF_HEADR heads too (A/B)
 struct DevCfg {
     int32_t max_rt;
     int32_t occupy_timeout;

@@ -1072,6 +1072,15 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 any_mix = true;
             }
             if (p.n_flow <= 2 && p.n_degrade <= 2 && n_rl == 0) p.pflags |= PF_J16;
+            // one flow rule and nothing else on the ClusterNode: a THREAD-grade DefaultController or a QPS
+            // RateLimiter head is decided by the event-driven head owner (head.hip k_head)
+            if (p.n_param == 0 && p.n_flow == 1 && p.n_degrade == 0 && !p.multi && !(p.pflags & PF_SERIAL)) {
+                const DRule& d = rules[p.rule_off];
+                if (d.strategy == SG_STRATEGY_DIRECT && d.la_kind == LA_DEFAULT) {
+                    if (d.grade == SG_FLOW_GRADE_THREAD && d.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) p.xf |= XF_HEADT;
+                    else if (d.grade == SG_FLOW_GRADE_QPS && d.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) p.xf |= XF_HEADR;
+                }
+            }
         }
         // carry controller / breaker state of kinds that were not reloaded
         if (!old_rst.empty()) {

@@ -1,0 +1,521 @@
+// head.hip -- event-driven owners of single-rule head segments (one wavefront per segment).
+//
+// A resource whose only rule is one flow rule on its ClusterNode (no degrade, no param rule, DIRECT, limitApp
+// default) of one of two kinds has a decision chain with a single piece of state:
+//   XF_HEADT  THREAD-grade DefaultController (core/slots/block/flow/controller/DefaultController.java:49-81): an ENTRY
+//             passes iff curThreadNum + acquire <= count; StatisticSlot adds 1 to curThreadNum per pass and takes 1
+//             off per effective EXIT (core/slots/statistic/StatisticSlot.java:54-173).  State: the thread count c.
+//   XF_HEADR  QPS RateLimiterController (core/slots/block/flow/controller/RateLimiterController.java:46-91): an ENTRY
+//             of acquire > 0 passes iff latestPassedTime + cost <= now or latestPassedTime + cost - now <= maxQueue,
+//             and then latestPassedTime = max(latestPassedTime + cost, now).  State: latestPassedTime L.
+// The cooperative owner (decide.hip k_jac) decides such a head by Jacobi iterations over 256- / 1024-lane tiles, whose
+// per-iteration chain of block-wide scans and barriers bounds it (C3: 14-17 ms a 2^24-event batch).  Here one wave
+// owns the segment and walks it in chunks of 1,024 positions (16 a lane, consecutive), each decided by
+// guess-and-verify rounds that need no barrier:
+//   THREAD  the passes P_i before position i follow P_{i+1} = min(P_i + [ENTRY], u_i), u_i = max(0, floor(count) -
+//           acquire - c + X_i + 1), X_i the effective EXITs before i -- an affine map of the (min, +) semiring, so one
+//           wave scan of (a, b) pairs gives every ENTRY's verdict once the EXITs' effectiveness is known.  An EXIT
+//           naming an ENTRY of the same chunk is effective iff that ENTRY passed: its guess is the ENTRY's verdict of
+//           the round before (the chunk's first round: the last verdict of the chunk before).
+//   RATE    with the passes guessed, L before every ENTRY is one wave scan of (max, +) maps x -> max(x + cost, t).
+//           Guesses: every ENTRY passes after a pass; after a block, the saturated lattice -- the first ENTRY at or
+//           after L + j * cost - maxQueue passes for j = 1, 2, ... (each pass moves L by exactly cost while arrivals
+//           are dense), so a saturated chunk is one round.
+// Each round then evaluates every ENTRY exactly at its guessed prefix state; the first event whose evaluation (or, for
+// an EXIT, whose ENTRY's verdict) differs from its guess ends the round: everything before it is exact, it takes its
+// evaluated outcome, and the next round starts after it.  Statistics follow once the chunk is decided: per 500 ms
+// bucket wave reductions folded into the node exactly as k_jac's round_fold folds a round.  EXIT references into
+// earlier chunks read a 2^18-position status ring in LDS (older ones the dec[] word).
+#include "chain.h"
+#include "dev_types.h"
+
+namespace sg {
+
+#define HD_EP 16u                 // events per lane of a chunk (one 16-bit status word a lane)
+#define HD_CH (64u * HD_EP)       // positions per chunk
+#define HD_RW 16384u              // status ring words (32 KiB of LDS): 2^18 positions
+#define HD_INF 0x3FFFFFFF
+#define HD_NONE 0xFFFFFFFFu
+#define HD_NEG (-(1ll << 62))
+
+// inclusive wave scans (DPP row shifts + row broadcasts, wave64)
+#define HD_DPP(old, v, ctrl, rmask) __builtin_amdgcn_update_dpp((int)(old), (int)(v), ctrl, rmask, 0xf, false)
+#define HD_SCAN_STEPS(STEP) \
+    STEP(0x111, 0xf) STEP(0x112, 0xf) STEP(0x114, 0xf) STEP(0x118, 0xf) STEP(0x142, 0xa) STEP(0x143, 0xc)
+
+__device__ __forceinline__ uint32_t hd_add_scan(uint32_t v) {
+#define S_(c, m) v += (uint32_t)HD_DPP(0, v, c, m);
+    HD_SCAN_STEPS(S_)
+#undef S_
+    return v;
+}
+__device__ __forceinline__ uint32_t hd_max_scan(uint32_t v) {  // identity 0
+#define S_(c, m) { const uint32_t o = (uint32_t)HD_DPP(0, v, c, m); v = o > v ? o : v; }
+    HD_SCAN_STEPS(S_)
+#undef S_
+    return v;
+}
+__device__ __forceinline__ uint32_t hd_min_red(uint32_t v) {  // wave minimum, uniform
+#define S_(c, m) { const uint32_t o = (uint32_t)HD_DPP(0xFFFFFFFFu, v, c, m); v = o < v ? o : v; }
+    HD_SCAN_STEPS(S_)
+#undef S_
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t hd_sum_red(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)hd_add_scan(v), 63); }
+__device__ __forceinline__ uint64_t hd_sum_red64(uint64_t v) {  // in 32 + 16 + 16-bit pieces (no carry lost)
+    return ((uint64_t)hd_sum_red((uint32_t)(v >> 32)) << 32) + ((uint64_t)hd_sum_red((uint32_t)v >> 16) << 16) +
+           (uint64_t)hd_sum_red((uint32_t)v & 0xFFFFu);
+}
+// (min, +) maps x -> min(x + a, b), composed in position order: inclusive scan
+__device__ __forceinline__ void hd_minplus_scan(int32_t& a, int32_t& b) {
+#define S_(c, m) { const int32_t pa = HD_DPP(0, a, c, m), pb = HD_DPP(HD_INF, b, c, m); \
+                   const int32_t nb = pb + a; b = nb < b ? nb : b; a = pa + a; }
+    HD_SCAN_STEPS(S_)
+#undef S_
+}
+// (max, +) maps x -> max(x + a, b) on int64: inclusive scan
+__device__ __forceinline__ void hd_maxplus_scan(int64_t& a, int64_t& b) {
+#define D64(old, v, c, m) ((int64_t)(((uint64_t)(uint32_t)HD_DPP((uint32_t)((uint64_t)(old) >> 32), (uint32_t)((uint64_t)(v) >> 32), c, m) << 32) | \
+                                    (uint64_t)(uint32_t)HD_DPP((uint32_t)(uint64_t)(old), (uint32_t)(uint64_t)(v), c, m)))
+#define S_(c, m) { const int64_t pa = D64(0, a, c, m), pb = D64(HD_NEG, b, c, m); \
+                   const int64_t nb = pb + a; b = nb > b ? nb : b; a = pa + a; }
+    HD_SCAN_STEPS(S_)
+#undef S_
+#undef D64
+}
+
+enum : uint32_t { HK_ENT = 1u, HK_EXIT = 2u, HK_TRACE = 3u, HK_KIND = 3u, HK_EFF = 4u /* effective, known */,
+                  HK_DYN = 8u /* effective iff the ENTRY at ref (same chunk) passed */ };
+
+__device__ __forceinline__ uint32_t hd_bit(const uint16_t* win, uint32_t p) { return (win[(p >> 4) & (HD_RW - 1)] >> (p & 15)) & 1u; }
+
+// RL: the ENTRY's cost (RateLimiterController.java:53: Math.round(1.0 * acquireCount / count * 1000))
+__device__ __attribute__((noinline)) int64_t hd_cost(double count, uint32_t cnt, int64_t cost1) {
+    if (cnt == 1) return cost1;
+    if (cnt == 0 || count <= 0) return 0;
+    return j_round(1.0 * (double)cnt / count * 1000);
+}
+
+// leader: k_jac round_fold of one collected 500 ms bucket (out of line: rare, and its 64-bit node arithmetic would
+// otherwise take the round loop's scalar registers)
+__device__ __attribute__((noinline)) void hd_fold(Node& node, Ctx C, int64_t cb, uint64_t aP, uint64_t aB, uint64_t aS,
+                                                  uint64_t aRT, uint64_t aE, uint32_t aMin) {
+    const int64_t tc = cb * 500;
+    const int sl = sec_current(node, tc, C.max_rt);
+    const int64_t mrt = aMin == HD_NONE ? INT64_MAX : (int64_t)aMin;
+    sec_add(node, sl, (int64_t)aP, (int64_t)aB, (int64_t)aS, (int64_t)aRT, (int64_t)aE, mrt);
+    min_current(node, C.minb, tc, C.max_rt, C.pflags);
+    if (!(node.mst & MS_DETACHED)) {
+        min_add(node, (int64_t)aP, (int64_t)aB, (int64_t)aS, (int64_t)aRT, (int64_t)aE, mrt);
+        if (node.exc_sum_sec == tc - tc % 1000) node.exc_sum += (int64_t)aE;
+    }
+}
+__device__ __forceinline__ int64_t hd_rl64(int64_t v, uint32_t l) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), l) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l));
+}
+__device__ __forceinline__ int64_t hd_shr64(int64_t v, int64_t ident) {  // the lane below's value (wave_shr:1)
+    return (int64_t)(((uint64_t)(uint32_t)HD_DPP((uint32_t)((uint64_t)ident >> 32), (uint32_t)((uint64_t)v >> 32), 0x138, 0xf) << 32) |
+                     (uint64_t)(uint32_t)HD_DPP((uint32_t)(uint64_t)ident, (uint32_t)(uint64_t)v, 0x138, 0xf));
+}
+
+template <bool RL>
+__global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                             const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                             int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    __shared__ Node node;
+    __shared__ uint16_t win[HD_RW];
+    if (blockIdx.x >= m) return;
+    const uint32_t lane = threadIdx.x;
+    const Seg sg = segs[order[blockIdx.x]];
+    const uint32_t res = sg.res;
+    const Prog pg = S.prog[res];
+    if (!(pg.xf & (RL ? XF_HEADR : XF_HEADT))) return;  // the cooperative owner's segment
+    const double rcount = S.rules[pg.rule_off].count;
+    const uint32_t rslot = S.rules[pg.rule_off].slot;
+    const int32_t rmaxq = S.rules[pg.rule_off].max_queue;
+    if (lane == 0) node_load(node, S, res);
+    __syncthreads();
+    if (!(node.flags & NI_CHAIN)) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted
+        for (uint32_t p = lane; p < sg.len; p += 64)
+            dec[sg.start + p] = recs[sg.start + p].kind == SG_EV_ENTRY ? mk_dec(ST_NO_CHECK, 0, 0) : mk_dec(ST_NOT_ENTRY, 0, 0);
+        return;
+    }
+    if (lane == 0) {
+        const int64_t tf = t0 + recs[sg.start].dt;
+        if (tf < (node.sb[0].ws > node.sb[1].ws ? node.sb[0].ws : node.sb[1].ws)) atomicOr(bflags, BF_BACKWARD);
+    }
+    const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
+    const uint32_t dblock = mk_dec(ST_BLOCK_FLOW, rslot, 0), dnot = mk_dec(ST_NOT_ENTRY, 0, 0);
+    // THREAD: floor(count) clamped (the closed form's u saturates; the verification compares the double exactly)
+    const double cf = rcount != rcount ? 1e18 : floor(rcount);
+    const int32_t Flc = cf > (double)(1 << 29) ? (1 << 29) : cf < -(double)(1 << 29) ? -(1 << 29) : (int32_t)cf;
+    // RATE: the cost of acquire 1, maxQueueingTimeMs
+    const int64_t cost1 = (rcount <= 0) ? 0 : j_round(1.0 / rcount * 1000);
+    const double inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
+    const int64_t Q = rmaxq;
+    const bool cpos = rcount > 0;
+
+    int32_t c = node.thread;                            // THREAD: curThreadNum (uniform)
+    int64_t L = RL ? S.rstate[pg.rule_off].c - t0 : 0;  // RATE: latestPassedTime relative to t0 (uniform)
+    int32_t thd = 0;                                    // RATE: curThreadNum delta
+    bool last_pass = true;                              // the last decided ENTRY passed (round guesses)
+    // the 500 ms bucket being collected and its sums (uniform)
+    // (per lane; reduced over the wave only when the bucket changes)
+    int64_t cb = -1;
+    uint64_t aP = 0, aB = 0, aS = 0, aRT = 0, aE = 0;
+    uint32_t aMin = HD_NONE, aT = 0;
+    auto fold = [&]() {
+        const uint32_t t = hd_sum_red(aT);
+        if (t) {
+            const uint64_t P = hd_sum_red64(aP), Bk = hd_sum_red64(aB), Su = hd_sum_red64(aS), RT = hd_sum_red64(aRT),
+                           Ex = hd_sum_red64(aE);
+            const uint32_t mn = hd_min_red(aMin);
+            if (lane == 0) hd_fold(node, C, cb, P, Bk, Su, RT, Ex, mn);
+        }
+        aP = aB = aS = aRT = aE = 0;
+        aMin = HD_NONE;
+        aT = 0;
+    };
+    const int32_t toff = (int32_t)(((t0 % 500) + 500) % 500);
+    const int64_t tb0 = (t0 - toff) / 500;  // bucket of relative time -toff
+    // diagnostics (SG_DEBUG=1 with this bin's SG_PROF_BIN): the slowest segment's length, chunks, rounds, bucket
+    // folds and round cycles in dbg[59..63], dbg[30]
+    const bool prof = S.dbg != nullptr;
+    const unsigned long long tm0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long tround = 0, tdec = 0, tstore = 0;
+    uint32_t n_round = 0, n_fold = 0;
+
+    const uint32_t lp0 = lane * HD_EP;
+    uint4 nxt[HD_EP];
+    auto load = [&](uint32_t base) {
+#pragma unroll
+        for (uint32_t e = 0; e < HD_EP; ++e) {
+            const uint32_t p = base + lp0 + e;
+            nxt[e] = make_uint4(0u, 0u, 0u, 0xFFu);
+            if (p < sg.len) nxt[e] = reinterpret_cast<const uint4*>(recs + sg.start)[p];
+        }
+    };
+    load(0);
+    uint32_t nch = 0;
+    for (uint32_t base = 0; base < sg.len; base += HD_CH, ++nch) {
+        const unsigned long long td0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+        // ---- decode the chunk (SEv: dt | x | cnt, rt | kind, flags, code): per-lane bit masks of its 16 positions
+        int32_t dt[HD_EP];
+        uint32_t cz[HD_EP], ref[HD_EP];
+        uint32_t emask = 0, xk = 0, tk = 0, xs = 0, xd = 0, og = 0, badm = 0, vmask = 0, c1 = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < HD_EP; ++e) {
+            const uint4 w = nxt[e];
+            const uint32_t pos = base + lp0 + e;
+            const uint32_t kind = w.w & 0xFFu, code = (w.w >> 16) & 0xFFu;
+            dt[e] = (int32_t)w.x;
+            cz[e] = w.z;
+            uint32_t rr = w.y - sg.start;
+            const bool isE = kind == SG_EV_ENTRY, isX = kind == SG_EV_EXIT, isT = kind == SG_EV_TRACE;
+            const bool batch = (isX || isT) && code == RC_BATCH;
+            const bool bad = batch && rr >= pos;  // not an earlier ENTRY of this resource
+            rr = bad ? 0u : rr;
+            const bool dyn = batch && rr >= base;                                // an ENTRY of this chunk
+            const bool inr = batch && !dyn && rr + HD_RW * 16u >= base + HD_CH;  // in the LDS ring
+            const uint32_t wb = ((uint32_t)win[(rr >> 4) & (HD_RW - 1)] >> (rr & 15)) & 1u;
+            const bool eff = (isX || isT) && (code == RC_NONE || code == RC_PASSED || (inr && wb));  // the chain exists
+            emask |= (uint32_t)isE << e;
+            xk |= (uint32_t)isX << e;
+            tk |= (uint32_t)isT << e;
+            xs |= (uint32_t)eff << e;
+            xd |= (uint32_t)dyn << e;
+            og |= (uint32_t)(batch && !dyn && !inr) << e;
+            badm |= (uint32_t)bad << e;
+            vmask |= (uint32_t)(pos < sg.len) << e;
+            c1 |= (uint32_t)(isE && (w.z & 0xFFFFu) != 1u) << e;
+            ref[e] = rr;
+        }
+        if (badm) atomicOr(bflags, BF_BAD_REF);
+        if (og) {  // older than the ring: the dec[] word (stored >= 255 chunks ago, fenced every 64)
+#pragma unroll
+            for (uint32_t e = 0; e < HD_EP; ++e)
+                if ((og >> e) & 1)
+                    if (st_passed(__hip_atomic_load(&dec[sg.start + ref[e]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu))
+                        xs |= 1u << e;
+        }
+        if (base + HD_CH < sg.len) load(base + HD_CH);
+        if ((nch & 63u) == 63u) __threadfence_block();
+        const uint32_t cnt_t = sg.len - base < HD_CH ? sg.len - base : HD_CH;
+        const uint32_t wi = ((base >> 4) + lane) & (HD_RW - 1);
+        const bool uni = __ballot(c1 != 0) == 0;  // every ENTRY of the chunk acquires 1
+        // status bits of the lane's positions: committed verdicts below c0, the round's guesses above
+        uint32_t st = last_pass ? emask : 0u;
+        win[wi] = (uint16_t)st;
+        uint32_t wq[HD_EP];  // RATE: the passes' waits
+#pragma unroll
+        for (uint32_t e = 0; e < HD_EP; ++e) wq[e] = 0;
+        uint32_t c0 = 0;
+        const unsigned long long tr0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (prof) tdec += tr0 - td0;
+        while (c0 < cnt_t) {
+            ++n_round;
+            const uint32_t lo = c0 > lp0 ? (c0 - lp0 < HD_EP ? c0 - lp0 : HD_EP) : 0u;
+            const uint32_t amask = lo >= HD_EP ? 0u : (0xFFFFu << lo) & 0xFFFFu;  // the lane's active positions
+            const uint32_t am = amask & emask;                                      // ... its active ENTRYs
+            uint32_t gm = 0;        // the round's guesses: ENTRYs that pass
+            uint32_t mm = 0;        // events whose evaluation differs from the guess
+            uint32_t tm = 0;        // evaluated outcomes (ENTRY passes / EXIT effective)
+            int64_t mstate = 0;     // the state right after the lane's first mismatch (THREAD c, RATE L)
+            int64_t endstate = 0;   // the state after the lane's last position
+            if (!RL) {
+                // EXITs' effectiveness under the guesses (LDS: committed verdicts / the last round's guesses)
+                const uint32_t dx = xd & xk & amask;
+                uint32_t dg = 0;
+                if (dx) {
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) dg |= (hd_bit(win, ref[e]) & (dx >> e)) << e;
+                }
+                const uint32_t xm = (xs | dg) & xk & amask;
+                const uint32_t xl = (uint32_t)__popc(xm);
+                const uint32_t xin = hd_add_scan(xl);
+                const int32_t X0 = (int32_t)(xin - xl);
+                const int32_t bu = Flc + 1 - c;  // u = max(0, floor(count) - acquire - c + X + 1)
+                int32_t A = 0, B = HD_INF;
+                {
+                    int32_t X = X0;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const int32_t a = (int32_t)((am >> e) & 1);
+                        int32_t u = bu - (int32_t)(cz[e] & 0xFFFFu) + X;
+                        u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
+                        const int32_t nb = B + 1 < u ? B + 1 : u;
+                        B = a ? nb : B;
+                        A += a;
+                        X += (int32_t)((xm >> e) & 1);
+                    }
+                }
+                int32_t ia = A, ib = B;
+                hd_minplus_scan(ia, ib);
+                int32_t pa = HD_DPP(0, ia, 0x138, 0xf), pb = HD_DPP(HD_INF, ib, 0x138, 0xf);  // wave_shr:1
+                pa = lane == 0 ? 0 : pa;
+                pb = lane == 0 ? HD_INF : pb;
+                {  // the closed form's guesses (exact for acquire counts of 1 and right EXIT guesses)
+                    int32_t P = pa < pb ? pa : pb, X = X0;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const bool a = (am >> e) & 1;
+                        int32_t u = bu - (int32_t)(cz[e] & 0xFFFFu) + X;
+                        u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
+                        const int32_t Pn = a ? (P + 1 < u ? P + 1 : u) : P;
+                        gm |= (uint32_t)(Pn > P) << e;
+                        P = Pn;
+                        X += (int32_t)((xm >> e) & 1);
+                    }
+                }
+                // publish the guesses (same-chunk EXITs read them; a wave's LDS operations complete in order)
+                st = (st & ~amask) | gm;
+                win[wi] = (uint16_t)st;
+                const uint32_t gl = (uint32_t)__popc(gm);
+                const uint32_t gin = hd_add_scan(gl);
+                const int32_t P0 = (int32_t)(gin - gl);
+                if (!uni) {  // mixed acquire counts: the closed form is a guess; evaluate at the counted prefix
+                    int32_t Pc = P0, Xc = X0;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const bool a = (am >> e) & 1, g = (gm >> e) & 1;
+                        const int32_t ci = c + Pc - Xc;
+                        const bool tr = !((double)j_iadd(ci, (int32_t)(cz[e] & 0xFFFFu)) > rcount);
+                        mm |= (uint32_t)(a && tr != g) << e;
+                        tm |= (uint32_t)(a && tr) << e;
+                        Pc += g ? 1 : 0;
+                        Xc += (int32_t)((xm >> e) & 1);
+                    }
+                } else {
+                    tm |= gm;
+                }
+                if (dx) {  // same-chunk EXITs: effective iff their ENTRY's new guess passes
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const uint32_t now = hd_bit(win, ref[e]), d = (dx >> e) & 1, was = (xm >> e) & 1;
+                        mm |= (d & (now ^ was)) << e;
+                        tm |= (d & now) << e;
+                    }
+                }
+                if (mm) {  // the state right after the lane's first mismatch
+                    const uint32_t e1 = (uint32_t)__ffs((int)mm) - 1, below = (1u << e1) - 1u;
+                    const int32_t cb1 = c + P0 + __popc(gm & below) - (X0 + __popc(xm & below));
+                    const int32_t t1 = (int32_t)((tm >> e1) & 1);
+                    mstate = ((emask >> e1) & 1) ? cb1 + t1 : cb1 - t1;
+                }
+                endstate = (int64_t)c + (int32_t)gin - (int32_t)xin;
+            } else {
+                // RATE: the round's guesses -- all pass after a pass; after a block the saturated lattice
+                const bool lattice = !last_pass && cost1 > 0;
+                uint32_t lastt = 0;  // the lane's last active ENTRY time (+ 2^31 + 1; 0 none)
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) lastt = ((am >> e) & 1) ? (uint32_t)dt[e] + 0x80000001u : lastt;
+                const uint32_t tin = hd_max_scan(lastt);
+                uint32_t tpv = (uint32_t)HD_DPP(0, tin, 0x138, 0xf);
+                tpv = lane == 0 ? 0u : tpv;
+                const double Lq = (double)(L - Q) - 0.5;  // lattice index of t: floor((t - L + Q + 0.5) / cost)
+                double kp = tpv ? floor(((double)(int32_t)(tpv - 0x80000001u) - Lq) * inv1) : 0.0;
+                kp = kp > 0.0 ? kp : 0.0;
+                int64_t A = 0, B = HD_NEG;
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    const bool a = (am >> e) & 1;
+                    const uint32_t cnt = cz[e] & 0xFFFFu;
+                    const double k = floor(((double)dt[e] - Lq) * inv1);
+                    const bool g = a && (cnt == 0 || (cpos && (!lattice || k > kp)));
+                    kp = (a && k > kp) ? k : kp;
+                    gm |= (uint32_t)g << e;
+                    const int64_t cs = uni ? cost1 : hd_cost(rcount, cnt, cost1);
+                    const bool up = g && cnt > 0 && cpos;
+                    const int64_t nb = B + cs > (int64_t)dt[e] ? B + cs : (int64_t)dt[e];
+                    B = up ? nb : B;
+                    A += up ? cs : 0;
+                }
+                int64_t ia = A, ib = B;
+                hd_maxplus_scan(ia, ib);
+                int64_t pa = hd_shr64(ia, 0), pb = hd_shr64(ib, HD_NEG);
+                pa = lane == 0 ? 0 : pa;
+                pb = lane == 0 ? HD_NEG : pb;
+                int64_t Lc = L + pa > pb ? L + pa : pb;  // L before the lane's first active position
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    const bool a = (am >> e) & 1, g = (gm >> e) & 1;
+                    const uint32_t cnt = cz[e] & 0xFFFFu;
+                    const int64_t t = dt[e];
+                    const int64_t cs = uni ? cost1 : hd_cost(rcount, cnt, cost1);
+                    const bool up = cnt > 0 && cpos;
+                    const bool tr = cnt == 0 || (cpos && ((Lc + cs <= t) || (Lc + cs - t <= Q)));
+                    const int64_t Ln = Lc + cs > t ? Lc + cs : t;
+                    const int64_t wv = Lc + cs - t;
+                    const uint32_t w = (tr && up && wv > 0) ? (wv > 0xFFFF ? 0xFFFFu : (uint32_t)wv) : 0u;
+                    wq[e] = a ? w : wq[e];
+                    const bool mis = a && tr != g;
+                    mstate = (mis && !mm) ? ((tr && up) ? Ln : Lc) : mstate;
+                    mm |= (uint32_t)mis << e;
+                    tm |= (uint32_t)(a && tr) << e;
+                    Lc = (a && g && up) ? Ln : Lc;
+                }
+                endstate = Lc;
+                st = (st & ~amask) | gm;
+            }
+            // the wave's first mismatch (lanes in position order): it takes its evaluated outcome, everything before
+            // it stands, positions after it keep the round's guesses for the next round
+            const uint64_t bal = __ballot(mm != 0);
+            uint32_t cend, ml = 63, me = HD_EP;
+            int64_t ns;
+            if (bal) {
+                ml = (uint32_t)__ffsll((long long)bal) - 1;
+                me = (uint32_t)__ffs(__builtin_amdgcn_readlane((int)mm, ml)) - 1;
+                const uint32_t mt = ((uint32_t)__builtin_amdgcn_readlane((int)tm, ml) >> me) & 1u;
+                cend = ml * HD_EP + me + 1;
+                const uint32_t fb = (lane == ml) ? (emask & (1u << me)) : 0u;
+                st = (st & ~fb) | (mt ? fb : 0u);
+                ns = hd_rl64(mstate, ml);
+            } else {
+                cend = cnt_t;
+                ns = hd_rl64(endstate, 63);
+            }
+            win[wi] = (uint16_t)st;
+            if (RL) L = ns; else c = (int32_t)ns;
+            {  // the last committed ENTRY's verdict seeds the next round's guesses
+                const uint32_t cm = lane < ml ? 0xFFFFu : lane == ml ? (me >= HD_EP ? 0xFFFFu : (2u << me) - 1u) : 0u;
+                const uint32_t em = am & cm;
+                const uint64_t eb = __ballot(em != 0);
+                if (eb) {
+                    const uint32_t ll = 63u - (uint32_t)__clzll((long long)eb);
+                    const uint32_t lem = (uint32_t)__builtin_amdgcn_readlane((int)em, ll);
+                    const uint32_t lst = (uint32_t)__builtin_amdgcn_readlane((int)st, ll);
+                    last_pass = (lst >> (31u - (uint32_t)__clz(lem))) & 1u;
+                }
+            }
+            c0 = cend;
+        }
+        if (prof) tround += __builtin_amdgcn_s_memtime() - tr0;
+        // ---- the chunk is decided: verdict words, effective EXIT / TRACEs, statistics per 500 ms bucket
+        uint32_t xe = xs;
+        if (xd) {
+#pragma unroll
+            for (uint32_t e = 0; e < HD_EP; ++e) xe |= (hd_bit(win, ref[e]) & (xd >> e)) << e;
+        }
+        xe &= xk | tk;
+#pragma unroll
+        for (uint32_t e = 0; e < HD_EP; ++e) {
+            const uint32_t d = ((emask >> e) & 1) ? (((st >> e) & 1) ? mk_dec(ST_PASS, 0, RL ? (int64_t)wq[e] : 0) : dblock) : dnot;
+            if ((vmask >> e) & 1) dec[sg.start + base + lp0 + e] = d;
+        }
+        if (prof) tstore += __builtin_amdgcn_s_memtime() - tr0;
+        if (RL) thd += (int32_t)hd_sum_red((uint32_t)(__popc(emask & st) - __popc(xe & xk)));
+        uint32_t left = vmask;  // events not yet in a bucket
+        for (;;) {
+            const uint64_t lb = __ballot(left != 0);
+            if (!lb) break;
+            ++n_fold;
+            const uint32_t fl = (uint32_t)__ffsll((long long)lb) - 1;
+            const uint32_t fe = (uint32_t)__ffs((int)left) - 1;
+            int32_t fdt = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dt[e] : fdt;
+            const int32_t bdt = __builtin_amdgcn_readlane(fdt, fl) + toff;
+            const int32_t brel = bdt >= 0 ? bdt / 500 : -((499 - bdt) / 500);
+            const int64_t b = tb0 + brel;
+            if (b != cb) {
+                fold();
+                cb = b;
+            }
+            const int32_t lo_dt = brel * 500 - toff, hi_dt = lo_dt + 500;  // the bucket's relative times
+            uint32_t sP = 0, sB = 0, sS = 0, sRT = 0, sE = 0, sT = 0, sMin = HD_NONE;
+#pragma unroll
+            for (uint32_t e = 0; e < HD_EP; ++e) {
+                const bool in = ((left >> e) & 1) && dt[e] >= lo_dt && dt[e] < hi_dt;
+                const uint32_t cnt = cz[e] & 0xFFFFu, rtv = cz[e] >> 16;
+                const bool ent = in && ((emask >> e) & 1), ps = ent && ((st >> e) & 1);
+                const bool xx = in && ((xe & xk) >> e) & 1, tt = in && ((xe & tk) >> e) & 1 && cnt > 0;
+                sP += ps ? cnt : 0u;
+                sB += (ent && !ps) ? cnt : 0u;
+                sS += xx ? cnt : 0u;
+                sRT += xx ? rtv : 0u;
+                sMin = (xx && rtv < sMin) ? rtv : sMin;
+                sE += tt ? cnt : 0u;
+                sT += (ent || xx || tt) ? 1u : 0u;
+                left &= ~((uint32_t)in << e);
+            }
+            aP += sP;
+            aB += sB;
+            aS += sS;
+            aRT += sRT;
+            aE += sE;
+            aT += sT;
+            aMin = sMin < aMin ? sMin : aMin;
+        }
+    }
+    fold();
+    if (prof && lane == 0) {
+        const unsigned long long tot = __builtin_amdgcn_s_memtime() - tm0;
+        if (atomicMax(&S.dbg[59], tot) < tot) {
+            S.dbg[60] = sg.len;
+            S.dbg[61] = nch;
+            S.dbg[62] = n_round;
+            S.dbg[63] = n_fold;
+            S.dbg[30] = tround;
+            S.dbg[44] = tdec;
+            S.dbg[45] = tstore;
+            S.dbg[31] = (unsigned long long)rcount;
+        }
+    }
+    if (lane == 0) {
+        node.thread = RL ? node.thread + thd : c;
+        min_flush(node, C.minb);
+        node_store(node, S, res, pg.pflags);
+        if (RL) S.rstate[pg.rule_off].c = L + t0;
+    }
+}
+
+hipError_t launch_head(const SEv* recs, const Seg* segs, const uint32_t* order, uint32_t m, const DevState& S,
+                       const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_head<false>, dim3(m), dim3(64), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_head<true>, dim3(m), dim3(64), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    return hipGetLastError();
+}
+
+} // namespace sg
