@@ -112,7 +112,7 @@ enum : uint16_t {
                          // checks by pvalue.hip's passes, k_pq then folding the statistics only (SG_PV_PQ)
     XF_HEADT = 16,       // the only rule is one THREAD-grade DefaultController flow rule on the ClusterNode (DIRECT,
                          // limitApp default): its J16 / J4 segments take the event-driven head owner (head.hip)
-    XF_HEADR = 32        // ... one QPS RateLimiter flow rule likewise
+    XF_HEADR = 32        // ... one QPS RateLimiter (or WarmUpRateLimiter of count > 0) flow rule likewise
 };
 enum : uint32_t {
     PX_MULTI = 1,        // representative of a STRATEGY_RELATE component (its members share one segment)

@@ -1078,7 +1078,9 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                 const DRule& d = rules[p.rule_off];
                 if (d.strategy == SG_STRATEGY_DIRECT && d.la_kind == LA_DEFAULT) {
                     if (d.grade == SG_FLOW_GRADE_THREAD && d.behavior == SG_CONTROL_BEHAVIOR_DEFAULT) p.xf |= XF_HEADT;
-                    else if (d.grade == SG_FLOW_GRADE_QPS && d.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER) p.xf |= XF_HEADR;
+                    else if (d.grade == SG_FLOW_GRADE_QPS && (d.behavior == SG_CONTROL_BEHAVIOR_RATE_LIMITER ||
+                                                              (d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER && d.count > 0)))
+                        p.xf |= XF_HEADR;
                 }
             }
         }

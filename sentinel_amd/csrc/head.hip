@@ -33,7 +33,7 @@ namespace sg {
 
 #define HD_EP 16u                 // events per lane of a chunk (one 16-bit status word a lane)
 #define HD_CH (64u * HD_EP)       // positions per chunk
-#define HD_RW 16384u              // status ring words (32 KiB of LDS): 2^18 positions
+#define HD_RW 8192u               // status ring words (16 KiB of LDS): 2^17 positions
 #define HD_INF 0x3FFFFFFF
 #define HD_NONE 0xFFFFFFFFu
 #define HD_NEG (-(1ll << 62))
@@ -90,10 +90,21 @@ enum : uint32_t { HK_ENT = 1u, HK_EXIT = 2u, HK_TRACE = 3u, HK_KIND = 3u, HK_EFF
 __device__ __forceinline__ uint32_t hd_bit(const uint16_t* win, uint32_t p) { return (win[(p >> 4) & (HD_RW - 1)] >> (p & 15)) & 1u; }
 
 // RL: the ENTRY's cost (RateLimiterController.java:53: Math.round(1.0 * acquireCount / count * 1000))
-__device__ __attribute__((noinline)) int64_t hd_cost(double count, uint32_t cnt, int64_t cost1) {
+// (WarmUpRateLimiterController.java:50-70: the warming QPS of the second's synced storedTokens, else count)
+__device__ __attribute__((noinline)) int64_t hd_cost(double qps, uint32_t cnt, int64_t cost1) {
     if (cnt == 1) return cost1;
-    if (cnt == 0 || count <= 0) return 0;
-    return j_round(1.0 * (double)cnt / count * 1000);
+    if (cnt == 0 || qps <= 0) return 0;
+    return j_round(1.0 * (double)cnt / qps * 1000);
+}
+// leader, WarmUpRateLimiter: syncToken at the second of the first ENTRY (WarmUpController.java:141-174 with
+// previousPassQps: the minute window's pass of the second before, LeapArray.getPreviousWindow), then the QPS its
+// cost follows for the rest of the second
+__device__ __attribute__((noinline)) double hd_warm_second(const DRule* rp, RState* rs, int64_t now, int64_t prev) {
+    const DRule r = *rp;
+    RState s = *rs;
+    warm_sync(r, s, now, prev);
+    *rs = s;
+    return s.a >= r.warning_token ? warm_qps(r, s.a) : r.count;
 }
 
 // leader: k_jac round_fold of one collected 500 ms bucket (out of line: rare, and its 64-bit node arithmetic would
@@ -119,14 +130,37 @@ __device__ __forceinline__ int64_t hd_shr64(int64_t v, int64_t ident) {  // the 
                      (uint64_t)(uint32_t)HD_DPP((uint32_t)(uint64_t)ident, (uint32_t)(uint64_t)v, 0x138, 0xf));
 }
 
+// one chunk's decoded inputs in LDS, [field][owner lane] (a lane's words in its own bank); three in flight: the
+// decoders fill chunk j while the owner decides chunk j - 1 and the statistics wave closes chunk j - 2
+enum { HM_E = 0, HM_X, HM_T, HM_XS, HM_XD, HM_C1, HM_V, HD_NM };  // ENTRY / EXIT / TRACE kinds, effective (known),
+                                                                   // effective iff the ENTRY at ref passed, acquire
+                                                                   // != 1, valid
 template <bool RL>
-__global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
-                                             const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
-                                             int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+struct HdSlot {
+    uint32_t m[2][HD_NM][64];  // [decoder half][mask][owner lane]: bits of the lane's 16 positions
+    uint32_t ref[HD_EP][64];
+    uint32_t cz[HD_EP][64];
+    int32_t dt[HD_EP][64];
+    uint32_t wq[RL ? HD_EP : 1][64];  // RATE: the passes' waits (the owner writes them, the statistics wave reads them)
+};
+__device__ __forceinline__ void hd_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A workgroup of four waves per head segment, pipelined over its chunks: waves 1 and 2 decode chunk j (eight
+// positions of each owner lane apiece), wave 0 -- the owner -- decides chunk j - 1 (the guess-and-verify rounds), wave
+// 3 writes chunk j - 2's verdict words and folds its statistics; one LDS barrier a step.  EXIT references into the
+// chunk being decided or the one before it are resolved by the owner (their verdicts are not final when decoded).
+template <bool RL>
+__global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     __shared__ Node node;
     __shared__ uint16_t win[HD_RW];
+    __shared__ HdSlot<RL> slot[3];
+    __shared__ int32_t hthd;
     if (blockIdx.x >= m) return;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t lane = tid & 63;
     const Seg sg = segs[order[blockIdx.x]];
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
@@ -134,129 +168,186 @@ __global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const
     const double rcount = S.rules[pg.rule_off].count;
     const uint32_t rslot = S.rules[pg.rule_off].slot;
     const int32_t rmaxq = S.rules[pg.rule_off].max_queue;
-    if (lane == 0) node_load(node, S, res);
+    if (tid == 0) node_load(node, S, res);
     __syncthreads();
     if (!(node.flags & NI_CHAIN)) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted
-        for (uint32_t p = lane; p < sg.len; p += 64)
+        for (uint32_t p = tid; p < sg.len; p += 256)
             dec[sg.start + p] = recs[sg.start + p].kind == SG_EV_ENTRY ? mk_dec(ST_NO_CHECK, 0, 0) : mk_dec(ST_NOT_ENTRY, 0, 0);
         return;
     }
-    if (lane == 0) {
+    if (tid == 0) {
         const int64_t tf = t0 + recs[sg.start].dt;
         if (tf < (node.sb[0].ws > node.sb[1].ws ? node.sb[0].ws : node.sb[1].ws)) atomicOr(bflags, BF_BACKWARD);
     }
     const Ctx C{S.minb + (uint64_t)res * 60, cfg.max_rt, pg.pflags};
-    const uint32_t dblock = mk_dec(ST_BLOCK_FLOW, rslot, 0), dnot = mk_dec(ST_NOT_ENTRY, 0, 0);
-    // THREAD: floor(count) clamped (the closed form's u saturates; the verification compares the double exactly)
-    const double cf = rcount != rcount ? 1e18 : floor(rcount);
-    const int32_t Flc = cf > (double)(1 << 29) ? (1 << 29) : cf < -(double)(1 << 29) ? -(1 << 29) : (int32_t)cf;
-    // RATE: the cost of acquire 1, maxQueueingTimeMs
-    const int64_t cost1 = (rcount <= 0) ? 0 : j_round(1.0 / rcount * 1000);
-    const double inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
-    const int64_t Q = rmaxq;
-    const bool cpos = rcount > 0;
-
-    int32_t c = node.thread;                            // THREAD: curThreadNum (uniform)
-    int64_t L = RL ? S.rstate[pg.rule_off].c - t0 : 0;  // RATE: latestPassedTime relative to t0 (uniform)
-    int32_t thd = 0;                                    // RATE: curThreadNum delta
-    bool last_pass = true;                              // the last decided ENTRY passed (round guesses)
-    // the 500 ms bucket being collected and its sums (uniform)
-    // (per lane; reduced over the wave only when the bucket changes)
-    int64_t cb = -1;
-    uint64_t aP = 0, aB = 0, aS = 0, aRT = 0, aE = 0;
-    uint32_t aMin = HD_NONE, aT = 0;
-    auto fold = [&]() {
-        const uint32_t t = hd_sum_red(aT);
-        if (t) {
-            const uint64_t P = hd_sum_red64(aP), Bk = hd_sum_red64(aB), Su = hd_sum_red64(aS), RT = hd_sum_red64(aRT),
-                           Ex = hd_sum_red64(aE);
-            const uint32_t mn = hd_min_red(aMin);
-            if (lane == 0) hd_fold(node, C, cb, P, Bk, Su, RT, Ex, mn);
+    // WarmUpRateLimiter: the owner syncs the stored tokens at the first ENTRY of every second; previousPassQps is the
+    // minute bucket of the second before as the kernel started (its (ws, pass) in LDS) plus this kernel's passes in it
+    const bool warm = RL && S.rules[pg.rule_off].behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER;
+    __shared__ RState hrs;
+    __shared__ int64_t hmws[60], hmpass[60];
+    __shared__ double hqps;
+    if (warm) {
+        if (tid < 60) {
+            hmws[tid] = C.minb[tid].ws;
+            hmpass[tid] = C.minb[tid].pass;
         }
-        aP = aB = aS = aRT = aE = 0;
-        aMin = HD_NONE;
-        aT = 0;
-    };
-    const int32_t toff = (int32_t)(((t0 % 500) + 500) % 500);
-    const int64_t tb0 = (t0 - toff) / 500;  // bucket of relative time -toff
-    // diagnostics (SG_DEBUG=1 with this bin's SG_PROF_BIN): the slowest segment's length, chunks, rounds, bucket
-    // folds and round cycles in dbg[59..63], dbg[30]
+        if (tid == 0) hrs = S.rstate[pg.rule_off];
+    }
+    if (tid == 0) hthd = 0;
+    __syncthreads();
     const bool prof = S.dbg != nullptr;
     const unsigned long long tm0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
-    unsigned long long tround = 0, tdec = 0, tstore = 0;
-    uint32_t n_round = 0, n_fold = 0;
-
+    const uint32_t nch = (sg.len + HD_CH - 1) / HD_CH;
     const uint32_t lp0 = lane * HD_EP;
-    uint4 nxt[HD_EP];
-    auto load = [&](uint32_t base) {
+
+    if (wv == 1 || wv == 2) {
+        // ================= decoders: positions [8h, 8h + 8) of owner lane `lane`, one chunk a step
+        const uint32_t h = wv - 1, e0 = h * 8;
+        uint4 nxt[8];
+        auto load = [&](uint32_t base) {
 #pragma unroll
-        for (uint32_t e = 0; e < HD_EP; ++e) {
-            const uint32_t p = base + lp0 + e;
-            nxt[e] = make_uint4(0u, 0u, 0u, 0xFFu);
-            if (p < sg.len) nxt[e] = reinterpret_cast<const uint4*>(recs + sg.start)[p];
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t p = base + lp0 + e0 + k;
+                nxt[k] = make_uint4(0u, 0u, 0u, 0xFFu);
+                if (p < sg.len) nxt[k] = reinterpret_cast<const uint4*>(recs + sg.start)[p];
+            }
+        };
+        load(0);
+        for (uint32_t j = 0; j < nch + 2; ++j) {
+            if (j < nch) {
+                const uint32_t base = j * HD_CH;
+                HdSlot<RL>& so = slot[j % 3];
+                uint32_t mk[HD_NM] = {0, 0, 0, 0, 0, 0, 0};
+                uint32_t og = 0, badm = 0;
+                uint32_t rref[8];
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t e = e0 + k;
+                    const uint4 w = nxt[k];
+                    const uint32_t pos = base + lp0 + e;
+                    const uint32_t kind = w.w & 0xFFu, code = (w.w >> 16) & 0xFFu;
+                    uint32_t rr = w.y - sg.start;
+                    const bool isE = kind == SG_EV_ENTRY, isX = kind == SG_EV_EXIT, isT = kind == SG_EV_TRACE;
+                    const bool batch = (isX || isT) && code == RC_BATCH;
+                    const bool bad = batch && rr >= pos;  // not an earlier ENTRY of this resource
+                    rr = bad ? 0u : rr;
+                    const bool dyn = batch && rr + HD_CH >= base;                        // this chunk or the one before
+                    const bool inr = batch && !dyn && rr + HD_RW * 16u >= base + HD_CH;  // in the LDS ring
+                    const uint32_t wb = ((uint32_t)win[(rr >> 4) & (HD_RW - 1)] >> (rr & 15)) & 1u;
+                    const bool eff = (isX || isT) && (code == RC_NONE || code == RC_PASSED || (inr && wb));
+                    mk[HM_E] |= (uint32_t)isE << e;
+                    mk[HM_X] |= (uint32_t)isX << e;
+                    mk[HM_T] |= (uint32_t)isT << e;
+                    mk[HM_XS] |= (uint32_t)eff << e;
+                    mk[HM_XD] |= (uint32_t)dyn << e;
+                    mk[HM_C1] |= (uint32_t)(pos < sg.len && (w.z & 0xFFFFu) != 1u) << e;
+                    mk[HM_V] |= (uint32_t)(pos < sg.len) << e;
+                    og |= (uint32_t)(batch && !dyn && !inr) << e;
+                    badm |= (uint32_t)bad << e;
+                    rref[k] = rr;
+                    so.ref[e][lane] = rr;
+                    so.cz[e][lane] = w.z;
+                    so.dt[e][lane] = (int32_t)w.x;
+                }
+                if (badm) atomicOr(bflags, BF_BAD_REF);
+                if (og) {  // older than the ring: the dec[] word (stored >= 120 chunks ago)
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; ++k)
+                        if ((og >> (e0 + k)) & 1)
+                            if (st_passed(__hip_atomic_load(&dec[sg.start + rref[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu))
+                                mk[HM_XS] |= 1u << (e0 + k);
+                }
+#pragma unroll
+                for (int q = 0; q < HD_NM; ++q) so.m[h][q][lane] = mk[q];
+                if (j + 1 < nch) load(base + HD_CH);
+            }
+            hd_lds_barrier();
         }
-    };
-    load(0);
-    uint32_t nch = 0;
-    for (uint32_t base = 0; base < sg.len; base += HD_CH, ++nch) {
-        const unsigned long long td0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
-        // ---- decode the chunk (SEv: dt | x | cnt, rt | kind, flags, code): per-lane bit masks of its 16 positions
-        int32_t dt[HD_EP];
-        uint32_t cz[HD_EP], ref[HD_EP];
-        uint32_t emask = 0, xk = 0, tk = 0, xs = 0, xd = 0, og = 0, badm = 0, vmask = 0, c1 = 0;
+    } else if (wv == 0) {
+        // ================= the owner: the guess-and-verify rounds of chunk j - 1
+        const double cf = rcount != rcount ? 1e18 : floor(rcount);
+        const int32_t Flc = cf > (double)(1 << 29) ? (1 << 29) : cf < -(double)(1 << 29) ? -(1 << 29) : (int32_t)cf;
+        int64_t cost1 = (rcount <= 0) ? 0 : j_round(1.0 / rcount * 1000);
+        double inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
+        double qps = rcount;  // the QPS the cost of acquire n follows (WarmUpRateLimiter: per second)
+        int64_t ksec = INT64_MIN, kcur = 0;  // the second being decided and this kernel's passes in it (uniform)
+        const int64_t Q = rmaxq;
+        const bool cpos = rcount > 0;
+        int32_t c = node.thread;                            // THREAD: curThreadNum (uniform)
+        int64_t L = RL ? S.rstate[pg.rule_off].c - t0 : 0;  // RATE: latestPassedTime relative to t0 (uniform)
+        bool last_pass = true;                              // the last decided ENTRY passed (round guesses)
+        uint32_t n_round = 0;
+        unsigned long long tround = 0;
+        for (uint32_t j = 0; j < nch + 2; ++j) {
+            if (j >= 1 && j <= nch) {
+                const unsigned long long tr0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+                const uint32_t q = j - 1, base = q * HD_CH;
+                HdSlot<RL>& so = slot[q % 3];
+                const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
+                const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
+                const uint32_t xs = so.m[0][HM_XS][lane] | so.m[1][HM_XS][lane];
+                const uint32_t xd = so.m[0][HM_XD][lane] | so.m[1][HM_XD][lane];
+                const uint32_t c1 = so.m[0][HM_C1][lane] | so.m[1][HM_C1][lane];
+                int32_t dt[HD_EP];
+                uint32_t cz[HD_EP], ref[HD_EP];
 #pragma unroll
-        for (uint32_t e = 0; e < HD_EP; ++e) {
-            const uint4 w = nxt[e];
-            const uint32_t pos = base + lp0 + e;
-            const uint32_t kind = w.w & 0xFFu, code = (w.w >> 16) & 0xFFu;
-            dt[e] = (int32_t)w.x;
-            cz[e] = w.z;
-            uint32_t rr = w.y - sg.start;
-            const bool isE = kind == SG_EV_ENTRY, isX = kind == SG_EV_EXIT, isT = kind == SG_EV_TRACE;
-            const bool batch = (isX || isT) && code == RC_BATCH;
-            const bool bad = batch && rr >= pos;  // not an earlier ENTRY of this resource
-            rr = bad ? 0u : rr;
-            const bool dyn = batch && rr >= base;                                // an ENTRY of this chunk
-            const bool inr = batch && !dyn && rr + HD_RW * 16u >= base + HD_CH;  // in the LDS ring
-            const uint32_t wb = ((uint32_t)win[(rr >> 4) & (HD_RW - 1)] >> (rr & 15)) & 1u;
-            const bool eff = (isX || isT) && (code == RC_NONE || code == RC_PASSED || (inr && wb));  // the chain exists
-            emask |= (uint32_t)isE << e;
-            xk |= (uint32_t)isX << e;
-            tk |= (uint32_t)isT << e;
-            xs |= (uint32_t)eff << e;
-            xd |= (uint32_t)dyn << e;
-            og |= (uint32_t)(batch && !dyn && !inr) << e;
-            badm |= (uint32_t)bad << e;
-            vmask |= (uint32_t)(pos < sg.len) << e;
-            c1 |= (uint32_t)(isE && (w.z & 0xFFFFu) != 1u) << e;
-            ref[e] = rr;
-        }
-        if (badm) atomicOr(bflags, BF_BAD_REF);
-        if (og) {  // older than the ring: the dec[] word (stored >= 255 chunks ago, fenced every 64)
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    dt[e] = so.dt[e][lane];
+                    cz[e] = so.cz[e][lane];
+                    ref[e] = so.ref[e][lane];
+                }
+                const uint32_t cnt_t = sg.len - base < HD_CH ? sg.len - base : HD_CH;
+                const uint32_t wi = ((base >> 4) + lane) & (HD_RW - 1);
+                const bool uni = __ballot(c1 != 0) == 0;  // every event of the chunk counts 1
+                uint32_t st = last_pass ? emask : 0u;      // committed verdicts below c0, the round's guesses above
+                win[wi] = (uint16_t)st;
+                uint32_t wq[HD_EP];
 #pragma unroll
-            for (uint32_t e = 0; e < HD_EP; ++e)
-                if ((og >> e) & 1)
-                    if (st_passed(__hip_atomic_load(&dec[sg.start + ref[e]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu))
-                        xs |= 1u << e;
-        }
-        if (base + HD_CH < sg.len) load(base + HD_CH);
-        if ((nch & 63u) == 63u) __threadfence_block();
-        const uint32_t cnt_t = sg.len - base < HD_CH ? sg.len - base : HD_CH;
-        const uint32_t wi = ((base >> 4) + lane) & (HD_RW - 1);
-        const bool uni = __ballot(c1 != 0) == 0;  // every ENTRY of the chunk acquires 1
-        // status bits of the lane's positions: committed verdicts below c0, the round's guesses above
-        uint32_t st = last_pass ? emask : 0u;
-        win[wi] = (uint16_t)st;
-        uint32_t wq[HD_EP];  // RATE: the passes' waits
-#pragma unroll
-        for (uint32_t e = 0; e < HD_EP; ++e) wq[e] = 0;
-        uint32_t c0 = 0;
-        const unsigned long long tr0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
-        if (prof) tdec += tr0 - td0;
+                for (uint32_t e = 0; e < HD_EP; ++e) wq[e] = 0;
+                uint32_t c0 = 0;
         while (c0 < cnt_t) {
             ++n_round;
             const uint32_t lo = c0 > lp0 ? (c0 - lp0 < HD_EP ? c0 - lp0 : HD_EP) : 0u;
-            const uint32_t amask = lo >= HD_EP ? 0u : (0xFFFFu << lo) & 0xFFFFu;  // the lane's active positions
+            uint32_t amask = lo >= HD_EP ? 0u : (0xFFFFu << lo) & 0xFFFFu;  // the lane's active positions
+            uint32_t act_end = cnt_t;                                         // the round's active range ends here
+            if (warm) {  // a round stays in the second of its first ENTRY (the cost is fixed there)
+                const uint32_t ae = amask & emask;
+                const uint64_t eb = __ballot(ae != 0);
+                if (eb) {
+                    const uint32_t fl = (uint32_t)__ffsll((long long)eb) - 1;
+                    const uint32_t fe = (uint32_t)__ffs(__builtin_amdgcn_readlane((int)ae, fl)) - 1;
+                    int32_t fdt = 0;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dt[e] : fdt;
+                    const int64_t tn = t0 + __builtin_amdgcn_readlane(fdt, fl);
+                    const int64_t T = tn - tn % 1000;
+                    if (T != ksec) {
+                        const int64_t pk = (T - 1000 == ksec) ? kcur : 0;
+                        const int sl = (int)(((T - 1000) / 1000) % 60);
+                        const int64_t prev = (hmws[sl] == T - 1000 ? hmpass[sl] : 0) + pk;
+                        if (lane == 0) hqps = hd_warm_second(S.rules + pg.rule_off, &hrs, tn, prev);
+                        __builtin_amdgcn_wave_barrier();  // (one wave: its LDS write lands before its reads)
+                        qps = hqps;
+                        cost1 = j_round(1.0 / qps * 1000);
+                        inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
+                        ksec = T;
+                        kcur = 0;
+                    }
+                    const int64_t se = T + 1000 - t0;  // the second's end, relative
+                    const int32_t sei = se > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)se;
+                    uint32_t after = 0;  // the lane's active positions at or past it
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) after |= (uint32_t)(dt[e] >= sei) << e;
+                    after &= amask;
+                    const uint64_t ab = __ballot(after != 0);
+                    if (ab) {
+                        const uint32_t al = (uint32_t)__ffsll((long long)ab) - 1;
+                        act_end = al * HD_EP + (uint32_t)__ffs(__builtin_amdgcn_readlane((int)after, al)) - 1;
+                    }
+                    const uint32_t le = act_end > lp0 ? (act_end - lp0 < HD_EP ? act_end - lp0 : HD_EP) : 0u;
+                    amask &= (1u << le) - 1u;
+                }
+            }
             const uint32_t am = amask & emask;                                      // ... its active ENTRYs
             uint32_t gm = 0;        // the round's guesses: ENTRYs that pass
             uint32_t mm = 0;        // events whose evaluation differs from the guess
@@ -365,8 +456,8 @@ __global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const
                     const bool g = a && (cnt == 0 || (cpos && (!lattice || k > kp)));
                     kp = (a && k > kp) ? k : kp;
                     gm |= (uint32_t)g << e;
-                    const int64_t cs = uni ? cost1 : hd_cost(rcount, cnt, cost1);
-                    const bool up = g && cnt > 0 && cpos;
+                    const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
+                    const bool up = g && (warm || (cnt > 0 && cpos));
                     const int64_t nb = B + cs > (int64_t)dt[e] ? B + cs : (int64_t)dt[e];
                     B = up ? nb : B;
                     A += up ? cs : 0;
@@ -382,9 +473,9 @@ __global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const
                     const bool a = (am >> e) & 1, g = (gm >> e) & 1;
                     const uint32_t cnt = cz[e] & 0xFFFFu;
                     const int64_t t = dt[e];
-                    const int64_t cs = uni ? cost1 : hd_cost(rcount, cnt, cost1);
-                    const bool up = cnt > 0 && cpos;
-                    const bool tr = cnt == 0 || (cpos && ((Lc + cs <= t) || (Lc + cs - t <= Q)));
+                    const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
+                    const bool up = warm || (cnt > 0 && cpos);  // (WarmUpRateLimiter: acquire 0 is a check of cost 0)
+                    const bool tr = (!warm && cnt == 0) || (cpos && ((Lc + cs <= t) || (Lc + cs - t <= Q)));
                     const int64_t Ln = Lc + cs > t ? Lc + cs : t;
                     const int64_t wv = Lc + cs - t;
                     const uint32_t w = (tr && up && wv > 0) ? (wv > 0xFFFF ? 0xFFFFu : (uint32_t)wv) : 0u;
@@ -412,7 +503,7 @@ __global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const
                 st = (st & ~fb) | (mt ? fb : 0u);
                 ns = hd_rl64(mstate, ml);
             } else {
-                cend = cnt_t;
+                cend = act_end;
                 ns = hd_rl64(endstate, 63);
             }
             win[wi] = (uint16_t)st;
@@ -428,93 +519,186 @@ __global__ __launch_bounds__(64) void k_head(const SEv* __restrict__ recs, const
                     last_pass = (lst >> (31u - (uint32_t)__clz(lem))) & 1u;
                 }
             }
+            if (warm) {  // the round's passes (all in second ksec) for the next second's previousPassQps
+                const uint32_t cm = lane < ml ? 0xFFFFu : lane == ml ? (me >= HD_EP ? 0xFFFFu : (2u << me) - 1u) : 0u;
+                const uint32_t pm = am & cm & st;
+                uint32_t sp = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (cz[e] & 0xFFFFu) : 0u;
+                kcur += hd_sum_red(sp);
+            }
             c0 = cend;
         }
-        if (prof) tround += __builtin_amdgcn_s_memtime() - tr0;
-        // ---- the chunk is decided: verdict words, effective EXIT / TRACEs, statistics per 500 ms bucket
-        uint32_t xe = xs;
-        if (xd) {
+                if (RL) {
 #pragma unroll
-            for (uint32_t e = 0; e < HD_EP; ++e) xe |= (hd_bit(win, ref[e]) & (xd >> e)) << e;
-        }
-        xe &= xk | tk;
-#pragma unroll
-        for (uint32_t e = 0; e < HD_EP; ++e) {
-            const uint32_t d = ((emask >> e) & 1) ? (((st >> e) & 1) ? mk_dec(ST_PASS, 0, RL ? (int64_t)wq[e] : 0) : dblock) : dnot;
-            if ((vmask >> e) & 1) dec[sg.start + base + lp0 + e] = d;
-        }
-        if (prof) tstore += __builtin_amdgcn_s_memtime() - tr0;
-        if (RL) thd += (int32_t)hd_sum_red((uint32_t)(__popc(emask & st) - __popc(xe & xk)));
-        uint32_t left = vmask;  // events not yet in a bucket
-        for (;;) {
-            const uint64_t lb = __ballot(left != 0);
-            if (!lb) break;
-            ++n_fold;
-            const uint32_t fl = (uint32_t)__ffsll((long long)lb) - 1;
-            const uint32_t fe = (uint32_t)__ffs((int)left) - 1;
-            int32_t fdt = 0;
-#pragma unroll
-            for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dt[e] : fdt;
-            const int32_t bdt = __builtin_amdgcn_readlane(fdt, fl) + toff;
-            const int32_t brel = bdt >= 0 ? bdt / 500 : -((499 - bdt) / 500);
-            const int64_t b = tb0 + brel;
-            if (b != cb) {
-                fold();
-                cb = b;
+                    for (uint32_t e = 0; e < HD_EP; ++e) so.wq[e][lane] = wq[e];
+                }
+                if (prof) tround += __builtin_amdgcn_s_memtime() - tr0;
             }
-            const int32_t lo_dt = brel * 500 - toff, hi_dt = lo_dt + 500;  // the bucket's relative times
-            uint32_t sP = 0, sB = 0, sS = 0, sRT = 0, sE = 0, sT = 0, sMin = HD_NONE;
-#pragma unroll
-            for (uint32_t e = 0; e < HD_EP; ++e) {
-                const bool in = ((left >> e) & 1) && dt[e] >= lo_dt && dt[e] < hi_dt;
-                const uint32_t cnt = cz[e] & 0xFFFFu, rtv = cz[e] >> 16;
-                const bool ent = in && ((emask >> e) & 1), ps = ent && ((st >> e) & 1);
-                const bool xx = in && ((xe & xk) >> e) & 1, tt = in && ((xe & tk) >> e) & 1 && cnt > 0;
-                sP += ps ? cnt : 0u;
-                sB += (ent && !ps) ? cnt : 0u;
-                sS += xx ? cnt : 0u;
-                sRT += xx ? rtv : 0u;
-                sMin = (xx && rtv < sMin) ? rtv : sMin;
-                sE += tt ? cnt : 0u;
-                sT += (ent || xx || tt) ? 1u : 0u;
-                left &= ~((uint32_t)in << e);
+            hd_lds_barrier();
+        }
+        // the segment's end (after the statistics wave's last fold: the loop's last barrier)
+        if (lane == 0) {
+            node.thread = RL ? node.thread + hthd : c;
+            min_flush(node, C.minb);
+            node_store(node, S, res, pg.pflags);
+            if (RL) {
+                RState o = warm ? hrs : S.rstate[pg.rule_off];
+                o.c = L + t0;
+                S.rstate[pg.rule_off] = o;
             }
-            aP += sP;
-            aB += sB;
-            aS += sS;
-            aRT += sRT;
-            aE += sE;
-            aT += sT;
-            aMin = sMin < aMin ? sMin : aMin;
+            if (prof) {
+                const unsigned long long tot = __builtin_amdgcn_s_memtime() - tm0;
+                if (atomicMax(&S.dbg[59], tot) < tot) {
+                    S.dbg[60] = sg.len;
+                    S.dbg[61] = nch;
+                    S.dbg[62] = n_round;
+                    S.dbg[30] = tround;
+                    S.dbg[31] = (unsigned long long)rcount;
+                }
+            }
         }
-    }
-    fold();
-    if (prof && lane == 0) {
-        const unsigned long long tot = __builtin_amdgcn_s_memtime() - tm0;
-        if (atomicMax(&S.dbg[59], tot) < tot) {
-            S.dbg[60] = sg.len;
-            S.dbg[61] = nch;
-            S.dbg[62] = n_round;
-            S.dbg[63] = n_fold;
-            S.dbg[30] = tround;
-            S.dbg[44] = tdec;
-            S.dbg[45] = tstore;
-            S.dbg[31] = (unsigned long long)rcount;
+    } else {
+        // ================= wave 3: chunk j - 2's verdict words and statistics (per 500 ms bucket, k_jac round_fold)
+        const uint32_t dblock = mk_dec(ST_BLOCK_FLOW, rslot, 0), dnot = mk_dec(ST_NOT_ENTRY, 0, 0);
+        const int32_t toff = (int32_t)(((t0 % 500) + 500) % 500);
+        const int64_t tb0 = (t0 - toff) / 500;  // bucket of relative time -toff
+        int64_t cb = -1;                        // the bucket being collected (uniform); per-lane sums
+        uint64_t aP = 0, aB = 0, aS = 0, aRT = 0, aE = 0;
+        uint32_t aMin = HD_NONE, aT = 0;
+        int32_t thd = 0;
+        auto fold = [&]() {
+            const uint32_t t = hd_sum_red(aT);
+            if (t) {
+                const uint64_t P = hd_sum_red64(aP), Bk = hd_sum_red64(aB), Su = hd_sum_red64(aS), RT = hd_sum_red64(aRT),
+                               Ex = hd_sum_red64(aE);
+                const uint32_t mn = hd_min_red(aMin);
+                if (lane == 0) hd_fold(node, C, cb, P, Bk, Su, RT, Ex, mn);
+            }
+            aP = aB = aS = aRT = aE = 0;
+            aMin = HD_NONE;
+            aT = 0;
+        };
+        for (uint32_t j = 0; j < nch + 2; ++j) {
+            if (j >= 2) {
+                const uint32_t q = j - 2, base = q * HD_CH;
+                HdSlot<RL>& so = slot[q % 3];
+                const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
+                const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
+                const uint32_t tk = so.m[0][HM_T][lane] | so.m[1][HM_T][lane];
+                const uint32_t xd = so.m[0][HM_XD][lane] | so.m[1][HM_XD][lane];
+                const uint32_t c1 = so.m[0][HM_C1][lane] | so.m[1][HM_C1][lane];
+                const uint32_t vmask = so.m[0][HM_V][lane] | so.m[1][HM_V][lane];
+                uint32_t xe = so.m[0][HM_XS][lane] | so.m[1][HM_XS][lane];
+                const uint32_t st = win[((base >> 4) + lane) & (HD_RW - 1)];
+                if (xd) {
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) xe |= (hd_bit(win, so.ref[e][lane]) & (xd >> e)) << e;
+                }
+                xe &= xk | tk;
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    const uint32_t d = ((emask >> e) & 1) ? (((st >> e) & 1) ? mk_dec(ST_PASS, 0, RL ? (int64_t)so.wq[e][lane] : 0) : dblock) : dnot;
+                    if ((vmask >> e) & 1) dec[sg.start + base + lp0 + e] = d;
+                }
+                if (RL) thd += (int32_t)hd_sum_red((uint32_t)(__popc(emask & st) - __popc(xe & xk)));
+                int32_t dt[HD_EP];
+                uint32_t cz[HD_EP];
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    dt[e] = so.dt[e][lane];
+                    cz[e] = so.cz[e][lane];
+                }
+                // one bucket for the whole chunk with every count 1 (the usual case): popcounts
+                const int32_t dfirst = __builtin_amdgcn_readfirstlane(dt[0]);
+                const uint64_t vb = __ballot(vmask != 0);
+                const uint32_t ll = 63u - (uint32_t)__clzll((long long)vb);
+                int32_t dl = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) dl = ((vmask >> e) & 1) ? dt[e] : dl;
+                const int32_t dlast = __builtin_amdgcn_readlane(dl, ll);
+                auto bkt_of = [&](int32_t d) -> int32_t { const int32_t x = d + toff; return x >= 0 ? x / 500 : -((499 - x) / 500); };
+                const int32_t bf = bkt_of(dfirst);
+                if (bf == bkt_of(dlast) && __ballot(c1 != 0) == 0) {
+                    const int64_t b = tb0 + bf;
+                    if (b != cb) {
+                        fold();
+                        cb = b;
+                    }
+                    const uint32_t xx = xe & xk, tt = xe & tk, ne = (uint32_t)__popc(emask & vmask), np = (uint32_t)__popc(emask & st);
+                    aP += np;
+                    aB += ne - np;
+                    aS += (uint32_t)__popc(xx);
+                    aE += (uint32_t)__popc(tt);
+                    aT += ne + (uint32_t)__popc(xx) + (uint32_t)__popc(tt);
+                    uint32_t sRT = 0, sMin = HD_NONE;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const uint32_t rtv = cz[e] >> 16;
+                        const bool x = (xx >> e) & 1;
+                        sRT += x ? rtv : 0u;
+                        sMin = (x && rtv < sMin) ? rtv : sMin;
+                    }
+                    aRT += sRT;
+                    aMin = sMin < aMin ? sMin : aMin;
+                } else {
+                    uint32_t left = vmask;  // events not yet in a bucket
+                    for (;;) {
+                        const uint64_t lb = __ballot(left != 0);
+                        if (!lb) break;
+                        const uint32_t fl = (uint32_t)__ffsll((long long)lb) - 1;
+                        const uint32_t fe = (uint32_t)__ffs((int)left) - 1;
+                        int32_t fdt = 0;
+#pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dt[e] : fdt;
+                        const int32_t brel = bkt_of(__builtin_amdgcn_readlane(fdt, fl));
+                        const int64_t b = tb0 + brel;
+                        if (b != cb) {
+                            fold();
+                            cb = b;
+                        }
+                        const int32_t lo_dt = brel * 500 - toff, hi_dt = lo_dt + 500;  // the bucket's relative times
+                        uint32_t sP = 0, sB = 0, sS = 0, sRT = 0, sE = 0, sT = 0, sMin = HD_NONE;
+#pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) {
+                            const bool in = ((left >> e) & 1) && dt[e] >= lo_dt && dt[e] < hi_dt;
+                            const uint32_t cnt = cz[e] & 0xFFFFu, rtv = cz[e] >> 16;
+                            const bool ent = in && ((emask >> e) & 1), ps = ent && ((st >> e) & 1);
+                            const bool x = in && ((xe & xk) >> e) & 1, t = in && ((xe & tk) >> e) & 1 && cnt > 0;
+                            sP += ps ? cnt : 0u;
+                            sB += (ent && !ps) ? cnt : 0u;
+                            sS += x ? cnt : 0u;
+                            sRT += x ? rtv : 0u;
+                            sMin = (x && rtv < sMin) ? rtv : sMin;
+                            sE += t ? cnt : 0u;
+                            sT += (ent || x || t) ? 1u : 0u;
+                            left &= ~((uint32_t)in << e);
+                        }
+                        aP += sP;
+                        aB += sB;
+                        aS += sS;
+                        aRT += sRT;
+                        aE += sE;
+                        aT += sT;
+                        aMin = sMin < aMin ? sMin : aMin;
+                    }
+                }
+                if (q + 1 == nch) {
+                    fold();
+                    if (lane == 0) hthd = thd;
+                }
+                if ((q & 31u) == 31u) __threadfence_block();  // (old references read the dec[] words)
+            }
+            hd_lds_barrier();
         }
-    }
-    if (lane == 0) {
-        node.thread = RL ? node.thread + thd : c;
-        min_flush(node, C.minb);
-        node_store(node, S, res, pg.pflags);
-        if (RL) S.rstate[pg.rule_off].c = L + t0;
     }
 }
 
 hipError_t launch_head(const SEv* recs, const Seg* segs, const uint32_t* order, uint32_t m, const DevState& S,
                        const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
-    hipLaunchKernelGGL(k_head<false>, dim3(m), dim3(64), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
-    hipLaunchKernelGGL(k_head<true>, dim3(m), dim3(64), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_head<false>, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_head<true>, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
     return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@ The trace here is built to reach every branch of those rounds:
 * acquire counts of 0 / 1 / 2 / 3 on some resources (the closed form is then only a guess; the verification decides);
 * RateLimiter counts 0 (blocks every acquire > 0) / 0.3 / 5 / 50 / 500 / 3,000 (cost 0) with maxQueueingTimeMs
   0 / 20 / 500: the lattice guesses of saturated stretches, the all-pass guesses of open ones, queueing waits;
+* WarmUpRateLimiters (WarmUpRateLimiterController.java) warming up over 2-3 s, acquire 0 / 1 / 2 on one: the
+  cost changes every second with the stored tokens the leader syncs from the second before's passes;
 * one resource with 200k entries/s and 1 % of its RTs at 1.5 s: EXITs naming ENTRYs more than 2^18 positions back
   (past the LDS ring: the dec[] word).
 
@@ -44,7 +46,11 @@ def _spec():
             s.append((dict(count=cnt, max_queueing_time_ms=q, **rl), 6000, 20, (1,)))
     s.append((dict(count=80, max_queueing_time_ms=300, **rl), 3000, 20, (0, 1, 2)))
     s.append((dict(count=200, max_queueing_time_ms=100, **rl), 300, 10, (1,)))  # sparse: open stretches
-    s.append((dict(count=16, grade=th), 200000, None, (1,)))  # the ring-overflow resource
+    wrl = dict(control_behavior=A.CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER)
+    for cnt, q, rate in ((50, 500, 6000), (500, 20, 6000), (5, 500, 800), (2000, 100, 30000)):
+        s.append((dict(count=cnt, max_queueing_time_ms=q, warm_up_period_sec=3, **wrl), rate, 20, (1,)))
+    s.append((dict(count=40, max_queueing_time_ms=200, warm_up_period_sec=2, **wrl), 4000, 20, (0, 1, 2)))
+    s.append((dict(count=16, grade=th), 200000, None, (1,)))  # the ring-overflow resource (last)
     return s
 
 
