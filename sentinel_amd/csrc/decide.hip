@@ -1875,7 +1875,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 1
     const uint32_t res = sg.res;
     const Prog pg = S.prog[res];
     if (CLS != 0 && (((pg.pflags & PF_FROZEN) != 0) != (CLS == 1))) return;  // the other instantiation's segment
-    if ((NW == 16 || NW == 4) && (pg.xf & (XF_HEADT | XF_HEADR)) && !(cfg.dbg_flags & HEAD_OFF)) return;  // k_head's
+    if ((NW == 16 || NW == 4 || NW == 1) && (pg.xf & (XF_HEADT | XF_HEADR)) && !(cfg.dbg_flags & HEAD_OFF)) return;  // k_head's
     const int nf = pg.n_flow, nd = pg.n_degrade, nr = nf + nd;
     // the minute window in LDS (sh.minl): loaded here, written back at the segment's end; no other kernel of the
     // decide stage touches this resource's minute buckets while its owner runs
@@ -4084,7 +4084,7 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     if (!m) return hipSuccess;
     // single-rule THREAD-grade / RateLimiter heads (XF_HEADT / XF_HEADR): the event-driven owner, before the
     // cooperative one (which leaves those segments)
-    if ((bin == BIN_J16 || bin == BIN_J4) && !(cfg.dbg_flags & HEAD_OFF)) {
+    if ((bin == BIN_J16 || bin == BIN_J4 || bin == BIN_J1) && !(cfg.dbg_flags & HEAD_OFF)) {
         const hipError_t he = launch_head(recs, segs, order, m, S, cfg, t0, dec, bflags, st);
         if (he != hipSuccess) return he;
     }

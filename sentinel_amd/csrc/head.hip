@@ -135,13 +135,21 @@ __device__ __forceinline__ int64_t hd_shr64(int64_t v, int64_t ident) {  // the 
 enum { HM_E = 0, HM_X, HM_T, HM_XS, HM_XD, HM_C1, HM_V, HD_NM };  // ENTRY / EXIT / TRACE kinds, effective (known),
                                                                    // effective iff the ENTRY at ref passed, acquire
                                                                    // != 1, valid
-template <bool RL>
 struct HdSlot {
     uint32_t m[2][HD_NM][64];  // [decoder half][mask][owner lane]: bits of the lane's 16 positions
     uint32_t ref[HD_EP][64];
     uint32_t cz[HD_EP][64];
     int32_t dt[HD_EP][64];
-    uint32_t wq[RL ? HD_EP : 1][64];  // RATE: the passes' waits (the owner writes them, the statistics wave reads them)
+    uint32_t wq[HD_EP][64];    // RATE: the passes' waits (the owner writes them, the statistics wave reads them)
+};
+struct HdShared {
+    Node node;
+    uint16_t win[HD_RW];       // status ring: a bit a position, a 16-bit word an owner lane's chunk positions
+    HdSlot slot[3];
+    int32_t hthd;              // RATE: the statistics wave's curThreadNum delta
+    RState hrs;                // WarmUpRateLimiter: storedTokens / lastFilledTime as the owner syncs them
+    int64_t hmws[60], hmpass[60];
+    double hqps;
 };
 __device__ __forceinline__ void hd_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -150,21 +158,21 @@ __device__ __forceinline__ void hd_lds_barrier() { asm volatile("s_waitcnt lgkmc
 // 3 writes chunk j - 2's verdict words and folds its statistics; one LDS barrier a step.  EXIT references into the
 // chunk being decided or the one before it are resolved by the owner (their verdicts are not final when decoded).
 template <bool RL>
-__global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
-                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
-                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
-    __shared__ Node node;
-    __shared__ uint16_t win[HD_RW];
-    __shared__ HdSlot<RL> slot[3];
-    __shared__ int32_t hthd;
-    if (blockIdx.x >= m) return;
+__device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ recs, const Seg& sg, const Prog& pg,
+                                         const DevState& S, const DevCfg& cfg, int64_t t0, uint32_t* __restrict__ dec,
+                                         uint32_t* __restrict__ bflags) {
+    Node& node = sh.node;
+    uint16_t* win = sh.win;
+    HdSlot* slot = sh.slot;
+    int32_t& hthd = sh.hthd;
+    RState& hrs = sh.hrs;
+    int64_t* hmws = sh.hmws;
+    int64_t* hmpass = sh.hmpass;
+    double& hqps = sh.hqps;
     const uint32_t tid = threadIdx.x;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint32_t lane = tid & 63;
-    const Seg sg = segs[order[blockIdx.x]];
     const uint32_t res = sg.res;
-    const Prog pg = S.prog[res];
-    if (!(pg.xf & (RL ? XF_HEADR : XF_HEADT))) return;  // the cooperative owner's segment
     const double rcount = S.rules[pg.rule_off].count;
     const uint32_t rslot = S.rules[pg.rule_off].slot;
     const int32_t rmaxq = S.rules[pg.rule_off].max_queue;
@@ -183,9 +191,6 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
     // WarmUpRateLimiter: the owner syncs the stored tokens at the first ENTRY of every second; previousPassQps is the
     // minute bucket of the second before as the kernel started (its (ws, pass) in LDS) plus this kernel's passes in it
     const bool warm = RL && S.rules[pg.rule_off].behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER;
-    __shared__ RState hrs;
-    __shared__ int64_t hmws[60], hmpass[60];
-    __shared__ double hqps;
     if (warm) {
         if (tid < 60) {
             hmws[tid] = C.minb[tid].ws;
@@ -216,7 +221,7 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
         for (uint32_t j = 0; j < nch + 2; ++j) {
             if (j < nch) {
                 const uint32_t base = j * HD_CH;
-                HdSlot<RL>& so = slot[j % 3];
+                HdSlot& so = slot[j % 3];
                 uint32_t mk[HD_NM] = {0, 0, 0, 0, 0, 0, 0};
                 uint32_t og = 0, badm = 0;
                 uint32_t rref[8];
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
             if (j >= 1 && j <= nch) {
                 const unsigned long long tr0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
                 const uint32_t q = j - 1, base = q * HD_CH;
-                HdSlot<RL>& so = slot[q % 3];
+                HdSlot& so = slot[q % 3];
                 const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
                 const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
                 const uint32_t xs = so.m[0][HM_XS][lane] | so.m[1][HM_XS][lane];
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
         for (uint32_t j = 0; j < nch + 2; ++j) {
             if (j >= 2) {
                 const uint32_t q = j - 2, base = q * HD_CH;
-                HdSlot<RL>& so = slot[q % 3];
+                HdSlot& so = slot[q % 3];
                 const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
                 const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
                 const uint32_t tk = so.m[0][HM_T][lane] | so.m[1][HM_T][lane];
@@ -694,11 +699,23 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
     }
 }
 
+// one launch for both kinds (a bin's THREAD-grade and rate-limiter heads run side by side)
+__global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+                                              const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
+                                              int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
+    __shared__ HdShared sh;
+    if (blockIdx.x >= m) return;
+    const Seg sg = segs[order[blockIdx.x]];
+    const Prog pg = S.prog[sg.res];
+    if (pg.xf & XF_HEADT) head_seg<false>(sh, recs, sg, pg, S, cfg, t0, dec, bflags);
+    else if (pg.xf & XF_HEADR) head_seg<true>(sh, recs, sg, pg, S, cfg, t0, dec, bflags);
+    // (else: the cooperative owner's segment)
+}
+
 hipError_t launch_head(const SEv* recs, const Seg* segs, const uint32_t* order, uint32_t m, const DevState& S,
                        const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
-    hipLaunchKernelGGL(k_head<false>, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
-    hipLaunchKernelGGL(k_head<true>, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_head, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
     return hipGetLastError();
 }
 
