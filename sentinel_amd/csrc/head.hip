@@ -132,11 +132,12 @@ __device__ __forceinline__ int64_t hd_shr64(int64_t v, int64_t ident) {  // the 
 
 // one chunk's decoded inputs in LDS, [field][owner lane] (a lane's words in its own bank); three in flight: the
 // decoders fill chunk j while the owner decides chunk j - 1 and the statistics wave closes chunk j - 2
+#define HD_ND 4u  // decoder waves (four positions of each owner lane apiece)
 enum { HM_E = 0, HM_X, HM_T, HM_XS, HM_XD, HM_C1, HM_V, HD_NM };  // ENTRY / EXIT / TRACE kinds, effective (known),
                                                                    // effective iff the ENTRY at ref passed, acquire
                                                                    // != 1, valid
 struct HdSlot {
-    uint32_t m[2][HD_NM][64];  // [decoder half][mask][owner lane]: bits of the lane's 16 positions
+    uint16_t m[HD_ND][HD_NM][64];  // [decoder][mask][owner lane]: bits of the lane's 16 positions
     uint32_t ref[HD_EP][64];
     uint32_t cz[HD_EP][64];
     int32_t dt[HD_EP][64];
@@ -150,12 +151,19 @@ struct HdShared {
     RState hrs;                // WarmUpRateLimiter: storedTokens / lastFilledTime as the owner syncs them
     int64_t hmws[60], hmpass[60];
     double hqps;
+    unsigned long long tbusy[2];  // diagnostics: a decoder's and the statistics wave's busy cycles
 };
+__device__ __forceinline__ uint32_t hd_mask(const HdSlot& so, int q, uint32_t lane) {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t h = 0; h < HD_ND; ++h) v |= so.m[h][q][lane];
+    return v;
+}
 __device__ __forceinline__ void hd_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// A workgroup of four waves per head segment, pipelined over its chunks: waves 1 and 2 decode chunk j (eight
-// positions of each owner lane apiece), wave 0 -- the owner -- decides chunk j - 1 (the guess-and-verify rounds), wave
-// 3 writes chunk j - 2's verdict words and folds its statistics; one LDS barrier a step.  EXIT references into the
+// A workgroup of seven waves per head segment, pipelined over its chunks: waves 1-4 decode chunk j (four positions of
+// each owner lane apiece), wave 0 -- the owner -- decides chunk j - 1 (the guess-and-verify rounds), wave 5 writes
+// chunk j - 2's verdict words and wave 6 folds its statistics; one LDS barrier a step.  EXIT references into the
 // chunk being decided or the one before it are resolved by the owner (their verdicts are not final when decoded).
 template <bool RL>
 __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ recs, const Seg& sg, const Prog& pg,
@@ -179,7 +187,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
     if (tid == 0) node_load(node, S, res);
     __syncthreads();
     if (!(node.flags & NI_CHAIN)) {  // no slot chain: every ENTRY is NO_CHECK, nothing is counted
-        for (uint32_t p = tid; p < sg.len; p += 256)
+        for (uint32_t p = tid; p < sg.len; p += blockDim.x)
             dec[sg.start + p] = recs[sg.start + p].kind == SG_EV_ENTRY ? mk_dec(ST_NO_CHECK, 0, 0) : mk_dec(ST_NOT_ENTRY, 0, 0);
         return;
     }
@@ -205,28 +213,31 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
     const uint32_t nch = (sg.len + HD_CH - 1) / HD_CH;
     const uint32_t lp0 = lane * HD_EP;
 
-    if (wv == 1 || wv == 2) {
+    if (wv >= 1 && wv <= HD_ND) {
         // ================= decoders: positions [8h, 8h + 8) of owner lane `lane`, one chunk a step
-        const uint32_t h = wv - 1, e0 = h * 8;
-        uint4 nxt[8];
+        const uint32_t h = wv - 1, e0 = h * (HD_EP / HD_ND);
+        constexpr uint32_t NE = HD_EP / HD_ND;
+        uint4 nxt[NE];
         auto load = [&](uint32_t base) {
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
+            for (uint32_t k = 0; k < NE; ++k) {
                 const uint32_t p = base + lp0 + e0 + k;
                 nxt[k] = make_uint4(0u, 0u, 0u, 0xFFu);
                 if (p < sg.len) nxt[k] = reinterpret_cast<const uint4*>(recs + sg.start)[p];
             }
         };
         load(0);
+        unsigned long long tbusy = 0;
         for (uint32_t j = 0; j < nch + 2; ++j) {
             if (j < nch) {
+                const unsigned long long tb = prof ? __builtin_amdgcn_s_memtime() : 0ull;
                 const uint32_t base = j * HD_CH;
                 HdSlot& so = slot[j % 3];
                 uint32_t mk[HD_NM] = {0, 0, 0, 0, 0, 0, 0};
                 uint32_t og = 0, badm = 0;
-                uint32_t rref[8];
+                uint32_t rref[NE];
 #pragma unroll
-                for (uint32_t k = 0; k < 8; ++k) {
+                for (uint32_t k = 0; k < NE; ++k) {
                     const uint32_t e = e0 + k;
                     const uint4 w = nxt[k];
                     const uint32_t pos = base + lp0 + e;
@@ -257,17 +268,19 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 if (badm) atomicOr(bflags, BF_BAD_REF);
                 if (og) {  // older than the ring: the dec[] word (stored >= 120 chunks ago)
 #pragma unroll
-                    for (uint32_t k = 0; k < 8; ++k)
+                    for (uint32_t k = 0; k < NE; ++k)
                         if ((og >> (e0 + k)) & 1)
                             if (st_passed(__hip_atomic_load(&dec[sg.start + rref[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu))
                                 mk[HM_XS] |= 1u << (e0 + k);
                 }
 #pragma unroll
-                for (int q = 0; q < HD_NM; ++q) so.m[h][q][lane] = mk[q];
+                for (int q = 0; q < HD_NM; ++q) so.m[h][q][lane] = (uint16_t)mk[q];
                 if (j + 1 < nch) load(base + HD_CH);
+                if (prof) tbusy += __builtin_amdgcn_s_memtime() - tb;
             }
             hd_lds_barrier();
         }
+        if (prof && h == 0 && lane == 0) sh.tbusy[0] = tbusy;
     } else if (wv == 0) {
         // ================= the owner: the guess-and-verify rounds of chunk j - 1
         const double cf = rcount != rcount ? 1e18 : floor(rcount);
@@ -288,27 +301,18 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 const unsigned long long tr0 = prof ? __builtin_amdgcn_s_memtime() : 0ull;
                 const uint32_t q = j - 1, base = q * HD_CH;
                 HdSlot& so = slot[q % 3];
-                const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
-                const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
-                const uint32_t xs = so.m[0][HM_XS][lane] | so.m[1][HM_XS][lane];
-                const uint32_t xd = so.m[0][HM_XD][lane] | so.m[1][HM_XD][lane];
-                const uint32_t c1 = so.m[0][HM_C1][lane] | so.m[1][HM_C1][lane];
-                int32_t dt[HD_EP];
-                uint32_t cz[HD_EP], ref[HD_EP];
-#pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) {
-                    dt[e] = so.dt[e][lane];
-                    cz[e] = so.cz[e][lane];
-                    ref[e] = so.ref[e][lane];
-                }
+                const uint32_t emask = hd_mask(so, HM_E, lane), xk = hd_mask(so, HM_X, lane);
+                const uint32_t xs = hd_mask(so, HM_XS, lane), xd = hd_mask(so, HM_XD, lane), c1 = hd_mask(so, HM_C1, lane);
+                // (the chunk's times, counts and references stay in LDS: read where a round needs them)
                 const uint32_t cnt_t = sg.len - base < HD_CH ? sg.len - base : HD_CH;
                 const uint32_t wi = ((base >> 4) + lane) & (HD_RW - 1);
                 const bool uni = __ballot(c1 != 0) == 0;  // every event of the chunk counts 1
                 uint32_t st = last_pass ? emask : 0u;      // committed verdicts below c0, the round's guesses above
                 win[wi] = (uint16_t)st;
-                uint32_t wq[HD_EP];
+                if (RL) {
 #pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) wq[e] = 0;
+                    for (uint32_t e = 0; e < HD_EP; ++e) so.wq[e][lane] = 0;
+                }
                 uint32_t c0 = 0;
         while (c0 < cnt_t) {
             ++n_round;
@@ -323,7 +327,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     const uint32_t fe = (uint32_t)__ffs(__builtin_amdgcn_readlane((int)ae, fl)) - 1;
                     int32_t fdt = 0;
 #pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dt[e] : fdt;
+                    for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? so.dt[e][lane] : fdt;
                     const int64_t tn = t0 + __builtin_amdgcn_readlane(fdt, fl);
                     const int64_t T = tn - tn % 1000;
                     if (T != ksec) {
@@ -342,7 +346,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     const int32_t sei = se > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)se;
                     uint32_t after = 0;  // the lane's active positions at or past it
 #pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) after |= (uint32_t)(dt[e] >= sei) << e;
+                    for (uint32_t e = 0; e < HD_EP; ++e) after |= (uint32_t)(so.dt[e][lane] >= sei) << e;
                     after &= amask;
                     const uint64_t ab = __ballot(after != 0);
                     if (ab) {
@@ -365,7 +369,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 uint32_t dg = 0;
                 if (dx) {
 #pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) dg |= (hd_bit(win, ref[e]) & (dx >> e)) << e;
+                    for (uint32_t e = 0; e < HD_EP; ++e) dg |= (hd_bit(win, so.ref[e][lane]) & (dx >> e)) << e;
                 }
                 const uint32_t xm = (xs | dg) & xk & amask;
                 const uint32_t xl = (uint32_t)__popc(xm);
@@ -378,7 +382,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const int32_t a = (int32_t)((am >> e) & 1);
-                        int32_t u = bu - (int32_t)(cz[e] & 0xFFFFu) + X;
+                        int32_t u = bu - (int32_t)(so.cz[e][lane] & 0xFFFFu) + X;
                         u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
                         const int32_t nb = B + 1 < u ? B + 1 : u;
                         B = a ? nb : B;
@@ -396,7 +400,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const bool a = (am >> e) & 1;
-                        int32_t u = bu - (int32_t)(cz[e] & 0xFFFFu) + X;
+                        int32_t u = bu - (int32_t)(so.cz[e][lane] & 0xFFFFu) + X;
                         u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
                         const int32_t Pn = a ? (P + 1 < u ? P + 1 : u) : P;
                         gm |= (uint32_t)(Pn > P) << e;
@@ -416,7 +420,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const bool a = (am >> e) & 1, g = (gm >> e) & 1;
                         const int32_t ci = c + Pc - Xc;
-                        const bool tr = !((double)j_iadd(ci, (int32_t)(cz[e] & 0xFFFFu)) > rcount);
+                        const bool tr = !((double)j_iadd(ci, (int32_t)(so.cz[e][lane] & 0xFFFFu)) > rcount);
                         mm |= (uint32_t)(a && tr != g) << e;
                         tm |= (uint32_t)(a && tr) << e;
                         Pc += g ? 1 : 0;
@@ -428,7 +432,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 if (dx) {  // same-chunk EXITs: effective iff their ENTRY's new guess passes
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) {
-                        const uint32_t now = hd_bit(win, ref[e]), d = (dx >> e) & 1, was = (xm >> e) & 1;
+                        const uint32_t now = hd_bit(win, so.ref[e][lane]), d = (dx >> e) & 1, was = (xm >> e) & 1;
                         mm |= (d & (now ^ was)) << e;
                         tm |= (d & now) << e;
                     }
@@ -445,7 +449,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 const bool lattice = !last_pass && cost1 > 0;
                 uint32_t lastt = 0;  // the lane's last active ENTRY time (+ 2^31 + 1; 0 none)
 #pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) lastt = ((am >> e) & 1) ? (uint32_t)dt[e] + 0x80000001u : lastt;
+                for (uint32_t e = 0; e < HD_EP; ++e) lastt = ((am >> e) & 1) ? (uint32_t)so.dt[e][lane] + 0x80000001u : lastt;
                 const uint32_t tin = hd_max_scan(lastt);
                 uint32_t tpv = (uint32_t)HD_DPP(0, tin, 0x138, 0xf);
                 tpv = lane == 0 ? 0u : tpv;
@@ -456,14 +460,14 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e) {
                     const bool a = (am >> e) & 1;
-                    const uint32_t cnt = cz[e] & 0xFFFFu;
-                    const double k = floor(((double)dt[e] - Lq) * inv1);
+                    const uint32_t cnt = so.cz[e][lane] & 0xFFFFu;
+                    const double k = floor(((double)so.dt[e][lane] - Lq) * inv1);
                     const bool g = a && (cnt == 0 || (cpos && (!lattice || k > kp)));
                     kp = (a && k > kp) ? k : kp;
                     gm |= (uint32_t)g << e;
                     const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
                     const bool up = g && (warm || (cnt > 0 && cpos));
-                    const int64_t nb = B + cs > (int64_t)dt[e] ? B + cs : (int64_t)dt[e];
+                    const int64_t nb = B + cs > (int64_t)so.dt[e][lane] ? B + cs : (int64_t)so.dt[e][lane];
                     B = up ? nb : B;
                     A += up ? cs : 0;
                 }
@@ -476,15 +480,15 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e) {
                     const bool a = (am >> e) & 1, g = (gm >> e) & 1;
-                    const uint32_t cnt = cz[e] & 0xFFFFu;
-                    const int64_t t = dt[e];
+                    const uint32_t cnt = so.cz[e][lane] & 0xFFFFu;
+                    const int64_t t = so.dt[e][lane];
                     const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
                     const bool up = warm || (cnt > 0 && cpos);  // (WarmUpRateLimiter: acquire 0 is a check of cost 0)
                     const bool tr = (!warm && cnt == 0) || (cpos && ((Lc + cs <= t) || (Lc + cs - t <= Q)));
                     const int64_t Ln = Lc + cs > t ? Lc + cs : t;
                     const int64_t wv = Lc + cs - t;
                     const uint32_t w = (tr && up && wv > 0) ? (wv > 0xFFFF ? 0xFFFFu : (uint32_t)wv) : 0u;
-                    wq[e] = a ? w : wq[e];
+                    if (a) so.wq[e][lane] = w;
                     const bool mis = a && tr != g;
                     mstate = (mis && !mm) ? ((tr && up) ? Ln : Lc) : mstate;
                     mm |= (uint32_t)mis << e;
@@ -529,15 +533,11 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 const uint32_t pm = am & cm & st;
                 uint32_t sp = 0;
 #pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (cz[e] & 0xFFFFu) : 0u;
+                for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (so.cz[e][lane] & 0xFFFFu) : 0u;
                 kcur += hd_sum_red(sp);
             }
             c0 = cend;
         }
-                if (RL) {
-#pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) so.wq[e][lane] = wq[e];
-                }
                 if (prof) tround += __builtin_amdgcn_s_memtime() - tr0;
             }
             hd_lds_barrier();
@@ -559,13 +559,32 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     S.dbg[61] = nch;
                     S.dbg[62] = n_round;
                     S.dbg[30] = tround;
+                    S.dbg[44] = sh.tbusy[0];
+                    S.dbg[45] = sh.tbusy[1];
                     S.dbg[31] = (unsigned long long)rcount;
                 }
             }
         }
-    } else {
-        // ================= wave 3: chunk j - 2's verdict words and statistics (per 500 ms bucket, k_jac round_fold)
+    } else if (wv == HD_ND + 1) {
+        // ================= chunk j - 2's verdict words
         const uint32_t dblock = mk_dec(ST_BLOCK_FLOW, rslot, 0), dnot = mk_dec(ST_NOT_ENTRY, 0, 0);
+        for (uint32_t j = 0; j < nch + 2; ++j) {
+            if (j >= 2) {
+                const uint32_t q = j - 2, base = q * HD_CH;
+                const HdSlot& so = slot[q % 3];
+                const uint32_t emask = hd_mask(so, HM_E, lane), vmask = hd_mask(so, HM_V, lane);
+                const uint32_t st = win[((base >> 4) + lane) & (HD_RW - 1)];
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e) {
+                    const uint32_t d = ((emask >> e) & 1) ? (((st >> e) & 1) ? mk_dec(ST_PASS, 0, RL ? (int64_t)so.wq[e][lane] : 0) : dblock) : dnot;
+                    if ((vmask >> e) & 1) dec[sg.start + base + lp0 + e] = d;
+                }
+                if ((q & 31u) == 31u) __threadfence_block();  // (old references read the dec[] words)
+            }
+            hd_lds_barrier();
+        }
+    } else if (wv == HD_ND + 2) {
+        // ================= chunk j - 2's statistics (per 500 ms bucket, as k_jac's round_fold)
         const int32_t toff = (int32_t)(((t0 % 500) + 500) % 500);
         const int64_t tb0 = (t0 - toff) / 500;  // bucket of relative time -toff
         int64_t cb = -1;                        // the bucket being collected (uniform); per-lane sums
@@ -584,28 +603,21 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
             aMin = HD_NONE;
             aT = 0;
         };
+        unsigned long long tbusy = 0;
         for (uint32_t j = 0; j < nch + 2; ++j) {
             if (j >= 2) {
+                const unsigned long long tb = prof ? __builtin_amdgcn_s_memtime() : 0ull;
                 const uint32_t q = j - 2, base = q * HD_CH;
                 HdSlot& so = slot[q % 3];
-                const uint32_t emask = so.m[0][HM_E][lane] | so.m[1][HM_E][lane];
-                const uint32_t xk = so.m[0][HM_X][lane] | so.m[1][HM_X][lane];
-                const uint32_t tk = so.m[0][HM_T][lane] | so.m[1][HM_T][lane];
-                const uint32_t xd = so.m[0][HM_XD][lane] | so.m[1][HM_XD][lane];
-                const uint32_t c1 = so.m[0][HM_C1][lane] | so.m[1][HM_C1][lane];
-                const uint32_t vmask = so.m[0][HM_V][lane] | so.m[1][HM_V][lane];
-                uint32_t xe = so.m[0][HM_XS][lane] | so.m[1][HM_XS][lane];
+                const uint32_t emask = hd_mask(so, HM_E, lane), xk = hd_mask(so, HM_X, lane), tk = hd_mask(so, HM_T, lane);
+                const uint32_t xd = hd_mask(so, HM_XD, lane), c1 = hd_mask(so, HM_C1, lane), vmask = hd_mask(so, HM_V, lane);
+                uint32_t xe = hd_mask(so, HM_XS, lane);
                 const uint32_t st = win[((base >> 4) + lane) & (HD_RW - 1)];
                 if (xd) {
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) xe |= (hd_bit(win, so.ref[e][lane]) & (xd >> e)) << e;
                 }
                 xe &= xk | tk;
-#pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) {
-                    const uint32_t d = ((emask >> e) & 1) ? (((st >> e) & 1) ? mk_dec(ST_PASS, 0, RL ? (int64_t)so.wq[e][lane] : 0) : dblock) : dnot;
-                    if ((vmask >> e) & 1) dec[sg.start + base + lp0 + e] = d;
-                }
                 if (RL) thd += (int32_t)hd_sum_red((uint32_t)(__popc(emask & st) - __popc(xe & xk)));
                 int32_t dt[HD_EP];
                 uint32_t cz[HD_EP];
@@ -692,15 +704,16 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     fold();
                     if (lane == 0) hthd = thd;
                 }
-                if ((q & 31u) == 31u) __threadfence_block();  // (old references read the dec[] words)
+                if (prof) tbusy += __builtin_amdgcn_s_memtime() - tb;
             }
             hd_lds_barrier();
         }
+        if (prof && lane == 0) sh.tbusy[1] = tbusy;
     }
 }
 
 // one launch for both kinds (a bin's THREAD-grade and rate-limiter heads run side by side)
-__global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
+__global__ __launch_bounds__(64 * (HD_ND + 3)) void k_head(const SEv* __restrict__ recs, const Seg* __restrict__ segs,
                                               const uint32_t* __restrict__ order, uint32_t m, DevState S, DevCfg cfg,
                                               int64_t t0, uint32_t* __restrict__ dec, uint32_t* __restrict__ bflags) {
     __shared__ HdShared sh;
@@ -715,7 +728,7 @@ __global__ __launch_bounds__(256) void k_head(const SEv* __restrict__ recs, cons
 hipError_t launch_head(const SEv* recs, const Seg* segs, const uint32_t* order, uint32_t m, const DevState& S,
                        const DevCfg& cfg, int64_t t0, uint32_t* dec, uint32_t* bflags, hipStream_t st) {
     if (!m) return hipSuccess;
-    hipLaunchKernelGGL(k_head, dim3(m), dim3(256), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
+    hipLaunchKernelGGL(k_head, dim3(m), dim3(64 * (HD_ND + 3)), 0, st, recs, segs, order, m, S, cfg, t0, dec, bflags);
     return hipGetLastError();
 }
 

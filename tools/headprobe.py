@@ -33,6 +33,6 @@ for i in range(nb):
     L.sgx_debug_counters(eng.h, buf, 64)
     v = np.array(list(buf), dtype=np.uint64)
     print("batch %d: wall %.1f ms decide %.2f ms | slowest head: len %d chunks %d rounds %d folds %d cycles %d "
-          "(rounds %d, decode %d, rounds+stores %d) count %d" % (i, (time.time() - t) * 1e3, tm[1], v[60], v[61], v[62], v[63],
+          "(owner rounds %d, a decoder %d, statistics %d) count %d" % (i, (time.time() - t) * 1e3, tm[1], v[60], v[61], v[62], v[63],
                                                               v[59], v[30], v[44], v[45], v[31]),
           flush=True)
