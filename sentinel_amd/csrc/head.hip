@@ -286,7 +286,6 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
         const double cf = rcount != rcount ? 1e18 : floor(rcount);
         const int32_t Flc = cf > (double)(1 << 29) ? (1 << 29) : cf < -(double)(1 << 29) ? -(1 << 29) : (int32_t)cf;
         int64_t cost1 = (rcount <= 0) ? 0 : j_round(1.0 / rcount * 1000);
-        double inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
         double qps = rcount;  // the QPS the cost of acquire n follows (WarmUpRateLimiter: per second)
         int64_t ksec = INT64_MIN, kcur = 0;  // the second being decided and this kernel's passes in it (uniform)
         const int64_t Q = rmaxq;
@@ -303,10 +302,32 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 HdSlot& so = slot[q % 3];
                 const uint32_t emask = hd_mask(so, HM_E, lane), xk = hd_mask(so, HM_X, lane);
                 const uint32_t xs = hd_mask(so, HM_XS, lane), xd = hd_mask(so, HM_XD, lane), c1 = hd_mask(so, HM_C1, lane);
-                // (the chunk's times, counts and references stay in LDS: read where a round needs them)
                 const uint32_t cnt_t = sg.len - base < HD_CH ? sg.len - base : HD_CH;
                 const uint32_t wi = ((base >> 4) + lane) & (HD_RW - 1);
                 const bool uni = __ballot(c1 != 0) == 0;  // every event of the chunk counts 1
+                // the chunk's times and counts in registers (a round reads them several times; the references stay in
+                // LDS, read for the same-chunk EXITs only)
+                int32_t dtr[HD_EP];
+                uint32_t czr[HD_EP];
+                if (RL) {
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        dtr[e] = so.dt[e][lane];
+                        czr[e] = so.cz[e][lane];
+                    }
+                } else if (!uni) {
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        dtr[e] = 0;
+                        czr[e] = so.cz[e][lane];
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        dtr[e] = 0;
+                        czr[e] = 1u;
+                    }
+                }
                 uint32_t st = last_pass ? emask : 0u;      // committed verdicts below c0, the round's guesses above
                 win[wi] = (uint16_t)st;
                 if (RL) {
@@ -327,7 +348,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     const uint32_t fe = (uint32_t)__ffs(__builtin_amdgcn_readlane((int)ae, fl)) - 1;
                     int32_t fdt = 0;
 #pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? so.dt[e][lane] : fdt;
+                    for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dtr[e] : fdt;
                     const int64_t tn = t0 + __builtin_amdgcn_readlane(fdt, fl);
                     const int64_t T = tn - tn % 1000;
                     if (T != ksec) {
@@ -338,7 +359,6 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                         __builtin_amdgcn_wave_barrier();  // (one wave: its LDS write lands before its reads)
                         qps = hqps;
                         cost1 = j_round(1.0 / qps * 1000);
-                        inv1 = cost1 > 0 ? 1.0 / (double)cost1 : 0.0;
                         ksec = T;
                         kcur = 0;
                     }
@@ -346,7 +366,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     const int32_t sei = se > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)se;
                     uint32_t after = 0;  // the lane's active positions at or past it
 #pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) after |= (uint32_t)(so.dt[e][lane] >= sei) << e;
+                    for (uint32_t e = 0; e < HD_EP; ++e) after |= (uint32_t)(dtr[e] >= sei) << e;
                     after &= amask;
                     const uint64_t ab = __ballot(after != 0);
                     if (ab) {
@@ -382,7 +402,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const int32_t a = (int32_t)((am >> e) & 1);
-                        int32_t u = bu - (int32_t)(so.cz[e][lane] & 0xFFFFu) + X;
+                        int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
                         u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
                         const int32_t nb = B + 1 < u ? B + 1 : u;
                         B = a ? nb : B;
@@ -400,7 +420,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const bool a = (am >> e) & 1;
-                        int32_t u = bu - (int32_t)(so.cz[e][lane] & 0xFFFFu) + X;
+                        int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
                         u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
                         const int32_t Pn = a ? (P + 1 < u ? P + 1 : u) : P;
                         gm |= (uint32_t)(Pn > P) << e;
@@ -420,7 +440,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     for (uint32_t e = 0; e < HD_EP; ++e) {
                         const bool a = (am >> e) & 1, g = (gm >> e) & 1;
                         const int32_t ci = c + Pc - Xc;
-                        const bool tr = !((double)j_iadd(ci, (int32_t)(so.cz[e][lane] & 0xFFFFu)) > rcount);
+                        const bool tr = !((double)j_iadd(ci, (int32_t)(czr[e] & 0xFFFFu)) > rcount);
                         mm |= (uint32_t)(a && tr != g) << e;
                         tm |= (uint32_t)(a && tr) << e;
                         Pc += g ? 1 : 0;
@@ -445,29 +465,77 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 }
                 endstate = (int64_t)c + (int32_t)gin - (int32_t)xin;
             } else {
-                // RATE: the round's guesses -- all pass after a pass; after a block the saturated lattice
-                const bool lattice = !last_pass && cost1 > 0;
-                uint32_t lastt = 0;  // the lane's last active ENTRY time (+ 2^31 + 1; 0 none)
+                // RATE: the round's guesses.  Queueing (L + cost after the first active ENTRY's arrival): the saturated
+                // lattice -- the n-th pass of the round is the first ENTRY at or after L + n * cost - maxQueue while each
+                // pass moves L by exactly cost, i.e. P_{i+1} = min(P_i + 1, k(t_i)) with k(t) the lattice points up to t:
+                // the (min, +) scan of the THREAD owner.  Idle (L + cost at or before it): every ENTRY passes.
+                uint32_t tf = 0x7FFFFFFFu;
+                {
+                    const uint64_t eb = __ballot(am != 0);
+                    if (eb) {
+                        const uint32_t fl = (uint32_t)__ffsll((long long)eb) - 1;
+                        const uint32_t fe = (uint32_t)__ffs(__builtin_amdgcn_readlane((int)am, fl)) - 1;
+                        int32_t fdt = 0;
 #pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) lastt = ((am >> e) & 1) ? (uint32_t)so.dt[e][lane] + 0x80000001u : lastt;
-                const uint32_t tin = hd_max_scan(lastt);
-                uint32_t tpv = (uint32_t)HD_DPP(0, tin, 0x138, 0xf);
-                tpv = lane == 0 ? 0u : tpv;
-                const double Lq = (double)(L - Q) - 0.5;  // lattice index of t: floor((t - L + Q + 0.5) / cost)
-                double kp = tpv ? floor(((double)(int32_t)(tpv - 0x80000001u) - Lq) * inv1) : 0.0;
-                kp = kp > 0.0 ? kp : 0.0;
+                        for (uint32_t e = 0; e < HD_EP; ++e) fdt = e == fe ? dtr[e] : fdt;
+                        tf = (uint32_t)__builtin_amdgcn_readlane(fdt, fl);
+                    }
+                }
+                const bool lattice = cost1 > 0 && cost1 < (1 << 24) && L + cost1 > (int64_t)(int32_t)tf;
+                // lattice points up to t: floor((t - (L - Q)) / cost), in 32-bit arithmetic (lattice: L is within a
+                // cost of the round's first arrival, so the offsets of the chunk's times fit; clamped regardless)
+                const int64_t lq64 = L - Q;
+                const int32_t lq = lq64 > (1 << 30) ? (1 << 30) : lq64 < -(1 << 30) ? -(1 << 30) : (int32_t)lq64;
+                const int32_t ci = (int32_t)cost1;
+                const float rc = 1.0f / (float)ci;
+                auto lat = [&](int32_t t) -> int32_t {  // max(0, floor((t - lq) / cost)), exact
+                    int32_t x = t - lq;
+                    x = x < 0 ? -1 : x > (1 << 30) ? (1 << 30) : x;
+                    int32_t k = (int32_t)((float)x * rc);
+                    k = k * ci > x ? k - 1 : k;
+                    k = (k + 1) * ci <= x ? k + 1 : k;
+                    return k < 0 ? 0 : k;
+                };
+                // the lattice ENTRYs: acquire > 0 (an acquire-0 ENTRY of a RateLimiter passes without moving L)
+                uint32_t lm = 0;
+#pragma unroll
+                for (uint32_t e = 0; e < HD_EP; ++e)
+                    lm |= (uint32_t)(((am >> e) & 1) && (warm || (czr[e] & 0xFFFFu) != 0)) << e;
+                uint32_t lg = 0;  // lattice guesses
+                if (lattice) {
+                    int32_t A2 = 0, B2 = HD_INF;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const int32_t u = lat(dtr[e]);
+                        const int32_t a2 = (int32_t)((lm >> e) & 1);
+                        const int32_t nb = B2 + 1 < u ? B2 + 1 : u;
+                        B2 = a2 ? nb : B2;
+                        A2 += a2;
+                    }
+                    int32_t ia2 = A2, ib2 = B2;
+                    hd_minplus_scan(ia2, ib2);
+                    int32_t pa2 = HD_DPP(0, ia2, 0x138, 0xf), pb2 = HD_DPP(HD_INF, ib2, 0x138, 0xf);
+                    pa2 = lane == 0 ? 0 : pa2;
+                    pb2 = lane == 0 ? HD_INF : pb2;
+                    int32_t P = pa2 < pb2 ? pa2 : pb2;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) {
+                        const int32_t u = lat(dtr[e]);
+                        const int32_t Pn = ((lm >> e) & 1) ? (P + 1 < u ? P + 1 : u) : P;
+                        lg |= (uint32_t)(Pn > P) << e;
+                        P = Pn;
+                    }
+                }
                 int64_t A = 0, B = HD_NEG;
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e) {
                     const bool a = (am >> e) & 1;
-                    const uint32_t cnt = so.cz[e][lane] & 0xFFFFu;
-                    const double k = floor(((double)so.dt[e][lane] - Lq) * inv1);
-                    const bool g = a && (cnt == 0 || (cpos && (!lattice || k > kp)));
-                    kp = (a && k > kp) ? k : kp;
+                    const uint32_t cnt = czr[e] & 0xFFFFu;
+                    const bool g = a && (cnt == 0 || (cpos && (!lattice || ((lg >> e) & 1))));
                     gm |= (uint32_t)g << e;
                     const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
                     const bool up = g && (warm || (cnt > 0 && cpos));
-                    const int64_t nb = B + cs > (int64_t)so.dt[e][lane] ? B + cs : (int64_t)so.dt[e][lane];
+                    const int64_t nb = B + cs > (int64_t)dtr[e] ? B + cs : (int64_t)dtr[e];
                     B = up ? nb : B;
                     A += up ? cs : 0;
                 }
@@ -480,8 +548,8 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e) {
                     const bool a = (am >> e) & 1, g = (gm >> e) & 1;
-                    const uint32_t cnt = so.cz[e][lane] & 0xFFFFu;
-                    const int64_t t = so.dt[e][lane];
+                    const uint32_t cnt = czr[e] & 0xFFFFu;
+                    const int64_t t = dtr[e];
                     const int64_t cs = uni ? cost1 : hd_cost(qps, cnt, cost1);
                     const bool up = warm || (cnt > 0 && cpos);  // (WarmUpRateLimiter: acquire 0 is a check of cost 0)
                     const bool tr = (!warm && cnt == 0) || (cpos && ((Lc + cs <= t) || (Lc + cs - t <= Q)));
@@ -533,7 +601,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 const uint32_t pm = am & cm & st;
                 uint32_t sp = 0;
 #pragma unroll
-                for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (so.cz[e][lane] & 0xFFFFu) : 0u;
+                for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (czr[e] & 0xFFFFu) : 0u;
                 kcur += hd_sum_red(sp);
             }
             c0 = cend;
