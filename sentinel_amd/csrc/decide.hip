@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
                                                  uint32_t* __restrict__ ashort, uint64_t* __restrict__ along,
                                                  uint64_t* __restrict__ amulti, uint32_t* __restrict__ mixc,
                                                  uint32_t* __restrict__ mix, uint32_t mix_cap,
-                                                 uint32_t* __restrict__ mixlen, uint32_t mix_wide) {
+                                                 uint32_t* __restrict__ mixlen, uint32_t mix_wide, uint32_t head_min) {
     __shared__ uint32_t cnt[N_BINS];
     for (uint32_t b = threadIdx.x; b < N_BINS; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
@@ -191,7 +191,9 @@ __global__ __launch_bounds__(256) void k_seg_bin(Seg* __restrict__ segs, const u
         const int nr = p.multi ? 16 : p.n_param + p.n_flow + p.n_degrade;  // PX_*: decided with 16-rule lanes
         // XF_MIX: the param checks run in k_pq's pre pass (args[0] from the key ring: no argument lists)
         const bool mixp = (p.xf & XF_MIX) && pq && mix && !(pm & PM_ARGL);
-        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && (p.n_param == 0 || mixp) && sg.len > lane_max &&
+        // single-rule THREAD-grade / rate-limiter heads (head.hip k_head) leave the lane bins from head_min events on
+        const uint32_t cmin = (head_min && (p.xf & (XF_HEADT | XF_HEADR)) && head_min < lane_max) ? head_min : lane_max;
+        const bool coop = !force_lane && !(p.pflags & PF_SERIAL) && (p.n_param == 0 || mixp) && sg.len > cmin &&
                           !lane_only && !p.multi;
         if (coop && p.n_param) mixk = sg.len > mix_wide ? 2u : 1u;  // (wide: pvalue.hip's passes, where on)
         if (mixk == 2 && mixlen) atomicAdd(mixlen, sg.len);  // (pvalue.hip's scratch bound)
@@ -4013,11 +4015,12 @@ hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
-                          uint32_t mix_wide, hipStream_t st) {
+                          uint32_t mix_wide, uint32_t head_min, hipStream_t st) {
     const uint32_t nblk = (mb + 255) / 256;
     if (!nblk) return hipSuccess;
     hipLaunchKernelGGL(k_seg_bin, dim3(nblk), dim3(256), 0, st, segs, mp, n, prog, prio, lane_max, j1_max, j4_max, force_lane,
-                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap, mixlen, mix_wide);
+                       blkcnt, nblk, pq_ok, pq_wide, aux, ashort, along, amulti, mixc, mix, mix_cap, mixlen, mix_wide,
+                       head_min);
     return hipGetLastError();
 }
 // off = exclusive scan of blkcnt (bin-major); writes the per-bin offsets to bin_off[0..N_BINS]

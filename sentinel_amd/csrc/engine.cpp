@@ -84,7 +84,7 @@ hipError_t launch_seg_bin(Seg* segs, const uint32_t* mp, uint32_t mb, uint64_t n
                           uint32_t lane_max, uint32_t j1_max, uint32_t j4_max, uint32_t force_lane, uint32_t* blkcnt,
                           uint32_t pq_ok, uint32_t pq_wide, uint32_t* aux, uint32_t* ashort, uint64_t* along,
                           uint64_t* amulti, uint32_t* mixc, uint32_t* mix, uint32_t mix_cap, uint32_t* mixlen,
-                          uint32_t mix_wide,
+                          uint32_t mix_wide, uint32_t head_min,
                           hipStream_t st);
 // aux.hip
 hipError_t launch_aux(const SEv* recs, const Seg* segs, const uint32_t* aux, const uint32_t* ashort,
@@ -662,6 +662,9 @@ struct sg_engine {
     int j1_stream = -1;     // SG_J1_STREAM=1 / 0: J1 after J16 / J8 on bin_stream[0] / after the lane bins (default:
                             // bin_stream[0] when the short aux nodes take the main stream, else the main stream)
     uint32_t lane_max = 256, j1_max = 4096, j4_max = 65536;
+    uint32_t head_min = 0;       // SG_HEAD_MIN: single-rule THREAD / rate-limiter head segments longer than this leave
+                                 // the lane bins for the event-driven head owner (0: the lane bins keep up to lane_max;
+                                 // C3 A/B: 64 -> 1.15, 128 -> 1.27, 0 -> 1.27 G entries/s)
     bool bins_pinned = false;  // SG_LANE_MAX / SG_J1_MAX / SG_J4_MAX set: no per-batch adaptation
     uint32_t skip_min = 32768;  // frozen stretches shorter than this (x NW/16) are streamed, not skipped
     bool pq_on = true;          // PF_PQ segments to k_pq (SG_PQ=0: the per-lane kernel, as before round 3)
@@ -1313,6 +1316,7 @@ int sg_engine_create(const sg_config* cfg_in, sg_engine** out) {
     // decide-bin thresholds (segment lengths); tuning knobs, the defaults are the measured best
     if (const char* v = std::getenv("SG_LANE_MAX")) { e->lane_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_J1_MAX")) { e->j1_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
+    if (const char* v = std::getenv("SG_HEAD_MIN")) e->head_min = (uint32_t)std::strtoul(v, nullptr, 0);
     if (const char* v = std::getenv("SG_J4_MAX")) { e->j4_max = (uint32_t)std::strtoul(v, nullptr, 0); e->bins_pinned = true; }
     if (const char* v = std::getenv("SG_PIPELINE")) e->pipeline = v[0] == '1';
     if (const char* v = std::getenv("SG_TINY")) e->tiny_on = v[0] != '0';
@@ -2391,7 +2395,8 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     HIPCHK(launch_seg_bin(e->d_segs, e->d_bsmall + 1, mb, n, e->d_prog, e->d_prio, lane_max, j1_max, j4_max,
                           force_lane ? 1 : 0, e->d_blkcnt, e->pq_on ? 1u : 0u, e->pq_wide, ext ? e->d_bsmall + 130 : nullptr,
                           B.d_ashort, B.d_along, B.d_amulti, e->d_bsmall + 6, e->has_mix ? B.d_mix : nullptr,
-                          (uint32_t)B.mix_cap, e->d_bsmall + 72, (e->pv_on || e->pvt_on) ? 0u : e->pq_wide, gs));
+                          (uint32_t)B.mix_cap, e->d_bsmall + 72, (e->pv_on || e->pvt_on) ? 0u : e->pq_wide,
+                          (e->dbg_flags & HEAD_OFF) ? 0u : e->head_min, gs));
     HIPCHK(launch_scan(e->d_blkcnt, e->d_blkcnt, (uint64_t)nblk * N_BINS, e->d_part, nullptr, gs));
     HIPCHK(launch_seg_order(e->d_segs, e->d_bsmall + 1, mb, e->d_blkcnt, e->d_order, e->d_bsmall + 8, gs));
     // the next batch's hot ids: this batch's resources of >= n / 8192 events (about one per 4096-event tile, so
