@@ -294,6 +294,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
         int64_t L = RL ? S.rstate[pg.rule_off].c - t0 : 0;  // RATE: latestPassedTime relative to t0 (uniform)
         bool last_pass = true;                              // the last decided ENTRY passed (round guesses)
         uint32_t n_round = 0;
+        unsigned long long ph[4] = {0, 0, 0, 0};  // diagnostics: the owner's round phases
         unsigned long long tround = 0;
         for (uint32_t j = 0; j < nch + 2; ++j) {
             if (j >= 1 && j <= nch) {
@@ -340,6 +341,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
             const uint32_t lo = c0 > lp0 ? (c0 - lp0 < HD_EP ? c0 - lp0 : HD_EP) : 0u;
             uint32_t amask = lo >= HD_EP ? 0u : (0xFFFFu << lo) & 0xFFFFu;  // the lane's active positions
             uint32_t act_end = cnt_t;                                         // the round's active range ends here
+            unsigned long long pt = prof ? __builtin_amdgcn_s_memtime() : 0ull;
             if (warm) {  // a round stays in the second of its first ENTRY (the cost is fixed there)
                 const uint32_t ae = amask & emask;
                 const uint64_t eb = __ballot(ae != 0);
@@ -377,6 +379,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     amask &= (1u << le) - 1u;
                 }
             }
+            if (prof) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); ph[0] += _n - pt; pt = _n; }
             const uint32_t am = amask & emask;                                      // ... its active ENTRYs
             uint32_t gm = 0;        // the round's guesses: ENTRYs that pass
             uint32_t mm = 0;        // events whose evaluation differs from the guess
@@ -526,6 +529,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                         P = Pn;
                     }
                 }
+                if (prof) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); ph[1] += _n - pt; pt = _n; }
                 int64_t A = 0, B = HD_NEG;
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e) {
@@ -566,6 +570,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 endstate = Lc;
                 st = (st & ~amask) | gm;
             }
+            if (prof) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); ph[2] += _n - pt; pt = _n; }
             // the wave's first mismatch (lanes in position order): it takes its evaluated outcome, everything before
             // it stands, positions after it keep the round's guesses for the next round
             const uint64_t bal = __ballot(mm != 0);
@@ -604,6 +609,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 for (uint32_t e = 0; e < HD_EP; ++e) sp += ((pm >> e) & 1) ? (czr[e] & 0xFFFFu) : 0u;
                 kcur += hd_sum_red(sp);
             }
+            if (prof) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); ph[3] += _n - pt; pt = _n; }
             c0 = cend;
         }
                 if (prof) tround += __builtin_amdgcn_s_memtime() - tr0;
@@ -630,6 +636,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                     S.dbg[44] = sh.tbusy[0];
                     S.dbg[45] = sh.tbusy[1];
                     S.dbg[31] = (unsigned long long)rcount;
+                    S.dbg[46] = ph[0]; S.dbg[47] = ph[1]; S.dbg[48] = ph[2]; S.dbg[49] = ph[3];
                 }
             }
         }

@@ -35,4 +35,5 @@ for i in range(nb):
     print("batch %d: wall %.1f ms decide %.2f ms | slowest head: len %d chunks %d rounds %d folds %d cycles %d "
           "(owner rounds %d, a decoder %d, statistics %d) count %d" % (i, (time.time() - t) * 1e3, tm[1], v[60], v[61], v[62], v[63],
                                                               v[59], v[30], v[44], v[45], v[31]),
+          "| owner phases: warm/tf %d, RL guesses %d, scans+evaluation %d, commit %d" % (v[46], v[47], v[48], v[49]),
           flush=True)
