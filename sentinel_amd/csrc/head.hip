@@ -398,75 +398,84 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 const uint32_t xl = (uint32_t)__popc(xm);
                 const uint32_t xin = hd_add_scan(xl);
                 const int32_t X0 = (int32_t)(xin - xl);
-                const int32_t bu = Flc + 1 - c;  // u = max(0, floor(count) - acquire - c + X + 1)
-                int32_t A = 0, B = HD_INF;
-                {
-                    int32_t X = X0;
-#pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) {
-                        const int32_t a = (int32_t)((am >> e) & 1);
-                        int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
-                        u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
-                        const int32_t nb = B + 1 < u ? B + 1 : u;
-                        B = a ? nb : B;
-                        A += a;
-                        X += (int32_t)((xm >> e) & 1);
-                    }
-                }
-                int32_t ia = A, ib = B;
-                hd_minplus_scan(ia, ib);
-                int32_t pa = HD_DPP(0, ia, 0x138, 0xf), pb = HD_DPP(HD_INF, ib, 0x138, 0xf);  // wave_shr:1
-                pa = lane == 0 ? 0 : pa;
-                pb = lane == 0 ? HD_INF : pb;
-                {  // the closed form's guesses (exact for acquire counts of 1 and right EXIT guesses)
-                    int32_t P = pa < pb ? pa : pb, X = X0;
-#pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) {
-                        const bool a = (am >> e) & 1;
-                        int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
-                        u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
-                        const int32_t Pn = a ? (P + 1 < u ? P + 1 : u) : P;
-                        gm |= (uint32_t)(Pn > P) << e;
-                        P = Pn;
-                        X += (int32_t)((xm >> e) & 1);
-                    }
-                }
-                // publish the guesses (same-chunk EXITs read them; a wave's LDS operations complete in order)
-                st = (st & ~amask) | gm;
-                win[wi] = (uint16_t)st;
-                const uint32_t gl = (uint32_t)__popc(gm);
-                const uint32_t gin = hd_add_scan(gl);
-                const int32_t P0 = (int32_t)(gin - gl);
-                if (!uni) {  // mixed acquire counts: the closed form is a guess; evaluate at the counted prefix
-                    int32_t Pc = P0, Xc = X0;
-#pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) {
-                        const bool a = (am >> e) & 1, g = (gm >> e) & 1;
-                        const int32_t ci = c + Pc - Xc;
-                        const bool tr = !((double)j_iadd(ci, (int32_t)(czr[e] & 0xFFFFu)) > rcount);
-                        mm |= (uint32_t)(a && tr != g) << e;
-                        tm |= (uint32_t)(a && tr) << e;
-                        Pc += g ? 1 : 0;
-                        Xc += (int32_t)((xm >> e) & 1);
-                    }
+                // frozen round: saturated (c + 1 > count), unit acquire counts and no effective EXIT among the active
+                // positions -- no ENTRY can pass, every guess is exact: all blocked, nothing to scan
+                const bool frz = uni && Flc <= c && __builtin_amdgcn_readlane((int)xin, 63) == 0;
+                if (frz) {
+                    st &= ~amask;
+                    win[wi] = (uint16_t)st;
+                    endstate = c;
                 } else {
-                    tm |= gm;
-                }
-                if (dx) {  // same-chunk EXITs: effective iff their ENTRY's new guess passes
-#pragma unroll
-                    for (uint32_t e = 0; e < HD_EP; ++e) {
-                        const uint32_t now = hd_bit(win, so.ref[e][lane]), d = (dx >> e) & 1, was = (xm >> e) & 1;
-                        mm |= (d & (now ^ was)) << e;
-                        tm |= (d & now) << e;
+                    const int32_t bu = Flc + 1 - c;  // u = max(0, floor(count) - acquire - c + X + 1)
+                    int32_t A = 0, B = HD_INF;
+                    {
+                        int32_t X = X0;
+    #pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) {
+                            const int32_t a = (int32_t)((am >> e) & 1);
+                            int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
+                            u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
+                            const int32_t nb = B + 1 < u ? B + 1 : u;
+                            B = a ? nb : B;
+                            A += a;
+                            X += (int32_t)((xm >> e) & 1);
+                        }
                     }
+                    int32_t ia = A, ib = B;
+                    hd_minplus_scan(ia, ib);
+                    int32_t pa = HD_DPP(0, ia, 0x138, 0xf), pb = HD_DPP(HD_INF, ib, 0x138, 0xf);  // wave_shr:1
+                    pa = lane == 0 ? 0 : pa;
+                    pb = lane == 0 ? HD_INF : pb;
+                    {  // the closed form's guesses (exact for acquire counts of 1 and right EXIT guesses)
+                        int32_t P = pa < pb ? pa : pb, X = X0;
+    #pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) {
+                            const bool a = (am >> e) & 1;
+                            int32_t u = bu - (int32_t)(czr[e] & 0xFFFFu) + X;
+                            u = u < 0 ? 0 : u > HD_INF ? HD_INF : u;
+                            const int32_t Pn = a ? (P + 1 < u ? P + 1 : u) : P;
+                            gm |= (uint32_t)(Pn > P) << e;
+                            P = Pn;
+                            X += (int32_t)((xm >> e) & 1);
+                        }
+                    }
+                    // publish the guesses (same-chunk EXITs read them; a wave's LDS operations complete in order)
+                    st = (st & ~amask) | gm;
+                    win[wi] = (uint16_t)st;
+                    const uint32_t gl = (uint32_t)__popc(gm);
+                    const uint32_t gin = hd_add_scan(gl);
+                    const int32_t P0 = (int32_t)(gin - gl);
+                    if (!uni) {  // mixed acquire counts: the closed form is a guess; evaluate at the counted prefix
+                        int32_t Pc = P0, Xc = X0;
+    #pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) {
+                            const bool a = (am >> e) & 1, g = (gm >> e) & 1;
+                            const int32_t ci = c + Pc - Xc;
+                            const bool tr = !((double)j_iadd(ci, (int32_t)(czr[e] & 0xFFFFu)) > rcount);
+                            mm |= (uint32_t)(a && tr != g) << e;
+                            tm |= (uint32_t)(a && tr) << e;
+                            Pc += g ? 1 : 0;
+                            Xc += (int32_t)((xm >> e) & 1);
+                        }
+                    } else {
+                        tm |= gm;
+                    }
+                    if (dx) {  // same-chunk EXITs: effective iff their ENTRY's new guess passes
+    #pragma unroll
+                        for (uint32_t e = 0; e < HD_EP; ++e) {
+                            const uint32_t now = hd_bit(win, so.ref[e][lane]), d = (dx >> e) & 1, was = (xm >> e) & 1;
+                            mm |= (d & (now ^ was)) << e;
+                            tm |= (d & now) << e;
+                        }
+                    }
+                    if (mm) {  // the state right after the lane's first mismatch
+                        const uint32_t e1 = (uint32_t)__ffs((int)mm) - 1, below = (1u << e1) - 1u;
+                        const int32_t cb1 = c + P0 + __popc(gm & below) - (X0 + __popc(xm & below));
+                        const int32_t t1 = (int32_t)((tm >> e1) & 1);
+                        mstate = ((emask >> e1) & 1) ? cb1 + t1 : cb1 - t1;
+                    }
+                    endstate = (int64_t)c + (int32_t)gin - (int32_t)xin;
                 }
-                if (mm) {  // the state right after the lane's first mismatch
-                    const uint32_t e1 = (uint32_t)__ffs((int)mm) - 1, below = (1u << e1) - 1u;
-                    const int32_t cb1 = c + P0 + __popc(gm & below) - (X0 + __popc(xm & below));
-                    const int32_t t1 = (int32_t)((tm >> e1) & 1);
-                    mstate = ((emask >> e1) & 1) ? cb1 + t1 : cb1 - t1;
-                }
-                endstate = (int64_t)c + (int32_t)gin - (int32_t)xin;
             } else {
                 // RATE: the round's guesses.  Queueing (L + cost after the first active ENTRY's arrival): the saturated
                 // lattice -- the n-th pass of the round is the first ENTRY at or after L + n * cost - maxQueue while each
@@ -504,7 +513,22 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
 #pragma unroll
                 for (uint32_t e = 0; e < HD_EP; ++e)
                     lm |= (uint32_t)(((am >> e) & 1) && (warm || (czr[e] & 0xFFFFu) != 0)) << e;
+                // frozen round: queueing, unit acquire counts and no lattice point up to the last active arrival -- every
+                // active ENTRY blocks (L + cost - t > maxQueue for all of them) and L stays: nothing to scan
+                bool frz = false;
+                if (lattice && uni) {
+                    const uint64_t lb2 = __ballot(am != 0);
+                    const uint32_t ll2 = 63u - (uint32_t)__clzll((long long)lb2);
+                    int32_t ldt = 0;
+#pragma unroll
+                    for (uint32_t e = 0; e < HD_EP; ++e) ldt = ((am >> e) & 1) ? dtr[e] : ldt;
+                    frz = lat(__builtin_amdgcn_readlane(ldt, ll2)) == 0;
+                }
                 uint32_t lg = 0;  // lattice guesses
+                if (frz) {
+                    endstate = L;
+                    st &= ~amask;
+                } else {
                 if (lattice) {
                     int32_t A2 = 0, B2 = HD_INF;
 #pragma unroll
@@ -569,6 +593,7 @@ __device__ __forceinline__ void head_seg(HdShared& sh, const SEv* __restrict__ r
                 }
                 endstate = Lc;
                 st = (st & ~amask) | gm;
+                }
             }
             if (prof) { const unsigned long long _n = __builtin_amdgcn_s_memtime(); ph[2] += _n - pt; pt = _n; }
             // the wave's first mismatch (lanes in position order): it takes its evaluated outcome, everything before
