@@ -4087,7 +4087,7 @@ hipError_t launch_decide_bin(int bin, const SEv* recs, const sg_event* ev, const
     if (!m) return hipSuccess;
     // single-rule THREAD-grade / RateLimiter heads (XF_HEADT / XF_HEADR): the event-driven owner, before the
     // cooperative one (which leaves those segments)
-    if ((bin == BIN_J16 || bin == BIN_J4 || bin == BIN_J1) && !(cfg.dbg_flags & HEAD_OFF)) {
+    if ((bin == BIN_J16 || bin == BIN_J4 || bin == BIN_J1) && cfg.heads && !(cfg.dbg_flags & HEAD_OFF)) {
         const hipError_t he = launch_head(recs, segs, order, m, S, cfg, t0, dec, bflags, st);
         if (he != hipSuccess) return he;
     }

@@ -238,7 +238,7 @@ struct DevCfg {
     uint64_t reserved0;
     uint64_t ring_mask;
     uint32_t dbg_flags;  // SG_DEBUG_FLAGS experiment switches (0 in production)
-    uint32_t pad;
+    uint32_t heads;      // some program is XF_HEADT / XF_HEADR: the head owner (head.hip) runs beside the bins
 };
 
 // one resource's events inside a batch: sorted positions [start, start+len)

@@ -673,6 +673,7 @@ struct sg_engine {
     bool mix_pq = false;        // SG_MIX_PQ=1: param-only programs of the XF_MIX shape decided as XF_MIX too
     bool pv_pq = true;          // SG_PV_PQ (default 1): XF_PVPQ programs' long segments through the value-parallel passes
     bool has_mix = false;       // some resource's program is XF_MIX (the batches keep the pre / post pass lists)
+    bool has_head = false;      // some resource's program is XF_HEADT / XF_HEADR (head.hip k_head is launched)
     bool pv_on = true;          // SG_PV (default 1): the value-parallel pre pass (pvalue.hip) for the long XF_MIX segments
     PvBuf pvb{};                // its scratch: the pre pass's (launch_pv_a / _b) ...
     PvBuf pvbt{};               // ... and the post pass's (launch_pvt), so that the next batch's extraction and sort
@@ -876,7 +877,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
         HIPCHK(hipMemcpy(old_prog.data(), e->d_prog, R * sizeof(Prog), hipMemcpyDeviceToHost));
     }
     size_t nres = e->names.size();
-    bool any_mix = false;
+    bool any_mix = false, any_head = false;
     std::vector<std::pair<uint32_t, uint32_t>> relate;  // (resource, referenced resource) of RELATE rules
     for (size_t r = 0; r < nres && r < R; ++r) {
         Prog p;
@@ -1085,6 +1086,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
                                                               (d.behavior == SG_CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER && d.count > 0)))
                         p.xf |= XF_HEADR;
                 }
+                if (p.xf & (XF_HEADT | XF_HEADR)) any_head = true;
             }
         }
         // carry controller / breaker state of kinds that were not reloaded
@@ -1183,6 +1185,7 @@ int upload_rules(sg_engine* e, bool reset_flow_state, bool reset_deg_state, bool
     HIPCHK(hipMemcpy(e->d_prog, prog.data(), R * sizeof(Prog), hipMemcpyHostToDevice));
     e->n_dev_rules = (uint32_t)rules.size();
     e->has_mix = any_mix;
+    e->has_head = any_head;
     e->has_multi = any_multi;
     if (comp.empty()) {
         dfree(e->d_comp);
@@ -2437,6 +2440,7 @@ static int submit_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext
     dc.switch_on = e->cfg.switch_on;
     dc.ring_mask = ring_mask;
     dc.dbg_flags = e->dbg_flags;
+    dc.heads = e->has_head ? 1u : 0u;
     DevState S{};
     std::memset(&S, 0, sizeof(S));
     S.sec = e->d_sec;
@@ -2760,6 +2764,7 @@ static int tiny_impl(sg_engine* e, const sg_event* ev, const sg_event_ext* ext, 
     dc.switch_on = e->cfg.switch_on;
     dc.ring_mask = (1ull << e->cfg.status_ring_log2) - 1;
     dc.dbg_flags = e->dbg_flags;
+    dc.heads = e->has_head ? 1u : 0u;
     DevState S{};
     std::memset(&S, 0, sizeof(S));
     S.sec = e->d_sec; S.minb = e->d_minb; S.info = e->d_info; S.prog = e->d_prog; S.rules = e->d_rules;
