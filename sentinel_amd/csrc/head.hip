@@ -1,31 +1,34 @@
-// head.hip -- event-driven owners of single-rule head segments (one wavefront per segment).
+// head.hip -- the event-driven owner of single-rule head segments (C3's THREAD-grade and rate-limiter heads).
 //
 // A resource whose only rule is one flow rule on its ClusterNode (no degrade, no param rule, DIRECT, limitApp
-// default) of one of two kinds has a decision chain with a single piece of state:
+// default) of these kinds has a decision chain with a single piece of state:
 //   XF_HEADT  THREAD-grade DefaultController (core/slots/block/flow/controller/DefaultController.java:49-81): an ENTRY
 //             passes iff curThreadNum + acquire <= count; StatisticSlot adds 1 to curThreadNum per pass and takes 1
 //             off per effective EXIT (core/slots/statistic/StatisticSlot.java:54-173).  State: the thread count c.
 //   XF_HEADR  QPS RateLimiterController (core/slots/block/flow/controller/RateLimiterController.java:46-91): an ENTRY
 //             of acquire > 0 passes iff latestPassedTime + cost <= now or latestPassedTime + cost - now <= maxQueue,
-//             and then latestPassedTime = max(latestPassedTime + cost, now).  State: latestPassedTime L.
-// The cooperative owner (decide.hip k_jac) decides such a head by Jacobi iterations over 256- / 1024-lane tiles, whose
-// per-iteration chain of block-wide scans and barriers bounds it (C3: 14-17 ms a 2^24-event batch).  Here one wave
-// owns the segment and walks it in chunks of 1,024 positions (16 a lane, consecutive), each decided by
-// guess-and-verify rounds that need no barrier:
+//             and then latestPassedTime = max(latestPassedTime + cost, now); WarmUpRateLimiterController likewise, its
+//             cost following the stored tokens synced once a second (WarmUpController.java:141-174).  State: L.
+// The cooperative owner (decide.hip k_jac) decided such a head by Jacobi iterations over 256- / 1024-lane tiles, whose
+// per-iteration chain of block-wide scans and barriers bounded it (C3: 14-17 ms a 2^24-event batch).  Here the owner
+// wave walks the segment in chunks of 1,024 positions (16 consecutive a lane), each decided by guess-and-verify rounds
+// that need no barrier:
 //   THREAD  the passes P_i before position i follow P_{i+1} = min(P_i + [ENTRY], u_i), u_i = max(0, floor(count) -
 //           acquire - c + X_i + 1), X_i the effective EXITs before i -- an affine map of the (min, +) semiring, so one
 //           wave scan of (a, b) pairs gives every ENTRY's verdict once the EXITs' effectiveness is known.  An EXIT
-//           naming an ENTRY of the same chunk is effective iff that ENTRY passed: its guess is the ENTRY's verdict of
-//           the round before (the chunk's first round: the last verdict of the chunk before).
+//           naming an ENTRY of this chunk or the one before is effective iff that ENTRY passed: its guess is that
+//           ENTRY's verdict of the round before (a chunk's first round: the last verdict of the chunk before).
 //   RATE    with the passes guessed, L before every ENTRY is one wave scan of (max, +) maps x -> max(x + cost, t).
-//           Guesses: every ENTRY passes after a pass; after a block, the saturated lattice -- the first ENTRY at or
-//           after L + j * cost - maxQueue passes for j = 1, 2, ... (each pass moves L by exactly cost while arrivals
-//           are dense), so a saturated chunk is one round.
+//           Guesses: queueing (L + cost after the round's first arrival) -- the saturated lattice, the n-th pass the
+//           first ENTRY at or after L + n * cost - maxQueue, i.e. the THREAD scan over the lattice points up to each
+//           arrival; idle -- every ENTRY passes.  A WarmUpRateLimiter round stays inside one second.
 // Each round then evaluates every ENTRY exactly at its guessed prefix state; the first event whose evaluation (or, for
 // an EXIT, whose ENTRY's verdict) differs from its guess ends the round: everything before it is exact, it takes its
-// evaluated outcome, and the next round starts after it.  Statistics follow once the chunk is decided: per 500 ms
-// bucket wave reductions folded into the node exactly as k_jac's round_fold folds a round.  EXIT references into
-// earlier chunks read a 2^18-position status ring in LDS (older ones the dec[] word).
+// evaluated outcome, and the next round starts after it.  A round that cannot pass anything (saturated, no effective
+// EXIT / no lattice point) is committed as blocked without scans.  Statistics follow once a chunk is decided: per
+// 500 ms bucket, folded into the node exactly as k_jac's round_fold folds a round.  EXIT references into earlier
+// chunks read a 2^17-position status ring in LDS (older ones the dec[] word).  Seven waves pipeline the chunks
+// (head_seg below); one launch takes both kinds (k_head).
 #include "chain.h"
 #include "dev_types.h"
 
@@ -83,9 +86,6 @@ __device__ __forceinline__ void hd_maxplus_scan(int64_t& a, int64_t& b) {
 #undef S_
 #undef D64
 }
-
-enum : uint32_t { HK_ENT = 1u, HK_EXIT = 2u, HK_TRACE = 3u, HK_KIND = 3u, HK_EFF = 4u /* effective, known */,
-                  HK_DYN = 8u /* effective iff the ENTRY at ref (same chunk) passed */ };
 
 __device__ __forceinline__ uint32_t hd_bit(const uint16_t* win, uint32_t p) { return (win[(p >> 4) & (HD_RW - 1)] >> (p & 15)) & 1u; }
 
