@@ -78,12 +78,14 @@ def _compare(eng, orc, ev, dg, do, n_res, io, ic, sample):
     return sum(_check_aux(eng, orc, int(r), io, ic, t_end) for r in sample)
 
 
-@pytest.mark.parametrize("cfg", [4, 2])
+@pytest.mark.parametrize("cfg", [4, 2, 3])
 def test_ext_post_pass_parity(cfg):
     # C4 (flow + degrade: k_jac / k_lite) and C2 (flow only) shapes at 3000 resources: the Zipf head is a
-    # segment of ~100k events (pieces + merge), the body single pieces, the tail one lane each
+    # segment of ~100k events (pieces + merge), the body single pieces, the tail one lane each; C3 (THREAD-grade /
+    # WarmUp / rate-limiter heads: head.hip k_head decides the single-rule heads, the post-pass their nodes)
     n_res = 3000
-    w = T.Workload(cfg, seed=T.SEED_BASE + 40 + cfg, n_res=n_res, n_entries=400_000)
+    var = T.V_WARM_RL if cfg == 3 else 0
+    w = T.Workload(cfg, seed=T.SEED_BASE + 40 + cfg, n_res=n_res, n_entries=400_000, variant=var)
     ev = w.events
     eng = E.Engine(max_resources=4096, max_slot_chain_size=0, status_ring_log2=24, aux_node_capacity=1 << 17)
     orc = O.Oracle(max_slot_chain_size=0)
@@ -108,7 +110,8 @@ def test_ext_post_pass_parity(cfg):
                           warm_up_period_sec=2) for r in range(0, n_res, 3)]
     for x in (eng, orc):
         x.load_flow_rules(rules)
-    w2 = T.Workload(cfg, seed=T.SEED_BASE + 40 + cfg, n_res=n_res, n_entries=60_000, t0=int(ev["ts"][-1]) + 1)
+    w2 = T.Workload(cfg, seed=T.SEED_BASE + 40 + cfg, n_res=n_res, n_entries=60_000, t0=int(ev["ts"][-1]) + 1,
+                    variant=var)
     ev2 = w2.events.copy()
     isref = (ev2["kind"] != A.EV_ENTRY) & ((ev2["aux"] & np.uint64(A.REF_NONE)) != np.uint64(A.REF_NONE))
     ext2 = T.ext_for(ev2, io, ic, seed=6)  # (refs still local to ev2 here)
